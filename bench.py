@@ -1,0 +1,266 @@
+"""Benchmark: device-resident rx classify + Jenkins flow hash (BASELINE.json).
+
+One step = one pass of the classify kernel over this GPU's batch of frames
+already resident in HBM (the rx_one_pkt loop of iokernel/rx.c:281-287 for a
+whole batch), plus -- with more than one GPU -- an RCCL all_gather of every
+rank's per-runtime packet counts and rx counters over xGMI.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Rank 0 prints one JSON line.  Workload (configs[1] of BASELINE.json): 32 Mi
+synthetic 64-B Eth/IPv4/UDP frames per GPU, uniform 5-tuples, 16 runtimes x 8
+kthreads, JENKINS flow hash; packets are sharded round-robin across ranks in
+64 Ki-packet blocks (weak scaling: per-GPU work is fixed).  At N=1 the
+secondary config (1500-B TCP, Zipf-0.99 flows, 1024 runtimes) and the CPU
+baseline (the oracle's restatement of rx.c on this host's cores) are added.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from caladan_amd import gclassify as g  # noqa: E402
+from caladan_amd import shard  # noqa: E402
+
+METRIC = "Mpkt/s device-resident rx classify+Jenkins-hash, 64B & 1500B frames"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak (spec)
+SEED = 0xCA1ADA4
+SHARD_BLOCK = 64 * 1024
+
+WORKLOADS = {
+    # name: (generator, pkts per GPU, slot stride, runtimes, threads, description)
+    "udp64": (g.WL_UDP64, 32 << 20, 64, 16, 8,
+              "32Mi Eth/IPv4/UDP 64B frames per GPU in HBM, uniform 5-tuples, 16 runtimes x 8 kthreads"),
+    "tcp1500": (g.WL_TCP1500_ZIPF, 8 << 20, 1536, 1024, 4,
+                "8Mi Eth/IPv4/TCP 1500B frames (1536B slots), Zipf-0.99 over 1Mi flows, 1024 runtimes x 4 kthreads"),
+    "mixed": (g.WL_MIXED, 1 << 20, 9216, 16, 8,
+              "1Mi mixed frames (70% IPv4 TCP/UDP 64..9014B, 20% IPv6, 10% ARP), 9216B slots, 16 runtimes"),
+}
+# algorithmic bytes per packet: one 64-B header granule read + one 8-B verdict
+# written (DESIGN.md "Roofline"); tables and counters amortise to ~0.
+BYTES_PER_PKT = 64 + 8
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def setup_tables(clf, R, T, seed=SEED):
+    """Runtime r owns 10.0.0.(r+1); active kthreads seeded in [1, T];
+    flow tables from the sched_steer_flows rule (gcl_steer_flows)."""
+    rng = np.random.default_rng(seed)
+    tables = []
+    for r in range(R):
+        act = int(rng.integers(1, T + 1))
+        idx = [int(x) for x in rng.choice(T, size=act, replace=False)]
+        fl = g.steer_flows(T, idx)
+        clf.runtime_set(r, g.runtime_ip(r), T, act, fl)
+        tables.append((r, g.runtime_ip(r), T, act, fl))
+    return tables
+
+
+class Workload:
+    def __init__(self, name, rank, world, device, hash_mode=g.HASH_JENKINS):
+        wl, n, stride, R, T, desc = WORKLOADS[name]
+        self.name, self.wl, self.n, self.stride, self.R, self.T, self.desc = name, wl, n, stride, R, T, desc
+        self.frames = torch.zeros(n * stride, dtype=torch.uint8, device=device)
+        self.verdicts = torch.empty(n * 8, dtype=torch.uint8, device=device)
+        self.counts = torch.zeros(R + g.NR_STATS, dtype=torch.int64, device=device)
+        cdf_dev = None
+        nflows = 0
+        if wl == g.WL_TCP1500_ZIPF:
+            nflows = 1 << 20
+            cdf_dev = torch.from_numpy(g.zipf_cdf(nflows, 0.99).view(np.int64)).to(device)
+        g.generate(wl, n, stride, R, self.frames, seed=SEED, rank=rank, world=world,
+                   shard_block=SHARD_BLOCK, zipf_cdf_dev=cdf_dev, nflows=nflows)
+        self.clf = g.Classifier(device.index or 0, R, hash_mode, g.CFG_PROFILE)
+        self.tables = setup_tables(self.clf, R, T)
+        torch.cuda.synchronize()
+
+    def step(self, stream):
+        self.clf.classify(self.frames, self.n, self.stride, verdicts=self.verdicts,
+                          counts=self.counts[:self.R], stats=self.counts[self.R:], stream=stream)
+
+
+def run_timed(w, steps, warmup, world, gathered):
+    stream = torch.cuda.current_stream().cuda_stream
+    for _ in range(warmup):
+        w.step(stream)
+        if world > 1:
+            shard.allgather_counts(w.counts, gathered)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    w.clf.kernel_time(reset=True)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        w.step(stream)
+        if world > 1:
+            shard.allgather_counts(w.counts, gathered)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    kms, nl = w.clf.kernel_time(reset=True)
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        el = float(t.item())
+    return el, kms / max(nl, 1)
+
+
+def roofline(w, kernel_ms):
+    bytes_per_launch = w.n * BYTES_PER_PKT
+    achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
+    traffic = None
+    prof = os.path.join(ROOT, "profiles", f"pmc_{w.name}.json")
+    if os.path.exists(prof):
+        try:
+            with open(prof) as f:
+                traffic = json.load(f).get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "bytes_per_pkt": BYTES_PER_PKT, "kernel_ms": round(kernel_ms, 4)}
+
+
+def cpu_baseline(budget_s=12.0):
+    """The oracle's rx.c restatement on this host (TEST INFRASTRUCTURE as the
+    checker/baseline only).  Sample: the first 2 Mi packets of the udp64
+    stream (identical bytes to the GPU's), bursts of 64, prefetch stride 2."""
+    from oracle import orc
+    try:
+        orc.build(native=True)
+        native = True
+    except Exception as e:  # pragma: no cover - gcc missing on the box
+        log("native oracle build failed, using portable build:", e)
+        native = False
+    wl, _, stride, R, T, _ = WORKLOADS["udp64"]
+    n = 2 << 20
+    frames, _, _ = orc.generate(wl, n, stride, R, seed=SEED, native=native)
+    t = orc.Tables(R, g.HASH_JENKINS, 0, g.F_RSS_HASH | g.F_IP_CKSUM_GOOD, native=native)
+    rng = np.random.default_rng(SEED)
+    for r in range(R):
+        act = int(rng.integers(1, T + 1))
+        idx = [int(x) for x in rng.choice(T, size=act, replace=False)]
+        t.runtime_set(r, orc.runtime_ip(r), T, act, orc.steer_flows(T, idx))
+    probe = t.bench(frames, n, stride, threads=1, passes=1)
+    passes = max(1, int(budget_s * 0.45 / max(probe, 1e-6)))
+    s1 = t.bench(frames, n, stride, threads=1, passes=passes)
+    rate1 = n * passes / s1 / 1e6
+    s_l = t.bench(frames, n, stride, threads=1, passes=max(1, passes // 2), lrpc=True)
+    rate_l = n * max(1, passes // 2) / s_l / 1e6
+    threads = min(16, os.cpu_count() or 1)
+    pm = max(1, int(budget_s * 0.25 / max(probe / threads, 1e-6)))
+    sm = t.bench(frames, n, stride, threads=threads, passes=pm)
+    rate_m = n * pm / sm / 1e6
+    cpu_model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu_model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {
+        "value": round(rate1, 2), "unit": "Mpkt/s", "cores": 1, "kind": "port",
+        "sample": f"first {n} pkts of the udp64 stream x {passes} passes, classify-only "
+                  f"(rx_one_pkt restatement, bursts of 64, -O3 -march={'native' if native else 'x86-64-v2'})",
+        "lrpc_1core_mpps": round(rate_l, 2),
+        "all_cores": {"value": round(rate_m, 2), "cores": threads, "passes": pm},
+        "cpu_model": cpu_model, "nproc": os.cpu_count(),
+        "seconds": round(probe + s1 + s_l + sm, 2),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="udp64", choices=sorted(WORKLOADS))
+    ap.add_argument("--no-secondary", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    args = ap.parse_args()
+
+    rank, world, local = shard.dist_env()
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        shard.init(rank, world)
+
+    w = Workload(args.workload, rank, world, device)
+    gathered = torch.zeros(world * w.counts.numel(), dtype=torch.int64, device=device)
+    el, kms = run_timed(w, args.steps, args.warmup, world, gathered)
+    total_pkts = w.n * world * args.steps
+    value = total_pkts / el / 1e6
+    # correctness spot check: every packet of every step was accounted for
+    if world > 1:
+        tot = gathered.view(world, -1)[:, :w.R].sum().item()
+        expect = w.n * world * (args.steps + args.warmup)
+    else:
+        tot = w.counts[:w.R].sum().item()
+        expect = w.n * (args.steps + args.warmup)
+    result = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "Mpkt/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(el / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic",
+        "config": {"workload": f"{args.workload}: {w.desc}", "pkts_per_gpu": w.n,
+                   "slot_stride": w.stride, "runtimes": w.R, "kthreads": w.T,
+                   "hash": "jenkins (lookup3 13-B 5-tuple)",
+                   "parallelism": (f"dp{world}: round-robin 64Ki-pkt shards, RCCL all_gather "
+                                   "of per-runtime counts" if world > 1 else "single GPU")},
+        "roofline": roofline(w, kms),
+        "counts_check": "ok" if tot == expect else f"MISMATCH {tot} != {expect}",
+    }
+    del w
+    torch.cuda.empty_cache()
+
+    if world == 1 and not args.no_secondary and args.workload == "udp64":
+        w2 = Workload("tcp1500", rank, world, device)
+        el2, kms2 = run_timed(w2, max(5, args.steps // 5), 2, 1, None)
+        steps2 = max(5, args.steps // 5)
+        result["secondary"] = {
+            "workload": f"tcp1500: {w2.desc}",
+            "value": round(w2.n * steps2 / el2 / 1e6, 1), "unit": "Mpkt/s",
+            "ms_per_step": round(el2 / steps2 * 1e3, 4), "steps": steps2,
+            "roofline": roofline(w2, kms2),
+            "frame_bytes_rate_GBs": round(w2.n * 1500 / (kms2 * 1e-3) / 1e9, 1),
+        }
+        del w2
+        torch.cuda.empty_cache()
+
+    if world == 1 and not args.no_cpu:
+        result["cpu_baseline"] = cpu_baseline(args.cpu_budget)
+    if world > 1:
+        shard.finish()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,112 @@
+/*
+ * gcl_device.h - device-side building blocks shared by the classify and
+ * generator kernels (gfx950).  Integer-only: lookup3, Toeplitz, header field
+ * extraction from little-endian dwords, Lemire fastmod.
+ */
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gcl {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+/* 16-byte streaming load that does not keep the line (read-once frames) */
+__device__ __forceinline__ uint4 load16_nt(const void *p)
+{
+	u32x4 v = __builtin_nontemporal_load((const u32x4 *)p);
+	return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+__device__ __forceinline__ uint32_t rotl(uint32_t x, int k)
+{
+	return (x << k) | (x >> (32 - k));
+}
+
+/* lookup3 mix / final (base/jenkins_hash.c:79-87, :114-123) */
+__device__ __forceinline__ void jmix(uint32_t &a, uint32_t &b, uint32_t &c)
+{
+	a -= c; a ^= rotl(c, 4);  c += b;
+	b -= a; b ^= rotl(a, 6);  a += c;
+	c -= b; c ^= rotl(b, 8);  b += a;
+	a -= c; a ^= rotl(c, 16); c += b;
+	b -= a; b ^= rotl(a, 19); a += c;
+	c -= b; c ^= rotl(b, 4);  b += a;
+}
+
+__device__ __forceinline__ void jfinal(uint32_t &a, uint32_t &b, uint32_t &c)
+{
+	c ^= b; c -= rotl(b, 14);
+	a ^= c; a -= rotl(c, 11);
+	b ^= a; b -= rotl(a, 25);
+	c ^= b; c -= rotl(b, 16);
+	a ^= c; a -= rotl(c, 4);
+	b ^= a; b -= rotl(a, 14);
+	c ^= b; c -= rotl(b, 24);
+}
+
+/* jenkins_hash(&ip, 4): the rte_jhash key of dp.ip_to_proc (dp_clients.c:360) */
+__device__ __forceinline__ uint32_t jhash_u32(uint32_t ip)
+{
+	uint32_t a = 0xdeadbeefu + 4u, b = a, c = a;
+	a += ip;
+	jfinal(a, b, c);
+	return c;
+}
+
+/* jenkins_hash over the 13-byte flow key {saddr, daddr, dport, sport, proto}
+ * (host-order fields, little-endian bytes): one 12-byte block + 1 tail byte. */
+__device__ __forceinline__ uint32_t jhash_5tuple(uint32_t saddr, uint32_t daddr,
+                                                 uint32_t sport, uint32_t dport,
+                                                 uint32_t proto)
+{
+	uint32_t a = 0xdeadbeefu + 13u, b = a, c = a;
+	a += saddr;
+	b += daddr;
+	c += dport | (sport << 16);
+	jmix(a, b, c);
+	a += proto;
+	jfinal(a, b, c);
+	return c;
+}
+
+__device__ __forceinline__ uint32_t bswap16(uint32_t x)
+{
+	return ((x & 0xFFu) << 8) | ((x >> 8) & 0xFFu);
+}
+
+__device__ __forceinline__ uint32_t bswap32(uint32_t x)
+{
+	return __builtin_bswap32(x);
+}
+
+/* bytes [2..5] of the 8-byte little-endian pair (lo, hi) */
+__device__ __forceinline__ uint32_t mid32(uint32_t lo, uint32_t hi)
+{
+	return __builtin_amdgcn_alignbit(hi, lo, 16);
+}
+
+/* n % d for d in [1, 2^16) with M = ceil(2^64 / d) (0 for d == 1). */
+__device__ __forceinline__ uint32_t fastmod(uint32_t n, uint64_t M, uint32_t d)
+{
+	uint64_t low = M * (uint64_t)n;
+	uint32_t lo = (uint32_t)low, hi = (uint32_t)(low >> 32);
+	uint64_t t = (uint64_t)hi * d + __umulhi(lo, d);
+	return (uint32_t)(t >> 32);
+}
+
+/* splitmix64 output function at stream position x (generator) */
+__device__ __forceinline__ uint64_t mix64(uint64_t z)
+{
+	z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+	z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+	return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ uint64_t rw(uint64_t seed, uint64_t g, uint64_t k)
+{
+	return mix64(seed + (g * 8 + k + 1) * 0x9E3779B97F4A7C15ull);
+}
+
+} // namespace gcl

@@ -1,0 +1,258 @@
+/*
+ * gcl_host.c - host-side C of the rx classify path: table helpers, the CPU
+ * forms of the two hashes, and the verdict post-pass that feeds lrpc rings.
+ */
+#include <errno.h>
+#include <math.h>
+#include <string.h>
+
+#include "../../include/gcl_host.h"
+#include "../../include/gclassify.h"
+
+#define ROT(x, k) (((x) << (k)) | ((x) >> (32 - (k))))
+
+/*
+ * gcl_jenkins_hash - lookup3 hashlittle, initval 0 (base/jenkins_hash.c:
+ * 126-297), the function rte_jhash(key, len, 0) applies to the ip_to_proc
+ * keys.  Reads 12-byte blocks as little-endian words (memcpy, any alignment).
+ */
+uint32_t gcl_jenkins_hash(const void *key, size_t length)
+{
+	const uint8_t *k = key;
+	uint32_t a, b, c, w[3];
+
+	a = b = c = 0xdeadbeefu + (uint32_t)length;
+	while (length > 12) {
+		memcpy(w, k, 12);
+		a += w[0];
+		b += w[1];
+		c += w[2];
+		a -= c; a ^= ROT(c, 4);  c += b;
+		b -= a; b ^= ROT(a, 6);  a += c;
+		c -= b; c ^= ROT(b, 8);  b += a;
+		a -= c; a ^= ROT(c, 16); c += b;
+		b -= a; b ^= ROT(a, 19); a += c;
+		c -= b; c ^= ROT(b, 4);  b += a;
+		length -= 12;
+		k += 12;
+	}
+	if (length == 0)
+		return c;
+	w[0] = w[1] = w[2] = 0;
+	memcpy(w, k, length); /* the masked tail of the aligned path, :166-181 */
+	a += w[0];
+	b += w[1];
+	c += w[2];
+	c ^= b; c -= ROT(b, 14);
+	a ^= c; a -= ROT(c, 11);
+	b ^= a; b -= ROT(a, 25);
+	c ^= b; c -= ROT(b, 16);
+	a ^= c; a -= ROT(c, 4);
+	b ^= a; b -= ROT(a, 14);
+	c ^= b; c -= ROT(b, 24);
+	return c;
+}
+
+/*
+ * gcl_toeplitz - Toeplitz hash of @input under @key, bit i of the input
+ * (MSB first) selecting the 32-bit key window starting at bit i.  For the
+ * 12-byte IPv4 tuple this equals do_toeplitz (runtime/net/core.c:120-139).
+ */
+uint32_t gcl_toeplitz(const uint8_t *key, size_t keylen, const uint8_t *input, size_t len)
+{
+	uint32_t ret = 0;
+	uint64_t window = 0;
+	size_t kb = 0;
+
+	/* 64-bit sliding window over the key bits */
+	for (; kb < 8; kb++)
+		window = window << 8 | (kb < keylen ? key[kb] : 0);
+	for (size_t i = 0; i < len; i++) {
+		for (int bit = 7; bit >= 0; bit--) {
+			int shift = 7 - bit; /* bits consumed from this byte so far */
+			if (input[i] & (1u << bit))
+				ret ^= (uint32_t)(window >> (32 - shift));
+		}
+		window = window << 8 | (kb < keylen ? key[kb] : 0);
+		kb++;
+	}
+	return ret;
+}
+
+/* sched_steer_flows rule (iokernel/sched.c:122-147) */
+int gcl_steer_flows(uint16_t thread_count, const uint16_t *active_idx,
+                    uint16_t active_count, uint16_t *flow_tbl)
+{
+	unsigned int rr = 0;
+
+	if (thread_count == 0 || thread_count > GCL_NCPU || active_count > thread_count ||
+	    !flow_tbl || (active_count && !active_idx))
+		return -EINVAL;
+	if (active_count == 0)
+		return 0; /* "don't do anything if zero threads are active" */
+	for (unsigned int i = 0; i < active_count; i++)
+		if (active_idx[i] >= thread_count)
+			return -EINVAL;
+	for (unsigned int i = 0; i < thread_count; i++)
+		flow_tbl[i] = UINT16_MAX;
+	for (unsigned int i = 0; i < active_count; i++)
+		flow_tbl[active_idx[i]] = active_idx[i];
+	for (unsigned int i = 0; i < thread_count; i++)
+		if (flow_tbl[i] == UINT16_MAX)
+			flow_tbl[i] = active_idx[rr++ % active_count];
+	return 0;
+}
+
+uint32_t gcl_runtime_ip(uint32_t r)
+{
+	return 0x0A000000u + r + 1;
+}
+
+int gcl_zipf_cdf(uint32_t nflows, double s, uint64_t *cdf_out)
+{
+	double h = 0.0, acc = 0.0;
+
+	if (!nflows || !cdf_out)
+		return -EINVAL;
+	for (uint32_t k = 0; k < nflows; k++)
+		h += pow((double)k + 1.0, -s);
+	for (uint32_t k = 0; k < nflows; k++) {
+		double x;
+		acc += pow((double)k + 1.0, -s);
+		x = ldexp(acc / h, 64);
+		cdf_out[k] = x >= 18446744073709551615.0 ? UINT64_MAX : (uint64_t)x;
+	}
+	cdf_out[nflows - 1] = UINT64_MAX;
+	return 0;
+}
+
+/* ---------------------------------------------------------------------- */
+
+int gcl_lrpc_init_out(struct gcl_lrpc_chan_out *chan, struct gcl_lrpc_msg *tbl,
+                      unsigned int size, uint32_t *recv_head_wb)
+{
+	if (!size || (size & (size - 1)))
+		return -EINVAL;
+	memset(chan, 0, sizeof(*chan));
+	chan->tbl = tbl;
+	chan->size = size;
+	chan->recv_head_wb = recv_head_wb;
+	return 0;
+}
+
+bool gcl_lrpc_send(struct gcl_lrpc_chan_out *chan, uint64_t cmd, unsigned long payload)
+{
+	struct gcl_lrpc_msg *dst;
+
+	if (chan->send_head - chan->send_tail >= chan->size) {
+		/* __lrpc_send: refresh the consumer position (base/lrpc.c:16-19) */
+		chan->send_tail = __atomic_load_n(chan->recv_head_wb, __ATOMIC_ACQUIRE);
+		if (chan->send_head - chan->send_tail == chan->size)
+			return false;
+	}
+	dst = &chan->tbl[chan->send_head & (chan->size - 1)];
+	cmd |= (chan->send_head++ & chan->size) ? 0 : GCL_LRPC_DONE_PARITY;
+	dst->payload = payload;
+	__atomic_store_n(&dst->cmd, cmd, __ATOMIC_RELEASE);
+	return true;
+}
+
+uint64_t gcl_rx_make_cmd(uint16_t pkt_len, uint8_t olflags)
+{
+	uint64_t csum = (olflags & GCL_F_IP_CKSUM_MASK) == GCL_F_IP_CKSUM_GOOD ? 1 : 0;
+	return 0 /* RX_NET_RECV */ | (uint64_t)pkt_len << 16 | csum << 48;
+}
+
+/* rx_send_to_runtime (rx.c:50-73); @via_flow_tbl selects the GPU's thread */
+static bool send_to_runtime(struct gcl_host_proc *p, uint32_t hash, int gpu_thread,
+                            uint64_t cmd, unsigned long payload,
+                            const struct gcl_host_ops *ops)
+{
+	int th;
+
+	if (gpu_thread >= 0) {
+		th = gpu_thread;
+	} else if (p->active_thread_count > 0) {
+		th = p->flow_tbl[hash % p->thread_count];
+	} else {
+		if (ops && ops->sched_add_core)
+			ops->sched_add_core(ops->arg, p);
+		if (p->active_thread_count == 0)
+			th = p->idle_top;
+		else
+			th = p->flow_tbl[hash % p->thread_count];
+	}
+	if (th < 0 || th >= p->thread_count || !p->rxq[th])
+		return false;
+	if (ops && ops->enable_poll)
+		ops->enable_poll(ops->arg, p, (unsigned int)th);
+	return gcl_lrpc_send(p->rxq[th], cmd, payload);
+}
+
+uint64_t gcl_host_deliver(struct gcl_host_proc *const *clients_by_id, uint32_t max_runtimes,
+                          struct gcl_host_proc *const *clients, int nr_clients,
+                          const struct gcl_verdict *v, const uint16_t *pkt_len,
+                          const uint8_t *olflags, uint8_t default_olflags,
+                          const uint64_t *shmptr, uint64_t n,
+                          const struct gcl_host_ops *ops, uint64_t *stats)
+{
+	uint64_t delivered = 0;
+
+	for (uint64_t i = 0; i < n; i++) {
+		uint8_t act = v[i].action & GCL_ACT_MASK;
+		uint8_t fl = olflags ? olflags[i] : default_olflags;
+		uint64_t cmd = gcl_rx_make_cmd(pkt_len ? pkt_len[i] : 0, fl);
+		unsigned long payload = shmptr ? shmptr[i] : 0;
+		struct gcl_host_proc *p = NULL;
+		bool ok;
+
+		if (act == GCL_ACT_DELIVER || act == GCL_ACT_WAKE) {
+			if (v[i].uniqid < max_runtimes)
+				p = clients_by_id[v[i].uniqid];
+			ok = p && send_to_runtime(p, v[i].hash,
+			                          act == GCL_ACT_DELIVER ? v[i].thread : -1,
+			                          cmd, payload, ops);
+			if (ok) {
+				delivered++;
+				if (ops && ops->owned)
+					ops->owned(ops->arg, p, i);
+				continue;
+			}
+			stats[GCL_RX_UNICAST_FAIL]++; /* rx.c:140-142, :213-215 */
+		} else if (act == GCL_ACT_BROADCAST) {
+			int n_sent = 0;
+			for (int c = 0; c < nr_clients; c++) {
+				if (send_to_runtime(clients[c], v[i].hash, -1, cmd, payload, ops)) {
+					n_sent++;
+					if (ops && ops->owned)
+						ops->owned(ops->arg, clients[c], i);
+				} else {
+					stats[GCL_RX_BROADCAST_FAIL]++;
+				}
+			}
+			if (n_sent == 0) {
+				if (ops && ops->free_pkt)
+					ops->free_pkt(ops->arg, i);
+			} else {
+				delivered++;
+				if (ops && ops->refcnt_update)
+					ops->refcnt_update(ops->arg, i, n_sent - 1);
+			}
+			continue; /* rx.c:185-189: no RX_UNHANDLED */
+		} else if (act == GCL_ACT_ARP_RESPOND) {
+			if (ops && ops->arp_respond && ops->arp_respond(ops->arg, i))
+				continue;
+			stats[GCL_RX_UNREGISTERED_MAC]++; /* rx.c:205 */
+		} else {
+			/* DROP_*: the device already counted them */
+			if (ops && ops->free_pkt)
+				ops->free_pkt(ops->arg, i);
+			continue;
+		}
+		/* fail_free, rx.c:225-232 */
+		if (ops && ops->free_pkt)
+			ops->free_pkt(ops->arg, i);
+		stats[GCL_RX_UNHANDLED]++;
+	}
+	return delivered;
+}

@@ -1,0 +1,893 @@
+/*
+ * gclassify.hip - MI355X (gfx950) rx classifier: kernels + C ABI.
+ *
+ * Replaces the rx_one_pkt loop of rx_burst (iokernel/rx.c:116-233, :281-287):
+ * one lane per packet, the first 64 bytes of every frame staged through LDS
+ * with coalesced 16-byte loads, the IP->runtime table and flow tables resident
+ * in LDS when they fit, per-runtime packet counts aggregated in LDS and
+ * flushed with one global atomic per (block, runtime).
+ *
+ * Layout in HBM: frames are fixed-stride slots (or a u64
+ * offset array, like mbuf data pointers into the 2 GiB ingress region);
+ * verdicts are a dense gcl_verdict[n] (8 B per packet); the table image is one
+ * contiguous buffer [ip slots | runtime entries | flow bytes | toeplitz LUT].
+ */
+#include <errno.h>
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "../../include/gclassify.h"
+#include "gcl_device.h"
+
+#define GCL_VERSION "gclassify 0.1 (gfx950)"
+
+namespace {
+
+constexpr int kThreads = 256;            /* packets per tile = lanes per block */
+constexpr int kTileBytes = kThreads * 64; /* LDS header tile */
+constexpr uint32_t kEmpty = 0xFFFFFFFFu;
+constexpr uint32_t kToepBytes = 12 * 256 * 4;
+constexpr uint32_t kLdsTableBudget = 96 * 1024;
+
+struct RtEntry {            /* 16 B per uniqid */
+	uint32_t m_lo, m_hi;     /* fastmod magic for thread_count */
+	uint16_t tc, active;     /* thread_count, active_thread_count */
+	uint32_t flow_off;       /* byte offset of flow_tbl in the flow area */
+};
+static_assert(sizeof(RtEntry) == 16, "RtEntry");
+
+struct KParams {
+	const uint8_t *frames;
+	uint64_t frames_len;
+	uint64_t stride;
+	const uint64_t *offs;
+	const uint8_t *olflags;
+	const uint32_t *rss;
+	const uint32_t *fdir;
+	uint64_t n;
+	uint64_t ntiles;
+	uint2 *verdicts;
+	unsigned long long *counts;
+	unsigned long long *stats;
+	const uint8_t *tables;     /* device table image */
+	uint32_t ipt_mask;         /* ip slots - 1 */
+	uint32_t max_rt;
+	uint32_t off_rt, off_flow, off_toep, tables_lds_bytes;
+	uint32_t cflags;
+	uint32_t default_flags;
+};
+
+/* ------------------------------------------------------------------------
+ * Header tile: 256 packets x 64 B, 16-B chunks XOR-swizzled so that both the
+ * coalesced ds_write_b128 fill and the row-per-lane ds_read_b128 are
+ * bank-conflict free (chunk q of packet p lives at p*4 + (q ^ ((p>>2)&3))).
+ */
+__device__ __forceinline__ int tile_slot(int p, int q)
+{
+	return p * 4 + (q ^ ((p >> 2) & 3));
+}
+
+__device__ __forceinline__ uint8_t frame_byte(const KParams &k, uint64_t a)
+{
+	return a < k.frames_len ? k.frames[a] : 0;
+}
+
+template <bool GENERAL>
+__device__ __forceinline__ uint64_t frame_off(const KParams &k, uint64_t idx)
+{
+	if (GENERAL && k.offs)
+		return k.offs[idx];
+	return idx * k.stride;
+}
+
+template <bool GENERAL>
+__device__ __forceinline__ void load_tile(const KParams &k, uint64_t tile, uint4 r[4])
+{
+#pragma unroll
+	for (int j = 0; j < 4; j++) {
+		int c = j * kThreads + (int)threadIdx.x;
+		uint64_t idx = tile * kThreads + (uint64_t)(c >> 2);
+		uint4 v = make_uint4(0, 0, 0, 0);
+		if (idx < k.n) {
+			uint64_t a = frame_off<GENERAL>(k, idx) + (uint64_t)(c & 3) * 16;
+			if (!GENERAL || a + 16 <= k.frames_len) {
+				v = gcl::load16_nt(k.frames + a);
+			} else {
+				uint32_t w[4];
+				for (int b = 0; b < 4; b++)
+					w[b] = frame_byte(k, a + 4 * b) | frame_byte(k, a + 4 * b + 1) << 8 |
+					       frame_byte(k, a + 4 * b + 2) << 16 |
+					       (uint32_t)frame_byte(k, a + 4 * b + 3) << 24;
+				v = make_uint4(w[0], w[1], w[2], w[3]);
+			}
+		}
+		r[j] = v;
+	}
+}
+
+/* dword at byte offset b (4-aligned, < 64) of this lane's staged header */
+__device__ __forceinline__ uint32_t tile_dword(const uint4 *tile, int p, int b)
+{
+	const uint32_t *t32 = (const uint32_t *)tile;
+	return t32[tile_slot(p, b >> 4) * 4 + ((b & 15) >> 2)];
+}
+
+template <int MODE, bool TLDS, bool GENERAL>
+__global__ void __launch_bounds__(kThreads)
+classify_kernel(KParams k)
+{
+	extern __shared__ uint4 smem[];
+	uint4 *tile = smem;
+	uint32_t *hist = (uint32_t *)(smem + kTileBytes / 16);
+	uint8_t *lds_tab = (uint8_t *)(hist + ((k.max_rt + 3) & ~3u));
+	const int tid = threadIdx.x;
+
+	/* stage tables and zero the histogram */
+	for (uint32_t i = tid; i < k.max_rt; i += kThreads)
+		hist[i] = 0;
+	const uint8_t *tab = k.tables;
+	if (TLDS) {
+		const uint4 *src = (const uint4 *)k.tables;
+		uint4 *dst = (uint4 *)lds_tab;
+		for (uint32_t i = tid; i < k.tables_lds_bytes / 16; i += kThreads)
+			dst[i] = src[i];
+		tab = lds_tab;
+	}
+	const uint2 *ipt = (const uint2 *)tab;
+	const RtEntry *rtab = (const RtEntry *)(tab + k.off_rt);
+	const uint8_t *flow = tab + k.off_flow;
+	const uint32_t *toep = (const uint32_t *)(tab + k.off_toep);
+	__syncthreads();
+
+	uint32_t n_flowtag = 0, n_hashmiss = 0, n_unreg = 0, n_unhandled = 0;
+	uint4 r[4];
+	uint64_t t = blockIdx.x;
+	if (t < k.ntiles)
+		load_tile<GENERAL>(k, t, r);
+
+	for (; t < k.ntiles; t += gridDim.x) {
+#pragma unroll
+		for (int j = 0; j < 4; j++) {
+			int c = j * kThreads + tid;
+			tile[tile_slot(c >> 2, c & 3)] = r[j];
+		}
+		__syncthreads();
+		uint64_t nt = t + gridDim.x;
+		if (nt < k.ntiles)
+			load_tile<GENERAL>(k, nt, r); /* in flight while this tile is parsed */
+
+		uint64_t idx = t * kThreads + tid;
+		if (idx < k.n) {
+			const uint4 w0 = tile[tile_slot(tid, 0)];
+			const uint4 w1 = tile[tile_slot(tid, 1)];
+			const uint4 w2 = tile[tile_slot(tid, 2)];
+			const uint32_t d3 = w0.w, d5 = w1.y, d6 = w1.z, d7 = w1.w;
+			const uint32_t d8 = w2.x, d9 = w2.y, d10 = w2.z;
+
+			const uint32_t et = gcl::bswap16(d3 & 0xFFFF);       /* rx.c:154 */
+			const uint32_t vihl = (d3 >> 16) & 0xFF;
+			const uint32_t frag = gcl::bswap16(d5 & 0xFFFF);     /* also ARP op */
+			const uint32_t proto = d5 >> 24;
+			const uint32_t saddr = gcl::bswap32(gcl::mid32(d6, d7));
+			const uint32_t daddr = gcl::bswap32(gcl::mid32(d7, d8));   /* rx.c:159 */
+			const uint32_t arp_tip = gcl::bswap32(gcl::mid32(d9, d10)); /* rx.c:167 */
+			const uint32_t flags = (GENERAL && k.olflags) ? k.olflags[idx] : k.default_flags;
+
+			/* steering hash */
+			uint32_t hash = 0;
+			if (MODE == GCL_HASH_NIC) {
+				if (k.rss)
+					hash = k.rss[idx];
+			} else {
+				const uint32_t ihl = vihl & 0xF;
+				const bool hashable = et == GCL_ETHTYPE_IP && ihl >= 5 &&
+				                      (frag & 0x3FFF) == 0 && (proto == 6 || proto == 17);
+				if (hashable) {
+					uint32_t sport, dport;
+					if (ihl == 5) {
+						sport = gcl::bswap16(d8 >> 16);
+						dport = gcl::bswap16(d9 & 0xFFFF);
+					} else if (ihl <= 11) {
+						int o = 14 + 4 * (int)ihl;
+						sport = gcl::bswap16(tile_dword(tile, tid, o - 2) >> 16);
+						dport = gcl::bswap16(tile_dword(tile, tid, o + 2) & 0xFFFF);
+					} else {
+						uint64_t a = frame_off<GENERAL>(k, idx) + 14 + 4 * ihl;
+						sport = (uint32_t)frame_byte(k, a) << 8 | frame_byte(k, a + 1);
+						dport = (uint32_t)frame_byte(k, a + 2) << 8 | frame_byte(k, a + 3);
+					}
+					if (MODE == GCL_HASH_JENKINS) {
+						hash = gcl::jhash_5tuple(saddr, daddr, sport, dport, proto);
+					} else {
+						hash = toep[0 * 256 + (saddr >> 24)] ^
+						       toep[1 * 256 + ((saddr >> 16) & 0xFF)] ^
+						       toep[2 * 256 + ((saddr >> 8) & 0xFF)] ^
+						       toep[3 * 256 + (saddr & 0xFF)] ^
+						       toep[4 * 256 + (daddr >> 24)] ^
+						       toep[5 * 256 + ((daddr >> 16) & 0xFF)] ^
+						       toep[6 * 256 + ((daddr >> 8) & 0xFF)] ^
+						       toep[7 * 256 + (daddr & 0xFF)] ^
+						       toep[8 * 256 + (sport >> 8)] ^
+						       toep[9 * 256 + (sport & 0xFF)] ^
+						       toep[10 * 256 + (dport >> 8)] ^
+						       toep[11 * 256 + (dport & 0xFF)];
+					}
+				}
+			}
+			if (k.cflags & GCL_CFG_HASH16)
+				hash &= 0xFFFF;
+
+			int p = -1;
+			uint32_t action = GCL_ACT_DELIVER;
+			/* hardware flow tag, rx.c:131-146 */
+			if (GENERAL && (flags & GCL_F_FDIR_ID)) {
+				uint32_t mark = k.fdir ? k.fdir[idx] : 0;
+				n_flowtag++;
+				if (mark < k.max_rt && rtab[mark].tc != 0) {
+					p = (int)mark;
+					action = GCL_ACT_F_FDIR;
+				}
+			}
+			if (p < 0) {
+				uint32_t dst = 0;
+				bool lookup = true;
+				if (et == GCL_ETHTYPE_IP) {
+					dst = daddr;
+					n_hashmiss += !(flags & GCL_F_RSS_HASH); /* rx.c:160-163 */
+				} else if (et == GCL_ETHTYPE_ARP) {
+					dst = arp_tip;
+					if ((k.cflags & GCL_CFG_AZURE_ARP) && frag == GCL_ARP_OP_REPLY) {
+						action = GCL_ACT_BROADCAST; /* rx.c:171-190 */
+						lookup = false;
+					}
+				} else {
+					action = GCL_ACT_DROP_ETHERTYPE; /* rx.c:191-194 */
+					n_unhandled++;
+					lookup = false;
+				}
+				if (lookup) {
+					/* ip_to_proc: open addressing keyed by rte_jhash(&ip, 4, 0) */
+					uint32_t s = gcl::jhash_u32(dst) & k.ipt_mask;
+					for (;;) {
+						uint2 e = ipt[s];
+						if (e.y == kEmpty)
+							break;
+						if (e.x == dst) {
+							p = (int)e.y;
+							break;
+						}
+						s = (s + 1) & k.ipt_mask;
+					}
+					if (p < 0) {
+						if ((k.cflags & GCL_CFG_AZURE_ARP) && et == GCL_ETHTYPE_ARP &&
+						    frag == GCL_ARP_OP_REQUEST) {
+							action = GCL_ACT_ARP_RESPOND; /* rx.c:200-203 */
+						} else {
+							action = GCL_ACT_DROP_UNREG; /* rx.c:205, :232 */
+							n_unreg++;
+							n_unhandled++;
+						}
+					}
+				}
+			}
+
+			uint32_t uniq = GCL_NO_RUNTIME, thr = GCL_NO_THREAD;
+			if (p >= 0) {
+				/* rx_send_to_runtime, rx.c:55-72 */
+				const RtEntry re = rtab[p];
+				uniq = (uint32_t)p;
+				if (re.active) {
+					uint64_t M = (uint64_t)re.m_hi << 32 | re.m_lo;
+					thr = flow[re.flow_off + gcl::fastmod(hash, M, re.tc)];
+				} else {
+					action |= GCL_ACT_WAKE;
+				}
+				atomicAdd(&hist[p], 1u);
+			}
+			k.verdicts[idx] = make_uint2(hash, uniq | thr << 16 | action << 24);
+		}
+		__syncthreads();
+	}
+
+	/* flush per-block counters */
+	for (uint32_t i = tid; i < k.max_rt; i += kThreads) {
+		uint32_t v = hist[i];
+		if (v && k.counts)
+			atomicAdd(&k.counts[i], (unsigned long long)v);
+	}
+	if (k.stats) {
+		for (int off = 32; off > 0; off >>= 1) {
+			n_flowtag += __shfl_xor(n_flowtag, off);
+			n_hashmiss += __shfl_xor(n_hashmiss, off);
+			n_unreg += __shfl_xor(n_unreg, off);
+			n_unhandled += __shfl_xor(n_unhandled, off);
+		}
+		if ((tid & 63) == 0) {
+			if (n_flowtag)
+				atomicAdd(&k.stats[GCL_RX_FLOW_TAG_MATCH], (unsigned long long)n_flowtag);
+			if (n_hashmiss)
+				atomicAdd(&k.stats[GCL_RX_HASH_MISSING], (unsigned long long)n_hashmiss);
+			if (n_unreg)
+				atomicAdd(&k.stats[GCL_RX_UNREGISTERED_MAC], (unsigned long long)n_unreg);
+			if (n_unhandled)
+				atomicAdd(&k.stats[GCL_RX_UNHANDLED], (unsigned long long)n_unhandled);
+		}
+		if (blockIdx.x == 0 && tid == 0)
+			atomicAdd(&k.stats[GCL_RX_PULLED], (unsigned long long)k.n);
+	}
+}
+
+/* ------------------------------------------------------------------------
+ * Synthetic generator kernel: one lane per packet writes its 64-B header.
+ */
+struct Hdr {
+	uint32_t w[16];
+	__device__ void b8(int o, uint32_t v) { w[o >> 2] |= (v & 0xFF) << ((o & 3) * 8); }
+	__device__ void b16(int o, uint32_t v) { b8(o, v >> 8); b8(o + 1, v); }
+	__device__ void b32(int o, uint32_t v) { b16(o, v >> 16); b16(o + 2, v); }
+};
+
+__device__ __forceinline__ void gen_eth(Hdr &h, uint64_t srcbits, uint32_t et)
+{
+	h.b8(0, 0x02); h.b8(5, 0x01); /* dst 02:00:00:00:00:01 */
+	h.b8(6, 0x02);
+	h.b32(8, (uint32_t)srcbits);
+	h.b16(12, et);
+}
+
+__device__ __forceinline__ void gen_ipv4(Hdr &h, uint32_t totlen, uint32_t id,
+                                         uint32_t proto, uint32_t saddr, uint32_t daddr)
+{
+	h.b8(14, 0x45);
+	h.b16(16, totlen);
+	h.b16(18, id);
+	h.b16(20, 0x4000);
+	h.b8(22, 64);
+	h.b8(23, proto);
+	h.b32(26, saddr);
+	h.b32(30, daddr);
+	uint32_t s = 0x4500 + (totlen & 0xFFFF) + (id & 0xFFFF) + 0x4000 + (64u << 8 | proto) +
+	             (saddr >> 16) + (saddr & 0xFFFF) + (daddr >> 16) + (daddr & 0xFFFF);
+	while (s >> 16)
+		s = (s & 0xFFFF) + (s >> 16);
+	h.b16(24, ~s & 0xFFFF);
+}
+
+struct GParams {
+	uint32_t workload, nruntimes;
+	uint64_t seed, n, stride;
+	uint32_t rank, world;
+	uint64_t shard_block;
+	const uint64_t *zipf;
+	uint32_t nflows;
+	uint8_t *frames;
+	uint8_t *olflags;
+	uint32_t *rss;
+};
+
+__device__ __forceinline__ uint32_t runtime_ip(uint32_t r) { return 0x0A000000u + r + 1; }
+
+__global__ void __launch_bounds__(256) generate_kernel(GParams p)
+{
+	uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	if (j >= p.n)
+		return;
+	uint64_t g = j;
+	if (p.shard_block && p.world > 1)
+		g = ((j / p.shard_block) * p.world + p.rank) * p.shard_block + j % p.shard_block;
+	const uint64_t r0 = gcl::rw(p.seed, g, 0), r1 = gcl::rw(p.seed, g, 1);
+	uint32_t fl = GCL_F_RSS_HASH | GCL_F_IP_CKSUM_GOOD;
+	Hdr h;
+#pragma unroll
+	for (int i = 0; i < 16; i++)
+		h.w[i] = 0;
+
+	if (p.workload == GCL_WL_UDP64) {
+		uint32_t rt = (uint32_t)(((uint64_t)(uint32_t)r1 * p.nruntimes) >> 32);
+		gen_eth(h, r1 >> 32, GCL_ETHTYPE_IP);
+		gen_ipv4(h, 50, (uint32_t)(r1 >> 16) & 0xFFFF, 17, (uint32_t)r0, runtime_ip(rt));
+		h.b16(34, (uint32_t)(r0 >> 32) & 0xFFFF);
+		h.b16(36, (uint32_t)(r0 >> 48));
+		h.b16(38, 30);
+	} else if (p.workload == GCL_WL_TCP1500_ZIPF) {
+		uint32_t lo = 0, hi = p.nflows - 1;
+		while (lo < hi) {
+			uint32_t mid = lo + (hi - lo) / 2;
+			if (r0 < p.zipf[mid])
+				hi = mid;
+			else
+				lo = mid + 1;
+		}
+		const uint32_t flow = lo;
+		const uint64_t fr = gcl::rw(p.seed ^ 0xF10F10F10F10F10Full, flow, 0);
+		const uint32_t rt = flow % p.nruntimes;
+		gen_eth(h, fr >> 16, GCL_ETHTYPE_IP);
+		gen_ipv4(h, 1486, (uint32_t)r1 & 0xFFFF, 6, (uint32_t)fr, runtime_ip(rt));
+		h.b16(34, (uint32_t)(fr >> 32) & 0xFFFF);
+		h.b16(36, (uint32_t)(fr >> 48));
+		h.b32(38, (uint32_t)(r1 >> 32));
+		h.b8(46, 0x50);
+		h.b8(47, 0x10);
+		h.b16(48, 0xFFFF);
+	} else {
+		const uint64_t r2 = gcl::rw(p.seed, g, 2);
+		const uint32_t kind = (uint32_t)r0 % 100;
+		const uint32_t rt = (uint32_t)(((uint64_t)(uint32_t)r1 * p.nruntimes) >> 32);
+		bool unreg = (uint32_t)(r0 >> 40) % 20 == 0;
+		uint32_t dst = unreg ? (0xC0A80000u | (uint32_t)(r1 >> 48)) : runtime_ip(rt);
+		if (kind < 70) {
+			uint32_t len = 64 + (uint32_t)(r1 >> 32) % (9014 - 64 + 1);
+			uint32_t proto = (r0 >> 32) & 1 ? 6 : 17;
+			gen_eth(h, r2 >> 8, GCL_ETHTYPE_IP);
+			gen_ipv4(h, len - 14, (uint32_t)r2 & 0xFFFF, proto, (uint32_t)r2, dst);
+			h.b16(34, (uint32_t)(r2 >> 32) & 0xFFFF);
+			h.b16(36, (uint32_t)(r2 >> 48));
+		} else if (kind < 90) {
+			gen_eth(h, r2 >> 8, GCL_ETHTYPE_IPV6);
+			h.b8(14, 0x60);
+			h.b16(18, (uint32_t)(r1 >> 32) & 0x1FFF);
+			h.b8(20, 17);
+			h.b8(21, 64);
+			h.b32(22, (uint32_t)r2);
+			h.b32(38, dst);
+			fl = 0;
+		} else {
+			unreg = (uint32_t)(r0 >> 40) % 10 == 0;
+			dst = unreg ? (0xC0A80000u | (uint32_t)(r1 >> 48)) : runtime_ip(rt);
+			gen_eth(h, r2 >> 8, GCL_ETHTYPE_ARP);
+			h.b16(14, 1);
+			h.b16(16, 0x0800);
+			h.b8(18, 6);
+			h.b8(19, 4);
+			h.b16(20, (r0 >> 33) & 1 ? GCL_ARP_OP_REPLY : GCL_ARP_OP_REQUEST);
+			h.b32(24, (uint32_t)(r2 >> 16));
+			h.b32(28, (uint32_t)r2);
+			h.b32(38, dst);
+			fl = 0;
+		}
+	}
+	uint4 *dst4 = (uint4 *)(p.frames + j * p.stride);
+#pragma unroll
+	for (int i = 0; i < 4; i++)
+		dst4[i] = make_uint4(h.w[4 * i], h.w[4 * i + 1], h.w[4 * i + 2], h.w[4 * i + 3]);
+	if (p.olflags)
+		p.olflags[j] = (uint8_t)fl;
+	if (p.rss)
+		p.rss[j] = (uint32_t)gcl::rw(p.seed, g, 3);
+}
+
+} // namespace
+
+/* ==========================================================================
+ * Host side of the C ABI.
+ */
+struct gcl_ctx {
+	int device;
+	struct gcl_cfg cfg;
+	int num_cus;
+	/* host mirror of the tables (dp.clients_by_id + ip_to_proc + flow_tbl) */
+	struct Rt {
+		bool present;
+		uint32_t ip;
+		uint16_t tc, active;
+		uint8_t flow[GCL_NCPU];
+	};
+	std::vector<Rt> rt;
+	uint32_t ipt_slots;
+	uint32_t off_rt, off_flow, off_toep, image_cap;
+	uint32_t flow_used;
+	bool dirty;
+	/* two device images + pinned staging, each guarded by an event */
+	uint8_t *dimg[2];
+	hipEvent_t img_free[2];
+	uint8_t *staging;
+	hipEvent_t staging_free;
+	int cur;
+	hipStream_t last_stream;
+	/* profiling */
+	std::vector<hipEvent_t> ev_pool;
+	std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending;
+	double prof_ms;
+	uint64_t prof_launches;
+};
+
+extern "C" {
+uint32_t gcl_jenkins_hash(const void *key, size_t len);
+uint32_t gcl_toeplitz(const uint8_t *key, size_t keylen, const uint8_t *input, size_t len);
+}
+
+static uint32_t pow2_at_least(uint32_t x)
+{
+	uint32_t p = 1;
+	while (p < x)
+		p <<= 1;
+	return p;
+}
+
+static uint32_t align16(uint32_t x) { return (x + 15u) & ~15u; }
+
+extern "C" int gcl_open(int hip_device, const struct gcl_cfg *cfg, struct gcl_ctx **out)
+{
+	int ndev = 0;
+	if (!cfg || !out || cfg->max_runtimes == 0 || cfg->max_runtimes > GCL_MAX_PROC ||
+	    cfg->hash_mode > GCL_HASH_TOEPLITZ)
+		return -EINVAL;
+	if (hipGetDeviceCount(&ndev) != hipSuccess || hip_device < 0 || hip_device >= ndev)
+		return -ENODEV;
+	if (hipSetDevice(hip_device) != hipSuccess)
+		return -ENODEV;
+
+	gcl_ctx *c = new (std::nothrow) gcl_ctx();
+	if (!c)
+		return -ENOMEM;
+	c->device = hip_device;
+	c->cfg = *cfg;
+	hipDeviceGetAttribute(&c->num_cus, hipDeviceAttributeMultiprocessorCount, hip_device);
+	c->rt.resize(cfg->max_runtimes);
+	c->ipt_slots = pow2_at_least(cfg->max_runtimes * 2 < 16 ? 16 : cfg->max_runtimes * 2);
+	c->off_rt = c->ipt_slots * 8;
+	c->off_flow = c->off_rt + cfg->max_runtimes * 16;
+	/* the Toeplitz LUT offset depends on flow_used; reserve worst case */
+	c->image_cap = c->off_flow + cfg->max_runtimes * GCL_NCPU + 16 + kToepBytes;
+	c->flow_used = 0;
+	c->dirty = true;
+	c->cur = 0;
+	c->last_stream = nullptr;
+	c->prof_ms = 0;
+	c->prof_launches = 0;
+	for (int i = 0; i < 2; i++) {
+		c->dimg[i] = nullptr;
+		if (hipMalloc(&c->dimg[i], c->image_cap) != hipSuccess)
+			goto fail;
+		hipEventCreateWithFlags(&c->img_free[i], hipEventDisableTiming);
+	}
+	if (hipHostMalloc(&c->staging, c->image_cap, hipHostMallocDefault) != hipSuccess)
+		goto fail;
+	hipEventCreateWithFlags(&c->staging_free, hipEventDisableTiming);
+	*out = c;
+	return 0;
+fail:
+	for (int i = 0; i < 2; i++)
+		if (c->dimg[i])
+			hipFree(c->dimg[i]);
+	delete c;
+	return -ENOMEM;
+}
+
+extern "C" void gcl_close(struct gcl_ctx *c)
+{
+	if (!c)
+		return;
+	hipSetDevice(c->device);
+	hipDeviceSynchronize();
+	for (int i = 0; i < 2; i++) {
+		hipFree(c->dimg[i]);
+		hipEventDestroy(c->img_free[i]);
+	}
+	hipHostFree(c->staging);
+	hipEventDestroy(c->staging_free);
+	for (auto &pr : c->ev_pending) {
+		hipEventDestroy(pr.first);
+		hipEventDestroy(pr.second);
+	}
+	for (auto e : c->ev_pool)
+		hipEventDestroy(e);
+	delete c;
+}
+
+static uint32_t ip_owner(const gcl_ctx *c, uint32_t ip)
+{
+	for (uint32_t i = 0; i < c->cfg.max_runtimes; i++)
+		if (c->rt[i].present && c->rt[i].ip == ip)
+			return i;
+	return kEmpty;
+}
+
+extern "C" int gcl_runtime_set(struct gcl_ctx *c, uint16_t uniqid, uint32_t ip_host,
+                               uint16_t thread_count, uint16_t active_count,
+                               const uint16_t *flow_tbl)
+{
+	if (!c || uniqid >= c->cfg.max_runtimes || thread_count == 0 ||
+	    thread_count > GCL_NCPU || active_count > thread_count)
+		return -EINVAL;
+	if (active_count) {
+		if (!flow_tbl)
+			return -EINVAL;
+		for (int i = 0; i < thread_count; i++)
+			if (flow_tbl[i] >= thread_count)
+				return -EINVAL;
+	}
+	uint32_t owner = ip_owner(c, ip_host);
+	if (owner != kEmpty && owner != uniqid)
+		return -EEXIST; /* dp_clients.c:174-179 */
+	gcl_ctx::Rt &r = c->rt[uniqid];
+	r.present = true;
+	r.ip = ip_host;
+	r.tc = thread_count;
+	r.active = active_count;
+	memset(r.flow, 0, sizeof(r.flow));
+	if (active_count)
+		for (int i = 0; i < thread_count; i++)
+			r.flow[i] = (uint8_t)flow_tbl[i];
+	c->dirty = true;
+	return 0;
+}
+
+extern "C" int gcl_runtime_del(struct gcl_ctx *c, uint16_t uniqid)
+{
+	if (!c || uniqid >= c->cfg.max_runtimes || !c->rt[uniqid].present)
+		return -ENOENT;
+	c->rt[uniqid] = gcl_ctx::Rt();
+	c->dirty = true;
+	return 0;
+}
+
+/* Serialise the host mirror into the staging buffer. Returns image bytes. */
+static uint32_t build_image(gcl_ctx *c)
+{
+	uint8_t *img = c->staging;
+	const uint32_t max_rt = c->cfg.max_runtimes;
+	uint2 *ipt = (uint2 *)img;
+	for (uint32_t i = 0; i < c->ipt_slots; i++)
+		ipt[i] = make_uint2(0, kEmpty);
+	RtEntry *re = (RtEntry *)(img + c->off_rt);
+	uint8_t *flow = img + c->off_flow;
+	uint32_t fo = 0;
+	for (uint32_t u = 0; u < max_rt; u++) {
+		const gcl_ctx::Rt &r = c->rt[u];
+		RtEntry e = {};
+		if (r.present) {
+			uint64_t M = r.tc == 1 ? 0 : (UINT64_MAX / r.tc + 1);
+			e.m_lo = (uint32_t)M;
+			e.m_hi = (uint32_t)(M >> 32);
+			e.tc = r.tc;
+			e.active = r.active;
+			e.flow_off = fo;
+			memcpy(flow + fo, r.flow, r.tc);
+			fo += r.tc;
+			uint32_t s = gcl_jenkins_hash(&r.ip, 4) & (c->ipt_slots - 1);
+			while (ipt[s].y != kEmpty)
+				s = (s + 1) & (c->ipt_slots - 1);
+			ipt[s] = make_uint2(r.ip, u);
+		}
+		re[u] = e;
+	}
+	c->flow_used = fo;
+	c->off_toep = align16(c->off_flow + fo);
+	uint32_t bytes = c->off_toep;
+	if (c->cfg.hash_mode == GCL_HASH_TOEPLITZ) {
+		uint32_t *lut = (uint32_t *)(img + c->off_toep);
+		for (int i = 0; i < 12; i++)
+			for (int v = 0; v < 256; v++) {
+				uint8_t in[12] = {0};
+				in[i] = (uint8_t)v;
+				lut[i * 256 + v] = gcl_toeplitz(c->cfg.rss_key, 40, in, 12);
+			}
+		bytes += kToepBytes;
+	}
+	return align16(bytes);
+}
+
+static hipEvent_t prof_event(gcl_ctx *c)
+{
+	if (!c->ev_pool.empty()) {
+		hipEvent_t e = c->ev_pool.back();
+		c->ev_pool.pop_back();
+		return e;
+	}
+	hipEvent_t e;
+	hipEventCreate(&e);
+	return e;
+}
+
+template <int MODE, bool TLDS, bool GENERAL>
+static hipError_t launch_t(const KParams &k, uint32_t lds, int num_cus, hipStream_t s)
+{
+	static std::mutex mu;
+	static int occ_cache[64];
+	static uint32_t occ_lds[64];
+	int slot = (lds / 1024) & 63;
+	int occ;
+	if (lds > 64 * 1024) {
+		static bool raised = false;
+		if (!raised) {
+			hipFuncSetAttribute((const void *)classify_kernel<MODE, TLDS, GENERAL>,
+			                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+			raised = true;
+		}
+	}
+	{
+		std::lock_guard<std::mutex> g(mu);
+		if (occ_lds[slot] != lds + 1) {
+			int o = 0;
+			if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+			        &o, classify_kernel<MODE, TLDS, GENERAL>, kThreads, lds) != hipSuccess ||
+			    o < 1)
+				o = 1;
+			occ_cache[slot] = o;
+			occ_lds[slot] = lds + 1;
+		}
+		occ = occ_cache[slot];
+	}
+	uint64_t grid = (uint64_t)num_cus * (uint64_t)occ;
+	if (grid > k.ntiles)
+		grid = k.ntiles;
+	if (grid < 1)
+		grid = 1;
+	hipLaunchKernelGGL((classify_kernel<MODE, TLDS, GENERAL>), dim3((unsigned)grid),
+	                   dim3(kThreads), lds, s, k);
+	return hipGetLastError();
+}
+
+template <int MODE>
+static hipError_t launch_mode(const KParams &k, bool tlds, bool general, uint32_t lds,
+                              int num_cus, hipStream_t s)
+{
+	if (tlds)
+		return general ? launch_t<MODE, true, true>(k, lds, num_cus, s)
+		               : launch_t<MODE, true, false>(k, lds, num_cus, s);
+	return general ? launch_t<MODE, false, true>(k, lds, num_cus, s)
+	               : launch_t<MODE, false, false>(k, lds, num_cus, s);
+}
+
+extern "C" int gcl_classify(struct gcl_ctx *c, const struct gcl_batch *b,
+                            struct gcl_verdict *verdicts, uint64_t *runtime_counts,
+                            uint64_t *stats, void *hip_stream)
+{
+	if (!c || !b)
+		return -EINVAL;
+	hipStream_t s = (hipStream_t)hip_stream;
+	if (b->n == 0)
+		return 0;
+	if (!b->frames || (!b->offs && (b->stride < 16 || (b->stride & 15))))
+		return -EINVAL;
+	if (!verdicts)
+		return -EINVAL;
+	hipSetDevice(c->device);
+
+	/* upload a new table snapshot on this stream if anything changed */
+	if (c->dirty) {
+		hipEventSynchronize(c->staging_free);
+		uint32_t bytes = build_image(c);
+		int nxt = c->cur ^ 1;
+		hipStreamWaitEvent(s, c->img_free[nxt], 0);
+		if (hipMemcpyAsync(c->dimg[nxt], c->staging, bytes, hipMemcpyHostToDevice, s) !=
+		    hipSuccess)
+			return -EIO;
+		hipEventRecord(c->staging_free, s);
+		c->cur = nxt;
+		c->dirty = false;
+	}
+
+	KParams k = {};
+	k.frames = b->frames;
+	k.frames_len = b->frames_len;
+	k.stride = b->stride;
+	k.offs = b->offs;
+	k.olflags = b->olflags;
+	k.rss = b->rss;
+	k.fdir = b->fdir_hi;
+	k.n = b->n;
+	k.ntiles = (b->n + kThreads - 1) / kThreads;
+	k.verdicts = (uint2 *)verdicts;
+	k.counts = (unsigned long long *)runtime_counts;
+	k.stats = (unsigned long long *)stats;
+	k.tables = c->dimg[c->cur];
+	k.ipt_mask = c->ipt_slots - 1;
+	k.max_rt = c->cfg.max_runtimes;
+	k.off_rt = c->off_rt;
+	k.off_flow = c->off_flow;
+	k.off_toep = c->off_toep;
+	k.cflags = c->cfg.flags;
+	k.default_flags = c->cfg.default_olflags;
+
+	/* the specialised fast path needs every header granule in range */
+	bool general = b->offs || b->olflags || b->fdir_hi ||
+	               (c->cfg.default_olflags & GCL_F_FDIR_ID) ||
+	               b->frames_len < (b->n - 1) * b->stride + GCL_HDR_GRANULE;
+	uint32_t tab_bytes = c->off_toep +
+	                     (c->cfg.hash_mode == GCL_HASH_TOEPLITZ ? kToepBytes : 0);
+	tab_bytes = align16(tab_bytes);
+	uint32_t hist_bytes = ((c->cfg.max_runtimes + 3) & ~3u) * 4;
+	bool tlds = tab_bytes <= kLdsTableBudget;
+	k.tables_lds_bytes = tlds ? tab_bytes : 0;
+	uint32_t lds = kTileBytes + hist_bytes + (tlds ? tab_bytes : 0);
+
+	hipEvent_t e0 = nullptr, e1 = nullptr;
+	if (c->cfg.flags & GCL_CFG_PROFILE) {
+		e0 = prof_event(c);
+		e1 = prof_event(c);
+		hipEventRecord(e0, s);
+	}
+	hipError_t err;
+	switch (c->cfg.hash_mode) {
+	case GCL_HASH_NIC:
+		err = launch_mode<GCL_HASH_NIC>(k, tlds, general, lds, c->num_cus, s);
+		break;
+	case GCL_HASH_JENKINS:
+		err = launch_mode<GCL_HASH_JENKINS>(k, tlds, general, lds, c->num_cus, s);
+		break;
+	default:
+		err = launch_mode<GCL_HASH_TOEPLITZ>(k, tlds, general, lds, c->num_cus, s);
+		break;
+	}
+	if (e0) {
+		hipEventRecord(e1, s);
+		c->ev_pending.push_back({e0, e1});
+	}
+	hipEventRecord(c->img_free[c->cur], s);
+	c->last_stream = s;
+	return err == hipSuccess ? 0 : -EIO;
+}
+
+extern "C" int gcl_sync(struct gcl_ctx *c)
+{
+	if (!c)
+		return -EINVAL;
+	hipSetDevice(c->device);
+	return hipStreamSynchronize(c->last_stream) == hipSuccess ? 0 : -EIO;
+}
+
+extern "C" int gcl_kernel_time(struct gcl_ctx *c, double *ms, uint64_t *launches, int reset)
+{
+	if (!c)
+		return -EINVAL;
+	hipSetDevice(c->device);
+	for (auto &pr : c->ev_pending) {
+		float f = 0;
+		hipEventSynchronize(pr.second);
+		hipEventElapsedTime(&f, pr.first, pr.second);
+		c->prof_ms += f;
+		c->prof_launches++;
+		c->ev_pool.push_back(pr.first);
+		c->ev_pool.push_back(pr.second);
+	}
+	c->ev_pending.clear();
+	if (ms)
+		*ms = c->prof_ms;
+	if (launches)
+		*launches = c->prof_launches;
+	if (reset) {
+		c->prof_ms = 0;
+		c->prof_launches = 0;
+	}
+	return 0;
+}
+
+extern "C" int gcl_generate(const struct gcl_gen_params *p, uint8_t *frames, uint8_t *olflags,
+                            uint32_t *rss, void *hip_stream)
+{
+	if (!p || !frames || p->stride < 64 || (p->stride & 15) || p->nruntimes == 0 ||
+	    p->workload > GCL_WL_MIXED)
+		return -EINVAL;
+	if (p->workload == GCL_WL_TCP1500_ZIPF && (!p->zipf_cdf || !p->nflows))
+		return -EINVAL;
+	if (p->n == 0)
+		return 0;
+	GParams g = {};
+	g.workload = p->workload;
+	g.nruntimes = p->nruntimes;
+	g.seed = p->seed;
+	g.n = p->n;
+	g.stride = p->stride;
+	g.rank = p->rank;
+	g.world = p->world;
+	g.shard_block = p->shard_block;
+	g.zipf = p->zipf_cdf;
+	g.nflows = p->nflows;
+	g.frames = frames;
+	g.olflags = olflags;
+	g.rss = rss;
+	uint64_t blocks = (p->n + 255) / 256;
+	hipLaunchKernelGGL(generate_kernel, dim3((unsigned)blocks), dim3(256), 0,
+	                   (hipStream_t)hip_stream, g);
+	return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+extern "C" const char *gcl_version(void) { return GCL_VERSION; }

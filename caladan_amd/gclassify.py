@@ -1,0 +1,289 @@
+"""Python binding of libgclassify.so (ctypes), for tests and bench.py.
+
+The product boundary is the C ABI in include/gclassify.h; the dataplane side
+that consumes verdicts is C (include/gcl_host.h).  This module is a thin
+mirror of that ABI with the reference's names and error behaviour: every call
+that returns -errno raises OSError(errno) here, the way the reference's init
+paths fail (rx_init, dp_clients_init return -1/-errno).
+
+There is no CPU fallback: if the shared library is missing, importing the
+binding raises, and classify() needs device (HBM) buffers.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libgclassify.so")
+
+GCL_MAX_PROC = 4096
+GCL_NCPU = 256
+GCL_RX_BURST_SIZE = 64
+
+HASH_NIC, HASH_JENKINS, HASH_TOEPLITZ = 0, 1, 2
+HASH_MODES = {"nic": HASH_NIC, "jenkins": HASH_JENKINS, "toeplitz": HASH_TOEPLITZ}
+
+CFG_AZURE_ARP, CFG_HASH16, CFG_PROFILE = 0x1, 0x2, 0x4
+
+F_RSS_HASH, F_FDIR_ID = 0x01, 0x02
+F_IP_CKSUM_MASK, F_IP_CKSUM_UNKNOWN, F_IP_CKSUM_BAD = 0x0C, 0x00, 0x04
+F_IP_CKSUM_GOOD, F_IP_CKSUM_NONE = 0x08, 0x0C
+
+ACT_DELIVER, ACT_WAKE, ACT_DROP_ETHERTYPE, ACT_DROP_UNREG = 0, 1, 2, 3
+ACT_BROADCAST, ACT_ARP_RESPOND = 4, 5
+ACT_MASK, ACT_F_FDIR = 0x7F, 0x80
+NO_RUNTIME, NO_THREAD = 0xFFFF, 0xFF
+
+(RX_UNREGISTERED_MAC, RX_UNICAST_FAIL, RX_BROADCAST_FAIL, RX_FLOW_TAG_MATCH,
+ RX_UNHANDLED, RX_HASH_MISSING, RX_PULLED) = range(7)
+NR_STATS = 8
+STAT_NAMES = ["RX_UNREGISTERED_MAC", "RX_UNICAST_FAIL", "RX_BROADCAST_FAIL",
+              "RX_FLOW_TAG_MATCH", "RX_UNHANDLED", "RX_HASH_MISSING", "RX_PULLED"]
+
+WL_UDP64, WL_TCP1500_ZIPF, WL_MIXED = 0, 1, 2
+
+# Fixed 40-B Toeplitz key of the reference (iokernel/directpath/core.c:35-39)
+CALADAN_RSS_KEY = bytes([
+    0x82, 0x19, 0xFA, 0x80, 0xA4, 0x31, 0x06, 0x59, 0x3E, 0x3F, 0x9A,
+    0xAC, 0x3D, 0xAE, 0xD6, 0xD9, 0xF5, 0xFC, 0x0C, 0x63, 0x94, 0xBF,
+    0x8F, 0xDE, 0xD2, 0xC5, 0xE2, 0x04, 0xB1, 0xCF, 0xB1, 0xB1, 0xA1,
+    0x0D, 0x6D, 0x86, 0xBA, 0x61, 0x78, 0xEB])
+
+VERDICT_DTYPE = np.dtype([("hash", "<u4"), ("uniqid", "<u2"), ("thread", "u1"), ("action", "u1")])
+
+
+class GclCfg(ctypes.Structure):
+    _fields_ = [("max_runtimes", ctypes.c_uint32), ("hash_mode", ctypes.c_uint32),
+                ("flags", ctypes.c_uint32), ("default_olflags", ctypes.c_uint8),
+                ("rss_key", ctypes.c_uint8 * 40), ("pad", ctypes.c_uint8 * 3)]
+
+
+class GclBatch(ctypes.Structure):
+    _fields_ = [("frames", ctypes.c_void_p), ("frames_len", ctypes.c_uint64),
+                ("stride", ctypes.c_uint64), ("offs", ctypes.c_void_p),
+                ("olflags", ctypes.c_void_p), ("rss", ctypes.c_void_p),
+                ("fdir_hi", ctypes.c_void_p), ("pkt_len", ctypes.c_void_p),
+                ("n", ctypes.c_uint64)]
+
+
+class GclGenParams(ctypes.Structure):
+    _fields_ = [("workload", ctypes.c_uint32), ("nruntimes", ctypes.c_uint32),
+                ("seed", ctypes.c_uint64), ("n", ctypes.c_uint64), ("stride", ctypes.c_uint64),
+                ("rank", ctypes.c_uint32), ("world", ctypes.c_uint32),
+                ("shard_block", ctypes.c_uint64), ("zipf_cdf", ctypes.c_void_p),
+                ("nflows", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
+
+
+class GclVerdict(ctypes.Structure):
+    _fields_ = [("hash", ctypes.c_uint32), ("uniqid", ctypes.c_uint16),
+                ("thread", ctypes.c_uint8), ("action", ctypes.c_uint8)]
+
+
+assert ctypes.sizeof(GclVerdict) == 8 and VERDICT_DTYPE.itemsize == 8
+
+
+class GclLrpcMsg(ctypes.Structure):
+    _fields_ = [("cmd", ctypes.c_uint64), ("payload", ctypes.c_ulong)]
+
+
+class GclLrpcChanOut(ctypes.Structure):
+    _fields_ = [("send_head", ctypes.c_uint32), ("send_tail", ctypes.c_uint32),
+                ("tbl", ctypes.POINTER(GclLrpcMsg)), ("recv_head_wb", ctypes.POINTER(ctypes.c_uint32)),
+                ("size", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
+
+
+class GclHostProc(ctypes.Structure):
+    _fields_ = [("uniqid", ctypes.c_uint16), ("thread_count", ctypes.c_uint16),
+                ("active_thread_count", ctypes.c_uint16), ("idle_top", ctypes.c_int16),
+                ("flow_tbl", ctypes.c_uint16 * GCL_NCPU),
+                ("rxq", ctypes.POINTER(GclLrpcChanOut) * GCL_NCPU)]
+
+
+SCHED_ADD_CORE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.POINTER(GclHostProc))
+ENABLE_POLL_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.POINTER(GclHostProc), ctypes.c_uint)
+FREE_PKT_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64)
+OWNED_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.POINTER(GclHostProc), ctypes.c_uint64)
+REFCNT_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int)
+ARP_RESPOND_FN = ctypes.CFUNCTYPE(ctypes.c_bool, ctypes.c_void_p, ctypes.c_uint64)
+
+
+class GclHostOps(ctypes.Structure):
+    _fields_ = [("arg", ctypes.c_void_p), ("sched_add_core", SCHED_ADD_CORE_FN),
+                ("enable_poll", ENABLE_POLL_FN), ("free_pkt", FREE_PKT_FN),
+                ("owned", OWNED_FN), ("refcnt_update", REFCNT_FN),
+                ("arp_respond", ARP_RESPOND_FN)]
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} missing: run `python caladan_amd/build.py` "
+                          "(the classifier has no CPU fallback)")
+    lib = ctypes.CDLL(LIB_PATH)
+    vp, u16, u32, u64, i32 = ctypes.c_void_p, ctypes.c_uint16, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+    sig = {
+        "gcl_open": (i32, [i32, ctypes.POINTER(GclCfg), ctypes.POINTER(vp)]),
+        "gcl_close": (None, [vp]),
+        "gcl_runtime_set": (i32, [vp, u16, u32, u16, u16, ctypes.POINTER(u16)]),
+        "gcl_runtime_del": (i32, [vp, u16]),
+        "gcl_steer_flows": (i32, [u16, ctypes.POINTER(u16), u16, ctypes.POINTER(u16)]),
+        "gcl_classify": (i32, [vp, ctypes.POINTER(GclBatch), vp, vp, vp, vp]),
+        "gcl_sync": (i32, [vp]),
+        "gcl_kernel_time": (i32, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64), i32]),
+        "gcl_generate": (i32, [ctypes.POINTER(GclGenParams), vp, vp, vp, vp]),
+        "gcl_runtime_ip": (u32, [u32]),
+        "gcl_zipf_cdf": (i32, [u32, ctypes.c_double, vp]),
+        "gcl_jenkins_hash": (u32, [ctypes.c_char_p, ctypes.c_size_t]),
+        "gcl_toeplitz": (u32, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t]),
+        "gcl_version": (ctypes.c_char_p, []),
+        "gcl_lrpc_init_out": (i32, [ctypes.POINTER(GclLrpcChanOut), ctypes.POINTER(GclLrpcMsg), ctypes.c_uint, ctypes.POINTER(u32)]),
+        "gcl_lrpc_send": (ctypes.c_bool, [ctypes.POINTER(GclLrpcChanOut), u64, ctypes.c_ulong]),
+        "gcl_rx_make_cmd": (u64, [u16, ctypes.c_uint8]),
+        "gcl_host_deliver": (u64, [vp, u32, vp, i32, vp, vp, vp, ctypes.c_uint8, vp, u64,
+                                   ctypes.POINTER(GclHostOps), vp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def _check(ret, what):
+    if ret < 0:
+        raise OSError(-ret, f"{what}: {os.strerror(-ret)}")
+    return ret
+
+
+def _ptr(x):
+    """Device/host address of a torch tensor or numpy array (None -> NULL)."""
+    if x is None:
+        return None
+    if hasattr(x, "data_ptr"):
+        return x.data_ptr()
+    if isinstance(x, np.ndarray):
+        return x.ctypes.data
+    return int(x)
+
+
+def _nbytes(x):
+    if hasattr(x, "numel"):
+        return x.numel() * x.element_size()
+    return x.nbytes
+
+
+def jenkins_hash(key: bytes) -> int:
+    return lib.gcl_jenkins_hash(key, len(key))
+
+
+def toeplitz(key: bytes, data: bytes) -> int:
+    return lib.gcl_toeplitz(key, len(key), data, len(data))
+
+
+def runtime_ip(r: int) -> int:
+    return lib.gcl_runtime_ip(r)
+
+
+def steer_flows(thread_count, active_idx):
+    """sched_steer_flows (iokernel/sched.c:122-147); returns the flow table."""
+    n = len(active_idx)
+    act = (ctypes.c_uint16 * max(n, 1))(*active_idx)
+    out = (ctypes.c_uint16 * thread_count)(*([0] * thread_count))
+    _check(lib.gcl_steer_flows(thread_count, act, n, out), "gcl_steer_flows")
+    return list(out)
+
+
+def zipf_cdf(nflows, s=0.99):
+    cdf = np.empty(nflows, dtype=np.uint64)
+    _check(lib.gcl_zipf_cdf(nflows, s, cdf.ctypes.data), "gcl_zipf_cdf")
+    return cdf
+
+
+def generate(workload, n, stride, nruntimes, frames, olflags=None, rss=None, seed=0xCA1ADA4,
+             rank=0, world=1, shard_block=0, zipf_cdf_dev=None, nflows=0, stream=None):
+    """Fill device buffers with synthetic rx traffic (gcl_generate)."""
+    if _nbytes(frames) < n * stride:
+        raise ValueError("frames buffer too small")
+    p = GclGenParams(workload=workload, nruntimes=nruntimes, seed=seed, n=n, stride=stride,
+                     rank=rank, world=world, shard_block=shard_block,
+                     zipf_cdf=_ptr(zipf_cdf_dev), nflows=nflows)
+    _check(lib.gcl_generate(ctypes.byref(p), _ptr(frames), _ptr(olflags), _ptr(rss), stream),
+           "gcl_generate")
+
+
+class Classifier:
+    """One gcl_ctx: the GPU side of one dataplane (iokernel/dpdk.c:276-280)."""
+
+    def __init__(self, device=0, max_runtimes=16, hash_mode=HASH_JENKINS, flags=0,
+                 default_olflags=F_RSS_HASH | F_IP_CKSUM_GOOD, rss_key=CALADAN_RSS_KEY):
+        if isinstance(hash_mode, str):
+            hash_mode = HASH_MODES[hash_mode]
+        cfg = GclCfg(max_runtimes=max_runtimes, hash_mode=hash_mode, flags=flags,
+                     default_olflags=default_olflags)
+        key = bytes(rss_key)[:40].ljust(40, b"\0")
+        for i in range(40):
+            cfg.rss_key[i] = key[i]
+        self.cfg = cfg
+        self.max_runtimes = max_runtimes
+        self._ctx = ctypes.c_void_p()
+        _check(lib.gcl_open(device, ctypes.byref(cfg), ctypes.byref(self._ctx)), "gcl_open")
+
+    def close(self):
+        if self._ctx:
+            lib.gcl_close(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def runtime_set(self, uniqid, ip, thread_count, active_count, flow_tbl=None):
+        tbl = None
+        if flow_tbl is not None:
+            tbl = (ctypes.c_uint16 * max(len(flow_tbl), 1))(*flow_tbl)
+        return _check(lib.gcl_runtime_set(self._ctx, uniqid, ip, thread_count, active_count, tbl),
+                      "gcl_runtime_set")
+
+    def runtime_del(self, uniqid):
+        return _check(lib.gcl_runtime_del(self._ctx, uniqid), "gcl_runtime_del")
+
+    def classify(self, frames, n, stride=0, verdicts=None, counts=None, stats=None, offs=None,
+                 olflags=None, rss=None, fdir_hi=None, frames_len=None, stream=None):
+        """Launch the classify kernel on device buffers (asynchronous)."""
+        if verdicts is not None and _nbytes(verdicts) < 8 * n:
+            raise ValueError("verdict buffer too small")
+        if counts is not None and _nbytes(counts) < 8 * self.max_runtimes:
+            raise ValueError("counts buffer too small")
+        if stats is not None and _nbytes(stats) < 8 * NR_STATS:
+            raise ValueError("stats buffer too small")
+        for arr, w in ((offs, 8), (olflags, 1), (rss, 4), (fdir_hi, 4)):
+            if arr is not None and _nbytes(arr) < w * n:
+                raise ValueError("per-packet array too small")
+        b = GclBatch(frames=_ptr(frames),
+                     frames_len=_nbytes(frames) if frames_len is None else frames_len,
+                     stride=stride, offs=_ptr(offs), olflags=_ptr(olflags), rss=_ptr(rss),
+                     fdir_hi=_ptr(fdir_hi), pkt_len=None, n=n)
+        return _check(lib.gcl_classify(self._ctx, ctypes.byref(b), _ptr(verdicts), _ptr(counts),
+                                       _ptr(stats), stream), "gcl_classify")
+
+    def sync(self):
+        return _check(lib.gcl_sync(self._ctx), "gcl_sync")
+
+    def kernel_time(self, reset=False):
+        ms = ctypes.c_double()
+        nl = ctypes.c_uint64()
+        _check(lib.gcl_kernel_time(self._ctx, ctypes.byref(ms), ctypes.byref(nl), int(reset)),
+               "gcl_kernel_time")
+        return ms.value, nl.value
+
+
+def version():
+    return lib.gcl_version().decode()
+
+
+__all__ = [n for n in dir() if not n.startswith("_")]

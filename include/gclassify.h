@@ -1,0 +1,267 @@
+/*
+ * gclassify.h - C ABI of the MI355X (gfx950) rx packet classifier.
+ *
+ * This library replaces the per-packet work that Caladan's IOKernel does in
+ * rx_burst()/rx_one_pkt() (iokernel/rx.c:116-233, :270-290): parse the
+ * Ethernet/IPv4/ARP header, look the destination IP up in the IP->runtime
+ * table (dp.ip_to_proc, an rte_hash keyed by rte_jhash, iokernel/dp_clients.c:
+ * 349-363), and steer the packet to a runtime kthread through that runtime's
+ * flow table (rx_send_to_runtime, iokernel/rx.c:50-73).  The GPU emits one
+ * 8-byte verdict per packet; the host (one dataplane thread, as in the
+ * reference) turns verdicts into lrpc_send() calls (see gcl_host.h).
+ *
+ * Conventions follow the reference: every function returns 0 or -errno
+ * (rx_init iokernel/rx.c:398-415, lrpc_init_out base/lrpc.c:38-52), nothing is
+ * thread-safe, and one context serves one GPU the way one dataplane core
+ * serves one NIC queue (iokernel/dpdk.c:276-280).  There are no per-packet
+ * error returns: outcomes are verdict actions plus counters, exactly like the
+ * reference's STAT_INC counters (iokernel/defs.h:417-460).
+ *
+ * All pointers passed to gcl_classify() are DEVICE pointers (HBM); table
+ * setters take host pointers.  Table updates are applied on the stream of the
+ * next gcl_classify() call, before its kernel, giving the snapshot semantics
+ * of the reference's single-threaded dataplane (tables only change between
+ * bursts, iokernel/main.c:144-176).
+ */
+#ifndef GCLASSIFY_H
+#define GCLASSIFY_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Limits of the reference data model. */
+#define GCL_MAX_PROC      4096  /* IOKERNEL_MAX_PROC, iokernel/defs.h:69 */
+#define GCL_NCPU          256   /* NCPU, inc/base/limits.h:7: max threads per proc */
+#define GCL_RX_BURST_SIZE 64    /* IOKERNEL_RX_BURST_SIZE, iokernel/defs.h:75 */
+
+/* Header constants parsed on the path (inc/net/ethernet.h, inc/net/arp.h). */
+#define GCL_ETHTYPE_IP    0x0800
+#define GCL_ETHTYPE_ARP   0x0806
+#define GCL_ETHTYPE_IPV6  0x86DD
+#define GCL_ARP_OP_REQUEST 1
+#define GCL_ARP_OP_REPLY   2
+#define GCL_HDR_GRANULE   64    /* bytes of each frame the kernel stages */
+
+/*
+ * Per-packet offload flags: one byte that carries the rte_mbuf ol_flags bits
+ * rx.c reads (RTE_MBUF_F_RX_RSS_HASH at rx.c:132/:160, RTE_MBUF_F_RX_FDIR_ID at
+ * rx.c:131, RTE_MBUF_F_RX_IP_CKSUM_MASK at rx.c:31-35).
+ */
+#define GCL_F_RSS_HASH           0x01
+#define GCL_F_FDIR_ID            0x02
+#define GCL_F_IP_CKSUM_MASK      0x0C
+#define GCL_F_IP_CKSUM_UNKNOWN   0x00
+#define GCL_F_IP_CKSUM_BAD       0x04
+#define GCL_F_IP_CKSUM_GOOD      0x08
+#define GCL_F_IP_CKSUM_NONE      0x0C
+
+/*
+ * Steering-hash source.  The reference steers with buf->hash.rss (rx.c:83),
+ * i.e. the NIC's Toeplitz RSS over IPv4 TCP/UDP (iokernel/dpdk.c:67-82).
+ *  NIC      - use the per-packet rss[] array, exactly like rx.c.
+ *  JENKINS  - compute lookup3 (base/jenkins_hash.c:126-297) over the 13-byte
+ *             key {saddr, daddr, dport, sport, proto} (host-order fields).
+ *  TOEPLITZ - compute the NIC's Toeplitz hash in software, bit-exact with
+ *             do_toeplitz (runtime/net/core.c:120-139) for the configured key.
+ * In the two computed modes the hash is 0 unless the frame is IPv4 with
+ * IHL >= 5, not a fragment (MF clear, offset 0) and protocol TCP or UDP
+ * (the NIC's RTE_ETH_RSS_NONFRAG_IPV4_TCP|UDP, dpdk.c:79).
+ */
+enum gcl_hash_mode {
+	GCL_HASH_NIC = 0,
+	GCL_HASH_JENKINS = 1,
+	GCL_HASH_TOEPLITZ = 2,
+};
+
+/* gcl_cfg.flags */
+#define GCL_CFG_AZURE_ARP  0x1  /* cfg.azure_arp_mode: rx.c:171-190, :200-203 */
+#define GCL_CFG_HASH16     0x2  /* truncate the steering hash to 16 bits, as the
+                                   loopback hint does (runtime/net/core.c:524,
+                                   iokernel/tx.c:81-83, inc/iokernel/queue.h:120-134) */
+#define GCL_CFG_PROFILE    0x4  /* record HIP events around every classify kernel */
+
+struct gcl_cfg {
+	uint32_t max_runtimes;    /* uniqids must be < max_runtimes (<= GCL_MAX_PROC) */
+	uint32_t hash_mode;       /* enum gcl_hash_mode */
+	uint32_t flags;           /* GCL_CFG_* */
+	uint8_t  default_olflags; /* flags of every packet when gcl_batch.olflags == NULL */
+	uint8_t  rss_key[40];     /* Toeplitz key (NIC key, dpdk.c:219-228) */
+	uint8_t  pad[3];
+};
+
+/* One batch of received frames, resident in device memory. */
+struct gcl_batch {
+	const uint8_t  *frames;     /* frame bytes (mbuf data) */
+	uint64_t        frames_len; /* readable bytes at frames; reads past it see 0 */
+	uint64_t        stride;     /* slot stride when offs == NULL (multiple of 16) */
+	const uint64_t *offs;       /* optional u64[n] frame start offsets (16-B aligned) */
+	const uint8_t  *olflags;    /* optional u8[n]  GCL_F_* per packet */
+	const uint32_t *rss;        /* optional u32[n] buf->hash.rss (NIC mode) */
+	const uint32_t *fdir_hi;    /* optional u32[n] buf->hash.fdir.hi (FDIR mark) */
+	const uint16_t *pkt_len;    /* optional u16[n] rte_pktmbuf_pkt_len; NOT read by
+	                               the kernel, only by the host post-pass that
+	                               builds rxq_cmd (rx_make_cmd, rx.c:24-38) */
+	uint64_t        n;          /* packets in the batch */
+};
+
+/*
+ * Verdict actions.  Each is one exit of rx_one_pkt (rx.c:116-233).
+ * GCL_ACT_F_FDIR is or-ed in when the runtime was found by the FDIR mark.
+ */
+enum gcl_action {
+	GCL_ACT_DELIVER = 0,       /* rx_send_pkt_to_runtime(p) -> threads[thread] */
+	GCL_ACT_WAKE = 1,          /* runtime has no active thread: the host must
+	                              replay rx_send_to_runtime (sched_add_core,
+	                              rx.c:62-72) in packet order */
+	GCL_ACT_DROP_ETHERTYPE = 2,/* rx.c:191-194 -> fail_free, RX_UNHANDLED */
+	GCL_ACT_DROP_UNREG = 3,    /* rx.c:198-207: RX_UNREGISTERED_MAC, RX_UNHANDLED */
+	GCL_ACT_BROADCAST = 4,     /* azure ARP reply, rx.c:171-190 (host fans out) */
+	GCL_ACT_ARP_RESPOND = 5,   /* azure ARP request miss, rx.c:200-203 (host) */
+};
+#define GCL_ACT_MASK    0x7F
+#define GCL_ACT_F_FDIR  0x80
+#define GCL_NO_RUNTIME  0xFFFF
+#define GCL_NO_THREAD   0xFF
+
+struct gcl_verdict {
+	uint32_t hash;    /* steering hash (hash.rss, or the computed flow hash) */
+	uint16_t uniqid;  /* proc->uniqid of the destination, GCL_NO_RUNTIME if none */
+	uint8_t  thread;  /* flow_tbl[hash % thread_count], GCL_NO_THREAD if none */
+	uint8_t  action;  /* enum gcl_action | GCL_ACT_F_FDIR */
+};
+
+/*
+ * Counter slots; indices 0..5 keep the order of the reference enum
+ * (iokernel/defs.h:421-426).  The device adds RX_PULLED, RX_FLOW_TAG_MATCH,
+ * RX_HASH_MISSING, RX_UNREGISTERED_MAC and RX_UNHANDLED (for its drops); the
+ * host adds RX_UNICAST_FAIL / RX_BROADCAST_FAIL (ring full) and the UNHANDLED
+ * that goes with them.
+ */
+enum {
+	GCL_RX_UNREGISTERED_MAC = 0,
+	GCL_RX_UNICAST_FAIL,
+	GCL_RX_BROADCAST_FAIL,
+	GCL_RX_FLOW_TAG_MATCH,
+	GCL_RX_UNHANDLED,
+	GCL_RX_HASH_MISSING,
+	GCL_RX_PULLED,
+	GCL_NR_STATS = 8, /* padded */
+};
+
+struct gcl_ctx;
+
+/*
+ * gcl_open - create a classifier context on HIP device @hip_device.
+ * Replaces the ip_to_proc creation in dp_clients_init (dp_clients.c:349-363)
+ * and the flow tables held in struct proc (defs.h:244).
+ * Returns 0, -EINVAL (bad cfg), -ENODEV (no such device) or -ENOMEM.
+ */
+int gcl_open(int hip_device, const struct gcl_cfg *cfg, struct gcl_ctx **out);
+void gcl_close(struct gcl_ctx *ctx);
+
+/*
+ * gcl_runtime_set - add or update a runtime (proc).
+ * Mirrors dp_clients_add_client (dp_clients.c:156-185: clients_by_id[uniqid],
+ * rte_hash_add_key_data(ip)) plus the flow table that sched_steer_flows writes
+ * (sched.c:122-147).  @flow_tbl holds @thread_count entries (ignored when
+ * @active_count == 0).  Returns -EEXIST if another runtime owns @ip_host
+ * (dp_clients.c:174-179), -EINVAL on out-of-range arguments.
+ */
+int gcl_runtime_set(struct gcl_ctx *ctx, uint16_t uniqid, uint32_t ip_host,
+                    uint16_t thread_count, uint16_t active_count,
+                    const uint16_t *flow_tbl);
+
+/* gcl_runtime_del - remove a runtime (dp_clients_remove_client,
+ * dp_clients.c:230-250).  Returns -ENOENT if @uniqid is not present. */
+int gcl_runtime_del(struct gcl_ctx *ctx, uint16_t uniqid);
+
+/*
+ * gcl_steer_flows - the flow_tbl rule of sched_steer_flows (sched.c:122-147):
+ * identity for the active threads, the rest round-robin over them.  Host-only
+ * helper; leaves @flow_tbl untouched when @active_count == 0, like the
+ * reference.  @active_idx lists the active thread indices in activation order.
+ */
+int gcl_steer_flows(uint16_t thread_count, const uint16_t *active_idx,
+                    uint16_t active_count, uint16_t *flow_tbl);
+
+/*
+ * gcl_classify - classify @b->n packets on @hip_stream (NULL = null stream).
+ * @verdicts       device gcl_verdict[n] (may be NULL: counters only)
+ * @runtime_counts device u64[max_runtimes], ACCUMULATED: packets steered to
+ *                 each runtime (DELIVER + WAKE), may be NULL
+ * @stats          device u64[GCL_NR_STATS], ACCUMULATED, may be NULL
+ * Asynchronous; returns -EINVAL for malformed batches.
+ * Replaces the rx_one_pkt loop of rx_burst (rx.c:281-287).
+ */
+int gcl_classify(struct gcl_ctx *ctx, const struct gcl_batch *b,
+                 struct gcl_verdict *verdicts, uint64_t *runtime_counts,
+                 uint64_t *stats, void *hip_stream);
+
+/* Synchronise the context's last stream. */
+int gcl_sync(struct gcl_ctx *ctx);
+
+/*
+ * gcl_kernel_time - with GCL_CFG_PROFILE: total milliseconds the classify
+ * kernel ran (HIP events around each launch, on its own stream) and the
+ * number of launches since the last reset.  Synchronises.
+ */
+int gcl_kernel_time(struct gcl_ctx *ctx, double *ms, uint64_t *launches, int reset);
+
+/*
+ * Synthetic rx traffic generator (device).  Counter-based: packet g of the
+ * global stream depends only on (seed, g), so every rank and the CPU oracle
+ * produce identical bytes.  Packet j of this call is global packet
+ * ((j / shard_block) * world + rank) * shard_block + j % shard_block
+ * (round-robin block sharding across ranks).
+ */
+enum gcl_workload {
+	GCL_WL_UDP64 = 0,       /* 64-B Eth/IPv4/UDP, uniform 5-tuples */
+	GCL_WL_TCP1500_ZIPF = 1,/* 1500-B Eth/IPv4/TCP, Zipf flow ranks */
+	GCL_WL_MIXED = 2,       /* IPv4 TCP/UDP + IPv6 + ARP, jumbo lengths */
+};
+
+struct gcl_gen_params {
+	uint32_t workload;      /* enum gcl_workload */
+	uint32_t nruntimes;     /* R: destination IPs are gcl_runtime_ip(r), r < R */
+	uint64_t seed;
+	uint64_t n;             /* packets to generate */
+	uint64_t stride;        /* slot stride (>= 64, multiple of 16) */
+	uint32_t rank, world;   /* shard position */
+	uint64_t shard_block;   /* packets per round-robin block (0 = no sharding) */
+	const uint64_t *zipf_cdf; /* device u64[nflows] (TCP1500_ZIPF only) */
+	uint32_t nflows;
+	uint32_t pad;
+};
+
+/* Write the first GCL_HDR_GRANULE bytes of every slot of @frames (n * stride
+ * bytes; the rest of each slot is left as the caller initialised it), and
+ * optionally olflags[n] (what the NIC would report) and rss[n] (an arbitrary
+ * 32-bit NIC hash value, so NIC mode can be exercised). */
+int gcl_generate(const struct gcl_gen_params *p, uint8_t *frames,
+                 uint8_t *olflags, uint32_t *rss, void *hip_stream);
+
+/* IP address of runtime r in the synthetic workloads: 10.0.0.0 + r + 1. */
+uint32_t gcl_runtime_ip(uint32_t r);
+
+/* Host helper: Zipf(s) CDF over @nflows ranks as u64 fixed point
+ * (cdf[k] = floor(P(rank <= k) * 2^64), last entry saturated). */
+int gcl_zipf_cdf(uint32_t nflows, double s, uint64_t *cdf_out);
+
+/* Host reference of the two hashes the kernel computes (for callers that
+ * need the same value on the CPU, e.g. the loopback hint). */
+uint32_t gcl_jenkins_hash(const void *key, size_t len);
+uint32_t gcl_toeplitz(const uint8_t *key, size_t keylen, const uint8_t *input,
+                      size_t len);
+
+/* Library version string. */
+const char *gcl_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GCLASSIFY_H */

@@ -1,0 +1,828 @@
+/*
+ * orc.c - CPU oracle for the rx classify path.  TEST INFRASTRUCTURE ONLY:
+ * linked by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg,
+ * never by the product.  See orc.h for what each function restates.
+ */
+#define _GNU_SOURCE
+#include <errno.h>
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "orc.h"
+
+#define ROT(x, k) (((x) << (k)) | ((x) >> (32 - (k))))
+
+/* lookup3 mix/final, base/jenkins_hash.c:79-87 and :114-123 */
+#define MIX(a, b, c) do { \
+	a -= c; a ^= ROT(c, 4);  c += b; \
+	b -= a; b ^= ROT(a, 6);  a += c; \
+	c -= b; c ^= ROT(b, 8);  b += a; \
+	a -= c; a ^= ROT(c, 16); c += b; \
+	b -= a; b ^= ROT(a, 19); a += c; \
+	c -= b; c ^= ROT(b, 4);  b += a; \
+} while (0)
+#define FINAL(a, b, c) do { \
+	c ^= b; c -= ROT(b, 14); \
+	a ^= c; a -= ROT(c, 11); \
+	b ^= a; b -= ROT(a, 25); \
+	c ^= b; c -= ROT(b, 16); \
+	a ^= c; a -= ROT(c, 4);  \
+	b ^= a; b -= ROT(a, 14); \
+	c ^= b; c -= ROT(b, 24); \
+} while (0)
+
+/*
+ * orc_jhash - lookup3 hashlittle with initval 0 (base/jenkins_hash.c:126-297).
+ * Restated on the byte-at-a-time branch (:252-293), which yields the same
+ * value as the aligned branches for every input.
+ */
+uint32_t orc_jhash(const void *key, size_t len)
+{
+	const uint8_t *k = key;
+	uint32_t a, b, c;
+
+	a = b = c = 0xdeadbeefu + (uint32_t)len;
+	while (len > 12) {
+		a += k[0] | (uint32_t)k[1] << 8 | (uint32_t)k[2] << 16 | (uint32_t)k[3] << 24;
+		b += k[4] | (uint32_t)k[5] << 8 | (uint32_t)k[6] << 16 | (uint32_t)k[7] << 24;
+		c += k[8] | (uint32_t)k[9] << 8 | (uint32_t)k[10] << 16 | (uint32_t)k[11] << 24;
+		MIX(a, b, c);
+		len -= 12;
+		k += 12;
+	}
+	switch (len) {
+	case 12: c += (uint32_t)k[11] << 24; /* fall through */
+	case 11: c += (uint32_t)k[10] << 16; /* fall through */
+	case 10: c += (uint32_t)k[9] << 8;   /* fall through */
+	case 9:  c += k[8];                  /* fall through */
+	case 8:  b += (uint32_t)k[7] << 24;  /* fall through */
+	case 7:  b += (uint32_t)k[6] << 16;  /* fall through */
+	case 6:  b += (uint32_t)k[5] << 8;   /* fall through */
+	case 5:  b += k[4];                  /* fall through */
+	case 4:  a += (uint32_t)k[3] << 24;  /* fall through */
+	case 3:  a += (uint32_t)k[2] << 16;  /* fall through */
+	case 2:  a += (uint32_t)k[1] << 8;   /* fall through */
+	case 1:  a += k[0]; break;
+	case 0:  return c; /* zero length: no mixing, :180 */
+	}
+	FINAL(a, b, c);
+	return c;
+}
+
+static inline uint32_t be32_of(const uint8_t *p)
+{
+	return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3];
+}
+
+/*
+ * orc_do_toeplitz - runtime/net/core.c:120-139.  Input words are
+ * {saddr, daddr, dport | sport << 16} in host order; for every set bit i of
+ * word j the 32-bit key window starting at that bit is xor-ed in.
+ */
+uint32_t orc_do_toeplitz(const uint8_t *key, uint32_t saddr, uint32_t daddr,
+                         uint16_t sport, uint16_t dport)
+{
+	uint32_t in[3] = { saddr, daddr, (uint32_t)dport | (uint32_t)sport << 16 };
+	uint32_t ret = 0;
+
+	for (int j = 0; j < 3; j++) {
+		uint32_t kj = be32_of(key + 4 * j), kj1 = be32_of(key + 4 * j + 4);
+		for (uint32_t map = in[j]; map; map &= map - 1) {
+			uint32_t i = (uint32_t)__builtin_ctz(map);
+			ret ^= kj << (31 - i) | (uint32_t)((uint64_t)kj1 >> (i + 1));
+		}
+	}
+	return ret;
+}
+
+/* Textbook Toeplitz over a byte string, MSB first (MS RSS verification). */
+uint32_t orc_toeplitz_bytes(const uint8_t *key, size_t keylen,
+                            const uint8_t *in, size_t len)
+{
+	uint32_t ret = 0;
+	for (size_t p = 0; p < len * 8; p++) {
+		if (!(in[p / 8] & (0x80 >> (p % 8))))
+			continue;
+		uint32_t w = 0;
+		for (int q = 0; q < 32; q++) {
+			size_t kb = p + q;
+			int bit = kb / 8 < keylen ? (key[kb / 8] >> (7 - kb % 8)) & 1 : 0;
+			w = w << 1 | (uint32_t)bit;
+		}
+		ret ^= w;
+	}
+	return ret;
+}
+
+/* sched_steer_flows, iokernel/sched.c:122-147 */
+void orc_steer_flows(uint16_t thread_count, const uint16_t *active_idx,
+                     uint16_t active_count, uint16_t *flow_tbl)
+{
+	int j = 0;
+
+	if (active_count == 0)
+		return;
+	memset(flow_tbl, 0xFF, sizeof(*flow_tbl) * thread_count);
+	for (int i = 0; i < active_count; i++)
+		flow_tbl[active_idx[i]] = active_idx[i];
+	for (int i = 0; i < thread_count; i++) {
+		if (flow_tbl[i] != UINT16_MAX)
+			continue;
+		flow_tbl[i] = active_idx[j++ % active_count];
+	}
+}
+
+/* ------------------------------------------------------------------------
+ * IP -> runtime map.  Same contract as the rte_hash in dp_clients.c:349-363
+ * (exact match on the 4-byte host-order IP, hashed with jhash initval 0);
+ * laid out as 8-way buckets with a primary and an alternative bucket like
+ * DPDK's cuckoo table, so the CPU baseline pays a comparable lookup.
+ */
+#define ORC_BKT 8
+struct orc_bucket {
+	uint32_t sig[ORC_BKT];
+	uint32_t ip[ORC_BKT];
+	int32_t  uid[ORC_BKT];
+};
+
+struct orc_tables {
+	uint32_t max_runtimes;
+	uint32_t hash_mode;
+	uint32_t flags;
+	uint8_t  default_olflags;
+	uint8_t  rss_key[40];
+	struct orc_runtime *rt;     /* [max_runtimes] = dp.clients_by_id */
+	struct orc_bucket *bkt;
+	uint32_t nbkt_mask;
+};
+
+static uint32_t alt_bucket(uint32_t h, uint32_t mask)
+{
+	return (h ^ ((h >> 16) | 1u) * 0x9E3779B1u) & mask;
+}
+
+struct orc_tables *orc_tables_new(uint32_t max_runtimes, uint32_t hash_mode,
+                                  uint32_t flags, uint8_t default_olflags,
+                                  const uint8_t *rss_key40)
+{
+	struct orc_tables *t;
+	uint32_t nb = 2;
+
+	if (max_runtimes == 0 || max_runtimes > GCL_MAX_PROC)
+		return NULL;
+	t = calloc(1, sizeof(*t));
+	if (!t)
+		return NULL;
+	t->max_runtimes = max_runtimes;
+	t->hash_mode = hash_mode;
+	t->flags = flags;
+	t->default_olflags = default_olflags;
+	if (rss_key40)
+		memcpy(t->rss_key, rss_key40, 40);
+	t->rt = calloc(max_runtimes, sizeof(*t->rt));
+	while (nb * ORC_BKT < 2 * max_runtimes)
+		nb <<= 1;
+	t->bkt = malloc(nb * sizeof(*t->bkt));
+	if (!t->rt || !t->bkt) {
+		orc_tables_free(t);
+		return NULL;
+	}
+	for (uint32_t i = 0; i < nb; i++)
+		for (int s = 0; s < ORC_BKT; s++)
+			t->bkt[i].uid[s] = -1;
+	t->nbkt_mask = nb - 1;
+	return t;
+}
+
+void orc_tables_free(struct orc_tables *t)
+{
+	if (!t)
+		return;
+	free(t->rt);
+	free(t->bkt);
+	free(t);
+}
+
+static int iptab_lookup(const struct orc_tables *t, uint32_t ip)
+{
+	uint32_t h = orc_jhash(&ip, 4);
+	uint32_t b[2] = { h & t->nbkt_mask, alt_bucket(h, t->nbkt_mask) };
+
+	for (int k = 0; k < 2; k++) {
+		const struct orc_bucket *bk = &t->bkt[b[k]];
+		for (int s = 0; s < ORC_BKT; s++)
+			if (bk->uid[s] >= 0 && bk->sig[s] == h && bk->ip[s] == ip)
+				return bk->uid[s];
+	}
+	return -1;
+}
+
+static int iptab_add(struct orc_tables *t, uint32_t ip, int uid)
+{
+	uint32_t h = orc_jhash(&ip, 4);
+	uint32_t b[2] = { h & t->nbkt_mask, alt_bucket(h, t->nbkt_mask) };
+
+	for (int k = 0; k < 2; k++) {
+		struct orc_bucket *bk = &t->bkt[b[k]];
+		for (int s = 0; s < ORC_BKT; s++) {
+			if (bk->uid[s] < 0) {
+				bk->uid[s] = uid;
+				bk->sig[s] = h;
+				bk->ip[s] = ip;
+				return 0;
+			}
+		}
+	}
+	return -ENOSPC;
+}
+
+static void iptab_del(struct orc_tables *t, uint32_t ip)
+{
+	uint32_t h = orc_jhash(&ip, 4);
+	uint32_t b[2] = { h & t->nbkt_mask, alt_bucket(h, t->nbkt_mask) };
+
+	for (int k = 0; k < 2; k++) {
+		struct orc_bucket *bk = &t->bkt[b[k]];
+		for (int s = 0; s < ORC_BKT; s++)
+			if (bk->uid[s] >= 0 && bk->ip[s] == ip)
+				bk->uid[s] = -1;
+	}
+}
+
+int orc_runtime_set(struct orc_tables *t, uint16_t uniqid, uint32_t ip,
+                    uint16_t thread_count, uint16_t active,
+                    const uint16_t *flow_tbl)
+{
+	struct orc_runtime *r;
+	int owner;
+
+	if (uniqid >= t->max_runtimes || thread_count == 0 ||
+	    thread_count > GCL_NCPU || active > thread_count)
+		return -EINVAL;
+	if (active) {
+		for (int i = 0; i < thread_count; i++)
+			if (flow_tbl[i] >= thread_count)
+				return -EINVAL;
+	}
+	owner = iptab_lookup(t, ip);
+	if (owner >= 0 && owner != uniqid)
+		return -EEXIST; /* dp_clients.c:174-179 */
+	r = &t->rt[uniqid];
+	if (r->present && r->ip != ip)
+		iptab_del(t, r->ip);
+	if (owner < 0 || (r->present && r->ip != ip)) {
+		int ret = iptab_add(t, ip, uniqid);
+		if (ret)
+			return ret;
+	}
+	r->present = 1;
+	r->ip = ip;
+	r->thread_count = thread_count;
+	r->active = active;
+	if (active)
+		memcpy(r->flow_tbl, flow_tbl, thread_count * sizeof(uint16_t));
+	return 0;
+}
+
+int orc_runtime_del(struct orc_tables *t, uint16_t uniqid)
+{
+	if (uniqid >= t->max_runtimes || !t->rt[uniqid].present)
+		return -ENOENT;
+	iptab_del(t, t->rt[uniqid].ip);
+	memset(&t->rt[uniqid], 0, sizeof(t->rt[uniqid]));
+	return 0;
+}
+
+/* ------------------------------------------------------------------------
+ * Classifier.
+ */
+struct pkt_view {
+	const uint8_t *base;  /* frame start, or NULL if out of range */
+	uint64_t off;
+	uint64_t frames_len;
+	const uint8_t *frames;
+};
+
+/* byte k of the frame; bytes past frames_len read as 0 */
+static inline uint8_t fb(const struct pkt_view *pv, uint64_t k)
+{
+	uint64_t a = pv->off + k;
+	return a < pv->frames_len ? pv->frames[a] : 0;
+}
+
+static inline uint16_t fbe16(const struct pkt_view *pv, uint64_t k)
+{
+	return (uint16_t)(fb(pv, k) << 8 | fb(pv, k + 1));
+}
+
+static inline uint32_t fbe32(const struct pkt_view *pv, uint64_t k)
+{
+	return (uint32_t)fbe16(pv, k) << 16 | fbe16(pv, k + 2);
+}
+
+/* The build-defined flow hash of the computed modes (gclassify.h). */
+static uint32_t flow_hash(const struct orc_tables *t, const struct pkt_view *pv)
+{
+	uint8_t key[13];
+	uint32_t saddr, daddr;
+	uint16_t sport, dport, frag;
+	uint8_t ihl, proto;
+
+	if (fbe16(pv, 12) != GCL_ETHTYPE_IP)
+		return 0;
+	ihl = fb(pv, 14) & 0xF;
+	frag = fbe16(pv, 20);
+	proto = fb(pv, 23);
+	if (ihl < 5 || (frag & 0x3FFF) || (proto != 6 && proto != 17))
+		return 0;
+	saddr = fbe32(pv, 26);
+	daddr = fbe32(pv, 30);
+	sport = fbe16(pv, 14 + 4u * ihl);
+	dport = fbe16(pv, 16 + 4u * ihl);
+	if (t->hash_mode == GCL_HASH_TOEPLITZ)
+		return orc_do_toeplitz(t->rss_key, saddr, daddr, sport, dport);
+	memcpy(key, &saddr, 4);      /* host-order (LE) fields */
+	memcpy(key + 4, &daddr, 4);
+	memcpy(key + 8, &dport, 2);
+	memcpy(key + 10, &sport, 2);
+	key[12] = proto;
+	return orc_jhash(key, 13);
+}
+
+/*
+ * rx_one_pkt, iokernel/rx.c:116-233, with rx_send_pkt_to_runtime (:76-92)
+ * and rx_send_to_runtime (:50-73) reduced to the steering decision.
+ */
+static void orc_rx_one_pkt(const struct orc_tables *t, const struct gcl_batch *b,
+                           uint64_t i, struct gcl_verdict *v, uint64_t *counts,
+                           uint64_t *stats)
+{
+	struct pkt_view pv;
+	uint8_t flags = b->olflags ? b->olflags[i] : t->default_olflags;
+	uint32_t hash, dst_ip = 0;
+	uint16_t et;
+	int p = -1, fdir = 0;
+
+	pv.frames = b->frames;
+	pv.frames_len = b->frames_len;
+	pv.off = b->offs ? b->offs[i] : i * b->stride;
+
+	if (t->hash_mode == GCL_HASH_NIC)
+		hash = b->rss ? b->rss[i] : 0;
+	else
+		hash = flow_hash(t, &pv);
+	if (t->flags & GCL_CFG_HASH16)
+		hash &= 0xFFFF;
+	v->hash = hash;
+	v->uniqid = GCL_NO_RUNTIME;
+	v->thread = GCL_NO_THREAD;
+
+	/* hardware flow tag, rx.c:131-146 */
+	if (flags & GCL_F_FDIR_ID) {
+		uint32_t mark = b->fdir_hi ? b->fdir_hi[i] : 0;
+		stats[GCL_RX_FLOW_TAG_MATCH]++;
+		if (mark < t->max_runtimes && t->rt[mark].present) {
+			p = (int)mark;
+			fdir = GCL_ACT_F_FDIR;
+			goto deliver;
+		}
+		/* NULL proc: fall through to the header parse */
+	}
+
+	et = fbe16(&pv, 12); /* rx.c:154 */
+	if (et == GCL_ETHTYPE_IP) {
+		dst_ip = fbe32(&pv, 30); /* rx.c:157-159: fixed offset, no IHL */
+		if (!(flags & GCL_F_RSS_HASH))
+			stats[GCL_RX_HASH_MISSING]++;
+	} else if (et == GCL_ETHTYPE_ARP) {
+		dst_ip = fbe32(&pv, 38); /* arp_tip, rx.c:165-167 */
+		if ((t->flags & GCL_CFG_AZURE_ARP) &&
+		    fbe16(&pv, 20) == GCL_ARP_OP_REPLY) {
+			v->action = GCL_ACT_BROADCAST; /* rx.c:171-190 */
+			return;
+		}
+	} else {
+		v->action = GCL_ACT_DROP_ETHERTYPE; /* rx.c:191-194 */
+		stats[GCL_RX_UNHANDLED]++;
+		return;
+	}
+
+	p = iptab_lookup(t, dst_ip); /* rx.c:197 */
+	if (p < 0) {
+		if ((t->flags & GCL_CFG_AZURE_ARP) && et == GCL_ETHTYPE_ARP &&
+		    fbe16(&pv, 20) == GCL_ARP_OP_REQUEST) {
+			v->action = GCL_ACT_ARP_RESPOND; /* rx.c:200-203 */
+			return;
+		}
+		stats[GCL_RX_UNREGISTERED_MAC]++; /* rx.c:205 */
+		stats[GCL_RX_UNHANDLED]++;        /* rx.c:232 */
+		v->action = GCL_ACT_DROP_UNREG;
+		return;
+	}
+
+deliver:
+	v->uniqid = (uint16_t)p;
+	counts[p]++;
+	if (t->rt[p].active > 0) { /* rx.c:55-59 */
+		const struct orc_runtime *r = &t->rt[p];
+		v->thread = (uint8_t)r->flow_tbl[hash % r->thread_count];
+		v->action = (uint8_t)(GCL_ACT_DELIVER | fdir);
+	} else {
+		v->action = (uint8_t)(GCL_ACT_WAKE | fdir); /* rx.c:62-72 */
+	}
+}
+
+#define RX_PREFETCH_STRIDE 2 /* rx.c:22 */
+
+static void classify_range(const struct orc_tables *t, const struct gcl_batch *b,
+                           uint64_t lo, uint64_t hi, struct gcl_verdict *v,
+                           uint64_t *counts, uint64_t *stats)
+{
+	/* rx_burst, rx.c:270-290: bursts of IOKERNEL_RX_BURST_SIZE */
+	for (uint64_t s = lo; s < hi; s += GCL_RX_BURST_SIZE) {
+		uint64_t nb = hi - s < GCL_RX_BURST_SIZE ? hi - s : GCL_RX_BURST_SIZE;
+		stats[GCL_RX_PULLED] += nb;
+		for (uint64_t i = 0; i < nb; i++) {
+			if (i + RX_PREFETCH_STRIDE < nb) {
+				uint64_t j = s + i + RX_PREFETCH_STRIDE;
+				uint64_t off = b->offs ? b->offs[j] : j * b->stride;
+				if (off < b->frames_len)
+					__builtin_prefetch(b->frames + off);
+			}
+			orc_rx_one_pkt(t, b, s + i, &v[s + i - lo], counts, stats);
+		}
+	}
+}
+
+void orc_classify(const struct orc_tables *t, const struct gcl_batch *b,
+                  struct gcl_verdict *v, uint64_t *counts, uint64_t *stats)
+{
+	classify_range(t, b, 0, b->n, v, counts, stats);
+}
+
+/* lrpc ring, inc/base/lrpc.h:15-63 (16-B messages, parity in bit 63) */
+struct orc_lrpc {
+	uint32_t send_head, send_tail, size;
+	uint64_t *tbl; /* 2 words per message */
+};
+
+static int lrpc_send(struct orc_lrpc *c, uint64_t cmd, uint64_t payload)
+{
+	uint64_t *dst;
+
+	if (c->send_head - c->send_tail >= c->size)
+		return 0; /* ring full: RX_UNICAST_FAIL */
+	dst = &c->tbl[2 * (c->send_head & (c->size - 1))];
+	cmd |= (c->send_head++ & c->size) ? 0 : (1ull << 63);
+	dst[1] = payload;
+	__atomic_store_n(&dst[0], cmd, __ATOMIC_RELEASE);
+	return 1;
+}
+
+struct lrpc_set {
+	struct orc_lrpc *rings; /* [max_runtimes * GCL_NCPU_USED] lazily allocated */
+	uint32_t stride;
+};
+
+#define LRPC_DEPTH 4096 /* runtime/ioqueues.c:31-40 */
+
+static struct orc_lrpc *ring_of(struct lrpc_set *s, uint32_t p, uint32_t th)
+{
+	struct orc_lrpc *r = &s->rings[p * s->stride + th];
+	if (!r->tbl) {
+		r->tbl = calloc(2 * LRPC_DEPTH, sizeof(uint64_t));
+		r->size = LRPC_DEPTH;
+	}
+	return r;
+}
+
+static void classify_range_lrpc(const struct orc_tables *t, const struct gcl_batch *b,
+                                uint64_t lo, uint64_t hi, struct gcl_verdict *v,
+                                uint64_t *counts, uint64_t *stats,
+                                struct lrpc_set *rs)
+{
+	for (uint64_t s = lo; s < hi; s += GCL_RX_BURST_SIZE) {
+		uint64_t nb = hi - s < GCL_RX_BURST_SIZE ? hi - s : GCL_RX_BURST_SIZE;
+		stats[GCL_RX_PULLED] += nb;
+		for (uint64_t i = 0; i < nb; i++) {
+			uint64_t k = s + i;
+			struct gcl_verdict *vk = &v[k - lo];
+			if (i + RX_PREFETCH_STRIDE < nb) {
+				uint64_t j = k + RX_PREFETCH_STRIDE;
+				uint64_t off = b->offs ? b->offs[j] : j * b->stride;
+				if (off < b->frames_len)
+					__builtin_prefetch(b->frames + off);
+			}
+			orc_rx_one_pkt(t, b, k, vk, counts, stats);
+			if ((vk->action & GCL_ACT_MASK) == GCL_ACT_DELIVER) {
+				/* rx_make_cmd, rx.c:24-38 */
+				uint8_t fl = b->olflags ? b->olflags[k] : t->default_olflags;
+				uint64_t len = b->pkt_len ? b->pkt_len[k] : b->stride;
+				uint64_t csum = (fl & GCL_F_IP_CKSUM_MASK) == GCL_F_IP_CKSUM_GOOD;
+				uint64_t cmd = 0 | (len & 0xFFFF) << 16 | csum << 48;
+				uint64_t off = b->offs ? b->offs[k] : k * b->stride;
+				if (!lrpc_send(ring_of(rs, vk->uniqid, vk->thread), cmd, off)) {
+					stats[GCL_RX_UNICAST_FAIL]++;
+					stats[GCL_RX_UNHANDLED]++;
+				}
+			}
+		}
+		/* the runtimes drain their rings between bursts */
+		for (uint64_t i = 0; i < nb; i++) {
+			struct gcl_verdict *vk = &v[s + i - lo];
+			if ((vk->action & GCL_ACT_MASK) == GCL_ACT_DELIVER) {
+				struct orc_lrpc *r = ring_of(rs, vk->uniqid, vk->thread);
+				r->send_tail = r->send_head;
+			}
+		}
+	}
+}
+
+static uint32_t max_threads(const struct orc_tables *t)
+{
+	uint32_t m = 1;
+	for (uint32_t i = 0; i < t->max_runtimes; i++)
+		if (t->rt[i].present && t->rt[i].thread_count > m)
+			m = t->rt[i].thread_count;
+	return m;
+}
+
+static void lrpc_set_init(struct lrpc_set *s, const struct orc_tables *t)
+{
+	s->stride = max_threads(t);
+	s->rings = calloc((size_t)t->max_runtimes * s->stride, sizeof(*s->rings));
+}
+
+static void lrpc_set_free(struct lrpc_set *s, const struct orc_tables *t)
+{
+	for (size_t i = 0; i < (size_t)t->max_runtimes * s->stride; i++)
+		free(s->rings[i].tbl);
+	free(s->rings);
+}
+
+void orc_classify_lrpc(const struct orc_tables *t, const struct gcl_batch *b,
+                       struct gcl_verdict *v, uint64_t *counts, uint64_t *stats)
+{
+	struct lrpc_set rs;
+	lrpc_set_init(&rs, t);
+	classify_range_lrpc(t, b, 0, b->n, v, counts, stats, &rs);
+	lrpc_set_free(&rs, t);
+}
+
+/* ------------------------------------------------------------------------
+ * CPU baseline timer.
+ */
+struct bench_arg {
+	const struct orc_tables *t;
+	const struct gcl_batch *b;
+	uint64_t lo, hi;
+	int passes, with_lrpc;
+	pthread_barrier_t *bar;
+};
+
+static void *bench_thread(void *arg)
+{
+	struct bench_arg *a = arg;
+	uint64_t n = a->hi - a->lo;
+	struct gcl_verdict *v = malloc((n ? n : 1) * sizeof(*v));
+	uint64_t *counts = calloc(a->t->max_runtimes, sizeof(uint64_t));
+	uint64_t stats[GCL_NR_STATS] = { 0 };
+	struct lrpc_set rs;
+
+	if (a->with_lrpc)
+		lrpc_set_init(&rs, a->t);
+	/* touch the verdict buffer before the clock starts */
+	memset(v, 0, (n ? n : 1) * sizeof(*v));
+	pthread_barrier_wait(a->bar);
+	for (int p = 0; p < a->passes; p++) {
+		if (a->with_lrpc)
+			classify_range_lrpc(a->t, a->b, a->lo, a->hi, v, counts, stats, &rs);
+		else
+			classify_range(a->t, a->b, a->lo, a->hi, v, counts, stats);
+	}
+	pthread_barrier_wait(a->bar);
+	if (a->with_lrpc)
+		lrpc_set_free(&rs, a->t);
+	free(v);
+	free(counts);
+	return NULL;
+}
+
+double orc_bench(const struct orc_tables *t, const struct gcl_batch *b,
+                 int threads, int passes, int with_lrpc)
+{
+	pthread_t tid[256];
+	struct bench_arg arg[256];
+	pthread_barrier_t bar;
+	struct timespec t0, t1;
+
+	if (threads < 1)
+		threads = 1;
+	if (threads > 256)
+		threads = 256;
+	pthread_barrier_init(&bar, NULL, (unsigned)threads + 1);
+	for (int i = 0; i < threads; i++) {
+		arg[i].t = t;
+		arg[i].b = b;
+		arg[i].lo = b->n * (uint64_t)i / (uint64_t)threads;
+		arg[i].hi = b->n * (uint64_t)(i + 1) / (uint64_t)threads;
+		arg[i].passes = passes;
+		arg[i].with_lrpc = with_lrpc;
+		arg[i].bar = &bar;
+		pthread_create(&tid[i], NULL, bench_thread, &arg[i]);
+	}
+	pthread_barrier_wait(&bar);
+	clock_gettime(CLOCK_MONOTONIC, &t0);
+	pthread_barrier_wait(&bar);
+	clock_gettime(CLOCK_MONOTONIC, &t1);
+	for (int i = 0; i < threads; i++)
+		pthread_join(tid[i], NULL);
+	pthread_barrier_destroy(&bar);
+	return (double)(t1.tv_sec - t0.tv_sec) + (double)(t1.tv_nsec - t0.tv_nsec) * 1e-9;
+}
+
+/* ------------------------------------------------------------------------
+ * Synthetic generator (same streams as the device generator).
+ */
+static inline uint64_t mix64(uint64_t z)
+{
+	z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+	z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+	return z ^ (z >> 31);
+}
+
+/* k-th random word of global packet g: splitmix64 at position 8g+k */
+static inline uint64_t rw(uint64_t seed, uint64_t g, uint64_t k)
+{
+	return mix64(seed + (g * 8 + k + 1) * 0x9E3779B97F4A7C15ull);
+}
+
+uint32_t orc_runtime_ip(uint32_t r)
+{
+	return 0x0A000000u + r + 1; /* 10.0.0.0 + r + 1 */
+}
+
+int orc_zipf_cdf(uint32_t nflows, double s, uint64_t *cdf)
+{
+	double h = 0.0, acc = 0.0;
+
+	if (nflows == 0)
+		return -EINVAL;
+	for (uint32_t k = 0; k < nflows; k++)
+		h += pow((double)k + 1.0, -s);
+	for (uint32_t k = 0; k < nflows; k++) {
+		double x;
+		acc += pow((double)k + 1.0, -s);
+		x = ldexp(acc / h, 64);
+		cdf[k] = x >= 18446744073709551615.0 ? UINT64_MAX : (uint64_t)x;
+	}
+	cdf[nflows - 1] = UINT64_MAX;
+	return 0;
+}
+
+static uint32_t zipf_pick(const uint64_t *cdf, uint32_t nflows, uint64_t u)
+{
+	uint32_t lo = 0, hi = nflows - 1;
+	while (lo < hi) { /* first k with u < cdf[k] */
+		uint32_t mid = lo + (hi - lo) / 2;
+		if (u < cdf[mid])
+			hi = mid;
+		else
+			lo = mid + 1;
+	}
+	return lo;
+}
+
+static void put16(uint8_t *p, uint16_t v) { p[0] = (uint8_t)(v >> 8); p[1] = (uint8_t)v; }
+static void put32(uint8_t *p, uint32_t v) { put16(p, (uint16_t)(v >> 16)); put16(p + 2, (uint16_t)v); }
+
+static void ip_csum(uint8_t *ip)
+{
+	uint32_t s = 0;
+	ip[10] = ip[11] = 0;
+	for (int i = 0; i < 20; i += 2)
+		s += (uint32_t)ip[i] << 8 | ip[i + 1];
+	while (s >> 16)
+		s = (s & 0xFFFF) + (s >> 16);
+	put16(ip + 10, (uint16_t)~s);
+}
+
+static void eth(uint8_t *f, uint64_t srcbits, uint16_t et)
+{
+	static const uint8_t dmac[6] = { 0x02, 0x00, 0x00, 0x00, 0x00, 0x01 };
+	memcpy(f, dmac, 6);
+	f[6] = 0x02;
+	f[7] = 0x00;
+	put32(f + 8, (uint32_t)srcbits);
+	put16(f + 12, et);
+}
+
+static void ipv4(uint8_t *ip, uint16_t totlen, uint16_t id, uint8_t proto,
+                 uint32_t saddr, uint32_t daddr)
+{
+	ip[0] = 0x45;
+	ip[1] = 0;
+	put16(ip + 2, totlen);
+	put16(ip + 4, id);
+	put16(ip + 6, 0x4000); /* DF */
+	ip[8] = 64;
+	ip[9] = proto;
+	put32(ip + 12, saddr);
+	put32(ip + 16, daddr);
+	ip_csum(ip);
+}
+
+static uint64_t global_index(const struct gcl_gen_params *p, uint64_t j)
+{
+	if (!p->shard_block || p->world <= 1)
+		return j;
+	return ((j / p->shard_block) * p->world + p->rank) * p->shard_block +
+	       j % p->shard_block;
+}
+
+int orc_generate(const struct gcl_gen_params *p, const uint64_t *zipf_cdf,
+                 uint8_t *frames, uint8_t *olflags, uint32_t *rss)
+{
+	if (p->stride < 64 || p->nruntimes == 0)
+		return -EINVAL;
+	for (uint64_t j = 0; j < p->n; j++) {
+		uint64_t g = global_index(p, j);
+		uint8_t *f = frames + j * p->stride;
+		uint64_t r0 = rw(p->seed, g, 0), r1 = rw(p->seed, g, 1);
+		uint8_t fl = GCL_F_RSS_HASH | GCL_F_IP_CKSUM_GOOD;
+
+		memset(f, 0, 64);
+		if (p->workload == GCL_WL_UDP64) {
+			uint32_t rt = (uint32_t)(((uint64_t)(uint32_t)r1 * p->nruntimes) >> 32);
+			eth(f, r1 >> 32, GCL_ETHTYPE_IP);
+			ipv4(f + 14, 50, (uint16_t)(r1 >> 16), 17, (uint32_t)r0,
+			     orc_runtime_ip(rt));
+			put16(f + 34, (uint16_t)(r0 >> 32));
+			put16(f + 36, (uint16_t)(r0 >> 48));
+			put16(f + 38, 30);
+		} else if (p->workload == GCL_WL_TCP1500_ZIPF) {
+			uint32_t flow, rt;
+			uint64_t fr;
+			if (!zipf_cdf || !p->nflows)
+				return -EINVAL;
+			flow = zipf_pick(zipf_cdf, p->nflows, r0);
+			fr = rw(p->seed ^ 0xF10F10F10F10F10Full, flow, 0);
+			rt = flow % p->nruntimes;
+			eth(f, fr >> 16, GCL_ETHTYPE_IP);
+			ipv4(f + 14, 1486, (uint16_t)r1, 6, (uint32_t)fr, orc_runtime_ip(rt));
+			put16(f + 34, (uint16_t)(fr >> 32));
+			put16(f + 36, (uint16_t)(fr >> 48));
+			put32(f + 38, (uint32_t)(r1 >> 32)); /* seq */
+			f[46] = 0x50;                         /* data offset 5 */
+			f[47] = 0x10;                         /* ACK */
+			put16(f + 48, 0xFFFF);                /* window */
+		} else if (p->workload == GCL_WL_MIXED) {
+			uint64_t r2 = rw(p->seed, g, 2);
+			uint32_t kind = (uint32_t)r0 % 100;
+			uint32_t rt = (uint32_t)(((uint64_t)(uint32_t)r1 * p->nruntimes) >> 32);
+			int unreg = (uint32_t)(r0 >> 40) % 20 == 0;
+			uint32_t dst = unreg ? 0xC0A80000u | (uint32_t)(r1 >> 48) : orc_runtime_ip(rt);
+			if (kind < 70) {
+				uint16_t len = (uint16_t)(64 + (uint32_t)(r1 >> 32) % (9014 - 64 + 1));
+				uint8_t proto = (r0 >> 32) & 1 ? 6 : 17;
+				eth(f, r2 >> 8, GCL_ETHTYPE_IP);
+				ipv4(f + 14, (uint16_t)(len - 14), (uint16_t)r2, proto,
+				     (uint32_t)r2, dst);
+				put16(f + 34, (uint16_t)(r2 >> 32));
+				put16(f + 36, (uint16_t)(r2 >> 48));
+			} else if (kind < 90) {
+				eth(f, r2 >> 8, GCL_ETHTYPE_IPV6);
+				f[14] = 0x60;
+				put16(f + 18, (uint16_t)(r1 >> 32) & 0x1FFF);
+				f[20] = 17;
+				f[21] = 64;
+				put32(f + 22, (uint32_t)r2);
+				put32(f + 38, dst);
+				fl = 0;
+			} else {
+				unreg = (uint32_t)(r0 >> 40) % 10 == 0;
+				dst = unreg ? 0xC0A80000u | (uint32_t)(r1 >> 48) : orc_runtime_ip(rt);
+				eth(f, r2 >> 8, GCL_ETHTYPE_ARP);
+				put16(f + 14, 1);      /* htype ether */
+				put16(f + 16, 0x0800); /* ptype */
+				f[18] = 6;
+				f[19] = 4;
+				put16(f + 20, (r0 >> 33) & 1 ? GCL_ARP_OP_REPLY : GCL_ARP_OP_REQUEST);
+				put32(f + 24, (uint32_t)(r2 >> 16)); /* sha (part) */
+				put32(f + 28, (uint32_t)r2);         /* sip */
+				put32(f + 38, dst);                  /* tip */
+				fl = 0;
+			}
+		} else {
+			return -EINVAL;
+		}
+		if (olflags)
+			olflags[j] = fl;
+		if (rss)
+			rss[j] = (uint32_t)rw(p->seed, g, 3);
+	}
+	return 0;
+}

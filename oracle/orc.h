@@ -1,0 +1,95 @@
+/*
+ * orc.h - CPU oracle for the rx classify path.  TEST INFRASTRUCTURE ONLY.
+ *
+ * A plain-C restatement of the reference algorithm, used by tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg as the checker and
+ * as the timed CPU baseline.  The product (caladan_amd/) never links, loads or
+ * calls anything in oracle/.
+ *
+ * What it restates (each function cites its reference lines):
+ *   orc_jhash         base/jenkins_hash.c:126-297 (lookup3 hashlittle, initval 0)
+ *   orc_do_toeplitz   runtime/net/core.c:120-139
+ *   orc_steer_flows   iokernel/sched.c:122-147
+ *   orc_rx_burst      iokernel/rx.c:270-290 (bursts of 64, prefetch stride 2)
+ *   orc_rx_one_pkt    iokernel/rx.c:116-233 (+ rx_send_to_runtime :50-73)
+ *   orc_iptab_*       the ip_to_proc rte_hash (iokernel/dp_clients.c:349-363),
+ *                     keyed by jhash of the 4-byte host-order IP like rte_jhash
+ *
+ * Pinning: orc_jhash is checked against base/jenkins_hash.c compiled from the
+ * reference tree (oracle/_ref, see oracle/Makefile) and the published lookup3
+ * KATs; orc_do_toeplitz against the Microsoft RSS verification vectors, which
+ * the survey ran through the reference's do_toeplitz; orc_rx_one_pkt against
+ * hand-derived scenario fixtures (tests/golden/rx_scenarios.json) that cite
+ * rx.c line by line.  iokernel/rx.c itself needs DPDK headers that are not in
+ * this image, so it is not compiled here (see DESIGN.md "Oracle").
+ */
+#ifndef ORC_H
+#define ORC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../include/gclassify.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+uint32_t orc_jhash(const void *key, size_t len);
+uint32_t orc_do_toeplitz(const uint8_t *key, uint32_t saddr, uint32_t daddr,
+                         uint16_t sport, uint16_t dport);
+/* generic Toeplitz over a byte string (MSB-first), for the KAT vectors */
+uint32_t orc_toeplitz_bytes(const uint8_t *key, size_t keylen,
+                            const uint8_t *in, size_t len);
+void orc_steer_flows(uint16_t thread_count, const uint16_t *active_idx,
+                     uint16_t active_count, uint16_t *flow_tbl);
+
+struct orc_runtime {
+	int      present;
+	uint32_t ip;
+	uint16_t thread_count;
+	uint16_t active;
+	uint16_t flow_tbl[GCL_NCPU];
+};
+
+struct orc_tables;
+
+struct orc_tables *orc_tables_new(uint32_t max_runtimes, uint32_t hash_mode,
+                                  uint32_t flags, uint8_t default_olflags,
+                                  const uint8_t *rss_key40);
+void orc_tables_free(struct orc_tables *t);
+/* 0, -EEXIST (duplicate ip), -EINVAL */
+int orc_runtime_set(struct orc_tables *t, uint16_t uniqid, uint32_t ip,
+                    uint16_t thread_count, uint16_t active,
+                    const uint16_t *flow_tbl);
+int orc_runtime_del(struct orc_tables *t, uint16_t uniqid);
+
+/* Classify a host batch (gcl_batch with host pointers), accumulating counts
+ * and stats.  Processes bursts of 64 with the rx.c prefetch stride. */
+void orc_classify(const struct orc_tables *t, const struct gcl_batch *b,
+                  struct gcl_verdict *v, uint64_t *counts, uint64_t *stats);
+
+/* Same, plus lrpc_send of a 16-B message per delivered packet into
+ * 4096-deep per-(runtime, thread) rings that are drained after every burst
+ * (inc/base/lrpc.h:48-63, runtime/ioqueues.c:31-40). */
+void orc_classify_lrpc(const struct orc_tables *t, const struct gcl_batch *b,
+                       struct gcl_verdict *v, uint64_t *counts, uint64_t *stats);
+
+/* CPU baseline timer: classify the batch @passes times on @threads threads
+ * (each thread a contiguous shard, its own verdict/count buffers).  Returns
+ * wall seconds. */
+double orc_bench(const struct orc_tables *t, const struct gcl_batch *b,
+                 int threads, int passes, int with_lrpc);
+
+/* Synthetic generator: the same streams as gcl_generate, written on the CPU.
+ * frames must hold n*stride bytes (pre-zeroed by the caller). */
+int orc_generate(const struct gcl_gen_params *p, const uint64_t *zipf_cdf,
+                 uint8_t *frames, uint8_t *olflags, uint32_t *rss);
+uint32_t orc_runtime_ip(uint32_t r);
+int orc_zipf_cdf(uint32_t nflows, double s, uint64_t *cdf);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,129 @@
+"""Test-side builders: golden scenario loader and a seeded edge-case packet
+generator that exercises every branch of rx_one_pkt (iokernel/rx.c:116-233)."""
+import json
+import os
+import struct
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLDEN = os.path.join(HERE, "golden")
+
+F_RSS, F_FDIR = 0x01, 0x02
+
+
+def load_json(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+def scenario_sets():
+    return load_json("rx_scenarios.json")["sets"]
+
+
+def scenario_batch(s, slot=128):
+    """Frames of a scenario set in `slot`-byte slots plus per-packet arrays."""
+    pk = s["packets"]
+    n = len(pk)
+    frames = np.zeros(n * slot, dtype=np.uint8)
+    for i, p in enumerate(pk):
+        b = bytes.fromhex(p["frame"])
+        assert len(b) <= slot
+        frames[i * slot:i * slot + len(b)] = np.frombuffer(b, dtype=np.uint8)
+    olflags = np.array([p["olflags"] for p in pk], dtype=np.uint8)
+    rss = np.array([p["rss"] for p in pk], dtype=np.uint32)
+    fdir = np.array([p["fdir_hi"] for p in pk], dtype=np.uint32)
+    exp = np.zeros(n, dtype=[("hash", "<u4"), ("uniqid", "<u2"), ("thread", "u1"), ("action", "u1")])
+    for i, p in enumerate(pk):
+        e = p["expect"]
+        exp[i] = (e["hash"], e["uniqid"], e["thread"], e["action"])
+    return frames, olflags, rss, fdir, exp
+
+
+def apply_runtimes(target, runtimes):
+    """target: oracle Tables or gclassify.Classifier (same runtime_set API)."""
+    for r in runtimes:
+        ret = target.runtime_set(r["uniqid"], r["ip"], r["thread_count"], r["active"], r["flow_tbl"])
+        assert ret == 0, (r, ret)
+
+
+# ---------------------------------------------------------------- fuzz
+def _csum(hdr):
+    s = sum(struct.unpack("!%dH" % (len(hdr) // 2), hdr))
+    while s >> 16:
+        s = (s & 0xFFFF) + (s >> 16)
+    return (~s) & 0xFFFF
+
+
+def random_runtimes(rng, max_runtimes, count, max_threads=16):
+    """Runtimes with random IPs, thread counts (incl. non-powers of two) and
+    active sets (incl. zero active threads); flow tables by sched_steer_flows."""
+    from oracle import orc
+    uniqs = rng.choice(max_runtimes, size=count, replace=False)
+    ips = set()
+    out = []
+    for u in uniqs:
+        while True:
+            ip = int(rng.integers(1, 2**32 - 1))
+            if ip not in ips:
+                ips.add(ip)
+                break
+        tc = int(rng.integers(1, max_threads + 1))
+        active = int(rng.integers(0, tc + 1)) if rng.random() < 0.85 else 0
+        act_idx = [int(x) for x in rng.choice(tc, size=active, replace=False)]
+        flow = orc.steer_flows(tc, act_idx) if active else None
+        out.append({"uniqid": int(u), "ip": ip, "thread_count": tc, "active": active,
+                    "active_idx": act_idx, "flow_tbl": flow})
+    return out
+
+
+def fuzz_batch(rng, n, runtimes, max_runtimes, slot=128, tail_runts=True):
+    """Random frames hitting every branch; 16-B aligned shuffled offsets, the
+    last frames straddling the end of the buffer (reads past it see 0)."""
+    ips = [r["ip"] for r in runtimes] or [0x0A000001]
+    buf_slots = n + 8
+    frames = np.zeros(buf_slots * slot, dtype=np.uint8)
+    order = rng.permutation(buf_slots)[:n]
+    offs = (order.astype(np.uint64) * slot)
+    olflags = rng.integers(0, 16, size=n, dtype=np.uint8)
+    rss = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
+    fdir = np.where(rng.random(n) < 0.7,
+                    rng.choice([r["uniqid"] for r in runtimes] or [0], size=n),
+                    rng.integers(0, max_runtimes + 64, size=n)).astype(np.uint32)
+    for i in range(n):
+        kind = rng.random()
+        dst = int(rng.choice(ips)) if rng.random() < 0.75 else int(rng.integers(0, 2**32))
+        src = int(rng.integers(0, 2**32))
+        eth = bytes(rng.integers(0, 256, size=12, dtype=np.uint8))
+        if kind < 0.55:
+            ihl = 5 if rng.random() < 0.6 else int(rng.integers(0, 16))
+            ver = 4 if rng.random() < 0.95 else int(rng.integers(0, 16))
+            proto = int(rng.choice([6, 17, 6, 17, 1, 47, 132]))
+            frag = int(rng.choice([0, 0x4000, 0x4000, 0x2000, 0x0001, 0x1FFF, 0x8000]))
+            optlen = max(0, 4 * ihl - 20)
+            hdr = struct.pack("!BBHHHBBHII", ver << 4 | ihl, 0, 100, 7, frag, 64, proto, 0, src, dst)
+            hdr = hdr[:10] + struct.pack("!H", _csum(hdr)) + hdr[12:]
+            opts = bytes(rng.integers(0, 256, size=optlen, dtype=np.uint8))
+            l4 = struct.pack("!HH", int(rng.integers(0, 65536)), int(rng.integers(0, 65536)))
+            fr = eth + b"\x08\x00" + hdr + opts + l4 + bytes(8)
+        elif kind < 0.72:
+            op = int(rng.choice([1, 2, 3]))
+            fr = eth + b"\x08\x06" + struct.pack("!HHBBH", 1, 0x0800, 6, 4, op) + bytes(6) + \
+                struct.pack("!I", src) + bytes(6) + struct.pack("!I", dst)
+        elif kind < 0.80:
+            fr = eth + b"\x86\xdd" + bytes(rng.integers(0, 256, size=40, dtype=np.uint8))
+        elif kind < 0.86:
+            fr = eth + b"\x81\x00\x00\x05\x08\x00" + bytes(rng.integers(0, 256, size=40, dtype=np.uint8))
+        else:
+            fr = bytes(rng.integers(0, 256, size=int(rng.integers(14, slot)), dtype=np.uint8))
+        fr = fr[:slot]
+        o = int(offs[i])
+        frames[o:o + len(fr)] = np.frombuffer(fr, dtype=np.uint8)
+    frames_len = frames.nbytes
+    if tail_runts and n >= 4:
+        # put 3 packets at the very end so their headers straddle frames_len
+        last = (buf_slots - 1) * slot
+        for j, cut in enumerate((20, 36, 60)):
+            offs[n - 1 - j] = last + 16 * j
+        frames_len = last + 16 * 2 + 40
+    return frames, frames_len, offs, olflags, rss, fdir

@@ -1,0 +1,250 @@
+"""GPU parity: the HIP classifier through the C ABI vs the CPU oracle and the
+golden fixtures.  Bit-exact on every verdict, count and counter."""
+import numpy as np
+import pytest
+
+from tests.rxcases import apply_runtimes, fuzz_batch, random_runtimes, scenario_batch, scenario_sets
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def g():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from caladan_amd import gclassify
+    return gclassify
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda() if a is not None else None
+
+
+def gpu_run(g, clf, frames, n, stride=0, offs=None, olflags=None, rss=None, fdir=None,
+            frames_len=None, counts=None, stats=None):
+    f = dev(frames.view(np.uint8))
+    v = torch.zeros(n * 8, dtype=torch.uint8, device="cuda")
+    c = counts if counts is not None else torch.zeros(clf.max_runtimes, dtype=torch.int64, device="cuda")
+    s = stats if stats is not None else torch.zeros(g.NR_STATS, dtype=torch.int64, device="cuda")
+    o = dev(offs.astype(np.int64)) if offs is not None else None
+    clf.classify(f, n, stride, verdicts=v, counts=c, stats=s, offs=o, olflags=dev(olflags),
+                 rss=dev(rss.view(np.int32)) if rss is not None else None,
+                 fdir_hi=dev(fdir.astype(np.int32)) if fdir is not None else None,
+                 frames_len=frames_len)
+    torch.cuda.synchronize()
+    return (v.cpu().numpy().view(g.VERDICT_DTYPE), c.cpu().numpy().astype(np.uint64),
+            s.cpu().numpy().astype(np.uint64))
+
+
+def assert_same(v, ve, what=""):
+    if not (v == ve).all():
+        bad = np.nonzero(v != ve)[0]
+        i = bad[0]
+        raise AssertionError(f"{what}: {len(bad)} verdicts differ, first at {i}: gpu={v[i]} want={ve[i]}")
+
+
+SETS = scenario_sets()
+
+
+@pytest.mark.parametrize("s", SETS, ids=[s["name"] for s in SETS])
+def test_gpu_scenarios(g, s):
+    cfg = s["cfg"]
+    clf = g.Classifier(0, cfg["max_runtimes"], cfg["hash_mode"], cfg["flags"], cfg["default_olflags"],
+                       bytes.fromhex(cfg["rss_key"]))
+    apply_runtimes(clf, s["runtimes"])
+    frames, olflags, rss, fdir, exp = scenario_batch(s)
+    v, c, st = gpu_run(g, clf, frames, len(exp), 128, olflags=olflags, rss=rss, fdir=fdir)
+    for i in range(len(exp)):
+        assert tuple(v[i]) == tuple(exp[i]), (s["packets"][i]["cite"], v[i], exp[i])
+    assert list(st) == s["expect_stats"]
+    assert list(c) == s["expect_counts"]
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("flags", [0, 1, 2])
+@pytest.mark.parametrize("max_rt", [16, 1024, 4096])
+def test_gpu_fuzz_vs_oracle(g, orc, mode, flags, max_rt):
+    rng = np.random.default_rng(1000 * mode + 10 * flags + max_rt)
+    rts = random_runtimes(rng, max_rt, min(max_rt, 40 if max_rt == 16 else 300))
+    n = 5000
+    frames, flen, offs, olf, rss, fdir = fuzz_batch(rng, n, rts, max_rt)
+    key = bytes(rng.integers(0, 256, size=40, dtype=np.uint8))
+    t = orc.Tables(max_rt, mode, flags, 0x09, key)
+    apply_runtimes(t, rts)
+    ve, ce, se = t.classify(frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir_hi=fdir, frames_len=flen)
+    clf = g.Classifier(0, max_rt, mode, flags, 0x09, key)
+    apply_runtimes(clf, rts)
+    v, c, st = gpu_run(g, clf, frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir=fdir, frames_len=flen)
+    assert_same(v, ve, f"mode={mode} flags={flags} R={max_rt}")
+    assert (c == ce).all()
+    assert (st == se).all(), (st, se)
+
+
+@pytest.mark.parametrize("wl,stride,R", [(0, 64, 16), (1, 1536, 1024), (2, 9216, 16)])
+def test_gpu_generator_matches_oracle(g, orc, wl, stride, R):
+    n = 20000
+    cdf = orc.zipf_cdf(1 << 16) if wl == 1 else None
+    fe, ofe, rse = orc.generate(wl, n, stride, R, cdf=cdf)
+    frames = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
+    olf = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    rss = torch.zeros(n, dtype=torch.int32, device="cuda")
+    cdf_dev = dev(cdf.view(np.int64)) if cdf is not None else None
+    g.generate(wl, n, stride, R, frames, olf, rss, zipf_cdf_dev=cdf_dev, nflows=0 if cdf is None else len(cdf))
+    torch.cuda.synchronize()
+    assert (frames.cpu().numpy() == fe).all()
+    assert (olf.cpu().numpy() == ofe).all()
+    assert (rss.cpu().numpy().view(np.uint32) == rse).all()
+
+
+def test_gpu_generator_sharding(g, orc):
+    """Rank r's shard equals blocks r, r+W, ... of the global stream."""
+    n, blk, W = 8192, 1024, 4
+    full, _, _ = orc.generate(0, n * W, 64, 16)
+    full = full.reshape(n * W, 64)
+    for r in range(W):
+        frames = torch.zeros(n * 64, dtype=torch.uint8, device="cuda")
+        g.generate(0, n, 64, 16, frames, rank=r, world=W, shard_block=blk)
+        torch.cuda.synchronize()
+        got = frames.cpu().numpy().reshape(n, 64)
+        idx = np.concatenate([np.arange(b * blk, (b + 1) * blk) for b in range(r, n * W // blk, W)])
+        assert (got == full[idx]).all()
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("wl,stride,R,T", [(0, 64, 16, 8), (1, 1536, 1024, 4), (2, 9216, 16, 8)])
+def test_gpu_workloads_vs_oracle(g, orc, mode, wl, stride, R, T):
+    n = 100000 if wl != 2 else 20000
+    cdf = orc.zipf_cdf(1 << 20) if wl == 1 else None
+    frames, olf, rss = orc.generate(wl, n, stride, R, cdf=cdf)
+    rng = np.random.default_rng(wl)
+    t = orc.Tables(R, mode, 0, 0x09, bytes(range(40)))
+    clf = g.Classifier(0, R, mode, 0, 0x09, bytes(range(40)))
+    for r in range(R):
+        act = int(rng.integers(1, T + 1))
+        idx = [int(x) for x in rng.choice(T, size=act, replace=False)]
+        fl = orc.steer_flows(T, idx)
+        assert t.runtime_set(r, orc.runtime_ip(r), T, act, fl) == 0
+        clf.runtime_set(r, g.runtime_ip(r), T, act, fl)
+    ve, ce, se = t.classify(frames, n, stride, olflags=olf, rss=rss)
+    v, c, st = gpu_run(g, clf, frames, n, stride, olflags=olf, rss=rss)
+    assert_same(v, ve)
+    assert (c == ce).all() and (st == se).all()
+    # the bench path: no per-packet arrays (default flags), stride layout
+    ve, ce, se = t.classify(frames, n, stride)
+    v, c, st = gpu_run(g, clf, frames, n, stride)
+    assert_same(v, ve, "fast path")
+    assert (c == ce).all() and (st == se).all()
+
+
+def test_gpu_table_updates_between_batches(g, orc):
+    """Snapshot semantics: a runtime_set between two classify calls is seen by
+    the second only (tables change between bursts, iokernel/main.c:144-176)."""
+    n, R = 50000, 16
+    frames, _, _ = orc.generate(0, n, 64, R)
+    t = orc.Tables(R, 1, 0, 0x09)
+    clf = g.Classifier(0, R, 1)
+    for r in range(R):
+        t.runtime_set(r, orc.runtime_ip(r), 4, 4, [0, 1, 2, 3])
+        clf.runtime_set(r, g.runtime_ip(r), 4, 4, [0, 1, 2, 3])
+    f = dev(frames)
+    outs = []
+    for step in range(3):
+        v = torch.zeros(n * 8, dtype=torch.uint8, device="cuda")
+        c = torch.zeros(R, dtype=torch.int64, device="cuda")
+        s = torch.zeros(8, dtype=torch.int64, device="cuda")
+        clf.classify(f, n, 64, verdicts=v, counts=c, stats=s)
+        outs.append((v, c, s))
+        if step == 0:
+            clf.runtime_set(3, g.runtime_ip(3), 3, 0, None)   # no active thread: wake
+            clf.runtime_del(5)
+        if step == 1:
+            clf.runtime_set(5, g.runtime_ip(5), 7, 2, orc.steer_flows(7, [4, 1]))
+    torch.cuda.synchronize()
+    exp = [t.classify(frames, n, 64)]
+    t.runtime_set(3, orc.runtime_ip(3), 3, 0, None)
+    t.runtime_del(5)
+    exp.append(t.classify(frames, n, 64))
+    t.runtime_set(5, orc.runtime_ip(5), 7, 2, orc.steer_flows(7, [4, 1]))
+    exp.append(t.classify(frames, n, 64))
+    for (v, c, s), (ve, ce, se) in zip(outs, exp):
+        assert_same(v.cpu().numpy().view(g.VERDICT_DTYPE), ve)
+        assert (c.cpu().numpy().astype(np.uint64) == ce).all()
+        assert (s.cpu().numpy().astype(np.uint64) == se).all()
+
+
+def test_gpu_counts_accumulate_and_edge_sizes(g, orc):
+    """Counters accumulate across calls; n = 1, ragged tails, empty batch."""
+    R = 16
+    t = orc.Tables(R, 1, 0, 0x09)
+    clf = g.Classifier(0, R, 1)
+    for r in range(R):
+        t.runtime_set(r, orc.runtime_ip(r), 8, 8, list(range(8)))
+        clf.runtime_set(r, g.runtime_ip(r), 8, 8, list(range(8)))
+    frames, _, _ = orc.generate(0, 70001, 64, R)
+    f = dev(frames)
+    c = torch.zeros(R, dtype=torch.int64, device="cuda")
+    s = torch.zeros(8, dtype=torch.int64, device="cuda")
+    tot_c = np.zeros(R, dtype=np.uint64)
+    tot_s = np.zeros(8, dtype=np.uint64)
+    for n in (1, 255, 256, 257, 70001):
+        v = torch.zeros(n * 8, dtype=torch.uint8, device="cuda")
+        clf.classify(f, n, 64, verdicts=v, counts=c, stats=s)
+        ve, ce, se = t.classify(frames, n, 64)
+        torch.cuda.synchronize()
+        assert_same(v.cpu().numpy().view(g.VERDICT_DTYPE), ve, f"n={n}")
+        tot_c += ce
+        tot_s += se
+    assert clf.classify(f, 0, 64, verdicts=torch.zeros(8, dtype=torch.uint8, device="cuda")) == 0
+    torch.cuda.synchronize()
+    assert (c.cpu().numpy().astype(np.uint64) == tot_c).all()
+    assert (s.cpu().numpy().astype(np.uint64) == tot_s).all()
+
+
+def test_gpu_errors(g):
+    clf = g.Classifier(0, 16, 1)
+    with pytest.raises(OSError):
+        clf.runtime_set(16, 1, 4, 4, [0, 1, 2, 3])
+    clf.runtime_set(1, 0x0A000001, 4, 4, [0, 1, 2, 3])
+    with pytest.raises(OSError):
+        clf.runtime_set(2, 0x0A000001, 4, 4, [0, 1, 2, 3])
+    with pytest.raises(OSError):
+        clf.runtime_del(9)
+    f = torch.zeros(640, dtype=torch.uint8, device="cuda")
+    v = torch.zeros(80, dtype=torch.uint8, device="cuda")
+    with pytest.raises(OSError):
+        clf.classify(f, 10, 8, verdicts=v)   # stride not a multiple of 16
+    with pytest.raises(OSError):
+        g.Classifier(0, 5000, 1)
+
+
+def test_gpu_full_size_properties(g, orc):
+    """Config 2 at full size (32 Mi x 64 B): every packet is accounted for,
+    and a 65536-packet random sample matches the oracle bit for bit."""
+    n, R, T, stride = 32 << 20, 16, 8, 64
+    frames = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
+    g.generate(0, n, stride, R, frames)
+    clf = g.Classifier(0, R, 1)
+    t = orc.Tables(R, 1, 0, 0x09)
+    rng = np.random.default_rng(5)
+    for r in range(R):
+        act = int(rng.integers(1, T + 1))
+        fl = orc.steer_flows(T, [int(x) for x in rng.choice(T, size=act, replace=False)])
+        clf.runtime_set(r, g.runtime_ip(r), T, act, fl)
+        t.runtime_set(r, orc.runtime_ip(r), T, act, fl)
+    v = torch.zeros(n * 8, dtype=torch.uint8, device="cuda")
+    c = torch.zeros(R, dtype=torch.int64, device="cuda")
+    s = torch.zeros(8, dtype=torch.int64, device="cuda")
+    clf.classify(frames, n, stride, verdicts=v, counts=c, stats=s)
+    torch.cuda.synchronize()
+    vv = v.view(torch.int64).cpu().numpy().view(g.VERDICT_DTYPE)
+    cc = c.cpu().numpy()
+    ss = s.cpu().numpy()
+    assert cc.sum() == n and ss[g.RX_PULLED] == n and ss[g.RX_UNHANDLED] == 0
+    assert (np.bincount(vv["uniqid"], minlength=R)[:R] == cc).all()
+    assert ((vv["action"] & 0x7F) == 0).all()
+    sample = np.sort(rng.choice(n, size=65536, replace=False))
+    fr = frames.view(n, stride)[torch.from_numpy(sample).cuda()].cpu().numpy().reshape(-1)
+    ve, _, _ = t.classify(fr, len(sample), stride)
+    assert_same(vv[sample], ve, "sample")

@@ -1,0 +1,57 @@
+"""The oracle against the hand-derived rx.c scenario fixtures (CPU)."""
+import numpy as np
+import pytest
+
+from tests.rxcases import apply_runtimes, scenario_batch, scenario_sets
+
+SETS = scenario_sets()
+
+
+@pytest.mark.parametrize("s", SETS, ids=[s["name"] for s in SETS])
+def test_oracle_matches_scenarios(orc, s):
+    cfg = s["cfg"]
+    t = orc.Tables(cfg["max_runtimes"], cfg["hash_mode"], cfg["flags"], cfg["default_olflags"],
+                   bytes.fromhex(cfg["rss_key"]))
+    apply_runtimes(t, s["runtimes"])
+    frames, olflags, rss, fdir, exp = scenario_batch(s)
+    n = len(exp)
+    v, counts, stats = t.classify(frames, n, 128, olflags=olflags, rss=rss, fdir_hi=fdir)
+    for i in range(n):
+        assert tuple(v[i]) == tuple(exp[i]), (s["packets"][i]["cite"], v[i], exp[i])
+    assert list(stats) == s["expect_stats"]
+    assert list(counts) == s["expect_counts"]
+
+
+def test_oracle_runt_reads_zero(orc):
+    """Bytes past frames_len read as 0 (build-defined; the reference reads the
+    mbuf's stale bytes): a 20-byte IPv4 stub has daddr 0.0.0.0."""
+    t = orc.Tables(16, 0, 0, 0x09)
+    assert t.runtime_set(1, 0, 2, 2, [0, 1]) == 0  # a runtime that owns 0.0.0.0
+    frames = np.zeros(64, dtype=np.uint8)
+    frames[12:14] = [0x08, 0x00]
+    v, counts, stats = t.classify(frames, 1, 64, frames_len=20)
+    assert v[0]["uniqid"] == 1 and counts[1] == 1
+
+
+def test_oracle_table_semantics(orc):
+    t = orc.Tables(16, 1, 0, 0x09)
+    assert t.runtime_set(1, 0x0A000001, 4, 4, [0, 1, 2, 3]) == 0
+    assert t.runtime_set(2, 0x0A000001, 4, 4, [0, 1, 2, 3]) == -17  # EEXIST
+    assert t.runtime_set(16, 0x0A000002, 4, 4, [0, 1, 2, 3]) == -22
+    assert t.runtime_set(3, 0x0A000003, 4, 2, [0, 1, 9, 0]) == -22
+    assert t.runtime_del(5) == -2
+    assert t.runtime_del(1) == 0
+    assert t.runtime_set(2, 0x0A000001, 4, 4, [0, 1, 2, 3]) == 0
+
+
+def test_oracle_lrpc_variant_matches(orc):
+    """The classify+lrpc_send CPU variant yields the same verdicts."""
+    from oracle.orc import generate
+    frames, olf, rss = generate(0, 4096, 64, 16)
+    t = orc.Tables(16, 1, 0, 0x09)
+    for r in range(16):
+        assert t.runtime_set(r, orc.runtime_ip(r), 8, 8, list(range(8))) == 0
+    v1, c1, s1 = t.classify(frames, 4096, 64)
+    v2, c2, s2 = t.classify(frames, 4096, 64, lrpc=True)
+    assert (v1 == v2).all() and (c1 == c2).all()
+    assert s1[6] == s2[6] == 4096 and s2[1] == 0
