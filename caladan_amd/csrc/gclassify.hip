@@ -35,6 +35,9 @@ constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 constexpr uint32_t kToepBytes = 12 * 256 * 4;
 constexpr uint32_t kLdsTableBudget = 96 * 1024;
 
+/* tuning knobs for experiments (GCL_TUNE_BLOCKS_PER_CU caps the grid) */
+static int g_tune_bpc = 0;
+
 struct RtEntry {            /* 16 B per uniqid */
 	uint32_t m_lo, m_hi;     /* fastmod magic for thread_count */
 	uint16_t tc, active;     /* thread_count, active_thread_count */
@@ -61,6 +64,7 @@ struct KParams {
 	uint32_t off_rt, off_flow, off_toep, tables_lds_bytes;
 	uint32_t cflags;
 	uint32_t default_flags;
+	uint32_t nt_store;
 };
 
 /* ------------------------------------------------------------------------
@@ -118,7 +122,177 @@ __device__ __forceinline__ uint32_t tile_dword(const uint4 *tile, int p, int b)
 	return t32[tile_slot(p, b >> 4) * 4 + ((b & 15) >> 2)];
 }
 
-template <int MODE, bool TLDS, bool GENERAL>
+struct Counters {
+	uint32_t flowtag, hashmiss, unreg, unhandled;
+};
+
+struct Tables {
+	const uint2 *ipt;
+	const RtEntry *rtab;
+	const uint8_t *flow;
+	const uint32_t *toep;
+};
+
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+/* rx_one_pkt for the packet staged in row `tid` of the tile (rx.c:116-233) */
+template <int MODE, bool GENERAL>
+__device__ __forceinline__ void classify_one(const KParams &k, const uint4 *tile, int tid,
+                                             uint64_t idx, const Tables &tb, uint32_t *hist,
+                                             Counters &cnt)
+{
+	const uint2 *ipt = tb.ipt;
+	const RtEntry *rtab = tb.rtab;
+	const uint8_t *flow = tb.flow;
+	const uint32_t *toep = tb.toep;
+		const uint4 w0 = tile[tile_slot(tid, 0)];
+		const uint4 w1 = tile[tile_slot(tid, 1)];
+		const uint4 w2 = tile[tile_slot(tid, 2)];
+		const uint32_t d3 = w0.w, d5 = w1.y, d6 = w1.z, d7 = w1.w;
+		const uint32_t d8 = w2.x, d9 = w2.y, d10 = w2.z;
+
+		const uint32_t et = gcl::bswap16(d3 & 0xFFFF);       /* rx.c:154 */
+		const uint32_t vihl = (d3 >> 16) & 0xFF;
+		const uint32_t frag = gcl::bswap16(d5 & 0xFFFF);     /* also ARP op */
+		const uint32_t proto = d5 >> 24;
+		const uint32_t saddr = gcl::bswap32(gcl::mid32(d6, d7));
+		const uint32_t daddr = gcl::bswap32(gcl::mid32(d7, d8));   /* rx.c:159 */
+		const uint32_t arp_tip = gcl::bswap32(gcl::mid32(d9, d10)); /* rx.c:167 */
+		const uint32_t flags = (GENERAL && k.olflags) ? k.olflags[idx] : k.default_flags;
+
+		/* steering hash */
+		uint32_t hash = 0;
+		if (MODE == GCL_HASH_NIC) {
+			if (k.rss)
+				hash = k.rss[idx];
+		} else {
+			const uint32_t ihl = vihl & 0xF;
+			const bool hashable = et == GCL_ETHTYPE_IP && ihl >= 5 &&
+			                      (frag & 0x3FFF) == 0 && (proto == 6 || proto == 17);
+			if (hashable) {
+				uint32_t sport, dport;
+				if (ihl == 5) {
+					sport = gcl::bswap16(d8 >> 16);
+					dport = gcl::bswap16(d9 & 0xFFFF);
+				} else if (ihl <= 11) {
+					int o = 14 + 4 * (int)ihl;
+					sport = gcl::bswap16(tile_dword(tile, tid, o - 2) >> 16);
+					dport = gcl::bswap16(tile_dword(tile, tid, o + 2) & 0xFFFF);
+				} else {
+					uint64_t a = frame_off<GENERAL>(k, idx) + 14 + 4 * ihl;
+					sport = (uint32_t)frame_byte(k, a) << 8 | frame_byte(k, a + 1);
+					dport = (uint32_t)frame_byte(k, a + 2) << 8 | frame_byte(k, a + 3);
+				}
+				if (MODE == GCL_HASH_JENKINS) {
+					hash = gcl::jhash_5tuple(saddr, daddr, sport, dport, proto);
+				} else {
+					hash = toep[0 * 256 + (saddr >> 24)] ^
+					       toep[1 * 256 + ((saddr >> 16) & 0xFF)] ^
+					       toep[2 * 256 + ((saddr >> 8) & 0xFF)] ^
+					       toep[3 * 256 + (saddr & 0xFF)] ^
+					       toep[4 * 256 + (daddr >> 24)] ^
+					       toep[5 * 256 + ((daddr >> 16) & 0xFF)] ^
+					       toep[6 * 256 + ((daddr >> 8) & 0xFF)] ^
+					       toep[7 * 256 + (daddr & 0xFF)] ^
+					       toep[8 * 256 + (sport >> 8)] ^
+					       toep[9 * 256 + (sport & 0xFF)] ^
+					       toep[10 * 256 + (dport >> 8)] ^
+					       toep[11 * 256 + (dport & 0xFF)];
+				}
+			}
+		}
+		if (k.cflags & GCL_CFG_HASH16)
+			hash &= 0xFFFF;
+
+		int p = -1;
+		uint32_t action = GCL_ACT_DELIVER;
+		/* hardware flow tag, rx.c:131-146 */
+		if (GENERAL && (flags & GCL_F_FDIR_ID)) {
+			uint32_t mark = k.fdir ? k.fdir[idx] : 0;
+			cnt.flowtag++;
+			if (mark < k.max_rt && rtab[mark].tc != 0) {
+				p = (int)mark;
+				action = GCL_ACT_F_FDIR;
+			}
+		}
+		if (p < 0) {
+			uint32_t dst = 0;
+			bool lookup = true;
+			if (et == GCL_ETHTYPE_IP) {
+				dst = daddr;
+				cnt.hashmiss += !(flags & GCL_F_RSS_HASH); /* rx.c:160-163 */
+			} else if (et == GCL_ETHTYPE_ARP) {
+				dst = arp_tip;
+				if ((k.cflags & GCL_CFG_AZURE_ARP) && frag == GCL_ARP_OP_REPLY) {
+					action = GCL_ACT_BROADCAST; /* rx.c:171-190 */
+					lookup = false;
+				}
+			} else {
+				action = GCL_ACT_DROP_ETHERTYPE; /* rx.c:191-194 */
+				cnt.unhandled++;
+				lookup = false;
+			}
+			if (lookup) {
+				/* ip_to_proc: open addressing keyed by rte_jhash(&ip, 4, 0) */
+				uint32_t s = gcl::jhash_u32(dst) & k.ipt_mask;
+				for (;;) {
+					uint2 e = ipt[s];
+					if (e.y == kEmpty)
+						break;
+					if (e.x == dst) {
+						p = (int)e.y;
+						break;
+					}
+					s = (s + 1) & k.ipt_mask;
+				}
+				if (p < 0) {
+					if ((k.cflags & GCL_CFG_AZURE_ARP) && et == GCL_ETHTYPE_ARP &&
+					    frag == GCL_ARP_OP_REQUEST) {
+						action = GCL_ACT_ARP_RESPOND; /* rx.c:200-203 */
+					} else {
+						action = GCL_ACT_DROP_UNREG; /* rx.c:205, :232 */
+						cnt.unreg++;
+						cnt.unhandled++;
+					}
+				}
+			}
+		}
+
+		uint32_t uniq = GCL_NO_RUNTIME, thr = GCL_NO_THREAD;
+		if (p >= 0) {
+			/* rx_send_to_runtime, rx.c:55-72 */
+			const RtEntry re = rtab[p];
+			uniq = (uint32_t)p;
+			if (re.active) {
+				uint64_t M = (uint64_t)re.m_hi << 32 | re.m_lo;
+				thr = flow[re.flow_off + gcl::fastmod(hash, M, re.tc)];
+			} else {
+				action |= GCL_ACT_WAKE;
+			}
+			atomicAdd(&hist[p], 1u);
+		}
+	const u32x2 vd = {hash, uniq | thr << 16 | action << 24};
+	if (k.nt_store)
+		__builtin_nontemporal_store(vd, (u32x2 *)&k.verdicts[idx]);
+	else
+		*(u32x2 *)&k.verdicts[idx] = vd;
+}
+
+template <bool GENERAL>
+__device__ __forceinline__ void stage_tile(uint4 *tile, const uint4 r[4])
+{
+#pragma unroll
+	for (int j = 0; j < 4; j++) {
+		int c = j * kThreads + (int)threadIdx.x;
+		tile[tile_slot(c >> 2, c & 3)] = r[j];
+	}
+}
+
+/*
+ * Persistent grid: block b handles tiles b, b + G, b + 2G, ...; the frames of
+ * the next DEPTH tiles are in flight in registers while a tile is parsed.
+ */
+template <int MODE, bool TLDS, bool GENERAL, int DEPTH>
 __global__ void __launch_bounds__(kThreads)
 classify_kernel(KParams k)
 {
@@ -139,161 +313,46 @@ classify_kernel(KParams k)
 			dst[i] = src[i];
 		tab = lds_tab;
 	}
-	const uint2 *ipt = (const uint2 *)tab;
-	const RtEntry *rtab = (const RtEntry *)(tab + k.off_rt);
-	const uint8_t *flow = tab + k.off_flow;
-	const uint32_t *toep = (const uint32_t *)(tab + k.off_toep);
+	Tables tb;
+	tb.ipt = (const uint2 *)tab;
+	tb.rtab = (const RtEntry *)(tab + k.off_rt);
+	tb.flow = tab + k.off_flow;
+	tb.toep = (const uint32_t *)(tab + k.off_toep);
 	__syncthreads();
 
-	uint32_t n_flowtag = 0, n_hashmiss = 0, n_unreg = 0, n_unhandled = 0;
-	uint4 r[4];
+	Counters cnt = {0, 0, 0, 0};
+	const uint64_t G = gridDim.x;
+	uint4 ra[4], rb[4];
 	uint64_t t = blockIdx.x;
 	if (t < k.ntiles)
-		load_tile<GENERAL>(k, t, r);
+		load_tile<GENERAL>(k, t, ra);
+	if (DEPTH == 2 && t + G < k.ntiles)
+		load_tile<GENERAL>(k, t + G, rb);
 
-	for (; t < k.ntiles; t += gridDim.x) {
-#pragma unroll
-		for (int j = 0; j < 4; j++) {
-			int c = j * kThreads + tid;
-			tile[tile_slot(c >> 2, c & 3)] = r[j];
-		}
+	while (t < k.ntiles) {
+		stage_tile<GENERAL>(tile, ra);
 		__syncthreads();
-		uint64_t nt = t + gridDim.x;
-		if (nt < k.ntiles)
-			load_tile<GENERAL>(k, nt, r); /* in flight while this tile is parsed */
-
-		uint64_t idx = t * kThreads + tid;
-		if (idx < k.n) {
-			const uint4 w0 = tile[tile_slot(tid, 0)];
-			const uint4 w1 = tile[tile_slot(tid, 1)];
-			const uint4 w2 = tile[tile_slot(tid, 2)];
-			const uint32_t d3 = w0.w, d5 = w1.y, d6 = w1.z, d7 = w1.w;
-			const uint32_t d8 = w2.x, d9 = w2.y, d10 = w2.z;
-
-			const uint32_t et = gcl::bswap16(d3 & 0xFFFF);       /* rx.c:154 */
-			const uint32_t vihl = (d3 >> 16) & 0xFF;
-			const uint32_t frag = gcl::bswap16(d5 & 0xFFFF);     /* also ARP op */
-			const uint32_t proto = d5 >> 24;
-			const uint32_t saddr = gcl::bswap32(gcl::mid32(d6, d7));
-			const uint32_t daddr = gcl::bswap32(gcl::mid32(d7, d8));   /* rx.c:159 */
-			const uint32_t arp_tip = gcl::bswap32(gcl::mid32(d9, d10)); /* rx.c:167 */
-			const uint32_t flags = (GENERAL && k.olflags) ? k.olflags[idx] : k.default_flags;
-
-			/* steering hash */
-			uint32_t hash = 0;
-			if (MODE == GCL_HASH_NIC) {
-				if (k.rss)
-					hash = k.rss[idx];
-			} else {
-				const uint32_t ihl = vihl & 0xF;
-				const bool hashable = et == GCL_ETHTYPE_IP && ihl >= 5 &&
-				                      (frag & 0x3FFF) == 0 && (proto == 6 || proto == 17);
-				if (hashable) {
-					uint32_t sport, dport;
-					if (ihl == 5) {
-						sport = gcl::bswap16(d8 >> 16);
-						dport = gcl::bswap16(d9 & 0xFFFF);
-					} else if (ihl <= 11) {
-						int o = 14 + 4 * (int)ihl;
-						sport = gcl::bswap16(tile_dword(tile, tid, o - 2) >> 16);
-						dport = gcl::bswap16(tile_dword(tile, tid, o + 2) & 0xFFFF);
-					} else {
-						uint64_t a = frame_off<GENERAL>(k, idx) + 14 + 4 * ihl;
-						sport = (uint32_t)frame_byte(k, a) << 8 | frame_byte(k, a + 1);
-						dport = (uint32_t)frame_byte(k, a + 2) << 8 | frame_byte(k, a + 3);
-					}
-					if (MODE == GCL_HASH_JENKINS) {
-						hash = gcl::jhash_5tuple(saddr, daddr, sport, dport, proto);
-					} else {
-						hash = toep[0 * 256 + (saddr >> 24)] ^
-						       toep[1 * 256 + ((saddr >> 16) & 0xFF)] ^
-						       toep[2 * 256 + ((saddr >> 8) & 0xFF)] ^
-						       toep[3 * 256 + (saddr & 0xFF)] ^
-						       toep[4 * 256 + (daddr >> 24)] ^
-						       toep[5 * 256 + ((daddr >> 16) & 0xFF)] ^
-						       toep[6 * 256 + ((daddr >> 8) & 0xFF)] ^
-						       toep[7 * 256 + (daddr & 0xFF)] ^
-						       toep[8 * 256 + (sport >> 8)] ^
-						       toep[9 * 256 + (sport & 0xFF)] ^
-						       toep[10 * 256 + (dport >> 8)] ^
-						       toep[11 * 256 + (dport & 0xFF)];
-					}
-				}
-			}
-			if (k.cflags & GCL_CFG_HASH16)
-				hash &= 0xFFFF;
-
-			int p = -1;
-			uint32_t action = GCL_ACT_DELIVER;
-			/* hardware flow tag, rx.c:131-146 */
-			if (GENERAL && (flags & GCL_F_FDIR_ID)) {
-				uint32_t mark = k.fdir ? k.fdir[idx] : 0;
-				n_flowtag++;
-				if (mark < k.max_rt && rtab[mark].tc != 0) {
-					p = (int)mark;
-					action = GCL_ACT_F_FDIR;
-				}
-			}
-			if (p < 0) {
-				uint32_t dst = 0;
-				bool lookup = true;
-				if (et == GCL_ETHTYPE_IP) {
-					dst = daddr;
-					n_hashmiss += !(flags & GCL_F_RSS_HASH); /* rx.c:160-163 */
-				} else if (et == GCL_ETHTYPE_ARP) {
-					dst = arp_tip;
-					if ((k.cflags & GCL_CFG_AZURE_ARP) && frag == GCL_ARP_OP_REPLY) {
-						action = GCL_ACT_BROADCAST; /* rx.c:171-190 */
-						lookup = false;
-					}
-				} else {
-					action = GCL_ACT_DROP_ETHERTYPE; /* rx.c:191-194 */
-					n_unhandled++;
-					lookup = false;
-				}
-				if (lookup) {
-					/* ip_to_proc: open addressing keyed by rte_jhash(&ip, 4, 0) */
-					uint32_t s = gcl::jhash_u32(dst) & k.ipt_mask;
-					for (;;) {
-						uint2 e = ipt[s];
-						if (e.y == kEmpty)
-							break;
-						if (e.x == dst) {
-							p = (int)e.y;
-							break;
-						}
-						s = (s + 1) & k.ipt_mask;
-					}
-					if (p < 0) {
-						if ((k.cflags & GCL_CFG_AZURE_ARP) && et == GCL_ETHTYPE_ARP &&
-						    frag == GCL_ARP_OP_REQUEST) {
-							action = GCL_ACT_ARP_RESPOND; /* rx.c:200-203 */
-						} else {
-							action = GCL_ACT_DROP_UNREG; /* rx.c:205, :232 */
-							n_unreg++;
-							n_unhandled++;
-						}
-					}
-				}
-			}
-
-			uint32_t uniq = GCL_NO_RUNTIME, thr = GCL_NO_THREAD;
-			if (p >= 0) {
-				/* rx_send_to_runtime, rx.c:55-72 */
-				const RtEntry re = rtab[p];
-				uniq = (uint32_t)p;
-				if (re.active) {
-					uint64_t M = (uint64_t)re.m_hi << 32 | re.m_lo;
-					thr = flow[re.flow_off + gcl::fastmod(hash, M, re.tc)];
-				} else {
-					action |= GCL_ACT_WAKE;
-				}
-				atomicAdd(&hist[p], 1u);
-			}
-			k.verdicts[idx] = make_uint2(hash, uniq | thr << 16 | action << 24);
-		}
+		if (t + DEPTH * G < k.ntiles)
+			load_tile<GENERAL>(k, t + DEPTH * G, ra); /* in flight while parsing */
+		if (t * kThreads + tid < k.n)
+			classify_one<MODE, GENERAL>(k, tile, tid, t * kThreads + tid, tb, hist, cnt);
 		__syncthreads();
+		t += G;
+		if (DEPTH == 2) {
+			if (t >= k.ntiles)
+				break;
+			stage_tile<GENERAL>(tile, rb);
+			__syncthreads();
+			if (t + 2 * G < k.ntiles)
+				load_tile<GENERAL>(k, t + 2 * G, rb);
+			if (t * kThreads + tid < k.n)
+				classify_one<MODE, GENERAL>(k, tile, tid, t * kThreads + tid, tb, hist, cnt);
+			__syncthreads();
+			t += G;
+		}
 	}
+	uint32_t n_flowtag = cnt.flowtag, n_hashmiss = cnt.hashmiss;
+	uint32_t n_unreg = cnt.unreg, n_unhandled = cnt.unhandled;
 
 	/* flush per-block counters */
 	for (uint32_t i = tid; i < k.max_rt; i += kThreads) {
@@ -495,6 +554,9 @@ struct gcl_ctx {
 	std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending;
 	double prof_ms;
 	uint64_t prof_launches;
+	int tune_tables; /* GCL_TUNE_TABLES: 0 auto, 1 global, 2 lds-if-fits */
+	int tune_depth;  /* GCL_TUNE_DEPTH: tiles in flight per block (1 or 2) */
+	int tune_nt_store; /* GCL_TUNE_NT_STORE: non-temporal verdict stores */
 };
 
 extern "C" {
@@ -541,6 +603,16 @@ extern "C" int gcl_open(int hip_device, const struct gcl_cfg *cfg, struct gcl_ct
 	c->last_stream = nullptr;
 	c->prof_ms = 0;
 	c->prof_launches = 0;
+	{
+		const char *e = getenv("GCL_TUNE_TABLES");
+		c->tune_tables = e ? atoi(e) : 0;
+		e = getenv("GCL_TUNE_DEPTH");
+		c->tune_depth = e ? atoi(e) : 1;
+		e = getenv("GCL_TUNE_NT_STORE");
+		c->tune_nt_store = e ? atoi(e) : 0;
+		e = getenv("GCL_TUNE_BLOCKS_PER_CU");
+		g_tune_bpc = e ? atoi(e) : 0;
+	}
 	for (int i = 0; i < 2; i++) {
 		c->dimg[i] = nullptr;
 		if (hipMalloc(&c->dimg[i], c->image_cap) != hipSuccess)
@@ -686,7 +758,7 @@ static hipEvent_t prof_event(gcl_ctx *c)
 	return e;
 }
 
-template <int MODE, bool TLDS, bool GENERAL>
+template <int MODE, bool TLDS, bool GENERAL, int DEPTH>
 static hipError_t launch_t(const KParams &k, uint32_t lds, int num_cus, hipStream_t s)
 {
 	static std::mutex mu;
@@ -697,7 +769,7 @@ static hipError_t launch_t(const KParams &k, uint32_t lds, int num_cus, hipStrea
 	if (lds > 64 * 1024) {
 		static bool raised = false;
 		if (!raised) {
-			hipFuncSetAttribute((const void *)classify_kernel<MODE, TLDS, GENERAL>,
+			hipFuncSetAttribute((const void *)classify_kernel<MODE, TLDS, GENERAL, DEPTH>,
 			                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 			raised = true;
 		}
@@ -707,7 +779,7 @@ static hipError_t launch_t(const KParams &k, uint32_t lds, int num_cus, hipStrea
 		if (occ_lds[slot] != lds + 1) {
 			int o = 0;
 			if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-			        &o, classify_kernel<MODE, TLDS, GENERAL>, kThreads, lds) != hipSuccess ||
+			        &o, classify_kernel<MODE, TLDS, GENERAL, DEPTH>, kThreads, lds) != hipSuccess ||
 			    o < 1)
 				o = 1;
 			occ_cache[slot] = o;
@@ -715,25 +787,36 @@ static hipError_t launch_t(const KParams &k, uint32_t lds, int num_cus, hipStrea
 		}
 		occ = occ_cache[slot];
 	}
+	if (g_tune_bpc > 0 && g_tune_bpc < occ)
+		occ = g_tune_bpc;
 	uint64_t grid = (uint64_t)num_cus * (uint64_t)occ;
 	if (grid > k.ntiles)
 		grid = k.ntiles;
 	if (grid < 1)
 		grid = 1;
-	hipLaunchKernelGGL((classify_kernel<MODE, TLDS, GENERAL>), dim3((unsigned)grid),
+	hipLaunchKernelGGL((classify_kernel<MODE, TLDS, GENERAL, DEPTH>), dim3((unsigned)grid),
 	                   dim3(kThreads), lds, s, k);
 	return hipGetLastError();
 }
 
-template <int MODE>
-static hipError_t launch_mode(const KParams &k, bool tlds, bool general, uint32_t lds,
-                              int num_cus, hipStream_t s)
+template <int MODE, int DEPTH>
+static hipError_t launch_depth(const KParams &k, bool tlds, bool general, uint32_t lds,
+                               int num_cus, hipStream_t s)
 {
 	if (tlds)
-		return general ? launch_t<MODE, true, true>(k, lds, num_cus, s)
-		               : launch_t<MODE, true, false>(k, lds, num_cus, s);
-	return general ? launch_t<MODE, false, true>(k, lds, num_cus, s)
-	               : launch_t<MODE, false, false>(k, lds, num_cus, s);
+		return general ? launch_t<MODE, true, true, DEPTH>(k, lds, num_cus, s)
+		               : launch_t<MODE, true, false, DEPTH>(k, lds, num_cus, s);
+	return general ? launch_t<MODE, false, true, DEPTH>(k, lds, num_cus, s)
+	               : launch_t<MODE, false, false, DEPTH>(k, lds, num_cus, s);
+}
+
+template <int MODE>
+static hipError_t launch_mode(const KParams &k, bool tlds, bool general, int depth,
+                              uint32_t lds, int num_cus, hipStream_t s)
+{
+	if (depth == 2)
+		return launch_depth<MODE, 2>(k, tlds, general, lds, num_cus, s);
+	return launch_depth<MODE, 1>(k, tlds, general, lds, num_cus, s);
 }
 
 extern "C" int gcl_classify(struct gcl_ctx *c, const struct gcl_batch *b,
@@ -786,6 +869,7 @@ extern "C" int gcl_classify(struct gcl_ctx *c, const struct gcl_batch *b,
 	k.off_toep = c->off_toep;
 	k.cflags = c->cfg.flags;
 	k.default_flags = c->cfg.default_olflags;
+	k.nt_store = c->tune_nt_store;
 
 	/* the specialised fast path needs every header granule in range */
 	bool general = b->offs || b->olflags || b->fdir_hi ||
@@ -796,6 +880,10 @@ extern "C" int gcl_classify(struct gcl_ctx *c, const struct gcl_batch *b,
 	tab_bytes = align16(tab_bytes);
 	uint32_t hist_bytes = ((c->cfg.max_runtimes + 3) & ~3u) * 4;
 	bool tlds = tab_bytes <= kLdsTableBudget;
+	if (c->tune_tables == 1)
+		tlds = false;
+	else if (c->tune_tables == 2)
+		tlds = tab_bytes <= kLdsTableBudget;
 	k.tables_lds_bytes = tlds ? tab_bytes : 0;
 	uint32_t lds = kTileBytes + hist_bytes + (tlds ? tab_bytes : 0);
 
@@ -808,13 +896,13 @@ extern "C" int gcl_classify(struct gcl_ctx *c, const struct gcl_batch *b,
 	hipError_t err;
 	switch (c->cfg.hash_mode) {
 	case GCL_HASH_NIC:
-		err = launch_mode<GCL_HASH_NIC>(k, tlds, general, lds, c->num_cus, s);
+		err = launch_mode<GCL_HASH_NIC>(k, tlds, general, c->tune_depth, lds, c->num_cus, s);
 		break;
 	case GCL_HASH_JENKINS:
-		err = launch_mode<GCL_HASH_JENKINS>(k, tlds, general, lds, c->num_cus, s);
+		err = launch_mode<GCL_HASH_JENKINS>(k, tlds, general, c->tune_depth, lds, c->num_cus, s);
 		break;
 	default:
-		err = launch_mode<GCL_HASH_TOEPLITZ>(k, tlds, general, lds, c->num_cus, s);
+		err = launch_mode<GCL_HASH_TOEPLITZ>(k, tlds, general, c->tune_depth, lds, c->num_cus, s);
 		break;
 	}
 	if (e0) {

@@ -1,0 +1,102 @@
+"""Summarise a round's rocprofv3 outputs (gpurun_out/prof_<round>) into
+profiles/: kernel stats per workload, PMC bytes per classify launch corrected
+as MI355X_MICROARCH.md §HBM prescribes, and the membench calibration that
+justifies the correction.
+
+    python tools/prof_summary.py r01
+
+FETCH_SIZE correction: on gfx950 FETCH_SIZE reports half of the bytes of a
+wide coalesced read.  tools/membench.hip `calib` dispatches of known size
+measure the factor for each access pattern this kernel uses: a 2 GiB
+coalesced stream and 64-, 128- and 32-byte header reads at a 1536-B stride all
+report exactly half a 128-B line per line touched, so hbm_read = 2 x FETCH_SIZE.
+WRITE_SIZE reads exactly (calib rw kernels: 8 B per packet).
+"""
+import csv
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BYTES_PER_PKT = 72
+PKTS = {"udp64": 32 << 20, "tcp1500": 8 << 20, "mixed": 1 << 20}
+
+
+def rows(path):
+    with open(path) as f:
+        return list(csv.DictReader(f))
+
+
+def calib(base):
+    names = []
+    jl = os.path.join(base, "calib_FETCH_SIZE.jsonl")
+    for line in open(jl):
+        line = line.strip()
+        if line.startswith("{"):
+            names.append(json.loads(line))
+    out = {}
+    for c in ("FETCH_SIZE", "WRITE_SIZE"):
+        rs = [r for r in rows(os.path.join(base, f"calib_{c}", "run_counter_collection.csv"))
+              if "read_kernel" in r["Kernel_Name"] or "rw_kernel" in r["Kernel_Name"]]
+        # each pattern is dispatched twice (warm-up + timed)
+        for i, meta in enumerate(names):
+            vals = [float(rs[2 * i]["Counter_Value"]), float(rs[2 * i + 1]["Counter_Value"])]
+            d = out.setdefault(meta["pattern"], {"useful_bytes": meta["useful_bytes"]})
+            d[c + "_KB"] = sum(vals) / 2
+    for p, d in out.items():
+        read_bytes = d["useful_bytes"] if not p.startswith("rw_") else d["useful_bytes"] / 72 * 64
+        d["read_bytes_requested"] = read_bytes
+        d["fetch_reported_over_requested"] = round(d["FETCH_SIZE_KB"] * 1024 / read_bytes, 4)
+    return out
+
+
+def main(rnd):
+    base = os.path.join(ROOT, "gpurun_out", f"prof_{rnd}")
+    prof = os.path.join(ROOT, "profiles")
+    os.makedirs(prof, exist_ok=True)
+    cal = calib(base)
+    with open(os.path.join(prof, f"{rnd}_calibration.json"), "w") as f:
+        json.dump({"note": __doc__.strip().split("\n\n")[2], "patterns": cal}, f, indent=1)
+    for wl in PKTS:
+        tdir = os.path.join(base, f"{wl}_trace")
+        if not os.path.isdir(tdir):
+            continue
+        shutil.copy(os.path.join(tdir, "run_kernel_stats.csv"),
+                    os.path.join(prof, f"{rnd}_{wl}_kernel_stats.csv"))
+        st = [r for r in rows(os.path.join(tdir, "run_kernel_stats.csv")) if "classify_kernel" in r["Name"]]
+        pm = {}
+        for c in ("FETCH_SIZE", "WRITE_SIZE"):
+            vals = [float(r["Counter_Value"]) for r in
+                    rows(os.path.join(base, f"{wl}_{c}", "run_counter_collection.csv"))
+                    if "classify_kernel" in r["Kernel_Name"]]
+            pm[c] = sum(vals) / len(vals)
+        hbm_read = 2.0 * pm["FETCH_SIZE"] * 1024
+        hbm_write = pm["WRITE_SIZE"] * 1024
+        algo = PKTS[wl] * BYTES_PER_PKT
+        avg_ns = float(st[0]["AverageNs"])
+        out = {
+            "workload": wl,
+            "kernel": st[0]["Name"],
+            "calls": int(st[0]["Calls"]),
+            "avg_kernel_ns": avg_ns,
+            "min_kernel_ns": float(st[0]["MinNs"]),
+            "FETCH_SIZE_KB_per_launch": pm["FETCH_SIZE"],
+            "WRITE_SIZE_KB_per_launch": pm["WRITE_SIZE"],
+            "fetch_correction": 2.0,
+            "hbm_read_bytes_per_launch": hbm_read,
+            "hbm_write_bytes_per_launch": hbm_write,
+            "hbm_bytes_per_launch": hbm_read + hbm_write,
+            "algorithmic_bytes_per_launch": algo,
+            "traffic_over_algorithmic": round((hbm_read + hbm_write) / algo, 4),
+            "hbm_GBs_from_traffic": round((hbm_read + hbm_write) / (avg_ns * 1e-9) / 1e9, 1),
+            "algorithmic_GBs": round(algo / (avg_ns * 1e-9) / 1e9, 1),
+            "source": f"gpurun_out/prof_{rnd}/{wl}_{{trace,FETCH_SIZE,WRITE_SIZE}} (rocprofv3)",
+        }
+        with open(os.path.join(prof, f"pmc_{wl}.json"), "w") as f:
+            json.dump(out, f, indent=1)
+        print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "r01")
