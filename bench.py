@@ -90,12 +90,60 @@ class Workload:
                           counts=self.counts[:self.R], stats=self.counts[self.R:], stream=stream)
 
 
-def run_timed(w, steps, warmup, world, gathered):
+class Exchange:
+    """Multi-GPU step: classify into a per-step [counts | stats] vector, then
+    one RCCL all_gather of it on a side stream that overlaps the next step's
+    kernel; node-wide totals accumulate on that stream.  Two vectors
+    alternate so a step never zeroes one that a gather still reads."""
+
+    def __init__(self, w, world, device):
+        L = w.R + g.NR_STATS
+        self.world = world
+        self.cnt = [torch.zeros(L, dtype=torch.int64, device=device) for _ in range(2)]
+        self.gat = [torch.zeros(world * L, dtype=torch.int64, device=device) for _ in range(2)]
+        self.acc = torch.zeros(L, dtype=torch.int64, device=device)
+        self.done = [None, None]
+        self.comm = torch.cuda.Stream(device=device)
+        self.k = 0
+
+    def step(self, w):
+        b = self.k & 1
+        cur = torch.cuda.current_stream()
+        if self.done[b] is not None:
+            cur.wait_event(self.done[b])
+        self.cnt[b].zero_()
+        w.clf.classify(w.frames, w.n, w.stride, verdicts=w.verdicts, counts=self.cnt[b][:w.R],
+                       stats=self.cnt[b][w.R:], stream=cur.cuda_stream)
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        with torch.cuda.stream(self.comm):
+            self.comm.wait_event(ev)
+            work = shard.allgather_counts(self.cnt[b], self.gat[b], async_op=True)
+            if work is not None:
+                work.wait()
+            self.acc.add_(shard.global_counts(self.gat[b], self.world))
+            d = torch.cuda.Event()
+            d.record(self.comm)
+            self.done[b] = d
+        self.k += 1
+
+    def drain(self):
+        torch.cuda.current_stream().wait_stream(self.comm)
+
+
+def run_timed(w, steps, warmup, world, ex=None):
     stream = torch.cuda.current_stream().cuda_stream
+
+    def one():
+        if ex is not None:
+            ex.step(w)
+        else:
+            w.step(stream)
+
     for _ in range(warmup):
-        w.step(stream)
-        if world > 1:
-            shard.allgather_counts(w.counts, gathered)
+        one()
+    if ex is not None:
+        ex.drain()
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -103,9 +151,9 @@ def run_timed(w, steps, warmup, world, gathered):
     w.clf.kernel_time(reset=True)
     t0 = time.perf_counter()
     for _ in range(steps):
-        w.step(stream)
-        if world > 1:
-            shard.allgather_counts(w.counts, gathered)
+        one()
+    if ex is not None:
+        ex.drain()
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -113,7 +161,9 @@ def run_timed(w, steps, warmup, world, gathered):
     el = time.perf_counter() - t0
     kms, nl = w.clf.kernel_time(reset=True)
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        t = torch.tensor([el], dtype=torch.float64)
+        if torch.distributed.get_backend() == "nccl":
+            t = t.cuda()
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         el = float(t.item())
     return el, kms / max(nl, 1)
@@ -133,6 +183,48 @@ def roofline(w, kernel_ms):
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             "bytes_per_pkt": BYTES_PER_PKT, "kernel_ms": round(kernel_ms, 4)}
+
+
+def e2e_bench(device, reps=3):
+    """Rates with the frames in pinned HOST memory (the NIC's mbufs) and the
+    verdicts returned to host memory: PCIe-inclusive, never `value`.
+    DMA-gather of the 64-B header granules (COPY), PCIe zero-copy reads by the
+    kernel (ZEROCOPY), and for jumbo frames the naive full-frame H2D copy."""
+    out = {}
+    for name, n in (("udp64", 32 << 20), ("mixed", 256 << 10)):
+        wl, _, stride, R, T, _ = WORKLOADS[name]
+        dfr = torch.zeros(n * stride, dtype=torch.uint8, device=device)
+        g.generate(wl, n, stride, R, dfr, seed=SEED)
+        hfr = torch.empty(n * stride, dtype=torch.uint8).pin_memory()
+        hfr.copy_(dfr)
+        hv = torch.empty(n * 8, dtype=torch.uint8).pin_memory()
+        clf = g.Classifier(device.index or 0, R, g.HASH_JENKINS)
+        setup_tables(clf, R, T)
+        res = {"pkts": n, "slot_stride": stride}
+        for tag, mode, nst in (("copy_hdr_2streams", g.E2E_COPY, 2), ("copy_hdr_4streams", g.E2E_COPY, 4),
+                               ("zerocopy", g.E2E_ZEROCOPY, 1)):
+            clf.classify_host(hfr, n, stride, verdicts=hv, mode=mode, nstreams=nst)
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                clf.classify_host(hfr, n, stride, verdicts=hv, mode=mode, nstreams=nst)
+            dt = (time.perf_counter() - t0) / reps
+            res[tag + "_mpps"] = round(n / dt / 1e6, 1)
+        # naive: copy whole frames H2D, classify in HBM, copy verdicts back
+        dv = torch.empty(n * 8, dtype=torch.uint8, device=device)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            dfr.copy_(hfr, non_blocking=True)
+            clf.classify(dfr, n, stride, verdicts=dv, stream=torch.cuda.current_stream().cuda_stream)
+            hv.copy_(dv, non_blocking=True)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / reps
+        res["copy_full_frames_mpps"] = round(n / dt / 1e6, 2)
+        res["h2d_full_frames_GBs"] = round(n * stride / dt / 1e9, 1)
+        out[name] = res
+        del dfr, hfr, hv, dv, clf
+        torch.cuda.empty_cache()
+    return out
 
 
 def cpu_baseline(budget_s=12.0):
@@ -193,25 +285,30 @@ def main():
     ap.add_argument("--workload", default="udp64", choices=sorted(WORKLOADS))
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo only to rehearse N>1 on one GPU")
     args = ap.parse_args()
 
     rank, world, local = shard.dist_env()
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    dev_index = local % ndev
+    torch.cuda.set_device(dev_index)
+    device = torch.device("cuda", dev_index)
     if world > 1:
-        shard.init(rank, world)
+        shard.init(rank, world, backend=args.dist_backend)
 
     w = Workload(args.workload, rank, world, device)
-    gathered = torch.zeros(world * w.counts.numel(), dtype=torch.int64, device=device)
-    el, kms = run_timed(w, args.steps, args.warmup, world, gathered)
+    ex = Exchange(w, world, device) if world > 1 else None
+    el, kms = run_timed(w, args.steps, args.warmup, world, ex)
     total_pkts = w.n * world * args.steps
     value = total_pkts / el / 1e6
     # correctness spot check: every packet of every step was accounted for
     if world > 1:
-        tot = gathered.view(world, -1)[:, :w.R].sum().item()
+        tot = ex.acc[:w.R].sum().item()
         expect = w.n * world * (args.steps + args.warmup)
     else:
         tot = w.counts[:w.R].sum().item()
@@ -232,8 +329,9 @@ def main():
         "config": {"workload": f"{args.workload}: {w.desc}", "pkts_per_gpu": w.n,
                    "slot_stride": w.stride, "runtimes": w.R, "kthreads": w.T,
                    "hash": "jenkins (lookup3 13-B 5-tuple)",
-                   "parallelism": (f"dp{world}: round-robin 64Ki-pkt shards, RCCL all_gather "
-                                   "of per-runtime counts" if world > 1 else "single GPU")},
+                   "parallelism": (f"dp{world}: round-robin 64Ki-pkt shards, {args.dist_backend} "
+                                   "all_gather of per-runtime counts per step (overlapped)"
+                                   if world > 1 else "single GPU")},
         "roofline": roofline(w, kms),
         "counts_check": "ok" if tot == expect else f"MISMATCH {tot} != {expect}",
     }
@@ -242,7 +340,7 @@ def main():
 
     if world == 1 and not args.no_secondary and args.workload == "udp64":
         w2 = Workload("tcp1500", rank, world, device)
-        el2, kms2 = run_timed(w2, max(5, args.steps // 5), 2, 1, None)
+        el2, kms2 = run_timed(w2, max(5, args.steps // 5), 2, 1)
         steps2 = max(5, args.steps // 5)
         result["secondary"] = {
             "workload": f"tcp1500: {w2.desc}",
@@ -253,6 +351,9 @@ def main():
         }
         del w2
         torch.cuda.empty_cache()
+
+    if world == 1 and not args.no_e2e and args.workload == "udp64":
+        result["e2e"] = e2e_bench(device)
 
     if world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(args.cpu_budget)

@@ -547,6 +547,17 @@ struct gcl_ctx {
 	hipEvent_t img_free[2];
 	uint8_t *staging;
 	hipEvent_t staging_free;
+	hipEvent_t tables_ready;   /* recorded after each table upload */
+	/* end-to-end (host buffers) resources, allocated on first use */
+	struct E2E {
+		int nstreams;
+		uint64_t chunk;
+		hipStream_t st[4];
+		uint8_t *slab[4];        /* header granules of one chunk */
+		uint8_t *side[4];        /* per-packet olflags/rss/fdir of one chunk */
+		struct gcl_verdict *verd[4];
+		uint64_t *acc;           /* device counts | stats */
+	} e2e;
 	int cur;
 	hipStream_t last_stream;
 	/* profiling */
@@ -622,6 +633,8 @@ extern "C" int gcl_open(int hip_device, const struct gcl_cfg *cfg, struct gcl_ct
 	if (hipHostMalloc(&c->staging, c->image_cap, hipHostMallocDefault) != hipSuccess)
 		goto fail;
 	hipEventCreateWithFlags(&c->staging_free, hipEventDisableTiming);
+	hipEventCreateWithFlags(&c->tables_ready, hipEventDisableTiming);
+	memset(&c->e2e, 0, sizeof(c->e2e));
 	*out = c;
 	return 0;
 fail:
@@ -644,6 +657,14 @@ extern "C" void gcl_close(struct gcl_ctx *c)
 	}
 	hipHostFree(c->staging);
 	hipEventDestroy(c->staging_free);
+	hipEventDestroy(c->tables_ready);
+	for (int i = 0; i < c->e2e.nstreams; i++) {
+		hipStreamDestroy(c->e2e.st[i]);
+		hipFree(c->e2e.slab[i]);
+		hipFree(c->e2e.side[i]);
+		hipFree(c->e2e.verd[i]);
+	}
+	hipFree(c->e2e.acc);
 	for (auto &pr : c->ev_pending) {
 		hipEventDestroy(pr.first);
 		hipEventDestroy(pr.second);
@@ -819,6 +840,25 @@ static hipError_t launch_mode(const KParams &k, bool tlds, bool general, int dep
 	return launch_depth<MODE, 1>(k, tlds, general, lds, num_cus, s);
 }
 
+/* Upload a new table snapshot on @s if anything changed; launches on any
+ * stream wait for c->tables_ready before reading the image. */
+static int upload_tables(gcl_ctx *c, hipStream_t s)
+{
+	if (!c->dirty)
+		return 0;
+	hipEventSynchronize(c->staging_free);
+	uint32_t bytes = build_image(c);
+	int nxt = c->cur ^ 1;
+	hipStreamWaitEvent(s, c->img_free[nxt], 0);
+	if (hipMemcpyAsync(c->dimg[nxt], c->staging, bytes, hipMemcpyHostToDevice, s) != hipSuccess)
+		return -EIO;
+	hipEventRecord(c->staging_free, s);
+	hipEventRecord(c->tables_ready, s);
+	c->cur = nxt;
+	c->dirty = false;
+	return 0;
+}
+
 extern "C" int gcl_classify(struct gcl_ctx *c, const struct gcl_batch *b,
                             struct gcl_verdict *verdicts, uint64_t *runtime_counts,
                             uint64_t *stats, void *hip_stream)
@@ -834,19 +874,9 @@ extern "C" int gcl_classify(struct gcl_ctx *c, const struct gcl_batch *b,
 		return -EINVAL;
 	hipSetDevice(c->device);
 
-	/* upload a new table snapshot on this stream if anything changed */
-	if (c->dirty) {
-		hipEventSynchronize(c->staging_free);
-		uint32_t bytes = build_image(c);
-		int nxt = c->cur ^ 1;
-		hipStreamWaitEvent(s, c->img_free[nxt], 0);
-		if (hipMemcpyAsync(c->dimg[nxt], c->staging, bytes, hipMemcpyHostToDevice, s) !=
-		    hipSuccess)
-			return -EIO;
-		hipEventRecord(c->staging_free, s);
-		c->cur = nxt;
-		c->dirty = false;
-	}
+	if (upload_tables(c, s))
+		return -EIO;
+	hipStreamWaitEvent(s, c->tables_ready, 0);
 
 	KParams k = {};
 	k.frames = b->frames;
@@ -979,3 +1009,168 @@ extern "C" int gcl_generate(const struct gcl_gen_params *p, uint8_t *frames, uin
 }
 
 extern "C" const char *gcl_version(void) { return GCL_VERSION; }
+
+/* ==========================================================================
+ * End-to-end: frames in host memory (the NIC's mbufs), verdicts back to host.
+ */
+extern "C" int gcl_host_register(void *p, size_t len)
+{
+	if (!p || !len)
+		return -EINVAL;
+	return hipHostRegister(p, len, hipHostRegisterMapped | hipHostRegisterPortable) == hipSuccess
+	               ? 0 : -ENOMEM;
+}
+
+extern "C" int gcl_host_unregister(void *p)
+{
+	return hipHostUnregister(p) == hipSuccess ? 0 : -EINVAL;
+}
+
+static int e2e_setup(gcl_ctx *c, int nstreams, uint64_t chunk)
+{
+	gcl_ctx::E2E &e = c->e2e;
+	if (e.nstreams == nstreams && e.chunk == chunk)
+		return 0;
+	for (int i = 0; i < e.nstreams; i++) {
+		hipStreamDestroy(e.st[i]);
+		hipFree(e.slab[i]);
+		hipFree(e.side[i]);
+		hipFree(e.verd[i]);
+	}
+	if (!e.acc && hipMalloc(&e.acc, (GCL_MAX_PROC + GCL_NR_STATS) * 8) != hipSuccess)
+		return -ENOMEM;
+	e.nstreams = 0;
+	for (int i = 0; i < nstreams; i++) {
+		if (hipStreamCreateWithFlags(&e.st[i], hipStreamNonBlocking) != hipSuccess ||
+		    hipMalloc(&e.slab[i], chunk * GCL_HDR_GRANULE) != hipSuccess ||
+		    hipMalloc(&e.side[i], chunk * 9) != hipSuccess ||
+		    hipMalloc(&e.verd[i], chunk * sizeof(struct gcl_verdict)) != hipSuccess)
+			return -ENOMEM;
+		e.nstreams = i + 1;
+	}
+	e.chunk = chunk;
+	return 0;
+}
+
+/* device address of pinned / registered host memory, or NULL */
+static void *mapped(const void *h)
+{
+	void *d = nullptr;
+	if (!h)
+		return nullptr;
+	if (hipHostGetDevicePointer(&d, (void *)h, 0) != hipSuccess)
+		return nullptr;
+	return d;
+}
+
+extern "C" int gcl_classify_host(struct gcl_ctx *c, const struct gcl_batch *hb,
+                                 struct gcl_verdict *host_verdicts, uint64_t *host_counts,
+                                 uint64_t *host_stats, const struct gcl_e2e_opts *o)
+{
+	if (!c || !hb || !host_verdicts || !o || o->mode > GCL_E2E_ZEROCOPY)
+		return -EINVAL;
+	if (hb->n == 0)
+		return 0;
+	hipSetDevice(c->device);
+	const uint32_t max_rt = c->cfg.max_runtimes;
+	int nst = o->nstreams ? (int)o->nstreams : 2;
+	if (nst > 4)
+		nst = 4;
+	uint64_t chunk = o->chunk ? o->chunk : (1ull << 20);
+	int ret = e2e_setup(c, nst, chunk);
+	if (ret)
+		return ret;
+	gcl_ctx::E2E &e = c->e2e;
+	hipStream_t s0 = e.st[0];
+	hipMemsetAsync(e.acc, 0, (max_rt + GCL_NR_STATS) * 8, s0);
+	if (upload_tables(c, s0))
+		return -EIO;
+	hipEvent_t ready;
+	hipEventCreateWithFlags(&ready, hipEventDisableTiming);
+	hipEventRecord(ready, s0);
+	for (int i = 1; i < nst; i++)
+		hipStreamWaitEvent(e.st[i], ready, 0);
+
+	uint64_t *dcounts = e.acc, *dstats = e.acc + max_rt;
+	if (o->mode == GCL_E2E_ZEROCOPY) {
+		/* the kernel reads the headers straight out of host memory over
+		 * PCIe and writes verdicts straight into host memory */
+		struct gcl_batch db = *hb;
+		db.frames = (const uint8_t *)mapped(hb->frames);
+		db.offs = (const uint64_t *)mapped(hb->offs);
+		db.olflags = (const uint8_t *)mapped(hb->olflags);
+		db.rss = (const uint32_t *)mapped(hb->rss);
+		db.fdir_hi = (const uint32_t *)mapped(hb->fdir_hi);
+		struct gcl_verdict *dv = (struct gcl_verdict *)mapped(host_verdicts);
+		if (!db.frames || !dv || (hb->offs && !db.offs) || (hb->olflags && !db.olflags) ||
+		    (hb->rss && !db.rss) || (hb->fdir_hi && !db.fdir_hi)) {
+			hipEventDestroy(ready);
+			return -EFAULT; /* not pinned/registered: see gcl_host_register */
+		}
+		ret = gcl_classify(c, &db, dv, dcounts, dstats, s0);
+	} else {
+		if (hb->offs || (hb->stride & 15) || hb->stride < GCL_HDR_GRANULE) {
+			hipEventDestroy(ready);
+			return -EINVAL; /* the copy path gathers fixed-stride header granules */
+		}
+		for (uint64_t s = 0, ci = 0; s < hb->n && !ret; s += chunk, ci++) {
+			const int i = (int)(ci % nst);
+			const uint64_t m = hb->n - s < chunk ? hb->n - s : chunk;
+			hipStream_t st = e.st[i];
+			/* H2D of only the 64-B header granule of every slot (2D DMA) */
+			const uint8_t *src = hb->frames + s * hb->stride;
+			uint64_t avail = hb->frames_len > s * hb->stride ? hb->frames_len - s * hb->stride : 0;
+			if (avail < (m - 1) * hb->stride + GCL_HDR_GRANULE) {
+				ret = -EINVAL;
+				break;
+			}
+			if (hb->stride == GCL_HDR_GRANULE)
+				hipMemcpyAsync(e.slab[i], src, m * GCL_HDR_GRANULE, hipMemcpyHostToDevice, st);
+			else
+				hipMemcpy2DAsync(e.slab[i], GCL_HDR_GRANULE, src, hb->stride, GCL_HDR_GRANULE, m,
+				                 hipMemcpyHostToDevice, st);
+			struct gcl_batch db = {};
+			db.frames = e.slab[i];
+			db.frames_len = m * GCL_HDR_GRANULE;
+			db.stride = GCL_HDR_GRANULE;
+			db.n = m;
+			uint8_t *side = e.side[i];
+			if (hb->olflags) {
+				hipMemcpyAsync(side, hb->olflags + s, m, hipMemcpyHostToDevice, st);
+				db.olflags = side;
+			}
+			if (hb->rss) {
+				hipMemcpyAsync(side + chunk, hb->rss + s, m * 4, hipMemcpyHostToDevice, st);
+				db.rss = (const uint32_t *)(side + chunk);
+			}
+			if (hb->fdir_hi) {
+				hipMemcpyAsync(side + 5 * chunk, hb->fdir_hi + s, m * 4, hipMemcpyHostToDevice, st);
+				db.fdir_hi = (const uint32_t *)(side + 5 * chunk);
+			}
+			ret = gcl_classify(c, &db, e.verd[i], dcounts, dstats, st);
+			hipMemcpyAsync(host_verdicts + s, e.verd[i], m * sizeof(struct gcl_verdict),
+			               hipMemcpyDeviceToHost, st);
+		}
+		for (int i = 1; i < nst; i++) {
+			hipEventRecord(ready, e.st[i]);
+			hipStreamWaitEvent(s0, ready, 0);
+		}
+		hipEventRecord(c->img_free[c->cur], s0);
+	}
+	uint64_t tmp[GCL_MAX_PROC + GCL_NR_STATS];
+	hipMemcpyAsync(tmp, e.acc, (max_rt + GCL_NR_STATS) * 8, hipMemcpyDeviceToHost, s0);
+	hipError_t err = hipStreamSynchronize(s0);
+	hipEventDestroy(ready);
+	if (ret)
+		return ret;
+	if (err != hipSuccess)
+		return -EIO;
+	if (host_counts)
+		for (uint32_t i = 0; i < max_rt; i++)
+			host_counts[i] += tmp[i];
+	if (host_stats)
+		for (int i = 0; i < GCL_NR_STATS; i++)
+			host_stats[i] += tmp[max_rt + i];
+	c->last_stream = s0;
+	return 0;
+}

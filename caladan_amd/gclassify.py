@@ -75,6 +75,13 @@ class GclGenParams(ctypes.Structure):
                 ("nflows", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
 
 
+class GclE2eOpts(ctypes.Structure):
+    _fields_ = [("mode", ctypes.c_uint32), ("nstreams", ctypes.c_uint32), ("chunk", ctypes.c_uint64)]
+
+
+E2E_COPY, E2E_ZEROCOPY = 0, 1
+
+
 class GclVerdict(ctypes.Structure):
     _fields_ = [("hash", ctypes.c_uint32), ("uniqid", ctypes.c_uint16),
                 ("thread", ctypes.c_uint8), ("action", ctypes.c_uint8)]
@@ -139,6 +146,9 @@ def _load():
         "gcl_lrpc_init_out": (i32, [ctypes.POINTER(GclLrpcChanOut), ctypes.POINTER(GclLrpcMsg), ctypes.c_uint, ctypes.POINTER(u32)]),
         "gcl_lrpc_send": (ctypes.c_bool, [ctypes.POINTER(GclLrpcChanOut), u64, ctypes.c_ulong]),
         "gcl_rx_make_cmd": (u64, [u16, ctypes.c_uint8]),
+        "gcl_classify_host": (i32, [vp, ctypes.POINTER(GclBatch), vp, vp, vp, ctypes.POINTER(GclE2eOpts)]),
+        "gcl_host_register": (i32, [vp, ctypes.c_size_t]),
+        "gcl_host_unregister": (i32, [vp]),
         "gcl_host_deliver": (u64, [vp, u32, vp, i32, vp, vp, vp, ctypes.c_uint8, vp, u64,
                                    ctypes.POINTER(GclHostOps), vp]),
     }
@@ -270,6 +280,18 @@ class Classifier:
                      fdir_hi=_ptr(fdir_hi), pkt_len=None, n=n)
         return _check(lib.gcl_classify(self._ctx, ctypes.byref(b), _ptr(verdicts), _ptr(counts),
                                        _ptr(stats), stream), "gcl_classify")
+
+    def classify_host(self, frames, n, stride=0, verdicts=None, counts=None, stats=None,
+                      olflags=None, rss=None, fdir_hi=None, offs=None, frames_len=None,
+                      mode=E2E_COPY, nstreams=2, chunk=1 << 20):
+        """End-to-end: host (pinned) frames in, host verdicts out (synchronous)."""
+        b = GclBatch(frames=_ptr(frames),
+                     frames_len=_nbytes(frames) if frames_len is None else frames_len,
+                     stride=stride, offs=_ptr(offs), olflags=_ptr(olflags), rss=_ptr(rss),
+                     fdir_hi=_ptr(fdir_hi), pkt_len=None, n=n)
+        o = GclE2eOpts(mode=mode, nstreams=nstreams, chunk=chunk)
+        return _check(lib.gcl_classify_host(self._ctx, ctypes.byref(b), _ptr(verdicts), _ptr(counts),
+                                            _ptr(stats), ctypes.byref(o)), "gcl_classify_host")
 
     def sync(self):
         return _check(lib.gcl_sync(self._ctx), "gcl_sync")

@@ -47,10 +47,17 @@ def shard_indices(n_global, rank, world, block):
     return np.concatenate(idx) if idx else np.zeros(0, dtype=np.int64)
 
 
-def allgather_counts(local, gathered):
-    """all_gather of this rank's [counts | stats] vector into gathered[W * len]."""
-    dist.all_gather_into_tensor(gathered, local)
-    return gathered
+def allgather_counts(local, gathered, async_op=False):
+    """all_gather of this rank's [counts | stats] vector into gathered[W * len].
+
+    On GPUs this is one RCCL all_gather (ProcessGroupNCCL) over xGMI; gloo
+    (CPU tests, single-GPU rehearsal) goes through host tensors."""
+    if dist.get_backend() == "nccl":
+        return dist.all_gather_into_tensor(gathered, local, async_op=async_op)
+    parts = [torch.empty_like(local, device="cpu") for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, local.cpu())
+    gathered.copy_(torch.cat(parts).to(gathered.device))
+    return None
 
 
 def global_counts(gathered, world):

@@ -201,6 +201,38 @@ int gcl_classify(struct gcl_ctx *ctx, const struct gcl_batch *b,
                  struct gcl_verdict *verdicts, uint64_t *runtime_counts,
                  uint64_t *stats, void *hip_stream);
 
+/*
+ * End-to-end classification of a batch whose frames are in HOST memory (the
+ * NIC's mbufs in the iokernel's ingress region), verdicts returned to host
+ * memory; synchronous.  Two transports:
+ *  GCL_E2E_COPY     the 64-B header granule of every fixed-stride slot is
+ *                   DMA-gathered into HBM (hipMemcpy2DAsync), classified, and
+ *                   the verdicts copied back; chunks pipelined over nstreams.
+ *  GCL_E2E_ZEROCOPY the kernel reads the headers directly from pinned or
+ *                   registered host memory over PCIe (gcl_host_register) and
+ *                   writes the verdicts directly into host memory.
+ * @host_counts / @host_stats are accumulated (may be NULL).
+ * Returns -EFAULT when a ZEROCOPY buffer is not pinned/registered.
+ */
+enum gcl_e2e_mode {
+	GCL_E2E_COPY = 0,
+	GCL_E2E_ZEROCOPY = 1,
+};
+
+struct gcl_e2e_opts {
+	uint32_t mode;      /* enum gcl_e2e_mode */
+	uint32_t nstreams;  /* COPY: chunks in flight (1..4, 0 = 2) */
+	uint64_t chunk;     /* COPY: packets per chunk (0 = 1 Mi) */
+};
+
+int gcl_classify_host(struct gcl_ctx *ctx, const struct gcl_batch *host_batch,
+                      struct gcl_verdict *host_verdicts, uint64_t *host_counts,
+                      uint64_t *host_stats, const struct gcl_e2e_opts *opts);
+
+/* Pin + map host memory for ZEROCOPY / async copies (hipHostRegister). */
+int gcl_host_register(void *p, size_t len);
+int gcl_host_unregister(void *p);
+
 /* Synchronise the context's last stream. */
 int gcl_sync(struct gcl_ctx *ctx);
 

@@ -1,0 +1,271 @@
+"""C-ABI surface checks that need no GPU: every declared symbol is exported,
+the host-side C (steer_flows, lrpc, rx_make_cmd, the verdict post-pass) behaves
+like the reference functions it replaces."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def g():
+    from caladan_amd import gclassify
+    return gclassify
+
+
+def declared_functions():
+    names = set()
+    for h in ("gclassify.h", "gcl_host.h"):
+        src = open(os.path.join(ROOT, "include", h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        names |= set(re.findall(r"\b(gcl_\w+)\s*\(", src))
+    return sorted(names)
+
+
+def test_library_exports_every_declared_symbol(g):
+    names = declared_functions()
+    assert len(names) >= 18, names
+    lib = ctypes.CDLL(g.LIB_PATH)
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_struct_layouts(g):
+    assert ctypes.sizeof(g.GclCfg) == 56
+    assert ctypes.sizeof(g.GclBatch) == 72
+    assert ctypes.sizeof(g.GclVerdict) == 8
+    assert ctypes.sizeof(g.GclLrpcMsg) == 16
+    assert ctypes.sizeof(g.GclLrpcChanOut) == 32  # struct lrpc_chan_out, lrpc.h:28-35
+
+
+def test_open_without_gpu_is_enodev(g):
+    torch = pytest.importorskip("torch")
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(OSError) as e:
+        g.Classifier(0, 16)
+    assert e.value.errno in (19, 22)
+
+
+def test_open_rejects_bad_cfg(g):
+    cfg = g.GclCfg(max_runtimes=0)
+    ctx = ctypes.c_void_p()
+    assert g.lib.gcl_open(0, ctypes.byref(cfg), ctypes.byref(ctx)) == -22
+    cfg = g.GclCfg(max_runtimes=4097)
+    assert g.lib.gcl_open(0, ctypes.byref(cfg), ctypes.byref(ctx)) == -22
+    cfg = g.GclCfg(max_runtimes=16, hash_mode=3)
+    assert g.lib.gcl_open(0, ctypes.byref(cfg), ctypes.byref(ctx)) == -22
+
+
+def test_steer_flows_matches_oracle(g, orc):
+    rng = np.random.default_rng(3)
+    for _ in range(500):
+        tc = int(rng.integers(1, 257))
+        act = int(rng.integers(1, tc + 1))
+        idx = [int(x) for x in rng.choice(tc, size=act, replace=False)]
+        assert g.steer_flows(tc, idx) == orc.steer_flows(tc, idx)
+    # sched.c:128-129: no active thread leaves the table untouched
+    out = (ctypes.c_uint16 * 4)(7, 7, 7, 7)
+    assert g.lib.gcl_steer_flows(4, None, 0, out) == 0 and list(out) == [7, 7, 7, 7]
+    # hand example: 8 threads, active [2, 5, 7]
+    assert g.steer_flows(8, [2, 5, 7]) == [2, 5, 2, 7, 2, 5, 5, 7]
+    with pytest.raises(OSError):
+        g.steer_flows(4, [4])
+    with pytest.raises(OSError):
+        g.steer_flows(300, [1])
+
+
+def test_rx_make_cmd(g):
+    # rx.c:24-38: RX_NET_RECV | len << 16 | csum_type << 48
+    assert g.lib.gcl_rx_make_cmd(1514, g.F_IP_CKSUM_GOOD) == (1514 << 16) | (1 << 48)
+    for f in (g.F_IP_CKSUM_UNKNOWN, g.F_IP_CKSUM_BAD, g.F_IP_CKSUM_NONE):
+        assert g.lib.gcl_rx_make_cmd(60, f | g.F_RSS_HASH) == 60 << 16
+
+
+class Ring:
+    def __init__(self, g, size):
+        self.tbl = (g.GclLrpcMsg * size)()
+        self.wb = ctypes.c_uint32(0)
+        self.chan = g.GclLrpcChanOut()
+        assert g.lib.gcl_lrpc_init_out(ctypes.byref(self.chan), self.tbl, size, ctypes.byref(self.wb)) == 0
+        self.size = size
+        self.read = 0
+
+    def drain(self):
+        """Consumer: lrpc_recv on the parity bit (lrpc.h:102-127)."""
+        out = []
+        while True:
+            m = self.tbl[self.read & (self.size - 1)]
+            parity = 0 if (self.read & self.size) else 1
+            if (m.cmd >> 63) != parity:
+                break
+            out.append((m.cmd & ~(1 << 63), m.payload))
+            self.read += 1
+        self.wb.value = self.read
+        return out
+
+
+def test_lrpc_ring_semantics(g):
+    tbl = (g.GclLrpcMsg * 3)()
+    ch = g.GclLrpcChanOut()
+    assert g.lib.gcl_lrpc_init_out(ctypes.byref(ch), tbl, 3, None) == -22
+    r = Ring(g, 4)
+    for i in range(4):
+        assert g.lib.gcl_lrpc_send(ctypes.byref(r.chan), i, 100 + i)
+    assert not g.lib.gcl_lrpc_send(ctypes.byref(r.chan), 9, 9)  # full
+    assert r.drain() == [(i, 100 + i) for i in range(4)]
+    for i in range(4):  # second lap flips the parity bit
+        assert g.lib.gcl_lrpc_send(ctypes.byref(r.chan), 10 + i, i)
+    assert r.drain() == [(10 + i, i) for i in range(4)]
+
+
+def _host_procs(g, runtimes, ring_size):
+    procs, rings, keep = {}, {}, []
+    for rt in runtimes:
+        p = g.GclHostProc()
+        p.uniqid = rt["uniqid"]
+        p.thread_count = rt["thread_count"]
+        p.active_thread_count = rt["active"]
+        p.idle_top = -1 if rt["active"] == rt["thread_count"] else \
+            min(set(range(rt["thread_count"])) - set(rt["active_idx"]))
+        if rt["flow_tbl"]:
+            for i, v in enumerate(rt["flow_tbl"]):
+                p.flow_tbl[i] = v
+        for th in range(rt["thread_count"]):
+            ring = Ring(g, ring_size)
+            rings[(rt["uniqid"], th)] = ring
+            p.rxq[th] = ctypes.pointer(ring.chan)
+        procs[rt["uniqid"]] = p
+        keep.append(p)
+    return procs, rings, keep
+
+
+def test_host_deliver_matches_reference_model(g, orc):
+    """gcl_host_deliver vs a direct model of rx_send_pkt_to_runtime /
+    rx_send_to_runtime (rx.c:50-92) with sched_add_core activating a thread."""
+    from tests.rxcases import fuzz_batch, random_runtimes
+    rng = np.random.default_rng(11)
+    R = 64
+    rts = random_runtimes(rng, R, 24, max_threads=6)
+    n = 3000
+    frames, flen, offs, olf, rss, fdir = fuzz_batch(rng, n, rts, R, tail_runts=False)
+    t = orc.Tables(R, 0, 0, 0x09)
+    for r in rts:
+        assert t.runtime_set(r["uniqid"], r["ip"], r["thread_count"], r["active"], r["flow_tbl"]) == 0
+    v, _, _ = t.classify(frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir_hi=fdir, frames_len=flen)
+    pkt_len = rng.integers(60, 1515, size=n).astype(np.uint16)
+
+    ring_size = 16
+    procs, rings, keep = _host_procs(g, rts, ring_size)
+    by_id = (ctypes.c_void_p * R)()
+    for u, p in procs.items():
+        by_id[u] = ctypes.addressof(p)
+    clients = (ctypes.c_void_p * len(procs))(*[ctypes.addressof(p) for p in procs.values()])
+
+    woke = []
+
+    @g.SCHED_ADD_CORE_FN
+    def add_core(arg, pp):
+        p = pp.contents
+        if p.active_thread_count == 0:  # activate thread 0: sched_steer_flows
+            p.active_thread_count = 1
+            for i in range(p.thread_count):
+                p.flow_tbl[i] = 0
+            woke.append(p.uniqid)
+
+    freed = []
+
+    @g.FREE_PKT_FN
+    def free_pkt(arg, i):
+        freed.append(i)
+
+    ops = g.GclHostOps()
+    ops.sched_add_core = add_core
+    ops.free_pkt = free_pkt
+    stats = np.zeros(8, dtype=np.uint64)
+    shm = offs.astype(np.uint64)
+    delivered = g.lib.gcl_host_deliver(by_id, R, clients, len(procs), v.ctypes.data, pkt_len.ctypes.data,
+                                       olf.ctypes.data, 0x09, shm.ctypes.data, n, ctypes.byref(ops),
+                                       stats.ctypes.data)
+
+    # model
+    active = {r["uniqid"]: r["active"] for r in rts}
+    flow = {r["uniqid"]: list(r["flow_tbl"]) if r["flow_tbl"] else [0] * r["thread_count"] for r in rts}
+    tc = {r["uniqid"]: r["thread_count"] for r in rts}
+    fill = {k: 0 for k in rings}
+    expect_msgs = {k: [] for k in rings}
+    exp_fail = exp_unh = exp_deliv = 0
+    exp_freed = []
+    for i in range(n):
+        act = v[i]["action"] & 0x7F
+        if act in (0, 1):
+            u = int(v[i]["uniqid"])
+            if act == 0:
+                th = int(v[i]["thread"])
+            else:
+                if active[u] == 0:
+                    active[u] = 1
+                    flow[u] = [0] * tc[u]
+                th = flow[u][int(v[i]["hash"]) % tc[u]]
+            cmd = (int(pkt_len[i]) << 16) | (((int(olf[i]) & 0x0C) == 0x08) << 48)
+            if fill[(u, th)] < ring_size:
+                fill[(u, th)] += 1
+                expect_msgs[(u, th)].append((cmd, int(shm[i])))
+                exp_deliv += 1
+            else:
+                exp_fail += 1
+                exp_unh += 1
+                exp_freed.append(i)
+        else:
+            exp_freed.append(i)
+    assert delivered == exp_deliv
+    assert stats[1] == exp_fail and stats[4] == exp_unh
+    assert freed == exp_freed
+    for k, ring in rings.items():
+        assert ring.drain() == expect_msgs[k], k
+    assert len(woke) == len(set(woke))
+
+
+def test_host_deliver_broadcast_and_arp(g):
+    procs, rings, keep = _host_procs(g, [
+        {"uniqid": 1, "thread_count": 2, "active": 2, "active_idx": [0, 1], "flow_tbl": [0, 1]},
+        {"uniqid": 2, "thread_count": 1, "active": 0, "active_idx": [], "flow_tbl": None},
+    ], 4)
+    procs[2].idle_top = 0
+    by_id = (ctypes.c_void_p * 4)(None, ctypes.addressof(procs[1]), ctypes.addressof(procs[2]), None)
+    clients = (ctypes.c_void_p * 2)(ctypes.addressof(procs[1]), ctypes.addressof(procs[2]))
+    v = np.zeros(3, dtype=g.VERDICT_DTYPE)
+    v[0] = (5, 0xFFFF, 0xFF, g.ACT_BROADCAST)
+    v[1] = (0, 0xFFFF, 0xFF, g.ACT_ARP_RESPOND)
+    v[2] = (0, 0xFFFF, 0xFF, g.ACT_ARP_RESPOND)
+    calls = []
+
+    @g.ARP_RESPOND_FN
+    def arp(arg, i):
+        calls.append(i)
+        return i == 1
+
+    refc = []
+
+    @g.REFCNT_FN
+    def refcnt(arg, i, d):
+        refc.append((i, d))
+
+    ops = g.GclHostOps()
+    ops.arp_respond = arp
+    ops.refcnt_update = refcnt
+    stats = np.zeros(8, dtype=np.uint64)
+    n = g.lib.gcl_host_deliver(by_id, 4, clients, 2, v.ctypes.data, None, None, 0, None, 3,
+                               ctypes.byref(ops), stats.ctypes.data)
+    assert n == 1
+    # rx.c:171-190: one copy to every runtime (the idle one to its idle thread)
+    assert rings[(1, 5 % 2)].drain() == [(0, 0)]
+    assert rings[(2, 0)].drain() == [(0, 0)]
+    assert refc == [(0, 1)]
+    # rx.c:200-207: a failed ARP response counts as unregistered + unhandled
+    assert calls == [1, 2]
+    assert stats[0] == 1 and stats[4] == 1

@@ -248,3 +248,32 @@ def test_gpu_full_size_properties(g, orc):
     fr = frames.view(n, stride)[torch.from_numpy(sample).cuda()].cpu().numpy().reshape(-1)
     ve, _, _ = t.classify(fr, len(sample), stride)
     assert_same(vv[sample], ve, "sample")
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("wl,stride,R,T,arrays", [(0, 64, 16, 8, False), (1, 1536, 1024, 4, False),
+                                                   (2, 9216, 16, 8, True)])
+def test_gpu_end_to_end_host_buffers(g, orc, mode, wl, stride, R, T, arrays):
+    """gcl_classify_host: frames in pinned host memory, verdicts back in host
+    memory, through the DMA-gather (COPY) and PCIe zero-copy transports."""
+    n = 300000 if wl != 2 else 40000
+    cdf = orc.zipf_cdf(1 << 16) if wl == 1 else None
+    frames, olf, rss = orc.generate(wl, n, stride, R, cdf=cdf)
+    t = orc.Tables(R, 1, 0, 0x09)
+    clf = g.Classifier(0, R, 1)
+    for r in range(R):
+        fl = orc.steer_flows(T, list(range(r % T + 1)))
+        t.runtime_set(r, orc.runtime_ip(r), T, r % T + 1, fl)
+        clf.runtime_set(r, g.runtime_ip(r), T, r % T + 1, fl)
+    kw = dict(olflags=olf, rss=rss) if arrays else {}
+    ve, ce, se = t.classify(frames, n, stride, **kw)
+    hf = torch.from_numpy(frames).pin_memory()
+    hv = torch.zeros(n * 8, dtype=torch.uint8).pin_memory()
+    pk = {k: torch.from_numpy(a.view(np.uint8) if k == "olflags" else a.view(np.int32)).pin_memory()
+          for k, a in kw.items()}
+    counts = np.zeros(R, dtype=np.uint64)
+    stats = np.zeros(8, dtype=np.uint64)
+    clf.classify_host(hf, n, stride, verdicts=hv, counts=counts, stats=stats, mode=mode,
+                      chunk=65536 + 17, nstreams=3, **pk)
+    assert_same(hv.numpy().view(g.VERDICT_DTYPE), ve, f"e2e mode={mode}")
+    assert (counts == ce).all() and (stats == se).all()
