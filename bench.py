@@ -67,13 +67,29 @@ def setup_tables(clf, R, T, seed=SEED):
     return tables
 
 
+def zero_fill(buf):
+    """Zero a DeviceBuffer with hipMemset (slots are only partly generated)."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemset.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t]
+    assert hip.hipMemset(buf.data_ptr(), 0, buf.numel()) == 0
+    hip.hipDeviceSynchronize()
+
+
 class Workload:
     def __init__(self, name, rank, world, device, hash_mode=g.HASH_JENKINS):
         wl, n, stride, R, T, desc = WORKLOADS[name]
         self.name, self.wl, self.n, self.stride, self.R, self.T, self.desc = name, wl, n, stride, R, T, desc
-        self.frames = torch.zeros(n * stride, dtype=torch.uint8, device=device)
-        self.verdicts = torch.empty(n * 8, dtype=torch.uint8, device=device)
+        if os.environ.get("GCL_BENCH_TORCH_ALLOC") == "1":
+            self.frames = torch.zeros(n * stride, dtype=torch.uint8, device=device)
+            self.verdicts = torch.empty(n * 8, dtype=torch.uint8, device=device)
+        else:  # library-owned hipMalloc (gcl_dev_alloc), zeroed
+            self.frames = g.DeviceBuffer(n * stride, device.index or 0)
+            self.verdicts = g.DeviceBuffer(n * 8, device.index or 0)
+            torch.cuda.synchronize()
+            zero_fill(self.frames)
         self.counts = torch.zeros(R + g.NR_STATS, dtype=torch.int64, device=device)
+
         cdf_dev = None
         nflows = 0
         if wl == g.WL_TCP1500_ZIPF:

@@ -29,14 +29,13 @@
 
 namespace {
 
-constexpr int kThreads = 256;            /* packets per tile = lanes per block */
-constexpr int kTileBytes = kThreads * 64; /* LDS header tile */
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 constexpr uint32_t kToepBytes = 12 * 256 * 4;
 constexpr uint32_t kLdsTableBudget = 96 * 1024;
 
 /* tuning knobs for experiments (GCL_TUNE_BLOCKS_PER_CU caps the grid) */
 static int g_tune_bpc = 0;
+static int g_tune_grid = 0;
 
 struct RtEntry {            /* 16 B per uniqid */
 	uint32_t m_lo, m_hi;     /* fastmod magic for thread_count */
@@ -65,6 +64,7 @@ struct KParams {
 	uint32_t cflags;
 	uint32_t default_flags;
 	uint32_t nt_store;
+	uint32_t ablate; /* GCL_TUNE_ABLATE: timing-only experiments, wrong results */
 };
 
 /* ------------------------------------------------------------------------
@@ -90,13 +90,25 @@ __device__ __forceinline__ uint64_t frame_off(const KParams &k, uint64_t idx)
 	return idx * k.stride;
 }
 
-template <bool GENERAL>
+template <bool GENERAL, int NT>
 __device__ __forceinline__ void load_tile(const KParams &k, uint64_t tile, uint4 r[4])
 {
+	if (!GENERAL && (tile + 1) * NT <= k.n) {
+		/* full tile, every granule in range (checked on the host): no
+		 * per-lane predicate, four back-to-back 16-B loads per lane */
+		const uint8_t *base = k.frames + tile * NT * k.stride;
+#pragma unroll
+		for (int j = 0; j < 4; j++) {
+			int c = j * NT + (int)threadIdx.x;
+			r[j] = gcl::load16_nt(base + ((uint32_t)(c >> 2) * (uint32_t)k.stride +
+			                              (uint32_t)(c & 3) * 16));
+		}
+		return;
+	}
 #pragma unroll
 	for (int j = 0; j < 4; j++) {
-		int c = j * kThreads + (int)threadIdx.x;
-		uint64_t idx = tile * kThreads + (uint64_t)(c >> 2);
+		int c = j * NT + (int)threadIdx.x;
+		uint64_t idx = tile * NT + (uint64_t)(c >> 2);
 		uint4 v = make_uint4(0, 0, 0, 0);
 		if (idx < k.n) {
 			uint64_t a = frame_off<GENERAL>(k, idx) + (uint64_t)(c & 3) * 16;
@@ -135,142 +147,137 @@ struct Tables {
 
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
-/* rx_one_pkt for the packet staged in row `tid` of the tile (rx.c:116-233) */
+/* Toeplitz over the 12-byte tuple with the per-byte LUT (12 x 256 words) */
+__device__ __forceinline__ uint32_t toeplitz_lut(const uint32_t *toep, uint32_t saddr,
+                                                 uint32_t daddr, uint32_t sport, uint32_t dport)
+{
+	return toep[0 * 256 + (saddr >> 24)] ^ toep[1 * 256 + ((saddr >> 16) & 0xFF)] ^
+	       toep[2 * 256 + ((saddr >> 8) & 0xFF)] ^ toep[3 * 256 + (saddr & 0xFF)] ^
+	       toep[4 * 256 + (daddr >> 24)] ^ toep[5 * 256 + ((daddr >> 16) & 0xFF)] ^
+	       toep[6 * 256 + ((daddr >> 8) & 0xFF)] ^ toep[7 * 256 + (daddr & 0xFF)] ^
+	       toep[8 * 256 + (sport >> 8)] ^ toep[9 * 256 + (sport & 0xFF)] ^
+	       toep[10 * 256 + (dport >> 8)] ^ toep[11 * 256 + (dport & 0xFF)];
+}
+
+/*
+ * rx_one_pkt for the packet staged in row `tid` of the tile (rx.c:116-233).
+ * Written as straight-line selects: every lane runs the same instruction
+ * stream (hash, probe, steer), and only the rare cases -- IHL != 5 ports, a
+ * probe chain longer than one slot -- take a divergent branch.
+ */
 template <int MODE, bool GENERAL>
 __device__ __forceinline__ void classify_one(const KParams &k, const uint4 *tile, int tid,
                                              uint64_t idx, const Tables &tb, uint32_t *hist,
                                              Counters &cnt)
 {
-	const uint2 *ipt = tb.ipt;
-	const RtEntry *rtab = tb.rtab;
-	const uint8_t *flow = tb.flow;
-	const uint32_t *toep = tb.toep;
-		const uint4 w0 = tile[tile_slot(tid, 0)];
-		const uint4 w1 = tile[tile_slot(tid, 1)];
-		const uint4 w2 = tile[tile_slot(tid, 2)];
-		const uint32_t d3 = w0.w, d5 = w1.y, d6 = w1.z, d7 = w1.w;
-		const uint32_t d8 = w2.x, d9 = w2.y, d10 = w2.z;
+	const uint4 w0 = tile[tile_slot(tid, 0)];
+	const uint4 w1 = tile[tile_slot(tid, 1)];
+	const uint4 w2 = tile[tile_slot(tid, 2)];
+	const uint32_t d3 = w0.w, d5 = w1.y, d6 = w1.z, d7 = w1.w;
+	const uint32_t d8 = w2.x, d9 = w2.y, d10 = w2.z;
 
-		const uint32_t et = gcl::bswap16(d3 & 0xFFFF);       /* rx.c:154 */
-		const uint32_t vihl = (d3 >> 16) & 0xFF;
-		const uint32_t frag = gcl::bswap16(d5 & 0xFFFF);     /* also ARP op */
-		const uint32_t proto = d5 >> 24;
-		const uint32_t saddr = gcl::bswap32(gcl::mid32(d6, d7));
-		const uint32_t daddr = gcl::bswap32(gcl::mid32(d7, d8));   /* rx.c:159 */
-		const uint32_t arp_tip = gcl::bswap32(gcl::mid32(d9, d10)); /* rx.c:167 */
-		const uint32_t flags = (GENERAL && k.olflags) ? k.olflags[idx] : k.default_flags;
+	const uint32_t et = gcl::bswap16(d3 & 0xFFFF);              /* rx.c:154 */
+	const uint32_t ihl = (d3 >> 16) & 0xF;
+	const uint32_t frag = gcl::bswap16(d5 & 0xFFFF);            /* ARP: opcode */
+	const uint32_t proto = d5 >> 24;
+	const uint32_t saddr = gcl::bswap32(gcl::mid32(d6, d7));
+	const uint32_t daddr = gcl::bswap32(gcl::mid32(d7, d8));     /* rx.c:157-159 */
+	const uint32_t arp_tip = gcl::bswap32(gcl::mid32(d9, d10));  /* rx.c:165-167 */
+	const uint32_t flags = (GENERAL && k.olflags) ? k.olflags[idx] : k.default_flags;
+	const bool is_ip = et == GCL_ETHTYPE_IP, is_arp = et == GCL_ETHTYPE_ARP;
+	const bool azure = k.cflags & GCL_CFG_AZURE_ARP;
 
-		/* steering hash */
-		uint32_t hash = 0;
-		if (MODE == GCL_HASH_NIC) {
-			if (k.rss)
-				hash = k.rss[idx];
+	/* steering hash (gclassify.h: NIC / JENKINS / TOEPLITZ) */
+	uint32_t hash = 0;
+	if (k.ablate & 1) {
+		hash = daddr;
+	} else if (MODE == GCL_HASH_NIC) {
+		if (k.rss)
+			hash = k.rss[idx];
+	} else {
+		const bool hashable = is_ip && ihl >= 5 && (frag & 0x3FFF) == 0 &&
+		                      (proto == 6 || proto == 17);
+		uint32_t sport = gcl::bswap16(d8 >> 16), dport = gcl::bswap16(d9 & 0xFFFF);
+		if (hashable && ihl != 5) {
+			if (ihl <= 11) {
+				const int o = 14 + 4 * (int)ihl;
+				sport = gcl::bswap16(tile_dword(tile, tid, o - 2) >> 16);
+				dport = gcl::bswap16(tile_dword(tile, tid, o + 2) & 0xFFFF);
+			} else { /* past the staged granule */
+				const uint64_t a = frame_off<GENERAL>(k, idx) + 14 + 4 * ihl;
+				sport = (uint32_t)frame_byte(k, a) << 8 | frame_byte(k, a + 1);
+				dport = (uint32_t)frame_byte(k, a + 2) << 8 | frame_byte(k, a + 3);
+			}
+		}
+		const uint32_t h = MODE == GCL_HASH_JENKINS
+		                       ? gcl::jhash_5tuple(saddr, daddr, sport, dport, proto)
+		                       : toeplitz_lut(tb.toep, saddr, daddr, sport, dport);
+		hash = hashable ? h : 0;
+	}
+	if (k.cflags & GCL_CFG_HASH16)
+		hash &= 0xFFFF;
+
+	/* hardware flow tag, rx.c:131-146 */
+	int p = -1;
+	uint32_t action = GCL_ACT_DELIVER;
+	if (GENERAL && (flags & GCL_F_FDIR_ID)) {
+		const uint32_t mark = k.fdir ? k.fdir[idx] : 0;
+		cnt.flowtag++;
+		if (mark < k.max_rt && tb.rtab[mark].tc != 0) {
+			p = (int)mark;
+			action = GCL_ACT_F_FDIR;
+		}
+	}
+	/* Ethertype dispatch, rx.c:154-194 */
+	const bool parse = p < 0;
+	const bool broadcast = parse && is_arp && azure && frag == GCL_ARP_OP_REPLY;
+	const bool lookup = parse && (is_ip || is_arp) && !broadcast;
+	cnt.hashmiss += parse && is_ip && !(flags & GCL_F_RSS_HASH); /* rx.c:160-163 */
+	const uint32_t dst = is_ip ? daddr : arp_tip;
+
+	/* ip_to_proc: open addressing keyed by rte_jhash(&ip, 4, 0), rx.c:197 */
+	if (k.ablate & 2) {
+		if (lookup)
+			p = (int)(dst & 15);
+	} else {
+		uint32_t s = gcl::jhash_u32(dst) & k.ipt_mask;
+		uint2 e = tb.ipt[s];
+		bool more = lookup && e.y != kEmpty && e.x != dst;
+		while (__builtin_expect(more, 0)) { /* collision chain: rare */
+			s = (s + 1) & k.ipt_mask;
+			e = tb.ipt[s];
+			more = e.y != kEmpty && e.x != dst;
+		}
+		if (lookup && e.y != kEmpty && e.x == dst)
+			p = (int)e.y;
+	}
+	const bool miss = lookup && p < 0;
+	const bool arp_respond = miss && azure && is_arp && frag == GCL_ARP_OP_REQUEST;
+	const bool unreg = miss && !arp_respond;                    /* rx.c:205 */
+	const bool bad_et = parse && !is_ip && !is_arp;              /* rx.c:191-194 */
+	cnt.unreg += unreg;
+	cnt.unhandled += unreg || bad_et;                            /* rx.c:232 */
+	action = bad_et ? GCL_ACT_DROP_ETHERTYPE
+	       : broadcast ? GCL_ACT_BROADCAST
+	       : arp_respond ? GCL_ACT_ARP_RESPOND
+	       : unreg ? GCL_ACT_DROP_UNREG : action;
+
+	/* rx_send_to_runtime, rx.c:55-72: flow_tbl[hash % thread_count] */
+	uint32_t uniq = GCL_NO_RUNTIME, thr = GCL_NO_THREAD;
+	if (p >= 0) {
+		const RtEntry re = tb.rtab[p];
+		uniq = (uint32_t)p;
+		if (k.ablate & 8) {
+			thr = hash & 7;
+		} else if (re.active) {
+			const uint64_t M = (uint64_t)re.m_hi << 32 | re.m_lo;
+			thr = tb.flow[re.flow_off + gcl::fastmod(hash, M, re.tc)];
 		} else {
-			const uint32_t ihl = vihl & 0xF;
-			const bool hashable = et == GCL_ETHTYPE_IP && ihl >= 5 &&
-			                      (frag & 0x3FFF) == 0 && (proto == 6 || proto == 17);
-			if (hashable) {
-				uint32_t sport, dport;
-				if (ihl == 5) {
-					sport = gcl::bswap16(d8 >> 16);
-					dport = gcl::bswap16(d9 & 0xFFFF);
-				} else if (ihl <= 11) {
-					int o = 14 + 4 * (int)ihl;
-					sport = gcl::bswap16(tile_dword(tile, tid, o - 2) >> 16);
-					dport = gcl::bswap16(tile_dword(tile, tid, o + 2) & 0xFFFF);
-				} else {
-					uint64_t a = frame_off<GENERAL>(k, idx) + 14 + 4 * ihl;
-					sport = (uint32_t)frame_byte(k, a) << 8 | frame_byte(k, a + 1);
-					dport = (uint32_t)frame_byte(k, a + 2) << 8 | frame_byte(k, a + 3);
-				}
-				if (MODE == GCL_HASH_JENKINS) {
-					hash = gcl::jhash_5tuple(saddr, daddr, sport, dport, proto);
-				} else {
-					hash = toep[0 * 256 + (saddr >> 24)] ^
-					       toep[1 * 256 + ((saddr >> 16) & 0xFF)] ^
-					       toep[2 * 256 + ((saddr >> 8) & 0xFF)] ^
-					       toep[3 * 256 + (saddr & 0xFF)] ^
-					       toep[4 * 256 + (daddr >> 24)] ^
-					       toep[5 * 256 + ((daddr >> 16) & 0xFF)] ^
-					       toep[6 * 256 + ((daddr >> 8) & 0xFF)] ^
-					       toep[7 * 256 + (daddr & 0xFF)] ^
-					       toep[8 * 256 + (sport >> 8)] ^
-					       toep[9 * 256 + (sport & 0xFF)] ^
-					       toep[10 * 256 + (dport >> 8)] ^
-					       toep[11 * 256 + (dport & 0xFF)];
-				}
-			}
+			action |= GCL_ACT_WAKE;
 		}
-		if (k.cflags & GCL_CFG_HASH16)
-			hash &= 0xFFFF;
-
-		int p = -1;
-		uint32_t action = GCL_ACT_DELIVER;
-		/* hardware flow tag, rx.c:131-146 */
-		if (GENERAL && (flags & GCL_F_FDIR_ID)) {
-			uint32_t mark = k.fdir ? k.fdir[idx] : 0;
-			cnt.flowtag++;
-			if (mark < k.max_rt && rtab[mark].tc != 0) {
-				p = (int)mark;
-				action = GCL_ACT_F_FDIR;
-			}
-		}
-		if (p < 0) {
-			uint32_t dst = 0;
-			bool lookup = true;
-			if (et == GCL_ETHTYPE_IP) {
-				dst = daddr;
-				cnt.hashmiss += !(flags & GCL_F_RSS_HASH); /* rx.c:160-163 */
-			} else if (et == GCL_ETHTYPE_ARP) {
-				dst = arp_tip;
-				if ((k.cflags & GCL_CFG_AZURE_ARP) && frag == GCL_ARP_OP_REPLY) {
-					action = GCL_ACT_BROADCAST; /* rx.c:171-190 */
-					lookup = false;
-				}
-			} else {
-				action = GCL_ACT_DROP_ETHERTYPE; /* rx.c:191-194 */
-				cnt.unhandled++;
-				lookup = false;
-			}
-			if (lookup) {
-				/* ip_to_proc: open addressing keyed by rte_jhash(&ip, 4, 0) */
-				uint32_t s = gcl::jhash_u32(dst) & k.ipt_mask;
-				for (;;) {
-					uint2 e = ipt[s];
-					if (e.y == kEmpty)
-						break;
-					if (e.x == dst) {
-						p = (int)e.y;
-						break;
-					}
-					s = (s + 1) & k.ipt_mask;
-				}
-				if (p < 0) {
-					if ((k.cflags & GCL_CFG_AZURE_ARP) && et == GCL_ETHTYPE_ARP &&
-					    frag == GCL_ARP_OP_REQUEST) {
-						action = GCL_ACT_ARP_RESPOND; /* rx.c:200-203 */
-					} else {
-						action = GCL_ACT_DROP_UNREG; /* rx.c:205, :232 */
-						cnt.unreg++;
-						cnt.unhandled++;
-					}
-				}
-			}
-		}
-
-		uint32_t uniq = GCL_NO_RUNTIME, thr = GCL_NO_THREAD;
-		if (p >= 0) {
-			/* rx_send_to_runtime, rx.c:55-72 */
-			const RtEntry re = rtab[p];
-			uniq = (uint32_t)p;
-			if (re.active) {
-				uint64_t M = (uint64_t)re.m_hi << 32 | re.m_lo;
-				thr = flow[re.flow_off + gcl::fastmod(hash, M, re.tc)];
-			} else {
-				action |= GCL_ACT_WAKE;
-			}
+		if (!(k.ablate & 4))
 			atomicAdd(&hist[p], 1u);
-		}
+	}
 	const u32x2 vd = {hash, uniq | thr << 16 | action << 24};
 	if (k.nt_store)
 		__builtin_nontemporal_store(vd, (u32x2 *)&k.verdicts[idx]);
@@ -278,12 +285,12 @@ __device__ __forceinline__ void classify_one(const KParams &k, const uint4 *tile
 		*(u32x2 *)&k.verdicts[idx] = vd;
 }
 
-template <bool GENERAL>
+template <int NT>
 __device__ __forceinline__ void stage_tile(uint4 *tile, const uint4 r[4])
 {
 #pragma unroll
 	for (int j = 0; j < 4; j++) {
-		int c = j * kThreads + (int)threadIdx.x;
+		int c = j * NT + (int)threadIdx.x;
 		tile[tile_slot(c >> 2, c & 3)] = r[j];
 	}
 }
@@ -292,24 +299,24 @@ __device__ __forceinline__ void stage_tile(uint4 *tile, const uint4 r[4])
  * Persistent grid: block b handles tiles b, b + G, b + 2G, ...; the frames of
  * the next DEPTH tiles are in flight in registers while a tile is parsed.
  */
-template <int MODE, bool TLDS, bool GENERAL, int DEPTH>
-__global__ void __launch_bounds__(kThreads)
+template <int MODE, bool TLDS, bool GENERAL, int DEPTH, int NT>
+__global__ void __launch_bounds__(NT)
 classify_kernel(KParams k)
 {
 	extern __shared__ uint4 smem[];
 	uint4 *tile = smem;
-	uint32_t *hist = (uint32_t *)(smem + kTileBytes / 16);
+	uint32_t *hist = (uint32_t *)(smem + NT * 4);
 	uint8_t *lds_tab = (uint8_t *)(hist + ((k.max_rt + 3) & ~3u));
 	const int tid = threadIdx.x;
 
 	/* stage tables and zero the histogram */
-	for (uint32_t i = tid; i < k.max_rt; i += kThreads)
+	for (uint32_t i = tid; i < k.max_rt; i += NT)
 		hist[i] = 0;
 	const uint8_t *tab = k.tables;
-	if (TLDS) {
+	if (TLDS && !(k.ablate & 32)) {
 		const uint4 *src = (const uint4 *)k.tables;
 		uint4 *dst = (uint4 *)lds_tab;
-		for (uint32_t i = tid; i < k.tables_lds_bytes / 16; i += kThreads)
+		for (uint32_t i = tid; i < k.tables_lds_bytes / 16; i += NT)
 			dst[i] = src[i];
 		tab = lds_tab;
 	}
@@ -325,28 +332,31 @@ classify_kernel(KParams k)
 	uint4 ra[4], rb[4];
 	uint64_t t = blockIdx.x;
 	if (t < k.ntiles)
-		load_tile<GENERAL>(k, t, ra);
+		load_tile<GENERAL, NT>(k, t, ra);
 	if (DEPTH == 2 && t + G < k.ntiles)
-		load_tile<GENERAL>(k, t + G, rb);
+		load_tile<GENERAL, NT>(k, t + G, rb);
 
 	while (t < k.ntiles) {
-		stage_tile<GENERAL>(tile, ra);
+		stage_tile<NT>(tile, ra);
 		__syncthreads();
 		if (t + DEPTH * G < k.ntiles)
-			load_tile<GENERAL>(k, t + DEPTH * G, ra); /* in flight while parsing */
-		if (t * kThreads + tid < k.n)
-			classify_one<MODE, GENERAL>(k, tile, tid, t * kThreads + tid, tb, hist, cnt);
+			load_tile<GENERAL, NT>(k, t + DEPTH * G, ra); /* in flight while parsing */
+		if (k.ablate & 16) { /* timing only: the membench tile_v0 body */
+			const uint4 a = tile[tile_slot(tid, 0)], b = tile[tile_slot(tid, 1)];
+			*(u32x2 *)&k.verdicts[t * NT + tid] = u32x2{b.z ^ a.x, a.w ^ b.y};
+		} else if (t * NT + tid < k.n)
+			classify_one<MODE, GENERAL>(k, tile, tid, t * NT + tid, tb, hist, cnt);
 		__syncthreads();
 		t += G;
 		if (DEPTH == 2) {
 			if (t >= k.ntiles)
 				break;
-			stage_tile<GENERAL>(tile, rb);
+			stage_tile<NT>(tile, rb);
 			__syncthreads();
 			if (t + 2 * G < k.ntiles)
-				load_tile<GENERAL>(k, t + 2 * G, rb);
-			if (t * kThreads + tid < k.n)
-				classify_one<MODE, GENERAL>(k, tile, tid, t * kThreads + tid, tb, hist, cnt);
+				load_tile<GENERAL, NT>(k, t + 2 * G, rb);
+			if (t * NT + tid < k.n)
+				classify_one<MODE, GENERAL>(k, tile, tid, t * NT + tid, tb, hist, cnt);
 			__syncthreads();
 			t += G;
 		}
@@ -355,7 +365,9 @@ classify_kernel(KParams k)
 	uint32_t n_unreg = cnt.unreg, n_unhandled = cnt.unhandled;
 
 	/* flush per-block counters */
-	for (uint32_t i = tid; i < k.max_rt; i += kThreads) {
+	if (k.ablate & 64)
+		return;
+	for (uint32_t i = tid; i < k.max_rt; i += NT) {
 		uint32_t v = hist[i];
 		if (v && k.counts)
 			atomicAdd(&k.counts[i], (unsigned long long)v);
@@ -567,7 +579,9 @@ struct gcl_ctx {
 	uint64_t prof_launches;
 	int tune_tables; /* GCL_TUNE_TABLES: 0 auto, 1 global, 2 lds-if-fits */
 	int tune_depth;  /* GCL_TUNE_DEPTH: tiles in flight per block (1 or 2) */
+	int tune_threads; /* GCL_TUNE_THREADS: 256, 512 or 1024 lanes per block */
 	int tune_nt_store; /* GCL_TUNE_NT_STORE: non-temporal verdict stores */
+	int tune_ablate;   /* GCL_TUNE_ABLATE bitmask (timing experiments only) */
 };
 
 extern "C" {
@@ -618,9 +632,17 @@ extern "C" int gcl_open(int hip_device, const struct gcl_cfg *cfg, struct gcl_ct
 		const char *e = getenv("GCL_TUNE_TABLES");
 		c->tune_tables = e ? atoi(e) : 0;
 		e = getenv("GCL_TUNE_DEPTH");
-		c->tune_depth = e ? atoi(e) : 1;
+		c->tune_depth = e ? atoi(e) : 0;
+		e = getenv("GCL_TUNE_THREADS");
+		c->tune_threads = e ? atoi(e) : 0;
+		if (c->tune_threads != 512 && c->tune_threads != 1024)
+			c->tune_threads = 0;
 		e = getenv("GCL_TUNE_NT_STORE");
 		c->tune_nt_store = e ? atoi(e) : 0;
+		e = getenv("GCL_TUNE_ABLATE");
+		c->tune_ablate = e ? atoi(e) : 0;
+		e = getenv("GCL_TUNE_GRID");
+		g_tune_grid = e ? atoi(e) : 0;
 		e = getenv("GCL_TUNE_BLOCKS_PER_CU");
 		g_tune_bpc = e ? atoi(e) : 0;
 	}
@@ -779,8 +801,8 @@ static hipEvent_t prof_event(gcl_ctx *c)
 	return e;
 }
 
-template <int MODE, bool TLDS, bool GENERAL, int DEPTH>
-static hipError_t launch_t(const KParams &k, uint32_t lds, int num_cus, hipStream_t s)
+template <int MODE, bool TLDS, bool GENERAL, int DEPTH, int NT>
+static hipError_t launch_t(KParams k, uint32_t lds, int num_cus, int bpc_cap, hipStream_t s)
 {
 	static std::mutex mu;
 	static int occ_cache[64];
@@ -790,7 +812,7 @@ static hipError_t launch_t(const KParams &k, uint32_t lds, int num_cus, hipStrea
 	if (lds > 64 * 1024) {
 		static bool raised = false;
 		if (!raised) {
-			hipFuncSetAttribute((const void *)classify_kernel<MODE, TLDS, GENERAL, DEPTH>,
+			hipFuncSetAttribute((const void *)classify_kernel<MODE, TLDS, GENERAL, DEPTH, NT>,
 			                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 			raised = true;
 		}
@@ -800,7 +822,7 @@ static hipError_t launch_t(const KParams &k, uint32_t lds, int num_cus, hipStrea
 		if (occ_lds[slot] != lds + 1) {
 			int o = 0;
 			if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-			        &o, classify_kernel<MODE, TLDS, GENERAL, DEPTH>, kThreads, lds) != hipSuccess ||
+			        &o, classify_kernel<MODE, TLDS, GENERAL, DEPTH, NT>, NT, lds) != hipSuccess ||
 			    o < 1)
 				o = 1;
 			occ_cache[slot] = o;
@@ -808,36 +830,94 @@ static hipError_t launch_t(const KParams &k, uint32_t lds, int num_cus, hipStrea
 		}
 		occ = occ_cache[slot];
 	}
+	if (bpc_cap > 0 && bpc_cap < occ)
+		occ = bpc_cap;
 	if (g_tune_bpc > 0 && g_tune_bpc < occ)
 		occ = g_tune_bpc;
+	k.ntiles = (k.n + NT - 1) / NT;
 	uint64_t grid = (uint64_t)num_cus * (uint64_t)occ;
+	if (g_tune_grid > 0)
+		grid = (uint64_t)g_tune_grid;
 	if (grid > k.ntiles)
 		grid = k.ntiles;
 	if (grid < 1)
 		grid = 1;
-	hipLaunchKernelGGL((classify_kernel<MODE, TLDS, GENERAL, DEPTH>), dim3((unsigned)grid),
-	                   dim3(kThreads), lds, s, k);
+	hipLaunchKernelGGL((classify_kernel<MODE, TLDS, GENERAL, DEPTH, NT>), dim3((unsigned)grid),
+	                   dim3(NT), lds, s, k);
 	return hipGetLastError();
 }
 
-template <int MODE, int DEPTH>
-static hipError_t launch_depth(const KParams &k, bool tlds, bool general, uint32_t lds,
-                               int num_cus, hipStream_t s)
+template <int MODE, int DEPTH, int NT>
+static hipError_t launch_nt(const KParams &k, bool tlds, bool general, uint32_t lds,
+                            int num_cus, int bpc_cap, hipStream_t s)
 {
 	if (tlds)
-		return general ? launch_t<MODE, true, true, DEPTH>(k, lds, num_cus, s)
-		               : launch_t<MODE, true, false, DEPTH>(k, lds, num_cus, s);
-	return general ? launch_t<MODE, false, true, DEPTH>(k, lds, num_cus, s)
-	               : launch_t<MODE, false, false, DEPTH>(k, lds, num_cus, s);
+		return general ? launch_t<MODE, true, true, DEPTH, NT>(k, lds, num_cus, bpc_cap, s)
+		               : launch_t<MODE, true, false, DEPTH, NT>(k, lds, num_cus, bpc_cap, s);
+	return general ? launch_t<MODE, false, true, DEPTH, NT>(k, lds, num_cus, bpc_cap, s)
+	               : launch_t<MODE, false, false, DEPTH, NT>(k, lds, num_cus, bpc_cap, s);
 }
 
+/* Launch geometry (measured on MI355X, tools/cbench.cpp): */
+struct Geometry {
+	int threads;  /* packets per tile = lanes per block */
+	int depth;    /* tiles in flight per block */
+	int bpc_cap;  /* blocks per CU */
+};
+
 template <int MODE>
-static hipError_t launch_mode(const KParams &k, bool tlds, bool general, int depth,
-                              uint32_t lds, int num_cus, hipStream_t s)
+static hipError_t launch_mode(const KParams &k, bool tlds, bool general, const Geometry &geo,
+                              uint32_t tab_lds, uint32_t hist_bytes, int num_cus, hipStream_t s)
 {
-	if (depth == 2)
-		return launch_depth<MODE, 2>(k, tlds, general, lds, num_cus, s);
-	return launch_depth<MODE, 1>(k, tlds, general, lds, num_cus, s);
+	const uint32_t lds = (uint32_t)geo.threads * 64 + hist_bytes + tab_lds;
+#define GCL_LAUNCH(D, T) \
+	return launch_nt<MODE, D, T>(k, tlds, general, lds, num_cus, geo.bpc_cap, s)
+	if (geo.depth == 2) {
+		if (geo.threads == 1024) GCL_LAUNCH(2, 1024);
+		if (geo.threads == 512) GCL_LAUNCH(2, 512);
+		GCL_LAUNCH(2, 256);
+	}
+	if (geo.threads == 1024) GCL_LAUNCH(1, 1024);
+	if (geo.threads == 512) GCL_LAUNCH(1, 512);
+	GCL_LAUNCH(1, 256);
+#undef GCL_LAUNCH
+}
+
+/*
+ * Launch geometry.  Measured on MI355X with tools/cbench.cpp (interleaved, in
+ * one process, against a compute-free kernel of the same traffic): the
+ * classifier is fastest with about 1024 resident lanes per CU -- 256-lane
+ * blocks x 4 when the tables are small, and for the 1024-runtime tables
+ * (37 KiB of LDS per block) 512-lane blocks x 2, so that one LDS copy of the
+ * tables serves twice the packets (tcp1500: 234 -> 206 us).  More resident
+ * waves than that only add contention (udp64: 446 us at 8 x 256).
+ */
+static Geometry choose_geometry(const gcl_ctx *c, uint32_t tab_lds, uint32_t hist_bytes)
+{
+	const uint32_t lds_cu = 160 * 1024, lanes_cu = 1024;
+	Geometry g;
+	g.depth = 1;
+	g.threads = 0;
+	for (int nt = 256; nt <= 1024 && !g.threads; nt *= 2) {
+		uint32_t per_block = (uint32_t)nt * 64 + hist_bytes + tab_lds;
+		if ((lanes_cu / nt) * per_block <= lds_cu) {
+			g.threads = nt;
+			g.bpc_cap = (int)(lanes_cu / (uint32_t)nt);
+		}
+	}
+	if (!g.threads) { /* big tables: as many 256-lane blocks as LDS admits */
+		g.threads = 256;
+		g.bpc_cap = (int)(lds_cu / (256u * 64 + hist_bytes + tab_lds));
+		if (g.bpc_cap < 1)
+			g.bpc_cap = 1;
+	}
+	if (c->tune_threads)
+		g.threads = c->tune_threads;
+	if (c->tune_depth)
+		g.depth = c->tune_depth;
+	if (g_tune_bpc)
+		g.bpc_cap = g_tune_bpc;
+	return g;
 }
 
 /* Upload a new table snapshot on @s if anything changed; launches on any
@@ -868,7 +948,7 @@ extern "C" int gcl_classify(struct gcl_ctx *c, const struct gcl_batch *b,
 	hipStream_t s = (hipStream_t)hip_stream;
 	if (b->n == 0)
 		return 0;
-	if (!b->frames || (!b->offs && (b->stride < 16 || (b->stride & 15))))
+	if (!b->frames || (!b->offs && (b->stride < 16 || (b->stride & 15) || b->stride > (1u << 20))))
 		return -EINVAL;
 	if (!verdicts)
 		return -EINVAL;
@@ -887,7 +967,6 @@ extern "C" int gcl_classify(struct gcl_ctx *c, const struct gcl_batch *b,
 	k.rss = b->rss;
 	k.fdir = b->fdir_hi;
 	k.n = b->n;
-	k.ntiles = (b->n + kThreads - 1) / kThreads;
 	k.verdicts = (uint2 *)verdicts;
 	k.counts = (unsigned long long *)runtime_counts;
 	k.stats = (unsigned long long *)stats;
@@ -900,6 +979,7 @@ extern "C" int gcl_classify(struct gcl_ctx *c, const struct gcl_batch *b,
 	k.cflags = c->cfg.flags;
 	k.default_flags = c->cfg.default_olflags;
 	k.nt_store = c->tune_nt_store;
+	k.ablate = c->tune_ablate;
 
 	/* the specialised fast path needs every header granule in range */
 	bool general = b->offs || b->olflags || b->fdir_hi ||
@@ -915,7 +995,7 @@ extern "C" int gcl_classify(struct gcl_ctx *c, const struct gcl_batch *b,
 	else if (c->tune_tables == 2)
 		tlds = tab_bytes <= kLdsTableBudget;
 	k.tables_lds_bytes = tlds ? tab_bytes : 0;
-	uint32_t lds = kTileBytes + hist_bytes + (tlds ? tab_bytes : 0);
+	Geometry geo = choose_geometry(c, tlds ? tab_bytes : 0, hist_bytes);
 
 	hipEvent_t e0 = nullptr, e1 = nullptr;
 	if (c->cfg.flags & GCL_CFG_PROFILE) {
@@ -926,13 +1006,16 @@ extern "C" int gcl_classify(struct gcl_ctx *c, const struct gcl_batch *b,
 	hipError_t err;
 	switch (c->cfg.hash_mode) {
 	case GCL_HASH_NIC:
-		err = launch_mode<GCL_HASH_NIC>(k, tlds, general, c->tune_depth, lds, c->num_cus, s);
+		err = launch_mode<GCL_HASH_NIC>(k, tlds, general, geo, tlds ? tab_bytes : 0, hist_bytes,
+		                                c->num_cus, s);
 		break;
 	case GCL_HASH_JENKINS:
-		err = launch_mode<GCL_HASH_JENKINS>(k, tlds, general, c->tune_depth, lds, c->num_cus, s);
+		err = launch_mode<GCL_HASH_JENKINS>(k, tlds, general, geo, tlds ? tab_bytes : 0,
+		                                    hist_bytes, c->num_cus, s);
 		break;
 	default:
-		err = launch_mode<GCL_HASH_TOEPLITZ>(k, tlds, general, c->tune_depth, lds, c->num_cus, s);
+		err = launch_mode<GCL_HASH_TOEPLITZ>(k, tlds, general, geo, tlds ? tab_bytes : 0,
+		                                     hist_bytes, c->num_cus, s);
 		break;
 	}
 	if (e0) {
@@ -1009,6 +1092,22 @@ extern "C" int gcl_generate(const struct gcl_gen_params *p, uint8_t *frames, uin
 }
 
 extern "C" const char *gcl_version(void) { return GCL_VERSION; }
+
+/* Device memory for frame slabs and verdict arrays: plain hipMalloc on the
+ * context's device, so large batches get the allocator's large-page path. */
+extern "C" int gcl_dev_alloc(int hip_device, size_t bytes, void **out)
+{
+	if (!out || !bytes)
+		return -EINVAL;
+	if (hipSetDevice(hip_device) != hipSuccess)
+		return -ENODEV;
+	return hipMalloc(out, bytes) == hipSuccess ? 0 : -ENOMEM;
+}
+
+extern "C" int gcl_dev_free(void *p)
+{
+	return hipFree(p) == hipSuccess ? 0 : -EINVAL;
+}
 
 /* ==========================================================================
  * End-to-end: frames in host memory (the NIC's mbufs), verdicts back to host.

@@ -148,6 +148,8 @@ def _load():
         "gcl_rx_make_cmd": (u64, [u16, ctypes.c_uint8]),
         "gcl_classify_host": (i32, [vp, ctypes.POINTER(GclBatch), vp, vp, vp, ctypes.POINTER(GclE2eOpts)]),
         "gcl_host_register": (i32, [vp, ctypes.c_size_t]),
+        "gcl_dev_alloc": (i32, [i32, ctypes.c_size_t, ctypes.POINTER(vp)]),
+        "gcl_dev_free": (i32, [vp]),
         "gcl_host_unregister": (i32, [vp]),
         "gcl_host_deliver": (u64, [vp, u32, vp, i32, vp, vp, vp, ctypes.c_uint8, vp, u64,
                                    ctypes.POINTER(GclHostOps), vp]),
@@ -182,6 +184,8 @@ def _ptr(x):
 def _nbytes(x):
     if hasattr(x, "numel"):
         return x.numel() * x.element_size()
+    if isinstance(x, int):  # raw device address: caller vouches for the size
+        return 1 << 62
     return x.nbytes
 
 
@@ -204,6 +208,37 @@ def steer_flows(thread_count, active_idx):
     out = (ctypes.c_uint16 * thread_count)(*([0] * thread_count))
     _check(lib.gcl_steer_flows(thread_count, act, n, out), "gcl_steer_flows")
     return list(out)
+
+
+class DeviceBuffer:
+    """hipMalloc'd device memory owned by the library (gcl_dev_alloc): a raw
+    address with the duck-typed interface the binding accepts (data_ptr,
+    numel, element_size)."""
+
+    def __init__(self, nbytes, device=0):
+        p = ctypes.c_void_p()
+        _check(lib.gcl_dev_alloc(device, nbytes, ctypes.byref(p)), "gcl_dev_alloc")
+        self.ptr, self.nbytes = p.value, nbytes
+
+    def data_ptr(self):
+        return self.ptr
+
+    def numel(self):
+        return self.nbytes
+
+    def element_size(self):
+        return 1
+
+    def free(self):
+        if self.ptr:
+            lib.gcl_dev_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
 
 
 def zipf_cdf(nflows, s=0.99):

@@ -289,6 +289,10 @@ uint32_t gcl_jenkins_hash(const void *key, size_t len);
 uint32_t gcl_toeplitz(const uint8_t *key, size_t keylen, const uint8_t *input,
                       size_t len);
 
+/* Device memory for batches (hipMalloc on @hip_device): 0, -ENODEV, -ENOMEM. */
+int gcl_dev_alloc(int hip_device, size_t bytes, void **out);
+int gcl_dev_free(void *p);
+
 /* Library version string. */
 const char *gcl_version(void);
 

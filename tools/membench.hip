@@ -71,6 +71,97 @@ __global__ void __launch_bounds__(256) rw_kernel(const unsigned char *buf, unsig
 	}
 }
 
+// variants of the classify traffic shape (udp64: 64-B slots), one tile of 256
+// packets per block iteration, staged through LDS like the real kernel:
+//  V=0: 8-B verdict store per lane; V=1: verdicts staged in LDS and written
+//  16 B per lane by half the lanes; V=2: as 0 with non-temporal stores;
+//  V=3: as 0 with two tiles in flight.
+template <int V>
+__global__ void __launch_bounds__(256) tile_kernel(const unsigned char *buf, unsigned long long npkt,
+                                                   unsigned long long stride, unsigned long long *out)
+{
+	__shared__ u32x4 tile[1024];
+	__shared__ unsigned long long vst[256];
+	const unsigned long long ntiles = npkt / 256;
+	unsigned long long t = blockIdx.x;
+	u32x4 r[4], r2[4];
+	auto ld = [&](unsigned long long tt, u32x4 *rr) {
+#pragma unroll
+		for (int j = 0; j < 4; j++) {
+			int c = j * 256 + threadIdx.x;
+			rr[j] = __builtin_nontemporal_load((const u32x4 *)(buf + (tt * 256 + (c >> 2)) * stride + (c & 3) * 16));
+		}
+	};
+	if (t < ntiles) ld(t, r);
+	if (V == 3 && t + gridDim.x < ntiles) ld(t + gridDim.x, r2);
+	while (t < ntiles) {
+#pragma unroll
+		for (int j = 0; j < 4; j++) {
+			int c = j * 256 + threadIdx.x;
+			int p = c >> 2, q = c & 3;
+			tile[p * 4 + (q ^ ((p >> 2) & 3))] = r[j];
+		}
+		__syncthreads();
+		unsigned long long nx = t + (V == 3 ? 2 : 1) * gridDim.x;
+		if (V == 3) {
+#pragma unroll
+			for (int j = 0; j < 4; j++) r[j] = r2[j];
+			if (nx < ntiles) ld(nx, r2);
+		} else if (nx < ntiles) {
+			ld(nx, r);
+		}
+		int p = threadIdx.x;
+		u32x4 a = tile[p * 4 + (0 ^ ((p >> 2) & 3))], b = tile[p * 4 + (1 ^ ((p >> 2) & 3))];
+		unsigned long long v = ((unsigned long long)(a.w ^ b.y) << 32) | (b.z ^ a.x);
+		unsigned long long idx = t * 256 + p;
+		if (V == 1) {
+			vst[p] = v;
+			__syncthreads();
+			if (p < 128) {
+				u32x4 w = *(u32x4 *)&vst[2 * p];
+				*(u32x4 *)&out[t * 256 + 2 * p] = w;
+			}
+		} else if (V == 2) {
+			__builtin_nontemporal_store(v, &out[idx]);
+		} else {
+			out[idx] = v;
+		}
+		__syncthreads();
+		t += gridDim.x;
+	}
+}
+
+template <int V>
+static void run_tile(const char *name, const unsigned char *buf, unsigned long long npkt,
+                     unsigned long long stride, unsigned long long *out, int blocks, int reps)
+{
+	hipEvent_t a, b;
+	CHECK(hipEventCreate(&a));
+	CHECK(hipEventCreate(&b));
+	hipLaunchKernelGGL(tile_kernel<V>, dim3(blocks), dim3(256), 0, 0, buf, npkt, stride, out);
+	CHECK(hipDeviceSynchronize());
+	CHECK(hipEventRecord(a, 0));
+	for (int i = 0; i < reps; i++)
+		hipLaunchKernelGGL(tile_kernel<V>, dim3(blocks), dim3(256), 0, 0, buf, npkt, stride, out);
+	CHECK(hipEventRecord(b, 0));
+	CHECK(hipEventSynchronize(b));
+	float ms = 0;
+	CHECK(hipEventElapsedTime(&ms, a, b));
+	double bytes = (double)npkt * 72;
+	printf("{\"pattern\": \"%s\", \"blocks\": %d, \"depth\": %d, \"useful_bytes\": %.0f, \"us\": %.2f, \"GBs\": %.1f, \"Mpkts\": %.1f}\n",
+	       name, blocks, V, bytes, ms * 1e3 / reps, bytes * reps / (ms * 1e-3) / 1e9,
+	       (double)npkt * reps / (ms * 1e-3) / 1e6);
+	fflush(stdout);
+}
+
+// pure streaming write of B bytes, 16 B per lane
+__global__ void __launch_bounds__(256) write_kernel(u32x4 *out, unsigned long long n16)
+{
+	unsigned long long nthreads = (unsigned long long)gridDim.x * blockDim.x;
+	for (unsigned long long c = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; c < n16; c += nthreads)
+		out[c] = u32x4{(unsigned)c, 1, 2, 3};
+}
+
 static double run_rw(const char *name, const unsigned char *buf, unsigned long long npkt,
                      unsigned long long stride, unsigned long long *out, int blocks, int reps)
 {
@@ -150,6 +241,32 @@ int main(int argc, char **argv)
 		run("hdr32_stride1536", buf, (8ull << 20) * 2, 2, 1536, out, cus * 8, 2, 1);
 		run_rw("rw_udp64", buf, 32ull << 20, 64, vout, cus * 8, 1);
 		run_rw("rw_tcp1500", buf, 8ull << 20, 1536, vout, cus * 8, 1);
+		return 0;
+	}
+	if (argc > 2 && !strcmp(argv[2], "tile")) {
+		for (int gi : {cus * 4, cus * 8, cus * 16}) {
+			run_tile<0>("tile_v0_store8", buf, 32ull << 20, 64, vout, gi, reps);
+			run_tile<1>("tile_v1_store16", buf, 32ull << 20, 64, vout, gi, reps);
+			run_tile<2>("tile_v2_store8_nt", buf, 32ull << 20, 64, vout, gi, reps);
+			run_tile<3>("tile_v3_depth2", buf, 32ull << 20, 64, vout, gi, reps);
+			run_tile<0>("tile_v0_tcp1500", buf, 8ull << 20, 1536, vout, gi, reps);
+		}
+		for (int gi : {cus * 4, cus * 8}) {
+			hipEvent_t a, b;
+			CHECK(hipEventCreate(&a));
+			CHECK(hipEventCreate(&b));
+			unsigned long long n16 = (2ull << 30) / 16;
+			hipLaunchKernelGGL(write_kernel, dim3(gi), dim3(256), 0, 0, (u32x4 *)buf, n16);
+			CHECK(hipEventRecord(a, 0));
+			for (int i = 0; i < reps; i++)
+				hipLaunchKernelGGL(write_kernel, dim3(gi), dim3(256), 0, 0, (u32x4 *)buf, n16);
+			CHECK(hipEventRecord(b, 0));
+			CHECK(hipEventSynchronize(b));
+			float ms = 0;
+			CHECK(hipEventElapsedTime(&ms, a, b));
+			printf("{\"pattern\": \"write_2GiB\", \"blocks\": %d, \"GBs\": %.1f}\n", gi,
+			       (2ull << 30) * (double)reps / (ms * 1e-3) / 1e9);
+		}
 		return 0;
 	}
 	for (int gi : {cus * 4, cus * 8, cus * 16}) {
