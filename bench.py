@@ -41,6 +41,10 @@ WORKLOADS = {
               "32Mi Eth/IPv4/UDP 64B frames per GPU in HBM, uniform 5-tuples, 16 runtimes x 8 kthreads"),
     "tcp1500": (g.WL_TCP1500_ZIPF, 8 << 20, 1536, 1024, 4,
                 "8Mi Eth/IPv4/TCP 1500B frames (1536B slots), Zipf-0.99 over 1Mi flows, 1024 runtimes x 4 kthreads"),
+    # the same 1500-B TCP stream with DPDK buffer split (RTE_ETH_RX_OFFLOAD_BUFFER_SPLIT):
+    # the NIC writes each frame's first 64 B into a dense header slab
+    "tcp1500_hsplit": (g.WL_TCP1500_ZIPF, 8 << 20, 64, 1024, 4,
+                       "8Mi Eth/IPv4/TCP 1500B frames, header-split: 64B header slab, Zipf-0.99, 1024 runtimes x 4 kthreads"),
     "mixed": (g.WL_MIXED, 1 << 20, 9216, 16, 8,
               "1Mi mixed frames (70% IPv4 TCP/UDP 64..9014B, 20% IPv6, 10% ARP), 9216B slots, 16 runtimes"),
 }
@@ -356,14 +360,21 @@ def main():
 
     if world == 1 and not args.no_secondary and args.workload == "udp64":
         w2 = Workload("tcp1500", rank, world, device)
-        el2, kms2 = run_timed(w2, max(5, args.steps // 5), 2, 1)
-        steps2 = max(5, args.steps // 5)
+        el2, kms2 = run_timed(w2, max(20, args.steps // 2), 3, 1)
+        steps2 = max(20, args.steps // 2)
+        w3 = Workload("tcp1500_hsplit", rank, world, device)
+        el3, kms3 = run_timed(w3, steps2, 2, 1)
+        hsplit = {"workload": f"tcp1500_hsplit: {w3.desc}",
+                  "value": round(w3.n * steps2 / el3 / 1e6, 1), "unit": "Mpkt/s",
+                  "roofline": roofline(w3, kms3)}
+        del w3
         result["secondary"] = {
             "workload": f"tcp1500: {w2.desc}",
             "value": round(w2.n * steps2 / el2 / 1e6, 1), "unit": "Mpkt/s",
             "ms_per_step": round(el2 / steps2 * 1e3, 4), "steps": steps2,
             "roofline": roofline(w2, kms2),
             "frame_bytes_rate_GBs": round(w2.n * 1500 / (kms2 * 1e-3) / 1e9, 1),
+            "header_split_layout": hsplit,
         }
         del w2
         torch.cuda.empty_cache()
