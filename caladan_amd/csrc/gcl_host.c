@@ -103,6 +103,20 @@ int gcl_steer_flows(uint16_t thread_count, const uint16_t *active_idx,
 	return 0;
 }
 
+/* tx_prepare_tx_mbuf (tx.c:81) + copy_batch (dma.c:182-185) */
+uint8_t gcl_loopback_olflags(uint8_t tx_olflags)
+{
+	const uint8_t TXFLAG_LOCAL_HINT = 1u << 6; /* inc/iokernel/queue.h:42 */
+	return (uint8_t)(((tx_olflags & TXFLAG_LOCAL_HINT) ? GCL_F_RSS_HASH : 0) |
+	                 GCL_F_IP_CKSUM_GOOD);
+}
+
+/* rss_from_txpkt_payload, inc/iokernel/queue.h:131-134 */
+uint32_t gcl_txpkt_rss(uint64_t payload)
+{
+	return (uint32_t)(payload >> 48);
+}
+
 uint32_t gcl_runtime_ip(uint32_t r)
 {
 	return 0x0A000000u + r + 1;

@@ -52,6 +52,7 @@ struct KParams {
 	const uint8_t *olflags;
 	const uint32_t *rss;
 	const uint32_t *fdir;
+	const uint32_t *dst_hint;
 	uint64_t n;
 	uint64_t ntiles;
 	uint2 *verdicts;
@@ -147,6 +148,18 @@ struct Tables {
 
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
+/* ip_to_proc: open addressing keyed by rte_jhash(&ip, 4, 0); -1 on a miss */
+__device__ __forceinline__ int ipt_lookup(const uint2 *ipt, uint32_t mask, uint32_t ip)
+{
+	uint32_t s = gcl::jhash_u32(ip) & mask;
+	uint2 e = ipt[s];
+	while (__builtin_expect(e.y != kEmpty && e.x != ip, 0)) { /* collision chain */
+		s = (s + 1) & mask;
+		e = ipt[s];
+	}
+	return e.y != kEmpty ? (int)e.y : -1;
+}
+
 /* Toeplitz over the 12-byte tuple with the per-byte LUT (12 x 256 words) */
 __device__ __forceinline__ uint32_t toeplitz_lut(const uint32_t *toep, uint32_t saddr,
                                                  uint32_t daddr, uint32_t sport, uint32_t dport)
@@ -217,11 +230,23 @@ __device__ __forceinline__ void classify_one(const KParams &k, const uint4 *tile
 	if (k.cflags & GCL_CFG_HASH16)
 		hash &= 0xFFFF;
 
+	/* loopback: rx_loopback's dst_ip hint lookup sets the flow tag,
+	 * rx.c:249-262 (a miss leaves the mbuf's own flags) */
+	uint32_t flags2 = flags, hint_mark = 0;
+	if (GENERAL && k.dst_hint) {
+		const uint32_t hint = k.dst_hint[idx];
+		const int q = hint ? ipt_lookup(tb.ipt, k.ipt_mask, hint) : -1;
+		if (q >= 0) {
+			flags2 |= GCL_F_FDIR_ID;
+			hint_mark = (uint32_t)q + 1;
+		}
+	}
+
 	/* hardware flow tag, rx.c:131-146 */
 	int p = -1;
 	uint32_t action = GCL_ACT_DELIVER;
-	if (GENERAL && (flags & GCL_F_FDIR_ID)) {
-		const uint32_t mark = k.fdir ? k.fdir[idx] : 0;
+	if (GENERAL && (flags2 & GCL_F_FDIR_ID)) {
+		const uint32_t mark = hint_mark ? hint_mark - 1 : (k.fdir ? k.fdir[idx] : 0);
 		cnt.flowtag++;
 		if (mark < k.max_rt && tb.rtab[mark].tc != 0) {
 			p = (int)mark;
@@ -239,17 +264,8 @@ __device__ __forceinline__ void classify_one(const KParams &k, const uint4 *tile
 	if (k.ablate & 2) {
 		if (lookup)
 			p = (int)(dst & 15);
-	} else {
-		uint32_t s = gcl::jhash_u32(dst) & k.ipt_mask;
-		uint2 e = tb.ipt[s];
-		bool more = lookup && e.y != kEmpty && e.x != dst;
-		while (__builtin_expect(more, 0)) { /* collision chain: rare */
-			s = (s + 1) & k.ipt_mask;
-			e = tb.ipt[s];
-			more = e.y != kEmpty && e.x != dst;
-		}
-		if (lookup && e.y != kEmpty && e.x == dst)
-			p = (int)e.y;
+	} else if (lookup) {
+		p = ipt_lookup(tb.ipt, k.ipt_mask, dst);
 	}
 	const bool miss = lookup && p < 0;
 	const bool arp_respond = miss && azure && is_arp && frag == GCL_ARP_OP_REQUEST;
@@ -966,6 +982,7 @@ extern "C" int gcl_classify(struct gcl_ctx *c, const struct gcl_batch *b,
 	k.olflags = b->olflags;
 	k.rss = b->rss;
 	k.fdir = b->fdir_hi;
+	k.dst_hint = b->dst_hint;
 	k.n = b->n;
 	k.verdicts = (uint2 *)verdicts;
 	k.counts = (unsigned long long *)runtime_counts;
@@ -982,7 +999,7 @@ extern "C" int gcl_classify(struct gcl_ctx *c, const struct gcl_batch *b,
 	k.ablate = c->tune_ablate;
 
 	/* the specialised fast path needs every header granule in range */
-	bool general = b->offs || b->olflags || b->fdir_hi ||
+	bool general = b->offs || b->olflags || b->fdir_hi || b->dst_hint ||
 	               (c->cfg.default_olflags & GCL_F_FDIR_ID) ||
 	               b->frames_len < (b->n - 1) * b->stride + GCL_HDR_GRANULE;
 	uint32_t tab_bytes = c->off_toep +
@@ -1142,7 +1159,7 @@ static int e2e_setup(gcl_ctx *c, int nstreams, uint64_t chunk)
 	for (int i = 0; i < nstreams; i++) {
 		if (hipStreamCreateWithFlags(&e.st[i], hipStreamNonBlocking) != hipSuccess ||
 		    hipMalloc(&e.slab[i], chunk * GCL_HDR_GRANULE) != hipSuccess ||
-		    hipMalloc(&e.side[i], chunk * 9) != hipSuccess ||
+		    hipMalloc(&e.side[i], chunk * 13) != hipSuccess ||
 		    hipMalloc(&e.verd[i], chunk * sizeof(struct gcl_verdict)) != hipSuccess)
 			return -ENOMEM;
 		e.nstreams = i + 1;
@@ -1200,9 +1217,11 @@ extern "C" int gcl_classify_host(struct gcl_ctx *c, const struct gcl_batch *hb,
 		db.olflags = (const uint8_t *)mapped(hb->olflags);
 		db.rss = (const uint32_t *)mapped(hb->rss);
 		db.fdir_hi = (const uint32_t *)mapped(hb->fdir_hi);
+		db.dst_hint = (const uint32_t *)mapped(hb->dst_hint);
 		struct gcl_verdict *dv = (struct gcl_verdict *)mapped(host_verdicts);
 		if (!db.frames || !dv || (hb->offs && !db.offs) || (hb->olflags && !db.olflags) ||
-		    (hb->rss && !db.rss) || (hb->fdir_hi && !db.fdir_hi)) {
+		    (hb->rss && !db.rss) || (hb->fdir_hi && !db.fdir_hi) ||
+		    (hb->dst_hint && !db.dst_hint)) {
 			hipEventDestroy(ready);
 			return -EFAULT; /* not pinned/registered: see gcl_host_register */
 		}
@@ -1245,6 +1264,10 @@ extern "C" int gcl_classify_host(struct gcl_ctx *c, const struct gcl_batch *hb,
 			if (hb->fdir_hi) {
 				hipMemcpyAsync(side + 5 * chunk, hb->fdir_hi + s, m * 4, hipMemcpyHostToDevice, st);
 				db.fdir_hi = (const uint32_t *)(side + 5 * chunk);
+			}
+			if (hb->dst_hint) {
+				hipMemcpyAsync(side + 9 * chunk, hb->dst_hint + s, m * 4, hipMemcpyHostToDevice, st);
+				db.dst_hint = (const uint32_t *)(side + 9 * chunk);
 			}
 			ret = gcl_classify(c, &db, e.verd[i], dcounts, dstats, st);
 			hipMemcpyAsync(host_verdicts + s, e.verd[i], m * sizeof(struct gcl_verdict),

@@ -64,7 +64,7 @@ class GclBatch(ctypes.Structure):
                 ("stride", ctypes.c_uint64), ("offs", ctypes.c_void_p),
                 ("olflags", ctypes.c_void_p), ("rss", ctypes.c_void_p),
                 ("fdir_hi", ctypes.c_void_p), ("pkt_len", ctypes.c_void_p),
-                ("n", ctypes.c_uint64)]
+                ("n", ctypes.c_uint64), ("dst_hint", ctypes.c_void_p)]
 
 
 class GclGenParams(ctypes.Structure):
@@ -139,6 +139,8 @@ def _load():
         "gcl_kernel_time": (i32, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64), i32]),
         "gcl_generate": (i32, [ctypes.POINTER(GclGenParams), vp, vp, vp, vp]),
         "gcl_runtime_ip": (u32, [u32]),
+        "gcl_loopback_olflags": (ctypes.c_uint8, [ctypes.c_uint8]),
+        "gcl_txpkt_rss": (u32, [u64]),
         "gcl_zipf_cdf": (i32, [u32, ctypes.c_double, vp]),
         "gcl_jenkins_hash": (u32, [ctypes.c_char_p, ctypes.c_size_t]),
         "gcl_toeplitz": (u32, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t]),
@@ -298,7 +300,8 @@ class Classifier:
         return _check(lib.gcl_runtime_del(self._ctx, uniqid), "gcl_runtime_del")
 
     def classify(self, frames, n, stride=0, verdicts=None, counts=None, stats=None, offs=None,
-                 olflags=None, rss=None, fdir_hi=None, frames_len=None, stream=None):
+                 olflags=None, rss=None, fdir_hi=None, frames_len=None, stream=None,
+                 dst_hint=None):
         """Launch the classify kernel on device buffers (asynchronous)."""
         if verdicts is not None and _nbytes(verdicts) < 8 * n:
             raise ValueError("verdict buffer too small")
@@ -306,24 +309,24 @@ class Classifier:
             raise ValueError("counts buffer too small")
         if stats is not None and _nbytes(stats) < 8 * NR_STATS:
             raise ValueError("stats buffer too small")
-        for arr, w in ((offs, 8), (olflags, 1), (rss, 4), (fdir_hi, 4)):
+        for arr, w in ((offs, 8), (olflags, 1), (rss, 4), (fdir_hi, 4), (dst_hint, 4)):
             if arr is not None and _nbytes(arr) < w * n:
                 raise ValueError("per-packet array too small")
         b = GclBatch(frames=_ptr(frames),
                      frames_len=_nbytes(frames) if frames_len is None else frames_len,
                      stride=stride, offs=_ptr(offs), olflags=_ptr(olflags), rss=_ptr(rss),
-                     fdir_hi=_ptr(fdir_hi), pkt_len=None, n=n)
+                     fdir_hi=_ptr(fdir_hi), pkt_len=None, n=n, dst_hint=_ptr(dst_hint))
         return _check(lib.gcl_classify(self._ctx, ctypes.byref(b), _ptr(verdicts), _ptr(counts),
                                        _ptr(stats), stream), "gcl_classify")
 
     def classify_host(self, frames, n, stride=0, verdicts=None, counts=None, stats=None,
                       olflags=None, rss=None, fdir_hi=None, offs=None, frames_len=None,
-                      mode=E2E_COPY, nstreams=2, chunk=1 << 20):
+                      mode=E2E_COPY, nstreams=2, chunk=1 << 20, dst_hint=None):
         """End-to-end: host (pinned) frames in, host verdicts out (synchronous)."""
         b = GclBatch(frames=_ptr(frames),
                      frames_len=_nbytes(frames) if frames_len is None else frames_len,
                      stride=stride, offs=_ptr(offs), olflags=_ptr(olflags), rss=_ptr(rss),
-                     fdir_hi=_ptr(fdir_hi), pkt_len=None, n=n)
+                     fdir_hi=_ptr(fdir_hi), pkt_len=None, n=n, dst_hint=_ptr(dst_hint))
         o = GclE2eOpts(mode=mode, nstreams=nstreams, chunk=chunk)
         return _check(lib.gcl_classify_host(self._ctx, ctypes.byref(b), _ptr(verdicts), _ptr(counts),
                                             _ptr(stats), ctypes.byref(o)), "gcl_classify_host")

@@ -106,6 +106,11 @@ struct gcl_batch {
 	                               the kernel, only by the host post-pass that
 	                               builds rxq_cmd (rx_make_cmd, rx.c:24-38) */
 	uint64_t        n;          /* packets in the batch */
+	const uint32_t *dst_hint;   /* optional u32[n] loopback hint: tx_pktmbuf_priv.dst_ip
+	                               (host order, 0 = none).  A hint found in ip_to_proc
+	                               marks the packet FDIR with hash.fdir.hi = uniqid
+	                               before classification, as rx_loopback does
+	                               (iokernel/rx.c:249-262); it overrides fdir_hi[] */
 };
 
 /*
@@ -282,6 +287,16 @@ uint32_t gcl_runtime_ip(uint32_t r);
 /* Host helper: Zipf(s) CDF over @nflows ranks as u64 fixed point
  * (cdf[k] = floor(P(rank <= k) * 2^64), last entry saturated). */
 int gcl_zipf_cdf(uint32_t nflows, double s, uint64_t *cdf_out);
+
+/*
+ * Loopback feed helpers (iokernel/tx.c:81-83, iokernel/dma.c:182-185): the rx
+ * olflags of a looped-back tx packet (RSS_HASH iff the runtime set
+ * TXFLAG_LOCAL_HINT; IP checksum always good after copy_batch), and the 16-bit
+ * steering hint carried in bits 48..63 of the txpkt payload
+ * (inc/iokernel/queue.h:120-134).
+ */
+uint8_t gcl_loopback_olflags(uint8_t tx_olflags);
+uint32_t gcl_txpkt_rss(uint64_t payload);
 
 /* Host reference of the two hashes the kernel computes (for callers that
  * need the same value on the CPU, e.g. the loopback hint). */

@@ -380,9 +380,18 @@ static void orc_rx_one_pkt(const struct orc_tables *t, const struct gcl_batch *b
 	v->uniqid = GCL_NO_RUNTIME;
 	v->thread = GCL_NO_THREAD;
 
+	/* rx_loopback, rx.c:249-262: a tx dst_ip hint found in ip_to_proc sets
+	 * RTE_MBUF_F_RX_FDIR_ID with hash.fdir.hi = p->uniqid */
+	int hint_p = -1;
+	if (b->dst_hint && b->dst_hint[i]) {
+		hint_p = iptab_lookup(t, b->dst_hint[i]);
+		if (hint_p >= 0)
+			flags |= GCL_F_FDIR_ID;
+	}
+
 	/* hardware flow tag, rx.c:131-146 */
 	if (flags & GCL_F_FDIR_ID) {
-		uint32_t mark = b->fdir_hi ? b->fdir_hi[i] : 0;
+		uint32_t mark = hint_p >= 0 ? (uint32_t)hint_p : (b->fdir_hi ? b->fdir_hi[i] : 0);
 		stats[GCL_RX_FLOW_TAG_MATCH]++;
 		if (mark < t->max_runtimes && t->rt[mark].present) {
 			p = (int)mark;

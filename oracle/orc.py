@@ -26,7 +26,7 @@ class Batch(ctypes.Structure):
                 ("stride", ctypes.c_uint64), ("offs", ctypes.c_void_p),
                 ("olflags", ctypes.c_void_p), ("rss", ctypes.c_void_p),
                 ("fdir_hi", ctypes.c_void_p), ("pkt_len", ctypes.c_void_p),
-                ("n", ctypes.c_uint64)]
+                ("n", ctypes.c_uint64), ("dst_hint", ctypes.c_void_p)]
 
 
 class GenParams(ctypes.Structure):
@@ -153,16 +153,18 @@ class Tables:
     def runtime_del(self, uniqid):
         return self._lib.orc_runtime_del(self.h, uniqid)
 
-    def _batch(self, frames, n, stride, offs, olflags, rss, fdir_hi, pkt_len, frames_len):
-        self._keep = [frames, offs, olflags, rss, fdir_hi, pkt_len]
+    def _batch(self, frames, n, stride, offs, olflags, rss, fdir_hi, pkt_len, frames_len,
+               dst_hint=None):
+        self._keep = [frames, offs, olflags, rss, fdir_hi, pkt_len, dst_hint]
         return Batch(frames=frames.ctypes.data, frames_len=frames.nbytes if frames_len is None else frames_len,
                      stride=stride, offs=_p(offs), olflags=_p(olflags), rss=_p(rss),
-                     fdir_hi=_p(fdir_hi), pkt_len=_p(pkt_len), n=n)
+                     fdir_hi=_p(fdir_hi), pkt_len=_p(pkt_len), n=n, dst_hint=_p(dst_hint))
 
     def classify(self, frames, n, stride=0, offs=None, olflags=None, rss=None, fdir_hi=None,
-                 pkt_len=None, frames_len=None, lrpc=False):
+                 pkt_len=None, frames_len=None, lrpc=False, dst_hint=None):
         """Returns (verdicts structured array, counts u64[R], stats u64[8])."""
-        b = self._batch(frames, n, stride, offs, olflags, rss, fdir_hi, pkt_len, frames_len)
+        b = self._batch(frames, n, stride, offs, olflags, rss, fdir_hi, pkt_len, frames_len,
+                        dst_hint)
         v = np.zeros(n, dtype=VERDICT_DTYPE)
         counts = np.zeros(self.max_runtimes, dtype=np.uint64)
         stats = np.zeros(NR_STATS, dtype=np.uint64)

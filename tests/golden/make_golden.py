@@ -117,13 +117,14 @@ def steer(uniq, h):
     return FLOW[uniq][h % TC[uniq]], DELIVER
 
 
-def pkt(cite, frame, flags, rss, fdir, hash_, uniq, action, thread=None):
+def pkt(cite, frame, flags, rss, fdir, hash_, uniq, action, thread=None, hint=0, hint_hit=False):
     if uniq is None:
         uniq, thread = 0xFFFF, 0xFF
     elif thread is None:
         thread, act = steer(uniq, hash_)
         action |= act
     return {"cite": cite, "frame": frame.hex(), "olflags": flags, "rss": rss, "fdir_hi": fdir,
+            "dst_hint": hint, "hint_hit": hint_hit,
             "expect": {"hash": hash_, "uniqid": uniq, "thread": thread, "action": action}}
 
 
@@ -187,6 +188,52 @@ def azure_set():
     return {
         "name": "azure_arp_mode",
         "cfg": {"max_runtimes": 16, "hash_mode": 0, "flags": 1, "default_olflags": 0,
+                "rss_key": MS_KEY.hex()},
+        "packets": P,
+    }
+
+
+def loopback_set():
+    """Local traffic re-entering rx through rx_loopback (rx.c:235-265):
+    tx_prepare_tx_mbuf sets hash.rss to the runtime's 16-bit hint and
+    RSS_HASH iff TXFLAG_LOCAL_HINT (tx.c:81-83); copy_batch adds
+    IP_CKSUM_GOOD (dma.c:182-185); a dst_ip hint found in ip_to_proc sets
+    FDIR_ID with fdir.hi = uniqid (rx.c:250-262) and rx_one_pkt delivers on
+    that mark (rx.c:131-146) whatever the frame holds."""
+    P = []
+    u = l4(40000, 80)
+    LH = F_RSS | CK_GOOD  # TXFLAG_LOCAL_HINT set
+    NH = CK_GOOD          # no local hint
+    P.append(pkt("rx.c:250-262 + :131-146: hint = A -> FDIR to A, thread flow_tbl[hint16 % 8]",
+                 eth(0x0800) + ipv4(A_IP - 1, A_IP, 17, u), LH, 0xBEEF, 0, 0xBEEF, 3, FDIR,
+                 hint=A_IP, hint_hit=True))
+    P.append(pkt("rx.c:258-260: the mark comes from the hint, not from the frame (hint B, daddr A)",
+                 eth(0x0800) + ipv4(A_IP - 1, A_IP, 17, u), LH, 0x1234, 0, 0x1234, 7, FDIR,
+                 hint=B_IP, hint_hit=True))
+    P.append(pkt("rx.c:252-253: no hint -> parse path; no LOCAL_HINT -> RX_HASH_MISSING",
+                 eth(0x0800) + ipv4(A_IP, B_IP, 17, u), NH, 0, 0, 0, 7, DELIVER))
+    P.append(pkt("rx.c:258: hint miss leaves the flags -> parse path to the frame's daddr",
+                 eth(0x0800) + ipv4(B_IP, A_IP, 17, u), LH, 0x55, 0, 0x55, 3, DELIVER,
+                 hint=ip("10.1.1.1")))
+    P.append(pkt("rx.c:62-72: hint to a runtime with no active thread -> wake",
+                 eth(0x0800) + ipv4(A_IP, C_IP, 17, u), LH, 0x77, 0, 0x77, 9, FDIR,
+                 hint=C_IP, hint_hit=True))
+    P.append(pkt("rx.c:131-146: FDIR delivery ignores the Ethertype (hinted ARP)",
+                 eth(0x0806, dst=b"\xff" * 6) + arp(1, B_IP, A_IP), LH, 0x3, 0, 0x3, 3, FDIR,
+                 hint=A_IP, hint_hit=True))
+    P.append(pkt("tx.c:285-289 broadcast loopback (no hint): ARP request parsed to its tip",
+                 eth(0x0806, dst=b"\xff" * 6) + arp(1, A_IP, B_IP), NH, 0, 0, 0, 7, DELIVER))
+    P.append(pkt("hint miss on IPv6 -> rx.c:191-194 drop",
+                 eth(0x86DD) + b"\x60" + b"\0" * 39, LH, 1, 0, 1, None, DROP_ET, hint=ip("10.1.1.2")))
+    P.append(pkt("rx.c:260: a hint hit overrides an mbuf's own fdir.hi",
+                 eth(0x0800) + ipv4(A_IP, C_IP, 17, u), F_FDIR | LH, 0x10, 7, 0x10, 3, FDIR,
+                 hint=A_IP, hint_hit=True))
+    P.append(pkt("hint miss keeps an mbuf's own FDIR mark (fdir.hi = B)",
+                 eth(0x0800) + ipv4(A_IP, C_IP, 17, u), F_FDIR | LH, 0x11, 7, 0x11, 7, FDIR,
+                 hint=ip("10.1.1.3")))
+    return {
+        "name": "loopback",
+        "cfg": {"max_runtimes": 16, "hash_mode": 0, "flags": 0, "default_olflags": 0,
                 "rss_key": MS_KEY.hex()},
         "packets": P,
     }
@@ -265,7 +312,7 @@ def expected_stats(s):
         act = e["action"] & 0x7F
         fl = p["olflags"]
         st[6] += 1  # RX_PULLED
-        if fl & F_FDIR:
+        if fl & F_FDIR or p.get("hint_hit"):
             st[3] += 1  # RX_FLOW_TAG_MATCH
         et = int(p["frame"][24:28], 16)
         if not (e["action"] & FDIR) and et == 0x0800 and not (fl & F_RSS):
@@ -320,7 +367,8 @@ def main():
                    "vectors": [{"dst": d, "dport": dp, "src": s, "sport": sp, "ipv4": h4,
                                 "ipv4_tcp": h4t} for d, dp, s, sp, h4, h4t in MS_VECTORS]},
                   f, indent=1)
-    sets = [nic_set(), azure_set(), jenkins_set(), toeplitz_set(False), toeplitz_set(True)]
+    sets = [nic_set(), azure_set(), loopback_set(), jenkins_set(), toeplitz_set(False),
+            toeplitz_set(True)]
     for s in sets:
         s["runtimes"] = RUNTIMES + s.pop("extra_runtimes", [])
         s["expect_stats"] = expected_stats(s)

@@ -33,11 +33,12 @@ def scenario_batch(s, slot=128):
     olflags = np.array([p["olflags"] for p in pk], dtype=np.uint8)
     rss = np.array([p["rss"] for p in pk], dtype=np.uint32)
     fdir = np.array([p["fdir_hi"] for p in pk], dtype=np.uint32)
+    hint = np.array([p.get("dst_hint", 0) for p in pk], dtype=np.uint32)
     exp = np.zeros(n, dtype=[("hash", "<u4"), ("uniqid", "<u2"), ("thread", "u1"), ("action", "u1")])
     for i, p in enumerate(pk):
         e = p["expect"]
         exp[i] = (e["hash"], e["uniqid"], e["thread"], e["action"])
-    return frames, olflags, rss, fdir, exp
+    return frames, olflags, rss, fdir, exp, (hint if hint.any() else None)
 
 
 def apply_runtimes(target, runtimes):
@@ -119,6 +120,10 @@ def fuzz_batch(rng, n, runtimes, max_runtimes, slot=128, tail_runts=True):
         fr = fr[:slot]
         o = int(offs[i])
         frames[o:o + len(fr)] = np.frombuffer(fr, dtype=np.uint8)
+    # loopback hints (tx_pktmbuf_priv.dst_ip): none, a registered IP, or a miss
+    u = rng.random(n)
+    hint = np.where(u < 0.5, 0, np.where(u < 0.85, rng.choice(ips, size=n),
+                                         rng.integers(1, 2**32, size=n))).astype(np.uint32)
     frames_len = frames.nbytes
     if tail_runts and n >= 4:
         # put 3 packets at the very end so their headers straddle frames_len
@@ -126,4 +131,4 @@ def fuzz_batch(rng, n, runtimes, max_runtimes, slot=128, tail_runts=True):
         for j, cut in enumerate((20, 36, 60)):
             offs[n - 1 - j] = last + 16 * j
         frames_len = last + 16 * 2 + 40
-    return frames, frames_len, offs, olflags, rss, fdir
+    return frames, frames_len, offs, olflags, rss, fdir, hint

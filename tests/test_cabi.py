@@ -36,7 +36,7 @@ def test_library_exports_every_declared_symbol(g):
 
 def test_struct_layouts(g):
     assert ctypes.sizeof(g.GclCfg) == 56
-    assert ctypes.sizeof(g.GclBatch) == 72
+    assert ctypes.sizeof(g.GclBatch) == 80
     assert ctypes.sizeof(g.GclVerdict) == 8
     assert ctypes.sizeof(g.GclLrpcMsg) == 16
     assert ctypes.sizeof(g.GclLrpcChanOut) == 32  # struct lrpc_chan_out, lrpc.h:28-35
@@ -77,6 +77,14 @@ def test_steer_flows_matches_oracle(g, orc):
         g.steer_flows(4, [4])
     with pytest.raises(OSError):
         g.steer_flows(300, [1])
+
+
+def test_loopback_helpers(g):
+    # tx.c:81: RSS_HASH iff TXFLAG_LOCAL_HINT (BIT(6), queue.h:42); dma.c:184 csum good
+    assert g.lib.gcl_loopback_olflags(1 << 6) == g.F_RSS_HASH | g.F_IP_CKSUM_GOOD
+    assert g.lib.gcl_loopback_olflags(1 << 4) == g.F_IP_CKSUM_GOOD
+    # queue.h:120-134: the 16-bit hint rides in bits 48..63 of the payload
+    assert g.lib.gcl_txpkt_rss((0xBEEF << 48) | 0x123456789A) == 0xBEEF
 
 
 def test_rx_make_cmd(g):
@@ -152,7 +160,7 @@ def test_host_deliver_matches_reference_model(g, orc):
     R = 64
     rts = random_runtimes(rng, R, 24, max_threads=6)
     n = 3000
-    frames, flen, offs, olf, rss, fdir = fuzz_batch(rng, n, rts, R, tail_runts=False)
+    frames, flen, offs, olf, rss, fdir, _ = fuzz_batch(rng, n, rts, R, tail_runts=False)
     t = orc.Tables(R, 0, 0, 0x09)
     for r in rts:
         assert t.runtime_set(r["uniqid"], r["ip"], r["thread_count"], r["active"], r["flow_tbl"]) == 0

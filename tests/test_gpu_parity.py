@@ -23,7 +23,7 @@ def dev(a):
 
 
 def gpu_run(g, clf, frames, n, stride=0, offs=None, olflags=None, rss=None, fdir=None,
-            frames_len=None, counts=None, stats=None):
+            frames_len=None, counts=None, stats=None, hint=None):
     f = dev(frames.view(np.uint8))
     v = torch.zeros(n * 8, dtype=torch.uint8, device="cuda")
     c = counts if counts is not None else torch.zeros(clf.max_runtimes, dtype=torch.int64, device="cuda")
@@ -32,7 +32,8 @@ def gpu_run(g, clf, frames, n, stride=0, offs=None, olflags=None, rss=None, fdir
     clf.classify(f, n, stride, verdicts=v, counts=c, stats=s, offs=o, olflags=dev(olflags),
                  rss=dev(rss.view(np.int32)) if rss is not None else None,
                  fdir_hi=dev(fdir.astype(np.int32)) if fdir is not None else None,
-                 frames_len=frames_len)
+                 frames_len=frames_len,
+                 dst_hint=dev(hint.view(np.int32)) if hint is not None else None)
     torch.cuda.synchronize()
     return (v.cpu().numpy().view(g.VERDICT_DTYPE), c.cpu().numpy().astype(np.uint64),
             s.cpu().numpy().astype(np.uint64))
@@ -54,8 +55,9 @@ def test_gpu_scenarios(g, s):
     clf = g.Classifier(0, cfg["max_runtimes"], cfg["hash_mode"], cfg["flags"], cfg["default_olflags"],
                        bytes.fromhex(cfg["rss_key"]))
     apply_runtimes(clf, s["runtimes"])
-    frames, olflags, rss, fdir, exp = scenario_batch(s)
-    v, c, st = gpu_run(g, clf, frames, len(exp), 128, olflags=olflags, rss=rss, fdir=fdir)
+    frames, olflags, rss, fdir, exp, hint = scenario_batch(s)
+    v, c, st = gpu_run(g, clf, frames, len(exp), 128, olflags=olflags, rss=rss, fdir=fdir,
+                       hint=hint)
     for i in range(len(exp)):
         assert tuple(v[i]) == tuple(exp[i]), (s["packets"][i]["cite"], v[i], exp[i])
     assert list(st) == s["expect_stats"]
@@ -69,14 +71,18 @@ def test_gpu_fuzz_vs_oracle(g, orc, mode, flags, max_rt):
     rng = np.random.default_rng(1000 * mode + 10 * flags + max_rt)
     rts = random_runtimes(rng, max_rt, min(max_rt, 40 if max_rt == 16 else 300))
     n = 5000
-    frames, flen, offs, olf, rss, fdir = fuzz_batch(rng, n, rts, max_rt)
+    frames, flen, offs, olf, rss, fdir, hint = fuzz_batch(rng, n, rts, max_rt)
+    if flags == 2:
+        hint = None  # keep one arm without the loopback feed
     key = bytes(rng.integers(0, 256, size=40, dtype=np.uint8))
     t = orc.Tables(max_rt, mode, flags, 0x09, key)
     apply_runtimes(t, rts)
-    ve, ce, se = t.classify(frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir_hi=fdir, frames_len=flen)
+    ve, ce, se = t.classify(frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir_hi=fdir, frames_len=flen,
+                            dst_hint=hint)
     clf = g.Classifier(0, max_rt, mode, flags, 0x09, key)
     apply_runtimes(clf, rts)
-    v, c, st = gpu_run(g, clf, frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir=fdir, frames_len=flen)
+    v, c, st = gpu_run(g, clf, frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir=fdir, frames_len=flen,
+                       hint=hint)
     assert_same(v, ve, f"mode={mode} flags={flags} R={max_rt}")
     assert (c == ce).all()
     assert (st == se).all(), (st, se)

@@ -13,9 +13,10 @@ def test_oracle_matches_scenarios(orc, s):
     t = orc.Tables(cfg["max_runtimes"], cfg["hash_mode"], cfg["flags"], cfg["default_olflags"],
                    bytes.fromhex(cfg["rss_key"]))
     apply_runtimes(t, s["runtimes"])
-    frames, olflags, rss, fdir, exp = scenario_batch(s)
+    frames, olflags, rss, fdir, exp, hint = scenario_batch(s)
     n = len(exp)
-    v, counts, stats = t.classify(frames, n, 128, olflags=olflags, rss=rss, fdir_hi=fdir)
+    v, counts, stats = t.classify(frames, n, 128, olflags=olflags, rss=rss, fdir_hi=fdir,
+                                  dst_hint=hint)
     for i in range(n):
         assert tuple(v[i]) == tuple(exp[i]), (s["packets"][i]["cite"], v[i], exp[i])
     assert list(stats) == s["expect_stats"]
