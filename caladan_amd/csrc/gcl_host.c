@@ -117,6 +117,29 @@ uint32_t gcl_txpkt_rss(uint64_t payload)
 	return (uint32_t)(payload >> 48);
 }
 
+/* CRC32C (Castagnoli, reflected 0x82F63B78) over the 8 little-endian bytes of
+ * @val starting from @crc with no inversion: the crc32q instruction that
+ * hash_crc32c_one/two use (inc/base/hash.h:23-40, inc/asm/ops.h:77-80). */
+uint32_t gcl_crc32c_u64(uint32_t crc, uint64_t val)
+{
+	for (int i = 0; i < 8; i++) {
+		crc ^= (uint8_t)(val >> (8 * i));
+		for (int b = 0; b < 8; b++)
+			crc = (crc >> 1) ^ (0x82F63B78u & (0u - (crc & 1)));
+	}
+	return crc;
+}
+
+/* trans_hash_5tuple / trans_hash_3tuple, runtime/net/transport.c:29-42 */
+void gcl_trans_hash(uint32_t seed, uint8_t proto, uint32_t lip, uint16_t lport, uint32_t rip,
+                    uint16_t rport, struct gcl_trans *out)
+{
+	uint64_t l = (uint64_t)lip | (uint64_t)lport << 32;
+	uint64_t r = (uint64_t)rip | (uint64_t)rport << 32 | (uint64_t)proto << 48;
+	out->h5 = gcl_crc32c_u64(gcl_crc32c_u64(seed, l), r);
+	out->h3 = gcl_crc32c_u64(seed, l | (uint64_t)proto << 48);
+}
+
 uint32_t gcl_runtime_ip(uint32_t r)
 {
 	return 0x0A000000u + r + 1;

@@ -31,6 +31,7 @@ namespace {
 
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 constexpr uint32_t kToepBytes = 12 * 256 * 4;
+constexpr uint32_t kCrcBytes = 8 * 256 * 4;
 constexpr uint32_t kLdsTableBudget = 96 * 1024;
 
 /* tuning knobs for experiments (GCL_TUNE_BLOCKS_PER_CU caps the grid) */
@@ -66,6 +67,8 @@ struct KParams {
 	uint32_t default_flags;
 	uint32_t nt_store;
 	uint32_t ablate; /* GCL_TUNE_ABLATE: timing-only experiments, wrong results */
+	uint2 *trans;    /* struct gcl_trans[n] or NULL */
+	uint32_t off_seed, off_crc;
 };
 
 /* ------------------------------------------------------------------------
@@ -144,7 +147,19 @@ struct Tables {
 	const RtEntry *rtab;
 	const uint8_t *flow;
 	const uint32_t *toep;
+	const uint32_t *seed;  /* per-runtime trans_seed */
+	const uint32_t *crc;   /* CRC32C slice-by-8 LUT, 8 x 256 words */
 };
+
+/* crc32q semantics (no inversion) over the 8 LE bytes of v, slice-by-8 */
+__device__ __forceinline__ uint32_t crc32c_u64(const uint32_t *T, uint32_t crc, uint64_t v)
+{
+	const uint32_t lo = crc ^ (uint32_t)v, hi = (uint32_t)(v >> 32);
+	return T[7 * 256 + (lo & 0xFF)] ^ T[6 * 256 + ((lo >> 8) & 0xFF)] ^
+	       T[5 * 256 + ((lo >> 16) & 0xFF)] ^ T[4 * 256 + (lo >> 24)] ^
+	       T[3 * 256 + (hi & 0xFF)] ^ T[2 * 256 + ((hi >> 8) & 0xFF)] ^
+	       T[1 * 256 + ((hi >> 16) & 0xFF)] ^ T[0 * 256 + (hi >> 24)];
+}
 
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
@@ -294,6 +309,24 @@ __device__ __forceinline__ void classify_one(const KParams &k, const uint4 *tile
 		if (!(k.ablate & 4))
 			atomicAdd(&hist[p], 1u);
 	}
+	if (k.trans) {
+		/* trans_lookup's hashes with runtime p's trans_seed
+		 * (transport.c:29-42, :366-375), for the packets net_rx_one passes
+		 * to net_rx_trans (core.c:203-209, :281-300) */
+		const bool supported = is_ip && (d3 >> 20 & 0xF) == 4 && ihl == 5 &&
+		                       !(d5 & 0x2000) && (proto == 6 || proto == 17);
+		uint2 tr = make_uint2(0, 0);
+		if (p >= 0 && supported) {
+			const uint32_t seed = tb.seed[p];
+			const uint64_t l = (uint64_t)daddr | (uint64_t)gcl::bswap16(d9 & 0xFFFF) << 32;
+			const uint64_t r = (uint64_t)saddr | (uint64_t)gcl::bswap16(d8 >> 16) << 32 |
+			                   (uint64_t)proto << 48;
+			tr.x = crc32c_u64(tb.crc, crc32c_u64(tb.crc, seed, l), r);
+			tr.y = crc32c_u64(tb.crc, seed, l | (uint64_t)proto << 48);
+			action |= GCL_ACT_F_TRANS;
+		}
+		k.trans[idx] = tr;
+	}
 	const u32x2 vd = {hash, uniq | thr << 16 | action << 24};
 	if (k.nt_store)
 		__builtin_nontemporal_store(vd, (u32x2 *)&k.verdicts[idx]);
@@ -341,6 +374,8 @@ classify_kernel(KParams k)
 	tb.rtab = (const RtEntry *)(tab + k.off_rt);
 	tb.flow = tab + k.off_flow;
 	tb.toep = (const uint32_t *)(tab + k.off_toep);
+	tb.seed = (const uint32_t *)(tab + k.off_seed);
+	tb.crc = (const uint32_t *)(tab + k.off_crc);
 	__syncthreads();
 
 	Counters cnt = {0, 0, 0, 0};
@@ -564,10 +599,11 @@ struct gcl_ctx {
 		uint32_t ip;
 		uint16_t tc, active;
 		uint8_t flow[GCL_NCPU];
+		uint32_t trans_seed;
 	};
 	std::vector<Rt> rt;
 	uint32_t ipt_slots;
-	uint32_t off_rt, off_flow, off_toep, image_cap;
+	uint32_t off_rt, off_flow, off_toep, off_seed, off_crc, image_cap, image_bytes;
 	uint32_t flow_used;
 	bool dirty;
 	/* two device images + pinned staging, each guarded by an event */
@@ -637,7 +673,9 @@ extern "C" int gcl_open(int hip_device, const struct gcl_cfg *cfg, struct gcl_ct
 	c->off_rt = c->ipt_slots * 8;
 	c->off_flow = c->off_rt + cfg->max_runtimes * 16;
 	/* the Toeplitz LUT offset depends on flow_used; reserve worst case */
-	c->image_cap = c->off_flow + cfg->max_runtimes * GCL_NCPU + 16 + kToepBytes;
+	c->image_cap = c->off_flow + cfg->max_runtimes * GCL_NCPU + 16 + kToepBytes +
+	               cfg->max_runtimes * 4 + 16 + kCrcBytes;
+	c->image_bytes = 0;
 	c->flow_used = 0;
 	c->dirty = true;
 	c->cur = 0;
@@ -738,6 +776,8 @@ extern "C" int gcl_runtime_set(struct gcl_ctx *c, uint16_t uniqid, uint32_t ip_h
 	if (owner != kEmpty && owner != uniqid)
 		return -EEXIST; /* dp_clients.c:174-179 */
 	gcl_ctx::Rt &r = c->rt[uniqid];
+	if (!r.present)
+		r.trans_seed = 0;
 	r.present = true;
 	r.ip = ip_host;
 	r.tc = thread_count;
@@ -746,6 +786,17 @@ extern "C" int gcl_runtime_set(struct gcl_ctx *c, uint16_t uniqid, uint32_t ip_h
 	if (active_count)
 		for (int i = 0; i < thread_count; i++)
 			r.flow[i] = (uint8_t)flow_tbl[i];
+	c->dirty = true;
+	return 0;
+}
+
+extern "C" int gcl_runtime_set_trans_seed(struct gcl_ctx *c, uint16_t uniqid, uint32_t seed)
+{
+	if (!c || !(c->cfg.flags & GCL_CFG_TRANS_HASH))
+		return -EINVAL;
+	if (uniqid >= c->cfg.max_runtimes || !c->rt[uniqid].present)
+		return -ENOENT;
+	c->rt[uniqid].trans_seed = seed;
 	c->dirty = true;
 	return 0;
 }
@@ -802,7 +853,28 @@ static uint32_t build_image(gcl_ctx *c)
 			}
 		bytes += kToepBytes;
 	}
-	return align16(bytes);
+	c->off_seed = c->off_crc = 0;
+	if (c->cfg.flags & GCL_CFG_TRANS_HASH) {
+		c->off_seed = bytes;
+		uint32_t *seed = (uint32_t *)(img + bytes);
+		for (uint32_t u = 0; u < max_rt; u++)
+			seed[u] = c->rt[u].present ? c->rt[u].trans_seed : 0;
+		bytes = align16(bytes + max_rt * 4);
+		c->off_crc = bytes;
+		uint32_t *T = (uint32_t *)(img + bytes);
+		for (uint32_t b = 0; b < 256; b++) {
+			uint32_t x = b;
+			for (int i = 0; i < 8; i++)
+				x = (x >> 1) ^ (0x82F63B78u & (0u - (x & 1)));
+			T[b] = x;
+		}
+		for (int t = 1; t < 8; t++)
+			for (uint32_t b = 0; b < 256; b++)
+				T[t * 256 + b] = (T[(t - 1) * 256 + b] >> 8) ^ T[T[(t - 1) * 256 + b] & 0xFF];
+		bytes += kCrcBytes;
+	}
+	c->image_bytes = align16(bytes);
+	return c->image_bytes;
 }
 
 static hipEvent_t prof_event(gcl_ctx *c)
@@ -959,7 +1031,18 @@ extern "C" int gcl_classify(struct gcl_ctx *c, const struct gcl_batch *b,
                             struct gcl_verdict *verdicts, uint64_t *runtime_counts,
                             uint64_t *stats, void *hip_stream)
 {
-	if (!c || !b)
+	struct gcl_out o = {verdicts, runtime_counts, stats, nullptr};
+	return gcl_classify_ex(c, b, &o, hip_stream);
+}
+
+extern "C" int gcl_classify_ex(struct gcl_ctx *c, const struct gcl_batch *b,
+                               const struct gcl_out *out, void *hip_stream)
+{
+	if (!c || !b || !out)
+		return -EINVAL;
+	struct gcl_verdict *verdicts = out->verdicts;
+	uint64_t *runtime_counts = out->runtime_counts, *stats = out->stats;
+	if (out->trans && !(c->cfg.flags & GCL_CFG_TRANS_HASH))
 		return -EINVAL;
 	hipStream_t s = (hipStream_t)hip_stream;
 	if (b->n == 0)
@@ -993,6 +1076,9 @@ extern "C" int gcl_classify(struct gcl_ctx *c, const struct gcl_batch *b,
 	k.off_rt = c->off_rt;
 	k.off_flow = c->off_flow;
 	k.off_toep = c->off_toep;
+	k.off_seed = c->off_seed;
+	k.off_crc = c->off_crc;
+	k.trans = (uint2 *)out->trans;
 	k.cflags = c->cfg.flags;
 	k.default_flags = c->cfg.default_olflags;
 	k.nt_store = c->tune_nt_store;
@@ -1002,9 +1088,7 @@ extern "C" int gcl_classify(struct gcl_ctx *c, const struct gcl_batch *b,
 	bool general = b->offs || b->olflags || b->fdir_hi || b->dst_hint ||
 	               (c->cfg.default_olflags & GCL_F_FDIR_ID) ||
 	               b->frames_len < (b->n - 1) * b->stride + GCL_HDR_GRANULE;
-	uint32_t tab_bytes = c->off_toep +
-	                     (c->cfg.hash_mode == GCL_HASH_TOEPLITZ ? kToepBytes : 0);
-	tab_bytes = align16(tab_bytes);
+	uint32_t tab_bytes = c->image_bytes;
 	uint32_t hist_bytes = ((c->cfg.max_runtimes + 3) & ~3u) * 4;
 	bool tlds = tab_bytes <= kLdsTableBudget;
 	if (c->tune_tables == 1)

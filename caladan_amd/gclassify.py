@@ -24,7 +24,7 @@ GCL_RX_BURST_SIZE = 64
 HASH_NIC, HASH_JENKINS, HASH_TOEPLITZ = 0, 1, 2
 HASH_MODES = {"nic": HASH_NIC, "jenkins": HASH_JENKINS, "toeplitz": HASH_TOEPLITZ}
 
-CFG_AZURE_ARP, CFG_HASH16, CFG_PROFILE = 0x1, 0x2, 0x4
+CFG_AZURE_ARP, CFG_HASH16, CFG_PROFILE, CFG_TRANS_HASH = 0x1, 0x2, 0x4, 0x8
 
 F_RSS_HASH, F_FDIR_ID = 0x01, 0x02
 F_IP_CKSUM_MASK, F_IP_CKSUM_UNKNOWN, F_IP_CKSUM_BAD = 0x0C, 0x00, 0x04
@@ -32,7 +32,7 @@ F_IP_CKSUM_GOOD, F_IP_CKSUM_NONE = 0x08, 0x0C
 
 ACT_DELIVER, ACT_WAKE, ACT_DROP_ETHERTYPE, ACT_DROP_UNREG = 0, 1, 2, 3
 ACT_BROADCAST, ACT_ARP_RESPOND = 4, 5
-ACT_MASK, ACT_F_FDIR = 0x7F, 0x80
+ACT_MASK, ACT_F_FDIR, ACT_F_TRANS = 0x3F, 0x80, 0x40
 NO_RUNTIME, NO_THREAD = 0xFFFF, 0xFF
 
 (RX_UNREGISTERED_MAC, RX_UNICAST_FAIL, RX_BROADCAST_FAIL, RX_FLOW_TAG_MATCH,
@@ -51,6 +51,7 @@ CALADAN_RSS_KEY = bytes([
     0x0D, 0x6D, 0x86, 0xBA, 0x61, 0x78, 0xEB])
 
 VERDICT_DTYPE = np.dtype([("hash", "<u4"), ("uniqid", "<u2"), ("thread", "u1"), ("action", "u1")])
+TRANS_DTYPE = np.dtype([("h5", "<u4"), ("h3", "<u4")])
 
 
 class GclCfg(ctypes.Structure):
@@ -73,6 +74,15 @@ class GclGenParams(ctypes.Structure):
                 ("rank", ctypes.c_uint32), ("world", ctypes.c_uint32),
                 ("shard_block", ctypes.c_uint64), ("zipf_cdf", ctypes.c_void_p),
                 ("nflows", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
+
+
+class GclOut(ctypes.Structure):
+    _fields_ = [("verdicts", ctypes.c_void_p), ("runtime_counts", ctypes.c_void_p),
+                ("stats", ctypes.c_void_p), ("trans", ctypes.c_void_p)]
+
+
+class GclTrans(ctypes.Structure):
+    _fields_ = [("h5", ctypes.c_uint32), ("h3", ctypes.c_uint32)]
 
 
 class GclE2eOpts(ctypes.Structure):
@@ -135,6 +145,10 @@ def _load():
         "gcl_runtime_del": (i32, [vp, u16]),
         "gcl_steer_flows": (i32, [u16, ctypes.POINTER(u16), u16, ctypes.POINTER(u16)]),
         "gcl_classify": (i32, [vp, ctypes.POINTER(GclBatch), vp, vp, vp, vp]),
+        "gcl_classify_ex": (i32, [vp, ctypes.POINTER(GclBatch), ctypes.POINTER(GclOut), vp]),
+        "gcl_runtime_set_trans_seed": (i32, [vp, u16, u32]),
+        "gcl_crc32c_u64": (u32, [u32, u64]),
+        "gcl_trans_hash": (None, [u32, ctypes.c_uint8, u32, u16, u32, u16, ctypes.POINTER(GclTrans)]),
         "gcl_sync": (i32, [vp]),
         "gcl_kernel_time": (i32, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64), i32]),
         "gcl_generate": (i32, [ctypes.POINTER(GclGenParams), vp, vp, vp, vp]),
@@ -197,6 +211,16 @@ def jenkins_hash(key: bytes) -> int:
 
 def toeplitz(key: bytes, data: bytes) -> int:
     return lib.gcl_toeplitz(key, len(key), data, len(data))
+
+
+def crc32c_u64(crc, val):
+    return lib.gcl_crc32c_u64(crc, val)
+
+
+def trans_hash(seed, proto, lip, lport, rip, rport):
+    t = GclTrans()
+    lib.gcl_trans_hash(seed, proto, lip, lport, rip, rport, ctypes.byref(t))
+    return t.h5, t.h3
 
 
 def runtime_ip(r: int) -> int:
@@ -299,9 +323,13 @@ class Classifier:
     def runtime_del(self, uniqid):
         return _check(lib.gcl_runtime_del(self._ctx, uniqid), "gcl_runtime_del")
 
+    def set_trans_seed(self, uniqid, seed):
+        return _check(lib.gcl_runtime_set_trans_seed(self._ctx, uniqid, seed),
+                      "gcl_runtime_set_trans_seed")
+
     def classify(self, frames, n, stride=0, verdicts=None, counts=None, stats=None, offs=None,
                  olflags=None, rss=None, fdir_hi=None, frames_len=None, stream=None,
-                 dst_hint=None):
+                 dst_hint=None, trans=None):
         """Launch the classify kernel on device buffers (asynchronous)."""
         if verdicts is not None and _nbytes(verdicts) < 8 * n:
             raise ValueError("verdict buffer too small")
@@ -316,8 +344,12 @@ class Classifier:
                      frames_len=_nbytes(frames) if frames_len is None else frames_len,
                      stride=stride, offs=_ptr(offs), olflags=_ptr(olflags), rss=_ptr(rss),
                      fdir_hi=_ptr(fdir_hi), pkt_len=None, n=n, dst_hint=_ptr(dst_hint))
-        return _check(lib.gcl_classify(self._ctx, ctypes.byref(b), _ptr(verdicts), _ptr(counts),
-                                       _ptr(stats), stream), "gcl_classify")
+        if trans is not None and _nbytes(trans) < 8 * n:
+            raise ValueError("trans buffer too small")
+        o = GclOut(verdicts=_ptr(verdicts), runtime_counts=_ptr(counts), stats=_ptr(stats),
+                   trans=_ptr(trans))
+        return _check(lib.gcl_classify_ex(self._ctx, ctypes.byref(b), ctypes.byref(o), stream),
+                      "gcl_classify_ex")
 
     def classify_host(self, frames, n, stride=0, verdicts=None, counts=None, stats=None,
                       olflags=None, rss=None, fdir_hi=None, offs=None, frames_len=None,

@@ -83,6 +83,8 @@ enum gcl_hash_mode {
                                    loopback hint does (runtime/net/core.c:524,
                                    iokernel/tx.c:81-83, inc/iokernel/queue.h:120-134) */
 #define GCL_CFG_PROFILE    0x4  /* record HIP events around every classify kernel */
+#define GCL_CFG_TRANS_HASH 0x8  /* also compute the destination runtime's transport
+                                   demux hashes (gcl_classify_ex, struct gcl_trans) */
 
 struct gcl_cfg {
 	uint32_t max_runtimes;    /* uniqids must be < max_runtimes (<= GCL_MAX_PROC) */
@@ -127,8 +129,9 @@ enum gcl_action {
 	GCL_ACT_BROADCAST = 4,     /* azure ARP reply, rx.c:171-190 (host fans out) */
 	GCL_ACT_ARP_RESPOND = 5,   /* azure ARP request miss, rx.c:200-203 (host) */
 };
-#define GCL_ACT_MASK    0x7F
+#define GCL_ACT_MASK    0x3F
 #define GCL_ACT_F_FDIR  0x80
+#define GCL_ACT_F_TRANS 0x40  /* struct gcl_trans of this packet is valid */
 #define GCL_NO_RUNTIME  0xFFFF
 #define GCL_NO_THREAD   0xFF
 
@@ -237,6 +240,45 @@ int gcl_classify_host(struct gcl_ctx *ctx, const struct gcl_batch *host_batch,
 /* Pin + map host memory for ZEROCOPY / async copies (hipHostRegister). */
 int gcl_host_register(void *p, size_t len);
 int gcl_host_unregister(void *p);
+
+/*
+ * Transport demux pre-hash (runtime/net/transport.c:29-42, :355-398).  For a
+ * packet delivered to runtime p that the runtime will hand to trans_lookup
+ * -- IPv4, version 4, IHL 5, the MF test of ip_hdr_supported as written
+ * (runtime/net/core.c:203-209: IP_MF applied to the network-order field),
+ * TCP or UDP -- the GPU computes, with p's trans_seed:
+ *   h5 = hash_crc32c_two(seed, laddr.ip | laddr.port << 32,
+ *                        raddr.ip | raddr.port << 32 | proto << 48)
+ *   h3 = hash_crc32c_one(seed, laddr.ip | laddr.port << 32 | proto << 48)
+ * with laddr = (daddr, dport), raddr = (saddr, sport) in host order, i.e.
+ * trans_hash_5tuple / trans_hash_3tuple; the runtime's table buckets are
+ * h % TRANS_TBL_SIZE.  GCL_ACT_F_TRANS marks valid entries.
+ */
+struct gcl_trans {
+	uint32_t h5;
+	uint32_t h3;
+};
+
+/* gcl_runtime_set_trans_seed - the runtime's trans_seed (transport.c:27,
+ * :459); needs GCL_CFG_TRANS_HASH.  -ENOENT if @uniqid is not present. */
+int gcl_runtime_set_trans_seed(struct gcl_ctx *ctx, uint16_t uniqid, uint32_t seed);
+
+/* All outputs of one classify launch (device pointers; NULL = not wanted). */
+struct gcl_out {
+	struct gcl_verdict *verdicts;    /* required */
+	uint64_t *runtime_counts;        /* accumulated */
+	uint64_t *stats;                 /* accumulated */
+	struct gcl_trans *trans;         /* GCL_CFG_TRANS_HASH only */
+};
+
+int gcl_classify_ex(struct gcl_ctx *ctx, const struct gcl_batch *b, const struct gcl_out *out,
+                    void *hip_stream);
+
+/* Host CRC32C step with the crc32q contract (no inversion, inc/asm/ops.h:77-80)
+ * and the two transport hashes, for the runtime side. */
+uint32_t gcl_crc32c_u64(uint32_t crc, uint64_t val);
+void gcl_trans_hash(uint32_t seed, uint8_t proto, uint32_t lip, uint16_t lport, uint32_t rip,
+                    uint16_t rport, struct gcl_trans *out);
 
 /* Synchronise the context's last stream. */
 int gcl_sync(struct gcl_ctx *ctx);

@@ -117,6 +117,25 @@ uint32_t orc_toeplitz_bytes(const uint8_t *key, size_t keylen,
 	return ret;
 }
 
+/*
+ * orc_crc32c_u64 - the crc32q instruction behind hash_crc32c_one/two
+ * (inc/base/hash.h:23-40, inc/asm/ops.h:77-80): CRC32C, reflected polynomial
+ * 0x82F63B78, over the 8 little-endian bytes of @val, no pre/post inversion.
+ * Bit-serial restatement; pinned against the reference's own inline
+ * functions compiled into oracle/_ref/libcrc_ref.so.
+ */
+uint32_t orc_crc32c_u64(uint32_t crc, uint64_t val)
+{
+	for (int bit = 0; bit < 64; bit++) {
+		uint32_t in = (uint32_t)(val >> bit) & 1u;
+		uint32_t fb = (crc ^ in) & 1u;
+		crc >>= 1;
+		if (fb)
+			crc ^= 0x82F63B78u;
+	}
+	return crc;
+}
+
 /* sched_steer_flows, iokernel/sched.c:122-147 */
 void orc_steer_flows(uint16_t thread_count, const uint16_t *active_idx,
                      uint16_t active_count, uint16_t *flow_tbl)
@@ -155,6 +174,7 @@ struct orc_tables {
 	uint8_t  default_olflags;
 	uint8_t  rss_key[40];
 	struct orc_runtime *rt;     /* [max_runtimes] = dp.clients_by_id */
+	uint32_t *trans_seed;       /* [max_runtimes] runtime trans_seed */
 	struct orc_bucket *bkt;
 	uint32_t nbkt_mask;
 };
@@ -183,6 +203,7 @@ struct orc_tables *orc_tables_new(uint32_t max_runtimes, uint32_t hash_mode,
 	if (rss_key40)
 		memcpy(t->rss_key, rss_key40, 40);
 	t->rt = calloc(max_runtimes, sizeof(*t->rt));
+	t->trans_seed = calloc(max_runtimes, sizeof(uint32_t));
 	while (nb * ORC_BKT < 2 * max_runtimes)
 		nb <<= 1;
 	t->bkt = malloc(nb * sizeof(*t->bkt));
@@ -202,6 +223,7 @@ void orc_tables_free(struct orc_tables *t)
 	if (!t)
 		return;
 	free(t->rt);
+	free(t->trans_seed);
 	free(t->bkt);
 	free(t);
 }
@@ -278,6 +300,8 @@ int orc_runtime_set(struct orc_tables *t, uint16_t uniqid, uint32_t ip,
 		if (ret)
 			return ret;
 	}
+	if (!r->present)
+		t->trans_seed[uniqid] = 0;
 	r->present = 1;
 	r->ip = ip;
 	r->thread_count = thread_count;
@@ -287,12 +311,21 @@ int orc_runtime_set(struct orc_tables *t, uint16_t uniqid, uint32_t ip,
 	return 0;
 }
 
+int orc_runtime_set_trans_seed(struct orc_tables *t, uint16_t uniqid, uint32_t seed)
+{
+	if (uniqid >= t->max_runtimes || !t->rt[uniqid].present)
+		return -ENOENT;
+	t->trans_seed[uniqid] = seed;
+	return 0;
+}
+
 int orc_runtime_del(struct orc_tables *t, uint16_t uniqid)
 {
 	if (uniqid >= t->max_runtimes || !t->rt[uniqid].present)
 		return -ENOENT;
 	iptab_del(t, t->rt[uniqid].ip);
 	memset(&t->rt[uniqid], 0, sizeof(t->rt[uniqid]));
+	t->trans_seed[uniqid] = 0;
 	return 0;
 }
 
@@ -356,9 +389,34 @@ static uint32_t flow_hash(const struct orc_tables *t, const struct pkt_view *pv)
  * rx_one_pkt, iokernel/rx.c:116-233, with rx_send_pkt_to_runtime (:76-92)
  * and rx_send_to_runtime (:50-73) reduced to the steering decision.
  */
+/*
+ * Transport demux hashes the destination runtime computes in trans_lookup
+ * (runtime/net/transport.c:29-42, :366-375) for the frames net_rx_one hands
+ * to net_rx_trans: IPv4, ip_hdr_supported as written (core.c:203-209, IP_MF
+ * tested on the network-order field), TCP or UDP.  L4 right after the
+ * 20-byte header (mbuf_pull_hdr of struct ip_hdr, core.c:272).
+ */
+static int orc_trans(const struct orc_tables *t, const struct pkt_view *pv, int p,
+                     struct gcl_trans *tr)
+{
+	uint8_t vihl = fb(pv, 14), proto = fb(pv, 23);
+	uint16_t off_raw = (uint16_t)(fb(pv, 20) | fb(pv, 21) << 8);
+	uint32_t seed = t->trans_seed[p];
+	uint64_t l, r;
+
+	if (fbe16(pv, 12) != GCL_ETHTYPE_IP || (vihl >> 4) != 4 || (vihl & 0xF) != 5 ||
+	    (off_raw & 0x2000) || (proto != 6 && proto != 17))
+		return 0;
+	l = (uint64_t)fbe32(pv, 30) | (uint64_t)fbe16(pv, 36) << 32;
+	r = (uint64_t)fbe32(pv, 26) | (uint64_t)fbe16(pv, 34) << 32 | (uint64_t)proto << 48;
+	tr->h5 = orc_crc32c_u64(orc_crc32c_u64(seed, l), r);
+	tr->h3 = orc_crc32c_u64(seed, l | (uint64_t)proto << 48);
+	return 1;
+}
+
 static void orc_rx_one_pkt(const struct orc_tables *t, const struct gcl_batch *b,
                            uint64_t i, struct gcl_verdict *v, uint64_t *counts,
-                           uint64_t *stats)
+                           uint64_t *stats, struct gcl_trans *tr)
 {
 	struct pkt_view pv;
 	uint8_t flags = b->olflags ? b->olflags[i] : t->default_olflags;
@@ -379,6 +437,8 @@ static void orc_rx_one_pkt(const struct orc_tables *t, const struct gcl_batch *b
 	v->hash = hash;
 	v->uniqid = GCL_NO_RUNTIME;
 	v->thread = GCL_NO_THREAD;
+	if (tr)
+		tr->h5 = tr->h3 = 0;
 
 	/* rx_loopback, rx.c:249-262: a tx dst_ip hint found in ip_to_proc sets
 	 * RTE_MBUF_F_RX_FDIR_ID with hash.fdir.hi = p->uniqid */
@@ -442,13 +502,15 @@ deliver:
 	} else {
 		v->action = (uint8_t)(GCL_ACT_WAKE | fdir); /* rx.c:62-72 */
 	}
+	if (tr && (t->flags & GCL_CFG_TRANS_HASH) && orc_trans(t, &pv, p, tr))
+		v->action |= GCL_ACT_F_TRANS;
 }
 
 #define RX_PREFETCH_STRIDE 2 /* rx.c:22 */
 
 static void classify_range(const struct orc_tables *t, const struct gcl_batch *b,
                            uint64_t lo, uint64_t hi, struct gcl_verdict *v,
-                           uint64_t *counts, uint64_t *stats)
+                           uint64_t *counts, uint64_t *stats, struct gcl_trans *tr)
 {
 	/* rx_burst, rx.c:270-290: bursts of IOKERNEL_RX_BURST_SIZE */
 	for (uint64_t s = lo; s < hi; s += GCL_RX_BURST_SIZE) {
@@ -461,7 +523,8 @@ static void classify_range(const struct orc_tables *t, const struct gcl_batch *b
 				if (off < b->frames_len)
 					__builtin_prefetch(b->frames + off);
 			}
-			orc_rx_one_pkt(t, b, s + i, &v[s + i - lo], counts, stats);
+			orc_rx_one_pkt(t, b, s + i, &v[s + i - lo], counts, stats,
+			               tr ? &tr[s + i - lo] : NULL);
 		}
 	}
 }
@@ -469,7 +532,14 @@ static void classify_range(const struct orc_tables *t, const struct gcl_batch *b
 void orc_classify(const struct orc_tables *t, const struct gcl_batch *b,
                   struct gcl_verdict *v, uint64_t *counts, uint64_t *stats)
 {
-	classify_range(t, b, 0, b->n, v, counts, stats);
+	classify_range(t, b, 0, b->n, v, counts, stats, NULL);
+}
+
+void orc_classify_ex(const struct orc_tables *t, const struct gcl_batch *b,
+                     struct gcl_verdict *v, uint64_t *counts, uint64_t *stats,
+                     struct gcl_trans *tr)
+{
+	classify_range(t, b, 0, b->n, v, counts, stats, tr);
 }
 
 /* lrpc ring, inc/base/lrpc.h:15-63 (16-B messages, parity in bit 63) */
@@ -525,7 +595,7 @@ static void classify_range_lrpc(const struct orc_tables *t, const struct gcl_bat
 				if (off < b->frames_len)
 					__builtin_prefetch(b->frames + off);
 			}
-			orc_rx_one_pkt(t, b, k, vk, counts, stats);
+			orc_rx_one_pkt(t, b, k, vk, counts, stats, NULL);
 			if ((vk->action & GCL_ACT_MASK) == GCL_ACT_DELIVER) {
 				/* rx_make_cmd, rx.c:24-38 */
 				uint8_t fl = b->olflags ? b->olflags[k] : t->default_olflags;
@@ -610,7 +680,7 @@ static void *bench_thread(void *arg)
 		if (a->with_lrpc)
 			classify_range_lrpc(a->t, a->b, a->lo, a->hi, v, counts, stats, &rs);
 		else
-			classify_range(a->t, a->b, a->lo, a->hi, v, counts, stats);
+			classify_range(a->t, a->b, a->lo, a->hi, v, counts, stats, NULL);
 	}
 	pthread_barrier_wait(a->bar);
 	if (a->with_lrpc)

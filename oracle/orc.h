@@ -12,6 +12,8 @@
  *   orc_steer_flows   iokernel/sched.c:122-147
  *   orc_rx_burst      iokernel/rx.c:270-290 (bursts of 64, prefetch stride 2)
  *   orc_rx_one_pkt    iokernel/rx.c:116-233 (+ rx_send_to_runtime :50-73)
+ *   orc_crc32c_u64    crc32q, inc/asm/ops.h:77-80 (hash_crc32c_one/two)
+ *   orc_trans         trans_hash_5tuple/3tuple, runtime/net/transport.c:29-42
  *   orc_iptab_*       the ip_to_proc rte_hash (iokernel/dp_clients.c:349-363),
  *                     keyed by jhash of the 4-byte host-order IP like rte_jhash
  *
@@ -41,6 +43,7 @@ uint32_t orc_do_toeplitz(const uint8_t *key, uint32_t saddr, uint32_t daddr,
 /* generic Toeplitz over a byte string (MSB-first), for the KAT vectors */
 uint32_t orc_toeplitz_bytes(const uint8_t *key, size_t keylen,
                             const uint8_t *in, size_t len);
+uint32_t orc_crc32c_u64(uint32_t crc, uint64_t val);
 void orc_steer_flows(uint16_t thread_count, const uint16_t *active_idx,
                      uint16_t active_count, uint16_t *flow_tbl);
 
@@ -63,11 +66,18 @@ int orc_runtime_set(struct orc_tables *t, uint16_t uniqid, uint32_t ip,
                     uint16_t thread_count, uint16_t active,
                     const uint16_t *flow_tbl);
 int orc_runtime_del(struct orc_tables *t, uint16_t uniqid);
+int orc_runtime_set_trans_seed(struct orc_tables *t, uint16_t uniqid, uint32_t seed);
 
 /* Classify a host batch (gcl_batch with host pointers), accumulating counts
  * and stats.  Processes bursts of 64 with the rx.c prefetch stride. */
 void orc_classify(const struct orc_tables *t, const struct gcl_batch *b,
                   struct gcl_verdict *v, uint64_t *counts, uint64_t *stats);
+
+/* Same, plus the runtime-side transport demux hashes when the tables were
+ * created with GCL_CFG_TRANS_HASH (trans may be NULL). */
+void orc_classify_ex(const struct orc_tables *t, const struct gcl_batch *b,
+                     struct gcl_verdict *v, uint64_t *counts, uint64_t *stats,
+                     struct gcl_trans *tr);
 
 /* Same, plus lrpc_send of a 16-B message per delivered packet into
  * 4096-deep per-(runtime, thread) rings that are drained after every burst

@@ -13,6 +13,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "build", "liborc.so")
 LIB_NATIVE = os.path.join(HERE, "build", "liborc_native.so")
 REF_JHASH = os.path.join(HERE, "_ref", "libjhash_ref.so")
+REF_CRC = os.path.join(HERE, "_ref", "libcrc_ref.so")
+TRANS_DTYPE = np.dtype([("h5", "<u4"), ("h3", "<u4")])
 
 NR_STATS = 8
 
@@ -59,6 +61,9 @@ def _bind(path):
         "orc_runtime_del": (i32, [vp, u16]),
         "orc_classify": (None, [vp, ctypes.POINTER(Batch), vp, vp, vp]),
         "orc_classify_lrpc": (None, [vp, ctypes.POINTER(Batch), vp, vp, vp]),
+        "orc_classify_ex": (None, [vp, ctypes.POINTER(Batch), vp, vp, vp, vp]),
+        "orc_crc32c_u64": (u32, [u32, u64]),
+        "orc_runtime_set_trans_seed": (i32, [vp, u16, u32]),
         "orc_bench": (ctypes.c_double, [vp, ctypes.POINTER(Batch), i32, i32, i32]),
         "orc_generate": (i32, [ctypes.POINTER(GenParams), vp, vp, vp, vp]),
         "orc_runtime_ip": (u32, [u32]),
@@ -91,6 +96,22 @@ def ref_jhash():
     l.jenkins_hash.restype = ctypes.c_uint32
     l.jenkins_hash.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
     return l
+
+
+def ref_crc():
+    """The reference's hash_crc32c_one/two (oracle/_ref/libcrc_ref.so), or None."""
+    if not os.path.exists(REF_CRC):
+        return None
+    l = ctypes.CDLL(REF_CRC)
+    l.ref_crc32c_one.restype = ctypes.c_uint32
+    l.ref_crc32c_one.argtypes = [ctypes.c_uint32, ctypes.c_uint64]
+    l.ref_crc32c_two.restype = ctypes.c_uint32
+    l.ref_crc32c_two.argtypes = [ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64]
+    return l
+
+
+def crc32c_u64(crc, val):
+    return lib().orc_crc32c_u64(crc, val)
 
 
 def jhash(key: bytes) -> int:
@@ -153,6 +174,9 @@ class Tables:
     def runtime_del(self, uniqid):
         return self._lib.orc_runtime_del(self.h, uniqid)
 
+    def set_trans_seed(self, uniqid, seed):
+        return self._lib.orc_runtime_set_trans_seed(self.h, uniqid, seed)
+
     def _batch(self, frames, n, stride, offs, olflags, rss, fdir_hi, pkt_len, frames_len,
                dst_hint=None):
         self._keep = [frames, offs, olflags, rss, fdir_hi, pkt_len, dst_hint]
@@ -161,13 +185,19 @@ class Tables:
                      fdir_hi=_p(fdir_hi), pkt_len=_p(pkt_len), n=n, dst_hint=_p(dst_hint))
 
     def classify(self, frames, n, stride=0, offs=None, olflags=None, rss=None, fdir_hi=None,
-                 pkt_len=None, frames_len=None, lrpc=False, dst_hint=None):
-        """Returns (verdicts structured array, counts u64[R], stats u64[8])."""
+                 pkt_len=None, frames_len=None, lrpc=False, dst_hint=None, trans=False):
+        """Returns (verdicts structured array, counts u64[R], stats u64[8])
+        [+ trans (h5, h3) array when trans=True]."""
         b = self._batch(frames, n, stride, offs, olflags, rss, fdir_hi, pkt_len, frames_len,
                         dst_hint)
         v = np.zeros(n, dtype=VERDICT_DTYPE)
         counts = np.zeros(self.max_runtimes, dtype=np.uint64)
         stats = np.zeros(NR_STATS, dtype=np.uint64)
+        if trans:
+            tr = np.zeros(n, dtype=TRANS_DTYPE)
+            self._lib.orc_classify_ex(self.h, ctypes.byref(b), v.ctypes.data, counts.ctypes.data,
+                                      stats.ctypes.data, tr.ctypes.data)
+            return v, counts, stats, tr
         fn = self._lib.orc_classify_lrpc if lrpc else self._lib.orc_classify
         fn(self.h, ctypes.byref(b), v.ctypes.data, counts.ctypes.data, stats.ctypes.data)
         return v, counts, stats

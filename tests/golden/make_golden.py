@@ -29,6 +29,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 REF_SO = os.path.join(ROOT, "oracle", "_ref", "libjhash_ref.so")
+REF_CRC_SO = os.path.join(ROOT, "oracle", "_ref", "libcrc_ref.so")
 
 MS_KEY = bytes.fromhex("6d5a56da255b0ec24167253d43a38fb0d0ca2bcbae7b30b477cb2da38030f20c"
                        "6a42b73bbeac01fa")
@@ -56,6 +57,26 @@ def ref_lib():
 
 
 REF = None
+CRC = None
+
+
+def ref_crc_lib():
+    if not os.path.exists(REF_CRC_SO):
+        sys.exit(f"{REF_CRC_SO} missing: run `make -C oracle` with /root/reference mounted")
+    lib = ctypes.CDLL(REF_CRC_SO)
+    lib.ref_crc32c_one.restype = ctypes.c_uint32
+    lib.ref_crc32c_one.argtypes = [ctypes.c_uint32, ctypes.c_uint64]
+    lib.ref_crc32c_two.restype = ctypes.c_uint32
+    lib.ref_crc32c_two.argtypes = [ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64]
+    return lib
+
+
+def ref_trans(seed, proto, lip, lport, rip, rport):
+    """trans_hash_5tuple / _3tuple (transport.c:29-42) via the reference's
+    own hash_crc32c_two / _one."""
+    l = lip | lport << 32
+    return (CRC.ref_crc32c_two(seed, l, rip | rport << 32 | proto << 48),
+            CRC.ref_crc32c_one(seed, l | proto << 48))
 
 
 def ref_jhash(key: bytes, align=0) -> int:
@@ -117,14 +138,17 @@ def steer(uniq, h):
     return FLOW[uniq][h % TC[uniq]], DELIVER
 
 
-def pkt(cite, frame, flags, rss, fdir, hash_, uniq, action, thread=None, hint=0, hint_hit=False):
+def pkt(cite, frame, flags, rss, fdir, hash_, uniq, action, thread=None, hint=0, hint_hit=False,
+        trans=None):
     if uniq is None:
         uniq, thread = 0xFFFF, 0xFF
     elif thread is None:
         thread, act = steer(uniq, hash_)
         action |= act
+    if trans is not None:
+        action |= 0x40  # GCL_ACT_F_TRANS
     return {"cite": cite, "frame": frame.hex(), "olflags": flags, "rss": rss, "fdir_hi": fdir,
-            "dst_hint": hint, "hint_hit": hint_hit,
+            "dst_hint": hint, "hint_hit": hint_hit, "expect_trans": list(trans or (0, 0)),
             "expect": {"hash": hash_, "uniqid": uniq, "thread": thread, "action": action}}
 
 
@@ -239,6 +263,61 @@ def loopback_set():
     }
 
 
+SEEDS = {3: 0x12345678, 7: 0xCAFEBABE, 9: 0x0BADF00D}
+
+
+def trans_set():
+    """Runtime-side demux pre-hash (gclassify.h struct gcl_trans): for a packet
+    delivered to runtime p, trans_hash_5tuple/_3tuple with p's trans_seed,
+    when net_rx_one would pass it to net_rx_trans (core.c:203-209, :288-290)."""
+    P = []
+    sa, sp, dp = ip("192.168.7.9"), 51000, 443
+    P.append(pkt("transport.c:29-42: UDP to A, laddr=(daddr,dport) raddr=(saddr,sport)",
+                 eth(0x0800) + ipv4(sa, A_IP, 17, l4(sp, dp)), F_RSS | CK_GOOD, 0x99, 0,
+                 0x99, 3, DELIVER, trans=ref_trans(SEEDS[3], 17, A_IP, dp, sa, sp)))
+    P.append(pkt("TCP to B with B's seed",
+                 eth(0x0800) + ipv4(sa, B_IP, 6, l4(sp, 80, True)), F_RSS, 0x5, 0, 0x5, 7, DELIVER,
+                 trans=ref_trans(SEEDS[7], 6, B_IP, 80, sa, sp)))
+    P.append(pkt("wake path still names the runtime: C's seed",
+                 eth(0x0800) + ipv4(sa, C_IP, 17, l4(7, 9)), F_RSS, 0x6, 0, 0x6, 9, 0,
+                 trans=ref_trans(SEEDS[9], 17, C_IP, 9, sa, 7)))
+    P.append(pkt("core.c:207: IP options (IHL 6) are dropped by the runtime: no pre-hash",
+                 eth(0x0800) + ipv4(sa, A_IP, 17, l4(sp, dp), ihl=6), F_RSS, 0x7, 0, 0x7, 3, DELIVER))
+    P.append(pkt("core.c:206: version 6 in an IPv4 frame: no pre-hash",
+                 eth(0x0800) + ipv4(sa, A_IP, 17, l4(sp, dp), version=6), F_RSS, 0x8, 0, 0x8, 3, DELIVER))
+    P.append(pkt("core.c:208 as written: IP_MF tested on the network-order field, so a real MF "
+                 "fragment (0x2000 BE) passes",
+                 eth(0x0800) + ipv4(sa, A_IP, 17, l4(sp, dp), frag=0x2000), F_RSS, 0x9, 0, 0x9, 3,
+                 DELIVER, trans=ref_trans(SEEDS[3], 17, A_IP, dp, sa, sp)))
+    P.append(pkt("core.c:208 as written: offset 0x0020 sets the tested bit: no pre-hash",
+                 eth(0x0800) + ipv4(sa, A_IP, 17, l4(sp, dp), frag=0x0020), F_RSS, 0xA, 0, 0xA, 3,
+                 DELIVER))
+    P.append(pkt("core.c:293-299: ICMP goes to net_rx_icmp: no pre-hash",
+                 eth(0x0800) + ipv4(sa, A_IP, 1, b"\x08" + b"\0" * 7), F_RSS, 0xB, 0, 0xB, 3, DELIVER))
+    P.append(pkt("unregistered IP: no runtime, no pre-hash",
+                 eth(0x0800) + ipv4(sa, ip("10.9.9.9"), 17, l4(sp, dp)), F_RSS, 0xC, 0, 0xC, None,
+                 DROP_UNREG))
+    P.append(pkt("FDIR delivery of an ARP frame: not IPv4, no pre-hash",
+                 eth(0x0806) + arp(1, sa, A_IP), F_FDIR | F_RSS, 0xD, 3, 0xD, 3, FDIR))
+    return {
+        "name": "trans_demux",
+        "cfg": {"max_runtimes": 16, "hash_mode": 0, "flags": 8, "default_olflags": 0,
+                "rss_key": MS_KEY.hex()},
+        "trans_seeds": {str(k): v for k, v in SEEDS.items()},
+        "packets": P,
+    }
+
+
+def crc_kats():
+    rnd = random.Random(0xC5C)
+    out = []
+    for _ in range(400):
+        seed, a, b = rnd.getrandbits(32), rnd.getrandbits(64), rnd.getrandbits(64)
+        out.append({"seed": seed, "a": a, "b": b, "one": CRC.ref_crc32c_one(seed, a),
+                    "two": CRC.ref_crc32c_two(seed, a, b)})
+    return out
+
+
 def jenkins_set():
     P = []
     cases = [
@@ -309,7 +388,7 @@ def expected_stats(s):
     fl_set = s["cfg"]["flags"]
     for p in s["packets"]:
         e = p["expect"]
-        act = e["action"] & 0x7F
+        act = e["action"] & 0x3F
         fl = p["olflags"]
         st[6] += 1  # RX_PULLED
         if fl & F_FDIR or p.get("hint_hit"):
@@ -330,7 +409,7 @@ def expected_counts(s):
     counts = [0] * s["cfg"]["max_runtimes"]
     for p in s["packets"]:
         e = p["expect"]
-        if e["action"] & 0x7F in (DELIVER, WAKE):
+        if e["action"] & 0x3F in (DELIVER, WAKE):
             counts[e["uniqid"]] += 1
     return counts
 
@@ -355,8 +434,12 @@ def jhash_kats():
 
 
 def main():
-    global REF
+    global REF, CRC
     REF = ref_lib()
+    CRC = ref_crc_lib()
+    with open(os.path.join(HERE, "crc32c_kat.json"), "w") as f:
+        json.dump({"source": "reference hash_crc32c_one/two (inc/base/hash.h) via oracle/_ref/libcrc_ref.so",
+                   "vectors": crc_kats()}, f, indent=0)
     assert ref_jhash(b"") == 0xdeadbeef
     assert ref_jhash(b"Four score and seven years ago") == 0x17770551
     with open(os.path.join(HERE, "jhash_kat.json"), "w") as f:
@@ -367,8 +450,8 @@ def main():
                    "vectors": [{"dst": d, "dport": dp, "src": s, "sport": sp, "ipv4": h4,
                                 "ipv4_tcp": h4t} for d, dp, s, sp, h4, h4t in MS_VECTORS]},
                   f, indent=1)
-    sets = [nic_set(), azure_set(), loopback_set(), jenkins_set(), toeplitz_set(False),
-            toeplitz_set(True)]
+    sets = [nic_set(), azure_set(), loopback_set(), trans_set(), jenkins_set(),
+            toeplitz_set(False), toeplitz_set(True)]
     for s in sets:
         s["runtimes"] = RUNTIMES + s.pop("extra_runtimes", [])
         s["expect_stats"] = expected_stats(s)

@@ -41,6 +41,21 @@ def scenario_batch(s, slot=128):
     return frames, olflags, rss, fdir, exp, (hint if hint.any() else None)
 
 
+def scenario_trans(s):
+    """Expected (h5, h3) per packet of a set, or None if the set has no seeds."""
+    if "trans_seeds" not in s:
+        return None
+    t = np.zeros(len(s["packets"]), dtype=[("h5", "<u4"), ("h3", "<u4")])
+    for i, p in enumerate(s["packets"]):
+        t[i] = tuple(p["expect_trans"])
+    return t
+
+
+def apply_seeds(target, s):
+    for u, seed in s.get("trans_seeds", {}).items():
+        assert target.set_trans_seed(int(u), seed) in (0, None)
+
+
 def apply_runtimes(target, runtimes):
     """target: oracle Tables or gclassify.Classifier (same runtime_set API)."""
     for r in runtimes:

@@ -209,7 +209,7 @@ def test_host_deliver_matches_reference_model(g, orc):
     exp_fail = exp_unh = exp_deliv = 0
     exp_freed = []
     for i in range(n):
-        act = v[i]["action"] & 0x7F
+        act = v[i]["action"] & 0x3F
         if act in (0, 1):
             u = int(v[i]["uniqid"])
             if act == 0:

@@ -3,7 +3,8 @@ golden fixtures.  Bit-exact on every verdict, count and counter."""
 import numpy as np
 import pytest
 
-from tests.rxcases import apply_runtimes, fuzz_batch, random_runtimes, scenario_batch, scenario_sets
+from tests.rxcases import (apply_runtimes, apply_seeds, fuzz_batch, random_runtimes, scenario_batch,
+                           scenario_sets, scenario_trans)
 
 pytestmark = pytest.mark.gpu
 
@@ -23,20 +24,24 @@ def dev(a):
 
 
 def gpu_run(g, clf, frames, n, stride=0, offs=None, olflags=None, rss=None, fdir=None,
-            frames_len=None, counts=None, stats=None, hint=None):
+            frames_len=None, counts=None, stats=None, hint=None, trans=False):
     f = dev(frames.view(np.uint8))
     v = torch.zeros(n * 8, dtype=torch.uint8, device="cuda")
     c = counts if counts is not None else torch.zeros(clf.max_runtimes, dtype=torch.int64, device="cuda")
     s = stats if stats is not None else torch.zeros(g.NR_STATS, dtype=torch.int64, device="cuda")
     o = dev(offs.astype(np.int64)) if offs is not None else None
-    clf.classify(f, n, stride, verdicts=v, counts=c, stats=s, offs=o, olflags=dev(olflags),
+    tr = torch.zeros(n * 8, dtype=torch.uint8, device="cuda") if trans else None
+    clf.classify(f, n, stride, verdicts=v, counts=c, stats=s, offs=o, olflags=dev(olflags), trans=tr,
                  rss=dev(rss.view(np.int32)) if rss is not None else None,
                  fdir_hi=dev(fdir.astype(np.int32)) if fdir is not None else None,
                  frames_len=frames_len,
                  dst_hint=dev(hint.view(np.int32)) if hint is not None else None)
     torch.cuda.synchronize()
-    return (v.cpu().numpy().view(g.VERDICT_DTYPE), c.cpu().numpy().astype(np.uint64),
-            s.cpu().numpy().astype(np.uint64))
+    res = (v.cpu().numpy().view(g.VERDICT_DTYPE), c.cpu().numpy().astype(np.uint64),
+           s.cpu().numpy().astype(np.uint64))
+    if trans:
+        res += (tr.cpu().numpy().view(g.TRANS_DTYPE),)
+    return res
 
 
 def assert_same(v, ve, what=""):
@@ -55,9 +60,14 @@ def test_gpu_scenarios(g, s):
     clf = g.Classifier(0, cfg["max_runtimes"], cfg["hash_mode"], cfg["flags"], cfg["default_olflags"],
                        bytes.fromhex(cfg["rss_key"]))
     apply_runtimes(clf, s["runtimes"])
+    apply_seeds(clf, s)
     frames, olflags, rss, fdir, exp, hint = scenario_batch(s)
-    v, c, st = gpu_run(g, clf, frames, len(exp), 128, olflags=olflags, rss=rss, fdir=fdir,
-                       hint=hint)
+    want_tr = scenario_trans(s)
+    out = gpu_run(g, clf, frames, len(exp), 128, olflags=olflags, rss=rss, fdir=fdir,
+                  hint=hint, trans=want_tr is not None)
+    v, c, st = out[:3]
+    if want_tr is not None:
+        assert (out[3] == want_tr).all(), (out[3], want_tr)
     for i in range(len(exp)):
         assert tuple(v[i]) == tuple(exp[i]), (s["packets"][i]["cite"], v[i], exp[i])
     assert list(st) == s["expect_stats"]
@@ -75,14 +85,25 @@ def test_gpu_fuzz_vs_oracle(g, orc, mode, flags, max_rt):
     if flags == 2:
         hint = None  # keep one arm without the loopback feed
     key = bytes(rng.integers(0, 256, size=40, dtype=np.uint8))
-    t = orc.Tables(max_rt, mode, flags, 0x09, key)
+    cflags = flags | (g.CFG_TRANS_HASH if flags != 1 else 0)
+    t = orc.Tables(max_rt, mode, cflags, 0x09, key)
     apply_runtimes(t, rts)
-    ve, ce, se = t.classify(frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir_hi=fdir, frames_len=flen,
-                            dst_hint=hint)
-    clf = g.Classifier(0, max_rt, mode, flags, 0x09, key)
+    clf = g.Classifier(0, max_rt, mode, cflags, 0x09, key)
     apply_runtimes(clf, rts)
-    v, c, st = gpu_run(g, clf, frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir=fdir, frames_len=flen,
-                       hint=hint)
+    want_tr = cflags & g.CFG_TRANS_HASH
+    if want_tr:
+        for r in rts:
+            seed = int(rng.integers(0, 2**32))
+            t.set_trans_seed(r["uniqid"], seed)
+            clf.set_trans_seed(r["uniqid"], seed)
+    oe = t.classify(frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir_hi=fdir, frames_len=flen,
+                    dst_hint=hint, trans=bool(want_tr))
+    og = gpu_run(g, clf, frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir=fdir, frames_len=flen,
+                 hint=hint, trans=bool(want_tr))
+    ve, ce, se = oe[:3]
+    v, c, st = og[:3]
+    if want_tr:
+        assert (og[3] == oe[3]).all(), "trans hashes differ"
     assert_same(v, ve, f"mode={mode} flags={flags} R={max_rt}")
     assert (c == ce).all()
     assert (st == se).all(), (st, se)
@@ -249,7 +270,7 @@ def test_gpu_full_size_properties(g, orc):
     ss = s.cpu().numpy()
     assert cc.sum() == n and ss[g.RX_PULLED] == n and ss[g.RX_UNHANDLED] == 0
     assert (np.bincount(vv["uniqid"], minlength=R)[:R] == cc).all()
-    assert ((vv["action"] & 0x7F) == 0).all()
+    assert ((vv["action"] & 0x3F) == 0).all()
     sample = np.sort(rng.choice(n, size=65536, replace=False))
     fr = frames.view(n, stride)[torch.from_numpy(sample).cuda()].cpu().numpy().reshape(-1)
     ve, _, _ = t.classify(fr, len(sample), stride)

@@ -2,7 +2,7 @@
 import numpy as np
 import pytest
 
-from tests.rxcases import apply_runtimes, scenario_batch, scenario_sets
+from tests.rxcases import apply_runtimes, apply_seeds, scenario_batch, scenario_sets, scenario_trans
 
 SETS = scenario_sets()
 
@@ -13,10 +13,15 @@ def test_oracle_matches_scenarios(orc, s):
     t = orc.Tables(cfg["max_runtimes"], cfg["hash_mode"], cfg["flags"], cfg["default_olflags"],
                    bytes.fromhex(cfg["rss_key"]))
     apply_runtimes(t, s["runtimes"])
+    apply_seeds(t, s)
     frames, olflags, rss, fdir, exp, hint = scenario_batch(s)
     n = len(exp)
-    v, counts, stats = t.classify(frames, n, 128, olflags=olflags, rss=rss, fdir_hi=fdir,
-                                  dst_hint=hint)
+    want_tr = scenario_trans(s)
+    out = t.classify(frames, n, 128, olflags=olflags, rss=rss, fdir_hi=fdir, dst_hint=hint,
+                     trans=want_tr is not None)
+    v, counts, stats = out[:3]
+    if want_tr is not None:
+        assert (out[3] == want_tr).all(), (out[3], want_tr)
     for i in range(n):
         assert tuple(v[i]) == tuple(exp[i]), (s["packets"][i]["cite"], v[i], exp[i])
     assert list(stats) == s["expect_stats"]
@@ -56,3 +61,20 @@ def test_oracle_lrpc_variant_matches(orc):
     v2, c2, s2 = t.classify(frames, 4096, 64, lrpc=True)
     assert (v1 == v2).all() and (c1 == c2).all()
     assert s1[6] == s2[6] == 4096 and s2[1] == 0
+
+
+def test_crc32c_golden_from_reference(orc):
+    """crc32c_kat.json: values of the reference's hash_crc32c_one/two."""
+    from caladan_amd import gclassify as g
+    from tests.rxcases import load_json
+    for v in load_json("crc32c_kat.json")["vectors"]:
+        assert orc.crc32c_u64(v["seed"], v["a"]) == v["one"]
+        assert orc.crc32c_u64(orc.crc32c_u64(v["seed"], v["a"]), v["b"]) == v["two"]
+        assert g.crc32c_u64(v["seed"], v["a"]) == v["one"]
+    ref = orc.ref_crc()
+    if ref is not None:
+        import random
+        rnd = random.Random(1)
+        for _ in range(5000):
+            s, a = rnd.getrandbits(32), rnd.getrandbits(64)
+            assert ref.ref_crc32c_one(s, a) == orc.crc32c_u64(s, a)
