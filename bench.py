@@ -244,7 +244,51 @@ def e2e_bench(device, reps=3):
         out[name] = res
         del dfr, hfr, hv, dv, clf
         torch.cuda.empty_cache()
+    out["mixed"]["trace_replay"] = trace_replay(device)
     return out
+
+
+def trace_replay(device, n=64 << 10, reps=3):
+    """Config 5's ingest path: the mixed jumbo stream written as a pcap trace,
+    loaded by gcl_pcap_load into host memory, registered, and classified by
+    the kernel over PCIe (ZEROCOPY, frames at arbitrary 16-B offsets)."""
+    import tempfile
+    wl, _, stride, R, T, _ = WORKLOADS["mixed"]
+    dfr = torch.zeros(n * stride, dtype=torch.uint8, device=device)
+    dpl = torch.zeros(n, dtype=torch.int16, device=device)
+    dfl = torch.zeros(n, dtype=torch.uint8, device=device)
+    g.generate(wl, n, stride, R, dfr, olflags=dfl, seed=SEED, pkt_len=dpl)
+    frames = dfr.cpu().numpy()
+    pl = dpl.cpu().numpy().view(np.uint16)
+    olf = np.ascontiguousarray(dfl.cpu().numpy())
+    del dfr
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "mixed.pcap")
+        g.pcap_write(path, frames, pl, stride=stride)
+        fsize = os.path.getsize(path)
+        t0 = time.perf_counter()
+        tr = g.Trace(path)
+        load_s = time.perf_counter() - t0
+    clf = g.Classifier(device.index or 0, R, g.HASH_JENKINS)
+    setup_tables(clf, R, T)
+    hv = np.zeros(n, dtype=g.VERDICT_DTYPE)
+    regs = (tr.frames, tr.offs, olf, hv)
+    for a in regs:
+        g.host_register(a)
+    try:
+        kw = dict(verdicts=hv, offs=tr.offs, olflags=olf, frames_len=tr.frames_len,
+                  mode=g.E2E_ZEROCOPY)
+        clf.classify_host(tr.frames, n, 0, **kw)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            clf.classify_host(tr.frames, n, 0, **kw)
+        dt = (time.perf_counter() - t0) / reps
+    finally:
+        for a in regs:
+            g.host_unregister(a)
+    return {"pkts": n, "pcap_bytes": fsize, "pcap_load_s": round(load_s, 3),
+            "zerocopy_mpps": round(n / dt / 1e6, 1),
+            "wire_bytes_rate_GBs": round(float(pl.astype(np.float64).sum()) / dt / 1e9, 1)}
 
 
 def cpu_baseline(budget_s=12.0):

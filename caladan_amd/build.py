@@ -19,8 +19,9 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("GCL_OFFLOAD_ARCH", "gfx950")
 
 SOURCES_HIP = ["gclassify.hip"]
-SOURCES_C = ["gcl_host.c"]
-DEPS = ["gcl_device.h", "../../include/gclassify.h", "../../include/gcl_host.h"]
+SOURCES_C = ["gcl_host.c", "gcl_pcap.c"]
+DEPS = ["gcl_device.h", "../../include/gclassify.h", "../../include/gcl_host.h",
+        "../../include/gcl_pcap.h"]
 
 
 def _run(cmd):

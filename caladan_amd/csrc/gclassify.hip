@@ -491,6 +491,7 @@ struct GParams {
 	uint8_t *frames;
 	uint8_t *olflags;
 	uint32_t *rss;
+	uint16_t *pkt_len;
 };
 
 __device__ __forceinline__ uint32_t runtime_ip(uint32_t r) { return 0x0A000000u + r + 1; }
@@ -505,6 +506,7 @@ __global__ void __launch_bounds__(256) generate_kernel(GParams p)
 		g = ((j / p.shard_block) * p.world + p.rank) * p.shard_block + j % p.shard_block;
 	const uint64_t r0 = gcl::rw(p.seed, g, 0), r1 = gcl::rw(p.seed, g, 1);
 	uint32_t fl = GCL_F_RSS_HASH | GCL_F_IP_CKSUM_GOOD;
+	uint32_t len = 64;
 	Hdr h;
 #pragma unroll
 	for (int i = 0; i < 16; i++)
@@ -537,6 +539,7 @@ __global__ void __launch_bounds__(256) generate_kernel(GParams p)
 		h.b8(46, 0x50);
 		h.b8(47, 0x10);
 		h.b16(48, 0xFFFF);
+		len = 1500;
 	} else {
 		const uint64_t r2 = gcl::rw(p.seed, g, 2);
 		const uint32_t kind = (uint32_t)r0 % 100;
@@ -544,7 +547,7 @@ __global__ void __launch_bounds__(256) generate_kernel(GParams p)
 		bool unreg = (uint32_t)(r0 >> 40) % 20 == 0;
 		uint32_t dst = unreg ? (0xC0A80000u | (uint32_t)(r1 >> 48)) : runtime_ip(rt);
 		if (kind < 70) {
-			uint32_t len = 64 + (uint32_t)(r1 >> 32) % (9014 - 64 + 1);
+			len = 64 + (uint32_t)(r1 >> 32) % (9014 - 64 + 1);
 			uint32_t proto = (r0 >> 32) & 1 ? 6 : 17;
 			gen_eth(h, r2 >> 8, GCL_ETHTYPE_IP);
 			gen_ipv4(h, len - 14, (uint32_t)r2 & 0xFFFF, proto, (uint32_t)r2, dst);
@@ -559,6 +562,8 @@ __global__ void __launch_bounds__(256) generate_kernel(GParams p)
 			h.b32(22, (uint32_t)r2);
 			h.b32(38, dst);
 			fl = 0;
+			len = 54 + ((uint32_t)(r1 >> 32) & 0x1FFF);
+			len = len < 60 ? 60 : len;
 		} else {
 			unreg = (uint32_t)(r0 >> 40) % 10 == 0;
 			dst = unreg ? (0xC0A80000u | (uint32_t)(r1 >> 48)) : runtime_ip(rt);
@@ -572,6 +577,7 @@ __global__ void __launch_bounds__(256) generate_kernel(GParams p)
 			h.b32(28, (uint32_t)r2);
 			h.b32(38, dst);
 			fl = 0;
+			len = 60;
 		}
 	}
 	uint4 *dst4 = (uint4 *)(p.frames + j * p.stride);
@@ -582,6 +588,8 @@ __global__ void __launch_bounds__(256) generate_kernel(GParams p)
 		p.olflags[j] = (uint8_t)fl;
 	if (p.rss)
 		p.rss[j] = (uint32_t)gcl::rw(p.seed, g, 3);
+	if (p.pkt_len)
+		p.pkt_len[j] = (uint16_t)len;
 }
 
 } // namespace
@@ -1186,6 +1194,7 @@ extern "C" int gcl_generate(const struct gcl_gen_params *p, uint8_t *frames, uin
 	g.frames = frames;
 	g.olflags = olflags;
 	g.rss = rss;
+	g.pkt_len = p->pkt_len;
 	uint64_t blocks = (p->n + 255) / 256;
 	hipLaunchKernelGGL(generate_kernel, dim3((unsigned)blocks), dim3(256), 0,
 	                   (hipStream_t)hip_stream, g);

@@ -73,7 +73,8 @@ class GclGenParams(ctypes.Structure):
                 ("seed", ctypes.c_uint64), ("n", ctypes.c_uint64), ("stride", ctypes.c_uint64),
                 ("rank", ctypes.c_uint32), ("world", ctypes.c_uint32),
                 ("shard_block", ctypes.c_uint64), ("zipf_cdf", ctypes.c_void_p),
-                ("nflows", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
+                ("nflows", ctypes.c_uint32), ("pad", ctypes.c_uint32),
+                ("pkt_len", ctypes.c_void_p)]
 
 
 class GclOut(ctypes.Structure):
@@ -83,6 +84,13 @@ class GclOut(ctypes.Structure):
 
 class GclTrans(ctypes.Structure):
     _fields_ = [("h5", ctypes.c_uint32), ("h3", ctypes.c_uint32)]
+
+
+class GclTrace(ctypes.Structure):
+    _fields_ = [("frames", ctypes.c_void_p), ("frames_len", ctypes.c_uint64),
+                ("alloc_len", ctypes.c_uint64), ("offs", ctypes.c_void_p),
+                ("pkt_len", ctypes.c_void_p), ("orig_len", ctypes.c_void_p),
+                ("ts_ns", ctypes.c_void_p), ("n", ctypes.c_uint64)]
 
 
 class GclE2eOpts(ctypes.Structure):
@@ -167,6 +175,9 @@ def _load():
         "gcl_dev_alloc": (i32, [i32, ctypes.c_size_t, ctypes.POINTER(vp)]),
         "gcl_dev_free": (i32, [vp]),
         "gcl_host_unregister": (i32, [vp]),
+        "gcl_pcap_write": (i32, [ctypes.c_char_p, vp, u64, vp, vp, vp, u64, u32]),
+        "gcl_pcap_load": (i32, [ctypes.c_char_p, ctypes.POINTER(GclTrace), u64]),
+        "gcl_pcap_free": (None, [ctypes.POINTER(GclTrace)]),
         "gcl_host_deliver": (u64, [vp, u32, vp, i32, vp, vp, vp, ctypes.c_uint8, vp, u64,
                                    ctypes.POINTER(GclHostOps), vp]),
     }
@@ -267,6 +278,56 @@ class DeviceBuffer:
             pass
 
 
+class Trace:
+    """A pcap trace loaded by gcl_pcap_load: packed 16-B-aligned frames in
+    host memory with numpy views of offsets, lengths and timestamps."""
+
+    def __init__(self, path, max_pkts=0):
+        self.t = GclTrace()
+        _check(lib.gcl_pcap_load(os.fsencode(path), ctypes.byref(self.t), max_pkts), "gcl_pcap_load")
+        n = self.t.n
+        self.n = n
+
+        def view(ptr, ctype, count, dtype):
+            if not count:
+                return np.zeros(0, dtype=dtype)
+            return np.ctypeslib.as_array((ctype * count).from_address(ptr)).view(dtype)
+        self.frames = view(self.t.frames, ctypes.c_uint8, self.t.alloc_len, np.uint8)
+        self.frames_len = self.t.frames_len
+        self.offs = view(self.t.offs, ctypes.c_uint64, n, np.uint64)
+        self.pkt_len = view(self.t.pkt_len, ctypes.c_uint16, n, np.uint16)
+        self.orig_len = view(self.t.orig_len, ctypes.c_uint32, n, np.uint32)
+        self.ts_ns = view(self.t.ts_ns, ctypes.c_uint64, n, np.uint64)
+
+    def close(self):
+        if self.t.frames:
+            lib.gcl_pcap_free(ctypes.byref(self.t))
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def host_register(arr):
+    """Pin + map a host numpy array for ZEROCOPY (gcl_host_register)."""
+    _check(lib.gcl_host_register(arr.ctypes.data, arr.nbytes), "gcl_host_register")
+
+
+def host_unregister(arr):
+    return lib.gcl_host_unregister(arr.ctypes.data)
+
+
+def pcap_write(path, frames, pkt_len, stride=0, offs=None, ts_ns=None, snaplen=0):
+    n = len(pkt_len)
+    pl = np.ascontiguousarray(pkt_len, dtype=np.uint16)
+    o = None if offs is None else np.ascontiguousarray(offs, dtype=np.uint64)
+    ts = None if ts_ns is None else np.ascontiguousarray(ts_ns, dtype=np.uint64)
+    _check(lib.gcl_pcap_write(os.fsencode(path), _ptr(frames), stride, _ptr(o), _ptr(pl),
+                              _ptr(ts), n, snaplen), "gcl_pcap_write")
+
+
 def zipf_cdf(nflows, s=0.99):
     cdf = np.empty(nflows, dtype=np.uint64)
     _check(lib.gcl_zipf_cdf(nflows, s, cdf.ctypes.data), "gcl_zipf_cdf")
@@ -274,13 +335,16 @@ def zipf_cdf(nflows, s=0.99):
 
 
 def generate(workload, n, stride, nruntimes, frames, olflags=None, rss=None, seed=0xCA1ADA4,
-             rank=0, world=1, shard_block=0, zipf_cdf_dev=None, nflows=0, stream=None):
+             rank=0, world=1, shard_block=0, zipf_cdf_dev=None, nflows=0, stream=None,
+             pkt_len=None):
     """Fill device buffers with synthetic rx traffic (gcl_generate)."""
     if _nbytes(frames) < n * stride:
         raise ValueError("frames buffer too small")
+    if pkt_len is not None and _nbytes(pkt_len) < 2 * n:
+        raise ValueError("pkt_len buffer too small")
     p = GclGenParams(workload=workload, nruntimes=nruntimes, seed=seed, n=n, stride=stride,
                      rank=rank, world=world, shard_block=shard_block,
-                     zipf_cdf=_ptr(zipf_cdf_dev), nflows=nflows)
+                     zipf_cdf=_ptr(zipf_cdf_dev), nflows=nflows, pkt_len=_ptr(pkt_len))
     _check(lib.gcl_generate(ctypes.byref(p), _ptr(frames), _ptr(olflags), _ptr(rss), stream),
            "gcl_generate")
 

@@ -314,6 +314,8 @@ struct gcl_gen_params {
 	const uint64_t *zipf_cdf; /* device u64[nflows] (TCP1500_ZIPF only) */
 	uint32_t nflows;
 	uint32_t pad;
+	uint16_t *pkt_len;      /* optional device u16[n]: frame length on the wire
+	                           (64, 1500, or the mixed stream's IP/ARP length) */
 };
 
 /* Write the first GCL_HDR_GRANULE bytes of every slot of @frames (n * stride

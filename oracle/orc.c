@@ -832,6 +832,7 @@ int orc_generate(const struct gcl_gen_params *p, const uint64_t *zipf_cdf,
 		uint8_t *f = frames + j * p->stride;
 		uint64_t r0 = rw(p->seed, g, 0), r1 = rw(p->seed, g, 1);
 		uint8_t fl = GCL_F_RSS_HASH | GCL_F_IP_CKSUM_GOOD;
+		uint16_t len = 64;
 
 		memset(f, 0, 64);
 		if (p->workload == GCL_WL_UDP64) {
@@ -858,6 +859,7 @@ int orc_generate(const struct gcl_gen_params *p, const uint64_t *zipf_cdf,
 			f[46] = 0x50;                         /* data offset 5 */
 			f[47] = 0x10;                         /* ACK */
 			put16(f + 48, 0xFFFF);                /* window */
+			len = 1500;
 		} else if (p->workload == GCL_WL_MIXED) {
 			uint64_t r2 = rw(p->seed, g, 2);
 			uint32_t kind = (uint32_t)r0 % 100;
@@ -865,7 +867,7 @@ int orc_generate(const struct gcl_gen_params *p, const uint64_t *zipf_cdf,
 			int unreg = (uint32_t)(r0 >> 40) % 20 == 0;
 			uint32_t dst = unreg ? 0xC0A80000u | (uint32_t)(r1 >> 48) : orc_runtime_ip(rt);
 			if (kind < 70) {
-				uint16_t len = (uint16_t)(64 + (uint32_t)(r1 >> 32) % (9014 - 64 + 1));
+				len = (uint16_t)(64 + (uint32_t)(r1 >> 32) % (9014 - 64 + 1));
 				uint8_t proto = (r0 >> 32) & 1 ? 6 : 17;
 				eth(f, r2 >> 8, GCL_ETHTYPE_IP);
 				ipv4(f + 14, (uint16_t)(len - 14), (uint16_t)r2, proto,
@@ -881,6 +883,8 @@ int orc_generate(const struct gcl_gen_params *p, const uint64_t *zipf_cdf,
 				put32(f + 22, (uint32_t)r2);
 				put32(f + 38, dst);
 				fl = 0;
+				len = (uint16_t)(54 + ((uint32_t)(r1 >> 32) & 0x1FFF));
+				len = len < 60 ? 60 : len;
 			} else {
 				unreg = (uint32_t)(r0 >> 40) % 10 == 0;
 				dst = unreg ? 0xC0A80000u | (uint32_t)(r1 >> 48) : orc_runtime_ip(rt);
@@ -894,6 +898,7 @@ int orc_generate(const struct gcl_gen_params *p, const uint64_t *zipf_cdf,
 				put32(f + 28, (uint32_t)r2);         /* sip */
 				put32(f + 38, dst);                  /* tip */
 				fl = 0;
+				len = 60;
 			}
 		} else {
 			return -EINVAL;
@@ -902,6 +907,8 @@ int orc_generate(const struct gcl_gen_params *p, const uint64_t *zipf_cdf,
 			olflags[j] = fl;
 		if (rss)
 			rss[j] = (uint32_t)rw(p->seed, g, 3);
+		if (p->pkt_len)
+			p->pkt_len[j] = len;
 	}
 	return 0;
 }

@@ -36,7 +36,8 @@ class GenParams(ctypes.Structure):
                 ("seed", ctypes.c_uint64), ("n", ctypes.c_uint64), ("stride", ctypes.c_uint64),
                 ("rank", ctypes.c_uint32), ("world", ctypes.c_uint32),
                 ("shard_block", ctypes.c_uint64), ("zipf_cdf", ctypes.c_void_p),
-                ("nflows", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
+                ("nflows", ctypes.c_uint32), ("pad", ctypes.c_uint32),
+                ("pkt_len", ctypes.c_void_p)]
 
 
 VERDICT_DTYPE = np.dtype([("hash", "<u4"), ("uniqid", "<u2"), ("thread", "u1"), ("action", "u1")])
@@ -209,14 +210,15 @@ class Tables:
 
 
 def generate(workload, n, stride, nruntimes, seed=0xCA1ADA4, rank=0, world=1, shard_block=0,
-             cdf=None, native=False):
-    """CPU copy of the synthetic streams: returns (frames, olflags, rss)."""
+             cdf=None, native=False, pkt_len=None):
+    """CPU copy of the synthetic streams: returns (frames, olflags, rss); fills
+    the optional uint16 `pkt_len` array in place."""
     frames = np.zeros(n * stride, dtype=np.uint8)
     olflags = np.zeros(n, dtype=np.uint8)
     rss = np.zeros(n, dtype=np.uint32)
     p = GenParams(workload=workload, nruntimes=nruntimes, seed=seed, n=n, stride=stride,
                   rank=rank, world=world, shard_block=shard_block,
-                  zipf_cdf=None, nflows=0 if cdf is None else len(cdf))
+                  zipf_cdf=None, nflows=0 if cdf is None else len(cdf), pkt_len=_p(pkt_len))
     ret = lib(native).orc_generate(ctypes.byref(p), _p(cdf), frames.ctypes.data,
                                    olflags.ctypes.data, rss.ctypes.data)
     if ret:

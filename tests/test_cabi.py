@@ -19,7 +19,7 @@ def g():
 
 def declared_functions():
     names = set()
-    for h in ("gclassify.h", "gcl_host.h"):
+    for h in ("gclassify.h", "gcl_host.h", "gcl_pcap.h"):
         src = open(os.path.join(ROOT, "include", h)).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
         names |= set(re.findall(r"\b(gcl_\w+)\s*\(", src))

@@ -304,3 +304,35 @@ def test_gpu_end_to_end_host_buffers(g, orc, mode, wl, stride, R, T, arrays):
                       chunk=65536 + 17, nstreams=3, **pk)
     assert_same(hv.numpy().view(g.VERDICT_DTYPE), ve, f"e2e mode={mode}")
     assert (counts == ce).all() and (stats == se).all()
+
+
+def test_gpu_trace_replay_zero_copy(g, orc, tmp_path):
+    """Config 5's path: a pcap trace loaded into host memory, registered, and
+    classified by the kernel straight over PCIe (gcl_classify_host ZEROCOPY)."""
+    n, R, T = 20000, 16, 8
+    pl = np.zeros(n, dtype=np.uint16)
+    frames, olf, _ = orc.generate(2, n, 9216, R, pkt_len=pl)
+    path = str(tmp_path / "t.pcap")
+    g.pcap_write(path, frames, pl, stride=9216)
+    tr = g.Trace(path)
+    t = orc.Tables(R, 1, 0, 0x09)
+    clf = g.Classifier(0, R, 1)
+    for r in range(R):
+        fl = orc.steer_flows(T, list(range(r % T + 1)))
+        t.runtime_set(r, orc.runtime_ip(r), T, r % T + 1, fl)
+        clf.runtime_set(r, g.runtime_ip(r), T, r % T + 1, fl)
+    ve, ce, se = t.classify(tr.frames, n, 0, offs=tr.offs, olflags=olf, frames_len=tr.frames_len)
+    hv = np.zeros(n, dtype=g.VERDICT_DTYPE)
+    olf = np.ascontiguousarray(olf)
+    for a in (tr.frames, tr.offs, olf, hv):
+        g.host_register(a)
+    try:
+        counts = np.zeros(R, dtype=np.uint64)
+        stats = np.zeros(8, dtype=np.uint64)
+        clf.classify_host(tr.frames, n, 0, verdicts=hv, counts=counts, stats=stats, offs=tr.offs,
+                          olflags=olf, frames_len=tr.frames_len, mode=g.E2E_ZEROCOPY)
+    finally:
+        for a in (tr.frames, tr.offs, olf, hv):
+            g.host_unregister(a)
+    assert_same(hv, ve, "trace replay")
+    assert (counts == ce).all() and (stats == se).all()
