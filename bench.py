@@ -57,6 +57,27 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+# One JSON line on stdout and nothing else: libraries that print banners to
+# stdout (RCCL's version block) are moved to stderr at the fd level.
+_JSON_FD = None
+
+
+def _claim_stdout():
+    global _JSON_FD
+    sys.stdout.flush()
+    _JSON_FD = os.dup(1)
+    os.dup2(2, 1)
+
+
+def emit_json(obj):
+    line = (json.dumps(obj) + "\n").encode()
+    if _JSON_FD is None:
+        sys.stdout.write(line.decode())
+        sys.stdout.flush()
+    else:
+        os.write(_JSON_FD, line)
+
+
 def setup_tables(clf, R, T, seed=SEED):
     """Runtime r owns 10.0.0.(r+1); active kthreads seeded in [1, T];
     flow tables from the sched_steer_flows rule (gcl_steer_flows)."""
@@ -112,22 +133,26 @@ class Workload:
 
 class Exchange:
     """Multi-GPU step: classify into a per-step [counts | stats] vector, then
-    one RCCL all_gather of it on a side stream that overlaps the next step's
-    kernel; node-wide totals accumulate on that stream.  Two vectors
-    alternate so a step never zeroes one that a gather still reads."""
+    one RCCL all_gather of it on a side stream that overlaps the following
+    steps' kernels; node-wide totals accumulate on that stream.  A ring of
+    NBUF vectors lets a gather finish up to NBUF-1 steps late before its
+    vector is reused, so the compute stream never waits on the exchange."""
+
+    NBUF = 4
 
     def __init__(self, w, world, device):
         L = w.R + g.NR_STATS
         self.world = world
-        self.cnt = [torch.zeros(L, dtype=torch.int64, device=device) for _ in range(2)]
-        self.gat = [torch.zeros(world * L, dtype=torch.int64, device=device) for _ in range(2)]
+        self.cnt = [torch.zeros(L, dtype=torch.int64, device=device) for _ in range(self.NBUF)]
+        self.gat = [torch.zeros(world * L, dtype=torch.int64, device=device)
+                    for _ in range(self.NBUF)]
         self.acc = torch.zeros(L, dtype=torch.int64, device=device)
-        self.done = [None, None]
+        self.done = [None] * self.NBUF
         self.comm = torch.cuda.Stream(device=device)
         self.k = 0
 
     def step(self, w):
-        b = self.k & 1
+        b = self.k % self.NBUF
         cur = torch.cuda.current_stream()
         if self.done[b] is not None:
             cur.wait_event(self.done[b])
@@ -353,7 +378,10 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo only to rehearse N>1 on one GPU")
+    ap.add_argument("--force-exchange", action="store_true",
+                    help="run the multi-GPU step (RCCL all_gather on a side stream) even at N=1")
     args = ap.parse_args()
+    _claim_stdout()
 
     rank, world, local = shard.dist_env()
     if world != args.gpus:
@@ -362,16 +390,17 @@ def main():
     dev_index = local % ndev
     torch.cuda.set_device(dev_index)
     device = torch.device("cuda", dev_index)
-    if world > 1:
+    dist_on = world > 1 or args.force_exchange
+    if dist_on:
         shard.init(rank, world, backend=args.dist_backend)
 
     w = Workload(args.workload, rank, world, device)
-    ex = Exchange(w, world, device) if world > 1 else None
+    ex = Exchange(w, world, device) if dist_on else None
     el, kms = run_timed(w, args.steps, args.warmup, world, ex)
     total_pkts = w.n * world * args.steps
     value = total_pkts / el / 1e6
     # correctness spot check: every packet of every step was accounted for
-    if world > 1:
+    if ex is not None:
         tot = ex.acc[:w.R].sum().item()
         expect = w.n * world * (args.steps + args.warmup)
     else:
@@ -395,7 +424,7 @@ def main():
                    "hash": "jenkins (lookup3 13-B 5-tuple)",
                    "parallelism": (f"dp{world}: round-robin 64Ki-pkt shards, {args.dist_backend} "
                                    "all_gather of per-runtime counts per step (overlapped)"
-                                   if world > 1 else "single GPU")},
+                                   if dist_on else "single GPU")},
         "roofline": roofline(w, kms),
         "counts_check": "ok" if tot == expect else f"MISMATCH {tot} != {expect}",
     }
@@ -428,10 +457,10 @@ def main():
 
     if world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(args.cpu_budget)
-    if world > 1:
+    if dist_on:
         shard.finish()
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        emit_json(result)
 
 
 if __name__ == "__main__":
