@@ -131,34 +131,47 @@ class Workload:
                           counts=self.counts[:self.R], stats=self.counts[self.R:], stream=stream)
 
 
+# classify launches timed with HIP events: one in PROFILE_EVERY (gcl_profile_sample)
+PROFILE_EVERY = 5
+
+
 class Exchange:
-    """Multi-GPU step: classify into a per-step [counts | stats] vector, then
-    one RCCL all_gather of it on a side stream that overlaps the following
-    steps' kernels; node-wide totals accumulate on that stream.  A ring of
-    NBUF vectors lets a gather finish up to NBUF-1 steps late before its
-    vector is reused, so the compute stream never waits on the exchange."""
+    """Multi-GPU step: classify into a [counts | stats] vector, then one RCCL
+    all_gather of it on a side stream that overlaps the following steps'
+    kernels; node-wide totals accumulate on that stream.  The vector covers
+    `period` steps (the iokernel reads its counters periodically, not per
+    burst).  A ring of NBUF vectors lets a gather finish up to NBUF-1 periods
+    late before its vector is reused, and the side stream zeroes a vector
+    after gathering it, so the compute stream only ever waits on an event."""
 
     NBUF = 4
 
-    def __init__(self, w, world, device):
+    def __init__(self, w, world, device, period=1):
         L = w.R + g.NR_STATS
         self.world = world
+        self.period = max(1, period)
         self.cnt = [torch.zeros(L, dtype=torch.int64, device=device) for _ in range(self.NBUF)]
         self.gat = [torch.zeros(world * L, dtype=torch.int64, device=device)
                     for _ in range(self.NBUF)]
         self.acc = torch.zeros(L, dtype=torch.int64, device=device)
         self.done = [None] * self.NBUF
         self.comm = torch.cuda.Stream(device=device)
-        self.k = 0
+        self.k = 0      # periods exchanged
+        self.inner = 0  # steps accumulated into the current vector
 
     def step(self, w):
         b = self.k % self.NBUF
         cur = torch.cuda.current_stream()
-        if self.done[b] is not None:
+        if self.inner == 0 and self.done[b] is not None:
             cur.wait_event(self.done[b])
-        self.cnt[b].zero_()
         w.clf.classify(w.frames, w.n, w.stride, verdicts=w.verdicts, counts=self.cnt[b][:w.R],
                        stats=self.cnt[b][w.R:], stream=cur.cuda_stream)
+        self.inner += 1
+        if self.inner == self.period:
+            self._exchange(cur)
+
+    def _exchange(self, cur):
+        b = self.k % self.NBUF
         ev = torch.cuda.Event()
         ev.record(cur)
         with torch.cuda.stream(self.comm):
@@ -167,16 +180,21 @@ class Exchange:
             if work is not None:
                 work.wait()
             self.acc.add_(shard.global_counts(self.gat[b], self.world))
+            self.cnt[b].zero_()
             d = torch.cuda.Event()
             d.record(self.comm)
             self.done[b] = d
         self.k += 1
+        self.inner = 0
 
     def drain(self):
-        torch.cuda.current_stream().wait_stream(self.comm)
+        cur = torch.cuda.current_stream()
+        if self.inner:
+            self._exchange(cur)
+        cur.wait_stream(self.comm)
 
 
-def run_timed(w, steps, warmup, world, ex=None):
+def run_timed(w, steps, warmup, world, ex=None, profile_every=PROFILE_EVERY):
     stream = torch.cuda.current_stream().cuda_stream
 
     def one():
@@ -194,6 +212,9 @@ def run_timed(w, steps, warmup, world, ex=None):
         torch.distributed.barrier()
     torch.cuda.synchronize()
     w.clf.kernel_time(reset=True)
+    # HIP events around one launch in `profile_every` (the first one timed):
+    # a timed event pair costs the stream ~10 us, 2% of a udp64 step
+    w.clf.profile_sample(profile_every)
     t0 = time.perf_counter()
     for _ in range(steps):
         one()
@@ -378,6 +399,10 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo only to rehearse N>1 on one GPU")
+    ap.add_argument("--profile-every", type=int, default=PROFILE_EVERY,
+                    help="time one classify launch in N with HIP events (roofline.kernel_ms)")
+    ap.add_argument("--exchange-every", type=int, default=1,
+                    help="steps per counts all_gather (multi-GPU exchange period)")
     ap.add_argument("--force-exchange", action="store_true",
                     help="run the multi-GPU step (RCCL all_gather on a side stream) even at N=1")
     args = ap.parse_args()
@@ -395,8 +420,8 @@ def main():
         shard.init(rank, world, backend=args.dist_backend)
 
     w = Workload(args.workload, rank, world, device)
-    ex = Exchange(w, world, device) if dist_on else None
-    el, kms = run_timed(w, args.steps, args.warmup, world, ex)
+    ex = Exchange(w, world, device, args.exchange_every) if dist_on else None
+    el, kms = run_timed(w, args.steps, args.warmup, world, ex, max(1, args.profile_every))
     total_pkts = w.n * world * args.steps
     value = total_pkts / el / 1e6
     # correctness spot check: every packet of every step was accounted for
@@ -423,7 +448,7 @@ def main():
                    "slot_stride": w.stride, "runtimes": w.R, "kthreads": w.T,
                    "hash": "jenkins (lookup3 13-B 5-tuple)",
                    "parallelism": (f"dp{world}: round-robin 64Ki-pkt shards, {args.dist_backend} "
-                                   "all_gather of per-runtime counts per step (overlapped)"
+                                   f"all_gather of per-runtime counts every {args.exchange_every} step(s), overlapped"
                                    if dist_on else "single GPU")},
         "roofline": roofline(w, kms),
         "counts_check": "ok" if tot == expect else f"MISMATCH {tot} != {expect}",

@@ -33,6 +33,8 @@ constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 constexpr uint32_t kToepBytes = 12 * 256 * 4;
 constexpr uint32_t kCrcBytes = 8 * 256 * 4;
 constexpr uint32_t kLdsTableBudget = 96 * 1024;
+constexpr uint32_t kLdsQueueBytes = 16; /* s_next[2] after the header tile */
+constexpr int kDefaultSched = 0; /* GCL_TUNE_SCHED default: static persistent grid */
 
 /* tuning knobs for experiments (GCL_TUNE_BLOCKS_PER_CU caps the grid) */
 static int g_tune_bpc = 0;
@@ -69,7 +71,17 @@ struct KParams {
 	uint32_t ablate; /* GCL_TUNE_ABLATE: timing-only experiments, wrong results */
 	uint2 *trans;    /* struct gcl_trans[n] or NULL */
 	uint32_t off_seed, off_crc;
+	uint32_t *sched; /* tile queue slot (SchedSlot) or NULL = static persistent grid */
 };
+
+/* Dynamic tile queue of one launch: tiles are dealt per XCD (tile t belongs
+ * to XCD t & 7, the one blockIdx.x & 7 is dispatched to), each XCD has its
+ * own head on its own 128-B line, and a block whose XCD has run dry steals
+ * from the next ones.  The last block to finish rewinds the slot. */
+#define GCL_SCHED_XCD 8
+#define GCL_SCHED_LINE 32 /* u32 per 128-B line */
+#define GCL_SCHED_WORDS ((GCL_SCHED_XCD + 1) * GCL_SCHED_LINE)
+#define GCL_SCHED_SLOTS 64
 
 /* ------------------------------------------------------------------------
  * Header tile: 256 packets x 64 B, 16-B chunks XOR-swizzled so that both the
@@ -344,9 +356,40 @@ __device__ __forceinline__ void stage_tile(uint4 *tile, const uint4 r[4])
 	}
 }
 
+__device__ __forceinline__ uint64_t sched_xcd_tiles(uint64_t ntiles, uint32_t x)
+{
+	return ntiles > x ? (ntiles - x + GCL_SCHED_XCD - 1) / GCL_SCHED_XCD : 0;
+}
+
+__device__ __forceinline__ uint32_t sched_xcd_blocks(uint32_t G, uint32_t x)
+{
+	return G > x ? (G - x + GCL_SCHED_XCD - 1) / GCL_SCHED_XCD : 0;
+}
+
+/* Resolve a dequeue from head @xs that returned @got; on an exhausted head,
+ * move on to the next XCD's head (at most 7 more atomics per block, at the
+ * very end of the launch).  Returns the tile or ntiles when all are gone. */
+__device__ __forceinline__ uint64_t sched_resolve(uint32_t *sched, uint64_t ntiles, uint32_t G,
+                                               uint32_t x0, uint32_t &xs, uint32_t got)
+{
+	for (;;) {
+		const uint64_t k = (uint64_t)sched_xcd_blocks(G, xs) + got;
+		if (k < sched_xcd_tiles(ntiles, xs))
+			return xs + GCL_SCHED_XCD * k;
+		xs = (xs + 1) & (GCL_SCHED_XCD - 1);
+		if (xs == x0)
+			return ntiles;
+		got = atomicAdd(&sched[xs * GCL_SCHED_LINE], 1u);
+	}
+}
+
 /*
- * Persistent grid: block b handles tiles b, b + G, b + 2G, ...; the frames of
- * the next DEPTH tiles are in flight in registers while a tile is parsed.
+ * Persistent grid.  Static schedule (k.sched == NULL): block b handles tiles
+ * b, b + G, b + 2G, ...  Dynamic (k.sched): block b starts on tile
+ * (b & 7) + 8 * (b >> 3) and then dequeues from its XCD's head, one tile
+ * ahead, so the atomic's latency hides behind the current tile.  Either way
+ * the frames of the next DEPTH tiles are in flight in registers while a tile
+ * is parsed.
  */
 template <int MODE, bool TLDS, bool GENERAL, int DEPTH, int NT>
 __global__ void __launch_bounds__(NT)
@@ -354,7 +397,8 @@ classify_kernel(KParams k)
 {
 	extern __shared__ uint4 smem[];
 	uint4 *tile = smem;
-	uint32_t *hist = (uint32_t *)(smem + NT * 4);
+	uint64_t *s_next = (uint64_t *)(smem + NT * 4); /* tile queue hand-off, 16 B */
+	uint32_t *hist = (uint32_t *)(smem + NT * 4 + 1);
 	uint8_t *lds_tab = (uint8_t *)(hist + ((k.max_rt + 3) & ~3u));
 	const int tid = threadIdx.x;
 
@@ -380,24 +424,55 @@ classify_kernel(KParams k)
 
 	Counters cnt = {0, 0, 0, 0};
 	const uint64_t G = gridDim.x;
+	const bool dyn = DEPTH == 1 && k.sched != nullptr;
+	const uint32_t x0 = blockIdx.x & (GCL_SCHED_XCD - 1);
+	uint32_t xs = x0; /* head this block dequeues from (thread 0 only) */
 	uint4 ra[4], rb[4];
 	uint64_t t = blockIdx.x;
+	uint32_t got = 0;
+	if (dyn) {
+		const uint64_t j = blockIdx.x / GCL_SCHED_XCD;
+		t = j < sched_xcd_tiles(k.ntiles, x0) ? x0 + GCL_SCHED_XCD * j : k.ntiles;
+		if (tid == 0 && t < k.ntiles)
+			got = atomicAdd(&k.sched[x0 * GCL_SCHED_LINE], 1u);
+	}
 	if (t < k.ntiles)
 		load_tile<GENERAL, NT>(k, t, ra);
 	if (DEPTH == 2 && t + G < k.ntiles)
 		load_tile<GENERAL, NT>(k, t + G, rb);
+	if (dyn && tid == 0)
+		s_next[0] = t < k.ntiles ? sched_resolve(k.sched, k.ntiles, (uint32_t)G, x0, xs, got)
+		                         : k.ntiles;
+	int par = 0;
 
 	while (t < k.ntiles) {
 		stage_tile<NT>(tile, ra);
 		__syncthreads();
-		if (t + DEPTH * G < k.ntiles)
-			load_tile<GENERAL, NT>(k, t + DEPTH * G, ra); /* in flight while parsing */
+		uint64_t nxt = t + DEPTH * G;
+		if (dyn) {
+			nxt = s_next[par];
+			/* issued before the tile loads, so waiting for it later does
+			 * not wait for them (vmcnt retires in order) */
+			if (tid == 0 && nxt < k.ntiles)
+				got = atomicAdd(&k.sched[xs * GCL_SCHED_LINE], 1u);
+		}
+		if (nxt < k.ntiles)
+			load_tile<GENERAL, NT>(k, nxt, ra); /* in flight while parsing */
 		if (k.ablate & 16) { /* timing only: the membench tile_v0 body */
 			const uint4 a = tile[tile_slot(tid, 0)], b = tile[tile_slot(tid, 1)];
 			*(u32x2 *)&k.verdicts[t * NT + tid] = u32x2{b.z ^ a.x, a.w ^ b.y};
 		} else if (t * NT + tid < k.n)
 			classify_one<MODE, GENERAL>(k, tile, tid, t * NT + tid, tb, hist, cnt);
+		if (dyn && tid == 0)
+			s_next[par ^ 1] = nxt < k.ntiles ? sched_resolve(k.sched, k.ntiles, (uint32_t)G,
+			                                                 x0, xs, got)
+			                                 : k.ntiles;
 		__syncthreads();
+		if (dyn) {
+			t = nxt;
+			par ^= 1;
+			continue;
+		}
 		t += G;
 		if (DEPTH == 2) {
 			if (t >= k.ntiles)
@@ -414,6 +489,17 @@ classify_kernel(KParams k)
 	}
 	uint32_t n_flowtag = cnt.flowtag, n_hashmiss = cnt.hashmiss;
 	uint32_t n_unreg = cnt.unreg, n_unhandled = cnt.unhandled;
+
+	/* every dequeue of this block has returned; the last block out rewinds */
+	if (dyn && tid == 0) {
+		uint32_t *done = &k.sched[GCL_SCHED_XCD * GCL_SCHED_LINE];
+		if (atomicAdd(done, 1u) == (uint32_t)G - 1) {
+			for (int x = 0; x < GCL_SCHED_XCD; x++)
+				__hip_atomic_store(&k.sched[x * GCL_SCHED_LINE], 0u, __ATOMIC_RELAXED,
+				                   __HIP_MEMORY_SCOPE_AGENT);
+			__hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		}
+	}
 
 	/* flush per-block counters */
 	if (k.ablate & 64)
@@ -637,11 +723,20 @@ struct gcl_ctx {
 	std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending;
 	double prof_ms;
 	uint64_t prof_launches;
+	uint32_t prof_every;  /* time one launch in prof_every (gcl_profile_sample) */
+	uint64_t prof_seq;
 	int tune_tables; /* GCL_TUNE_TABLES: 0 auto, 1 global, 2 lds-if-fits */
 	int tune_depth;  /* GCL_TUNE_DEPTH: tiles in flight per block (1 or 2) */
 	int tune_threads; /* GCL_TUNE_THREADS: 256, 512 or 1024 lanes per block */
 	int tune_nt_store; /* GCL_TUNE_NT_STORE: non-temporal verdict stores */
 	int tune_ablate;   /* GCL_TUNE_ABLATE bitmask (timing experiments only) */
+	int tune_sched;    /* GCL_TUNE_SCHED: 0 static persistent grid, 1 dynamic tile queue */
+	/* dynamic tile queue: one slot per launch in flight, reused in turn; a
+	 * launch waits for the previous user of its slot (same or other stream) */
+	uint32_t *sched;
+	hipEvent_t sched_ev[GCL_SCHED_SLOTS];
+	bool sched_used[GCL_SCHED_SLOTS];
+	uint32_t sched_seq;
 };
 
 extern "C" {
@@ -690,6 +785,8 @@ extern "C" int gcl_open(int hip_device, const struct gcl_cfg *cfg, struct gcl_ct
 	c->last_stream = nullptr;
 	c->prof_ms = 0;
 	c->prof_launches = 0;
+	c->prof_every = 1;
+	c->prof_seq = 0;
 	{
 		const char *e = getenv("GCL_TUNE_TABLES");
 		c->tune_tables = e ? atoi(e) : 0;
@@ -707,9 +804,20 @@ extern "C" int gcl_open(int hip_device, const struct gcl_cfg *cfg, struct gcl_ct
 		g_tune_grid = e ? atoi(e) : 0;
 		e = getenv("GCL_TUNE_BLOCKS_PER_CU");
 		g_tune_bpc = e ? atoi(e) : 0;
+		e = getenv("GCL_TUNE_SCHED");
+		c->tune_sched = e ? atoi(e) : kDefaultSched;
+	}
+	c->dimg[0] = c->dimg[1] = nullptr;
+	c->sched = nullptr;
+	c->sched_seq = 0;
+	if (hipMalloc(&c->sched, GCL_SCHED_SLOTS * GCL_SCHED_WORDS * 4) != hipSuccess ||
+	    hipMemset(c->sched, 0, GCL_SCHED_SLOTS * GCL_SCHED_WORDS * 4) != hipSuccess)
+		goto fail;
+	for (int i = 0; i < GCL_SCHED_SLOTS; i++) {
+		hipEventCreateWithFlags(&c->sched_ev[i], hipEventDisableTiming);
+		c->sched_used[i] = false;
 	}
 	for (int i = 0; i < 2; i++) {
-		c->dimg[i] = nullptr;
 		if (hipMalloc(&c->dimg[i], c->image_cap) != hipSuccess)
 			goto fail;
 		hipEventCreateWithFlags(&c->img_free[i], hipEventDisableTiming);
@@ -725,6 +833,8 @@ fail:
 	for (int i = 0; i < 2; i++)
 		if (c->dimg[i])
 			hipFree(c->dimg[i]);
+	if (c->sched)
+		hipFree(c->sched);
 	delete c;
 	return -ENOMEM;
 }
@@ -742,6 +852,9 @@ extern "C" void gcl_close(struct gcl_ctx *c)
 	hipHostFree(c->staging);
 	hipEventDestroy(c->staging_free);
 	hipEventDestroy(c->tables_ready);
+	hipFree(c->sched);
+	for (int i = 0; i < GCL_SCHED_SLOTS; i++)
+		hipEventDestroy(c->sched_ev[i]);
 	for (int i = 0; i < c->e2e.nstreams; i++) {
 		hipStreamDestroy(c->e2e.st[i]);
 		hipFree(c->e2e.slab[i]);
@@ -965,7 +1078,7 @@ template <int MODE>
 static hipError_t launch_mode(const KParams &k, bool tlds, bool general, const Geometry &geo,
                               uint32_t tab_lds, uint32_t hist_bytes, int num_cus, hipStream_t s)
 {
-	const uint32_t lds = (uint32_t)geo.threads * 64 + hist_bytes + tab_lds;
+	const uint32_t lds = (uint32_t)geo.threads * 64 + kLdsQueueBytes + hist_bytes + tab_lds;
 #define GCL_LAUNCH(D, T) \
 	return launch_nt<MODE, D, T>(k, tlds, general, lds, num_cus, geo.bpc_cap, s)
 	if (geo.depth == 2) {
@@ -995,7 +1108,7 @@ static Geometry choose_geometry(const gcl_ctx *c, uint32_t tab_lds, uint32_t his
 	g.depth = 1;
 	g.threads = 0;
 	for (int nt = 256; nt <= 1024 && !g.threads; nt *= 2) {
-		uint32_t per_block = (uint32_t)nt * 64 + hist_bytes + tab_lds;
+		uint32_t per_block = (uint32_t)nt * 64 + kLdsQueueBytes + hist_bytes + tab_lds;
 		if ((lanes_cu / nt) * per_block <= lds_cu) {
 			g.threads = nt;
 			g.bpc_cap = (int)(lanes_cu / (uint32_t)nt);
@@ -1003,7 +1116,7 @@ static Geometry choose_geometry(const gcl_ctx *c, uint32_t tab_lds, uint32_t his
 	}
 	if (!g.threads) { /* big tables: as many 256-lane blocks as LDS admits */
 		g.threads = 256;
-		g.bpc_cap = (int)(lds_cu / (256u * 64 + hist_bytes + tab_lds));
+		g.bpc_cap = (int)(lds_cu / (256u * 64 + kLdsQueueBytes + hist_bytes + tab_lds));
 		if (g.bpc_cap < 1)
 			g.bpc_cap = 1;
 	}
@@ -1106,8 +1219,16 @@ extern "C" int gcl_classify_ex(struct gcl_ctx *c, const struct gcl_batch *b,
 	k.tables_lds_bytes = tlds ? tab_bytes : 0;
 	Geometry geo = choose_geometry(c, tlds ? tab_bytes : 0, hist_bytes);
 
+	int slot = -1;
+	if (c->tune_sched && geo.depth == 1) {
+		slot = (int)(c->sched_seq++ % GCL_SCHED_SLOTS);
+		if (c->sched_used[slot])
+			hipStreamWaitEvent(s, c->sched_ev[slot], 0);
+		k.sched = c->sched + (size_t)slot * GCL_SCHED_WORDS;
+	}
+
 	hipEvent_t e0 = nullptr, e1 = nullptr;
-	if (c->cfg.flags & GCL_CFG_PROFILE) {
+	if ((c->cfg.flags & GCL_CFG_PROFILE) && c->prof_seq++ % c->prof_every == 0) {
 		e0 = prof_event(c);
 		e1 = prof_event(c);
 		hipEventRecord(e0, s);
@@ -1132,6 +1253,10 @@ extern "C" int gcl_classify_ex(struct gcl_ctx *c, const struct gcl_batch *b,
 		c->ev_pending.push_back({e0, e1});
 	}
 	hipEventRecord(c->img_free[c->cur], s);
+	if (slot >= 0) {
+		hipEventRecord(c->sched_ev[slot], s);
+		c->sched_used[slot] = true;
+	}
 	c->last_stream = s;
 	return err == hipSuccess ? 0 : -EIO;
 }
@@ -1142,6 +1267,15 @@ extern "C" int gcl_sync(struct gcl_ctx *c)
 		return -EINVAL;
 	hipSetDevice(c->device);
 	return hipStreamSynchronize(c->last_stream) == hipSuccess ? 0 : -EIO;
+}
+
+extern "C" int gcl_profile_sample(struct gcl_ctx *c, uint32_t every)
+{
+	if (!c || every == 0)
+		return -EINVAL;
+	c->prof_every = every;
+	c->prof_seq = 0;
+	return 0;
 }
 
 extern "C" int gcl_kernel_time(struct gcl_ctx *c, double *ms, uint64_t *launches, int reset)

@@ -159,6 +159,7 @@ def _load():
         "gcl_trans_hash": (None, [u32, ctypes.c_uint8, u32, u16, u32, u16, ctypes.POINTER(GclTrans)]),
         "gcl_sync": (i32, [vp]),
         "gcl_kernel_time": (i32, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64), i32]),
+        "gcl_profile_sample": (i32, [vp, u32]),
         "gcl_generate": (i32, [ctypes.POINTER(GclGenParams), vp, vp, vp, vp]),
         "gcl_runtime_ip": (u32, [u32]),
         "gcl_loopback_olflags": (ctypes.c_uint8, [ctypes.c_uint8]),
@@ -429,6 +430,10 @@ class Classifier:
 
     def sync(self):
         return _check(lib.gcl_sync(self._ctx), "gcl_sync")
+
+    def profile_sample(self, every):
+        """Time one launch in `every` (GCL_CFG_PROFILE); see gcl_profile_sample."""
+        return _check(lib.gcl_profile_sample(self._ctx, int(every)), "gcl_profile_sample")
 
     def kernel_time(self, reset=False):
         ms = ctypes.c_double()

@@ -291,6 +291,15 @@ int gcl_sync(struct gcl_ctx *ctx);
 int gcl_kernel_time(struct gcl_ctx *ctx, double *ms, uint64_t *launches, int reset);
 
 /*
+ * gcl_profile_sample - with GCL_CFG_PROFILE, time only one classify launch in
+ * @every (the first of each run of @every); gcl_kernel_time then reports the
+ * timed launches.  A timed HIP event pair costs the stream ~10 us per launch
+ * on MI355X; sampling keeps that out of the throughput it measures.
+ * Default 1 (every launch).  -EINVAL for @every == 0.
+ */
+int gcl_profile_sample(struct gcl_ctx *ctx, uint32_t every);
+
+/*
  * Synthetic rx traffic generator (device).  Counter-based: packet g of the
  * global stream depends only on (seed, g), so every rank and the CPU oracle
  * produce identical bytes.  Packet j of this call is global packet

@@ -3,7 +3,10 @@
 //
 //   cbench <workload> <steps> [cfg ...]
 //
-// Each cfg is "ABLATE:GRID:DEPTH:THREADS:BPC" (GCL_TUNE_* knobs, 0 = default).  Rounds
+// Each cfg is "ABLATE:GRID:DEPTH:THREADS:BPC:SCHED" (GCL_TUNE_* knobs, 0 = default).
+// CBENCH_NOISE_US=X co-runs, on a second stream, 32 one-wave blocks that each
+// spin for X us at the start of every classify launch (stand-in for an RCCL
+// kernel sharing the chip).  Rounds
 // interleave the configs (plus "ref", a compute-free kernel with the same
 // tile/LDS/traffic shape) so box-to-box and drift effects cancel; the median
 // kernel time per config is printed as JSON.
@@ -61,11 +64,22 @@ __global__ void __launch_bounds__(256) ref_kernel(const unsigned char *buf, unsi
 	}
 }
 
+// bounded spinner: every wave leaves after @us microseconds (100 MHz clock)
+__global__ void noise_kernel(unsigned us, unsigned long long *sink)
+{
+	const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+	unsigned long long x = threadIdx.x;
+	while (__builtin_amdgcn_s_memrealtime() - t0 < 100ull * us)
+		x = x * 6364136223846793005ull + 1;
+	if (x == 42)
+		sink[0] = x;
+}
+
 struct Cfg {
 	std::string name;
-	int ablate, grid, depth, threads, bpc;
+	int ablate, grid, depth, threads, bpc, sched;
 	bool ref;
-	std::vector<double> us;
+	std::vector<double> us, wall;
 };
 
 int main(int argc, char **argv)
@@ -76,14 +90,28 @@ int main(int argc, char **argv)
 	const uint64_t stride = wl == GCL_WL_UDP64 ? 64 : 1536;
 	const uint32_t R = wl == GCL_WL_UDP64 ? 16 : 1024, T = wl == GCL_WL_UDP64 ? 8 : 4;
 	std::vector<Cfg> cfgs;
-	cfgs.push_back({"ref", 0, 0, 0, 0, 0, true, {}});
+	cfgs.push_back({"ref", 0, 0, 0, 0, 0, 0, true, {}, {}});
 	for (int i = 3; i < argc; i++) {
-		Cfg c = {argv[i], 0, 0, 0, 0, 0, false, {}};
-		sscanf(argv[i], "%d:%d:%d:%d:%d", &c.ablate, &c.grid, &c.depth, &c.threads, &c.bpc);
+		Cfg c = {argv[i], 0, 0, 0, 0, 0, 0, false, {}, {}};
+		sscanf(argv[i], "%d:%d:%d:%d:%d:%d", &c.ablate, &c.grid, &c.depth, &c.threads, &c.bpc,
+		       &c.sched);
 		cfgs.push_back(c);
 	}
 	if (cfgs.size() == 1)
-		cfgs.push_back({"default", 0, 0, 0, 0, 0, false, {}});
+		cfgs.push_back({"default", 0, 0, 0, 0, 0, 0, false, {}, {}});
+	const char *pe = getenv("CBENCH_PROFILE");
+	const bool profile = !pe || atoi(pe) != 0; /* 0: no per-launch events, wall time only */
+	const char *ne = getenv("CBENCH_NOISE_US");
+	const unsigned noise_us = ne ? (unsigned)atoi(ne) : 0;
+	if (noise_us > 1000) {
+		fprintf(stderr, "CBENCH_NOISE_US too large\n");
+		return 1;
+	}
+	hipStream_t s1, s2;
+	CHECK(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking));
+	CHECK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+	hipEvent_t start_ev;
+	CHECK(hipEventCreateWithFlags(&start_ev, hipEventDisableTiming));
 
 	uint8_t *frames;
 	struct gcl_verdict *v;
@@ -139,6 +167,7 @@ int main(int argc, char **argv)
 				float ms = 0;
 				CHECK(hipEventElapsedTime(&ms, e0, e1));
 				c.us.push_back(ms * 1e3 / steps);
+				c.wall.push_back(ms * 1e3 / steps);
 				continue;
 			}
 			char buf[32];
@@ -152,10 +181,12 @@ int main(int argc, char **argv)
 			setenv("GCL_TUNE_THREADS", buf, 1);
 			snprintf(buf, sizeof(buf), "%d", c.bpc);
 			setenv("GCL_TUNE_BLOCKS_PER_CU", buf, 1);
+			snprintf(buf, sizeof(buf), "%d", c.sched);
+			setenv("GCL_TUNE_SCHED", buf, 1);
 			struct gcl_cfg cfg = {};
 			cfg.max_runtimes = R;
 			cfg.hash_mode = GCL_HASH_JENKINS;
-			cfg.flags = GCL_CFG_PROFILE;
+			cfg.flags = profile ? GCL_CFG_PROFILE : 0;
 			cfg.default_olflags = GCL_F_RSS_HASH | GCL_F_IP_CKSUM_GOOD;
 			struct gcl_ctx *ctx;
 			if (gcl_open(0, &cfg, &ctx)) {
@@ -170,28 +201,43 @@ int main(int argc, char **argv)
 				gcl_steer_flows((uint16_t)T, act, na, flow);
 				gcl_runtime_set(ctx, (uint16_t)r, gcl_runtime_ip(r), (uint16_t)T, na, flow);
 			}
-			gcl_classify(ctx, &b, v, acc, acc + R, nullptr);
+			gcl_classify(ctx, &b, v, acc, acc + R, s1);
 			CHECK(hipDeviceSynchronize());
 			double ms;
 			uint64_t launches;
 			gcl_kernel_time(ctx, &ms, &launches, 1);
-			for (int i = 0; i < steps; i++)
-				gcl_classify(ctx, &b, v, acc, acc + R, nullptr);
+			CHECK(hipEventRecord(e0, s1));
+			for (int i = 0; i < steps; i++) {
+				if (noise_us) {
+					CHECK(hipEventRecord(start_ev, s1));
+					CHECK(hipStreamWaitEvent(s2, start_ev, 0));
+					hipLaunchKernelGGL(noise_kernel, dim3(32), dim3(64), 0, s2, noise_us,
+					                   (unsigned long long *)acc);
+				}
+				gcl_classify(ctx, &b, v, acc, acc + R, s1);
+			}
+			CHECK(hipEventRecord(e1, s1));
+			CHECK(hipDeviceSynchronize());
+			float wms = 0;
+			CHECK(hipEventElapsedTime(&wms, e0, e1));
+			c.wall.push_back(wms * 1e3 / steps);
 			gcl_kernel_time(ctx, &ms, &launches, 1);
-			c.us.push_back(ms / launches * 1e3);
+			c.us.push_back(launches ? ms / launches * 1e3 : wms * 1e3 / steps);
 			gcl_close(ctx);
 		}
 	}
 	double ref = 0;
 	for (Cfg &c : cfgs) {
 		std::sort(c.us.begin(), c.us.end());
-		double med = c.us[c.us.size() / 2];
+		std::sort(c.wall.begin(), c.wall.end());
+		double med = c.us[c.us.size() / 2], wmed = c.wall[c.wall.size() / 2];
 		if (c.ref)
 			ref = med;
-		printf("{\"workload\": %d, \"cfg\": \"%s\", \"median_us\": %.2f, \"min_us\": %.2f, "
-		       "\"max_us\": %.2f, \"Mpkts\": %.1f, \"ref_over_this\": %.4f}\n",
-		       wl, c.name.c_str(), med, c.us.front(), c.us.back(), n / (med * 1e-6) / 1e6,
-		       ref / med);
+		printf("{\"workload\": %d, \"cfg\": \"%s\", \"profile\": %d, \"median_us\": %.2f, "
+		       "\"min_us\": %.2f, \"max_us\": %.2f, \"wall_us_per_step\": %.2f, \"Mpkts\": %.1f, "
+		       "\"ref_over_this\": %.4f}\n",
+		       wl, c.name.c_str(), (int)profile, med, c.us.front(), c.us.back(), wmed,
+		       n / (med * 1e-6) / 1e6, ref / med);
 	}
 	return 0;
 }
