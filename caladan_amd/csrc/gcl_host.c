@@ -200,24 +200,28 @@ uint64_t gcl_rx_make_cmd(uint16_t pkt_len, uint8_t olflags)
 	return 0 /* RX_NET_RECV */ | (uint64_t)pkt_len << 16 | csum << 48;
 }
 
-/* rx_send_to_runtime (rx.c:50-73); @via_flow_tbl selects the GPU's thread */
-static bool send_to_runtime(struct gcl_host_proc *p, uint32_t hash, int gpu_thread,
+/* rx_send_to_runtime (rx.c:50-73).  @gpu_thread >= 0 is the GPU's thread
+ * (DELIVER); otherwise the flow_tbl slot is @slot when >= 0 (a compact WAKE
+ * verdict), else hash % thread_count. */
+static bool send_to_runtime(struct gcl_host_proc *p, uint32_t hash, int slot, int gpu_thread,
                             uint64_t cmd, unsigned long payload,
                             const struct gcl_host_ops *ops)
 {
 	int th;
 
+	if (slot < 0)
+		slot = p->thread_count ? (int)(hash % p->thread_count) : 0;
 	if (gpu_thread >= 0) {
 		th = gpu_thread;
 	} else if (p->active_thread_count > 0) {
-		th = p->flow_tbl[hash % p->thread_count];
+		th = p->flow_tbl[slot];
 	} else {
 		if (ops && ops->sched_add_core)
 			ops->sched_add_core(ops->arg, p);
 		if (p->active_thread_count == 0)
 			th = p->idle_top;
 		else
-			th = p->flow_tbl[hash % p->thread_count];
+			th = p->flow_tbl[slot];
 	}
 	if (th < 0 || th >= p->thread_count || !p->rxq[th])
 		return false;
@@ -226,17 +230,23 @@ static bool send_to_runtime(struct gcl_host_proc *p, uint32_t hash, int gpu_thre
 	return gcl_lrpc_send(p->rxq[th], cmd, payload);
 }
 
-uint64_t gcl_host_deliver(struct gcl_host_proc *const *clients_by_id, uint32_t max_runtimes,
-                          struct gcl_host_proc *const *clients, int nr_clients,
-                          const struct gcl_verdict *v, const uint16_t *pkt_len,
-                          const uint8_t *olflags, uint8_t default_olflags,
-                          const uint64_t *shmptr, uint64_t n,
-                          const struct gcl_host_ops *ops, uint64_t *stats)
+/* One verdict stream, either format: @v8 (gcl_verdict) or @v4 (gcl_verdict4,
+ * whose broadcast hashes come from @bcast_hash). */
+static uint64_t deliver(struct gcl_host_proc *const *clients_by_id, uint32_t max_runtimes,
+                        struct gcl_host_proc *const *clients, int nr_clients,
+                        const struct gcl_verdict *v8, const struct gcl_verdict4 *v4,
+                        const uint32_t *bcast_hash, const uint16_t *pkt_len,
+                        const uint8_t *olflags, uint8_t default_olflags,
+                        const uint64_t *shmptr, uint64_t n,
+                        const struct gcl_host_ops *ops, uint64_t *stats)
 {
 	uint64_t delivered = 0;
 
 	for (uint64_t i = 0; i < n; i++) {
-		uint8_t act = v[i].action & GCL_ACT_MASK;
+		const uint16_t uniqid = v8 ? v8[i].uniqid : v4[i].uniqid;
+		const uint8_t thread = v8 ? v8[i].thread : v4[i].thread;
+		const uint8_t act = (v8 ? v8[i].action : v4[i].action) & GCL_ACT_MASK;
+		const uint32_t hash = v8 ? v8[i].hash : (bcast_hash ? bcast_hash[i] : 0);
 		uint8_t fl = olflags ? olflags[i] : default_olflags;
 		uint64_t cmd = gcl_rx_make_cmd(pkt_len ? pkt_len[i] : 0, fl);
 		unsigned long payload = shmptr ? shmptr[i] : 0;
@@ -244,10 +254,11 @@ uint64_t gcl_host_deliver(struct gcl_host_proc *const *clients_by_id, uint32_t m
 		bool ok;
 
 		if (act == GCL_ACT_DELIVER || act == GCL_ACT_WAKE) {
-			if (v[i].uniqid < max_runtimes)
-				p = clients_by_id[v[i].uniqid];
-			ok = p && send_to_runtime(p, v[i].hash,
-			                          act == GCL_ACT_DELIVER ? v[i].thread : -1,
+			if (uniqid < max_runtimes)
+				p = clients_by_id[uniqid];
+			ok = p && send_to_runtime(p, hash,
+			                          act == GCL_ACT_WAKE && v4 ? (int)thread : -1,
+			                          act == GCL_ACT_DELIVER ? (int)thread : -1,
 			                          cmd, payload, ops);
 			if (ok) {
 				delivered++;
@@ -259,7 +270,7 @@ uint64_t gcl_host_deliver(struct gcl_host_proc *const *clients_by_id, uint32_t m
 		} else if (act == GCL_ACT_BROADCAST) {
 			int n_sent = 0;
 			for (int c = 0; c < nr_clients; c++) {
-				if (send_to_runtime(clients[c], v[i].hash, -1, cmd, payload, ops)) {
+				if (send_to_runtime(clients[c], hash, -1, -1, cmd, payload, ops)) {
 					n_sent++;
 					if (ops && ops->owned)
 						ops->owned(ops->arg, clients[c], i);
@@ -292,4 +303,26 @@ uint64_t gcl_host_deliver(struct gcl_host_proc *const *clients_by_id, uint32_t m
 		stats[GCL_RX_UNHANDLED]++;
 	}
 	return delivered;
+}
+
+uint64_t gcl_host_deliver(struct gcl_host_proc *const *clients_by_id, uint32_t max_runtimes,
+                          struct gcl_host_proc *const *clients, int nr_clients,
+                          const struct gcl_verdict *v, const uint16_t *pkt_len,
+                          const uint8_t *olflags, uint8_t default_olflags,
+                          const uint64_t *shmptr, uint64_t n,
+                          const struct gcl_host_ops *ops, uint64_t *stats)
+{
+	return deliver(clients_by_id, max_runtimes, clients, nr_clients, v, NULL, NULL, pkt_len,
+	               olflags, default_olflags, shmptr, n, ops, stats);
+}
+
+uint64_t gcl_host_deliver4(struct gcl_host_proc *const *clients_by_id, uint32_t max_runtimes,
+                           struct gcl_host_proc *const *clients, int nr_clients,
+                           const struct gcl_verdict4 *v, const uint32_t *bcast_hash,
+                           const uint16_t *pkt_len, const uint8_t *olflags,
+                           uint8_t default_olflags, const uint64_t *shmptr, uint64_t n,
+                           const struct gcl_host_ops *ops, uint64_t *stats)
+{
+	return deliver(clients_by_id, max_runtimes, clients, nr_clients, NULL, v, bcast_hash,
+	               pkt_len, olflags, default_olflags, shmptr, n, ops, stats);
 }

@@ -33,6 +33,7 @@ constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 constexpr uint32_t kToepBytes = 12 * 256 * 4;
 constexpr uint32_t kCrcBytes = 8 * 256 * 4;
 constexpr uint32_t kLdsTableBudget = 96 * 1024;
+constexpr int kImgUsers = 8;             /* streams tracked per table image */
 constexpr uint32_t kLdsQueueBytes = 16; /* s_next[2] after the header tile */
 constexpr int kDefaultSched = 0; /* GCL_TUNE_SCHED default: static persistent grid */
 
@@ -312,11 +313,16 @@ __device__ __forceinline__ void classify_one(const KParams &k, const uint4 *tile
 		uniq = (uint32_t)p;
 		if (k.ablate & 8) {
 			thr = hash & 7;
-		} else if (re.active) {
-			const uint64_t M = (uint64_t)re.m_hi << 32 | re.m_lo;
-			thr = tb.flow[re.flow_off + gcl::fastmod(hash, M, re.tc)];
 		} else {
-			action |= GCL_ACT_WAKE;
+			const uint64_t M = (uint64_t)re.m_hi << 32 | re.m_lo;
+			const uint32_t slot = gcl::fastmod(hash, M, re.tc);
+			if (re.active) {
+				thr = tb.flow[re.flow_off + slot];
+			} else {
+				action |= GCL_ACT_WAKE;
+				if (k.cflags & GCL_CFG_VERDICT4)
+					thr = slot; /* the host replays flow_tbl[slot] */
+			}
 		}
 		if (!(k.ablate & 4))
 			atomicAdd(&hist[p], 1u);
@@ -339,11 +345,16 @@ __device__ __forceinline__ void classify_one(const KParams &k, const uint4 *tile
 		}
 		k.trans[idx] = tr;
 	}
-	const u32x2 vd = {hash, uniq | thr << 16 | action << 24};
-	if (k.nt_store)
-		__builtin_nontemporal_store(vd, (u32x2 *)&k.verdicts[idx]);
-	else
-		*(u32x2 *)&k.verdicts[idx] = vd;
+	const uint32_t vlo = uniq | thr << 16 | action << 24;
+	if (k.cflags & GCL_CFG_VERDICT4) {
+		((uint32_t *)k.verdicts)[idx] = vlo;
+	} else {
+		const u32x2 vd = {hash, vlo};
+		if (k.nt_store)
+			__builtin_nontemporal_store(vd, (u32x2 *)&k.verdicts[idx]);
+		else
+			*(u32x2 *)&k.verdicts[idx] = vd;
+	}
 }
 
 template <int NT>
@@ -700,12 +711,22 @@ struct gcl_ctx {
 	uint32_t off_rt, off_flow, off_toep, off_seed, off_crc, image_cap, image_bytes;
 	uint32_t flow_used;
 	bool dirty;
-	/* two device images + pinned staging, each guarded by an event */
+	/* Two device images + pinned staging.  No per-launch events: each image
+	 * remembers the streams that launched on it; when it stops being current
+	 * an event is recorded on each of them, and the upload that next
+	 * overwrites it waits on those events. */
 	uint8_t *dimg[2];
-	hipEvent_t img_free[2];
+	struct ImgUsers {
+		int n;
+		bool retired; /* events recorded, image not current */
+		hipStream_t st[kImgUsers];
+		hipEvent_t ev[kImgUsers];
+	} users[2];
 	uint8_t *staging;
 	hipEvent_t staging_free;
 	hipEvent_t tables_ready;   /* recorded after each table upload */
+	hipStream_t tables_stream; /* stream of the last upload */
+	bool tables_done;          /* tables_ready known complete */
 	/* end-to-end (host buffers) resources, allocated on first use */
 	struct E2E {
 		int nstreams;
@@ -713,7 +734,7 @@ struct gcl_ctx {
 		hipStream_t st[4];
 		uint8_t *slab[4];        /* header granules of one chunk */
 		uint8_t *side[4];        /* per-packet olflags/rss/fdir of one chunk */
-		struct gcl_verdict *verd[4];
+		uint8_t *verd[4];        /* verdicts of one chunk (sized for 8-B verdicts) */
 		uint64_t *acc;           /* device counts | stats */
 	} e2e;
 	int cur;
@@ -820,12 +841,17 @@ extern "C" int gcl_open(int hip_device, const struct gcl_cfg *cfg, struct gcl_ct
 	for (int i = 0; i < 2; i++) {
 		if (hipMalloc(&c->dimg[i], c->image_cap) != hipSuccess)
 			goto fail;
-		hipEventCreateWithFlags(&c->img_free[i], hipEventDisableTiming);
+		c->users[i].n = 0;
+		c->users[i].retired = false;
+		for (int j = 0; j < kImgUsers; j++)
+			hipEventCreateWithFlags(&c->users[i].ev[j], hipEventDisableTiming);
 	}
 	if (hipHostMalloc(&c->staging, c->image_cap, hipHostMallocDefault) != hipSuccess)
 		goto fail;
 	hipEventCreateWithFlags(&c->staging_free, hipEventDisableTiming);
 	hipEventCreateWithFlags(&c->tables_ready, hipEventDisableTiming);
+	c->tables_stream = nullptr;
+	c->tables_done = true;
 	memset(&c->e2e, 0, sizeof(c->e2e));
 	*out = c;
 	return 0;
@@ -847,7 +873,8 @@ extern "C" void gcl_close(struct gcl_ctx *c)
 	hipDeviceSynchronize();
 	for (int i = 0; i < 2; i++) {
 		hipFree(c->dimg[i]);
-		hipEventDestroy(c->img_free[i]);
+		for (int j = 0; j < kImgUsers; j++)
+			hipEventDestroy(c->users[i].ev[j]);
 	}
 	hipHostFree(c->staging);
 	hipEventDestroy(c->staging_free);
@@ -1129,27 +1156,72 @@ static Geometry choose_geometry(const gcl_ctx *c, uint32_t tab_lds, uint32_t his
 	return g;
 }
 
-/* Upload a new table snapshot on @s if anything changed; launches on any
- * stream wait for c->tables_ready before reading the image. */
+/* Note that a launch on @s reads the current image.  With more streams than
+ * kImgUsers, the new stream takes over the oldest one's slot after waiting
+ * for what that stream has queued so far, so the slot still covers it. */
+static void image_used(gcl_ctx *c, hipStream_t s)
+{
+	gcl_ctx::ImgUsers &u = c->users[c->cur];
+	for (int i = 0; i < u.n; i++)
+		if (u.st[i] == s)
+			return;
+	if (u.n == kImgUsers) {
+		hipEventRecord(u.ev[0], u.st[0]);
+		hipStreamWaitEvent(s, u.ev[0], 0);
+		u.st[0] = s;
+		return;
+	}
+	u.st[u.n++] = s;
+}
+
+/* Upload a new table snapshot on @s if anything changed; launches on other
+ * streams wait for c->tables_ready before reading the image. */
 static int upload_tables(gcl_ctx *c, hipStream_t s)
 {
 	if (!c->dirty)
 		return 0;
 	hipEventSynchronize(c->staging_free);
 	uint32_t bytes = build_image(c);
-	int nxt = c->cur ^ 1;
-	hipStreamWaitEvent(s, c->img_free[nxt], 0);
+	const int nxt = c->cur ^ 1;
+	/* the image about to be overwritten: wait for its last readers */
+	gcl_ctx::ImgUsers &old = c->users[nxt];
+	if (old.retired)
+		for (int i = 0; i < old.n; i++)
+			if (old.st[i] != s)
+				hipStreamWaitEvent(s, old.ev[i], 0);
+	old.n = 0;
+	old.retired = false;
+	/* the image going out of use: mark where each of its streams is */
+	gcl_ctx::ImgUsers &cur = c->users[c->cur];
+	for (int i = 0; i < cur.n; i++)
+		hipEventRecord(cur.ev[i], cur.st[i]);
+	cur.retired = true;
 	if (hipMemcpyAsync(c->dimg[nxt], c->staging, bytes, hipMemcpyHostToDevice, s) != hipSuccess)
 		return -EIO;
 	hipEventRecord(c->staging_free, s);
 	hipEventRecord(c->tables_ready, s);
+	c->tables_stream = s;
+	c->tables_done = false;
 	c->cur = nxt;
 	c->dirty = false;
 	return 0;
 }
 
+/* Order a launch on @s after the last table upload: free on the upload's own
+ * stream, and skipped once the upload is known to have completed. */
+static void wait_tables(gcl_ctx *c, hipStream_t s)
+{
+	if (c->tables_done || s == c->tables_stream)
+		return;
+	if (hipEventQuery(c->tables_ready) == hipSuccess) {
+		c->tables_done = true;
+		return;
+	}
+	hipStreamWaitEvent(s, c->tables_ready, 0);
+}
+
 extern "C" int gcl_classify(struct gcl_ctx *c, const struct gcl_batch *b,
-                            struct gcl_verdict *verdicts, uint64_t *runtime_counts,
+                            void *verdicts, uint64_t *runtime_counts,
                             uint64_t *stats, void *hip_stream)
 {
 	struct gcl_out o = {verdicts, runtime_counts, stats, nullptr};
@@ -1161,7 +1233,7 @@ extern "C" int gcl_classify_ex(struct gcl_ctx *c, const struct gcl_batch *b,
 {
 	if (!c || !b || !out)
 		return -EINVAL;
-	struct gcl_verdict *verdicts = out->verdicts;
+	void *verdicts = out->verdicts;
 	uint64_t *runtime_counts = out->runtime_counts, *stats = out->stats;
 	if (out->trans && !(c->cfg.flags & GCL_CFG_TRANS_HASH))
 		return -EINVAL;
@@ -1176,7 +1248,7 @@ extern "C" int gcl_classify_ex(struct gcl_ctx *c, const struct gcl_batch *b,
 
 	if (upload_tables(c, s))
 		return -EIO;
-	hipStreamWaitEvent(s, c->tables_ready, 0);
+	wait_tables(c, s);
 
 	KParams k = {};
 	k.frames = b->frames;
@@ -1252,7 +1324,7 @@ extern "C" int gcl_classify_ex(struct gcl_ctx *c, const struct gcl_batch *b,
 		hipEventRecord(e1, s);
 		c->ev_pending.push_back({e0, e1});
 	}
-	hipEventRecord(c->img_free[c->cur], s);
+	image_used(c, s);
 	if (slot >= 0) {
 		hipEventRecord(c->sched_ev[slot], s);
 		c->sched_used[slot] = true;
@@ -1407,7 +1479,7 @@ static void *mapped(const void *h)
 }
 
 extern "C" int gcl_classify_host(struct gcl_ctx *c, const struct gcl_batch *hb,
-                                 struct gcl_verdict *host_verdicts, uint64_t *host_counts,
+                                 void *host_verdicts, uint64_t *host_counts,
                                  uint64_t *host_stats, const struct gcl_e2e_opts *o)
 {
 	if (!c || !hb || !host_verdicts || !o || o->mode > GCL_E2E_ZEROCOPY)
@@ -1416,6 +1488,7 @@ extern "C" int gcl_classify_host(struct gcl_ctx *c, const struct gcl_batch *hb,
 		return 0;
 	hipSetDevice(c->device);
 	const uint32_t max_rt = c->cfg.max_runtimes;
+	const uint64_t vsize = (c->cfg.flags & GCL_CFG_VERDICT4) ? 4 : 8;
 	int nst = o->nstreams ? (int)o->nstreams : 2;
 	if (nst > 4)
 		nst = 4;
@@ -1445,7 +1518,7 @@ extern "C" int gcl_classify_host(struct gcl_ctx *c, const struct gcl_batch *hb,
 		db.rss = (const uint32_t *)mapped(hb->rss);
 		db.fdir_hi = (const uint32_t *)mapped(hb->fdir_hi);
 		db.dst_hint = (const uint32_t *)mapped(hb->dst_hint);
-		struct gcl_verdict *dv = (struct gcl_verdict *)mapped(host_verdicts);
+		void *dv = mapped(host_verdicts);
 		if (!db.frames || !dv || (hb->offs && !db.offs) || (hb->olflags && !db.olflags) ||
 		    (hb->rss && !db.rss) || (hb->fdir_hi && !db.fdir_hi) ||
 		    (hb->dst_hint && !db.dst_hint)) {
@@ -1497,14 +1570,13 @@ extern "C" int gcl_classify_host(struct gcl_ctx *c, const struct gcl_batch *hb,
 				db.dst_hint = (const uint32_t *)(side + 9 * chunk);
 			}
 			ret = gcl_classify(c, &db, e.verd[i], dcounts, dstats, st);
-			hipMemcpyAsync(host_verdicts + s, e.verd[i], m * sizeof(struct gcl_verdict),
+			hipMemcpyAsync((uint8_t *)host_verdicts + s * vsize, e.verd[i], m * vsize,
 			               hipMemcpyDeviceToHost, st);
 		}
 		for (int i = 1; i < nst; i++) {
 			hipEventRecord(ready, e.st[i]);
 			hipStreamWaitEvent(s0, ready, 0);
 		}
-		hipEventRecord(c->img_free[c->cur], s0);
 	}
 	uint64_t tmp[GCL_MAX_PROC + GCL_NR_STATS];
 	hipMemcpyAsync(tmp, e.acc, (max_rt + GCL_NR_STATS) * 8, hipMemcpyDeviceToHost, s0);

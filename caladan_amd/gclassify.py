@@ -24,7 +24,7 @@ GCL_RX_BURST_SIZE = 64
 HASH_NIC, HASH_JENKINS, HASH_TOEPLITZ = 0, 1, 2
 HASH_MODES = {"nic": HASH_NIC, "jenkins": HASH_JENKINS, "toeplitz": HASH_TOEPLITZ}
 
-CFG_AZURE_ARP, CFG_HASH16, CFG_PROFILE, CFG_TRANS_HASH = 0x1, 0x2, 0x4, 0x8
+CFG_AZURE_ARP, CFG_HASH16, CFG_PROFILE, CFG_TRANS_HASH, CFG_VERDICT4 = 0x1, 0x2, 0x4, 0x8, 0x10
 
 F_RSS_HASH, F_FDIR_ID = 0x01, 0x02
 F_IP_CKSUM_MASK, F_IP_CKSUM_UNKNOWN, F_IP_CKSUM_BAD = 0x0C, 0x00, 0x04
@@ -51,6 +51,8 @@ CALADAN_RSS_KEY = bytes([
     0x0D, 0x6D, 0x86, 0xBA, 0x61, 0x78, 0xEB])
 
 VERDICT_DTYPE = np.dtype([("hash", "<u4"), ("uniqid", "<u2"), ("thread", "u1"), ("action", "u1")])
+# GCL_CFG_VERDICT4: WAKE verdicts carry the flow_tbl slot (hash % thread_count) in `thread`
+VERDICT4_DTYPE = np.dtype([("uniqid", "<u2"), ("thread", "u1"), ("action", "u1")])
 TRANS_DTYPE = np.dtype([("h5", "<u4"), ("h3", "<u4")])
 
 
@@ -181,6 +183,8 @@ def _load():
         "gcl_pcap_free": (None, [ctypes.POINTER(GclTrace)]),
         "gcl_host_deliver": (u64, [vp, u32, vp, i32, vp, vp, vp, ctypes.c_uint8, vp, u64,
                                    ctypes.POINTER(GclHostOps), vp]),
+        "gcl_host_deliver4": (u64, [vp, u32, vp, i32, vp, vp, vp, vp, ctypes.c_uint8, vp, u64,
+                                    ctypes.POINTER(GclHostOps), vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -364,6 +368,7 @@ class Classifier:
             cfg.rss_key[i] = key[i]
         self.cfg = cfg
         self.max_runtimes = max_runtimes
+        self.vbytes = 4 if flags & CFG_VERDICT4 else 8  # bytes per verdict
         self._ctx = ctypes.c_void_p()
         _check(lib.gcl_open(device, ctypes.byref(cfg), ctypes.byref(self._ctx)), "gcl_open")
 
@@ -396,7 +401,7 @@ class Classifier:
                  olflags=None, rss=None, fdir_hi=None, frames_len=None, stream=None,
                  dst_hint=None, trans=None):
         """Launch the classify kernel on device buffers (asynchronous)."""
-        if verdicts is not None and _nbytes(verdicts) < 8 * n:
+        if verdicts is not None and _nbytes(verdicts) < self.vbytes * n:
             raise ValueError("verdict buffer too small")
         if counts is not None and _nbytes(counts) < 8 * self.max_runtimes:
             raise ValueError("counts buffer too small")
@@ -420,6 +425,8 @@ class Classifier:
                       olflags=None, rss=None, fdir_hi=None, offs=None, frames_len=None,
                       mode=E2E_COPY, nstreams=2, chunk=1 << 20, dst_hint=None):
         """End-to-end: host (pinned) frames in, host verdicts out (synchronous)."""
+        if verdicts is not None and _nbytes(verdicts) < self.vbytes * n:
+            raise ValueError("verdict buffer too small")
         b = GclBatch(frames=_ptr(frames),
                      frames_len=_nbytes(frames) if frames_len is None else frames_len,
                      stride=stride, offs=_ptr(offs), olflags=_ptr(olflags), rss=_ptr(rss),

@@ -94,6 +94,21 @@ uint64_t gcl_host_deliver(struct gcl_host_proc *const *clients_by_id, uint32_t m
                           const uint64_t *shmptr, uint64_t n,
                           const struct gcl_host_ops *ops, uint64_t *stats);
 
+/*
+ * gcl_host_deliver4 - the same over compact verdicts (GCL_CFG_VERDICT4).  A
+ * WAKE verdict's @thread is the flow_tbl slot (hash % thread_count).
+ * @bcast_hash     per-packet hash for GCL_ACT_BROADCAST fan-out: in
+ *                 GCL_HASH_NIC mode the mbuf hash.rss array the batch was
+ *                 classified with (masked to 16 bits under GCL_CFG_HASH16);
+ *                 NULL in the computed modes, where ARP hashes to 0.
+ */
+uint64_t gcl_host_deliver4(struct gcl_host_proc *const *clients_by_id, uint32_t max_runtimes,
+                           struct gcl_host_proc *const *clients, int nr_clients,
+                           const struct gcl_verdict4 *v, const uint32_t *bcast_hash,
+                           const uint16_t *pkt_len, const uint8_t *olflags,
+                           uint8_t default_olflags, const uint64_t *shmptr, uint64_t n,
+                           const struct gcl_host_ops *ops, uint64_t *stats);
+
 #ifdef __cplusplus
 }
 #endif

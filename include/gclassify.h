@@ -85,6 +85,8 @@ enum gcl_hash_mode {
 #define GCL_CFG_PROFILE    0x4  /* record HIP events around every classify kernel */
 #define GCL_CFG_TRANS_HASH 0x8  /* also compute the destination runtime's transport
                                    demux hashes (gcl_classify_ex, struct gcl_trans) */
+#define GCL_CFG_VERDICT4   0x10 /* write 4-byte struct gcl_verdict4 instead of
+                                   struct gcl_verdict (see there) */
 
 struct gcl_cfg {
 	uint32_t max_runtimes;    /* uniqids must be < max_runtimes (<= GCL_MAX_PROC) */
@@ -143,6 +145,23 @@ struct gcl_verdict {
 };
 
 /*
+ * Compact verdict (GCL_CFG_VERDICT4): the last four bytes of gcl_verdict,
+ * without the hash.  rx_send_to_runtime uses the hash only as
+ * hash % thread_count (rx.c:57, :68), and thread_count is fixed per runtime,
+ * so a WAKE verdict carries that flow_tbl slot in @thread instead: the host
+ * replay indexes the flow_tbl as it stands after sched_add_core.  The only
+ * other use of the hash is the Azure ARP broadcast fan-out, where it is
+ * the mbuf's hash.rss in GCL_HASH_NIC mode and 0 in the computed modes (ARP
+ * is not hashed): gcl_host_deliver4 takes it from the caller.
+ */
+struct gcl_verdict4 {
+	uint16_t uniqid;  /* as gcl_verdict */
+	uint8_t  thread;  /* DELIVER: flow_tbl[hash % thread_count];
+	                     WAKE: hash % thread_count; otherwise GCL_NO_THREAD */
+	uint8_t  action;  /* as gcl_verdict */
+};
+
+/*
  * Counter slots; indices 0..5 keep the order of the reference enum
  * (iokernel/defs.h:421-426).  The device adds RX_PULLED, RX_FLOW_TAG_MATCH,
  * RX_HASH_MISSING, RX_UNREGISTERED_MAC and RX_UNHANDLED (for its drops); the
@@ -198,7 +217,7 @@ int gcl_steer_flows(uint16_t thread_count, const uint16_t *active_idx,
 
 /*
  * gcl_classify - classify @b->n packets on @hip_stream (NULL = null stream).
- * @verdicts       device gcl_verdict[n] (may be NULL: counters only)
+ * @verdicts       device gcl_verdict[n] (gcl_verdict4[n] with GCL_CFG_VERDICT4)
  * @runtime_counts device u64[max_runtimes], ACCUMULATED: packets steered to
  *                 each runtime (DELIVER + WAKE), may be NULL
  * @stats          device u64[GCL_NR_STATS], ACCUMULATED, may be NULL
@@ -206,7 +225,7 @@ int gcl_steer_flows(uint16_t thread_count, const uint16_t *active_idx,
  * Replaces the rx_one_pkt loop of rx_burst (rx.c:281-287).
  */
 int gcl_classify(struct gcl_ctx *ctx, const struct gcl_batch *b,
-                 struct gcl_verdict *verdicts, uint64_t *runtime_counts,
+                 void *verdicts, uint64_t *runtime_counts,
                  uint64_t *stats, void *hip_stream);
 
 /*
@@ -234,7 +253,7 @@ struct gcl_e2e_opts {
 };
 
 int gcl_classify_host(struct gcl_ctx *ctx, const struct gcl_batch *host_batch,
-                      struct gcl_verdict *host_verdicts, uint64_t *host_counts,
+                      void *host_verdicts, uint64_t *host_counts,
                       uint64_t *host_stats, const struct gcl_e2e_opts *opts);
 
 /* Pin + map host memory for ZEROCOPY / async copies (hipHostRegister). */
@@ -265,7 +284,7 @@ int gcl_runtime_set_trans_seed(struct gcl_ctx *ctx, uint16_t uniqid, uint32_t se
 
 /* All outputs of one classify launch (device pointers; NULL = not wanted). */
 struct gcl_out {
-	struct gcl_verdict *verdicts;    /* required */
+	void *verdicts;                  /* required: gcl_verdict[n] or gcl_verdict4[n] */
 	uint64_t *runtime_counts;        /* accumulated */
 	uint64_t *stats;                 /* accumulated */
 	struct gcl_trans *trans;         /* GCL_CFG_TRANS_HASH only */

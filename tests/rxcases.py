@@ -147,3 +147,15 @@ def fuzz_batch(rng, n, runtimes, max_runtimes, slot=128, tail_runts=True):
             offs[n - 1 - j] = last + 16 * j
         frames_len = last + 16 * 2 + 40
     return frames, frames_len, offs, olflags, rss, fdir, hint
+
+
+def to_verdict4(v, thread_count):
+    """8-B verdicts -> the GCL_CFG_VERDICT4 form: drop the hash; a WAKE
+    verdict carries its flow_tbl slot, hash % thread_count (rx.c:57, :68).
+    thread_count maps uniqid -> thread_count (dict or array)."""
+    from caladan_amd.gclassify import VERDICT4_DTYPE
+    out = np.zeros(len(v), dtype=VERDICT4_DTYPE)
+    out["uniqid"], out["thread"], out["action"] = v["uniqid"], v["thread"], v["action"]
+    for i in np.nonzero((v["action"] & 0x3F) == 1)[0]:
+        out["thread"][i] = int(v["hash"][i]) % int(thread_count[int(v["uniqid"][i])])
+    return out

@@ -277,3 +277,67 @@ def test_host_deliver_broadcast_and_arp(g):
     # rx.c:200-207: a failed ARP response counts as unregistered + unhandled
     assert calls == [1, 2]
     assert stats[0] == 1 and stats[4] == 1
+
+
+def test_host_deliver4_matches_deliver(g, orc):
+    """Compact verdicts replay exactly like 8-B ones: same rings, counters and
+    frees, including wakes that change the flow_tbl mid-batch and broadcasts
+    fanned out with the caller's hashes."""
+    from tests.rxcases import fuzz_batch, random_runtimes, to_verdict4
+    rng = np.random.default_rng(12)
+    R = 64
+    rts = random_runtimes(rng, R, 24, max_threads=6)
+    n = 3000
+    frames, flen, offs, olf, rss, fdir, _ = fuzz_batch(rng, n, rts, R, tail_runts=False)
+    t = orc.Tables(R, 0, 0x1, 0x09)  # NIC hash, Azure ARP: broadcasts too
+    for r in rts:
+        assert t.runtime_set(r["uniqid"], r["ip"], r["thread_count"], r["active"], r["flow_tbl"]) == 0
+    v, _, _ = t.classify(frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir_hi=fdir, frames_len=flen)
+    assert ((v["action"] & 0x3F) == g.ACT_WAKE).any() and ((v["action"] & 0x3F) == g.ACT_BROADCAST).any()
+    v4 = to_verdict4(v, {r["uniqid"]: r["thread_count"] for r in rts})
+    pkt_len = rng.integers(60, 1515, size=n).astype(np.uint16)
+    shm = offs.astype(np.uint64)
+    bhash = rss.astype(np.uint32)  # NIC mode: the hash is hash.rss whatever the flags
+
+    def run(compact):
+        procs, rings, keep = _host_procs(g, rts, 8)
+        by_id = (ctypes.c_void_p * R)()
+        for u, p in procs.items():
+            by_id[u] = ctypes.addressof(p)
+        clients = (ctypes.c_void_p * len(procs))(*[ctypes.addressof(p) for p in procs.values()])
+        events = []
+
+        @g.SCHED_ADD_CORE_FN
+        def add_core(arg, pp):
+            p = pp.contents
+            if p.active_thread_count == 0:
+                p.active_thread_count = 1
+                for i in range(p.thread_count):
+                    p.flow_tbl[i] = p.thread_count - 1
+                events.append(("wake", p.uniqid))
+
+        @g.FREE_PKT_FN
+        def free_pkt(arg, i):
+            events.append(("free", i))
+
+        @g.REFCNT_FN
+        def refcnt(arg, i, d):
+            events.append(("ref", i, d))
+
+        ops = g.GclHostOps()
+        ops.sched_add_core, ops.free_pkt, ops.refcnt_update = add_core, free_pkt, refcnt
+        stats = np.zeros(8, dtype=np.uint64)
+        if compact:
+            d = g.lib.gcl_host_deliver4(by_id, R, clients, len(procs), v4.ctypes.data,
+                                        bhash.ctypes.data, pkt_len.ctypes.data, olf.ctypes.data,
+                                        0x09, shm.ctypes.data, n, ctypes.byref(ops),
+                                        stats.ctypes.data)
+        else:
+            d = g.lib.gcl_host_deliver(by_id, R, clients, len(procs), v.ctypes.data,
+                                       pkt_len.ctypes.data, olf.ctypes.data, 0x09,
+                                       shm.ctypes.data, n, ctypes.byref(ops), stats.ctypes.data)
+        return d, list(stats), events, {k: r.drain() for k, r in rings.items()}
+
+    full, compact = run(False), run(True)
+    assert full[0] > 0 and any(e[0] == "wake" for e in full[2])
+    assert full == compact

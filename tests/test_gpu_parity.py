@@ -4,6 +4,7 @@ import numpy as np
 import pytest
 
 from tests.rxcases import (apply_runtimes, apply_seeds, fuzz_batch, random_runtimes, scenario_batch,
+                           to_verdict4,
                            scenario_sets, scenario_trans)
 
 pytestmark = pytest.mark.gpu
@@ -26,7 +27,7 @@ def dev(a):
 def gpu_run(g, clf, frames, n, stride=0, offs=None, olflags=None, rss=None, fdir=None,
             frames_len=None, counts=None, stats=None, hint=None, trans=False):
     f = dev(frames.view(np.uint8))
-    v = torch.zeros(n * 8, dtype=torch.uint8, device="cuda")
+    v = torch.zeros(n * clf.vbytes, dtype=torch.uint8, device="cuda")
     c = counts if counts is not None else torch.zeros(clf.max_runtimes, dtype=torch.int64, device="cuda")
     s = stats if stats is not None else torch.zeros(g.NR_STATS, dtype=torch.int64, device="cuda")
     o = dev(offs.astype(np.int64)) if offs is not None else None
@@ -37,7 +38,7 @@ def gpu_run(g, clf, frames, n, stride=0, offs=None, olflags=None, rss=None, fdir
                  frames_len=frames_len,
                  dst_hint=dev(hint.view(np.int32)) if hint is not None else None)
     torch.cuda.synchronize()
-    res = (v.cpu().numpy().view(g.VERDICT_DTYPE), c.cpu().numpy().astype(np.uint64),
+    res = (v.cpu().numpy().view(g.VERDICT_DTYPE if clf.vbytes == 8 else g.VERDICT4_DTYPE), c.cpu().numpy().astype(np.uint64),
            s.cpu().numpy().astype(np.uint64))
     if trans:
         res += (tr.cpu().numpy().view(g.TRANS_DTYPE),)
@@ -107,6 +108,31 @@ def test_gpu_fuzz_vs_oracle(g, orc, mode, flags, max_rt):
     assert_same(v, ve, f"mode={mode} flags={flags} R={max_rt}")
     assert (c == ce).all()
     assert (st == se).all(), (st, se)
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("flags", [1, 2])
+@pytest.mark.parametrize("max_rt", [16, 1024])
+def test_gpu_fuzz_verdict4(g, orc, mode, flags, max_rt):
+    """GCL_CFG_VERDICT4: the same verdicts without the hash, WAKE carrying
+    its flow_tbl slot (hash % thread_count)."""
+    rng = np.random.default_rng(7000 + 1000 * mode + 10 * flags + max_rt)
+    rts = random_runtimes(rng, max_rt, min(max_rt, 40 if max_rt == 16 else 300))
+    n = 5000
+    frames, flen, offs, olf, rss, fdir, hint = fuzz_batch(rng, n, rts, max_rt)
+    key = bytes(rng.integers(0, 256, size=40, dtype=np.uint8))
+    t = orc.Tables(max_rt, mode, flags, 0x09, key)
+    apply_runtimes(t, rts)
+    clf = g.Classifier(0, max_rt, mode, flags | g.CFG_VERDICT4, 0x09, key)
+    apply_runtimes(clf, rts)
+    ve, ce, se = t.classify(frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir_hi=fdir,
+                            frames_len=flen, dst_hint=hint)
+    v, c, st = gpu_run(g, clf, frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir=fdir,
+                       frames_len=flen, hint=hint)
+    assert ((ve["action"] & 0x3F) == g.ACT_WAKE).any()
+    exp = to_verdict4(ve, {r["uniqid"]: r["thread_count"] for r in rts})
+    assert_same(v, exp, f"verdict4 mode={mode} flags={flags} R={max_rt}")
+    assert (c == ce).all() and (st == se).all()
 
 
 @pytest.mark.parametrize("wl,stride,R", [(0, 64, 16), (1, 1536, 1024), (2, 9216, 16)])
@@ -199,6 +225,43 @@ def test_gpu_table_updates_between_batches(g, orc):
         assert_same(v.cpu().numpy().view(g.VERDICT_DTYPE), ve)
         assert (c.cpu().numpy().astype(np.uint64) == ce).all()
         assert (s.cpu().numpy().astype(np.uint64) == se).all()
+
+
+def test_gpu_table_images_across_streams(g, orc):
+    """Double-buffered table images with launches in flight on another stream.
+
+    Stream A is held back by a bounded spin, then classifies with tables v0.
+    Meanwhile two updates classify on stream B, so the second upload overwrites
+    the image A's launch reads: it must wait for that launch.  A final launch
+    on A after the updates must wait for B's upload and see v2."""
+    n, R = 50000, 16
+    frames, _, _ = orc.generate(0, n, 64, R)
+    t = orc.Tables(R, 1, 0, 0x09)
+    clf = g.Classifier(0, R, 1)
+    for r in range(R):
+        t.runtime_set(r, orc.runtime_ip(r), 4, 4, [0, 1, 2, 3])
+        clf.runtime_set(r, g.runtime_ip(r), 4, 4, [0, 1, 2, 3])
+    f = dev(frames)
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    bufs = [torch.zeros(n * 8, dtype=torch.uint8, device="cuda") for _ in range(4)]
+    torch.cuda.synchronize()
+    with torch.cuda.stream(sa):
+        torch.cuda._sleep(200_000_000)  # ~80 ms of GPU spin, then the v0 launch
+    clf.classify(f, n, 64, verdicts=bufs[0], stream=sa.cuda_stream)
+    clf.runtime_set(3, g.runtime_ip(3), 3, 0, None)
+    clf.classify(f, n, 64, verdicts=bufs[1], stream=sb.cuda_stream)      # v1 -> image 1
+    clf.runtime_set(5, g.runtime_ip(5), 7, 2, orc.steer_flows(7, [4, 1]))
+    clf.classify(f, n, 64, verdicts=bufs[2], stream=sb.cuda_stream)      # v2 -> image 0
+    clf.classify(f, n, 64, verdicts=bufs[3], stream=sa.cuda_stream)      # v2, on A
+    torch.cuda.synchronize()
+    exp = [t.classify(frames, n, 64)[0]]
+    t.runtime_set(3, orc.runtime_ip(3), 3, 0, None)
+    exp.append(t.classify(frames, n, 64)[0])
+    t.runtime_set(5, orc.runtime_ip(5), 7, 2, orc.steer_flows(7, [4, 1]))
+    exp.append(t.classify(frames, n, 64)[0])
+    exp.append(exp[2])
+    for i, (v, ve) in enumerate(zip(bufs, exp)):
+        assert_same(v.cpu().numpy().view(g.VERDICT_DTYPE), ve, f"launch {i}")
 
 
 def test_gpu_counts_accumulate_and_edge_sizes(g, orc):
@@ -303,6 +366,28 @@ def test_gpu_end_to_end_host_buffers(g, orc, mode, wl, stride, R, T, arrays):
     clf.classify_host(hf, n, stride, verdicts=hv, counts=counts, stats=stats, mode=mode,
                       chunk=65536 + 17, nstreams=3, **pk)
     assert_same(hv.numpy().view(g.VERDICT_DTYPE), ve, f"e2e mode={mode}")
+    assert (counts == ce).all() and (stats == se).all()
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_gpu_end_to_end_verdict4(g, orc, mode):
+    """Both transports with 4-byte verdicts (half the verdict bytes on PCIe)."""
+    n, R, T = 300000, 16, 8
+    frames, olf, rss = orc.generate(0, n, 64, R)
+    t = orc.Tables(R, 1, 0, 0x09)
+    clf = g.Classifier(0, R, 1, g.CFG_VERDICT4)
+    for r in range(R):
+        fl = orc.steer_flows(T, list(range(r % T)))
+        t.runtime_set(r, orc.runtime_ip(r), T, r % T, fl if r % T else None)
+        clf.runtime_set(r, g.runtime_ip(r), T, r % T, fl if r % T else None)
+    ve, ce, se = t.classify(frames, n, 64)
+    hf = torch.from_numpy(frames).pin_memory()
+    hv = torch.zeros(n * 4, dtype=torch.uint8).pin_memory()
+    counts = np.zeros(R, dtype=np.uint64)
+    stats = np.zeros(8, dtype=np.uint64)
+    clf.classify_host(hf, n, 64, verdicts=hv, counts=counts, stats=stats, mode=mode,
+                      chunk=65536 + 17, nstreams=3)
+    assert_same(hv.numpy().view(g.VERDICT4_DTYPE), to_verdict4(ve, [T] * R), f"e2e4 mode={mode}")
     assert (counts == ce).all() and (stats == se).all()
 
 

@@ -3,7 +3,8 @@
 //
 //   cbench <workload> <steps> [cfg ...]
 //
-// Each cfg is "ABLATE:GRID:DEPTH:THREADS:BPC:SCHED" (GCL_TUNE_* knobs, 0 = default).
+// Each cfg is "ABLATE:GRID:DEPTH:THREADS:BPC:SCHED:V4" (GCL_TUNE_* knobs, 0 = default;
+// V4=1 classifies into 4-byte verdicts, GCL_CFG_VERDICT4).
 // CBENCH_NOISE_US=X co-runs, on a second stream, 32 one-wave blocks that each
 // spin for X us at the start of every classify launch (stand-in for an RCCL
 // kernel sharing the chip).  Rounds
@@ -77,7 +78,7 @@ __global__ void noise_kernel(unsigned us, unsigned long long *sink)
 
 struct Cfg {
 	std::string name;
-	int ablate, grid, depth, threads, bpc, sched;
+	int ablate, grid, depth, threads, bpc, sched, v4;
 	bool ref;
 	std::vector<double> us, wall;
 };
@@ -90,15 +91,15 @@ int main(int argc, char **argv)
 	const uint64_t stride = wl == GCL_WL_UDP64 ? 64 : 1536;
 	const uint32_t R = wl == GCL_WL_UDP64 ? 16 : 1024, T = wl == GCL_WL_UDP64 ? 8 : 4;
 	std::vector<Cfg> cfgs;
-	cfgs.push_back({"ref", 0, 0, 0, 0, 0, 0, true, {}, {}});
+	cfgs.push_back({"ref", 0, 0, 0, 0, 0, 0, 0, true, {}, {}});
 	for (int i = 3; i < argc; i++) {
-		Cfg c = {argv[i], 0, 0, 0, 0, 0, 0, false, {}, {}};
-		sscanf(argv[i], "%d:%d:%d:%d:%d:%d", &c.ablate, &c.grid, &c.depth, &c.threads, &c.bpc,
-		       &c.sched);
+		Cfg c = {argv[i], 0, 0, 0, 0, 0, 0, 0, false, {}, {}};
+		sscanf(argv[i], "%d:%d:%d:%d:%d:%d:%d", &c.ablate, &c.grid, &c.depth, &c.threads, &c.bpc,
+		       &c.sched, &c.v4);
 		cfgs.push_back(c);
 	}
 	if (cfgs.size() == 1)
-		cfgs.push_back({"default", 0, 0, 0, 0, 0, 0, false, {}, {}});
+		cfgs.push_back({"default", 0, 0, 0, 0, 0, 0, 0, false, {}, {}});
 	const char *pe = getenv("CBENCH_PROFILE");
 	const bool profile = !pe || atoi(pe) != 0; /* 0: no per-launch events, wall time only */
 	const char *ne = getenv("CBENCH_NOISE_US");
@@ -186,7 +187,7 @@ int main(int argc, char **argv)
 			struct gcl_cfg cfg = {};
 			cfg.max_runtimes = R;
 			cfg.hash_mode = GCL_HASH_JENKINS;
-			cfg.flags = profile ? GCL_CFG_PROFILE : 0;
+			cfg.flags = (profile ? GCL_CFG_PROFILE : 0) | (c.v4 ? GCL_CFG_VERDICT4 : 0);
 			cfg.default_olflags = GCL_F_RSS_HASH | GCL_F_IP_CKSUM_GOOD;
 			struct gcl_ctx *ctx;
 			if (gcl_open(0, &cfg, &ctx)) {
