@@ -48,9 +48,11 @@ WORKLOADS = {
     "mixed": (g.WL_MIXED, 1 << 20, 9216, 16, 8,
               "1Mi mixed frames (70% IPv4 TCP/UDP 64..9014B, 20% IPv6, 10% ARP), 9216B slots, 16 runtimes"),
 }
-# algorithmic bytes per packet: one 64-B header granule read + one 8-B verdict
-# written (DESIGN.md "Roofline"); tables and counters amortise to ~0.
-BYTES_PER_PKT = 64 + 8
+# algorithmic bytes per packet: one 64-B header granule read + one verdict
+# written, 8 B (gcl_verdict) or 4 B (gcl_verdict4) (DESIGN.md "Roofline");
+# tables and counters amortise to ~0.
+HDR_BYTES = 64
+VERDICT_BYTES = 4
 
 
 def log(*a):
@@ -102,15 +104,17 @@ def zero_fill(buf):
 
 
 class Workload:
-    def __init__(self, name, rank, world, device, hash_mode=g.HASH_JENKINS):
+    def __init__(self, name, rank, world, device, hash_mode=g.HASH_JENKINS, vbytes=VERDICT_BYTES):
         wl, n, stride, R, T, desc = WORKLOADS[name]
         self.name, self.wl, self.n, self.stride, self.R, self.T, self.desc = name, wl, n, stride, R, T, desc
+        self.vbytes = vbytes
+        self.bytes_per_pkt = HDR_BYTES + vbytes
         if os.environ.get("GCL_BENCH_TORCH_ALLOC") == "1":
             self.frames = torch.zeros(n * stride, dtype=torch.uint8, device=device)
-            self.verdicts = torch.empty(n * 8, dtype=torch.uint8, device=device)
+            self.verdicts = torch.empty(n * vbytes, dtype=torch.uint8, device=device)
         else:  # library-owned hipMalloc (gcl_dev_alloc), zeroed
             self.frames = g.DeviceBuffer(n * stride, device.index or 0)
-            self.verdicts = g.DeviceBuffer(n * 8, device.index or 0)
+            self.verdicts = g.DeviceBuffer(n * vbytes, device.index or 0)
             torch.cuda.synchronize()
             zero_fill(self.frames)
         self.counts = torch.zeros(R + g.NR_STATS, dtype=torch.int64, device=device)
@@ -122,7 +126,8 @@ class Workload:
             cdf_dev = torch.from_numpy(g.zipf_cdf(nflows, 0.99).view(np.int64)).to(device)
         g.generate(wl, n, stride, R, self.frames, seed=SEED, rank=rank, world=world,
                    shard_block=SHARD_BLOCK, zipf_cdf_dev=cdf_dev, nflows=nflows)
-        self.clf = g.Classifier(device.index or 0, R, hash_mode, g.CFG_PROFILE)
+        self.clf = g.Classifier(device.index or 0, R, hash_mode,
+                                g.CFG_PROFILE | (g.CFG_VERDICT4 if vbytes == 4 else 0))
         self.tables = setup_tables(self.clf, R, T)
         torch.cuda.synchronize()
 
@@ -240,10 +245,10 @@ def run_timed(w, steps, warmup, world, ex=None, profile_every=PROFILE_EVERY):
 
 
 def roofline(w, kernel_ms):
-    bytes_per_launch = w.n * BYTES_PER_PKT
+    bytes_per_launch = w.n * w.bytes_per_pkt
     achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
     traffic = None
-    prof = os.path.join(ROOT, "profiles", f"pmc_{w.name}.json")
+    prof = os.path.join(ROOT, "profiles", f"pmc_{w.name}{'_v4' if w.vbytes == 4 else ''}.json")
     if os.path.exists(prof):
         try:
             with open(prof) as f:
@@ -252,7 +257,7 @@ def roofline(w, kernel_ms):
             traffic = None
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "bytes_per_pkt": BYTES_PER_PKT, "kernel_ms": round(kernel_ms, 4)}
+            "bytes_per_pkt": w.bytes_per_pkt, "kernel_ms": round(kernel_ms, 4)}
 
 
 def e2e_bench(device, reps=3):
@@ -407,6 +412,8 @@ def main():
                     help="time one classify launch in N with HIP events (roofline.kernel_ms)")
     ap.add_argument("--exchange-every", type=int, default=EXCHANGE_EVERY,
                     help="steps per counts all_gather (multi-GPU exchange period)")
+    ap.add_argument("--verdict-bytes", type=int, default=VERDICT_BYTES, choices=[4, 8],
+                    help="8: struct gcl_verdict (with the hash); 4: struct gcl_verdict4")
     ap.add_argument("--force-exchange", action="store_true",
                     help="run the multi-GPU step (RCCL all_gather on a side stream) even at N=1")
     args = ap.parse_args()
@@ -423,7 +430,8 @@ def main():
     if dist_on:
         shard.init(rank, world, backend=args.dist_backend)
 
-    w = Workload(args.workload, rank, world, device)
+    vb = args.verdict_bytes
+    w = Workload(args.workload, rank, world, device, vbytes=vb)
     ex = Exchange(w, world, device, args.exchange_every) if dist_on else None
     el, kms = run_timed(w, args.steps, args.warmup, world, ex, max(1, args.profile_every))
     total_pkts = w.n * world * args.steps
@@ -451,6 +459,7 @@ def main():
         "config": {"workload": f"{args.workload}: {w.desc}", "pkts_per_gpu": w.n,
                    "slot_stride": w.stride, "runtimes": w.R, "kthreads": w.T,
                    "hash": "jenkins (lookup3 13-B 5-tuple)",
+                   "verdict": "gcl_verdict4, 4 B" if vb == 4 else "gcl_verdict, 8 B",
                    "parallelism": (f"dp{world}: round-robin 64Ki-pkt shards, {args.dist_backend} "
                                    f"all_gather of per-runtime counts every {args.exchange_every} step(s), overlapped"
                                    if dist_on else "single GPU")},
@@ -461,10 +470,18 @@ def main():
     torch.cuda.empty_cache()
 
     if world == 1 and not args.no_secondary and args.workload == "udp64":
-        w2 = Workload("tcp1500", rank, world, device)
+        # the same udp64 step with the other verdict format
+        w4 = Workload(args.workload, rank, world, device, vbytes=12 - vb)
+        el4, kms4 = run_timed(w4, args.steps, 3, 1)
+        other = {"verdict": "gcl_verdict, 8 B" if vb == 4 else "gcl_verdict4, 4 B",
+                 "value": round(w4.n * args.steps / el4 / 1e6, 1), "unit": "Mpkt/s",
+                 "ms_per_step": round(el4 / args.steps * 1e3, 4), "roofline": roofline(w4, kms4)}
+        del w4
+        torch.cuda.empty_cache()
+        w2 = Workload("tcp1500", rank, world, device, vbytes=vb)
         el2, kms2 = run_timed(w2, max(20, args.steps // 2), 3, 1)
         steps2 = max(20, args.steps // 2)
-        w3 = Workload("tcp1500_hsplit", rank, world, device)
+        w3 = Workload("tcp1500_hsplit", rank, world, device, vbytes=vb)
         el3, kms3 = run_timed(w3, steps2, 2, 1)
         hsplit = {"workload": f"tcp1500_hsplit: {w3.desc}",
                   "value": round(w3.n * steps2 / el3 / 1e6, 1), "unit": "Mpkt/s",
@@ -477,6 +494,7 @@ def main():
             "roofline": roofline(w2, kms2),
             "frame_bytes_rate_GBs": round(w2.n * 1500 / (kms2 * 1e-3) / 1e9, 1),
             "header_split_layout": hsplit,
+            "udp64_other_verdict": other,
         }
         del w2
         torch.cuda.empty_cache()

@@ -19,7 +19,7 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-BYTES_PER_PKT = 72
+HDR_BYTES = 64
 PKTS = {"udp64": 32 << 20, "tcp1500": 8 << 20, "mixed": 1 << 20}
 
 
@@ -55,28 +55,31 @@ def main(rnd):
     base = os.path.join(ROOT, "gpurun_out", f"prof_{rnd}")
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
-    cal = calib(base)
-    with open(os.path.join(prof, f"{rnd}_calibration.json"), "w") as f:
-        json.dump({"note": __doc__.strip().split("\n\n")[2], "patterns": cal}, f, indent=1)
-    for wl in PKTS:
-        tdir = os.path.join(base, f"{wl}_trace")
+    if os.path.isdir(os.path.join(base, "calib_FETCH_SIZE")):
+        cal = calib(base)
+        with open(os.path.join(prof, f"{rnd}_calibration.json"), "w") as f:
+            json.dump({"note": __doc__.strip().split("\n\n")[2], "patterns": cal}, f, indent=1)
+    for wl, vb in [(w, v) for w in PKTS for v in (4, 8)]:
+        tag = f"{wl}_v{vb}"
+        tdir = os.path.join(base, f"{tag}_trace")
         if not os.path.isdir(tdir):
             continue
         shutil.copy(os.path.join(tdir, "run_kernel_stats.csv"),
-                    os.path.join(prof, f"{rnd}_{wl}_kernel_stats.csv"))
+                    os.path.join(prof, f"{rnd}_{tag}_kernel_stats.csv"))
         st = [r for r in rows(os.path.join(tdir, "run_kernel_stats.csv")) if "classify_kernel" in r["Name"]]
         pm = {}
         for c in ("FETCH_SIZE", "WRITE_SIZE"):
             vals = [float(r["Counter_Value"]) for r in
-                    rows(os.path.join(base, f"{wl}_{c}", "run_counter_collection.csv"))
+                    rows(os.path.join(base, f"{tag}_{c}", "run_counter_collection.csv"))
                     if "classify_kernel" in r["Kernel_Name"]]
             pm[c] = sum(vals) / len(vals)
         hbm_read = 2.0 * pm["FETCH_SIZE"] * 1024
         hbm_write = pm["WRITE_SIZE"] * 1024
-        algo = PKTS[wl] * BYTES_PER_PKT
+        algo = PKTS[wl] * (HDR_BYTES + vb)
         avg_ns = float(st[0]["AverageNs"])
         out = {
             "workload": wl,
+            "verdict_bytes": vb,
             "kernel": st[0]["Name"],
             "calls": int(st[0]["Calls"]),
             "avg_kernel_ns": avg_ns,
@@ -91,9 +94,9 @@ def main(rnd):
             "traffic_over_algorithmic": round((hbm_read + hbm_write) / algo, 4),
             "hbm_GBs_from_traffic": round((hbm_read + hbm_write) / (avg_ns * 1e-9) / 1e9, 1),
             "algorithmic_GBs": round(algo / (avg_ns * 1e-9) / 1e9, 1),
-            "source": f"gpurun_out/prof_{rnd}/{wl}_{{trace,FETCH_SIZE,WRITE_SIZE}} (rocprofv3)",
+            "source": f"gpurun_out/prof_{rnd}/{tag}_{{trace,FETCH_SIZE,WRITE_SIZE}} (rocprofv3)",
         }
-        with open(os.path.join(prof, f"pmc_{wl}.json"), "w") as f:
+        with open(os.path.join(prof, f"pmc_{wl}{'_v4' if vb == 4 else ''}.json"), "w") as f:
             json.dump(out, f, indent=1)
         print(json.dumps(out))
 

@@ -1,20 +1,26 @@
 #!/bin/bash
-# rocprofv3 evidence for one round: per workload a kernel-trace/stats pass and
-# separate PMC passes (FETCH_SIZE, WRITE_SIZE), plus membench calibration
-# dispatches of known byte counts.  Never mixes --pmc with tracing domains.
+# rocprofv3 evidence for one round: per workload and verdict size a
+# kernel-trace/stats pass and separate PMC passes (FETCH_SIZE, WRITE_SIZE),
+# plus membench calibration dispatches of known byte counts.  Never mixes
+# --pmc with tracing domains.
 set -e
 export TMPDIR=/tmp
 R=${ROUND:-r01}
 OUT=gpurun_out/prof_$R
 mkdir -p $OUT
+for vb in ${VBS:-4 8}; do
 for wl in ${WLS:-udp64 tcp1500}; do
-  A="--workload $wl --steps 20 --warmup 3 --no-cpu --no-secondary --no-e2e"
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/${wl}_trace -o run -- python3 bench.py $A > $OUT/${wl}_bench.json 2> $OUT/${wl}_trace.err
+  A="--workload $wl --verdict-bytes $vb --no-cpu --no-secondary --no-e2e"
+  D=$OUT/${wl}_v${vb}
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d ${D}_trace -o run -- python3 bench.py $A --steps 20 --warmup 3 > ${D}_bench.json 2> ${D}_trace.err
   for c in FETCH_SIZE WRITE_SIZE; do
-    timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $OUT/${wl}_$c -o run -- python3 bench.py --workload $wl --steps 5 --warmup 1 --no-cpu --no-secondary --no-e2e > /dev/null 2> $OUT/${wl}_$c.err
+    timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d ${D}_$c -o run -- python3 bench.py $A --steps 5 --warmup 1 > /dev/null 2> ${D}_$c.err
   done
 done
-for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $OUT/calib_$c -o run -- ./tools/membench calib > $OUT/calib_$c.jsonl 2> $OUT/calib_$c.err
 done
+if [ -x ./tools/membench ] && [ -z "$NO_CALIB" ]; then
+  for c in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $OUT/calib_$c -o run -- ./tools/membench calib > $OUT/calib_$c.jsonl 2> $OUT/calib_$c.err
+  done
+fi
 echo profile-done
