@@ -260,7 +260,7 @@ def roofline(w, kernel_ms):
             "bytes_per_pkt": w.bytes_per_pkt, "kernel_ms": round(kernel_ms, 4)}
 
 
-def e2e_bench(device, reps=3):
+def e2e_bench(device, vbytes=VERDICT_BYTES, reps=3):
     """Rates with the frames in pinned HOST memory (the NIC's mbufs) and the
     verdicts returned to host memory: PCIe-inclusive, never `value`.
     DMA-gather of the 64-B header granules (COPY), PCIe zero-copy reads by the
@@ -272,8 +272,8 @@ def e2e_bench(device, reps=3):
         g.generate(wl, n, stride, R, dfr, seed=SEED)
         hfr = torch.empty(n * stride, dtype=torch.uint8).pin_memory()
         hfr.copy_(dfr)
-        hv = torch.empty(n * 8, dtype=torch.uint8).pin_memory()
-        clf = g.Classifier(device.index or 0, R, g.HASH_JENKINS)
+        hv = torch.empty(n * vbytes, dtype=torch.uint8).pin_memory()
+        clf = g.Classifier(device.index or 0, R, g.HASH_JENKINS, g.CFG_VERDICT4 if vbytes == 4 else 0)
         setup_tables(clf, R, T)
         res = {"pkts": n, "slot_stride": stride}
         for tag, mode, nst in (("copy_hdr_2streams", g.E2E_COPY, 2), ("copy_hdr_4streams", g.E2E_COPY, 4),
@@ -285,7 +285,7 @@ def e2e_bench(device, reps=3):
             dt = (time.perf_counter() - t0) / reps
             res[tag + "_mpps"] = round(n / dt / 1e6, 1)
         # naive: copy whole frames H2D, classify in HBM, copy verdicts back
-        dv = torch.empty(n * 8, dtype=torch.uint8, device=device)
+        dv = torch.empty(n * vbytes, dtype=torch.uint8, device=device)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(reps):
@@ -300,7 +300,62 @@ def e2e_bench(device, reps=3):
         del dfr, hfr, hv, dv, clf
         torch.cuda.empty_cache()
     out["mixed"]["trace_replay"] = trace_replay(device)
+    out["ingress_pool"] = ingress_pool_bench(device, vbytes)
     return out
+
+
+def ingress_pool_bench(device, vbytes, cycles=64, reps=10):
+    """Frames where the reference keeps them (§8f-2): the 131072-mbuf ingress
+    pool, 9408-B elements, 222 per 2 MiB page, frame data at element + 344
+    (8-B aligned; iokernel/defs.h:70, :503-523).  A batch is `cycles` random
+    passes over the pool (descriptor i -> offs[i], like rte_eth_rx_burst
+    handing back recycled mbufs).  Device-resident (pool in HBM) and PCIe
+    zero-copy (pool in pinned host memory, as the shm region would be)."""
+    wl, _, _, R, T, _ = WORKLOADS["udp64"]
+    P = g.IOKERNEL_NUM_MBUFS
+    hdr = torch.zeros(P * 64, dtype=torch.uint8, device=device)
+    g.generate(wl, P, 64, R, hdr, seed=SEED)
+    pool_offs = torch.from_numpy(g.mbuf_data_offsets(P).view(np.int64)).to(device)
+    region = torch.zeros(g.mbuf_region_bytes(P), dtype=torch.uint8, device=device)
+    region[(pool_offs[:, None] + torch.arange(64, device=device)).view(-1)] = hdr
+    del hdr
+    gen = torch.Generator(device="cpu").manual_seed(SEED)
+    order = torch.cat([torch.randperm(P, generator=gen) for _ in range(cycles)]).to(device)
+    offs = pool_offs[order].contiguous()
+    n = offs.numel()
+    clf = g.Classifier(device.index or 0, R, g.HASH_JENKINS, g.CFG_VERDICT4 if vbytes == 4 else 0)
+    setup_tables(clf, R, T)
+    cnt = torch.zeros(R + g.NR_STATS, dtype=torch.int64, device=device)
+    dv = torch.empty(n * vbytes, dtype=torch.uint8, device=device)
+    st = torch.cuda.current_stream().cuda_stream
+
+    def dev_step():
+        clf.classify(region, n, 0, verdicts=dv, counts=cnt[:R], stats=cnt[R:], offs=offs, stream=st)
+
+    dev_step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        dev_step()
+    torch.cuda.synchronize()
+    dt_dev = (time.perf_counter() - t0) / reps
+    ok = int(cnt[:R].sum().item()) == n * (reps + 1)
+    # zero-copy: the pool in pinned host memory, descriptors and verdicts too
+    hreg = torch.empty(region.numel(), dtype=torch.uint8).pin_memory()
+    hreg.copy_(region)
+    del region
+    hoffs = offs.cpu().pin_memory()
+    hv = torch.empty(n * vbytes, dtype=torch.uint8).pin_memory()
+    clf.classify_host(hreg, n, 0, verdicts=hv, offs=hoffs, mode=g.E2E_ZEROCOPY)
+    t0 = time.perf_counter()
+    for _ in range(3):
+        clf.classify_host(hreg, n, 0, verdicts=hv, offs=hoffs, mode=g.E2E_ZEROCOPY)
+    dt_zc = (time.perf_counter() - t0) / 3
+    del hreg, hoffs, hv, offs, dv, clf
+    torch.cuda.empty_cache()
+    return {"mbufs": P, "pkts_per_batch": n, "frame_data_offset": "element + 344 (8-B aligned)",
+            "device_resident_mpps": round(n / dt_dev / 1e6, 1), "counts_check": "ok" if ok else "MISMATCH",
+            "zerocopy_mpps": round(n / dt_zc / 1e6, 1)}
 
 
 def trace_replay(device, n=64 << 10, reps=3):
@@ -500,7 +555,7 @@ def main():
         torch.cuda.empty_cache()
 
     if world == 1 and not args.no_e2e and args.workload == "udp64":
-        result["e2e"] = e2e_bench(device)
+        result["e2e"] = e2e_bench(device, vb)
 
     if world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(args.cpu_budget)

@@ -129,8 +129,14 @@ __device__ __forceinline__ void load_tile(const KParams &k, uint64_t tile, uint4
 		uint4 v = make_uint4(0, 0, 0, 0);
 		if (idx < k.n) {
 			uint64_t a = frame_off<GENERAL>(k, idx) + (uint64_t)(c & 3) * 16;
-			if (!GENERAL || a + 16 <= k.frames_len) {
+			if (!GENERAL || (a + 16 <= k.frames_len && (a & 15) == 0)) {
 				v = gcl::load16_nt(k.frames + a);
+			} else if (a + 16 <= k.frames_len && (a & 7) == 0) {
+				/* mbuf data in the reference's ingress pool sits at
+				 * element + 344 (defs.h:503-506): 8-B aligned */
+				v = gcl::load16_a8(k.frames + a);
+			} else if (a + 16 <= k.frames_len && (a & 3) == 0) {
+				v = gcl::load16_a4(k.frames + a);
 			} else {
 				uint32_t w[4];
 				for (int b = 0; b < 4; b++)
@@ -815,7 +821,7 @@ extern "C" int gcl_open(int hip_device, const struct gcl_cfg *cfg, struct gcl_ct
 		c->tune_depth = e ? atoi(e) : 0;
 		e = getenv("GCL_TUNE_THREADS");
 		c->tune_threads = e ? atoi(e) : 0;
-		if (c->tune_threads != 512 && c->tune_threads != 1024)
+		if (c->tune_threads != 256 && c->tune_threads != 512 && c->tune_threads != 1024)
 			c->tune_threads = 0;
 		e = getenv("GCL_TUNE_NT_STORE");
 		c->tune_nt_store = e ? atoi(e) : 0;

@@ -333,6 +333,29 @@ def pcap_write(path, frames, pkt_len, stride=0, offs=None, ts_ns=None, snaplen=0
                               _ptr(ts), n, snaplen), "gcl_pcap_write")
 
 
+# The reference's ingress mbuf pool (iokernel/defs.h:70, :503-523; rx.c:398-415):
+# 2 MiB pages of 9408-B elements, 222 per page; an element is a 64-B mempool
+# object header, the 128-B rte_mbuf, 24 B of rx_priv_data and 128 B of
+# headroom before the frame, so frame data sits at element + 344 (8-B aligned).
+RX_ELT_SIZE = 9408
+RX_ELT_PER_PAGE = (2 << 20) // RX_ELT_SIZE
+RX_DATA_OFF = 64 + 128 + 24 + 128
+IOKERNEL_NUM_MBUFS = 8192 * 16
+
+
+def mbuf_data_offsets(nmbufs=IOKERNEL_NUM_MBUFS):
+    """Offset of mbuf i's frame data from the ingress region base
+    (rte_pktmbuf_mtod(m) - dp.ingress_mbuf_region.base, rx.c:82), u64[nmbufs]."""
+    i = np.arange(nmbufs, dtype=np.uint64)
+    return ((i // RX_ELT_PER_PAGE) * np.uint64(2 << 20) + (i % RX_ELT_PER_PAGE) * np.uint64(RX_ELT_SIZE)
+            + np.uint64(RX_DATA_OFF))
+
+
+def mbuf_region_bytes(nmbufs=IOKERNEL_NUM_MBUFS):
+    """Bytes of ingress region holding @nmbufs elements (whole 2 MiB pages)."""
+    return -(-nmbufs // RX_ELT_PER_PAGE) * (2 << 20)
+
+
 def zipf_cdf(nflows, s=0.99):
     cdf = np.empty(nflows, dtype=np.uint64)
     _check(lib.gcl_zipf_cdf(nflows, s, cdf.ctypes.data), "gcl_zipf_cdf")

@@ -102,7 +102,10 @@ struct gcl_batch {
 	const uint8_t  *frames;     /* frame bytes (mbuf data) */
 	uint64_t        frames_len; /* readable bytes at frames; reads past it see 0 */
 	uint64_t        stride;     /* slot stride when offs == NULL (multiple of 16) */
-	const uint64_t *offs;       /* optional u64[n] frame start offsets (16-B aligned) */
+	const uint64_t *offs;       /* optional u64[n] frame start offsets, any alignment:
+	                               16-B aligned is one 16-B load per granule chunk,
+	                               8-B aligned (the reference's mbuf data, element
+	                               + 344, iokernel/defs.h:503-506) two 8-B loads */
 	const uint8_t  *olflags;    /* optional u8[n]  GCL_F_* per packet */
 	const uint32_t *rss;        /* optional u32[n] buf->hash.rss (NIC mode) */
 	const uint32_t *fdir_hi;    /* optional u32[n] buf->hash.fdir.hi (FDIR mark) */

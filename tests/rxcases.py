@@ -93,14 +93,20 @@ def random_runtimes(rng, max_runtimes, count, max_threads=16):
     return out
 
 
-def fuzz_batch(rng, n, runtimes, max_runtimes, slot=128, tail_runts=True):
+def fuzz_batch(rng, n, runtimes, max_runtimes, slot=128, tail_runts=True, misalign=None):
     """Random frames hitting every branch; 16-B aligned shuffled offsets, the
-    last frames straddling the end of the buffer (reads past it see 0)."""
+    last frames straddling the end of the buffer (reads past it see 0).
+    misalign: None, "mbuf" (every frame at +8, like mbuf data in the
+    reference's ingress pool) or "mixed" (shifts of 0..15 bytes)."""
     ips = [r["ip"] for r in runtimes] or [0x0A000001]
     buf_slots = n + 8
     frames = np.zeros(buf_slots * slot, dtype=np.uint8)
     order = rng.permutation(buf_slots)[:n]
     offs = (order.astype(np.uint64) * slot)
+    if misalign == "mbuf":
+        offs += np.uint64(8)
+    elif misalign == "mixed":
+        offs += rng.choice([0, 8, 8, 4, 12, 1, 2, 3, 5, 15], size=n).astype(np.uint64)
     olflags = rng.integers(0, 16, size=n, dtype=np.uint8)
     rss = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
     fdir = np.where(rng.random(n) < 0.7,
@@ -132,7 +138,7 @@ def fuzz_batch(rng, n, runtimes, max_runtimes, slot=128, tail_runts=True):
             fr = eth + b"\x81\x00\x00\x05\x08\x00" + bytes(rng.integers(0, 256, size=40, dtype=np.uint8))
         else:
             fr = bytes(rng.integers(0, 256, size=int(rng.integers(14, slot)), dtype=np.uint8))
-        fr = fr[:slot]
+        fr = fr[:slot - (16 if misalign else 0)]
         o = int(offs[i])
         frames[o:o + len(fr)] = np.frombuffer(fr, dtype=np.uint8)
     # loopback hints (tx_pktmbuf_priv.dst_ip): none, a registered IP, or a miss

@@ -110,6 +110,28 @@ def test_gpu_fuzz_vs_oracle(g, orc, mode, flags, max_rt):
     assert (st == se).all(), (st, se)
 
 
+@pytest.mark.parametrize("misalign", ["mbuf", "mixed"])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_gpu_fuzz_misaligned_offsets(g, orc, misalign, mode):
+    """Frame offsets that are not 16-B aligned: 8-B aligned like mbuf data in
+    the reference's ingress pool (element + 344, iokernel/defs.h:503-506), and
+    arbitrary byte shifts."""
+    rng = np.random.default_rng(9100 + 10 * mode + (misalign == "mixed"))
+    rts = random_runtimes(rng, 1024, 300)
+    n = 5000
+    frames, flen, offs, olf, rss, fdir, hint = fuzz_batch(rng, n, rts, 1024, misalign=misalign)
+    t = orc.Tables(1024, mode, g.CFG_TRANS_HASH, 0x09)
+    apply_runtimes(t, rts)
+    clf = g.Classifier(0, 1024, mode, g.CFG_TRANS_HASH, 0x09)
+    apply_runtimes(clf, rts)
+    ve, ce, se, tre = t.classify(frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir_hi=fdir,
+                                 frames_len=flen, dst_hint=hint, trans=True)
+    v, c, st, tr = gpu_run(g, clf, frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir=fdir,
+                           frames_len=flen, hint=hint, trans=True)
+    assert_same(v, ve, f"misalign={misalign} mode={mode}")
+    assert (tr == tre).all() and (c == ce).all() and (st == se).all()
+
+
 @pytest.mark.parametrize("mode", [0, 1, 2])
 @pytest.mark.parametrize("flags", [1, 2])
 @pytest.mark.parametrize("max_rt", [16, 1024])
@@ -388,6 +410,38 @@ def test_gpu_end_to_end_verdict4(g, orc, mode):
     clf.classify_host(hf, n, 64, verdicts=hv, counts=counts, stats=stats, mode=mode,
                       chunk=65536 + 17, nstreams=3)
     assert_same(hv.numpy().view(g.VERDICT4_DTYPE), to_verdict4(ve, [T] * R), f"e2e4 mode={mode}")
+    assert (counts == ce).all() and (stats == se).all()
+
+
+def test_gpu_ingress_pool_geometry(g, orc):
+    """Frames at their real place in the reference's ingress mbuf pool
+    (9408-B elements, 222 per 2 MiB page, data at element + 344, so 8-B
+    aligned; iokernel/defs.h:503-523), in the order a NIC might have pulled
+    the mbufs from the mempool: device-resident and PCIe zero-copy."""
+    n, R, T = 20000, 16, 8
+    frames, olf, rss = orc.generate(0, n, 64, R)
+    rng = np.random.default_rng(5)
+    nm = n + 3000
+    offs = g.mbuf_data_offsets(nm)[rng.permutation(nm)[:n]]
+    region = np.zeros(g.mbuf_region_bytes(nm), dtype=np.uint8)
+    region[offs[:, None].astype(np.int64) + np.arange(64)] = frames.reshape(n, 64)
+    t = orc.Tables(R, 1, 0, 0x09)
+    clf = g.Classifier(0, R, 1)
+    for r in range(R):
+        fl = orc.steer_flows(T, list(range(r % T + 1)))
+        t.runtime_set(r, orc.runtime_ip(r), T, r % T + 1, fl)
+        clf.runtime_set(r, g.runtime_ip(r), T, r % T + 1, fl)
+    ve, ce, se = t.classify(region, n, 0, offs=offs)
+    v, c, st = gpu_run(g, clf, region, n, 0, offs=offs)
+    assert_same(v, ve, "ingress pool, device-resident")
+    assert (c == ce).all() and (st == se).all()
+    hr = torch.from_numpy(region).pin_memory()
+    ho = torch.from_numpy(offs.view(np.int64)).pin_memory()
+    hv = torch.zeros(n * 8, dtype=torch.uint8).pin_memory()
+    counts = np.zeros(R, dtype=np.uint64)
+    stats = np.zeros(8, dtype=np.uint64)
+    clf.classify_host(hr, n, 0, verdicts=hv, counts=counts, stats=stats, offs=ho, mode=g.E2E_ZEROCOPY)
+    assert_same(hv.numpy().view(g.VERDICT_DTYPE), ve, "ingress pool, zero-copy")
     assert (counts == ce).all() and (stats == se).all()
 
 
