@@ -35,7 +35,8 @@ constexpr uint32_t kCrcBytes = 8 * 256 * 4;
 constexpr uint32_t kLdsTableBudget = 96 * 1024;
 constexpr int kImgUsers = 8;             /* streams tracked per table image */
 constexpr uint32_t kLdsQueueBytes = 16; /* s_next[2] after the header tile */
-constexpr int kDefaultSched = 0; /* GCL_TUNE_SCHED default: static persistent grid */
+constexpr int kDefaultSched = 0;  /* GCL_TUNE_SCHED default: static persistent grid */
+constexpr int kDefaultXcdMap = 0; /* GCL_TUNE_XCD_MAP default: round-robin tiles */
 
 /* tuning knobs for experiments (GCL_TUNE_BLOCKS_PER_CU caps the grid) */
 static int g_tune_bpc = 0;
@@ -73,6 +74,7 @@ struct KParams {
 	uint2 *trans;    /* struct gcl_trans[n] or NULL */
 	uint32_t off_seed, off_crc;
 	uint32_t *sched; /* tile queue slot (SchedSlot) or NULL = static persistent grid */
+	uint32_t xcd_map; /* static grid: 1 = each XCD walks one contiguous eighth of the tiles */
 };
 
 /* Dynamic tile queue of one launch: tiles are dealt per XCD (tile t belongs
@@ -446,6 +448,21 @@ classify_kernel(KParams k)
 	uint32_t xs = x0; /* head this block dequeues from (thread 0 only) */
 	uint4 ra[4], rb[4];
 	uint64_t t = blockIdx.x;
+	/* static walk: tiles t, t + step, ... below t_end.  Default: tiles dealt
+	 * round-robin, so the whole chip sweeps one 16 MiB window of the batch.
+	 * xcd_map (GCL_TUNE_XCD_MAP=1): block b walks XCD (b & 7)'s contiguous
+	 * eighth instead, eight separate streams; that measured 7% slower on
+	 * every buffer placement tried (tools/alloc_ab.cpp,
+	 * profiles/r01_alloc_placement.jsonl), so it stays an experiment. */
+	uint64_t step = G, t_end = k.ntiles;
+	if (k.xcd_map && !k.sched) {
+		const uint64_t Gx = G / GCL_SCHED_XCD;
+		const uint64_t chunk = (k.ntiles + GCL_SCHED_XCD - 1) / GCL_SCHED_XCD;
+		const uint64_t lo = (blockIdx.x & (GCL_SCHED_XCD - 1)) * chunk;
+		t = lo + blockIdx.x / GCL_SCHED_XCD;
+		t_end = lo + chunk < k.ntiles ? lo + chunk : k.ntiles;
+		step = Gx;
+	}
 	uint32_t got = 0;
 	if (dyn) {
 		const uint64_t j = blockIdx.x / GCL_SCHED_XCD;
@@ -453,19 +470,19 @@ classify_kernel(KParams k)
 		if (tid == 0 && t < k.ntiles)
 			got = atomicAdd(&k.sched[x0 * GCL_SCHED_LINE], 1u);
 	}
-	if (t < k.ntiles)
+	if (t < t_end)
 		load_tile<GENERAL, NT>(k, t, ra);
-	if (DEPTH == 2 && t + G < k.ntiles)
-		load_tile<GENERAL, NT>(k, t + G, rb);
+	if (DEPTH == 2 && t + step < t_end)
+		load_tile<GENERAL, NT>(k, t + step, rb);
 	if (dyn && tid == 0)
 		s_next[0] = t < k.ntiles ? sched_resolve(k.sched, k.ntiles, (uint32_t)G, x0, xs, got)
 		                         : k.ntiles;
 	int par = 0;
 
-	while (t < k.ntiles) {
+	while (t < t_end) {
 		stage_tile<NT>(tile, ra);
 		__syncthreads();
-		uint64_t nxt = t + DEPTH * G;
+		uint64_t nxt = t + DEPTH * step;
 		if (dyn) {
 			nxt = s_next[par];
 			/* issued before the tile loads, so waiting for it later does
@@ -473,7 +490,7 @@ classify_kernel(KParams k)
 			if (tid == 0 && nxt < k.ntiles)
 				got = atomicAdd(&k.sched[xs * GCL_SCHED_LINE], 1u);
 		}
-		if (nxt < k.ntiles)
+		if (nxt < t_end)
 			load_tile<GENERAL, NT>(k, nxt, ra); /* in flight while parsing */
 		if (k.ablate & 16) { /* timing only: the membench tile_v0 body */
 			const uint4 a = tile[tile_slot(tid, 0)], b = tile[tile_slot(tid, 1)];
@@ -490,18 +507,18 @@ classify_kernel(KParams k)
 			par ^= 1;
 			continue;
 		}
-		t += G;
+		t += step;
 		if (DEPTH == 2) {
-			if (t >= k.ntiles)
+			if (t >= t_end)
 				break;
 			stage_tile<NT>(tile, rb);
 			__syncthreads();
-			if (t + 2 * G < k.ntiles)
-				load_tile<GENERAL, NT>(k, t + 2 * G, rb);
+			if (t + 2 * step < t_end)
+				load_tile<GENERAL, NT>(k, t + 2 * step, rb);
 			if (t * NT + tid < k.n)
 				classify_one<MODE, GENERAL>(k, tile, tid, t * NT + tid, tb, hist, cnt);
 			__syncthreads();
-			t += G;
+			t += step;
 		}
 	}
 	uint32_t n_flowtag = cnt.flowtag, n_hashmiss = cnt.hashmiss;
@@ -758,6 +775,7 @@ struct gcl_ctx {
 	int tune_nt_store; /* GCL_TUNE_NT_STORE: non-temporal verdict stores */
 	int tune_ablate;   /* GCL_TUNE_ABLATE bitmask (timing experiments only) */
 	int tune_sched;    /* GCL_TUNE_SCHED: 0 static persistent grid, 1 dynamic tile queue */
+	int tune_xcd_map;  /* GCL_TUNE_XCD_MAP: 1 contiguous eighth per XCD, 0 round-robin tiles */
 	/* dynamic tile queue: one slot per launch in flight, reused in turn; a
 	 * launch waits for the previous user of its slot (same or other stream) */
 	uint32_t *sched;
@@ -833,6 +851,8 @@ extern "C" int gcl_open(int hip_device, const struct gcl_cfg *cfg, struct gcl_ct
 		g_tune_bpc = e ? atoi(e) : 0;
 		e = getenv("GCL_TUNE_SCHED");
 		c->tune_sched = e ? atoi(e) : kDefaultSched;
+		e = getenv("GCL_TUNE_XCD_MAP");
+		c->tune_xcd_map = e ? atoi(e) : kDefaultXcdMap;
 	}
 	c->dimg[0] = c->dimg[1] = nullptr;
 	c->sched = nullptr;
@@ -1084,6 +1104,8 @@ static hipError_t launch_t(KParams k, uint32_t lds, int num_cus, int bpc_cap, hi
 		grid = k.ntiles;
 	if (grid < 1)
 		grid = 1;
+	if (grid % GCL_SCHED_XCD) /* the per-XCD walk needs whole rows of 8 blocks */
+		k.xcd_map = 0;
 	hipLaunchKernelGGL((classify_kernel<MODE, TLDS, GENERAL, DEPTH, NT>), dim3((unsigned)grid),
 	                   dim3(NT), lds, s, k);
 	return hipGetLastError();
@@ -1286,6 +1308,7 @@ extern "C" int gcl_classify_ex(struct gcl_ctx *c, const struct gcl_batch *b,
 	k.default_flags = c->cfg.default_olflags;
 	k.nt_store = c->tune_nt_store;
 	k.ablate = c->tune_ablate;
+	k.xcd_map = c->tune_xcd_map;
 
 	/* the specialised fast path needs every header granule in range */
 	bool general = b->offs || b->olflags || b->fdir_hi || b->dst_hint ||

@@ -119,8 +119,13 @@ int main(int argc, char **argv)
 	cfg.hash_mode = GCL_HASH_JENKINS;
 	cfg.flags = GCL_CFG_VERDICT4;
 	cfg.default_olflags = GCL_F_RSS_HASH | GCL_F_IP_CKSUM_GOOD;
-	struct gcl_ctx *ctx;
+	/* ctx: round-robin tiles over XCDs; ctx2: a contiguous eighth per XCD */
+	struct gcl_ctx *ctx, *ctx2;
+	setenv("GCL_TUNE_XCD_MAP", "0", 1);
 	if (gcl_open(0, &cfg, &ctx))
+		return 1;
+	setenv("GCL_TUNE_XCD_MAP", "1", 1);
+	if (gcl_open(0, &cfg, &ctx2))
 		return 1;
 	uint16_t act[GCL_NCPU], flow[GCL_NCPU];
 	for (uint32_t r = 0; r < R; r++) {
@@ -129,6 +134,7 @@ int main(int argc, char **argv)
 			act[i] = i;
 		gcl_steer_flows((uint16_t)T, act, na, flow);
 		gcl_runtime_set(ctx, (uint16_t)r, gcl_runtime_ip(r), (uint16_t)T, na, flow);
+		gcl_runtime_set(ctx2, (uint16_t)r, gcl_runtime_ip(r), (uint16_t)T, na, flow);
 	}
 	hipEvent_t e0, e1;
 	CHECK(hipEventCreate(&e0));
@@ -153,10 +159,11 @@ int main(int argc, char **argv)
 			float ms;
 			CHECK(hipEventElapsedTime(&ms, e0, e1));
 			us[i].push_back(ms * 1e3 / steps);
-			/* same frames, verdicts into the other buffer */
+			/* same frames, per-XCD contiguous tile walk */
+			gcl_classify(ctx2, &bt, v2, acc, acc + R, nullptr);
 			CHECK(hipEventRecord(e0, nullptr));
 			for (int s2 = 0; s2 < steps; s2++)
-				gcl_classify(ctx, &bt, v2, acc, acc + R, nullptr);
+				gcl_classify(ctx2, &bt, v2, acc, acc + R, nullptr);
 			CHECK(hipEventRecord(e1, nullptr));
 			CHECK(hipEventSynchronize(e1));
 			CHECK(hipEventElapsedTime(&ms, e0, e1));
@@ -178,10 +185,11 @@ int main(int argc, char **argv)
 		std::sort(us2[i].begin(), us2[i].end());
 		std::sort(rd[i].begin(), rd[i].end());
 		printf("{\"buffer\": \"%s\", \"va\": \"%p\", \"median_us\": %.2f, \"min_us\": %.2f, \"max_us\": %.2f, "
-		       "\"median_us_v2\": %.2f, \"read_only_us\": %.2f, \"read_TBs\": %.2f}\n",
+		       "\"median_us_xcdmap\": %.2f, \"read_only_us\": %.2f, \"read_TBs\": %.2f}\n",
 		       names[i], (void *)bufs[i], us[i][us[i].size() / 2], us[i].front(), us[i].back(),
 		       us2[i][us2[i].size() / 2], rd[i][rd[i].size() / 2], bytes / (rd[i][rd[i].size() / 2] * 1e-6) / 1e12);
 	}
 	gcl_close(ctx);
+	gcl_close(ctx2);
 	return 0;
 }
