@@ -113,8 +113,13 @@ class Workload:
             self.frames = torch.zeros(n * stride, dtype=torch.uint8, device=device)
             self.verdicts = torch.empty(n * vbytes, dtype=torch.uint8, device=device)
         else:  # library-owned hipMalloc (gcl_dev_alloc), zeroed
-            self.frames = g.DeviceBuffer(n * stride, device.index or 0)
+            # the verdict ring first, then the frame pool placed against it
+            # (gcl_dev_alloc_paired: DESIGN.md §4 "Buffer placement");
+            # GCL_BENCH_PLACEMENT=0 allocates both plainly, for the A/B
             self.verdicts = g.DeviceBuffer(n * vbytes, device.index or 0)
+            paired = os.environ.get("GCL_BENCH_PLACEMENT", "1") != "0"
+            self.frames = g.DeviceBuffer(n * stride, device.index or 0,
+                                         partner=self.verdicts if paired else None)
             torch.cuda.synchronize()
             zero_fill(self.frames)
         self.counts = torch.zeros(R + g.NR_STATS, dtype=torch.int64, device=device)
@@ -258,6 +263,15 @@ def roofline(w, kernel_ms):
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             "bytes_per_pkt": w.bytes_per_pkt, "kernel_ms": round(kernel_ms, 4)}
+
+
+def placement(w):
+    """How the frame pool was placed against the verdict ring."""
+    pu = getattr(w.frames, "probe_us", None)
+    if pu is None:
+        return {"policy": "plain hipMalloc"}
+    return {"policy": "gcl_dev_alloc_paired (frame pool placed against the verdict ring)",
+            "probe_us_chosen": round(pu[0], 2), "probe_us_worst": round(pu[1], 2)}
 
 
 def e2e_bench(device, vbytes=VERDICT_BYTES, reps=3):
@@ -519,6 +533,7 @@ def main():
                                    f"all_gather of per-runtime counts every {args.exchange_every} step(s), overlapped"
                                    if dist_on else "single GPU")},
         "roofline": roofline(w, kms),
+        "placement": placement(w),
         "counts_check": "ok" if tot == expect else f"MISMATCH {tot} != {expect}",
     }
     del w
@@ -530,7 +545,7 @@ def main():
         el4, kms4 = run_timed(w4, args.steps, 3, 1)
         other = {"verdict": "gcl_verdict, 8 B" if vb == 4 else "gcl_verdict4, 4 B",
                  "value": round(w4.n * args.steps / el4 / 1e6, 1), "unit": "Mpkt/s",
-                 "ms_per_step": round(el4 / args.steps * 1e3, 4), "roofline": roofline(w4, kms4)}
+                 "ms_per_step": round(el4 / args.steps * 1e3, 4), "roofline": roofline(w4, kms4), "placement": placement(w4)}
         del w4
         torch.cuda.empty_cache()
         w2 = Workload("tcp1500", rank, world, device, vbytes=vb)
@@ -540,13 +555,14 @@ def main():
         el3, kms3 = run_timed(w3, steps2, 2, 1)
         hsplit = {"workload": f"tcp1500_hsplit: {w3.desc}",
                   "value": round(w3.n * steps2 / el3 / 1e6, 1), "unit": "Mpkt/s",
-                  "roofline": roofline(w3, kms3)}
+                  "roofline": roofline(w3, kms3), "placement": placement(w3)}
         del w3
         result["secondary"] = {
             "workload": f"tcp1500: {w2.desc}",
             "value": round(w2.n * steps2 / el2 / 1e6, 1), "unit": "Mpkt/s",
             "ms_per_step": round(el2 / steps2 * 1e3, 4), "steps": steps2,
             "roofline": roofline(w2, kms2),
+            "placement": placement(w2),
             "frame_bytes_rate_GBs": round(w2.n * 1500 / (kms2 * 1e-3) / 1e9, 1),
             "header_split_layout": hsplit,
             "udp64_other_verdict": other,

@@ -25,6 +25,7 @@ HASH_NIC, HASH_JENKINS, HASH_TOEPLITZ = 0, 1, 2
 HASH_MODES = {"nic": HASH_NIC, "jenkins": HASH_JENKINS, "toeplitz": HASH_TOEPLITZ}
 
 CFG_AZURE_ARP, CFG_HASH16, CFG_PROFILE, CFG_TRANS_HASH, CFG_VERDICT4 = 0x1, 0x2, 0x4, 0x8, 0x10
+PAIR_NEW_READS, PAIR_NEW_WRITES, PAIR_TRIES = 0x1, 0x2, 6
 
 F_RSS_HASH, F_FDIR_ID = 0x01, 0x02
 F_IP_CKSUM_MASK, F_IP_CKSUM_UNKNOWN, F_IP_CKSUM_BAD = 0x0C, 0x00, 0x04
@@ -177,6 +178,8 @@ def _load():
         "gcl_host_register": (i32, [vp, ctypes.c_size_t]),
         "gcl_dev_alloc": (i32, [i32, ctypes.c_size_t, ctypes.POINTER(vp)]),
         "gcl_dev_free": (i32, [vp]),
+        "gcl_dev_alloc_paired": (i32, [i32, ctypes.c_size_t, vp, ctypes.c_size_t, u32,
+                                       ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_double)]),
         "gcl_host_unregister": (i32, [vp]),
         "gcl_pcap_write": (i32, [ctypes.c_char_p, vp, u64, vp, vp, vp, u64, u32]),
         "gcl_pcap_load": (i32, [ctypes.c_char_p, ctypes.POINTER(GclTrace), u64]),
@@ -257,9 +260,21 @@ class DeviceBuffer:
     address with the duck-typed interface the binding accepts (data_ptr,
     numel, element_size)."""
 
-    def __init__(self, nbytes, device=0):
+    def __init__(self, nbytes, device=0, partner=None, new_reads=True):
+        """partner: another buffer (data_ptr/numel); the new one is then placed
+        by gcl_dev_alloc_paired so that reading the frame side while writing
+        the verdict side does not hit the same-placement-class slowdown.
+        new_reads: the new buffer is the frame (read) side."""
         p = ctypes.c_void_p()
-        _check(lib.gcl_dev_alloc(device, nbytes, ctypes.byref(p)), "gcl_dev_alloc")
+        self.probe_us = None
+        if partner is None:
+            _check(lib.gcl_dev_alloc(device, nbytes, ctypes.byref(p)), "gcl_dev_alloc")
+        else:
+            us = (ctypes.c_double * 2)()
+            _check(lib.gcl_dev_alloc_paired(device, nbytes, _ptr(partner), _nbytes(partner),
+                                            PAIR_NEW_READS if new_reads else PAIR_NEW_WRITES,
+                                            ctypes.byref(p), us), "gcl_dev_alloc_paired")
+            self.probe_us = (us[0], us[1])
         self.ptr, self.nbytes = p.value, nbytes
 
     def data_ptr(self):

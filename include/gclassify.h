@@ -383,6 +383,33 @@ uint32_t gcl_toeplitz(const uint8_t *key, size_t keylen, const uint8_t *input,
 int gcl_dev_alloc(int hip_device, size_t bytes, void **out);
 int gcl_dev_free(void *p);
 
+/*
+ * Placement-aware device allocation for the two long-lived classify buffers
+ * (the frame pool and the verdict ring, the GPU-side counterparts of the
+ * iokernel's ingress region and rxq rings, shm.h:14-15, ioqueues.c:31-40).
+ * On MI355X the header read stream and the verdict write stream run ~15%
+ * slower when the two buffers fall in the same physical placement class
+ * (measured: DESIGN.md §4 "Buffer placement", profiles/r01_pair_*.jsonl).
+ * The class cannot be read from a virtual address, so this allocates a
+ * candidate, times a short read+write probe of the classify kernel's access
+ * shape against @partner, and keeps the first candidate whose probe differs
+ * from an earlier one by more than the class gap (the faster of the two),
+ * trying at most GCL_PAIR_TRIES candidates; losers are freed.
+ *
+ * GCL_PAIR_NEW_READS: the new buffer is the one stream-read (frames) and
+ *                     @partner the one written (verdicts);
+ * GCL_PAIR_NEW_WRITES: the reverse.
+ * The probe WRITES to the written side's first min(bytes, 32 MiB): call it
+ * before that buffer holds data.  @probe_us (optional, 2 doubles) returns the
+ * chosen and the slowest probe time in microseconds.
+ * Returns 0, -EINVAL, -ENODEV, -ENOMEM or -EIO.
+ */
+#define GCL_PAIR_NEW_READS  0x1
+#define GCL_PAIR_NEW_WRITES 0x2
+#define GCL_PAIR_TRIES      6
+int gcl_dev_alloc_paired(int hip_device, size_t bytes, const void *partner, size_t partner_bytes,
+                         uint32_t flags, void **out, double *probe_us);
+
 /* Library version string. */
 const char *gcl_version(void);
 

@@ -341,3 +341,16 @@ def test_host_deliver4_matches_deliver(g, orc):
     full, compact = run(False), run(True)
     assert full[0] > 0 and any(e[0] == "wake" for e in full[2])
     assert full == compact
+
+
+def test_dev_alloc_paired_rejects_bad_args(g):
+    """Argument checks come before any HIP call (no GPU needed)."""
+    out = ctypes.c_void_p()
+    f = g.lib.gcl_dev_alloc_paired
+    assert f(0, 1 << 20, None, 1 << 20, g.PAIR_NEW_READS, ctypes.byref(out), None) == -22
+    assert f(0, 0, 4096, 1 << 20, g.PAIR_NEW_READS, ctypes.byref(out), None) == -22
+    assert f(0, 1 << 20, 4096, 1 << 20, 0, ctypes.byref(out), None) == -22
+    assert f(0, 1 << 20, 4096, 1 << 20, 3, ctypes.byref(out), None) == -22
+    assert f(0, 1 << 20, 4096, 1 << 20, g.PAIR_NEW_READS, None, None) == -22
+    # the read side must hold one 256-packet tile of 64-B granules
+    assert f(0, 1 << 13, 4096, 1 << 20, g.PAIR_NEW_READS, ctypes.byref(out), None) == -22

@@ -475,3 +475,38 @@ def test_gpu_trace_replay_zero_copy(g, orc, tmp_path):
             g.host_unregister(a)
     assert_same(hv, ve, "trace replay")
     assert (counts == ce).all() and (stats == se).all()
+
+
+def test_gpu_dev_alloc_paired(g, orc):
+    """Placement-aware allocation (gcl_dev_alloc_paired): both directions give
+    working buffers, the probe times are sane, and a classify through the
+    paired frame pool / verdict ring is bit-exact against the oracle."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    n, stride, R, T = 1 << 18, 64, 16, 8
+    ring = g.DeviceBuffer(n * 4)
+    pool = g.DeviceBuffer(n * stride, partner=ring, new_reads=True)
+    assert pool.probe_us is not None and 0 < pool.probe_us[0] <= pool.probe_us[1]
+    ring2 = g.DeviceBuffer(n * 4, partner=pool, new_reads=False)
+    assert 0 < ring2.probe_us[0] <= ring2.probe_us[1]
+    frames, _, _ = orc.generate(0, n, stride, R)
+    assert hip.hipMemcpy(pool.data_ptr(), frames.ctypes.data, n * stride, 1) == 0  # H2D
+    t = orc.Tables(R, 1, 0, 0x09)
+    clf = g.Classifier(0, R, 1, g.CFG_VERDICT4, 0x09)
+    for r in range(R):
+        fl = orc.steer_flows(T, list(range(r % T + 1)))
+        t.runtime_set(r, orc.runtime_ip(r), T, r % T + 1, fl)
+        clf.runtime_set(r, g.runtime_ip(r), T, r % T + 1, fl)
+    c = torch.zeros(R, dtype=torch.int64, device="cuda")
+    s = torch.zeros(g.NR_STATS, dtype=torch.int64, device="cuda")
+    clf.classify(pool, n, stride, verdicts=ring2, counts=c, stats=s)
+    torch.cuda.synchronize()
+    got = np.empty(n, dtype=g.VERDICT4_DTYPE)
+    assert hip.hipMemcpy(got.ctypes.data, ring2.data_ptr(), n * 4, 2) == 0  # D2H
+    ve, ce, se = t.classify(frames, n, stride)
+    assert_same(got, to_verdict4(ve, [T] * R), "paired buffers")
+    assert (c.cpu().numpy().astype(np.uint64) == ce).all()
+    assert (s.cpu().numpy().astype(np.uint64) == se).all()
+    for b in (ring2, pool, ring):
+        b.free()

@@ -1,0 +1,219 @@
+// pair_ab.cpp - is the udp64 classify time a property of the frame buffer,
+// of the verdict buffer, or of the pair?  tools/alloc_ab.cpp showed 2 GiB
+// frame buffers of one process split into a 343-us and a 406-us group, with
+// identical TLB misses and HBM request counts.  Here F frame buffers x V
+// verdict buffers (allocated with gaps so they land in different places) are
+// timed pairwise with the classify kernel (4-B verdicts) and with a
+// compute-free kernel of the same traffic shape, rounds interleaved.
+// Build: hipcc --offload-arch=gfx950 -O2 -Iinclude -o tools/pair_ab tools/pair_ab.cpp \
+//          -Lcaladan_amd -lgclassify -Wl,-rpath,'$ORIGIN/../caladan_amd'
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "gclassify.h"
+
+#define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { \
+	fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); exit(1); } } while (0)
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+/* W: 0 st4, 1 verdicts of 16 tiles batched in LDS and written 16 B per lane,
+ * 2 st4 sc0 sc1, 3 st4 nt */
+template <int W>
+__global__ void __launch_bounds__(256) tile_kernel(const unsigned char *buf, unsigned long long ntiles,
+                                                   unsigned *out)
+{
+	__shared__ u32x4 tile[1024];
+	__shared__ unsigned vst[W == 1 ? 16 * 256 : 1];
+	int nb = 0;
+	unsigned long long tb0 = blockIdx.x;
+	unsigned long long t = blockIdx.x;
+	u32x4 r[4];
+	auto ld = [&](unsigned long long tt) {
+#pragma unroll
+		for (int j = 0; j < 4; j++) {
+			int c = j * 256 + threadIdx.x;
+			r[j] = __builtin_nontemporal_load((const u32x4 *)(buf + (tt * 256 + (c >> 2)) * 64 + (c & 3) * 16));
+		}
+	};
+	if (t < ntiles)
+		ld(t);
+	unsigned acc = 0;
+	while (t < ntiles) {
+#pragma unroll
+		for (int j = 0; j < 4; j++) {
+			int c = j * 256 + threadIdx.x;
+			int p = c >> 2, q = c & 3;
+			tile[p * 4 + (q ^ ((p >> 2) & 3))] = r[j];
+		}
+		__syncthreads();
+		unsigned long long nx = t + gridDim.x;
+		if (nx < ntiles)
+			ld(nx);
+		int p = threadIdx.x;
+		u32x4 a = tile[p * 4 + (0 ^ ((p >> 2) & 3))], b = tile[p * 4 + (1 ^ ((p >> 2) & 3))];
+		const unsigned vv = a.x ^ a.w ^ b.y ^ b.z;
+		if (out && W == 1) {
+			vst[nb * 256 + p] = vv;
+			if (++nb == 16 || nx >= ntiles) {
+				__syncthreads();
+				for (int i = threadIdx.x; i < nb * 64; i += 256) {
+					const unsigned long long tt = tb0 + (unsigned long long)(i >> 6) * gridDim.x;
+					*(u32x4 *)&out[tt * 256 + (i & 63) * 4] = *(u32x4 *)&vst[(i >> 6) * 256 + (i & 63) * 4];
+				}
+				nb = 0;
+				tb0 = nx;
+			}
+		} else if (out && W == 2) {
+			asm volatile("global_store_dword %0, %1, off sc0 sc1" : : "v"(&out[t * 256 + p]), "v"(vv) : "memory");
+		} else if (out && W == 3) {
+			__builtin_nontemporal_store(vv, &out[t * 256 + p]);
+		} else if (out)
+			out[t * 256 + p] = vv;
+		else
+			acc ^= a.x ^ a.w ^ b.y ^ b.z;
+		__syncthreads();
+		t = nx;
+	}
+	if (acc == 0x9E3779B9u)
+		((unsigned *)buf)[0] = acc;
+}
+
+/* the verdict stream alone: 4 B per packet, 256 per block iteration */
+__global__ void __launch_bounds__(256) wr_kernel(unsigned long long ntiles, unsigned *out)
+{
+	for (unsigned long long t = blockIdx.x; t < ntiles; t += gridDim.x)
+		out[t * 256 + threadIdx.x] = (unsigned)t;
+}
+
+int main(int argc, char **argv)
+{
+	const int steps = argc > 1 ? atoi(argv[1]) : 10;
+	const int NF = argc > 2 ? atoi(argv[2]) : 6, NV = argc > 3 ? atoi(argv[3]) : 4;
+	const uint64_t n = 32ull << 20, stride = 64, bytes = n * stride;
+	const uint32_t R = 16, T = 8;
+	std::vector<uint8_t *> fb;
+	std::vector<uint32_t *> vb;
+	/* V0 first, then F0 V1 F1 V2 ...: every frame buffer has a verdict
+	 * buffer allocated just before and just after it */
+	for (int i = 0; i < std::max(NF, NV); i++) {
+		if (i < NV) {
+			uint32_t *p;
+			CHECK(hipMalloc(&p, n * 4));
+			vb.push_back(p);
+		}
+		if (i < NF) {
+			uint8_t *p;
+			CHECK(hipMalloc(&p, bytes));
+			fb.push_back(p);
+		}
+	}
+	struct gcl_gen_params gp = {};
+	gp.workload = GCL_WL_UDP64;
+	gp.nruntimes = R;
+	gp.seed = 0xCA1ADA4;
+	gp.n = n;
+	gp.stride = stride;
+	gp.world = 1;
+	for (uint8_t *p : fb)
+		if (gcl_generate(&gp, p, nullptr, nullptr, nullptr))
+			return 1;
+	uint64_t *acc;
+	CHECK(hipMalloc(&acc, (R + GCL_NR_STATS) * 8));
+	struct gcl_cfg cfg = {};
+	cfg.max_runtimes = R;
+	cfg.hash_mode = GCL_HASH_JENKINS;
+	cfg.flags = GCL_CFG_VERDICT4;
+	cfg.default_olflags = GCL_F_RSS_HASH | GCL_F_IP_CKSUM_GOOD;
+	struct gcl_ctx *ctx;
+	if (gcl_open(0, &cfg, &ctx))
+		return 1;
+	uint16_t act[GCL_NCPU], flow[GCL_NCPU];
+	for (uint32_t r = 0; r < R; r++) {
+		uint16_t na = (uint16_t)(r % T + 1);
+		for (uint16_t i = 0; i < na; i++)
+			act[i] = i;
+		gcl_steer_flows((uint16_t)T, act, na, flow);
+		gcl_runtime_set(ctx, (uint16_t)r, gcl_runtime_ip(r), (uint16_t)T, na, flow);
+	}
+	int cus = 0;
+	CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+	hipEvent_t e0, e1;
+	CHECK(hipEventCreate(&e0));
+	CHECK(hipEventCreate(&e1));
+	std::vector<std::vector<double>> cl(NF * NV), tk(NF * NV);
+	for (int round = 0; round < 3; round++)
+		for (int f = 0; f < NF; f++)
+			for (int v = 0; v < NV; v++) {
+				struct gcl_batch bt = {};
+				bt.frames = fb[f];
+				bt.frames_len = bytes;
+				bt.stride = stride;
+				bt.n = n;
+				gcl_classify(ctx, &bt, vb[v], acc, acc + R, nullptr);
+				CHECK(hipEventRecord(e0, nullptr));
+				for (int s = 0; s < steps; s++)
+					gcl_classify(ctx, &bt, vb[v], acc, acc + R, nullptr);
+				CHECK(hipEventRecord(e1, nullptr));
+				CHECK(hipEventSynchronize(e1));
+				float ms;
+				CHECK(hipEventElapsedTime(&ms, e0, e1));
+				cl[f * NV + v].push_back(ms * 1e3 / steps);
+				CHECK(hipEventRecord(e0, nullptr));
+				for (int s = 0; s < steps; s++)
+					hipLaunchKernelGGL(tile_kernel<0>, dim3(cus * 4), dim3(256), 0, nullptr, fb[f],
+					                   (unsigned long long)(n / 256), vb[v]);
+				CHECK(hipEventRecord(e1, nullptr));
+				CHECK(hipEventSynchronize(e1));
+				CHECK(hipEventElapsedTime(&ms, e0, e1));
+				tk[f * NV + v].push_back(ms * 1e3 / steps);
+			}
+	auto tm = [&](auto fn) {
+		std::vector<double> x;
+		for (int r = 0; r < 3; r++) {
+			CHECK(hipEventRecord(e0, nullptr));
+			for (int s = 0; s < steps; s++)
+				fn();
+			CHECK(hipEventRecord(e1, nullptr));
+			CHECK(hipEventSynchronize(e1));
+			float ms;
+			CHECK(hipEventElapsedTime(&ms, e0, e1));
+			x.push_back(ms * 1e3 / steps);
+		}
+		std::sort(x.begin(), x.end());
+		return x[1];
+	};
+	for (int f : {0, NF / 2, NF - 1})
+		for (int v : {0, NV / 2, NV - 1}) {
+			auto go = [&](auto kern) {
+				return tm([&] { hipLaunchKernelGGL(kern, dim3(cus * 4), dim3(256), 0, nullptr, fb[f],
+				                                   (unsigned long long)(n / 256), vb[v]); });
+			};
+			printf("{\"f\": %d, \"v\": %d, \"st4\": %.2f, \"batch16\": %.2f, \"sc\": %.2f, \"nt\": %.2f}\n",
+			       f, v, go(tile_kernel<0>), go(tile_kernel<1>), go(tile_kernel<2>), go(tile_kernel<3>));
+		}
+	for (int f = 0; f < NF; f++)
+		printf("{\"f\": %d, \"fva\": \"%p\", \"read_only_us\": %.2f}\n", f, (void *)fb[f],
+		       tm([&] { hipLaunchKernelGGL(tile_kernel<0>, dim3(cus * 4), dim3(256), 0, nullptr, fb[f],
+		                                   (unsigned long long)(n / 256), (unsigned *)nullptr); }));
+	for (int v = 0; v < NV; v++)
+		printf("{\"v\": %d, \"vva\": \"%p\", \"write_only_us\": %.2f}\n", v, (void *)vb[v],
+		       tm([&] { hipLaunchKernelGGL(wr_kernel, dim3(cus * 4), dim3(256), 0, nullptr,
+		                                   (unsigned long long)(n / 256), vb[v]); }));
+	for (int f = 0; f < NF; f++)
+		for (int v = 0; v < NV; v++) {
+			auto &a = cl[f * NV + v], &b = tk[f * NV + v];
+			std::sort(a.begin(), a.end());
+			std::sort(b.begin(), b.end());
+			printf("{\"f\": %d, \"v\": %d, \"fva\": \"%p\", \"vva\": \"%p\", \"classify_us\": %.2f, "
+			       "\"tile_us\": %.2f}\n", f, v, (void *)fb[f], (void *)vb[v], a[a.size() / 2],
+			       b[b.size() / 2]);
+		}
+	gcl_close(ctx);
+	return 0;
+}
