@@ -117,8 +117,17 @@ int main(int argc, char **argv)
 	uint8_t *frames;
 	struct gcl_verdict *v;
 	uint64_t *acc, *zipf = nullptr;
-	CHECK(hipMalloc(&frames, n * stride));
 	CHECK(hipMalloc(&v, n * sizeof(*v)));
+	if (getenv("CBENCH_PAIRED")) { /* frame pool placed against the verdict ring */
+		double pu[2];
+		if (gcl_dev_alloc_paired(0, n * stride, v, n * 4, GCL_PAIR_NEW_READS, (void **)&frames, pu)) {
+			fprintf(stderr, "gcl_dev_alloc_paired failed\n");
+			return 1;
+		}
+		fprintf(stderr, "paired: probe %.2f us (worst %.2f)\n", pu[0], pu[1]);
+	} else {
+		CHECK(hipMalloc(&frames, n * stride));
+	}
 	CHECK(hipMalloc(&acc, (R + GCL_NR_STATS) * 8));
 	CHECK(hipMemset(frames, 0, n * stride));
 	CHECK(hipMemset(acc, 0, (R + GCL_NR_STATS) * 8));
