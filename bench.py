@@ -313,8 +313,56 @@ def e2e_bench(device, vbytes=VERDICT_BYTES, reps=3):
         out[name] = res
         del dfr, hfr, hv, dv, clf
         torch.cuda.empty_cache()
+    out["rxloop"] = rxloop_bench(device, vbytes)
     out["mixed"]["trace_replay"] = trace_replay(device)
     out["ingress_pool"] = ingress_pool_bench(device, vbytes)
+    return out
+
+
+def rxloop_bench(device, vbytes, iters=2000):
+    """Burst latency at the reference's granularity (rx_burst's <= 64 mbufs,
+    iokernel/rx.c:270-290): the persistent rx loop (gcl_rxloop_*) reading the
+    frames zero-copy from pinned host memory, against one launch per burst
+    (gcl_classify_host ZEROCOPY, timed from Python, so ctypes overhead is
+    included)."""
+    wl, _, stride, R, T, _ = WORKLOADS["udp64"]
+    n = 1 << 16
+    dfr = torch.zeros(n * stride, dtype=torch.uint8, device=device)
+    g.generate(wl, n, stride, R, dfr, seed=SEED)
+    hfr = torch.empty(n * stride, dtype=torch.uint8).pin_memory()
+    hfr.copy_(dfr)
+    torch.cuda.synchronize()
+    clf = g.Classifier(device.index or 0, R, g.HASH_JENKINS, g.CFG_VERDICT4 if vbytes == 4 else 0)
+    setup_tables(clf, R, T)
+    out = {"frames": "udp64 synthetic, pinned host memory, read zero-copy"}
+
+    def pct(lat):
+        us = np.sort(lat.astype(np.float64)) / 1e3
+        return {"p50_us": round(float(us[len(us) // 2]), 2),
+                "p99_us": round(float(us[int(len(us) * 0.99)]), 2),
+                "mean_us": round(float(us.mean()), 2)}
+
+    for burst, workers, depth in ((64, 1, 1), (256, 1, 1), (1024, 1, 1), (64, 4, 8), (1024, 8, 16)):
+        loop = clf.rxloop(hfr, slots=16, max_burst=burst, workers=workers, lifetime_ms=30000)
+        try:
+            offs = np.arange(burst, dtype=np.uint64) * np.uint64(stride)
+            loop.drive(offs, 50, depth)  # warm
+            lat, el = loop.drive(offs, iters, depth)
+        finally:
+            loop.stop()
+        r = pct(lat)
+        r["mpps"] = round(burst * iters / (el / 1e9) / 1e6, 2)
+        out[f"loop_burst{burst}_w{workers}_d{depth}"] = r
+    hv = torch.empty(64 * vbytes, dtype=torch.uint8).pin_memory()
+    lat = []
+    for i in range(iters // 4 + 20):
+        t0 = time.perf_counter_ns()
+        clf.classify_host(hfr, 64, stride, verdicts=hv, mode=g.E2E_ZEROCOPY, nstreams=1)
+        if i >= 20:
+            lat.append(time.perf_counter_ns() - t0)
+    out["launch_per_burst64"] = pct(np.array(lat))
+    del dfr, hfr, hv, clf
+    torch.cuda.empty_cache()
     return out
 
 

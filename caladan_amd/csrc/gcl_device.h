@@ -37,6 +37,58 @@ __device__ __forceinline__ uint4 load16_a4(const void *p)
 	                  __builtin_nontemporal_load(q + 2), __builtin_nontemporal_load(q + 3));
 }
 
+/* System-scope (sc0 sc1) accesses for host memory the CPU rewrites while a
+ * persistent kernel runs (the rx loop's burst slots, table images and the
+ * frames of a recycled mbuf pool): they miss in every GPU cache, so a line
+ * cached by an earlier burst can never be returned stale. */
+__device__ __forceinline__ uint32_t ld_sys32(const void *p)
+{
+	return __hip_atomic_load((const uint32_t *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ uint64_t ld_sys64(const void *p)
+{
+	return __hip_atomic_load((const uint64_t *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ void st_sys32(void *p, uint32_t v)
+{
+	__hip_atomic_store((uint32_t *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+/* byte @a of a host region of @len bytes, system scope; 0 past the end */
+__device__ __forceinline__ uint8_t byte_sys(const uint8_t *base, uint64_t len, uint64_t a)
+{
+	return a < len ? (uint8_t)(ld_sys32(base + (a & ~3ull)) >> (8 * (a & 3))) : 0;
+}
+
+/* 16 bytes at byte offset @a (any alignment) of a host region of @len bytes,
+ * system scope, bytes past the end read as 0: the dwords covering the range,
+ * funnel-shifted.  A dword that straddles @len lies inside the page that
+ * holds byte len-1, so loading it whole is safe. */
+__device__ __forceinline__ uint4 load16_sys(const uint8_t *base, uint64_t len, uint64_t a)
+{
+	const uint64_t a0 = a & ~3ull;
+	const uint32_t sh = (uint32_t)(a & 3);
+	uint32_t w[5];
+#pragma unroll
+	for (int i = 0; i < 5; i++) {
+		const uint64_t q = a0 + 4 * (uint64_t)i;
+		w[i] = (q < len && (i < 4 || sh)) ? ld_sys32(base + q) : 0;
+	}
+	uint32_t o[4];
+#pragma unroll
+	for (int i = 0; i < 4; i++)
+		o[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
+	if (a + 16 > len) {
+#pragma unroll
+		for (int b = 0; b < 16; b++)
+			if (a + b >= len)
+				o[b >> 2] &= ~(0xFFu << (8 * (b & 3)));
+	}
+	return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
 __device__ __forceinline__ uint32_t rotl(uint32_t x, int k)
 {
 	return (x << k) | (x >> (32 - k));

@@ -103,6 +103,13 @@ __device__ __forceinline__ uint8_t frame_byte(const KParams &k, uint64_t a)
 	return a < k.frames_len ? k.frames[a] : 0;
 }
 
+/* frame_byte with a system-scope load when SYS (the rx loop's host frames) */
+template <bool SYS>
+__device__ __forceinline__ uint8_t fbyte(const KParams &k, uint64_t a)
+{
+	return SYS ? gcl::byte_sys(k.frames, k.frames_len, a) : frame_byte(k, a);
+}
+
 template <bool GENERAL>
 __device__ __forceinline__ uint64_t frame_off(const KParams &k, uint64_t idx)
 {
@@ -216,7 +223,7 @@ __device__ __forceinline__ uint32_t toeplitz_lut(const uint32_t *toep, uint32_t 
  * stream (hash, probe, steer), and only the rare cases -- IHL != 5 ports, a
  * probe chain longer than one slot -- take a divergent branch.
  */
-template <int MODE, bool GENERAL>
+template <int MODE, bool GENERAL, bool SYS = false>
 __device__ __forceinline__ void classify_one(const KParams &k, const uint4 *tile, int tid,
                                              uint64_t idx, const Tables &tb, uint32_t *hist,
                                              Counters &cnt)
@@ -256,8 +263,8 @@ __device__ __forceinline__ void classify_one(const KParams &k, const uint4 *tile
 				dport = gcl::bswap16(tile_dword(tile, tid, o + 2) & 0xFFFF);
 			} else { /* past the staged granule */
 				const uint64_t a = frame_off<GENERAL>(k, idx) + 14 + 4 * ihl;
-				sport = (uint32_t)frame_byte(k, a) << 8 | frame_byte(k, a + 1);
-				dport = (uint32_t)frame_byte(k, a + 2) << 8 | frame_byte(k, a + 3);
+				sport = (uint32_t)fbyte<SYS>(k, a) << 8 | fbyte<SYS>(k, a + 1);
+				dport = (uint32_t)fbyte<SYS>(k, a + 2) << 8 | fbyte<SYS>(k, a + 3);
 			}
 		}
 		const uint32_t h = MODE == GCL_HASH_JENKINS
@@ -568,6 +575,199 @@ classify_kernel(KParams k)
 }
 
 /* ------------------------------------------------------------------------
+ * Persistent rx loop (gcl_rxloop_*): a burst-at-a-time classifier for the
+ * reference's own granularity, rx_burst's <= 64 mbufs (iokernel/rx.c:270-290).
+ * Each of `workers` 256-lane blocks owns tickets w+1, w+1+W, ...: it polls
+ * the ticket's ring slot in host memory, classifies the burst straight out of
+ * the registered ingress region, writes the verdicts back into the slot and
+ * publishes the ticket.  Everything the CPU writes is read with system-scope
+ * loads, so recycled mbufs and reused slots are never served from a stale
+ * cache line.  Every block leaves on the stop flag or at its own deadline
+ * (s_memrealtime, 100 MHz), so the grid always drains.
+ */
+struct LoopSlotHdr {       /* first 64 B of a ring slot */
+	uint64_t word;          /* host: the published burst, one load for the poller:
+	                           ticket[63:24] n[23:11] flags[10:7] img[6] img_seq%64[5:0] */
+	uint64_t done;          /* device: ticket completed */
+	uint32_t pad[12];
+};
+__host__ __device__ constexpr uint64_t loop_word(uint64_t t, uint32_t n, uint32_t fl, uint32_t img,
+                                                 uint32_t iseq)
+{
+	return (t & ((1ull << 40) - 1)) << 24 | (uint64_t)(n & 0x1FFF) << 11 | (fl & 0xF) << 7 |
+	       (img & 1) << 6 | (iseq & 63);
+}
+static_assert(sizeof(LoopSlotHdr) == 64, "LoopSlotHdr");
+
+struct LoopImgHdr {        /* first 64 B of a table image buffer */
+	uint32_t bytes, ipt_mask, off_rt, off_flow, off_toep, pad[11];
+};
+static_assert(sizeof(LoopImgHdr) == 64, "LoopImgHdr");
+
+#define GCL_LOOP_F_OLF  0x1
+#define GCL_LOOP_F_RSS  0x2
+#define GCL_LOOP_F_FDIR 0x4
+#define GCL_LOOP_F_HINT 0x8
+
+struct LoopParams {
+	uint8_t *slots;            /* device view of the slot ring */
+	uint64_t slot_bytes;
+	uint32_t nslots, workers;
+	uint32_t off_offs, off_olf, off_rss, off_fdir, off_hint, off_verd;
+	const uint8_t *img[2];     /* device views of the two image buffers */
+	const uint32_t *stop;
+	uint64_t lifetime_ticks;   /* s_memrealtime ticks each block may run */
+	const uint8_t *frames;     /* device view of the registered region */
+	uint64_t frames_len;
+	unsigned long long *counts, *stats;
+	uint32_t max_rt, cflags, default_flags;
+};
+
+constexpr uint32_t kLoopFixedLds = 256 * 64 + 256 * 8 + 3 * 256 * 4 + 256 * 8 + 256 + 64;
+
+template <int MODE>
+__global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
+{
+	extern __shared__ uint4 smem[];
+	uint4 *tile = smem;
+	uint64_t *s_offs = (uint64_t *)(tile + 1024);
+	uint32_t *s_rss = (uint32_t *)(s_offs + 256);
+	uint32_t *s_fdir = s_rss + 256;
+	uint32_t *s_hint = s_fdir + 256;
+	uint2 *s_verd = (uint2 *)(s_hint + 256);
+	uint8_t *s_olf = (uint8_t *)(s_verd + 256);
+	uint32_t *s_ctl = (uint32_t *)(s_olf + 256);
+	uint32_t *hist = s_ctl + 16;
+	uint8_t *lds_tab = (uint8_t *)(hist + ((L.max_rt + 3) & ~3u));
+	const int tid = threadIdx.x;
+	const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + L.lifetime_ticks;
+
+	KParams k = {};
+	k.frames = L.frames;
+	k.frames_len = L.frames_len;
+	k.offs = s_offs;
+	k.verdicts = s_verd;
+	k.max_rt = L.max_rt;
+	k.cflags = L.cflags;
+	k.default_flags = L.default_flags;
+	Tables tb = {};
+	uint32_t cur_seq = 0xFF; /* no image yet (versions are taken mod 64) */
+
+	for (uint64_t t = blockIdx.x + 1;; t += L.workers) {
+		uint8_t *slot = L.slots + ((t - 1) % L.nslots) * L.slot_bytes;
+		LoopSlotHdr *h = (LoopSlotHdr *)slot;
+		if (tid == 0) {
+			uint64_t w = 0;
+			for (;;) { /* one system-scope load per poll carries the whole burst header */
+				w = gcl::ld_sys64(&h->word);
+				if ((w >> 24) == (t & ((1ull << 40) - 1)))
+					break;
+				w = 0;
+				if (gcl::ld_sys32(L.stop) || __builtin_amdgcn_s_memrealtime() > t_end)
+					break;
+				__builtin_amdgcn_s_sleep(1);
+			}
+			s_ctl[0] = w != 0;
+			s_ctl[1] = (uint32_t)(w >> 11) & 0x1FFF;
+			s_ctl[2] = (uint32_t)(w >> 7) & 0xF;
+			s_ctl[3] = (uint32_t)(w >> 6) & 1;
+			s_ctl[4] = (uint32_t)w & 63;
+		}
+		__syncthreads();
+		if (!s_ctl[0])
+			break;
+		const uint32_t n = s_ctl[1], fl = s_ctl[2], img = s_ctl[3], img_seq = s_ctl[4];
+		if (img_seq != cur_seq) { /* a new table snapshot: copy it into LDS */
+			const uint8_t *ib = L.img[img];
+			const uint32_t bytes = gcl::ld_sys32(ib);
+			for (uint32_t i = tid; i < bytes / 4; i += 256)
+				((uint32_t *)lds_tab)[i] = gcl::ld_sys32(ib + 64 + 4 * i);
+			k.ipt_mask = gcl::ld_sys32(ib + 4);
+			tb.ipt = (const uint2 *)lds_tab;
+			tb.rtab = (const RtEntry *)(lds_tab + gcl::ld_sys32(ib + 8));
+			tb.flow = lds_tab + gcl::ld_sys32(ib + 12);
+			tb.toep = (const uint32_t *)(lds_tab + gcl::ld_sys32(ib + 16));
+			cur_seq = img_seq;
+		}
+		for (uint32_t i = tid; i < L.max_rt; i += 256)
+			hist[i] = 0;
+		Counters cnt = {0, 0, 0, 0};
+		__syncthreads(); /* s_ctl consumed, tables and hist ready */
+		for (uint32_t base = 0; base < n; base += 256) {
+			const uint32_t m = n - base < 256 ? n - base : 256;
+			if ((uint32_t)tid < m) {
+				const uint32_t i = base + tid;
+				s_offs[tid] = gcl::ld_sys64(slot + L.off_offs + 8 * i);
+				if (fl & GCL_LOOP_F_OLF)
+					s_olf[tid] = (uint8_t)(gcl::ld_sys32(slot + L.off_olf + (i & ~3u)) >> (8 * (i & 3)));
+				if (fl & GCL_LOOP_F_RSS)
+					s_rss[tid] = gcl::ld_sys32(slot + L.off_rss + 4 * i);
+				if (fl & GCL_LOOP_F_FDIR)
+					s_fdir[tid] = gcl::ld_sys32(slot + L.off_fdir + 4 * i);
+				if (fl & GCL_LOOP_F_HINT)
+					s_hint[tid] = gcl::ld_sys32(slot + L.off_hint + 4 * i);
+			}
+			__syncthreads();
+#pragma unroll
+			for (int j = 0; j < 4; j++) {
+				const int c = j * 256 + tid, p = c >> 2, q = c & 3;
+				tile[tile_slot(p, q)] = (uint32_t)p < m
+				        ? gcl::load16_sys(L.frames, L.frames_len, s_offs[p] + 16 * (uint64_t)q)
+				        : make_uint4(0, 0, 0, 0);
+			}
+			__syncthreads();
+			k.n = m;
+			k.olflags = (fl & GCL_LOOP_F_OLF) ? s_olf : nullptr;
+			k.rss = (fl & GCL_LOOP_F_RSS) ? s_rss : nullptr;
+			k.fdir = (fl & GCL_LOOP_F_FDIR) ? s_fdir : nullptr;
+			k.dst_hint = (fl & GCL_LOOP_F_HINT) ? s_hint : nullptr;
+			if ((uint32_t)tid < m) {
+				classify_one<MODE, true, true>(k, tile, tid, (uint64_t)tid, tb, hist, cnt);
+				uint8_t *vo = slot + L.off_verd;
+				if (L.cflags & GCL_CFG_VERDICT4) {
+					gcl::st_sys32(vo + 4 * (base + tid), ((const uint32_t *)s_verd)[tid]);
+				} else {
+					gcl::st_sys32(vo + 8 * (base + tid), s_verd[tid].x);
+					gcl::st_sys32(vo + 8 * (base + tid) + 4, s_verd[tid].y);
+				}
+			}
+			__syncthreads();
+		}
+		/* counters of this burst */
+		for (uint32_t i = tid; i < L.max_rt; i += 256)
+			if (hist[i] && L.counts)
+				atomicAdd(&L.counts[i], (unsigned long long)hist[i]);
+		if (L.stats) {
+			for (int off = 32; off > 0; off >>= 1) {
+				cnt.flowtag += __shfl_xor(cnt.flowtag, off);
+				cnt.hashmiss += __shfl_xor(cnt.hashmiss, off);
+				cnt.unreg += __shfl_xor(cnt.unreg, off);
+				cnt.unhandled += __shfl_xor(cnt.unhandled, off);
+			}
+			if ((tid & 63) == 0) {
+				if (cnt.flowtag)
+					atomicAdd(&L.stats[GCL_RX_FLOW_TAG_MATCH], (unsigned long long)cnt.flowtag);
+				if (cnt.hashmiss)
+					atomicAdd(&L.stats[GCL_RX_HASH_MISSING], (unsigned long long)cnt.hashmiss);
+				if (cnt.unreg)
+					atomicAdd(&L.stats[GCL_RX_UNREGISTERED_MAC], (unsigned long long)cnt.unreg);
+				if (cnt.unhandled)
+					atomicAdd(&L.stats[GCL_RX_UNHANDLED], (unsigned long long)cnt.unhandled);
+			}
+			if (tid == 0)
+				atomicAdd(&L.stats[GCL_RX_PULLED], (unsigned long long)n);
+		}
+		/* verdicts before the ticket: the verdict stores are system-scope
+		 * (write-through), so each wave only waits for its own to complete;
+		 * no L2 writeback (__threadfence_system) on the latency path */
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		__syncthreads();
+		if (tid == 0)
+			__hip_atomic_store(&h->done, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+	}
+}
+
+/* ------------------------------------------------------------------------
  * Synthetic generator kernel: one lane per packet writes its 64-B header.
  */
 struct Hdr {
@@ -736,6 +936,8 @@ struct gcl_ctx {
 	uint32_t off_rt, off_flow, off_toep, off_seed, off_crc, image_cap, image_bytes;
 	uint32_t flow_used;
 	bool dirty;
+	bool loop_dirty;              /* tables changed since the rx loop's last image */
+	struct gcl_rxloop *loop;      /* running persistent loop, or NULL */
 	/* Two device images + pinned staging.  No per-launch events: each image
 	 * remembers the streams that launched on it; when it stops being current
 	 * an event is recorded on each of them, and the upload that next
@@ -828,6 +1030,7 @@ extern "C" int gcl_open(int hip_device, const struct gcl_cfg *cfg, struct gcl_ct
 	c->image_bytes = 0;
 	c->flow_used = 0;
 	c->dirty = true;
+	c->loop_dirty = true;
 	c->cur = 0;
 	c->last_stream = nullptr;
 	c->prof_ms = 0;
@@ -898,6 +1101,8 @@ extern "C" void gcl_close(struct gcl_ctx *c)
 	if (!c)
 		return;
 	hipSetDevice(c->device);
+	if (c->loop)
+		gcl_rxloop_stop(c->loop);
 	hipDeviceSynchronize();
 	for (int i = 0; i < 2; i++) {
 		hipFree(c->dimg[i]);
@@ -963,6 +1168,7 @@ extern "C" int gcl_runtime_set(struct gcl_ctx *c, uint16_t uniqid, uint32_t ip_h
 		for (int i = 0; i < thread_count; i++)
 			r.flow[i] = (uint8_t)flow_tbl[i];
 	c->dirty = true;
+	c->loop_dirty = true;
 	return 0;
 }
 
@@ -974,6 +1180,7 @@ extern "C" int gcl_runtime_set_trans_seed(struct gcl_ctx *c, uint16_t uniqid, ui
 		return -ENOENT;
 	c->rt[uniqid].trans_seed = seed;
 	c->dirty = true;
+	c->loop_dirty = true;
 	return 0;
 }
 
@@ -983,6 +1190,7 @@ extern "C" int gcl_runtime_del(struct gcl_ctx *c, uint16_t uniqid)
 		return -ENOENT;
 	c->rt[uniqid] = gcl_ctx::Rt();
 	c->dirty = true;
+	c->loop_dirty = true;
 	return 0;
 }
 
@@ -1654,8 +1862,10 @@ static void *mapped(const void *h)
 	void *d = nullptr;
 	if (!h)
 		return nullptr;
-	if (hipHostGetDevicePointer(&d, (void *)h, 0) != hipSuccess)
+	if (hipHostGetDevicePointer(&d, (void *)h, 0) != hipSuccess) {
+		(void)hipGetLastError(); /* not registered: do not leave a sticky error */
 		return nullptr;
+	}
 	return d;
 }
 
@@ -1774,5 +1984,304 @@ extern "C" int gcl_classify_host(struct gcl_ctx *c, const struct gcl_batch *hb,
 		for (int i = 0; i < GCL_NR_STATS; i++)
 			host_stats[i] += tmp[max_rt + i];
 	c->last_stream = s0;
+	return 0;
+}
+
+/* ==========================================================================
+ * Persistent rx loop (host side).  Ring slots and table images live in
+ * coherent, mapped host memory; the CPU publishes a slot with a release store
+ * of its ticket, the kernel answers with a release store of `done`.
+ */
+#include <time.h>
+
+struct gcl_rxloop {
+	gcl_ctx *c;
+	hipStream_t st;
+	uint8_t *slots;          /* host view */
+	uint8_t *img[2];         /* host views: LoopImgHdr + image */
+	uint32_t *ctl;           /* stop flag */
+	LoopParams lp;
+	uint32_t max_burst, vbytes;
+	uint64_t next;           /* last ticket issued */
+	uint32_t cur_img, img_seq;
+	uint64_t img_last[2];    /* last ticket that read image i */
+	std::vector<uint64_t> retired; /* per slot: last ticket the host collected */
+	bool ended;
+};
+
+static uint64_t now_ns()
+{
+	struct timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
+static LoopSlotHdr *loop_slot(gcl_rxloop *L, uint64_t t)
+{
+	return (LoopSlotHdr *)(L->slots + ((t - 1) % L->lp.nslots) * L->lp.slot_bytes);
+}
+
+static bool loop_ended(gcl_rxloop *L)
+{
+	if (!L->ended && hipStreamQuery(L->st) != hipErrorNotReady)
+		L->ended = true;
+	return L->ended;
+}
+
+static bool ticket_done(gcl_rxloop *L, uint64_t t)
+{
+	if (t == 0 || t + L->lp.nslots <= L->next)
+		return true; /* never issued, or its slot has been reused since */
+	return __atomic_load_n(&loop_slot(L, t)->done, __ATOMIC_ACQUIRE) >= t;
+}
+
+/* Build the current tables into image buffer @i (host memory). */
+static int loop_write_image(gcl_rxloop *L, int i)
+{
+	gcl_ctx *c = L->c;
+	hipEventSynchronize(c->staging_free);
+	const uint32_t bytes = build_image(c);
+	if (bytes > kLdsTableBudget)
+		return -E2BIG;
+	LoopImgHdr hdr = {};
+	hdr.bytes = bytes;
+	hdr.ipt_mask = c->ipt_slots - 1;
+	hdr.off_rt = c->off_rt;
+	hdr.off_flow = c->off_flow;
+	hdr.off_toep = c->off_toep;
+	memcpy(L->img[i] + 64, c->staging, bytes);
+	memcpy(L->img[i], &hdr, sizeof(hdr));
+	c->loop_dirty = false;
+	return 0;
+}
+
+template <int MODE>
+static hipError_t loop_launch(const LoopParams &lp, uint32_t lds, hipStream_t s)
+{
+	if (lds > 64 * 1024)
+		hipFuncSetAttribute((const void *)rxloop_kernel<MODE>,
+		                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+	hipLaunchKernelGGL(rxloop_kernel<MODE>, dim3(lp.workers), dim3(256), lds, s, lp);
+	return hipGetLastError();
+}
+
+extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *cfg,
+                                struct gcl_rxloop **out)
+{
+	if (!c || !cfg || !out || !cfg->region || !cfg->region_len || cfg->slots < 2 ||
+	    cfg->slots > 1024 || (cfg->slots & (cfg->slots - 1)) || !cfg->max_burst ||
+	    cfg->max_burst > 4096 || !cfg->workers || cfg->workers > 16 || !cfg->lifetime_ms ||
+	    cfg->lifetime_ms > 600000)
+		return -EINVAL;
+	if (c->cfg.flags & GCL_CFG_TRANS_HASH)
+		return -ENOTSUP;
+	if (c->loop)
+		return -EBUSY;
+	if (hipSetDevice(c->device) != hipSuccess)
+		return -ENODEV;
+	void *frames_d = mapped(cfg->region);
+	if (!frames_d)
+		return -EINVAL; /* not registered */
+	gcl_rxloop *L = new (std::nothrow) gcl_rxloop();
+	if (!L)
+		return -ENOMEM;
+	L->c = c;
+	L->retired.assign(cfg->slots, 0);
+	L->max_burst = cfg->max_burst;
+	L->vbytes = (c->cfg.flags & GCL_CFG_VERDICT4) ? 4 : 8;
+	const uint64_t mb = align16(cfg->max_burst);
+	LoopParams &lp = L->lp;
+	lp.off_offs = 64;
+	lp.off_olf = lp.off_offs + 8 * mb;
+	lp.off_rss = lp.off_olf + mb;
+	lp.off_fdir = lp.off_rss + 4 * mb;
+	lp.off_hint = lp.off_fdir + 4 * mb;
+	lp.off_verd = lp.off_hint + 4 * mb;
+	lp.slot_bytes = (lp.off_verd + 8 * mb + 255) & ~255ull;
+	lp.nslots = cfg->slots;
+	lp.workers = cfg->workers;
+	lp.lifetime_ticks = (uint64_t)cfg->lifetime_ms * 100000ull;
+	lp.frames = (const uint8_t *)frames_d;
+	lp.frames_len = cfg->region_len;
+	lp.counts = (unsigned long long *)cfg->counts;
+	lp.stats = (unsigned long long *)cfg->stats;
+	lp.max_rt = c->cfg.max_runtimes;
+	lp.cflags = c->cfg.flags;
+	lp.default_flags = c->cfg.default_olflags;
+	const unsigned hf = hipHostMallocCoherent | hipHostMallocMapped;
+	int ret = -ENOMEM;
+	void *d;
+	if (hipHostMalloc((void **)&L->slots, lp.nslots * lp.slot_bytes, hf) != hipSuccess ||
+	    hipHostMalloc((void **)&L->img[0], 64 + c->image_cap, hf) != hipSuccess ||
+	    hipHostMalloc((void **)&L->img[1], 64 + c->image_cap, hf) != hipSuccess ||
+	    hipHostMalloc((void **)&L->ctl, 64, hf) != hipSuccess)
+		goto fail;
+	memset(L->slots, 0, lp.nslots * lp.slot_bytes);
+	memset(L->ctl, 0, 64);
+	ret = loop_write_image(L, 0);
+	if (ret)
+		goto fail;
+	L->cur_img = 0;
+	L->img_seq = 1;
+	ret = -EIO;
+	if (hipHostGetDevicePointer(&d, L->slots, 0) != hipSuccess)
+		goto fail;
+	lp.slots = (uint8_t *)d;
+	for (int i = 0; i < 2; i++) {
+		if (hipHostGetDevicePointer(&d, L->img[i], 0) != hipSuccess)
+			goto fail;
+		lp.img[i] = (const uint8_t *)d;
+	}
+	if (hipHostGetDevicePointer(&d, L->ctl, 0) != hipSuccess)
+		goto fail;
+	lp.stop = (const uint32_t *)d;
+	if (hipStreamCreateWithFlags(&L->st, hipStreamNonBlocking) != hipSuccess)
+		goto fail;
+	{
+		const uint32_t lds = kLoopFixedLds + ((lp.max_rt + 3) & ~3u) * 4 + kLdsTableBudget;
+		hipError_t e = c->cfg.hash_mode == GCL_HASH_NIC ? loop_launch<GCL_HASH_NIC>(lp, lds, L->st)
+		             : c->cfg.hash_mode == GCL_HASH_JENKINS ? loop_launch<GCL_HASH_JENKINS>(lp, lds, L->st)
+		             : loop_launch<GCL_HASH_TOEPLITZ>(lp, lds, L->st);
+		if (e != hipSuccess) {
+			hipStreamDestroy(L->st);
+			L->st = nullptr;
+			goto fail;
+		}
+	}
+	c->loop = L;
+	*out = L;
+	return 0;
+fail:
+	hipHostFree(L->slots);
+	hipHostFree(L->img[0]);
+	hipHostFree(L->img[1]);
+	hipHostFree(L->ctl);
+	delete L;
+	return ret;
+}
+
+extern "C" int64_t gcl_rxloop_submit(struct gcl_rxloop *L, uint32_t n, const uint64_t *offs,
+                                     const uint8_t *olflags, const uint32_t *rss,
+                                     const uint32_t *fdir_hi, const uint32_t *dst_hint)
+{
+	if (!L || !n || n > L->max_burst || !offs)
+		return -EINVAL;
+	if (loop_ended(L))
+		return -ESHUTDOWN;
+	const uint64_t t = L->next + 1;
+	/* a slot is reused only after the host collected its previous burst */
+	if (t > L->lp.nslots && L->retired[(t - 1) % L->lp.nslots] < t - L->lp.nslots)
+		return -EAGAIN;
+	if (L->c->loop_dirty) {
+		/* the other image buffer: wait for the last burst that read it */
+		const int x = L->cur_img ^ 1;
+		while (!ticket_done(L, L->img_last[x]))
+			if (loop_ended(L))
+				return -ESHUTDOWN;
+		const int ret = loop_write_image(L, x);
+		if (ret)
+			return ret;
+		L->cur_img = x;
+		L->img_seq++;
+	}
+	LoopSlotHdr *h = loop_slot(L, t);
+	uint8_t *s = (uint8_t *)h;
+	uint32_t fl = 0;
+	memcpy(s + L->lp.off_offs, offs, 8ull * n);
+	if (olflags) {
+		memcpy(s + L->lp.off_olf, olflags, n);
+		fl |= GCL_LOOP_F_OLF;
+	}
+	if (rss) {
+		memcpy(s + L->lp.off_rss, rss, 4ull * n);
+		fl |= GCL_LOOP_F_RSS;
+	}
+	if (fdir_hi) {
+		memcpy(s + L->lp.off_fdir, fdir_hi, 4ull * n);
+		fl |= GCL_LOOP_F_FDIR;
+	}
+	if (dst_hint) {
+		memcpy(s + L->lp.off_hint, dst_hint, 4ull * n);
+		fl |= GCL_LOOP_F_HINT;
+	}
+	__atomic_store_n(&h->word, loop_word(t, n, fl, L->cur_img, L->img_seq), __ATOMIC_RELEASE);
+	L->img_last[L->cur_img] = t;
+	L->next = t;
+	return (int64_t)t;
+}
+
+extern "C" int gcl_rxloop_wait(struct gcl_rxloop *L, int64_t ticket, void *verdicts_out,
+                               uint64_t spin_ns)
+{
+	if (!L || ticket < 1 || (uint64_t)ticket > L->next)
+		return -EINVAL;
+	const uint64_t t = (uint64_t)ticket;
+	if (t + L->lp.nslots <= L->next)
+		return -ESTALE;
+	LoopSlotHdr *h = loop_slot(L, t);
+	const uint64_t t0 = spin_ns ? now_ns() : 0;
+	uint32_t k = 0;
+	while (__atomic_load_n(&h->done, __ATOMIC_ACQUIRE) < t) {
+		if (!spin_ns || (++k & 255) == 0) {
+			if (loop_ended(L))
+				return __atomic_load_n(&h->done, __ATOMIC_ACQUIRE) >= t ? 0 : -ESHUTDOWN;
+			if (!spin_ns || now_ns() - t0 >= spin_ns)
+				return -EAGAIN;
+		}
+		__builtin_ia32_pause();
+	}
+	if (verdicts_out)
+		memcpy(verdicts_out, (uint8_t *)h + L->lp.off_verd,
+		       (size_t)((h->word >> 11) & 0x1FFF) * L->vbytes);
+	uint64_t &r = L->retired[(t - 1) % L->lp.nslots];
+	if (r < t)
+		r = t;
+	return 0;
+}
+
+extern "C" int gcl_rxloop_stop(struct gcl_rxloop *L)
+{
+	if (!L)
+		return -EINVAL;
+	__atomic_store_n(L->ctl, 1u, __ATOMIC_RELEASE);
+	const hipError_t e = hipStreamSynchronize(L->st);
+	hipStreamDestroy(L->st);
+	hipHostFree(L->slots);
+	hipHostFree(L->img[0]);
+	hipHostFree(L->img[1]);
+	hipHostFree(L->ctl);
+	if (L->c->loop == L)
+		L->c->loop = nullptr;
+	delete L;
+	return e == hipSuccess ? 0 : -EIO;
+}
+
+extern "C" int gcl_rxloop_drive(struct gcl_rxloop *L, uint32_t n, const uint64_t *offs,
+                                uint32_t iters, uint32_t depth, uint64_t *lat_ns,
+                                uint64_t *elapsed_ns)
+{
+	if (!L || !offs || !iters || !depth || depth > L->lp.nslots)
+		return -EINVAL;
+	std::vector<int64_t> tk(iters);
+	std::vector<uint64_t> t_sub(iters);
+	uint32_t head = 0, tail = 0; /* submitted, retired */
+	const uint64_t t0 = now_ns();
+	while (tail < iters) {
+		while (head < iters && head - tail < depth) {
+			t_sub[head] = now_ns();
+			const int64_t r = gcl_rxloop_submit(L, n, offs, nullptr, nullptr, nullptr, nullptr);
+			if (r < 0)
+				return (int)r;
+			tk[head++] = r;
+		}
+		const int r = gcl_rxloop_wait(L, tk[tail], nullptr, 1000000000ull);
+		if (r)
+			return r;
+		if (lat_ns)
+			lat_ns[tail] = now_ns() - t_sub[tail];
+		tail++;
+	}
+	if (elapsed_ns)
+		*elapsed_ns = now_ns() - t0;
 	return 0;
 }

@@ -103,6 +103,13 @@ class GclE2eOpts(ctypes.Structure):
 E2E_COPY, E2E_ZEROCOPY = 0, 1
 
 
+class GclRxloopCfg(ctypes.Structure):
+    _fields_ = [("slots", ctypes.c_uint32), ("max_burst", ctypes.c_uint32),
+                ("workers", ctypes.c_uint32), ("lifetime_ms", ctypes.c_uint32),
+                ("region", ctypes.c_void_p), ("region_len", ctypes.c_uint64),
+                ("counts", ctypes.c_void_p), ("stats", ctypes.c_void_p)]
+
+
 class GclVerdict(ctypes.Structure):
     _fields_ = [("hash", ctypes.c_uint32), ("uniqid", ctypes.c_uint16),
                 ("thread", ctypes.c_uint8), ("action", ctypes.c_uint8)]
@@ -178,6 +185,11 @@ def _load():
         "gcl_host_register": (i32, [vp, ctypes.c_size_t]),
         "gcl_dev_alloc": (i32, [i32, ctypes.c_size_t, ctypes.POINTER(vp)]),
         "gcl_dev_free": (i32, [vp]),
+        "gcl_rxloop_start": (i32, [vp, ctypes.POINTER(GclRxloopCfg), ctypes.POINTER(vp)]),
+        "gcl_rxloop_submit": (ctypes.c_int64, [vp, u32, vp, vp, vp, vp, vp]),
+        "gcl_rxloop_wait": (i32, [vp, ctypes.c_int64, vp, u64]),
+        "gcl_rxloop_stop": (i32, [vp]),
+        "gcl_rxloop_drive": (i32, [vp, u32, vp, u32, u32, vp, ctypes.POINTER(u64)]),
         "gcl_dev_alloc_paired": (i32, [i32, ctypes.c_size_t, vp, ctypes.c_size_t, u32,
                                        ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_double)]),
         "gcl_host_unregister": (i32, [vp]),
@@ -411,6 +423,9 @@ class Classifier:
         _check(lib.gcl_open(device, ctypes.byref(cfg), ctypes.byref(self._ctx)), "gcl_open")
 
     def close(self):
+        loop = getattr(self, "_loop", None)
+        if loop is not None:
+            loop.stop()  # gcl_close would free it under the RxLoop object
         if self._ctx:
             lib.gcl_close(self._ctx)
             self._ctx = ctypes.c_void_p()
@@ -473,6 +488,12 @@ class Classifier:
         return _check(lib.gcl_classify_host(self._ctx, ctypes.byref(b), _ptr(verdicts), _ptr(counts),
                                             _ptr(stats), ctypes.byref(o)), "gcl_classify_host")
 
+    def rxloop(self, region, slots=64, max_burst=GCL_RX_BURST_SIZE, workers=1, lifetime_ms=20000,
+               counts=None, stats=None, region_len=None):
+        """Start the persistent rx loop over a registered host region."""
+        return RxLoop(self, region, slots, max_burst, workers, lifetime_ms, counts, stats,
+                      region_len)
+
     def sync(self):
         return _check(lib.gcl_sync(self._ctx), "gcl_sync")
 
@@ -493,3 +514,58 @@ def version():
 
 
 __all__ = [n for n in dir() if not n.startswith("_")]
+
+
+class RxLoop:
+    """gcl_rxloop_*: burst-at-a-time classification by a persistent kernel."""
+
+    def __init__(self, clf, region, slots, max_burst, workers, lifetime_ms, counts, stats,
+                 region_len=None):
+        self.clf, self.max_burst = clf, max_burst
+        cfg = GclRxloopCfg(slots=slots, max_burst=max_burst, workers=workers,
+                           lifetime_ms=lifetime_ms, region=_ptr(region),
+                           region_len=_nbytes(region) if region_len is None else region_len,
+                           counts=_ptr(counts), stats=_ptr(stats))
+        h = ctypes.c_void_p()
+        _check(lib.gcl_rxloop_start(clf._ctx, ctypes.byref(cfg), ctypes.byref(h)), "gcl_rxloop_start")
+        self._h = h
+        clf._loop = self
+
+    def submit(self, offs, olflags=None, rss=None, fdir_hi=None, dst_hint=None):
+        """Returns the ticket, or a negative errno (-EAGAIN: ring full)."""
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        conv = lambda a, dt: None if a is None else np.ascontiguousarray(a, dtype=dt)
+        self._keep = [conv(olflags, np.uint8), conv(rss, np.uint32), conv(fdir_hi, np.uint32),
+                      conv(dst_hint, np.uint32)]
+        o, r, f, d = self._keep
+        return lib.gcl_rxloop_submit(self._h, len(offs), _ptr(offs), _ptr(o), _ptr(r), _ptr(f), _ptr(d))
+
+    def wait(self, ticket, n, spin_ns=2_000_000_000):
+        """Verdicts of a burst of @n packets (numpy structured array)."""
+        dt = VERDICT4_DTYPE if self.clf.vbytes == 4 else VERDICT_DTYPE
+        out = np.zeros(n, dtype=dt)
+        ret = lib.gcl_rxloop_wait(self._h, ticket, out.ctypes.data, spin_ns)
+        if ret:
+            raise OSError(-ret, f"gcl_rxloop_wait: {os.strerror(-ret)}")
+        return out
+
+    def drive(self, offs, iters, depth=1):
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        lat = np.zeros(iters, dtype=np.uint64)
+        el = ctypes.c_uint64()
+        _check(lib.gcl_rxloop_drive(self._h, len(offs), _ptr(offs), iters, depth, lat.ctypes.data,
+                                    ctypes.byref(el)), "gcl_rxloop_drive")
+        return lat, el.value
+
+    def stop(self):
+        if self._h:
+            h, self._h = self._h, None
+            if getattr(self.clf, "_loop", None) is self:
+                self.clf._loop = None
+            _check(lib.gcl_rxloop_stop(h), "gcl_rxloop_stop")
+
+    def __del__(self):
+        try:
+            self.stop()
+        except Exception:
+            pass

@@ -410,6 +410,56 @@ int gcl_dev_free(void *p);
 int gcl_dev_alloc_paired(int hip_device, size_t bytes, const void *partner, size_t partner_bytes,
                          uint32_t flags, void **out, double *probe_us);
 
+/*
+ * Persistent rx loop: the classifier at the reference's own granularity, one
+ * rx_burst of <= IOKERNEL_RX_BURST_SIZE mbufs at a time (iokernel/rx.c:270-290,
+ * defs.h:75), with microsecond latency instead of batch latency.  A
+ * persistent kernel polls a ring of burst slots in coherent host memory,
+ * classifies each burst straight from the registered ingress region (the 2
+ * GiB mbuf pool, shm.h:14-15) and writes the verdicts back into the slot.
+ *
+ * gcl_rxloop_start - launch the loop for @ctx.  @cfg->region must be
+ *   registered with gcl_host_register; frames are addressed by byte offsets
+ *   into it (mbuf data pointer - region base, like ptr_to_shmptr, shm.h:40-47).
+ *   The kernel leaves by itself after @cfg->lifetime_ms.  Tables must fit in
+ *   LDS (-E2BIG otherwise); GCL_CFG_TRANS_HASH is not supported (-ENOTSUP);
+ *   one loop per context (-EBUSY).  Table changes made with gcl_runtime_set /
+ *   _del apply from the next submitted burst on (snapshot semantics).
+ * gcl_rxloop_submit - publish one burst; returns its ticket (> 0), -EAGAIN
+ *   when the ring is full (a slot is reused only after gcl_rxloop_wait has
+ *   collected the burst it held, as an lrpc ring's consumer frees a slot), -EINVAL, -E2BIG (tables grew past LDS) or
+ *   -ESHUTDOWN when the kernel has left.  The arrays are copied; the side
+ *   arrays (olflags, rss, fdir_hi, dst_hint) are optional, as in gcl_batch.
+ * gcl_rxloop_wait - spin up to @spin_ns for @ticket; 0 and the burst's
+ *   verdicts (gcl_verdict or gcl_verdict4 per the context) copied to
+ *   @verdicts_out (may be NULL), -EAGAIN if not done yet, -ESTALE if the slot
+ *   was already reused, -ESHUTDOWN if the kernel left first.
+ * gcl_rxloop_stop - raise the stop flag, wait for the kernel, free the loop.
+ * gcl_rxloop_drive - measurement helper: @iters bursts of the same @n offsets
+ *   with @depth bursts in flight; lat_ns[i] = submit -> verdicts seen of
+ *   burst i, *elapsed_ns the whole run.
+ */
+struct gcl_rxloop;
+struct gcl_rxloop_cfg {
+	uint32_t slots;        /* ring depth: power of two, 2..1024 */
+	uint32_t max_burst;    /* packets per burst: 1..4096 */
+	uint32_t workers;      /* polling workgroups: 1..16 */
+	uint32_t lifetime_ms;  /* kernel lifetime bound: 1..600000 */
+	const void *region;    /* registered host region holding the frames */
+	uint64_t region_len;
+	uint64_t *counts;      /* device u64[max_runtimes] (optional), accumulated */
+	uint64_t *stats;       /* device u64[GCL_NR_STATS] (optional), accumulated */
+};
+int gcl_rxloop_start(struct gcl_ctx *ctx, const struct gcl_rxloop_cfg *cfg,
+                     struct gcl_rxloop **out);
+int64_t gcl_rxloop_submit(struct gcl_rxloop *loop, uint32_t n, const uint64_t *offs,
+                          const uint8_t *olflags, const uint32_t *rss, const uint32_t *fdir_hi,
+                          const uint32_t *dst_hint);
+int gcl_rxloop_wait(struct gcl_rxloop *loop, int64_t ticket, void *verdicts_out, uint64_t spin_ns);
+int gcl_rxloop_stop(struct gcl_rxloop *loop);
+int gcl_rxloop_drive(struct gcl_rxloop *loop, uint32_t n, const uint64_t *offs, uint32_t iters,
+                     uint32_t depth, uint64_t *lat_ns, uint64_t *elapsed_ns);
+
 /* Library version string. */
 const char *gcl_version(void);
 

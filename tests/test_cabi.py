@@ -354,3 +354,16 @@ def test_dev_alloc_paired_rejects_bad_args(g):
     assert f(0, 1 << 20, 4096, 1 << 20, g.PAIR_NEW_READS, None, None) == -22
     # the read side must hold one 256-packet tile of 64-B granules
     assert f(0, 1 << 13, 4096, 1 << 20, g.PAIR_NEW_READS, ctypes.byref(out), None) == -22
+
+
+def test_rxloop_rejects_bad_args(g):
+    """The persistent-loop entry points validate before touching the GPU."""
+    out = ctypes.c_void_p()
+    cfg = g.GclRxloopCfg(slots=64, max_burst=64, workers=1, lifetime_ms=1000, region=4096,
+                         region_len=1 << 20)
+    assert g.lib.gcl_rxloop_start(None, ctypes.byref(cfg), ctypes.byref(out)) == -22
+    assert g.lib.gcl_rxloop_submit(None, 1, 4096, None, None, None, None) == -22
+    assert g.lib.gcl_rxloop_wait(None, 1, None, 0) == -22
+    assert g.lib.gcl_rxloop_stop(None) == -22
+    assert g.lib.gcl_rxloop_drive(None, 1, 4096, 1, 1, None, None) == -22
+    assert ctypes.sizeof(g.GclRxloopCfg) == 48

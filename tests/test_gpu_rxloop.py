@@ -1,0 +1,179 @@
+"""GPU parity of the persistent rx loop (gcl_rxloop_*): bursts of <= 64
+mbufs (IOKERNEL_RX_BURST_SIZE, iokernel/defs.h:75) classified by a persistent
+kernel straight from a registered host region, bit-exact against the oracle
+run over the same packets, including table changes between bursts, recycled
+mbufs (the same addresses rewritten by the CPU), several workers and a full
+ring."""
+import time
+
+import numpy as np
+import pytest
+
+from tests.rxcases import apply_runtimes, fuzz_batch, random_runtimes, to_verdict4
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def g():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from caladan_amd import gclassify
+    return gclassify
+
+
+def bursts(n, size=64):
+    return [(s, min(n, s + size)) for s in range(0, n, size)]
+
+
+def want(ve, tc, v4):
+    return to_verdict4(ve, tc) if v4 else ve
+
+
+def tc_map(rts, max_rt):
+    tc = np.ones(max_rt, dtype=np.int64)
+    for r in rts:
+        tc[r["uniqid"]] = r["thread_count"]
+    return tc
+
+
+@pytest.mark.parametrize("v4", [False, True])
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_rxloop_fuzz_vs_oracle(g, orc, mode, v4):
+    rng = np.random.default_rng(7000 + 10 * mode + v4)
+    max_rt = 1024 if mode == 1 else 16
+    rts = random_runtimes(rng, max_rt, 300 if max_rt == 1024 else 12)
+    n = 3000
+    frames, flen, offs, olf, rss, fdir, hint = fuzz_batch(rng, n, rts, max_rt)
+    key = bytes(rng.integers(0, 256, size=40, dtype=np.uint8))
+    cflags = g.CFG_VERDICT4 if v4 else 0
+    t = orc.Tables(max_rt, mode, 0, 0x09, key)
+    apply_runtimes(t, rts)
+    clf = g.Classifier(0, max_rt, mode, cflags, 0x09, key)
+    apply_runtimes(clf, rts)
+    ve, ce, se = t.classify(frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir_hi=fdir,
+                            frames_len=flen, dst_hint=hint)
+    g.host_register(frames)
+    cnt = torch.zeros(max_rt, dtype=torch.int64, device="cuda")
+    st = torch.zeros(g.NR_STATS, dtype=torch.int64, device="cuda")
+    loop = clf.rxloop(frames, slots=8, counts=cnt, stats=st, region_len=flen)
+    try:
+        got = []
+        for a, b in bursts(n):
+            tk = loop.submit(offs[a:b], olf[a:b], rss[a:b], fdir[a:b], hint[a:b])
+            assert tk > 0
+            got.append(loop.wait(tk, b - a))
+        got = np.concatenate(got)
+    finally:
+        loop.stop()
+        g.host_unregister(frames)
+    w = want(ve, tc_map(rts, max_rt), v4)
+    bad = np.nonzero(got != w)[0]
+    assert not len(bad), f"{len(bad)} differ, first {bad[0]}: {got[bad[0]]} vs {w[bad[0]]}"
+    torch.cuda.synchronize()
+    assert (cnt.cpu().numpy().astype(np.uint64) == ce).all()
+    assert (st.cpu().numpy().astype(np.uint64) == se).all()
+
+
+def test_rxloop_tables_and_recycled_mbufs(g, orc):
+    """Table changes apply from the next burst on; frames rewritten in place
+    by the CPU between bursts are read fresh (system-scope loads)."""
+    rng = np.random.default_rng(7100)
+    max_rt = 64
+    rts = random_runtimes(rng, max_rt, 20)
+    n = 64
+    frames, flen, offs, olf, rss, fdir, hint = fuzz_batch(rng, n, rts, max_rt, tail_runts=False)
+    t = orc.Tables(max_rt, 1, 0, 0x09)
+    apply_runtimes(t, rts)
+    clf = g.Classifier(0, max_rt, 1, 0, 0x09)
+    apply_runtimes(clf, rts)
+    g.host_register(frames)
+    loop = clf.rxloop(frames, slots=4)
+    try:
+        for rnd in range(6):
+            tk = loop.submit(offs, olf, None, fdir, None)
+            got = loop.wait(tk, n)
+            ve, _, _ = t.classify(frames, n, 0, offs=offs, olflags=olf, fdir_hi=fdir)
+            assert (got == ve).all(), f"round {rnd}"
+            # tables: drop two runtimes, add a new one at a fresh uniqid
+            for r in rts[:2]:
+                assert t.runtime_del(r["uniqid"]) == 0
+                clf.runtime_del(r["uniqid"])
+            rts = rts[2:]
+            fresh = random_runtimes(rng, max_rt, 40)
+            used = {r["uniqid"] for r in rts} | {r["ip"] for r in rts}
+            add = [r for r in fresh if r["uniqid"] not in used and r["ip"] not in used][:1]
+            apply_runtimes(t, add)
+            apply_runtimes(clf, add)
+            rts += add
+            # recycled mbufs: new packets at the same addresses
+            nf, _, _, olf, _, fdir, _ = fuzz_batch(rng, n, rts, max_rt, tail_runts=False)
+            assert nf.shape == frames.shape
+            frames[:] = nf
+    finally:
+        loop.stop()
+        g.host_unregister(frames)
+
+
+def test_rxloop_workers_pipelined_and_full_ring(g, orc):
+    rng = np.random.default_rng(7200)
+    max_rt = 16
+    rts = random_runtimes(rng, max_rt, 12)
+    n = 64 * 40
+    frames, flen, offs, olf, rss, fdir, hint = fuzz_batch(rng, n, rts, max_rt)
+    t = orc.Tables(max_rt, 1, g.CFG_VERDICT4, 0x09)
+    apply_runtimes(t, rts)
+    clf = g.Classifier(0, max_rt, 1, g.CFG_VERDICT4, 0x09)
+    apply_runtimes(clf, rts)
+    ve, _, _ = t.classify(frames, n, 0, offs=offs, olflags=olf, frames_len=flen)
+    w = to_verdict4(ve, tc_map(rts, max_rt))
+    g.host_register(frames)
+    loop = clf.rxloop(frames, slots=8, workers=4, region_len=flen)
+    try:
+        bs = bursts(n)
+        # a full ring refuses the next burst until the oldest one is retired
+        tks = [loop.submit(offs[a:b], olf[a:b]) for a, b in bs[:8]]
+        assert all(x > 0 for x in tks)
+        assert loop.submit(offs[:64], olf[:64]) == -11  # -EAGAIN
+        got = [loop.wait(tk, 64) for tk in tks]
+        for a, b in bs[8:]:
+            tk = loop.submit(offs[a:b], olf[a:b])
+            assert tk > 0
+            tks.append(tk)
+            if len(tks) - len(got) == 8:
+                got.append(loop.wait(tks[len(got)], 64))
+        while len(got) < len(tks):
+            got.append(loop.wait(tks[len(got)], 64))
+        got = np.concatenate(got)
+        assert (got == w).all()
+        lat, el = loop.drive(offs[:64], 200, depth=4)
+        assert (lat > 0).all() and el > 0
+    finally:
+        loop.stop()
+        g.host_unregister(frames)
+
+
+def test_rxloop_lifetime_and_errors(g):
+    frames = np.zeros(1 << 16, dtype=np.uint8)
+    clf = g.Classifier(0, 16, 1)
+    with pytest.raises(OSError):  # region not registered
+        clf.rxloop(frames)
+    g.host_register(frames)
+    try:
+        loop = clf.rxloop(frames, slots=4, lifetime_ms=300)
+        with pytest.raises(OSError):  # one loop per context
+            clf.rxloop(frames)
+        offs = np.arange(4, dtype=np.uint64) * 64
+        tk = loop.submit(offs)
+        assert (loop.wait(tk, 4)["action"] == 2).all()  # zero frames: bad Ethertype
+        assert loop.submit(np.zeros(65, dtype=np.uint64)) == -22  # > max_burst
+        time.sleep(0.8)
+        assert loop.submit(offs) == -108  # -ESHUTDOWN: the kernel left on its own
+        loop.stop()
+        clf2 = g.Classifier(0, 16, 1, g.CFG_TRANS_HASH)
+        with pytest.raises(OSError):
+            clf2.rxloop(frames)
+    finally:
+        g.host_unregister(frames)
