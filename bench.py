@@ -319,6 +319,50 @@ def e2e_bench(device, vbytes=VERDICT_BYTES, reps=3):
     return out
 
 
+def e2e_multi(device, rank, world, vbytes, reps=3):
+    """Config 5 on N GPUs: every rank classifies its round-robin shard of the
+    mixed jumbo trace from pinned host memory, PCIe zero-copy and header
+    DMA-gather; barrier + max-over-ranks timing, RX_PULLED summed over ranks
+    as the accounting check.  PCIe-inclusive: never `value`."""
+    wl, _, stride, R, T, _ = WORKLOADS["mixed"]
+    n = 256 << 10
+    dfr = torch.zeros(n * stride, dtype=torch.uint8, device=device)
+    g.generate(wl, n, stride, R, dfr, seed=SEED, rank=rank, world=world, shard_block=SHARD_BLOCK)
+    hfr = torch.empty(n * stride, dtype=torch.uint8).pin_memory()
+    hfr.copy_(dfr)
+    del dfr
+    torch.cuda.synchronize()
+    hv = torch.empty(n * vbytes, dtype=torch.uint8).pin_memory()
+    clf = g.Classifier(device.index or 0, R, g.HASH_JENKINS, g.CFG_VERDICT4 if vbytes == 4 else 0)
+    setup_tables(clf, R, T)
+    nccl = torch.distributed.get_backend() == "nccl"
+    res = {"pkts_per_gpu": n, "slot_stride": stride, "n_gpus": world}
+    calls = 0
+    stats = np.zeros(g.NR_STATS, dtype=np.uint64)
+    for tag, mode, nst in (("zerocopy", g.E2E_ZEROCOPY, 1), ("copy_hdr_2streams", g.E2E_COPY, 2)):
+        clf.classify_host(hfr, n, stride, verdicts=hv, stats=stats, mode=mode, nstreams=nst)
+        calls += 1
+        torch.cuda.synchronize()
+        torch.distributed.barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            clf.classify_host(hfr, n, stride, verdicts=hv, stats=stats, mode=mode, nstreams=nst)
+        calls += reps
+        el = time.perf_counter() - t0
+        t = torch.tensor([el], dtype=torch.float64)
+        t = t.cuda() if nccl else t
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        res[tag + "_mpps"] = round(world * n * reps / float(t.item()) / 1e6, 1)
+    pulled = torch.tensor([int(stats[6])], dtype=torch.int64)  # GCL_RX_PULLED
+    pulled = pulled.cuda() if nccl else pulled
+    torch.distributed.all_reduce(pulled)
+    res["rx_pulled_check"] = "ok" if int(pulled.item()) == world * n * calls else \
+        f"MISMATCH {int(pulled.item())} != {world * n * calls}"
+    del hfr, hv, clf
+    torch.cuda.empty_cache()
+    return res
+
+
 def rxloop_bench(device, vbytes, iters=2000):
     """Burst latency at the reference's granularity (rx_burst's <= 64 mbufs,
     iokernel/rx.c:270-290): the persistent rx loop (gcl_rxloop_*) reading the
@@ -623,6 +667,8 @@ def main():
 
     if world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(args.cpu_budget)
+    if world > 1 and not args.no_e2e:
+        result["e2e_multi"] = e2e_multi(device, rank, world, vb)
     if dist_on:
         shard.finish()
     if rank == 0:
