@@ -117,9 +117,9 @@ __device__ __forceinline__ void jfinal(uint32_t &a, uint32_t &b, uint32_t &c)
 }
 
 /* jenkins_hash(&ip, 4): the rte_jhash key of dp.ip_to_proc (dp_clients.c:360) */
-__device__ __forceinline__ uint32_t jhash_u32(uint32_t ip)
+__device__ __forceinline__ uint32_t jhash_u32(uint32_t ip, uint32_t initval = 0)
 {
-	uint32_t a = 0xdeadbeefu + 4u, b = a, c = a;
+	uint32_t a = 0xdeadbeefu + 4u + initval, b = a, c = a;
 	a += ip;
 	jfinal(a, b, c);
 	return c;

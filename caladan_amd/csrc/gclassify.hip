@@ -66,7 +66,8 @@ struct KParams {
 	unsigned long long *counts;
 	unsigned long long *stats;
 	const uint8_t *tables;     /* device table image */
-	uint32_t ipt_mask;         /* ip slots - 1 */
+	uint32_t ipt_mask;         /* ip buckets - 1 (2 slots per bucket) */
+	uint32_t ipt_seed;         /* lookup3 initval of the bucket hash */
 	uint32_t max_rt;
 	uint32_t off_rt, off_flow, off_toep, tables_lds_bytes;
 	uint32_t cflags;
@@ -193,16 +194,26 @@ __device__ __forceinline__ uint32_t crc32c_u64(const uint32_t *T, uint32_t crc, 
 
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
-/* ip_to_proc: open addressing keyed by rte_jhash(&ip, 4, 0); -1 on a miss */
-__device__ __forceinline__ int ipt_lookup(const uint2 *ipt, uint32_t mask, uint32_t ip)
+/*
+ * ip_to_proc: a two-choice bucketised cuckoo table like DPDK's rte_hash (the
+ * reference's dp.ip_to_proc, dp_clients.c:349-363), keyed by lookup3 of the
+ * IP.  Buckets hold two {ip, uniqid} entries (16 B, one ds_read_b128); a key
+ * lives in bucket h or rotl(h, 16).  The host places every key (build_image),
+ * so a lookup is two independent LDS reads and four selects: no probe loop,
+ * no divergence.  -1 on a miss.
+ */
+__device__ __forceinline__ int ipt_lookup(const uint2 *ipt, uint32_t mask, uint32_t seed,
+                                          uint32_t ip)
 {
-	uint32_t s = gcl::jhash_u32(ip) & mask;
-	uint2 e = ipt[s];
-	while (__builtin_expect(e.y != kEmpty && e.x != ip, 0)) { /* collision chain */
-		s = (s + 1) & mask;
-		e = ipt[s];
-	}
-	return e.y != kEmpty ? (int)e.y : -1;
+	const uint32_t h = gcl::jhash_u32(ip, seed);
+	const uint4 *bk = (const uint4 *)ipt;
+	const uint4 x = bk[h & mask], y = bk[gcl::rotl(h, 16) & mask];
+	int r = -1;
+	r = (x.x == ip && x.y != kEmpty) ? (int)x.y : r;
+	r = (x.z == ip && x.w != kEmpty) ? (int)x.w : r;
+	r = (y.x == ip && y.y != kEmpty) ? (int)y.y : r;
+	r = (y.z == ip && y.w != kEmpty) ? (int)y.w : r;
+	return r;
 }
 
 /* Toeplitz over the 12-byte tuple with the per-byte LUT (12 x 256 words) */
@@ -280,7 +291,7 @@ __device__ __forceinline__ void classify_one(const KParams &k, const uint4 *tile
 	uint32_t flags2 = flags, hint_mark = 0;
 	if (GENERAL && k.dst_hint) {
 		const uint32_t hint = k.dst_hint[idx];
-		const int q = hint ? ipt_lookup(tb.ipt, k.ipt_mask, hint) : -1;
+		const int q = hint ? ipt_lookup(tb.ipt, k.ipt_mask, k.ipt_seed, hint) : -1;
 		if (q >= 0) {
 			flags2 |= GCL_F_FDIR_ID;
 			hint_mark = (uint32_t)q + 1;
@@ -310,7 +321,7 @@ __device__ __forceinline__ void classify_one(const KParams &k, const uint4 *tile
 		if (lookup)
 			p = (int)(dst & 15);
 	} else if (lookup) {
-		p = ipt_lookup(tb.ipt, k.ipt_mask, dst);
+		p = ipt_lookup(tb.ipt, k.ipt_mask, k.ipt_seed, dst);
 	}
 	const bool miss = lookup && p < 0;
 	const bool arp_respond = miss && azure && is_arp && frag == GCL_ARP_OP_REQUEST;
@@ -600,7 +611,7 @@ __host__ __device__ constexpr uint64_t loop_word(uint64_t t, uint32_t n, uint32_
 static_assert(sizeof(LoopSlotHdr) == 64, "LoopSlotHdr");
 
 struct LoopImgHdr {        /* first 64 B of a table image buffer */
-	uint32_t bytes, ipt_mask, off_rt, off_flow, off_toep, pad[11];
+	uint32_t bytes, ipt_mask, off_rt, off_flow, off_toep, ipt_seed, pad[10];
 };
 static_assert(sizeof(LoopImgHdr) == 64, "LoopImgHdr");
 
@@ -683,6 +694,7 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 			for (uint32_t i = tid; i < bytes / 4; i += 256)
 				((uint32_t *)lds_tab)[i] = gcl::ld_sys32(ib + 64 + 4 * i);
 			k.ipt_mask = gcl::ld_sys32(ib + 4);
+			k.ipt_seed = gcl::ld_sys32(ib + 20);
 			tb.ipt = (const uint2 *)lds_tab;
 			tb.rtab = (const RtEntry *)(lds_tab + gcl::ld_sys32(ib + 8));
 			tb.flow = lds_tab + gcl::ld_sys32(ib + 12);
@@ -933,6 +945,7 @@ struct gcl_ctx {
 	};
 	std::vector<Rt> rt;
 	uint32_t ipt_slots;
+	uint32_t ipt_seed;    /* lookup3 initval the current image's buckets use */
 	uint32_t off_rt, off_flow, off_toep, off_seed, off_crc, image_cap, image_bytes;
 	uint32_t flow_used;
 	bool dirty;
@@ -1194,14 +1207,67 @@ extern "C" int gcl_runtime_del(struct gcl_ctx *c, uint16_t uniqid)
 	return 0;
 }
 
+static uint32_t jhash_u32_host(uint32_t ip, uint32_t initval)
+{
+	auto rot = [](uint32_t x, int k) { return (x << k) | (x >> (32 - k)); };
+	uint32_t a = 0xdeadbeefu + 4u + initval, b = a, c = a;
+	a += ip;
+	c ^= b; c -= rot(b, 14);  /* final(), base/jenkins_hash.c:114-123 */
+	a ^= c; a -= rot(c, 11);
+	b ^= a; b -= rot(a, 25);
+	c ^= b; c -= rot(b, 16);
+	a ^= c; a -= rot(c, 4);
+	b ^= a; b -= rot(a, 14);
+	c ^= b; c -= rot(b, 24);
+	return c;
+}
+
+/* Cuckoo placement of every present runtime's IP into @nb two-slot buckets
+ * (the layout ipt_lookup reads).  Random-walk eviction; false if some key
+ * could not be placed with this seed. */
+static bool ipt_build(const gcl_ctx *c, uint2 *ipt, uint32_t nb, uint32_t seed)
+{
+	const uint32_t m = nb - 1;
+	for (uint32_t i = 0; i < 2 * nb; i++)
+		ipt[i] = make_uint2(0, kEmpty);
+	for (uint32_t u = 0; u < c->cfg.max_runtimes; u++) {
+		if (!c->rt[u].present)
+			continue;
+		uint2 cur = make_uint2(c->rt[u].ip, u);
+		bool placed = false;
+		for (uint32_t kick = 0; kick < 8 * nb + 64 && !placed; kick++) {
+			const uint32_t h = jhash_u32_host(cur.x, seed);
+			const uint32_t bs[2] = {h & m, ((h << 16) | (h >> 16)) & m};
+			for (int j = 0; j < 4 && !placed; j++) {
+				uint2 &e = ipt[2 * bs[j >> 1] + (j & 1)];
+				if (e.y == kEmpty) {
+					e = cur;
+					placed = true;
+				}
+			}
+			if (!placed) { /* evict a pseudo-random resident of one bucket */
+				uint2 &e = ipt[2 * bs[(kick >> 1) & 1] + (kick & 1)];
+				std::swap(e, cur);
+			}
+		}
+		if (!placed)
+			return false;
+	}
+	return true;
+}
+
 /* Serialise the host mirror into the staging buffer. Returns image bytes. */
 static uint32_t build_image(gcl_ctx *c)
 {
 	uint8_t *img = c->staging;
 	const uint32_t max_rt = c->cfg.max_runtimes;
 	uint2 *ipt = (uint2 *)img;
-	for (uint32_t i = 0; i < c->ipt_slots; i++)
-		ipt[i] = make_uint2(0, kEmpty);
+	/* load <= 1/2 per slot: seed 0 practically always places every key */
+	for (uint32_t seed = 0;; seed++)
+		if (ipt_build(c, ipt, c->ipt_slots / 2, seed) || seed == 255) {
+			c->ipt_seed = seed;
+			break;
+		}
 	RtEntry *re = (RtEntry *)(img + c->off_rt);
 	uint8_t *flow = img + c->off_flow;
 	uint32_t fo = 0;
@@ -1217,10 +1283,6 @@ static uint32_t build_image(gcl_ctx *c)
 			e.flow_off = fo;
 			memcpy(flow + fo, r.flow, r.tc);
 			fo += r.tc;
-			uint32_t s = gcl_jenkins_hash(&r.ip, 4) & (c->ipt_slots - 1);
-			while (ipt[s].y != kEmpty)
-				s = (s + 1) & (c->ipt_slots - 1);
-			ipt[s] = make_uint2(r.ip, u);
 		}
 		re[u] = e;
 	}
@@ -1506,7 +1568,8 @@ extern "C" int gcl_classify_ex(struct gcl_ctx *c, const struct gcl_batch *b,
 	k.counts = (unsigned long long *)runtime_counts;
 	k.stats = (unsigned long long *)stats;
 	k.tables = c->dimg[c->cur];
-	k.ipt_mask = c->ipt_slots - 1;
+	k.ipt_mask = c->ipt_slots / 2 - 1;
+	k.ipt_seed = c->ipt_seed;
 	k.max_rt = c->cfg.max_runtimes;
 	k.off_rt = c->off_rt;
 	k.off_flow = c->off_flow;
@@ -2045,7 +2108,8 @@ static int loop_write_image(gcl_rxloop *L, int i)
 		return -E2BIG;
 	LoopImgHdr hdr = {};
 	hdr.bytes = bytes;
-	hdr.ipt_mask = c->ipt_slots - 1;
+	hdr.ipt_mask = c->ipt_slots / 2 - 1;
+	hdr.ipt_seed = c->ipt_seed;
 	hdr.off_rt = c->off_rt;
 	hdr.off_flow = c->off_flow;
 	hdr.off_toep = c->off_toep;
