@@ -1263,11 +1263,13 @@ static uint32_t build_image(gcl_ctx *c)
 	const uint32_t max_rt = c->cfg.max_runtimes;
 	uint2 *ipt = (uint2 *)img;
 	/* load <= 1/2 per slot: seed 0 practically always places every key */
-	for (uint32_t seed = 0;; seed++)
-		if (ipt_build(c, ipt, c->ipt_slots / 2, seed) || seed == 255) {
-			c->ipt_seed = seed;
-			break;
-		}
+	bool placed = false;
+	for (uint32_t seed = 0; seed < 256 && !placed; seed++) {
+		placed = ipt_build(c, ipt, c->ipt_slots / 2, seed);
+		c->ipt_seed = seed;
+	}
+	if (!placed)
+		return 0; /* no seed placed every key: callers return -ENOSPC */
 	RtEntry *re = (RtEntry *)(img + c->off_rt);
 	uint8_t *flow = img + c->off_flow;
 	uint32_t fo = 0;
@@ -1486,6 +1488,8 @@ static int upload_tables(gcl_ctx *c, hipStream_t s)
 		return 0;
 	hipEventSynchronize(c->staging_free);
 	uint32_t bytes = build_image(c);
+	if (!bytes)
+		return -ENOSPC;
 	const int nxt = c->cur ^ 1;
 	/* the image about to be overwritten: wait for its last readers */
 	gcl_ctx::ImgUsers &old = c->users[nxt];
@@ -1550,8 +1554,9 @@ extern "C" int gcl_classify_ex(struct gcl_ctx *c, const struct gcl_batch *b,
 		return -EINVAL;
 	hipSetDevice(c->device);
 
-	if (upload_tables(c, s))
-		return -EIO;
+	const int up = upload_tables(c, s);
+	if (up)
+		return up;
 	wait_tables(c, s);
 
 	KParams k = {};
@@ -2104,6 +2109,8 @@ static int loop_write_image(gcl_rxloop *L, int i)
 	gcl_ctx *c = L->c;
 	hipEventSynchronize(c->staging_free);
 	const uint32_t bytes = build_image(c);
+	if (!bytes)
+		return -ENOSPC;
 	if (bytes > kLdsTableBudget)
 		return -E2BIG;
 	LoopImgHdr hdr = {};

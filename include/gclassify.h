@@ -224,7 +224,9 @@ int gcl_steer_flows(uint16_t thread_count, const uint16_t *active_idx,
  * @runtime_counts device u64[max_runtimes], ACCUMULATED: packets steered to
  *                 each runtime (DELIVER + WAKE), may be NULL
  * @stats          device u64[GCL_NR_STATS], ACCUMULATED, may be NULL
- * Asynchronous; returns -EINVAL for malformed batches.
+ * Asynchronous; returns -EINVAL for malformed batches, -EIO when the table
+ * upload fails, -ENOSPC when the IP table cannot place every key (cuckoo
+ * placement failed for all 256 seeds: not seen at the table's load <= 1/2).
  * Replaces the rx_one_pkt loop of rx_burst (rx.c:281-287).
  */
 int gcl_classify(struct gcl_ctx *ctx, const struct gcl_batch *b,

@@ -23,7 +23,10 @@
  * the survey ran through the reference's do_toeplitz; orc_rx_one_pkt against
  * hand-derived scenario fixtures (tests/golden/rx_scenarios.json) that cite
  * rx.c line by line.  iokernel/rx.c itself needs DPDK headers that are not in
- * this image, so it is not compiled here (see DESIGN.md "Oracle").
+ * this image, so it is not compiled here, and the reference ships no tests or
+ * fixtures for it: the decision tree of orc_rx_one_pkt is PARITY UNPINNED by
+ * reference outputs (pinned only by those hand-derived fixtures); the hashes
+ * it calls are pinned (see DESIGN.md "Oracle").
  */
 #ifndef ORC_H
 #define ORC_H

@@ -39,17 +39,21 @@ def tc_map(rts, max_rt):
     return tc
 
 
-@pytest.mark.parametrize("v4", [False, True])
-@pytest.mark.parametrize("mode", [0, 1, 2])
-def test_rxloop_fuzz_vs_oracle(g, orc, mode, v4):
-    rng = np.random.default_rng(7000 + 10 * mode + v4)
+LOOP_CASES = [(m, v4, 0) for m in (0, 1, 2) for v4 in (False, True)] + \
+    [(m, False, fl) for m in (0, 1, 2) for fl in (1, 2)]
+
+
+@pytest.mark.parametrize("mode,v4,flags", LOOP_CASES)
+def test_rxloop_fuzz_vs_oracle(g, orc, mode, v4, flags):
+    """flags: 0 plain, 1 Azure ARP mode (GCL_CFG_AZURE_ARP), 2 16-bit hash."""
+    rng = np.random.default_rng(7000 + 10 * mode + v4 + 100 * flags)
     max_rt = 1024 if mode == 1 else 16
     rts = random_runtimes(rng, max_rt, 300 if max_rt == 1024 else 12)
     n = 3000
     frames, flen, offs, olf, rss, fdir, hint = fuzz_batch(rng, n, rts, max_rt)
     key = bytes(rng.integers(0, 256, size=40, dtype=np.uint8))
-    cflags = g.CFG_VERDICT4 if v4 else 0
-    t = orc.Tables(max_rt, mode, 0, 0x09, key)
+    cflags = (g.CFG_VERDICT4 if v4 else 0) | flags
+    t = orc.Tables(max_rt, mode, flags, 0x09, key)
     apply_runtimes(t, rts)
     clf = g.Classifier(0, max_rt, mode, cflags, 0x09, key)
     apply_runtimes(clf, rts)
