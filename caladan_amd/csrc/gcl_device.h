@@ -89,6 +89,38 @@ __device__ __forceinline__ uint4 load16_sys(const uint8_t *base, uint64_t len, u
 	return make_uint4(o[0], o[1], o[2], o[3]);
 }
 
+/* Buffer-op cache policy sc0 | sc1: system scope, misses every GPU cache. */
+constexpr int kSysAux = 17;
+
+/* Buffer descriptor over host memory (< 4 GiB) the persistent loop reads or
+ * writes; build it from wave-uniform values only. */
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t host_rsrc(const void *p, uint64_t bytes)
+{
+	return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0,
+	                                         (int)(bytes < 0xFFFFFFFFull ? bytes : 0xFFFFFFFFull),
+	                                         0x00020000);
+}
+
+/* load16_sys as one 16-B (or two 8-B) system-scope buffer loads when the
+ * range is aligned and inside a region below 4 GiB: one PCIe read per lane
+ * instead of five dword reads */
+__device__ __forceinline__ uint4 load16_host(__amdgpu_buffer_rsrc_t rs, const uint8_t *base,
+                                             uint64_t len, uint64_t a)
+{
+	if (a + 16 <= len && len <= 0xFFFFFFFFull) {
+		if (!(a & 15)) {
+			const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)a, 0, kSysAux);
+			return make_uint4(v[0], v[1], v[2], v[3]);
+		}
+		if (!(a & 7)) {
+			const auto x = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)a, 0, kSysAux);
+			const auto y = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)a + 8, 0, kSysAux);
+			return make_uint4(x[0], x[1], y[0], y[1]);
+		}
+	}
+	return load16_sys(base, len, a);
+}
+
 __device__ __forceinline__ uint32_t rotl(uint32_t x, int k)
 {
 	return (x << k) | (x >> (32 - k));

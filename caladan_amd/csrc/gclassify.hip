@@ -599,9 +599,18 @@ classify_kernel(KParams k)
 struct LoopSlotHdr {       /* first 64 B of a ring slot */
 	uint64_t word;          /* host: the published burst, one load for the poller:
 	                           ticket[63:24] n[23:11] flags[10:7] img[6] img_seq%64[5:0] */
-	uint64_t done;          /* device: ticket completed */
-	uint32_t pad[12];
+	uint32_t pad[14];
 };
+
+/* One verdict record per packet of a burst, written by the kernel with ONE
+ * 16-B system-scope store: the verdict in the gcl_verdict layout plus the
+ * ticket.  The record is its own completion flag: the host polls the
+ * tickets, so the kernel neither waits for its stores nor raises a flag. */
+struct LoopRec {
+	uint32_t hash, vlo;
+	uint64_t ticket;
+};
+static_assert(sizeof(LoopRec) == 16, "LoopRec");
 __host__ __device__ constexpr uint64_t loop_word(uint64_t t, uint32_t n, uint32_t fl, uint32_t img,
                                                  uint32_t iseq)
 {
@@ -652,6 +661,7 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 	uint8_t *lds_tab = (uint8_t *)(hist + ((L.max_rt + 3) & ~3u));
 	const int tid = threadIdx.x;
 	const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + L.lifetime_ticks;
+	const __amdgpu_buffer_rsrc_t frs = gcl::host_rsrc(L.frames, L.frames_len);
 
 	KParams k = {};
 	k.frames = L.frames;
@@ -667,6 +677,7 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 	for (uint64_t t = blockIdx.x + 1;; t += L.workers) {
 		uint8_t *slot = L.slots + ((t - 1) % L.nslots) * L.slot_bytes;
 		LoopSlotHdr *h = (LoopSlotHdr *)slot;
+		const __amdgpu_buffer_rsrc_t srs = gcl::host_rsrc(slot, L.slot_bytes);
 		if (tid == 0) {
 			uint64_t w = 0;
 			for (;;) { /* one system-scope load per poll carries the whole burst header */
@@ -724,7 +735,7 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 			for (int j = 0; j < 4; j++) {
 				const int c = j * 256 + tid, p = c >> 2, q = c & 3;
 				tile[tile_slot(p, q)] = (uint32_t)p < m
-				        ? gcl::load16_sys(L.frames, L.frames_len, s_offs[p] + 16 * (uint64_t)q)
+				        ? gcl::load16_host(frs, L.frames, L.frames_len, s_offs[p] + 16 * (uint64_t)q)
 				        : make_uint4(0, 0, 0, 0);
 			}
 			__syncthreads();
@@ -735,13 +746,12 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 			k.dst_hint = (fl & GCL_LOOP_F_HINT) ? s_hint : nullptr;
 			if ((uint32_t)tid < m) {
 				classify_one<MODE, true, true>(k, tile, tid, (uint64_t)tid, tb, hist, cnt);
-				uint8_t *vo = slot + L.off_verd;
-				if (L.cflags & GCL_CFG_VERDICT4) {
-					gcl::st_sys32(vo + 4 * (base + tid), ((const uint32_t *)s_verd)[tid]);
-				} else {
-					gcl::st_sys32(vo + 8 * (base + tid), s_verd[tid].x);
-					gcl::st_sys32(vo + 8 * (base + tid) + 4, s_verd[tid].y);
-				}
+				const bool v4 = L.cflags & GCL_CFG_VERDICT4;
+				const uint32_t hsh = v4 ? 0u : s_verd[tid].x;
+				const uint32_t vlo = v4 ? ((const uint32_t *)s_verd)[tid] : s_verd[tid].y;
+				const gcl::u32x4 rec = {hsh, vlo, (uint32_t)t, (uint32_t)(t >> 32)};
+				__builtin_amdgcn_raw_buffer_store_b128(
+				        rec, srs, (int)(L.off_verd + sizeof(LoopRec) * (base + tid)), 0, gcl::kSysAux);
 			}
 			__syncthreads();
 		}
@@ -769,13 +779,6 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 			if (tid == 0)
 				atomicAdd(&L.stats[GCL_RX_PULLED], (unsigned long long)n);
 		}
-		/* verdicts before the ticket: the verdict stores are system-scope
-		 * (write-through), so each wave only waits for its own to complete;
-		 * no L2 writeback (__threadfence_system) on the latency path */
-		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-		__syncthreads();
-		if (tid == 0)
-			__hip_atomic_store(&h->done, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 	}
 }
 
@@ -2096,11 +2099,29 @@ static bool loop_ended(gcl_rxloop *L)
 	return L->ended;
 }
 
+static const LoopRec *loop_recs(gcl_rxloop *L, LoopSlotHdr *h)
+{
+	return (const LoopRec *)((const uint8_t *)h + L->lp.off_verd);
+}
+
+/* Every verdict record of ticket @t's burst carries @t (its slot must still
+ * hold @t).  The last records usually land last, so scan backwards. */
+static bool burst_complete(gcl_rxloop *L, uint64_t t)
+{
+	LoopSlotHdr *h = loop_slot(L, t);
+	const uint32_t n = (uint32_t)(h->word >> 11) & 0x1FFF;
+	const LoopRec *r = loop_recs(L, h);
+	for (uint32_t i = n; i-- > 0;)
+		if (__atomic_load_n(&r[i].ticket, __ATOMIC_ACQUIRE) != t)
+			return false;
+	return true;
+}
+
 static bool ticket_done(gcl_rxloop *L, uint64_t t)
 {
 	if (t == 0 || t + L->lp.nslots <= L->next)
 		return true; /* never issued, or its slot has been reused since */
-	return __atomic_load_n(&loop_slot(L, t)->done, __ATOMIC_ACQUIRE) >= t;
+	return burst_complete(L, t);
 }
 
 /* Build the current tables into image buffer @i (host memory). */
@@ -2168,7 +2189,7 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 	lp.off_fdir = lp.off_rss + 4 * mb;
 	lp.off_hint = lp.off_fdir + 4 * mb;
 	lp.off_verd = lp.off_hint + 4 * mb;
-	lp.slot_bytes = (lp.off_verd + 8 * mb + 255) & ~255ull;
+	lp.slot_bytes = (lp.off_verd + sizeof(LoopRec) * mb + 255) & ~255ull;
 	lp.nslots = cfg->slots;
 	lp.workers = cfg->workers;
 	lp.lifetime_ticks = (uint64_t)cfg->lifetime_ms * 100000ull;
@@ -2292,18 +2313,26 @@ extern "C" int gcl_rxloop_wait(struct gcl_rxloop *L, int64_t ticket, void *verdi
 	LoopSlotHdr *h = loop_slot(L, t);
 	const uint64_t t0 = spin_ns ? now_ns() : 0;
 	uint32_t k = 0;
-	while (__atomic_load_n(&h->done, __ATOMIC_ACQUIRE) < t) {
+	while (!burst_complete(L, t)) {
 		if (!spin_ns || (++k & 255) == 0) {
 			if (loop_ended(L))
-				return __atomic_load_n(&h->done, __ATOMIC_ACQUIRE) >= t ? 0 : -ESHUTDOWN;
+				return burst_complete(L, t) ? 0 : -ESHUTDOWN;
 			if (!spin_ns || now_ns() - t0 >= spin_ns)
 				return -EAGAIN;
 		}
 		__builtin_ia32_pause();
 	}
-	if (verdicts_out)
-		memcpy(verdicts_out, (uint8_t *)h + L->lp.off_verd,
-		       (size_t)((h->word >> 11) & 0x1FFF) * L->vbytes);
+	if (verdicts_out) {
+		const uint32_t n = (uint32_t)(h->word >> 11) & 0x1FFF;
+		const LoopRec *r = loop_recs(L, h);
+		if (L->vbytes == 4) {
+			for (uint32_t i = 0; i < n; i++)
+				((uint32_t *)verdicts_out)[i] = r[i].vlo;
+		} else {
+			for (uint32_t i = 0; i < n; i++)
+				((uint64_t *)verdicts_out)[i] = (uint64_t)r[i].vlo << 32 | r[i].hash;
+		}
+	}
 	uint64_t &r = L->retired[(t - 1) % L->lp.nslots];
 	if (r < t)
 		r = t;
