@@ -51,6 +51,38 @@ def calib(base):
     return out
 
 
+def request_bytes(base, tag):
+    """Fabric request counts per classify launch (TCC_EA0_RDREQ / _32B,
+    TCC_BUBBLE, TCC_EA0_WRREQ / _64B).  rocprof-compute's gfx950 'HBM
+    Bandwidth' formula prices reads as 128 x TCC_BUBBLE + 32 x RDREQ_32B + 64 x
+    the rest, but on this ROCm 7.2 / gfx950 TCC_BUBBLE reads 0 even for a
+    dense 2 GiB stream that is 16.8 M requests for 2.15 GB (tools/halfline.hip,
+    profiles/r01_halfline.jsonl): every read request carries a 128-B line, the
+    guide's x2.  So the request counts are reported, and the byte totals use
+    128 B per read request and the write counters as documented."""
+    d1 = os.path.join(base, f"{tag}_REQ", "run_counter_collection.csv")
+    d2 = os.path.join(base, f"{tag}_REQ64", "run_counter_collection.csv")
+    if not (os.path.exists(d1) and os.path.exists(d2)):
+        return None
+    per = {}
+    for path in (d1, d2):
+        launches = {}
+        for r in rows(path):
+            if "classify_kernel" in r["Kernel_Name"]:
+                launches.setdefault(r["Dispatch_Id"], {})[r["Counter_Name"].replace("_sum", "")] = \
+                    float(r["Counter_Value"])
+        for c in {k for v in launches.values() for k in v}:
+            vals = [v[c] for v in launches.values() if c in v]
+            per[c] = sum(vals) / len(vals)
+    b, rd, r32, wr, w64 = (per["TCC_BUBBLE"], per["TCC_EA0_RDREQ"], per["TCC_EA0_RDREQ_32B"],
+                           per["TCC_EA0_WRREQ"], per["TCC_EA0_WRREQ_64B"])
+    rbytes = 128 * (rd - r32) + 32 * r32
+    wbytes = 64 * w64 + 32 * (wr - w64)
+    return {"req_reads": rd, "req_reads_32B": r32, "req_TCC_BUBBLE": b, "req_writes": wr,
+            "req_writes_64B": w64, "hbm_read_bytes_from_requests": rbytes,
+            "hbm_write_bytes_from_requests": wbytes, "hbm_bytes_from_requests": rbytes + wbytes}
+
+
 def main(rnd):
     base = os.path.join(ROOT, "gpurun_out", f"prof_{rnd}")
     prof = os.path.join(ROOT, "profiles")
@@ -96,6 +128,11 @@ def main(rnd):
             "algorithmic_GBs": round(algo / (avg_ns * 1e-9) / 1e9, 1),
             "source": f"gpurun_out/prof_{rnd}/{tag}_{{trace,FETCH_SIZE,WRITE_SIZE}} (rocprofv3)",
         }
+        req = request_bytes(base, tag)
+        if req:
+            out.update(req)
+            out["traffic_over_algorithmic_from_requests"] = round(req["hbm_bytes_from_requests"] / algo, 4)
+            out["requests_per_pkt"] = round((req["req_reads"] + req["req_writes"]) / PKTS[wl], 4)
         with open(os.path.join(prof, f"pmc_{wl}{'_v4' if vb == 4 else ''}.json"), "w") as f:
             json.dump(out, f, indent=1)
         print(json.dumps(out))

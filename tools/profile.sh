@@ -12,10 +12,17 @@ for vb in ${VBS:-4 8}; do
 for wl in ${WLS:-udp64 tcp1500}; do
   A="--workload $wl --verdict-bytes $vb --no-cpu --no-secondary --no-e2e"
   D=$OUT/${wl}_v${vb}
+  if [ -z "$REQ_ONLY" ]; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d ${D}_trace -o run -- python3 bench.py $A --steps 20 --warmup 3 > ${D}_bench.json 2> ${D}_trace.err
   for c in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d ${D}_$c -o run -- python3 bench.py $A --steps 5 --warmup 1 > /dev/null 2> ${D}_$c.err
   done
+  fi
+  # request sizes at the L2/fabric boundary, for the rocprof-compute gfx950
+  # HBM formula (128 x TCC_BUBBLE + 32 x RDREQ_32B + 64 x the other reads;
+  # 64 x WRREQ_64B + 32 x the other writes): 4 TCC counters, then 1
+  timeout -k 10 300 rocprofv3 --pmc TCC_BUBBLE_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_WRREQ_sum --output-format csv -d ${D}_REQ -o run -- python3 bench.py $A --steps 5 --warmup 1 > /dev/null 2> ${D}_REQ.err
+  timeout -k 10 300 rocprofv3 --pmc TCC_EA0_WRREQ_64B_sum --output-format csv -d ${D}_REQ64 -o run -- python3 bench.py $A --steps 5 --warmup 1 > /dev/null 2> ${D}_REQ64.err
 done
 done
 if [ -x ./tools/membench ] && [ -z "$NO_CALIB" ]; then
