@@ -643,20 +643,47 @@ struct LoopParams {
 	uint32_t max_rt, cflags, default_flags;
 };
 
-constexpr uint32_t kLoopFixedLds = 256 * 64 + 256 * 8 + 3 * 256 * 4 + 256 * 8 + 256 + 64;
+/* header tile + 2 x side arrays (offs, rss, fdir, hint, olflags) + verdicts + ctl */
+constexpr uint32_t kLoopSide = 256 * 8 + 3 * 256 * 4 + 256;
+constexpr uint32_t kLoopFixedLds = 256 * 64 + 2 * kLoopSide + 256 * 8 + 64;
+
+/* Side arrays of one 256-packet chunk, double-buffered in LDS so the next
+ * chunk's arrive while the current one is classified. */
+struct LoopSide {
+	uint64_t *offs;
+	uint32_t *rss, *fdir, *hint;
+	uint8_t *olf;
+	__device__ LoopSide(uint8_t *b)
+	    : offs((uint64_t *)b), rss((uint32_t *)(b + 2048)), fdir(rss + 256), hint(fdir + 256),
+	      olf((uint8_t *)(hint + 256)) {}
+	/* packets [base, base + m) of the burst in @slot, one per lane */
+	__device__ void load(const uint8_t *slot, const LoopParams &L, uint32_t fl, uint32_t base,
+	                     uint32_t m, int tid)
+	{
+		if ((uint32_t)tid >= m)
+			return;
+		const uint32_t i = base + tid;
+		offs[tid] = gcl::ld_sys64(slot + L.off_offs + 8 * i);
+		if (fl & GCL_LOOP_F_OLF)
+			olf[tid] = (uint8_t)(gcl::ld_sys32(slot + L.off_olf + (i & ~3u)) >> (8 * (i & 3)));
+		if (fl & GCL_LOOP_F_RSS)
+			rss[tid] = gcl::ld_sys32(slot + L.off_rss + 4 * i);
+		if (fl & GCL_LOOP_F_FDIR)
+			fdir[tid] = gcl::ld_sys32(slot + L.off_fdir + 4 * i);
+		if (fl & GCL_LOOP_F_HINT)
+			hint[tid] = gcl::ld_sys32(slot + L.off_hint + 4 * i);
+	}
+};
 
 template <int MODE>
 __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 {
 	extern __shared__ uint4 smem[];
 	uint4 *tile = smem;
-	uint64_t *s_offs = (uint64_t *)(tile + 1024);
-	uint32_t *s_rss = (uint32_t *)(s_offs + 256);
-	uint32_t *s_fdir = s_rss + 256;
-	uint32_t *s_hint = s_fdir + 256;
-	uint2 *s_verd = (uint2 *)(s_hint + 256);
-	uint8_t *s_olf = (uint8_t *)(s_verd + 256);
-	uint32_t *s_ctl = (uint32_t *)(s_olf + 256);
+	uint8_t *side_mem = (uint8_t *)(tile + 1024);
+	LoopSide side[2] = {LoopSide(side_mem), LoopSide(side_mem + kLoopSide)};
+	uint2 *s_verd = (uint2 *)(side_mem + 2 * kLoopSide);
+	uint32_t *s_ctl = (uint32_t *)(s_verd + 256);
 	uint32_t *hist = s_ctl + 16;
 	uint8_t *lds_tab = (uint8_t *)(hist + ((L.max_rt + 3) & ~3u));
 	const int tid = threadIdx.x;
@@ -666,7 +693,6 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 	KParams k = {};
 	k.frames = L.frames;
 	k.frames_len = L.frames_len;
-	k.offs = s_offs;
 	k.verdicts = s_verd;
 	k.max_rt = L.max_rt;
 	k.cflags = L.cflags;
@@ -716,34 +742,43 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 			hist[i] = 0;
 		Counters cnt = {0, 0, 0, 0};
 		__syncthreads(); /* s_ctl consumed, tables and hist ready */
-		for (uint32_t base = 0; base < n; base += 256) {
-			const uint32_t m = n - base < 256 ? n - base : 256;
-			if ((uint32_t)tid < m) {
-				const uint32_t i = base + tid;
-				s_offs[tid] = gcl::ld_sys64(slot + L.off_offs + 8 * i);
-				if (fl & GCL_LOOP_F_OLF)
-					s_olf[tid] = (uint8_t)(gcl::ld_sys32(slot + L.off_olf + (i & ~3u)) >> (8 * (i & 3)));
-				if (fl & GCL_LOOP_F_RSS)
-					s_rss[tid] = gcl::ld_sys32(slot + L.off_rss + 4 * i);
-				if (fl & GCL_LOOP_F_FDIR)
-					s_fdir[tid] = gcl::ld_sys32(slot + L.off_fdir + 4 * i);
-				if (fl & GCL_LOOP_F_HINT)
-					s_hint[tid] = gcl::ld_sys32(slot + L.off_hint + 4 * i);
-			}
-			__syncthreads();
+		/* chunk pipeline: the side arrays of chunk c+1 and the frames of
+		 * chunk c are in flight together, and chunk c+1's frame loads are
+		 * issued before chunk c is classified */
+		const uint32_t nch = (n + 255) / 256;
+		uint4 r[4];
+		auto chunk_m = [&](uint32_t c) { return n - 256 * c < 256 ? n - 256 * c : 256u; };
+		auto load_frames = [&](const LoopSide &sd, uint32_t m) {
 #pragma unroll
 			for (int j = 0; j < 4; j++) {
 				const int c = j * 256 + tid, p = c >> 2, q = c & 3;
-				tile[tile_slot(p, q)] = (uint32_t)p < m
-				        ? gcl::load16_host(frs, L.frames, L.frames_len, s_offs[p] + 16 * (uint64_t)q)
-				        : make_uint4(0, 0, 0, 0);
+				r[j] = (uint32_t)p < m
+				       ? gcl::load16_host(frs, L.frames, L.frames_len, sd.offs[p] + 16 * (uint64_t)q)
+				       : make_uint4(0, 0, 0, 0);
 			}
-			__syncthreads();
+		};
+		side[0].load(slot, L, fl, 0, chunk_m(0), tid);
+		__syncthreads();
+		load_frames(side[0], chunk_m(0));
+		for (uint32_t c = 0; c < nch; c++) {
+			const uint32_t m = chunk_m(c), base = 256 * c;
+			LoopSide &cur = side[c & 1];
+			if (c + 1 < nch)
+				side[(c + 1) & 1].load(slot, L, fl, base + 256, chunk_m(c + 1), tid);
+#pragma unroll
+			for (int j = 0; j < 4; j++) {
+				const int cc = j * 256 + tid;
+				tile[tile_slot(cc >> 2, cc & 3)] = r[j];
+			}
+			__syncthreads(); /* tile of c and side arrays of c + 1 in LDS */
+			if (c + 1 < nch)
+				load_frames(side[(c + 1) & 1], chunk_m(c + 1));
 			k.n = m;
-			k.olflags = (fl & GCL_LOOP_F_OLF) ? s_olf : nullptr;
-			k.rss = (fl & GCL_LOOP_F_RSS) ? s_rss : nullptr;
-			k.fdir = (fl & GCL_LOOP_F_FDIR) ? s_fdir : nullptr;
-			k.dst_hint = (fl & GCL_LOOP_F_HINT) ? s_hint : nullptr;
+			k.offs = cur.offs;
+			k.olflags = (fl & GCL_LOOP_F_OLF) ? cur.olf : nullptr;
+			k.rss = (fl & GCL_LOOP_F_RSS) ? cur.rss : nullptr;
+			k.fdir = (fl & GCL_LOOP_F_FDIR) ? cur.fdir : nullptr;
+			k.dst_hint = (fl & GCL_LOOP_F_HINT) ? cur.hint : nullptr;
 			if ((uint32_t)tid < m) {
 				classify_one<MODE, true, true>(k, tile, tid, (uint64_t)tid, tb, hist, cnt);
 				const bool v4 = L.cflags & GCL_CFG_VERDICT4;
@@ -753,7 +788,7 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 				__builtin_amdgcn_raw_buffer_store_b128(
 				        rec, srs, (int)(L.off_verd + sizeof(LoopRec) * (base + tid)), 0, gcl::kSysAux);
 			}
-			__syncthreads();
+			__syncthreads(); /* tile and side[c & 1] free again */
 		}
 		/* counters of this burst */
 		for (uint32_t i = tid; i < L.max_rt; i += 256)
