@@ -314,6 +314,7 @@ def e2e_bench(device, vbytes=VERDICT_BYTES, reps=3):
         del dfr, hfr, hv, dv, clf
         torch.cuda.empty_cache()
     out["rxloop"] = rxloop_bench(device, vbytes)
+    out["rx_burst_pipeline"] = rxpipe_bench()
     out["mixed"]["trace_replay"] = trace_replay(device)
     out["ingress_pool"] = ingress_pool_bench(device, vbytes)
     return out
@@ -361,6 +362,31 @@ def e2e_multi(device, rank, world, vbytes, reps=3):
     del hfr, hv, clf
     torch.cuda.empty_cache()
     return res
+
+
+def rxpipe_bench():
+    """The whole rx_burst replacement on ONE host core (tools/rxpipe.cpp, C):
+    persistent GPU loop + the lrpc post-pass (gcl_host_deliver4) into 128
+    kthread rings, bursts of 64..4096 mbufs from a registered host region.
+    Compare with cpu_baseline.lrpc_1core_mpps (the reference's classify +
+    lrpc_send on one core).  Built by __graft_entry__.build()."""
+    import subprocess
+    exe = os.path.join(ROOT, "tools", "rxpipe")
+    if not os.access(exe, os.X_OK):
+        return {"skipped": "tools/rxpipe not built (python -c 'import __graft_entry__ as g; g.build()')"}
+    rows = []
+    for cfg in (("64", "1", "1", "20000"), ("64", "4", "8", "20000"), ("256", "4", "8", "10000"),
+                ("1024", "8", "16", "4000"), ("4096", "16", "16", "1000")):
+        try:
+            r = subprocess.run([exe, *cfg], capture_output=True, text=True, timeout=120)
+        except subprocess.TimeoutExpired:
+            rows.append({"burst": int(cfg[0]), "error": "timeout"})
+            break
+        if r.returncode != 0:
+            rows.append({"burst": int(cfg[0]), "error": r.stderr.strip()[-200:]})
+            break
+        rows.append(json.loads(r.stdout.strip().splitlines()[-1]))
+    return {"host_cores": 1, "runs": rows}
 
 
 def rxloop_bench(device, vbytes, iters=2000):

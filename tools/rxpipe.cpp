@@ -1,0 +1,185 @@
+// rxpipe.cpp - the whole rx_burst replacement on one dataplane core: bursts
+// of mbufs from a registered host ingress region go through the persistent
+// GPU loop (gcl_rxloop_*), and every verdict through the lrpc post-pass
+// (gcl_host_deliver4) into per-kthread rings, as INTEGRATION.md §4b wires it
+// into iokernel/rx.c:270-290.  The measured rate is what one host core
+// sustains with the GPU classifying, to set beside the reference's own
+// classify + lrpc_send rate on one core (bench.py cpu_baseline.lrpc_1core_mpps).
+//
+//   rxpipe <burst> <workers> <depth> <bursts>    -> one JSON line
+//
+// Runtime consumers are emulated as infinitely fast (each ring's consumer
+// position is set to its producer position after every burst), as in the CPU
+// baseline's lrpc variant.
+// Build: hipcc --offload-arch=gfx950 -O2 -Iinclude -o tools/rxpipe tools/rxpipe.cpp \
+//          -Lcaladan_amd -lgclassify -Wl,-rpath,'$ORIGIN/../caladan_amd'
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "gcl_host.h"
+#include "gclassify.h"
+
+#define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { \
+	fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); exit(1); } } while (0)
+
+static uint64_t now_ns()
+{
+	struct timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
+int main(int argc, char **argv)
+{
+	const uint32_t burst = argc > 1 ? (uint32_t)atoi(argv[1]) : 64;
+	const uint32_t workers = argc > 2 ? (uint32_t)atoi(argv[2]) : 1;
+	const uint32_t depth = argc > 3 ? (uint32_t)atoi(argv[3]) : 1;
+	const uint32_t nbursts = argc > 4 ? (uint32_t)atoi(argv[4]) : 20000;
+	const uint32_t R = 16, T = 8, RING = 4096;
+	const uint64_t nframes = 1 << 16, stride = 64;
+	if (!burst || burst > 4096 || !workers || workers > 16 || !depth || depth > 64) {
+		fprintf(stderr, "bad arguments\n");
+		return 1;
+	}
+
+	/* ingress region: udp64 frames generated on the GPU, copied to pinned host memory */
+	uint8_t *dfr, *region;
+	CHECK(hipMalloc(&dfr, nframes * stride));
+	CHECK(hipMemset(dfr, 0, nframes * stride));
+	struct gcl_gen_params gp = {};
+	gp.workload = GCL_WL_UDP64;
+	gp.nruntimes = R;
+	gp.seed = 0xCA1ADA4;
+	gp.n = nframes;
+	gp.stride = stride;
+	gp.world = 1;
+	if (gcl_generate(&gp, dfr, nullptr, nullptr, nullptr))
+		return 1;
+	CHECK(hipHostMalloc((void **)&region, nframes * stride, hipHostMallocMapped));
+	CHECK(hipMemcpy(region, dfr, nframes * stride, hipMemcpyDeviceToHost));
+	CHECK(hipFree(dfr));
+
+	struct gcl_cfg cfg = {};
+	cfg.max_runtimes = R;
+	cfg.hash_mode = GCL_HASH_JENKINS;
+	cfg.flags = GCL_CFG_VERDICT4;
+	cfg.default_olflags = GCL_F_RSS_HASH | GCL_F_IP_CKSUM_GOOD;
+	struct gcl_ctx *ctx;
+	if (gcl_open(0, &cfg, &ctx))
+		return 1;
+
+	/* host side of the runtimes: struct proc slices with one lrpc ring per kthread */
+	std::vector<gcl_host_proc> procs(R);
+	std::vector<gcl_host_proc *> by_id(R), clients(R);
+	std::vector<gcl_lrpc_chan_out> chans(R * T);
+	std::vector<gcl_lrpc_msg> msgs((size_t)R * T * RING);
+	std::vector<uint32_t> heads(R * T, 0);
+	for (uint32_t r = 0; r < R; r++) {
+		const uint16_t na = (uint16_t)(r % T + 1);
+		uint16_t act[GCL_NCPU];
+		for (uint16_t i = 0; i < na; i++)
+			act[i] = i;
+		gcl_host_proc &p = procs[r];
+		memset(&p, 0, sizeof(p));
+		p.uniqid = (uint16_t)r;
+		p.thread_count = (uint16_t)T;
+		p.active_thread_count = na;
+		p.idle_top = -1;
+		gcl_steer_flows((uint16_t)T, act, na, p.flow_tbl);
+		for (uint32_t t = 0; t < T; t++) {
+			gcl_lrpc_init_out(&chans[r * T + t], &msgs[(size_t)(r * T + t) * RING], RING,
+			                  &heads[r * T + t]);
+			p.rxq[t] = &chans[r * T + t];
+		}
+		by_id[r] = clients[r] = &p;
+		gcl_runtime_set(ctx, (uint16_t)r, gcl_runtime_ip(r), (uint16_t)T, na, p.flow_tbl);
+	}
+
+	struct gcl_rxloop_cfg lc = {};
+	lc.slots = 64;
+	lc.max_burst = burst;
+	lc.workers = workers;
+	lc.lifetime_ms = 60000;
+	lc.region = region;
+	lc.region_len = nframes * stride;
+	struct gcl_rxloop *loop;
+	int ret = gcl_rxloop_start(ctx, &lc, &loop);
+	if (ret) {
+		fprintf(stderr, "gcl_rxloop_start: %d\n", ret);
+		return 1;
+	}
+
+	/* bursts walk the region in order, like mbufs handed out by a mempool */
+	const uint32_t nb = (uint32_t)(nframes / burst);
+	std::vector<uint64_t> offs(nframes);
+	for (uint64_t i = 0; i < nframes; i++)
+		offs[i] = i * stride;
+	std::vector<uint16_t> len(burst, 60);
+	std::vector<gcl_verdict4> v(burst);
+	uint64_t stats[GCL_NR_STATS] = {0};
+	std::vector<int64_t> tk(depth);
+	std::vector<uint64_t> t_sub(depth), lat;
+	lat.reserve(nbursts);
+	uint64_t delivered = 0, t_deliver = 0, seq = 0;
+	/* @count bursts with up to @depth in flight, in ticket order */
+	auto pump = [&](uint32_t count, bool timed) {
+		uint32_t head = 0, tail = 0;
+		while (tail < count) {
+			while (head < count && head - tail < depth) {
+				const uint32_t b = (uint32_t)((seq + head) % nb);
+				t_sub[head % depth] = now_ns();
+				const int64_t r = gcl_rxloop_submit(loop, burst, &offs[(size_t)b * burst], nullptr,
+				                                    nullptr, nullptr, nullptr);
+				if (r < 0) {
+					fprintf(stderr, "submit: %lld\n", (long long)r);
+					exit(1);
+				}
+				tk[head % depth] = r;
+				head++;
+			}
+			const int w = gcl_rxloop_wait(loop, tk[tail % depth], v.data(), 1000000000ull);
+			if (w) {
+				fprintf(stderr, "wait: %d\n", w);
+				exit(1);
+			}
+			const uint32_t b = (uint32_t)((seq + tail) % nb);
+			const uint64_t d0 = now_ns();
+			delivered += gcl_host_deliver4(by_id.data(), R, clients.data(), (int)R, v.data(),
+			                               nullptr, len.data(), nullptr, cfg.default_olflags,
+			                               &offs[(size_t)b * burst], burst, nullptr, stats);
+			for (uint32_t i = 0; i < R * T; i++) /* the runtimes drained their rings */
+				heads[i] = chans[i].send_head;
+			const uint64_t d1 = now_ns();
+			if (timed) {
+				t_deliver += d1 - d0;
+				lat.push_back(d1 - t_sub[tail % depth]);
+			}
+			tail++;
+		}
+		seq += count;
+	};
+	const uint32_t warm = 200;
+	pump(warm, false);
+	const uint64_t t0 = now_ns();
+	pump(nbursts, true);
+	const uint64_t el = now_ns() - t0;
+	gcl_rxloop_stop(loop);
+	std::sort(lat.begin(), lat.end());
+	const double pkts = (double)burst * nbursts;
+	printf("{\"burst\": %u, \"workers\": %u, \"depth\": %u, \"bursts\": %u, \"mpps_one_core\": %.2f, "
+	       "\"burst_latency_p50_us\": %.2f, \"burst_latency_p99_us\": %.2f, "
+	       "\"deliver_ns_per_pkt\": %.2f, \"delivered_check\": \"%s\", \"unicast_fail\": %llu}\n",
+	       burst, workers, depth, nbursts, pkts / (el * 1e-3), lat[lat.size() / 2] * 1e-3,
+	       lat[lat.size() * 99 / 100] * 1e-3, t_deliver / pkts,
+	       delivered == (uint64_t)burst * (nbursts + warm) ? "ok" : "MISMATCH",
+	       (unsigned long long)stats[GCL_RX_UNICAST_FAIL]);
+	gcl_close(ctx);
+	CHECK(hipHostFree(region));
+	return 0;
+}
