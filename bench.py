@@ -412,8 +412,10 @@ def rxloop_bench(device, vbytes, iters=2000):
                 "p99_us": round(float(us[int(len(us) * 0.99)]), 2),
                 "mean_us": round(float(us.mean()), 2)}
 
-    for burst, workers, depth in ((64, 1, 1), (256, 1, 1), (1024, 1, 1), (64, 4, 8), (1024, 8, 16)):
-        loop = clf.rxloop(hfr, slots=16, max_burst=burst, workers=workers, lifetime_ms=30000)
+    for burst, workers, depth, fl in ((64, 1, 1, 0), (64, 1, 1, g.LOOP_INLINE_HDRS), (256, 1, 1, 0),
+                                      (1024, 1, 1, 0), (64, 4, 8, 0), (1024, 8, 16, 0)):
+        loop = clf.rxloop(hfr, slots=16, max_burst=burst, workers=workers, lifetime_ms=30000,
+                          flags=fl)
         try:
             offs = np.arange(burst, dtype=np.uint64) * np.uint64(stride)
             loop.drive(offs, 50, depth)  # warm
@@ -422,7 +424,7 @@ def rxloop_bench(device, vbytes, iters=2000):
             loop.stop()
         r = pct(lat)
         r["mpps"] = round(burst * iters / (el / 1e9) / 1e6, 2)
-        out[f"loop_burst{burst}_w{workers}_d{depth}"] = r
+        out[f"loop_burst{burst}_w{workers}_d{depth}" + ("_inline_hdrs" if fl else "")] = r
     hv = torch.empty(64 * vbytes, dtype=torch.uint8).pin_memory()
     lat = []
     for i in range(iters // 4 + 20):

@@ -641,6 +641,7 @@ struct LoopParams {
 	uint64_t frames_len;
 	unsigned long long *counts, *stats;
 	uint32_t max_rt, cflags, default_flags;
+	uint32_t off_hdr;          /* GCL_LOOP_INLINE_HDRS: 64-B granules in the slot; else 0 */
 };
 
 /* header tile + 2 x side arrays (offs, rss, fdir, hint, olflags) + verdicts + ctl */
@@ -748,18 +749,27 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 		const uint32_t nch = (n + 255) / 256;
 		uint4 r[4];
 		auto chunk_m = [&](uint32_t c) { return n - 256 * c < 256 ? n - 256 * c : 256u; };
-		auto load_frames = [&](const LoopSide &sd, uint32_t m) {
+		auto load_frames = [&](const LoopSide &sd, uint32_t c0, uint32_t m) {
 #pragma unroll
 			for (int j = 0; j < 4; j++) {
 				const int c = j * 256 + tid, p = c >> 2, q = c & 3;
-				r[j] = (uint32_t)p < m
-				       ? gcl::load16_host(frs, L.frames, L.frames_len, sd.offs[p] + 16 * (uint64_t)q)
-				       : make_uint4(0, 0, 0, 0);
+				if ((uint32_t)p >= m) {
+					r[j] = make_uint4(0, 0, 0, 0);
+				} else if (L.off_hdr) { /* granules inlined in the slot by the host */
+					const auto v = __builtin_amdgcn_raw_buffer_load_b128(
+					        srs, (int)(L.off_hdr + 64 * (256 * c0 + p) + 16 * q), 0, gcl::kSysAux);
+					r[j] = make_uint4(v[0], v[1], v[2], v[3]);
+				} else {
+					r[j] = gcl::load16_host(frs, L.frames, L.frames_len, sd.offs[p] + 16 * (uint64_t)q);
+				}
 			}
 		};
+		if (L.off_hdr) /* the granules do not wait for the offsets */
+			load_frames(side[0], 0, chunk_m(0));
 		side[0].load(slot, L, fl, 0, chunk_m(0), tid);
 		__syncthreads();
-		load_frames(side[0], chunk_m(0));
+		if (!L.off_hdr)
+			load_frames(side[0], 0, chunk_m(0));
 		for (uint32_t c = 0; c < nch; c++) {
 			const uint32_t m = chunk_m(c), base = 256 * c;
 			LoopSide &cur = side[c & 1];
@@ -772,7 +782,7 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 			}
 			__syncthreads(); /* tile of c and side arrays of c + 1 in LDS */
 			if (c + 1 < nch)
-				load_frames(side[(c + 1) & 1], chunk_m(c + 1));
+				load_frames(side[(c + 1) & 1], c + 1, chunk_m(c + 1));
 			k.n = m;
 			k.offs = cur.offs;
 			k.olflags = (fl & GCL_LOOP_F_OLF) ? cur.olf : nullptr;
@@ -2112,6 +2122,8 @@ struct gcl_rxloop {
 	uint32_t cur_img, img_seq;
 	uint64_t img_last[2];    /* last ticket that read image i */
 	std::vector<uint64_t> retired; /* per slot: last ticket the host collected */
+	const uint8_t *region;         /* host view, for GCL_LOOP_INLINE_HDRS */
+	uint64_t region_len;
 	bool ended;
 };
 
@@ -2202,6 +2214,8 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 		return -EINVAL;
 	if (c->cfg.flags & GCL_CFG_TRANS_HASH)
 		return -ENOTSUP;
+	if (cfg->flags & ~(uint32_t)GCL_LOOP_INLINE_HDRS)
+		return -EINVAL;
 	if (c->loop)
 		return -EBUSY;
 	if (hipSetDevice(c->device) != hipSuccess)
@@ -2213,6 +2227,8 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 	if (!L)
 		return -ENOMEM;
 	L->c = c;
+	L->region = (const uint8_t *)cfg->region;
+	L->region_len = cfg->region_len;
 	L->retired.assign(cfg->slots, 0);
 	L->max_burst = cfg->max_burst;
 	L->vbytes = (c->cfg.flags & GCL_CFG_VERDICT4) ? 4 : 8;
@@ -2224,7 +2240,9 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 	lp.off_fdir = lp.off_rss + 4 * mb;
 	lp.off_hint = lp.off_fdir + 4 * mb;
 	lp.off_verd = lp.off_hint + 4 * mb;
-	lp.slot_bytes = (lp.off_verd + sizeof(LoopRec) * mb + 255) & ~255ull;
+	lp.off_hdr = (cfg->flags & GCL_LOOP_INLINE_HDRS) ? lp.off_verd + sizeof(LoopRec) * mb : 0;
+	lp.slot_bytes = (lp.off_verd + sizeof(LoopRec) * mb + (lp.off_hdr ? GCL_HDR_GRANULE * mb : 0) +
+	                 255) & ~255ull;
 	lp.nslots = cfg->slots;
 	lp.workers = cfg->workers;
 	lp.lifetime_ticks = (uint64_t)cfg->lifetime_ms * 100000ull;
@@ -2315,6 +2333,19 @@ extern "C" int64_t gcl_rxloop_submit(struct gcl_rxloop *L, uint32_t n, const uin
 	uint8_t *s = (uint8_t *)h;
 	uint32_t fl = 0;
 	memcpy(s + L->lp.off_offs, offs, 8ull * n);
+	if (L->lp.off_hdr) { /* the header granules ride in the slot; past the region: 0 */
+		uint8_t *hd = s + L->lp.off_hdr;
+		for (uint32_t i = 0; i < n; i++, hd += GCL_HDR_GRANULE) {
+			const uint64_t o = offs[i];
+			if (o + GCL_HDR_GRANULE <= L->region_len) {
+				memcpy(hd, L->region + o, GCL_HDR_GRANULE);
+			} else {
+				const uint64_t k = o < L->region_len ? L->region_len - o : 0;
+				memcpy(hd, L->region + o, k);
+				memset(hd + k, 0, GCL_HDR_GRANULE - k);
+			}
+		}
+	}
 	if (olflags) {
 		memcpy(s + L->lp.off_olf, olflags, n);
 		fl |= GCL_LOOP_F_OLF;

@@ -107,7 +107,11 @@ class GclRxloopCfg(ctypes.Structure):
     _fields_ = [("slots", ctypes.c_uint32), ("max_burst", ctypes.c_uint32),
                 ("workers", ctypes.c_uint32), ("lifetime_ms", ctypes.c_uint32),
                 ("region", ctypes.c_void_p), ("region_len", ctypes.c_uint64),
-                ("counts", ctypes.c_void_p), ("stats", ctypes.c_void_p)]
+                ("counts", ctypes.c_void_p), ("stats", ctypes.c_void_p),
+                ("flags", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
+
+
+LOOP_INLINE_HDRS = 0x1
 
 
 class GclVerdict(ctypes.Structure):
@@ -489,10 +493,10 @@ class Classifier:
                                             _ptr(stats), ctypes.byref(o)), "gcl_classify_host")
 
     def rxloop(self, region, slots=64, max_burst=GCL_RX_BURST_SIZE, workers=1, lifetime_ms=20000,
-               counts=None, stats=None, region_len=None):
+               counts=None, stats=None, region_len=None, flags=0):
         """Start the persistent rx loop over a registered host region."""
         return RxLoop(self, region, slots, max_burst, workers, lifetime_ms, counts, stats,
-                      region_len)
+                      region_len, flags)
 
     def sync(self):
         return _check(lib.gcl_sync(self._ctx), "gcl_sync")
@@ -520,12 +524,12 @@ class RxLoop:
     """gcl_rxloop_*: burst-at-a-time classification by a persistent kernel."""
 
     def __init__(self, clf, region, slots, max_burst, workers, lifetime_ms, counts, stats,
-                 region_len=None):
+                 region_len=None, flags=0):
         self.clf, self.max_burst = clf, max_burst
         cfg = GclRxloopCfg(slots=slots, max_burst=max_burst, workers=workers,
                            lifetime_ms=lifetime_ms, region=_ptr(region),
                            region_len=_nbytes(region) if region_len is None else region_len,
-                           counts=_ptr(counts), stats=_ptr(stats))
+                           counts=_ptr(counts), stats=_ptr(stats), flags=flags)
         h = ctypes.c_void_p()
         _check(lib.gcl_rxloop_start(clf._ctx, ctypes.byref(cfg), ctypes.byref(h)), "gcl_rxloop_start")
         self._h = h

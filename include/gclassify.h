@@ -451,7 +451,14 @@ struct gcl_rxloop_cfg {
 	uint64_t region_len;
 	uint64_t *counts;      /* device u64[max_runtimes] (optional), accumulated */
 	uint64_t *stats;       /* device u64[GCL_NR_STATS] (optional), accumulated */
+	uint32_t flags;        /* GCL_LOOP_INLINE_HDRS */
+	uint32_t pad;
 };
+/* gcl_rxloop_submit copies each frame's first 64-B header granule into the
+ * ring slot (the dataplane core reads the headers, as rx_one_pkt does), so
+ * the kernel fetches them with the burst's side arrays instead of one PCIe
+ * round trip later from the region: lower latency for CPU time. */
+#define GCL_LOOP_INLINE_HDRS 0x1
 int gcl_rxloop_start(struct gcl_ctx *ctx, const struct gcl_rxloop_cfg *cfg,
                      struct gcl_rxloop **out);
 int64_t gcl_rxloop_submit(struct gcl_rxloop *loop, uint32_t n, const uint64_t *offs,

@@ -366,4 +366,4 @@ def test_rxloop_rejects_bad_args(g):
     assert g.lib.gcl_rxloop_wait(None, 1, None, 0) == -22
     assert g.lib.gcl_rxloop_stop(None) == -22
     assert g.lib.gcl_rxloop_drive(None, 1, 4096, 1, 1, None, None) == -22
-    assert ctypes.sizeof(g.GclRxloopCfg) == 48
+    assert ctypes.sizeof(g.GclRxloopCfg) == 56

@@ -39,14 +39,17 @@ def tc_map(rts, max_rt):
     return tc
 
 
-LOOP_CASES = [(m, v4, 0) for m in (0, 1, 2) for v4 in (False, True)] + \
-    [(m, False, fl) for m in (0, 1, 2) for fl in (1, 2)]
+LOOP_CASES = [(m, v4, 0, False) for m in (0, 1, 2) for v4 in (False, True)] + \
+    [(m, False, fl, False) for m in (0, 1, 2) for fl in (1, 2)] + \
+    [(0, False, 1, True), (1, True, 0, True), (2, False, 2, True)]
 
 
-@pytest.mark.parametrize("mode,v4,flags", LOOP_CASES)
-def test_rxloop_fuzz_vs_oracle(g, orc, mode, v4, flags):
-    """flags: 0 plain, 1 Azure ARP mode (GCL_CFG_AZURE_ARP), 2 16-bit hash."""
-    rng = np.random.default_rng(7000 + 10 * mode + v4 + 100 * flags)
+@pytest.mark.parametrize("mode,v4,flags,inline", LOOP_CASES)
+def test_rxloop_fuzz_vs_oracle(g, orc, mode, v4, flags, inline):
+    """flags: 0 plain, 1 Azure ARP mode (GCL_CFG_AZURE_ARP), 2 16-bit hash;
+    inline: header granules copied into the ring slot (GCL_LOOP_INLINE_HDRS),
+    including the frames that straddle the end of the region."""
+    rng = np.random.default_rng(7000 + 10 * mode + v4 + 100 * flags + 1000 * inline)
     max_rt = 1024 if mode == 1 else 16
     rts = random_runtimes(rng, max_rt, 300 if max_rt == 1024 else 12)
     n = 3000
@@ -62,7 +65,8 @@ def test_rxloop_fuzz_vs_oracle(g, orc, mode, v4, flags):
     g.host_register(frames)
     cnt = torch.zeros(max_rt, dtype=torch.int64, device="cuda")
     st = torch.zeros(g.NR_STATS, dtype=torch.int64, device="cuda")
-    loop = clf.rxloop(frames, slots=8, counts=cnt, stats=st, region_len=flen)
+    loop = clf.rxloop(frames, slots=8, counts=cnt, stats=st, region_len=flen,
+                      flags=g.LOOP_INLINE_HDRS if inline else 0)
     try:
         got = []
         for a, b in bursts(n):
