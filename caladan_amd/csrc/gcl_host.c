@@ -231,14 +231,15 @@ static bool send_to_runtime(struct gcl_host_proc *p, uint32_t hash, int slot, in
 }
 
 /* One verdict stream, either format: @v8 (gcl_verdict) or @v4 (gcl_verdict4,
- * whose broadcast hashes come from @bcast_hash). */
+ * whose broadcast hashes come from @bcast_hash).  Callbacks see packet
+ * index @base + i. */
 static uint64_t deliver(struct gcl_host_proc *const *clients_by_id, uint32_t max_runtimes,
                         struct gcl_host_proc *const *clients, int nr_clients,
                         const struct gcl_verdict *v8, const struct gcl_verdict4 *v4,
                         const uint32_t *bcast_hash, const uint16_t *pkt_len,
                         const uint8_t *olflags, uint8_t default_olflags,
                         const uint64_t *shmptr, uint64_t n,
-                        const struct gcl_host_ops *ops, uint64_t *stats)
+                        const struct gcl_host_ops *ops, uint64_t base, uint64_t *stats)
 {
 	uint64_t delivered = 0;
 
@@ -263,7 +264,7 @@ static uint64_t deliver(struct gcl_host_proc *const *clients_by_id, uint32_t max
 			if (ok) {
 				delivered++;
 				if (ops && ops->owned)
-					ops->owned(ops->arg, p, i);
+					ops->owned(ops->arg, p, base + i);
 				continue;
 			}
 			stats[GCL_RX_UNICAST_FAIL]++; /* rx.c:140-142, :213-215 */
@@ -273,33 +274,33 @@ static uint64_t deliver(struct gcl_host_proc *const *clients_by_id, uint32_t max
 				if (send_to_runtime(clients[c], hash, -1, -1, cmd, payload, ops)) {
 					n_sent++;
 					if (ops && ops->owned)
-						ops->owned(ops->arg, clients[c], i);
+						ops->owned(ops->arg, clients[c], base + i);
 				} else {
 					stats[GCL_RX_BROADCAST_FAIL]++;
 				}
 			}
 			if (n_sent == 0) {
 				if (ops && ops->free_pkt)
-					ops->free_pkt(ops->arg, i);
+					ops->free_pkt(ops->arg, base + i);
 			} else {
 				delivered++;
 				if (ops && ops->refcnt_update)
-					ops->refcnt_update(ops->arg, i, n_sent - 1);
+					ops->refcnt_update(ops->arg, base + i, n_sent - 1);
 			}
 			continue; /* rx.c:185-189: no RX_UNHANDLED */
 		} else if (act == GCL_ACT_ARP_RESPOND) {
-			if (ops && ops->arp_respond && ops->arp_respond(ops->arg, i))
+			if (ops && ops->arp_respond && ops->arp_respond(ops->arg, base + i))
 				continue;
 			stats[GCL_RX_UNREGISTERED_MAC]++; /* rx.c:205 */
 		} else {
 			/* DROP_*: the device already counted them */
 			if (ops && ops->free_pkt)
-				ops->free_pkt(ops->arg, i);
+				ops->free_pkt(ops->arg, base + i);
 			continue;
 		}
 		/* fail_free, rx.c:225-232 */
 		if (ops && ops->free_pkt)
-			ops->free_pkt(ops->arg, i);
+			ops->free_pkt(ops->arg, base + i);
 		stats[GCL_RX_UNHANDLED]++;
 	}
 	return delivered;
@@ -313,7 +314,61 @@ uint64_t gcl_host_deliver(struct gcl_host_proc *const *clients_by_id, uint32_t m
                           const struct gcl_host_ops *ops, uint64_t *stats)
 {
 	return deliver(clients_by_id, max_runtimes, clients, nr_clients, v, NULL, NULL, pkt_len,
-	               olflags, default_olflags, shmptr, n, ops, stats);
+	               olflags, default_olflags, shmptr, n, ops, 0, stats);
+}
+
+/* deliver() for compact verdicts, with the common case inlined: a DELIVER
+ * verdict names the kthread, so the packet goes straight into that ring
+ * (rx.c:56-58 with active threads, then :76-92) with the two per-delivery
+ * callbacks of the reference, thread_enable_sched_poll and the ownership
+ * record.  Everything else (WAKE, broadcast, drops, a full ring) takes
+ * deliver() for that one packet, in order, so the outcome is the same packet
+ * by packet.  2.1 ns/pkt against 3.1 for deliver() alone on the bench host
+ * (EPYC 9575F, 16 x 8 rings, no callbacks, profiles/r01_deliver.txt); a
+ * write prefetch of the ring slot 8-32 packets ahead made it slower. */
+static uint64_t deliver4_fast(struct gcl_host_proc *const *clients_by_id, uint32_t max_runtimes,
+                              struct gcl_host_proc *const *clients, int nr_clients,
+                              const struct gcl_verdict4 *v, const uint32_t *bcast_hash,
+                              const uint16_t *pkt_len, const uint8_t *olflags,
+                              uint8_t default_olflags, const uint64_t *shmptr, uint64_t n,
+                              const struct gcl_host_ops *ops, uint64_t *stats)
+{
+	const uint64_t csum_def = (default_olflags & GCL_F_IP_CKSUM_MASK) == GCL_F_IP_CKSUM_GOOD;
+	void (*const enable_poll)(void *, struct gcl_host_proc *, unsigned int) =
+		ops ? ops->enable_poll : NULL;
+	void (*const owned)(void *, struct gcl_host_proc *, uint64_t) = ops ? ops->owned : NULL;
+	uint64_t delivered = 0;
+
+	for (uint64_t i = 0; i < n; i++) {
+		const struct gcl_verdict4 x = v[i];
+		struct gcl_host_proc *p;
+		struct gcl_lrpc_chan_out *chan;
+
+		if ((x.action & GCL_ACT_MASK) != GCL_ACT_DELIVER || x.uniqid >= max_runtimes ||
+		    !(p = clients_by_id[x.uniqid]) || x.thread >= p->thread_count ||
+		    !(chan = p->rxq[x.thread]) ||
+		    chan->send_head - chan->send_tail >= chan->size) {
+			delivered += deliver(clients_by_id, max_runtimes, clients, nr_clients, NULL, v + i,
+			                     bcast_hash ? bcast_hash + i : NULL, pkt_len ? pkt_len + i : NULL,
+			                     olflags ? olflags + i : NULL, default_olflags,
+			                     shmptr ? shmptr + i : NULL, 1, ops, i, stats);
+			continue;
+		}
+		if (enable_poll)
+			enable_poll(ops->arg, p, x.thread);
+		const uint64_t csum = olflags ?
+			(olflags[i] & GCL_F_IP_CKSUM_MASK) == GCL_F_IP_CKSUM_GOOD : csum_def;
+		const uint32_t h = chan->send_head++;
+		struct gcl_lrpc_msg *dst = &chan->tbl[h & (chan->size - 1)];
+		dst->payload = shmptr ? shmptr[i] : 0;
+		__atomic_store_n(&dst->cmd, (uint64_t)(pkt_len ? pkt_len[i] : 0) << 16 | csum << 48 |
+		                            ((h & chan->size) ? 0 : GCL_LRPC_DONE_PARITY),
+		                 __ATOMIC_RELEASE);
+		if (owned)
+			owned(ops->arg, p, i);
+		delivered++;
+	}
+	return delivered;
 }
 
 uint64_t gcl_host_deliver4(struct gcl_host_proc *const *clients_by_id, uint32_t max_runtimes,
@@ -323,6 +378,6 @@ uint64_t gcl_host_deliver4(struct gcl_host_proc *const *clients_by_id, uint32_t 
                            uint8_t default_olflags, const uint64_t *shmptr, uint64_t n,
                            const struct gcl_host_ops *ops, uint64_t *stats)
 {
-	return deliver(clients_by_id, max_runtimes, clients, nr_clients, NULL, v, bcast_hash,
-	               pkt_len, olflags, default_olflags, shmptr, n, ops, stats);
+	return deliver4_fast(clients_by_id, max_runtimes, clients, nr_clients, v, bcast_hash,
+	                     pkt_len, olflags, default_olflags, shmptr, n, ops, stats);
 }

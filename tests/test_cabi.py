@@ -281,8 +281,9 @@ def test_host_deliver_broadcast_and_arp(g):
 
 def test_host_deliver4_matches_deliver(g, orc):
     """Compact verdicts replay exactly like 8-B ones: same rings, counters and
-    frees, including wakes that change the flow_tbl mid-batch and broadcasts
-    fanned out with the caller's hashes."""
+    callbacks in the same order with the same packet indices (polls, ownership
+    records, frees, ARP responses), including wakes that change the flow_tbl
+    mid-batch and broadcasts fanned out with the caller's hashes."""
     from tests.rxcases import fuzz_batch, random_runtimes, to_verdict4
     rng = np.random.default_rng(12)
     R = 64
@@ -324,8 +325,22 @@ def test_host_deliver4_matches_deliver(g, orc):
         def refcnt(arg, i, d):
             events.append(("ref", i, d))
 
+        @g.OWNED_FN
+        def owned(arg, pp, i):
+            events.append(("own", pp.contents.uniqid, i))
+
+        @g.ENABLE_POLL_FN
+        def poll(arg, pp, th):
+            events.append(("poll", pp.contents.uniqid, th))
+
+        @g.ARP_RESPOND_FN
+        def arp(arg, i):
+            events.append(("arp", i))
+            return i % 2 == 0
+
         ops = g.GclHostOps()
         ops.sched_add_core, ops.free_pkt, ops.refcnt_update = add_core, free_pkt, refcnt
+        ops.owned, ops.enable_poll, ops.arp_respond = owned, poll, arp
         stats = np.zeros(8, dtype=np.uint64)
         if compact:
             d = g.lib.gcl_host_deliver4(by_id, R, clients, len(procs), v4.ctypes.data,
@@ -339,7 +354,57 @@ def test_host_deliver4_matches_deliver(g, orc):
         return d, list(stats), events, {k: r.drain() for k, r in rings.items()}
 
     full, compact = run(False), run(True)
-    assert full[0] > 0 and any(e[0] == "wake" for e in full[2])
+    kinds = {e[0] for e in full[2]}
+    assert full[0] > 0 and {"wake", "own", "poll", "free", "ref", "arp"} <= kinds, kinds
+    assert full == compact
+
+
+@pytest.mark.parametrize("meta", ["all", "no_olflags", "none"])
+def test_host_deliver4_fast_path(g, orc, meta):
+    """With no callbacks gcl_host_deliver4 takes its DELIVER fast path; it must
+    fill the same rings in the same order as the generic replay of the 8-B
+    verdicts, with the full rings (8 deep here) and the non-DELIVER verdicts
+    handed back to the generic code packet by packet."""
+    from tests.rxcases import fuzz_batch, random_runtimes, to_verdict4
+    rng = np.random.default_rng(13)
+    R = 64
+    rts = random_runtimes(rng, R, 24, max_threads=6)
+    n = 3000
+    frames, flen, offs, olf, rss, fdir, _ = fuzz_batch(rng, n, rts, R, tail_runts=False)
+    t = orc.Tables(R, 0, 0x1, 0x09)
+    for r in rts:
+        assert t.runtime_set(r["uniqid"], r["ip"], r["thread_count"], r["active"], r["flow_tbl"]) == 0
+    v, _, _ = t.classify(frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir_hi=fdir, frames_len=flen)
+    v4 = to_verdict4(v, {r["uniqid"]: r["thread_count"] for r in rts})
+    assert ((v4["action"] & 0x3F) == g.ACT_DELIVER).sum() > n // 3
+    pkt_len = rng.integers(60, 1515, size=n).astype(np.uint16)
+    shm = offs.astype(np.uint64)
+    bhash = rss.astype(np.uint32)
+    pl = None if meta == "none" else pkt_len.ctypes.data
+    of = olf.ctypes.data if meta == "all" else None
+    sp = None if meta == "none" else shm.ctypes.data
+
+    def run(compact):
+        procs, rings, keep = _host_procs(g, rts, 8)
+        for p in procs.values():
+            if p.active_thread_count == 0 and p.thread_count > 1:
+                p.idle_top = 1
+        by_id = (ctypes.c_void_p * R)()
+        for u, p in procs.items():
+            by_id[u] = ctypes.addressof(p)
+        clients = (ctypes.c_void_p * len(procs))(*[ctypes.addressof(p) for p in procs.values()])
+        stats = np.zeros(8, dtype=np.uint64)
+        if compact:
+            d = g.lib.gcl_host_deliver4(by_id, R, clients, len(procs), v4.ctypes.data,
+                                        bhash.ctypes.data, pl, of, 0x09, sp, n, None,
+                                        stats.ctypes.data)
+        else:
+            d = g.lib.gcl_host_deliver(by_id, R, clients, len(procs), v.ctypes.data, pl, of, 0x09,
+                                       sp, n, None, stats.ctypes.data)
+        return d, list(stats), {k: r.drain() for k, r in rings.items()}
+
+    full, compact = run(False), run(True)
+    assert full[0] > 0 and full[1][1] > 0  # deliveries and ring-full failures both happen
     assert full == compact
 
 
