@@ -49,10 +49,26 @@ WORKLOADS = {
               "1Mi mixed frames (70% IPv4 TCP/UDP 64..9014B, 20% IPv6, 10% ARP), 9216B slots, 16 runtimes"),
 }
 # algorithmic bytes per packet: one 64-B header granule read + one verdict
-# written, 8 B (gcl_verdict) or 4 B (gcl_verdict4) (DESIGN.md "Roofline");
-# tables and counters amortise to ~0.
+# written, 8 B (gcl_verdict), 4 B (gcl_verdict4) or 2 B (the kthread-queue
+# verdict of GCL_CFG_VERDICT2) (DESIGN.md "Roofline"); tables and counters
+# amortise to ~0.
 HDR_BYTES = 64
 VERDICT_BYTES = 4
+VERDICT_NAMES = {8: "gcl_verdict, 8 B", 4: "gcl_verdict4, 4 B",
+                 2: "queue verdict (GCL_CFG_VERDICT2), 2 B"}
+
+
+def verdict_cfg(vbytes, R, T):
+    """(cfg flags, thread_bits) of a context writing @vbytes-byte verdicts
+    for R runtimes of up to T kthreads."""
+    if vbytes == 2:
+        return g.CFG_VERDICT2, g.thread_bits_for(R, T)
+    return (g.CFG_VERDICT4 if vbytes == 4 else 0), 0
+
+
+def classifier(device, R, T, vbytes, extra_flags=0):
+    fl, tb = verdict_cfg(vbytes, R, T)
+    return g.Classifier(device.index or 0, R, g.HASH_JENKINS, fl | extra_flags, thread_bits=tb)
 
 
 def log(*a):
@@ -131,8 +147,8 @@ class Workload:
             cdf_dev = torch.from_numpy(g.zipf_cdf(nflows, 0.99).view(np.int64)).to(device)
         g.generate(wl, n, stride, R, self.frames, seed=SEED, rank=rank, world=world,
                    shard_block=SHARD_BLOCK, zipf_cdf_dev=cdf_dev, nflows=nflows)
-        self.clf = g.Classifier(device.index or 0, R, hash_mode,
-                                g.CFG_PROFILE | (g.CFG_VERDICT4 if vbytes == 4 else 0))
+        fl, tb = verdict_cfg(vbytes, R, T)
+        self.clf = g.Classifier(device.index or 0, R, hash_mode, g.CFG_PROFILE | fl, thread_bits=tb)
         self.tables = setup_tables(self.clf, R, T)
         torch.cuda.synchronize()
 
@@ -253,7 +269,7 @@ def roofline(w, kernel_ms):
     bytes_per_launch = w.n * w.bytes_per_pkt
     achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
     traffic = None
-    prof = os.path.join(ROOT, "profiles", f"pmc_{w.name}{'_v4' if w.vbytes == 4 else ''}.json")
+    prof = os.path.join(ROOT, "profiles", f"pmc_{w.name}{'' if w.vbytes == 8 else f'_v{w.vbytes}'}.json")
     if os.path.exists(prof):
         try:
             with open(prof) as f:
@@ -287,7 +303,7 @@ def e2e_bench(device, vbytes=VERDICT_BYTES, reps=3):
         hfr = torch.empty(n * stride, dtype=torch.uint8).pin_memory()
         hfr.copy_(dfr)
         hv = torch.empty(n * vbytes, dtype=torch.uint8).pin_memory()
-        clf = g.Classifier(device.index or 0, R, g.HASH_JENKINS, g.CFG_VERDICT4 if vbytes == 4 else 0)
+        clf = classifier(device, R, T, vbytes)
         setup_tables(clf, R, T)
         res = {"pkts": n, "slot_stride": stride}
         for tag, mode, nst in (("copy_hdr_2streams", g.E2E_COPY, 2), ("copy_hdr_4streams", g.E2E_COPY, 4),
@@ -334,7 +350,7 @@ def e2e_multi(device, rank, world, vbytes, reps=3):
     del dfr
     torch.cuda.synchronize()
     hv = torch.empty(n * vbytes, dtype=torch.uint8).pin_memory()
-    clf = g.Classifier(device.index or 0, R, g.HASH_JENKINS, g.CFG_VERDICT4 if vbytes == 4 else 0)
+    clf = classifier(device, R, T, vbytes)
     setup_tables(clf, R, T)
     nccl = torch.distributed.get_backend() == "nccl"
     res = {"pkts_per_gpu": n, "slot_stride": stride, "n_gpus": world}
@@ -402,7 +418,7 @@ def rxloop_bench(device, vbytes, iters=2000):
     hfr = torch.empty(n * stride, dtype=torch.uint8).pin_memory()
     hfr.copy_(dfr)
     torch.cuda.synchronize()
-    clf = g.Classifier(device.index or 0, R, g.HASH_JENKINS, g.CFG_VERDICT4 if vbytes == 4 else 0)
+    clf = classifier(device, R, T, vbytes)
     setup_tables(clf, R, T)
     out = {"frames": "udp64 synthetic, pinned host memory, read zero-copy"}
 
@@ -457,7 +473,7 @@ def ingress_pool_bench(device, vbytes, cycles=64, reps=10):
     order = torch.cat([torch.randperm(P, generator=gen) for _ in range(cycles)]).to(device)
     offs = pool_offs[order].contiguous()
     n = offs.numel()
-    clf = g.Classifier(device.index or 0, R, g.HASH_JENKINS, g.CFG_VERDICT4 if vbytes == 4 else 0)
+    clf = classifier(device, R, T, vbytes)
     setup_tables(clf, R, T)
     cnt = torch.zeros(R + g.NR_STATS, dtype=torch.int64, device=device)
     dv = torch.empty(n * vbytes, dtype=torch.uint8, device=device)
@@ -601,8 +617,9 @@ def main():
                     help="time one classify launch in N with HIP events (roofline.kernel_ms)")
     ap.add_argument("--exchange-every", type=int, default=EXCHANGE_EVERY,
                     help="steps per counts all_gather (multi-GPU exchange period)")
-    ap.add_argument("--verdict-bytes", type=int, default=VERDICT_BYTES, choices=[4, 8],
-                    help="8: struct gcl_verdict (with the hash); 4: struct gcl_verdict4")
+    ap.add_argument("--verdict-bytes", type=int, default=VERDICT_BYTES, choices=[2, 4, 8],
+                    help="8: struct gcl_verdict (with the hash); 4: struct gcl_verdict4; "
+                         "2: kthread-queue verdict (GCL_CFG_VERDICT2)")
     ap.add_argument("--force-exchange", action="store_true",
                     help="run the multi-GPU step (RCCL all_gather on a side stream) even at N=1")
     args = ap.parse_args()
@@ -648,7 +665,7 @@ def main():
         "config": {"workload": f"{args.workload}: {w.desc}", "pkts_per_gpu": w.n,
                    "slot_stride": w.stride, "runtimes": w.R, "kthreads": w.T,
                    "hash": "jenkins (lookup3 13-B 5-tuple)",
-                   "verdict": "gcl_verdict4, 4 B" if vb == 4 else "gcl_verdict, 8 B",
+                   "verdict": VERDICT_NAMES[vb],
                    "parallelism": (f"dp{world}: round-robin 64Ki-pkt shards, {args.dist_backend} "
                                    f"all_gather of per-runtime counts every {args.exchange_every} step(s), overlapped"
                                    if dist_on else "single GPU")},
@@ -660,14 +677,17 @@ def main():
     torch.cuda.empty_cache()
 
     if world == 1 and not args.no_secondary and args.workload == "udp64":
-        # the same udp64 step with the other verdict format
-        w4 = Workload(args.workload, rank, world, device, vbytes=12 - vb)
-        el4, kms4 = run_timed(w4, args.steps, 3, 1)
-        other = {"verdict": "gcl_verdict, 8 B" if vb == 4 else "gcl_verdict4, 4 B",
-                 "value": round(w4.n * args.steps / el4 / 1e6, 1), "unit": "Mpkt/s",
-                 "ms_per_step": round(el4 / args.steps * 1e3, 4), "roofline": roofline(w4, kms4), "placement": placement(w4)}
-        del w4
-        torch.cuda.empty_cache()
+        # the same udp64 step with the other verdict formats
+        other = []
+        for ob in (b for b in (8, 4, 2) if b != vb):
+            w4 = Workload(args.workload, rank, world, device, vbytes=ob)
+            el4, kms4 = run_timed(w4, args.steps, 3, 1)
+            other.append({"verdict": VERDICT_NAMES[ob],
+                          "value": round(w4.n * args.steps / el4 / 1e6, 1), "unit": "Mpkt/s",
+                          "ms_per_step": round(el4 / args.steps * 1e3, 4), "roofline": roofline(w4, kms4),
+                          "placement": placement(w4)})
+            del w4
+            torch.cuda.empty_cache()
         w2 = Workload("tcp1500", rank, world, device, vbytes=vb)
         el2, kms2 = run_timed(w2, max(20, args.steps // 2), 3, 1)
         steps2 = max(20, args.steps // 2)
@@ -685,7 +705,7 @@ def main():
             "placement": placement(w2),
             "frame_bytes_rate_GBs": round(w2.n * 1500 / (kms2 * 1e-3) / 1e9, 1),
             "header_split_layout": hsplit,
-            "udp64_other_verdict": other,
+            "udp64_other_verdicts": other,
         }
         del w2
         torch.cuda.empty_cache()

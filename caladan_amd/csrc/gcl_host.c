@@ -317,6 +317,23 @@ uint64_t gcl_host_deliver(struct gcl_host_proc *const *clients_by_id, uint32_t m
 	               olflags, default_olflags, shmptr, n, ops, 0, stats);
 }
 
+struct gcl_verdict4 gcl_verdict2_to4(uint16_t v, uint8_t thread_bits)
+{
+	struct gcl_verdict4 o;
+	const uint16_t kind = v & GCL_V2_KIND, q = v & GCL_V2_Q_MASK;
+
+	if (kind == GCL_V2_DELIVER || kind == GCL_V2_WAKE) {
+		o.uniqid = (uint16_t)(q >> thread_bits);
+		o.thread = (uint8_t)(q & ((1u << thread_bits) - 1));
+		o.action = kind == GCL_V2_WAKE ? GCL_ACT_WAKE : GCL_ACT_DELIVER;
+	} else {
+		o.uniqid = GCL_NO_RUNTIME;
+		o.thread = GCL_NO_THREAD;
+		o.action = (uint8_t)(v & GCL_ACT_MASK);
+	}
+	return o;
+}
+
 /* deliver() for compact verdicts, with the common case inlined: a DELIVER
  * verdict names the kthread, so the packet goes straight into that ring
  * (rx.c:56-58 with active threads, then :76-92) with the two per-delivery
@@ -325,37 +342,53 @@ uint64_t gcl_host_deliver(struct gcl_host_proc *const *clients_by_id, uint32_t m
  * deliver() for that one packet, in order, so the outcome is the same packet
  * by packet.  2.1 ns/pkt against 3.1 for deliver() alone on the bench host
  * (EPYC 9575F, 16 x 8 rings, no callbacks, profiles/r01_deliver.txt); a
- * write prefetch of the ring slot 8-32 packets ahead made it slower. */
-static uint64_t deliver4_fast(struct gcl_host_proc *const *clients_by_id, uint32_t max_runtimes,
-                              struct gcl_host_proc *const *clients, int nr_clients,
-                              const struct gcl_verdict4 *v, const uint32_t *bcast_hash,
-                              const uint16_t *pkt_len, const uint8_t *olflags,
-                              uint8_t default_olflags, const uint64_t *shmptr, uint64_t n,
-                              const struct gcl_host_ops *ops, uint64_t *stats)
+ * write prefetch of the ring slot 8-32 packets ahead made it slower.
+ * Verdicts are @v2 (2-byte, of a context with @thread_bits) or @v4; always
+ * inlined with a constant @v2 == NULL or not. */
+static inline __attribute__((always_inline)) uint64_t
+deliver_compact(struct gcl_host_proc *const *clients_by_id, uint32_t max_runtimes,
+                struct gcl_host_proc *const *clients, int nr_clients,
+                const struct gcl_verdict4 *v4, const uint16_t *v2, uint8_t thread_bits,
+                const uint32_t *bcast_hash, const uint16_t *pkt_len, const uint8_t *olflags,
+                uint8_t default_olflags, const uint64_t *shmptr, uint64_t n,
+                const struct gcl_host_ops *ops, uint64_t *stats)
 {
 	const uint64_t csum_def = (default_olflags & GCL_F_IP_CKSUM_MASK) == GCL_F_IP_CKSUM_GOOD;
 	void (*const enable_poll)(void *, struct gcl_host_proc *, unsigned int) =
 		ops ? ops->enable_poll : NULL;
 	void (*const owned)(void *, struct gcl_host_proc *, uint64_t) = ops ? ops->owned : NULL;
+	const uint32_t tmask = (1u << thread_bits) - 1;
 	uint64_t delivered = 0;
 
 	for (uint64_t i = 0; i < n; i++) {
-		const struct gcl_verdict4 x = v[i];
 		struct gcl_host_proc *p;
 		struct gcl_lrpc_chan_out *chan;
+		uint32_t uniqid, thread;
+		bool fast;
 
-		if ((x.action & GCL_ACT_MASK) != GCL_ACT_DELIVER || x.uniqid >= max_runtimes ||
-		    !(p = clients_by_id[x.uniqid]) || x.thread >= p->thread_count ||
-		    !(chan = p->rxq[x.thread]) ||
+		if (v2) {
+			const uint16_t x = v2[i];
+			uniqid = (x & GCL_V2_Q_MASK) >> thread_bits;
+			thread = x & tmask;
+			fast = (x & GCL_V2_KIND) == GCL_V2_DELIVER;
+		} else {
+			const struct gcl_verdict4 x = v4[i];
+			uniqid = x.uniqid;
+			thread = x.thread;
+			fast = (x.action & GCL_ACT_MASK) == GCL_ACT_DELIVER;
+		}
+		if (!fast || uniqid >= max_runtimes || !(p = clients_by_id[uniqid]) ||
+		    thread >= p->thread_count || !(chan = p->rxq[thread]) ||
 		    chan->send_head - chan->send_tail >= chan->size) {
-			delivered += deliver(clients_by_id, max_runtimes, clients, nr_clients, NULL, v + i,
+			const struct gcl_verdict4 w = v2 ? gcl_verdict2_to4(v2[i], thread_bits) : v4[i];
+			delivered += deliver(clients_by_id, max_runtimes, clients, nr_clients, NULL, &w,
 			                     bcast_hash ? bcast_hash + i : NULL, pkt_len ? pkt_len + i : NULL,
 			                     olflags ? olflags + i : NULL, default_olflags,
 			                     shmptr ? shmptr + i : NULL, 1, ops, i, stats);
 			continue;
 		}
 		if (enable_poll)
-			enable_poll(ops->arg, p, x.thread);
+			enable_poll(ops->arg, p, thread);
 		const uint64_t csum = olflags ?
 			(olflags[i] & GCL_F_IP_CKSUM_MASK) == GCL_F_IP_CKSUM_GOOD : csum_def;
 		const uint32_t h = chan->send_head++;
@@ -378,6 +411,20 @@ uint64_t gcl_host_deliver4(struct gcl_host_proc *const *clients_by_id, uint32_t 
                            uint8_t default_olflags, const uint64_t *shmptr, uint64_t n,
                            const struct gcl_host_ops *ops, uint64_t *stats)
 {
-	return deliver4_fast(clients_by_id, max_runtimes, clients, nr_clients, v, bcast_hash,
-	                     pkt_len, olflags, default_olflags, shmptr, n, ops, stats);
+	return deliver_compact(clients_by_id, max_runtimes, clients, nr_clients, v, NULL, 0,
+	                       bcast_hash, pkt_len, olflags, default_olflags, shmptr, n, ops, stats);
+}
+
+uint64_t gcl_host_deliver2(struct gcl_host_proc *const *clients_by_id, uint32_t max_runtimes,
+                           struct gcl_host_proc *const *clients, int nr_clients,
+                           const uint16_t *v, uint8_t thread_bits, const uint32_t *bcast_hash,
+                           const uint16_t *pkt_len, const uint8_t *olflags,
+                           uint8_t default_olflags, const uint64_t *shmptr, uint64_t n,
+                           const struct gcl_host_ops *ops, uint64_t *stats)
+{
+	if (thread_bits > 8 || !v)
+		return 0;
+	return deliver_compact(clients_by_id, max_runtimes, clients, nr_clients, NULL, v,
+	                       thread_bits, bcast_hash, pkt_len, olflags, default_olflags, shmptr,
+	                       n, ops, stats);
 }

@@ -348,7 +348,7 @@ __device__ __forceinline__ void classify_one(const KParams &k, const uint4 *tile
 				thr = tb.flow[re.flow_off + slot];
 			} else {
 				action |= GCL_ACT_WAKE;
-				if (k.cflags & GCL_CFG_VERDICT4)
+				if (k.cflags & (GCL_CFG_VERDICT4 | GCL_CFG_VERDICT2))
 					thr = slot; /* the host replays flow_tbl[slot] */
 			}
 		}
@@ -374,7 +374,14 @@ __device__ __forceinline__ void classify_one(const KParams &k, const uint4 *tile
 		k.trans[idx] = tr;
 	}
 	const uint32_t vlo = uniq | thr << 16 | action << 24;
-	if (k.cflags & GCL_CFG_VERDICT4) {
+	if (k.cflags & GCL_CFG_VERDICT2) {
+		/* q = uniqid << thread_bits | thread (thread_bits in cflags[31:24]) */
+		const uint32_t a = action & GCL_ACT_MASK;
+		const uint32_t q = uniq << (k.cflags >> 24) | thr;
+		const uint32_t v2 = a == GCL_ACT_DELIVER ? q
+		                  : a == GCL_ACT_WAKE ? GCL_V2_WAKE | q : GCL_V2_OTHER | a;
+		((uint16_t *)k.verdicts)[idx] = (uint16_t)v2;
+	} else if (k.cflags & GCL_CFG_VERDICT4) {
 		((uint32_t *)k.verdicts)[idx] = vlo;
 	} else {
 		const u32x2 vd = {hash, vlo};
@@ -696,7 +703,7 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 	k.frames_len = L.frames_len;
 	k.verdicts = s_verd;
 	k.max_rt = L.max_rt;
-	k.cflags = L.cflags;
+	k.cflags = L.cflags; /* with thread_bits in [31:24] */
 	k.default_flags = L.default_flags;
 	Tables tb = {};
 	uint32_t cur_seq = 0xFF; /* no image yet (versions are taken mod 64) */
@@ -791,9 +798,10 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 			k.dst_hint = (fl & GCL_LOOP_F_HINT) ? cur.hint : nullptr;
 			if ((uint32_t)tid < m) {
 				classify_one<MODE, true, true>(k, tile, tid, (uint64_t)tid, tb, hist, cnt);
-				const bool v4 = L.cflags & GCL_CFG_VERDICT4;
-				const uint32_t hsh = v4 ? 0u : s_verd[tid].x;
-				const uint32_t vlo = v4 ? ((const uint32_t *)s_verd)[tid] : s_verd[tid].y;
+				const bool v4 = L.cflags & GCL_CFG_VERDICT4, v2 = L.cflags & GCL_CFG_VERDICT2;
+				const uint32_t hsh = v4 || v2 ? 0u : s_verd[tid].x;
+				const uint32_t vlo = v2 ? ((const uint16_t *)s_verd)[tid]
+				                   : v4 ? ((const uint32_t *)s_verd)[tid] : s_verd[tid].y;
 				const gcl::u32x4 rec = {hsh, vlo, (uint32_t)t, (uint32_t)(t >> 32)};
 				__builtin_amdgcn_raw_buffer_store_b128(
 				        rec, srs, (int)(L.off_verd + sizeof(LoopRec) * (base + tid)), 0, gcl::kSysAux);
@@ -1070,6 +1078,10 @@ extern "C" int gcl_open(int hip_device, const struct gcl_cfg *cfg, struct gcl_ct
 	if (!cfg || !out || cfg->max_runtimes == 0 || cfg->max_runtimes > GCL_MAX_PROC ||
 	    cfg->hash_mode > GCL_HASH_TOEPLITZ)
 		return -EINVAL;
+	if ((cfg->flags & GCL_CFG_VERDICT2) &&
+	    ((cfg->flags & (GCL_CFG_VERDICT4 | GCL_CFG_TRANS_HASH)) || cfg->thread_bits > 8 ||
+	     ((uint64_t)cfg->max_runtimes << cfg->thread_bits) > GCL_V2_QUEUES))
+		return -EINVAL;
 	if (hipGetDeviceCount(&ndev) != hipSuccess || hip_device < 0 || hip_device >= ndev)
 		return -ENODEV;
 	if (hipSetDevice(hip_device) != hipSuccess)
@@ -1207,6 +1219,8 @@ extern "C" int gcl_runtime_set(struct gcl_ctx *c, uint16_t uniqid, uint32_t ip_h
 	if (!c || uniqid >= c->cfg.max_runtimes || thread_count == 0 ||
 	    thread_count > GCL_NCPU || active_count > thread_count)
 		return -EINVAL;
+	if ((c->cfg.flags & GCL_CFG_VERDICT2) && thread_count > (1u << c->cfg.thread_bits))
+		return -EINVAL; /* its queues would not fit the 2-byte verdict */
 	if (active_count) {
 		if (!flow_tbl)
 			return -EINVAL;
@@ -1530,6 +1544,17 @@ static void image_used(gcl_ctx *c, hipStream_t s)
 
 /* Upload a new table snapshot on @s if anything changed; launches on other
  * streams wait for c->tables_ready before reading the image. */
+static uint32_t verdict_bytes(const gcl_ctx *c)
+{
+	return (c->cfg.flags & GCL_CFG_VERDICT2) ? 2 : (c->cfg.flags & GCL_CFG_VERDICT4) ? 4 : 8;
+}
+
+/* the kernels' cflags: cfg.flags with thread_bits in [31:24] */
+static uint32_t kernel_cflags(const gcl_ctx *c)
+{
+	return (c->cfg.flags & 0xFFFFFFu) | (uint32_t)c->cfg.thread_bits << 24;
+}
+
 static int upload_tables(gcl_ctx *c, hipStream_t s)
 {
 	if (!c->dirty)
@@ -1630,7 +1655,7 @@ extern "C" int gcl_classify_ex(struct gcl_ctx *c, const struct gcl_batch *b,
 	k.off_seed = c->off_seed;
 	k.off_crc = c->off_crc;
 	k.trans = (uint2 *)out->trans;
-	k.cflags = c->cfg.flags;
+	k.cflags = kernel_cflags(c);
 	k.default_flags = c->cfg.default_olflags;
 	k.nt_store = c->tune_nt_store;
 	k.ablate = c->tune_ablate;
@@ -1995,7 +2020,7 @@ extern "C" int gcl_classify_host(struct gcl_ctx *c, const struct gcl_batch *hb,
 		return 0;
 	hipSetDevice(c->device);
 	const uint32_t max_rt = c->cfg.max_runtimes;
-	const uint64_t vsize = (c->cfg.flags & GCL_CFG_VERDICT4) ? 4 : 8;
+	const uint64_t vsize = verdict_bytes(c);
 	int nst = o->nstreams ? (int)o->nstreams : 2;
 	if (nst > 4)
 		nst = 4;
@@ -2231,7 +2256,7 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 	L->region_len = cfg->region_len;
 	L->retired.assign(cfg->slots, 0);
 	L->max_burst = cfg->max_burst;
-	L->vbytes = (c->cfg.flags & GCL_CFG_VERDICT4) ? 4 : 8;
+	L->vbytes = verdict_bytes(c);
 	const uint64_t mb = align16(cfg->max_burst);
 	LoopParams &lp = L->lp;
 	lp.off_offs = 64;
@@ -2251,7 +2276,7 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 	lp.counts = (unsigned long long *)cfg->counts;
 	lp.stats = (unsigned long long *)cfg->stats;
 	lp.max_rt = c->cfg.max_runtimes;
-	lp.cflags = c->cfg.flags;
+	lp.cflags = kernel_cflags(c);
 	lp.default_flags = c->cfg.default_olflags;
 	const unsigned hf = hipHostMallocCoherent | hipHostMallocMapped;
 	int ret = -ENOMEM;
@@ -2391,7 +2416,10 @@ extern "C" int gcl_rxloop_wait(struct gcl_rxloop *L, int64_t ticket, void *verdi
 	if (verdicts_out) {
 		const uint32_t n = (uint32_t)(h->word >> 11) & 0x1FFF;
 		const LoopRec *r = loop_recs(L, h);
-		if (L->vbytes == 4) {
+		if (L->vbytes == 2) {
+			for (uint32_t i = 0; i < n; i++)
+				((uint16_t *)verdicts_out)[i] = (uint16_t)r[i].vlo;
+		} else if (L->vbytes == 4) {
 			for (uint32_t i = 0; i < n; i++)
 				((uint32_t *)verdicts_out)[i] = r[i].vlo;
 		} else {

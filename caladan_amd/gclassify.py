@@ -25,6 +25,9 @@ HASH_NIC, HASH_JENKINS, HASH_TOEPLITZ = 0, 1, 2
 HASH_MODES = {"nic": HASH_NIC, "jenkins": HASH_JENKINS, "toeplitz": HASH_TOEPLITZ}
 
 CFG_AZURE_ARP, CFG_HASH16, CFG_PROFILE, CFG_TRANS_HASH, CFG_VERDICT4 = 0x1, 0x2, 0x4, 0x8, 0x10
+CFG_VERDICT2 = 0x20
+# GCL_CFG_VERDICT2: u16 q = uniqid << thread_bits | thread; kind in the top two bits
+V2_Q_MASK, V2_KIND, V2_DELIVER, V2_WAKE, V2_OTHER, V2_QUEUES = 0x3FFF, 0xC000, 0, 0x4000, 0xC000, 0x4000
 PAIR_NEW_READS, PAIR_NEW_WRITES, PAIR_TRIES = 0x1, 0x2, 6
 
 F_RSS_HASH, F_FDIR_ID = 0x01, 0x02
@@ -60,7 +63,8 @@ TRANS_DTYPE = np.dtype([("h5", "<u4"), ("h3", "<u4")])
 class GclCfg(ctypes.Structure):
     _fields_ = [("max_runtimes", ctypes.c_uint32), ("hash_mode", ctypes.c_uint32),
                 ("flags", ctypes.c_uint32), ("default_olflags", ctypes.c_uint8),
-                ("rss_key", ctypes.c_uint8 * 40), ("pad", ctypes.c_uint8 * 3)]
+                ("rss_key", ctypes.c_uint8 * 40), ("thread_bits", ctypes.c_uint8),
+                ("pad", ctypes.c_uint8 * 2)]
 
 
 class GclBatch(ctypes.Structure):
@@ -204,6 +208,9 @@ def _load():
                                    ctypes.POINTER(GclHostOps), vp]),
         "gcl_host_deliver4": (u64, [vp, u32, vp, i32, vp, vp, vp, vp, ctypes.c_uint8, vp, u64,
                                     ctypes.POINTER(GclHostOps), vp]),
+        "gcl_host_deliver2": (u64, [vp, u32, vp, i32, vp, ctypes.c_uint8, vp, vp, vp,
+                                    ctypes.c_uint8, vp, u64, ctypes.POINTER(GclHostOps), vp]),
+        "gcl_verdict2_to4": (ctypes.c_uint32, [ctypes.c_uint16, ctypes.c_uint8]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -408,21 +415,38 @@ def generate(workload, n, stride, nruntimes, frames, olflags=None, rss=None, see
            "gcl_generate")
 
 
+def verdict_bytes(flags):
+    return 2 if flags & CFG_VERDICT2 else 4 if flags & CFG_VERDICT4 else 8
+
+
+def verdict_dtype(vbytes):
+    return {2: np.dtype("<u2"), 4: VERDICT4_DTYPE, 8: VERDICT_DTYPE}[vbytes]
+
+
+def thread_bits_for(max_runtimes, max_threads):
+    """Smallest GclCfg.thread_bits that holds @max_threads kthreads per runtime;
+    None when max_runtimes << thread_bits would exceed the 2-byte verdict."""
+    tb = max(0, (int(max_threads) - 1).bit_length())
+    return tb if tb <= 8 and (max_runtimes << tb) <= V2_QUEUES else None
+
+
 class Classifier:
     """One gcl_ctx: the GPU side of one dataplane (iokernel/dpdk.c:276-280)."""
 
     def __init__(self, device=0, max_runtimes=16, hash_mode=HASH_JENKINS, flags=0,
-                 default_olflags=F_RSS_HASH | F_IP_CKSUM_GOOD, rss_key=CALADAN_RSS_KEY):
+                 default_olflags=F_RSS_HASH | F_IP_CKSUM_GOOD, rss_key=CALADAN_RSS_KEY,
+                 thread_bits=0):
         if isinstance(hash_mode, str):
             hash_mode = HASH_MODES[hash_mode]
         cfg = GclCfg(max_runtimes=max_runtimes, hash_mode=hash_mode, flags=flags,
-                     default_olflags=default_olflags)
+                     default_olflags=default_olflags, thread_bits=thread_bits)
         key = bytes(rss_key)[:40].ljust(40, b"\0")
         for i in range(40):
             cfg.rss_key[i] = key[i]
         self.cfg = cfg
         self.max_runtimes = max_runtimes
-        self.vbytes = 4 if flags & CFG_VERDICT4 else 8  # bytes per verdict
+        self.vbytes = verdict_bytes(flags)  # bytes per verdict
+        self.thread_bits = thread_bits
         self._ctx = ctypes.c_void_p()
         _check(lib.gcl_open(device, ctypes.byref(cfg), ctypes.byref(self._ctx)), "gcl_open")
 
@@ -546,8 +570,7 @@ class RxLoop:
 
     def wait(self, ticket, n, spin_ns=2_000_000_000):
         """Verdicts of a burst of @n packets (numpy structured array)."""
-        dt = VERDICT4_DTYPE if self.clf.vbytes == 4 else VERDICT_DTYPE
-        out = np.zeros(n, dtype=dt)
+        out = np.zeros(n, dtype=verdict_dtype(self.clf.vbytes))
         ret = lib.gcl_rxloop_wait(self._h, ticket, out.ctypes.data, spin_ns)
         if ret:
             raise OSError(-ret, f"gcl_rxloop_wait: {os.strerror(-ret)}")

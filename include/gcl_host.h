@@ -109,6 +109,23 @@ uint64_t gcl_host_deliver4(struct gcl_host_proc *const *clients_by_id, uint32_t 
                            uint8_t default_olflags, const uint64_t *shmptr, uint64_t n,
                            const struct gcl_host_ops *ops, uint64_t *stats);
 
+/* gcl_verdict2_to4 - widen a GCL_CFG_VERDICT2 verdict of a context opened
+ * with @thread_bits to the gcl_verdict4 the same packet gets under
+ * GCL_CFG_VERDICT4 (GCL_ACT_F_FDIR aside, which the 2-byte form drops). */
+struct gcl_verdict4 gcl_verdict2_to4(uint16_t v, uint8_t thread_bits);
+
+/*
+ * gcl_host_deliver2 - gcl_host_deliver4 over 2-byte verdicts: the same
+ * replay, packet by packet, of @v widened by gcl_verdict2_to4.  The DELIVER
+ * fast path reads the destination ring straight from the queue index.
+ */
+uint64_t gcl_host_deliver2(struct gcl_host_proc *const *clients_by_id, uint32_t max_runtimes,
+                           struct gcl_host_proc *const *clients, int nr_clients,
+                           const uint16_t *v, uint8_t thread_bits, const uint32_t *bcast_hash,
+                           const uint16_t *pkt_len, const uint8_t *olflags,
+                           uint8_t default_olflags, const uint64_t *shmptr, uint64_t n,
+                           const struct gcl_host_ops *ops, uint64_t *stats);
+
 #ifdef __cplusplus
 }
 #endif

@@ -87,6 +87,9 @@ enum gcl_hash_mode {
                                    demux hashes (gcl_classify_ex, struct gcl_trans) */
 #define GCL_CFG_VERDICT4   0x10 /* write 4-byte struct gcl_verdict4 instead of
                                    struct gcl_verdict (see there) */
+#define GCL_CFG_VERDICT2   0x20 /* write 2-byte queue verdicts (gcl_verdict2 below);
+                                   needs cfg.thread_bits, excludes VERDICT4 and
+                                   TRANS_HASH */
 
 struct gcl_cfg {
 	uint32_t max_runtimes;    /* uniqids must be < max_runtimes (<= GCL_MAX_PROC) */
@@ -94,7 +97,10 @@ struct gcl_cfg {
 	uint32_t flags;           /* GCL_CFG_* */
 	uint8_t  default_olflags; /* flags of every packet when gcl_batch.olflags == NULL */
 	uint8_t  rss_key[40];     /* Toeplitz key (NIC key, dpdk.c:219-228) */
-	uint8_t  pad[3];
+	uint8_t  thread_bits;     /* GCL_CFG_VERDICT2: kthread queues per runtime are
+	                             1 << thread_bits (thread_count may not exceed it),
+	                             and max_runtimes << thread_bits <= GCL_V2_QUEUES */
+	uint8_t  pad[2];
 };
 
 /* One batch of received frames, resident in device memory. */
@@ -163,6 +169,25 @@ struct gcl_verdict4 {
 	                     WAKE: hash % thread_count; otherwise GCL_NO_THREAD */
 	uint8_t  action;  /* as gcl_verdict */
 };
+
+/*
+ * 2-byte verdict (GCL_CFG_VERDICT2): a u16 per packet naming a kthread queue
+ * q = uniqid << thread_bits | thread, one flat index over every runtime's
+ * rxq (&p->threads[thread].rxq, defs.h:244).
+ *   DELIVER (any flags)  q of flow_tbl[hash % thread_count]
+ *   WAKE                 GCL_V2_WAKE | uniqid << thread_bits | hash % thread_count
+ *                        (the flow_tbl slot, as gcl_verdict4's WAKE)
+ *   every other action   GCL_V2_OTHER | action (DROP_*, BROADCAST, ARP_RESPOND)
+ * It drops what gcl_verdict4 keeps beyond that: GCL_ACT_F_FDIR, which the
+ * host never reads (RX_FLOW_TAG_MATCH is counted on the device).  Half the
+ * verdict stores of the 4-byte form; gcl_verdict2_to4 (gcl_host.h) widens one.
+ */
+#define GCL_V2_QUEUES   0x4000
+#define GCL_V2_Q_MASK   0x3FFF
+#define GCL_V2_KIND     0xC000
+#define GCL_V2_DELIVER  0x0000
+#define GCL_V2_WAKE     0x4000
+#define GCL_V2_OTHER    0xC000
 
 /*
  * Counter slots; indices 0..5 keep the order of the reference enum

@@ -165,3 +165,14 @@ def to_verdict4(v, thread_count):
     for i in np.nonzero((v["action"] & 0x3F) == 1)[0]:
         out["thread"][i] = int(v["hash"][i]) % int(thread_count[int(v["uniqid"][i])])
     return out
+
+
+def to_verdict2(v, thread_count, thread_bits):
+    """8-B verdicts -> the GCL_CFG_VERDICT2 form (include/gclassify.h): u16
+    q = uniqid << thread_bits | thread for DELIVER, 0x4000 | q (q holding
+    the flow_tbl slot) for WAKE, 0xC000 | action otherwise."""
+    v4 = to_verdict4(v, thread_count)
+    act = v4["action"].astype(np.uint32) & 0x3F
+    q = v4["uniqid"].astype(np.uint32) << thread_bits | v4["thread"].astype(np.uint32)
+    out = np.where(act == 0, q, np.where(act == 1, 0x4000 | q, 0xC000 | act))
+    return out.astype(np.uint16)

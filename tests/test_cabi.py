@@ -280,11 +280,11 @@ def test_host_deliver_broadcast_and_arp(g):
 
 
 def test_host_deliver4_matches_deliver(g, orc):
-    """Compact verdicts replay exactly like 8-B ones: same rings, counters and
+    """Compact verdicts (4 and 2 bytes) replay exactly like 8-B ones: same rings, counters and
     callbacks in the same order with the same packet indices (polls, ownership
     records, frees, ARP responses), including wakes that change the flow_tbl
     mid-batch and broadcasts fanned out with the caller's hashes."""
-    from tests.rxcases import fuzz_batch, random_runtimes, to_verdict4
+    from tests.rxcases import fuzz_batch, random_runtimes, to_verdict2, to_verdict4
     rng = np.random.default_rng(12)
     R = 64
     rts = random_runtimes(rng, R, 24, max_threads=6)
@@ -296,6 +296,7 @@ def test_host_deliver4_matches_deliver(g, orc):
     v, _, _ = t.classify(frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir_hi=fdir, frames_len=flen)
     assert ((v["action"] & 0x3F) == g.ACT_WAKE).any() and ((v["action"] & 0x3F) == g.ACT_BROADCAST).any()
     v4 = to_verdict4(v, {r["uniqid"]: r["thread_count"] for r in rts})
+    v2 = to_verdict2(v, {r["uniqid"]: r["thread_count"] for r in rts}, 3)
     pkt_len = rng.integers(60, 1515, size=n).astype(np.uint16)
     shm = offs.astype(np.uint64)
     bhash = rss.astype(np.uint32)  # NIC mode: the hash is hash.rss whatever the flags
@@ -342,7 +343,12 @@ def test_host_deliver4_matches_deliver(g, orc):
         ops.sched_add_core, ops.free_pkt, ops.refcnt_update = add_core, free_pkt, refcnt
         ops.owned, ops.enable_poll, ops.arp_respond = owned, poll, arp
         stats = np.zeros(8, dtype=np.uint64)
-        if compact:
+        if compact == 2:
+            d = g.lib.gcl_host_deliver2(by_id, R, clients, len(procs), v2.ctypes.data, 3,
+                                        bhash.ctypes.data, pkt_len.ctypes.data, olf.ctypes.data,
+                                        0x09, shm.ctypes.data, n, ctypes.byref(ops),
+                                        stats.ctypes.data)
+        elif compact:
             d = g.lib.gcl_host_deliver4(by_id, R, clients, len(procs), v4.ctypes.data,
                                         bhash.ctypes.data, pkt_len.ctypes.data, olf.ctypes.data,
                                         0x09, shm.ctypes.data, n, ctypes.byref(ops),
@@ -353,10 +359,11 @@ def test_host_deliver4_matches_deliver(g, orc):
                                        shm.ctypes.data, n, ctypes.byref(ops), stats.ctypes.data)
         return d, list(stats), events, {k: r.drain() for k, r in rings.items()}
 
-    full, compact = run(False), run(True)
+    full, compact, compact2 = run(False), run(True), run(2)
     kinds = {e[0] for e in full[2]}
     assert full[0] > 0 and {"wake", "own", "poll", "free", "ref", "arp"} <= kinds, kinds
     assert full == compact
+    assert full == compact2
 
 
 @pytest.mark.parametrize("meta", ["all", "no_olflags", "none"])
@@ -432,3 +439,41 @@ def test_rxloop_rejects_bad_args(g):
     assert g.lib.gcl_rxloop_stop(None) == -22
     assert g.lib.gcl_rxloop_drive(None, 1, 4096, 1, 1, None, None) == -22
     assert ctypes.sizeof(g.GclRxloopCfg) == 56
+
+
+def test_verdict2_widening(g, orc):
+    """gcl_verdict2_to4 inverts the 2-byte encoding: every oracle verdict of a
+    fuzz batch, narrowed to u16 and widened again, is its gcl_verdict4 minus
+    the GCL_ACT_F_FDIR / F_TRANS flags."""
+    from tests.rxcases import fuzz_batch, random_runtimes, to_verdict2, to_verdict4
+    rng = np.random.default_rng(14)
+    for R, tb in [(64, 4), (1024, 4), (16, 0), (16, 8)]:
+        rts = random_runtimes(rng, R, min(R, 40), max_threads=1 << tb)
+        frames, flen, offs, olf, rss, fdir, hint = fuzz_batch(rng, 2000, rts, R)
+        t = orc.Tables(R, 0, 0x1, 0x09)
+        for r in rts:
+            assert t.runtime_set(r["uniqid"], r["ip"], r["thread_count"], r["active"], r["flow_tbl"]) == 0
+        v, _, _ = t.classify(frames, 2000, 0, offs=offs, olflags=olf, rss=rss, fdir_hi=fdir,
+                             frames_len=flen, dst_hint=hint)
+        tc = {r["uniqid"]: r["thread_count"] for r in rts}
+        v4, v2 = to_verdict4(v, tc), to_verdict2(v, tc, tb)
+        assert len(set((v4["action"] & 0x3F).tolist())) >= 4
+        w = np.array([g.lib.gcl_verdict2_to4(int(x), tb) for x in v2], dtype=np.uint32)
+        assert (w & 0xFFFF == v4["uniqid"]).all()
+        assert (w >> 16 & 0xFF == v4["thread"]).all()
+        assert (w >> 24 == v4["action"] & 0x3F).all()
+
+
+def test_open_rejects_bad_verdict2_cfg(g):
+    """Checked before the device: past 16 Ki queues, thread_bits > 8, or
+    combined with VERDICT4 / TRANS_HASH."""
+    ctx = ctypes.c_void_p()
+    for flags, R, tb in [(g.CFG_VERDICT2, 4096, 3), (g.CFG_VERDICT2, 16, 9),
+                         (g.CFG_VERDICT2, 2048, 4),
+                         (g.CFG_VERDICT2 | g.CFG_VERDICT4, 16, 2),
+                         (g.CFG_VERDICT2 | g.CFG_TRANS_HASH, 16, 2)]:
+        cfg = g.GclCfg(max_runtimes=R, hash_mode=1, flags=flags, thread_bits=tb)
+        assert g.lib.gcl_open(0, ctypes.byref(cfg), ctypes.byref(ctx)) == -22, (flags, R, tb)
+    assert g.thread_bits_for(16, 8) == 3 and g.thread_bits_for(1024, 4) == 2
+    assert g.thread_bits_for(1024, 16) == 4 and g.thread_bits_for(1024, 17) is None
+    assert g.thread_bits_for(16, 1) == 0 and g.thread_bits_for(16, 256) == 8

@@ -4,7 +4,7 @@ import numpy as np
 import pytest
 
 from tests.rxcases import (apply_runtimes, apply_seeds, fuzz_batch, random_runtimes, scenario_batch,
-                           to_verdict4,
+                           to_verdict2, to_verdict4,
                            scenario_sets, scenario_trans)
 
 pytestmark = pytest.mark.gpu
@@ -38,7 +38,7 @@ def gpu_run(g, clf, frames, n, stride=0, offs=None, olflags=None, rss=None, fdir
                  frames_len=frames_len,
                  dst_hint=dev(hint.view(np.int32)) if hint is not None else None)
     torch.cuda.synchronize()
-    res = (v.cpu().numpy().view(g.VERDICT_DTYPE if clf.vbytes == 8 else g.VERDICT4_DTYPE), c.cpu().numpy().astype(np.uint64),
+    res = (v.cpu().numpy().view(g.verdict_dtype(clf.vbytes)), c.cpu().numpy().astype(np.uint64),
            s.cpu().numpy().astype(np.uint64))
     if trans:
         res += (tr.cpu().numpy().view(g.TRANS_DTYPE),)
@@ -155,6 +155,51 @@ def test_gpu_fuzz_verdict4(g, orc, mode, flags, max_rt):
     exp = to_verdict4(ve, {r["uniqid"]: r["thread_count"] for r in rts})
     assert_same(v, exp, f"verdict4 mode={mode} flags={flags} R={max_rt}")
     assert (c == ce).all() and (st == se).all()
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("flags", [1, 2])
+@pytest.mark.parametrize("max_rt", [16, 1024])
+def test_gpu_fuzz_verdict2(g, orc, mode, flags, max_rt):
+    """GCL_CFG_VERDICT2: one u16 kthread-queue index per packet (WAKE with
+    its flow_tbl slot), up to the full 16 Ki queues at R=1024, 16 threads."""
+    rng = np.random.default_rng(7100 + 1000 * mode + 10 * flags + max_rt)
+    rts = random_runtimes(rng, max_rt, min(max_rt, 40 if max_rt == 16 else 300))
+    for r in rts[:2]:  # WAKE verdicts in every case
+        r.update(active=0, active_idx=[], flow_tbl=None)
+    n = 5000
+    frames, flen, offs, olf, rss, fdir, hint = fuzz_batch(rng, n, rts, max_rt)
+    key = bytes(rng.integers(0, 256, size=40, dtype=np.uint8))
+    tb = g.thread_bits_for(max_rt, 16)
+    assert tb == 4
+    t = orc.Tables(max_rt, mode, flags, 0x09, key)
+    apply_runtimes(t, rts)
+    clf = g.Classifier(0, max_rt, mode, flags | g.CFG_VERDICT2, 0x09, key, thread_bits=tb)
+    apply_runtimes(clf, rts)
+    ve, ce, se = t.classify(frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir_hi=fdir,
+                            frames_len=flen, dst_hint=hint)
+    v, c, st = gpu_run(g, clf, frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir=fdir,
+                       frames_len=flen, hint=hint)
+    assert ((ve["action"] & 0x3F) == g.ACT_WAKE).any()
+    exp = to_verdict2(ve, {r["uniqid"]: r["thread_count"] for r in rts}, tb)
+    assert_same(v, exp, f"verdict2 mode={mode} flags={flags} R={max_rt}")
+    assert (c == ce).all() and (st == se).all()
+
+
+def test_gpu_verdict2_limits(g):
+    """Runtimes with more kthreads than 1 << thread_bits are refused; a
+    configuration past 16 Ki queues, or combined with VERDICT4 or TRANS_HASH,
+    does not open."""
+    clf = g.Classifier(0, 64, 1, g.CFG_VERDICT2, thread_bits=3)
+    assert clf.runtime_set(5, 0x0A000001, 8, 8, list(range(8))) == 0
+    with pytest.raises(OSError):
+        clf.runtime_set(6, 0x0A000002, 9, 0, None)
+    for flags, R, tb in [(g.CFG_VERDICT2, 4096, 3), (g.CFG_VERDICT2, 16, 9),
+                         (g.CFG_VERDICT2 | g.CFG_VERDICT4, 16, 2),
+                         (g.CFG_VERDICT2 | g.CFG_TRANS_HASH, 16, 2)]:
+        with pytest.raises(OSError):
+            g.Classifier(0, R, 1, flags, thread_bits=tb)
+    g.Classifier(0, 4096, 1, g.CFG_VERDICT2, thread_bits=2).close()
 
 
 @pytest.mark.parametrize("wl,stride,R", [(0, 64, 16), (1, 1536, 1024), (2, 9216, 16)])
@@ -410,6 +455,28 @@ def test_gpu_end_to_end_verdict4(g, orc, mode):
     clf.classify_host(hf, n, 64, verdicts=hv, counts=counts, stats=stats, mode=mode,
                       chunk=65536 + 17, nstreams=3)
     assert_same(hv.numpy().view(g.VERDICT4_DTYPE), to_verdict4(ve, [T] * R), f"e2e4 mode={mode}")
+    assert (counts == ce).all() and (stats == se).all()
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_gpu_end_to_end_verdict2(g, orc, mode):
+    """Both transports with 2-byte verdicts, chunks of odd length."""
+    n, R, T = 300000, 16, 8
+    frames, olf, rss = orc.generate(0, n, 64, R)
+    t = orc.Tables(R, 1, 0, 0x09)
+    clf = g.Classifier(0, R, 1, g.CFG_VERDICT2, thread_bits=3)
+    for r in range(R):
+        fl = orc.steer_flows(T, list(range(r % T)))
+        t.runtime_set(r, orc.runtime_ip(r), T, r % T, fl if r % T else None)
+        clf.runtime_set(r, g.runtime_ip(r), T, r % T, fl if r % T else None)
+    ve, ce, se = t.classify(frames, n, 64)
+    hf = torch.from_numpy(frames).pin_memory()
+    hv = torch.zeros(n * 2, dtype=torch.uint8).pin_memory()
+    counts = np.zeros(R, dtype=np.uint64)
+    stats = np.zeros(8, dtype=np.uint64)
+    clf.classify_host(hf, n, 64, verdicts=hv, counts=counts, stats=stats, mode=mode,
+                      chunk=65536 + 17, nstreams=3)
+    assert_same(hv.numpy().view(np.uint16), to_verdict2(ve, [T] * R, 3), f"e2e2 mode={mode}")
     assert (counts == ce).all() and (stats == se).all()
 
 

@@ -9,7 +9,7 @@ import time
 import numpy as np
 import pytest
 
-from tests.rxcases import apply_runtimes, fuzz_batch, random_runtimes, to_verdict4
+from tests.rxcases import apply_runtimes, fuzz_batch, random_runtimes, to_verdict2, to_verdict4
 
 pytestmark = pytest.mark.gpu
 
@@ -28,8 +28,8 @@ def bursts(n, size=64):
     return [(s, min(n, s + size)) for s in range(0, n, size)]
 
 
-def want(ve, tc, v4):
-    return to_verdict4(ve, tc) if v4 else ve
+def want(ve, tc, vb, tb=4):
+    return to_verdict2(ve, tc, tb) if vb == 2 else to_verdict4(ve, tc) if vb == 4 else ve
 
 
 def tc_map(rts, max_rt):
@@ -39,26 +39,27 @@ def tc_map(rts, max_rt):
     return tc
 
 
-LOOP_CASES = [(m, v4, 0, False) for m in (0, 1, 2) for v4 in (False, True)] + \
-    [(m, False, fl, False) for m in (0, 1, 2) for fl in (1, 2)] + \
-    [(0, False, 1, True), (1, True, 0, True), (2, False, 2, True)]
+LOOP_CASES = [(m, vb, 0, False) for m in (0, 1, 2) for vb in (8, 4, 2)] + \
+    [(m, 8, fl, False) for m in (0, 1, 2) for fl in (1, 2)] + \
+    [(0, 8, 1, True), (1, 4, 0, True), (2, 8, 2, True), (1, 2, 1, True)]
 
 
-@pytest.mark.parametrize("mode,v4,flags,inline", LOOP_CASES)
-def test_rxloop_fuzz_vs_oracle(g, orc, mode, v4, flags, inline):
-    """flags: 0 plain, 1 Azure ARP mode (GCL_CFG_AZURE_ARP), 2 16-bit hash;
+@pytest.mark.parametrize("mode,vb,flags,inline", LOOP_CASES)
+def test_rxloop_fuzz_vs_oracle(g, orc, mode, vb, flags, inline):
+    """vb: verdict bytes (8 gcl_verdict, 4 VERDICT4, 2 VERDICT2);
+    flags: 0 plain, 1 Azure ARP mode (GCL_CFG_AZURE_ARP), 2 16-bit hash;
     inline: header granules copied into the ring slot (GCL_LOOP_INLINE_HDRS),
     including the frames that straddle the end of the region."""
-    rng = np.random.default_rng(7000 + 10 * mode + v4 + 100 * flags + 1000 * inline)
+    rng = np.random.default_rng(7000 + 10 * mode + vb + 100 * flags + 1000 * inline)
     max_rt = 1024 if mode == 1 else 16
     rts = random_runtimes(rng, max_rt, 300 if max_rt == 1024 else 12)
     n = 3000
     frames, flen, offs, olf, rss, fdir, hint = fuzz_batch(rng, n, rts, max_rt)
     key = bytes(rng.integers(0, 256, size=40, dtype=np.uint8))
-    cflags = (g.CFG_VERDICT4 if v4 else 0) | flags
+    cflags = {8: 0, 4: g.CFG_VERDICT4, 2: g.CFG_VERDICT2}[vb] | flags
     t = orc.Tables(max_rt, mode, flags, 0x09, key)
     apply_runtimes(t, rts)
-    clf = g.Classifier(0, max_rt, mode, cflags, 0x09, key)
+    clf = g.Classifier(0, max_rt, mode, cflags, 0x09, key, thread_bits=4)
     apply_runtimes(clf, rts)
     ve, ce, se = t.classify(frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir_hi=fdir,
                             frames_len=flen, dst_hint=hint)
@@ -77,7 +78,7 @@ def test_rxloop_fuzz_vs_oracle(g, orc, mode, v4, flags, inline):
     finally:
         loop.stop()
         g.host_unregister(frames)
-    w = want(ve, tc_map(rts, max_rt), v4)
+    w = want(ve, tc_map(rts, max_rt), vb)
     bad = np.nonzero(got != w)[0]
     assert not len(bad), f"{len(bad)} differ, first {bad[0]}: {got[bad[0]]} vs {w[bad[0]]}"
     torch.cuda.synchronize()
