@@ -1852,8 +1852,11 @@ __global__ void __launch_bounds__(256) pair_probe_kernel(const uint8_t *rd, uint
 double pair_probe(const uint8_t *rd, size_t rd_bytes, uint32_t *wr, size_t wr_bytes, hipStream_t s,
                   hipEvent_t e0, hipEvent_t e1, int cus)
 {
-	const uint64_t ntiles = std::min<size_t>(rd_bytes, 512ull << 20) / (256 * 64);
-	const uint64_t wtiles = std::min<size_t>(wr_bytes, 32ull << 20) / (256 * 4);
+	/* the whole of both buffers, as the kernel walks them (a 2 GiB frame
+	 * pool against a 128 MiB verdict ring is 0.35-0.4 ms): a probe of the
+	 * first 512 MiB against the first 32 MiB missed the class on some boxes */
+	const uint64_t ntiles = std::min<size_t>(rd_bytes, 4ull << 30) / (256 * 64);
+	const uint64_t wtiles = std::min<size_t>(wr_bytes, 256ull << 20) / (256 * 4);
 	if (!ntiles || !wtiles)
 		return -1;
 	double best = 1e30;
@@ -1875,8 +1878,8 @@ double pair_probe(const uint8_t *rd, size_t rd_bytes, uint32_t *wr, size_t wr_by
 } /* namespace */
 
 /* The class gap: same-class pairs measured 13-18% slower than cross-class
- * ones (406 vs 343 us classify, 390 vs 354 us probe shape); run-to-run noise
- * of one probe is under 1.5%. */
+ * ones (406 vs 343 us classify, 390 vs 354 us in the probe's shape at full
+ * size); run-to-run noise of one probe is under 1.5%. */
 constexpr double kPairGap = 0.06;
 
 extern "C" int gcl_dev_alloc_paired(int hip_device, size_t bytes, const void *partner,
@@ -1904,9 +1907,19 @@ extern "C" int gcl_dev_alloc_paired(int hip_device, size_t bytes, const void *pa
 	hipEventCreate(&e1);
 	const bool dbg = getenv("GCL_PAIR_DEBUG") != nullptr;
 	std::vector<std::pair<void *, double>> cand;
+	std::vector<void *> spacers;
 	int ret = 0;
 	for (int i = 0; i < GCL_PAIR_TRIES; i++) {
 		void *p = nullptr;
+		if (i && i % GCL_PAIR_RUN == 0) { /* one class so far: step past the run */
+			void *sp = nullptr;
+			if (hipMalloc(&sp, 2 * bytes) == hipSuccess)
+				spacers.push_back(sp);
+			else
+				(void)hipGetLastError();
+			if (dbg)
+				fprintf(stderr, "gcl_dev_alloc_paired: spacer %p\n", sp);
+		}
 		if (hipMalloc(&p, bytes) != hipSuccess) {
 			(void)hipGetLastError();
 			break;
@@ -1940,6 +1953,8 @@ extern "C" int gcl_dev_alloc_paired(int hip_device, size_t bytes, const void *pa
 	for (size_t i = 0; i < cand.size(); i++)
 		if (ret || i != best)
 			hipFree(cand[i].first);
+	for (void *sp : spacers)
+		hipFree(sp);
 	hipEventDestroy(e0);
 	hipEventDestroy(e1);
 	hipStreamDestroy(s);

@@ -28,7 +28,7 @@ CFG_AZURE_ARP, CFG_HASH16, CFG_PROFILE, CFG_TRANS_HASH, CFG_VERDICT4 = 0x1, 0x2,
 CFG_VERDICT2 = 0x20
 # GCL_CFG_VERDICT2: u16 q = uniqid << thread_bits | thread; kind in the top two bits
 V2_Q_MASK, V2_KIND, V2_DELIVER, V2_WAKE, V2_OTHER, V2_QUEUES = 0x3FFF, 0xC000, 0, 0x4000, 0xC000, 0x4000
-PAIR_NEW_READS, PAIR_NEW_WRITES, PAIR_TRIES = 0x1, 0x2, 6
+PAIR_NEW_READS, PAIR_NEW_WRITES, PAIR_TRIES, PAIR_RUN = 0x1, 0x2, 12, 3
 
 F_RSS_HASH, F_FDIR_ID = 0x01, 0x02
 F_IP_CKSUM_MASK, F_IP_CKSUM_UNKNOWN, F_IP_CKSUM_BAD = 0x0C, 0x00, 0x04

@@ -418,22 +418,27 @@ int gcl_dev_free(void *p);
  * slower when the two buffers fall in the same physical placement class
  * (measured: DESIGN.md §4 "Buffer placement", profiles/r01_pair_*.jsonl).
  * The class cannot be read from a virtual address, so this allocates a
- * candidate, times a short read+write probe of the classify kernel's access
- * shape against @partner, and keeps the first candidate whose probe differs
+ * candidate, times a read+write probe of the classify kernel's access shape
+ * over the whole of both buffers (up to 4 GiB read, 256 MiB written) against
+ * @partner, and keeps the first candidate whose probe differs
  * from an earlier one by more than the class gap (the faster of the two),
- * trying at most GCL_PAIR_TRIES candidates; losers are freed.
+ * trying at most GCL_PAIR_TRIES candidates; losers are freed.  Classes come
+ * in runs of consecutive allocations (up to six 2-GiB buffers in a row were
+ * measured), so after every GCL_PAIR_RUN candidates of one class a spacer
+ * of twice @bytes is allocated to step past the run; spacers are freed too.
  *
  * GCL_PAIR_NEW_READS: the new buffer is the one stream-read (frames) and
  *                     @partner the one written (verdicts);
  * GCL_PAIR_NEW_WRITES: the reverse.
- * The probe WRITES to the written side's first min(bytes, 32 MiB): call it
+ * The probe WRITES to the written side's first min(bytes, 256 MiB): call it
  * before that buffer holds data.  @probe_us (optional, 2 doubles) returns the
  * chosen and the slowest probe time in microseconds.
  * Returns 0, -EINVAL, -ENODEV, -ENOMEM or -EIO.
  */
 #define GCL_PAIR_NEW_READS  0x1
 #define GCL_PAIR_NEW_WRITES 0x2
-#define GCL_PAIR_TRIES      6
+#define GCL_PAIR_TRIES      12
+#define GCL_PAIR_RUN        3
 int gcl_dev_alloc_paired(int hip_device, size_t bytes, const void *partner, size_t partner_bytes,
                          uint32_t flags, void **out, double *probe_us);
 
