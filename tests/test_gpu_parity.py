@@ -577,3 +577,56 @@ def test_gpu_dev_alloc_paired(g, orc):
     assert (s.cpu().numpy().astype(np.uint64) == se).all()
     for b in (ring2, pool, ring):
         b.free()
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_gpu_tables_past_lds(g, orc, mode):
+    """1500 runtimes of GCL_MAX_PROC = 4096, thread counts up to NCPU = 256
+    (control.c:233): ~380 KiB of flow tables, past the 96 KiB LDS budget, so
+    the kernel reads its tables from HBM."""
+    rng = np.random.default_rng(8100 + mode)
+    R = 4096
+    rts = random_runtimes(rng, R, 1500, max_threads=256)
+    assert sum(r["thread_count"] for r in rts) * 2 > 96 * 1024
+    n = 20000
+    frames, flen, offs, olf, rss, fdir, hint = fuzz_batch(rng, n, rts, R)
+    key = bytes(rng.integers(0, 256, size=40, dtype=np.uint8))
+    t = orc.Tables(R, mode, 0, 0x09, key)
+    apply_runtimes(t, rts)
+    clf = g.Classifier(0, R, mode, 0, 0x09, key)
+    apply_runtimes(clf, rts)
+    ve, ce, se = t.classify(frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir_hi=fdir,
+                            frames_len=flen, dst_hint=hint)
+    v, c, st = gpu_run(g, clf, frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir=fdir,
+                       frames_len=flen, hint=hint)
+    assert_same(v, ve, f"tables past LDS mode={mode}")
+    assert (c == ce).all() and (st == se).all()
+    # the persistent loop keeps its tables in LDS: it refuses these
+    g.host_register(frames)
+    try:
+        with pytest.raises(OSError) as e:
+            clf.rxloop(frames)
+        assert e.value.errno == 7  # E2BIG
+    finally:
+        g.host_unregister(frames)
+
+
+def test_gpu_tables_in_hbm_forced(g, orc, monkeypatch):
+    """GCL_TUNE_TABLES=1 keeps small tables in HBM too: same verdicts."""
+    rng = np.random.default_rng(8200)
+    R = 64
+    rts = random_runtimes(rng, R, 40)
+    n = 8000
+    frames, flen, offs, olf, rss, fdir, hint = fuzz_batch(rng, n, rts, R)
+    t = orc.Tables(R, 1, 0, 0x09)
+    apply_runtimes(t, rts)
+    monkeypatch.setenv("GCL_TUNE_TABLES", "1")
+    clf = g.Classifier(0, R, 1, 0, 0x09)
+    monkeypatch.delenv("GCL_TUNE_TABLES")
+    apply_runtimes(clf, rts)
+    ve, ce, se = t.classify(frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir_hi=fdir,
+                            frames_len=flen, dst_hint=hint)
+    v, c, st = gpu_run(g, clf, frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir=fdir,
+                       frames_len=flen, hint=hint)
+    assert_same(v, ve, "tables forced to HBM")
+    assert (c == ce).all() and (st == se).all()
