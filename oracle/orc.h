@@ -26,7 +26,10 @@
  * this image, so it is not compiled here, and the reference ships no tests or
  * fixtures for it: the decision tree of orc_rx_one_pkt is PARITY UNPINNED by
  * reference outputs (pinned only by those hand-derived fixtures); the hashes
- * it calls are pinned (see DESIGN.md "Oracle").
+ * it calls are pinned (see DESIGN.md "Oracle").  The host post-pass's lrpc
+ * ring and rxq_cmd encoding are pinned against base/lrpc.c and
+ * inc/iokernel/queue.h built from the reference (oracle/ref_host.c,
+ * tests/test_ref_host.py).
  */
 #ifndef ORC_H
 #define ORC_H

@@ -14,6 +14,7 @@ LIB = os.path.join(HERE, "build", "liborc.so")
 LIB_NATIVE = os.path.join(HERE, "build", "liborc_native.so")
 REF_JHASH = os.path.join(HERE, "_ref", "libjhash_ref.so")
 REF_CRC = os.path.join(HERE, "_ref", "libcrc_ref.so")
+REF_HOST = os.path.join(HERE, "_ref", "libhost_ref.so")
 TRANS_DTYPE = np.dtype([("h5", "<u4"), ("h3", "<u4")])
 
 NR_STATS = 8
@@ -108,6 +109,29 @@ def ref_crc():
     l.ref_crc32c_one.argtypes = [ctypes.c_uint32, ctypes.c_uint64]
     l.ref_crc32c_two.restype = ctypes.c_uint32
     l.ref_crc32c_two.argtypes = [ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64]
+    return l
+
+
+def ref_host():
+    """The reference's base/lrpc.c and header-only rx host helpers
+    (oracle/_ref/libhost_ref.so, exported by oracle/ref_host.c), or None."""
+    if not os.path.exists(REF_HOST):
+        return None
+    l = ctypes.CDLL(REF_HOST)
+    vp, u32, u64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64
+    for name, res, args in [
+            ("ref_lrpc_send", ctypes.c_bool, [vp, u64, ctypes.c_ulong]),
+            ("ref_lrpc_recv", ctypes.c_bool, [vp, vp, vp]),
+            ("lrpc_init_out", ctypes.c_int, [vp, vp, ctypes.c_uint, vp]),
+            ("lrpc_init_in", ctypes.c_int, [vp, vp, ctypes.c_uint, vp]),
+            ("ref_lrpc_layout", None, [vp]),
+            ("ref_rxq_cmd", u64, [ctypes.c_uint16, ctypes.c_int]),
+            ("ref_rss_from_txpkt_payload", u64, [u64]),
+            ("ref_txpkt_to_payload", u64, [u64, ctypes.c_uint16]),
+            ("ref_txflag_local_hint", u32, []),
+            ("ref_ncpu", u32, [])]:
+        f = getattr(l, name)
+        f.restype, f.argtypes = res, args
     return l
 
 
