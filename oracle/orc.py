@@ -129,7 +129,11 @@ def ref_host():
             ("ref_rss_from_txpkt_payload", u64, [u64]),
             ("ref_txpkt_to_payload", u64, [u64, ctypes.c_uint16]),
             ("ref_txflag_local_hint", u32, []),
-            ("ref_ncpu", u32, [])]:
+            ("ref_ncpu", u32, []),
+            ("ref_build_frame", ctypes.c_int, [vp, ctypes.c_int, u32, u32, ctypes.c_uint16,
+                                               ctypes.c_uint16, ctypes.c_uint8, ctypes.c_uint16,
+                                               ctypes.c_uint16]),
+            ("ref_net_consts", None, [vp])]:
         f = getattr(l, name)
         f.restype, f.argtypes = res, args
     return l

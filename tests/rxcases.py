@@ -176,3 +176,32 @@ def to_verdict2(v, thread_count, thread_bits):
     q = v4["uniqid"].astype(np.uint32) << thread_bits | v4["thread"].astype(np.uint32)
     out = np.where(act == 0, q, np.where(act == 1, 0x4000 | q, 0xC000 | act))
     return out.astype(np.uint16)
+
+
+def ref_struct_batch(ref, orc, rng, n, R):
+    """@n 64-B frames written by the reference's own inc/net structs
+    (oracle/ref_host.c ref_build_frame): IPv4 UDP/TCP with IHL 5..11 and
+    fragment fields, and ARP requests/replies; 80% to one of @R runtime IPs.
+    Returns (ips, frames[n, 64], want) with want[i] = (uniqid or 0xFFFF,
+    JENKINS hash of the values put into the structs, hit)."""
+    import struct
+    ips = [int(x) for x in rng.choice(1 << 31, size=R, replace=False) + (1 << 30)]
+    frames = np.zeros((n, 64), dtype=np.uint8)
+    want = []
+    for i in range(n):
+        kind = int(rng.integers(0, 3))
+        u = int(rng.integers(0, R))
+        hit = rng.random() < 0.8
+        dst = ips[u] if hit else int(rng.integers(1, 1 << 30))
+        src = int(rng.integers(0, 1 << 32))
+        sp, dp = int(rng.integers(0, 1 << 16)), int(rng.integers(0, 1 << 16))
+        ihl = int(rng.choice([5, 5, 5, 6, 8, 11]))
+        off = int(rng.choice([0, 0, 0, 0x2000, 0x0010, 0x4000]))  # MF, offset, DF
+        op = int(rng.choice([1, 2]))
+        assert ref.ref_build_frame(frames[i].ctypes.data, kind, src, dst, sp, dp, ihl, off, op) == 0
+        if kind == 2 or off & 0x3FFF:
+            h = 0
+        else:
+            h = orc.jhash(struct.pack("<IIHHB", src, dst, dp, sp, 17 if kind == 0 else 6))
+        want.append((u if hit else 0xFFFF, h, hit))
+    return ips, frames, want

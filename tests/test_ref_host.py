@@ -182,3 +182,44 @@ def test_deliver_rings_read_by_reference_consumer(g, ref, orc):
     assert d == sum(len(x) for x in want.values()) > n // 3
     for k, ring in rings.items():
         assert ring.drain(5000) == want[k], k
+
+
+def test_protocol_constants_match_reference(ref):
+    """The kernel's ethertype / ARP opcode constants (include/gclassify.h)
+    are the reference's (ethernet.h:88,94,300, arp.h:42-43)."""
+    import os
+    import re
+    src = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                            "include", "gclassify.h")).read()
+    d = {m.group(1): int(m.group(2), 0)
+         for m in re.finditer(r"#define\s+GCL_(ETHTYPE_\w+|ARP_OP_\w+)\s+(0x[0-9A-Fa-f]+|\d+)", src)}
+    c = (ctypes.c_uint32 * 6)()
+    ref.ref_net_consts(c)
+    assert [d["ETHTYPE_IP"], d["ETHTYPE_ARP"], d["ETHTYPE_IPV6"], d["ARP_OP_REQUEST"],
+            d["ARP_OP_REPLY"]] == list(c)[:5]
+    assert c[5] == 0x3FFF  # IP_MF | IP_OFFMASK: what "is a fragment" tests
+
+
+def test_parse_offsets_match_reference_structs(g, ref, orc):
+    """Frames written through the reference's own struct eth_hdr / ip_hdr /
+    udp_hdr / tcp_hdr / arp_hdr(_ethip) classify as the values put into the
+    structs say: the destination (daddr, or the ARP target) picks the
+    runtime, and the JENKINS flow hash is lookup3 over {saddr, daddr, dport,
+    sport, proto} as set, 0 for fragments and ARP.  The GPU is bit-exact
+    with the oracle (tests/test_gpu_parity.py), so this pins both."""
+    from tests.rxcases import ref_struct_batch
+    rng = np.random.default_rng(16)
+    R, n = 64, 3000
+    ips, frames, want = ref_struct_batch(ref, orc, rng, n, R)
+    t = orc.Tables(R, 1, 0, 0x09)
+    for u, ip in enumerate(ips):
+        assert t.runtime_set(u, ip, 4, 4, [0, 1, 2, 3]) == 0
+    v, _, _ = t.classify(frames.reshape(-1), n, 64)
+    for i, (u, h, hit) in enumerate(want):
+        assert int(v["uniqid"][i]) == u, i
+        if hit:
+            assert int(v["action"][i]) & 0x3F == g.ACT_DELIVER, i
+            assert int(v["hash"][i]) == h, i
+            assert int(v["thread"][i]) == h % 4, i
+        else:
+            assert int(v["action"][i]) & 0x3F == g.ACT_DROP_UNREG, i
