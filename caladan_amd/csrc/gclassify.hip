@@ -689,7 +689,9 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 	extern __shared__ uint4 smem[];
 	uint4 *tile = smem;
 	uint8_t *side_mem = (uint8_t *)(tile + 1024);
-	LoopSide side[2] = {LoopSide(side_mem), LoopSide(side_mem + kLoopSide)};
+	/* the two side-array buffers, picked by arithmetic (an array of
+	 * LoopSide indexed by chunk parity would live in scratch) */
+	auto side = [&](uint32_t b) { return LoopSide(side_mem + (b & 1) * kLoopSide); };
 	uint2 *s_verd = (uint2 *)(side_mem + 2 * kLoopSide);
 	uint32_t *s_ctl = (uint32_t *)(s_verd + 256);
 	uint32_t *hist = s_ctl + 16;
@@ -772,16 +774,16 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 			}
 		};
 		if (L.off_hdr) /* the granules do not wait for the offsets */
-			load_frames(side[0], 0, chunk_m(0));
-		side[0].load(slot, L, fl, 0, chunk_m(0), tid);
+			load_frames(side(0), 0, chunk_m(0));
+		side(0).load(slot, L, fl, 0, chunk_m(0), tid);
 		__syncthreads();
 		if (!L.off_hdr)
-			load_frames(side[0], 0, chunk_m(0));
+			load_frames(side(0), 0, chunk_m(0));
 		for (uint32_t c = 0; c < nch; c++) {
 			const uint32_t m = chunk_m(c), base = 256 * c;
-			LoopSide &cur = side[c & 1];
+			const LoopSide cur = side(c);
 			if (c + 1 < nch)
-				side[(c + 1) & 1].load(slot, L, fl, base + 256, chunk_m(c + 1), tid);
+				side(c + 1).load(slot, L, fl, base + 256, chunk_m(c + 1), tid);
 #pragma unroll
 			for (int j = 0; j < 4; j++) {
 				const int cc = j * 256 + tid;
@@ -789,7 +791,7 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 			}
 			__syncthreads(); /* tile of c and side arrays of c + 1 in LDS */
 			if (c + 1 < nch)
-				load_frames(side[(c + 1) & 1], c + 1, chunk_m(c + 1));
+				load_frames(side(c + 1), c + 1, chunk_m(c + 1));
 			k.n = m;
 			k.offs = cur.offs;
 			k.olflags = (fl & GCL_LOOP_F_OLF) ? cur.olf : nullptr;
@@ -806,7 +808,7 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 				__builtin_amdgcn_raw_buffer_store_b128(
 				        rec, srs, (int)(L.off_verd + sizeof(LoopRec) * (base + tid)), 0, gcl::kSysAux);
 			}
-			__syncthreads(); /* tile and side[c & 1] free again */
+			__syncthreads(); /* tile and side(c) free again */
 		}
 		/* counters of this burst */
 		for (uint32_t i = tid; i < L.max_rt; i += 256)
