@@ -643,6 +643,7 @@ struct LoopParams {
 	uint32_t off_offs, off_olf, off_rss, off_fdir, off_hint, off_verd;
 	const uint8_t *img[2];     /* device views of the two image buffers */
 	const uint32_t *stop;
+	uint32_t *where;           /* host words: XCC_ID + 1 of worker b at [b] (b < 8) */
 	uint64_t lifetime_ticks;   /* s_memrealtime ticks each block may run */
 	const uint8_t *frames;     /* device view of the registered region */
 	uint64_t frames_len;
@@ -699,6 +700,8 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 	const int tid = threadIdx.x;
 	const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + L.lifetime_ticks;
 	const __amdgpu_buffer_rsrc_t frs = gcl::host_rsrc(L.frames, L.frames_len);
+	if (tid == 0 && blockIdx.x < 8) /* which XCD this worker runs on */
+		gcl::st_sys32(&L.where[blockIdx.x], __builtin_amdgcn_s_getreg((3 << 11) | 20) + 1);
 
 	KParams k = {};
 	k.frames = L.frames;
@@ -2150,7 +2153,20 @@ extern "C" int gcl_classify_host(struct gcl_ctx *c, const struct gcl_batch *hb,
  * coherent, mapped host memory; the CPU publishes a slot with a release store
  * of its ticket, the kernel answers with a release store of `done`.
  */
+#include <sys/syscall.h>
 #include <time.h>
+#include <unistd.h>
+
+/* NUMA node of the page holding @p (move_pages with no target nodes only
+ * reports), -1 if unknown */
+static int page_node(const void *p)
+{
+	void *pg = (void *)((uintptr_t)p & ~(uintptr_t)4095);
+	int status = -1;
+	if (!p || syscall(SYS_move_pages, 0, 1ul, &pg, nullptr, &status, 0) != 0)
+		return -1;
+	return status;
+}
 
 struct gcl_rxloop {
 	gcl_ctx *c;
@@ -2305,6 +2321,10 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 		goto fail;
 	memset(L->slots, 0, lp.nslots * lp.slot_bytes);
 	memset(L->ctl, 0, 64);
+	if (getenv("GCL_LOOP_DEBUG"))
+		fprintf(stderr, "gcl_rxloop_start: NUMA node of slots %d, image %d, ctl %d, region %d\n",
+		        page_node(L->slots), page_node(L->img[0]), page_node(L->ctl),
+		        page_node(cfg->region));
 	ret = loop_write_image(L, 0);
 	if (ret)
 		goto fail;
@@ -2322,6 +2342,7 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 	if (hipHostGetDevicePointer(&d, L->ctl, 0) != hipSuccess)
 		goto fail;
 	lp.stop = (const uint32_t *)d;
+	lp.where = (uint32_t *)d + 8;
 	if (hipStreamCreateWithFlags(&L->st, hipStreamNonBlocking) != hipSuccess)
 		goto fail;
 	{
@@ -2456,6 +2477,13 @@ extern "C" int gcl_rxloop_stop(struct gcl_rxloop *L)
 		return -EINVAL;
 	__atomic_store_n(L->ctl, 1u, __ATOMIC_RELEASE);
 	const hipError_t e = hipStreamSynchronize(L->st);
+	if (getenv("GCL_LOOP_DEBUG")) {
+		fprintf(stderr, "gcl_rxloop_stop: workers on XCC");
+		for (int b = 0; b < 8; b++)
+			if (L->ctl[8 + b])
+				fprintf(stderr, " %u", L->ctl[8 + b] - 1);
+		fprintf(stderr, "\n");
+	}
 	hipStreamDestroy(L->st);
 	hipHostFree(L->slots);
 	hipHostFree(L->img[0]);
