@@ -1515,9 +1515,11 @@ static Geometry choose_geometry(const gcl_ctx *c, uint32_t tab_lds, uint32_t his
 		g.bpc_cap = (int)(lds_cu / (256u * 64 + kLdsQueueBytes + hist_bytes + tab_lds));
 		if (g.bpc_cap < 1)
 			g.bpc_cap = 1;
-	} else if (g.threads == 256 && !c->tune_sched) {
-		/* small tables, 4 x 256 lanes: a second tile in flight per block
-		 * measured 1.1-1.7 % faster on udp64 (profiles/r01_cbench_depth_*) */
+	} else if (g.threads <= 512 && !c->tune_sched) {
+		/* a second tile in flight per block: 1.1-1.7 % faster on udp64 at
+		 * 4 x 256 lanes (profiles/r01_cbench_depth_*); at 2 x 512 lanes (the
+		 * 1024-runtime tables) 1 % on the 8 Mi header-split layout, 3.4 % at
+		 * 32 Mi, and no change on tcp1500 (profiles/r01_hsplit_geometry.jsonl) */
 		g.depth = 2;
 	}
 	if (c->tune_threads)

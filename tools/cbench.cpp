@@ -2,6 +2,7 @@
 // torch) and A/B kernel configurations inside one process.
 //
 //   cbench <workload> <steps> [cfg ...]
+// (env CBENCH_N, CBENCH_STRIDE, CBENCH_R override the workload's shape)
 //
 // Each cfg is "ABLATE:GRID:DEPTH:THREADS:BPC:SCHED:V4" (GCL_TUNE_* knobs, 0 = default;
 // V4=1 classifies into 4-byte verdicts, GCL_CFG_VERDICT4).
@@ -87,9 +88,18 @@ int main(int argc, char **argv)
 {
 	const int wl = argc > 1 ? atoi(argv[1]) : GCL_WL_UDP64;
 	const int steps = argc > 2 ? atoi(argv[2]) : 20;
-	const uint64_t n = wl == GCL_WL_UDP64 ? (32ull << 20) : (8ull << 20);
-	const uint64_t stride = wl == GCL_WL_UDP64 ? 64 : 1536;
-	const uint32_t R = wl == GCL_WL_UDP64 ? 16 : 1024, T = wl == GCL_WL_UDP64 ? 8 : 4;
+	/* CBENCH_N / CBENCH_STRIDE / CBENCH_R override the workload's packets per
+	 * launch, slot stride (64 with the tcp1500 stream = the header-split
+	 * layout) and runtime count */
+	auto env_u64 = [](const char *k, uint64_t d) { const char *e = getenv(k); return e ? strtoull(e, nullptr, 0) : d; };
+	const uint64_t n = env_u64("CBENCH_N", wl == GCL_WL_UDP64 ? (32ull << 20) : (8ull << 20));
+	const uint64_t stride = env_u64("CBENCH_STRIDE", wl == GCL_WL_UDP64 ? 64 : 1536);
+	const uint32_t R = (uint32_t)env_u64("CBENCH_R", wl == GCL_WL_UDP64 ? 16 : 1024);
+	const uint32_t T = wl == GCL_WL_UDP64 ? 8 : 4;
+	if (!n || n > (64ull << 20) || stride < 64 || stride % 16 || n * stride > (48ull << 30) || !R || R > 4096) {
+		fprintf(stderr, "bad CBENCH_N/STRIDE/R\n");
+		return 1;
+	}
 	std::vector<Cfg> cfgs;
 	cfgs.push_back({"ref", 0, 0, 0, 0, 0, 0, 0, true, {}, {}});
 	for (int i = 3; i < argc; i++) {
@@ -243,11 +253,12 @@ int main(int argc, char **argv)
 		double med = c.us[c.us.size() / 2], wmed = c.wall[c.wall.size() / 2];
 		if (c.ref)
 			ref = med;
-		printf("{\"workload\": %d, \"cfg\": \"%s\", \"profile\": %d, \"median_us\": %.2f, "
+		printf("{\"workload\": %d, \"n\": %llu, \"stride\": %llu, \"R\": %u, \"cfg\": \"%s\", "
+		       "\"profile\": %d, \"median_us\": %.2f, "
 		       "\"min_us\": %.2f, \"max_us\": %.2f, \"wall_us_per_step\": %.2f, \"Mpkts\": %.1f, "
 		       "\"ref_over_this\": %.4f}\n",
-		       wl, c.name.c_str(), (int)profile, med, c.us.front(), c.us.back(), wmed,
-		       n / (med * 1e-6) / 1e6, ref / med);
+		       wl, (unsigned long long)n, (unsigned long long)stride, R, c.name.c_str(), (int)profile,
+		       med, c.us.front(), c.us.back(), wmed, n / (med * 1e-6) / 1e6, ref / med);
 	}
 	return 0;
 }
