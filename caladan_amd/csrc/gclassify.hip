@@ -1630,7 +1630,9 @@ extern "C" int gcl_classify_ex(struct gcl_ctx *c, const struct gcl_batch *b,
 		return 0;
 	if (!b->frames || (!b->offs && (b->stride < 16 || (b->stride & 15) || b->stride > (1u << 20))))
 		return -EINVAL;
-	if (!verdicts)
+	/* at most 2^40 packets, so n * stride (and the fast-path range test on
+	 * it below) cannot wrap */
+	if (!verdicts || b->n > (1ull << 40))
 		return -EINVAL;
 	hipSetDevice(c->device);
 

@@ -245,11 +245,13 @@ int gcl_steer_flows(uint16_t thread_count, const uint16_t *active_idx,
 
 /*
  * gcl_classify - classify @b->n packets on @hip_stream (NULL = null stream).
- * @verdicts       device gcl_verdict[n] (gcl_verdict4[n] with GCL_CFG_VERDICT4)
+ * @verdicts       device gcl_verdict[n] (gcl_verdict4[n] with GCL_CFG_VERDICT4,
+ *                 u16[n] with GCL_CFG_VERDICT2)
  * @runtime_counts device u64[max_runtimes], ACCUMULATED: packets steered to
  *                 each runtime (DELIVER + WAKE), may be NULL
  * @stats          device u64[GCL_NR_STATS], ACCUMULATED, may be NULL
- * Asynchronous; returns -EINVAL for malformed batches, -EIO when the table
+ * Asynchronous; returns -EINVAL for malformed batches (including n > 2^40),
+ * -EIO when the table
  * upload fails, -ENOSPC when the IP table cannot place every key (cuckoo
  * placement failed for all 256 seeds: not seen at the table's load <= 1/2).
  * Replaces the rx_one_pkt loop of rx_burst (rx.c:281-287).

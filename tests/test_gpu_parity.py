@@ -655,3 +655,14 @@ def test_gpu_reference_struct_frames(g, orc):
     assert (v["thread"][hit] == exp_h[hit] % 4).all()
     assert ((v["action"][~hit] & 0x3F) == g.ACT_DROP_UNREG).all()
     assert int(c.sum()) == int(hit.sum())
+
+
+def test_gpu_rejects_oversized_batch(g):
+    """n > 2^40 is refused before any launch (n * stride must not wrap)."""
+    import ctypes
+    clf = g.Classifier(0, 16, 1)
+    f = torch.zeros(4096, dtype=torch.uint8, device="cuda")
+    v = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    b = g.GclBatch(frames=f.data_ptr(), frames_len=4096, stride=64, n=(1 << 40) + 1)
+    o = g.GclOut(verdicts=v.data_ptr())
+    assert g.lib.gcl_classify_ex(clf._ctx, ctypes.byref(b), ctypes.byref(o), None) == -22
