@@ -5,7 +5,8 @@
 // (env CBENCH_N, CBENCH_STRIDE, CBENCH_R override the workload's shape)
 //
 // Each cfg is "ABLATE:GRID:DEPTH:THREADS:BPC:SCHED:V4" (GCL_TUNE_* knobs, 0 = default;
-// V4=1 classifies into 4-byte verdicts, GCL_CFG_VERDICT4).
+// V4=1 classifies into 4-byte verdicts, GCL_CFG_VERDICT4; V4=2 into 2-byte queue
+// verdicts, GCL_CFG_VERDICT2).
 // CBENCH_NOISE_US=X co-runs, on a second stream, 32 one-wave blocks that each
 // spin for X us at the start of every classify launch (stand-in for an RCCL
 // kernel sharing the chip).  Rounds
@@ -206,7 +207,9 @@ int main(int argc, char **argv)
 			struct gcl_cfg cfg = {};
 			cfg.max_runtimes = R;
 			cfg.hash_mode = GCL_HASH_JENKINS;
-			cfg.flags = (profile ? GCL_CFG_PROFILE : 0) | (c.v4 ? GCL_CFG_VERDICT4 : 0);
+			cfg.flags = (profile ? GCL_CFG_PROFILE : 0) |
+			            (c.v4 == 2 ? GCL_CFG_VERDICT2 : c.v4 ? GCL_CFG_VERDICT4 : 0);
+			cfg.thread_bits = (uint8_t)(T <= 4 ? 2 : 3);
 			cfg.default_olflags = GCL_F_RSS_HASH | GCL_F_IP_CKSUM_GOOD;
 			struct gcl_ctx *ctx;
 			if (gcl_open(0, &cfg, &ctx)) {
