@@ -45,7 +45,7 @@ def build(force=False, verbose_resources=False):
         o = os.path.join(OBJ, src + ".o")
         if force or _stale(o, [s] + deps):
             cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
-                   "-Wall", "-Wno-unused-function", "-Wno-unused-value", "-Wno-unused-result", "-c", s, "-o", o]
+                   "-Wall", "-Wno-unused-function", "-c", s, "-o", o]
             if verbose_resources:
                 cmd.insert(1, "-Rpass-analysis=kernel-resource-usage")
             _run(cmd)

@@ -37,6 +37,18 @@ constexpr uint32_t kCrcBytes = 8 * 256 * 4;
 constexpr uint32_t kLdsTableBudget = 96 * 1024;
 constexpr int kImgUsers = 8;             /* streams tracked per table image */
 constexpr uint32_t kLdsQueueBytes = 16; /* s_next[2] after the header tile */
+
+/* The first failure of a sequence of HIP calls whose outcome is checked
+ * once, at the end (asynchronous copies, event records and waits). */
+struct HipErr {
+	hipError_t e = hipSuccess;
+	void operator()(hipError_t r)
+	{
+		if (r != hipSuccess && e == hipSuccess)
+			e = r;
+	}
+	bool bad() const { return e != hipSuccess; }
+};
 constexpr int kDefaultSched = 0;  /* GCL_TUNE_SCHED default: static persistent grid */
 constexpr int kDefaultXcdMap = 0; /* GCL_TUNE_XCD_MAP default: round-robin tiles */
 
@@ -1097,7 +1109,8 @@ extern "C" int gcl_open(int hip_device, const struct gcl_cfg *cfg, struct gcl_ct
 		return -ENOMEM;
 	c->device = hip_device;
 	c->cfg = *cfg;
-	hipDeviceGetAttribute(&c->num_cus, hipDeviceAttributeMultiprocessorCount, hip_device);
+	HipErr he;
+	he(hipDeviceGetAttribute(&c->num_cus, hipDeviceAttributeMultiprocessorCount, hip_device));
 	c->rt.resize(cfg->max_runtimes);
 	c->ipt_slots = pow2_at_least(cfg->max_runtimes * 2 < 16 ? 16 : cfg->max_runtimes * 2);
 	c->off_rt = c->ipt_slots * 8;
@@ -1144,7 +1157,7 @@ extern "C" int gcl_open(int hip_device, const struct gcl_cfg *cfg, struct gcl_ct
 	    hipMemset(c->sched, 0, GCL_SCHED_SLOTS * GCL_SCHED_WORDS * 4) != hipSuccess)
 		goto fail;
 	for (int i = 0; i < GCL_SCHED_SLOTS; i++) {
-		hipEventCreateWithFlags(&c->sched_ev[i], hipEventDisableTiming);
+		he(hipEventCreateWithFlags(&c->sched_ev[i], hipEventDisableTiming));
 		c->sched_used[i] = false;
 	}
 	for (int i = 0; i < 2; i++) {
@@ -1153,12 +1166,17 @@ extern "C" int gcl_open(int hip_device, const struct gcl_cfg *cfg, struct gcl_ct
 		c->users[i].n = 0;
 		c->users[i].retired = false;
 		for (int j = 0; j < kImgUsers; j++)
-			hipEventCreateWithFlags(&c->users[i].ev[j], hipEventDisableTiming);
+			he(hipEventCreateWithFlags(&c->users[i].ev[j], hipEventDisableTiming));
 	}
 	if (hipHostMalloc(&c->staging, c->image_cap, hipHostMallocDefault) != hipSuccess)
 		goto fail;
-	hipEventCreateWithFlags(&c->staging_free, hipEventDisableTiming);
-	hipEventCreateWithFlags(&c->tables_ready, hipEventDisableTiming);
+	he(hipEventCreateWithFlags(&c->staging_free, hipEventDisableTiming));
+	he(hipEventCreateWithFlags(&c->tables_ready, hipEventDisableTiming));
+	if (he.bad()) {
+		(void)hipGetLastError();
+		(void)hipHostFree(c->staging);
+		goto fail;
+	}
 	c->tables_stream = nullptr;
 	c->tables_done = true;
 	memset(&c->e2e, 0, sizeof(c->e2e));
@@ -1167,9 +1185,9 @@ extern "C" int gcl_open(int hip_device, const struct gcl_cfg *cfg, struct gcl_ct
 fail:
 	for (int i = 0; i < 2; i++)
 		if (c->dimg[i])
-			hipFree(c->dimg[i]);
+			(void)hipFree(c->dimg[i]);
 	if (c->sched)
-		hipFree(c->sched);
+		(void)hipFree(c->sched);
 	delete c;
 	return -ENOMEM;
 }
@@ -1178,34 +1196,34 @@ extern "C" void gcl_close(struct gcl_ctx *c)
 {
 	if (!c)
 		return;
-	hipSetDevice(c->device);
+	(void)hipSetDevice(c->device);
 	if (c->loop)
 		gcl_rxloop_stop(c->loop);
-	hipDeviceSynchronize();
+	(void)hipDeviceSynchronize();
 	for (int i = 0; i < 2; i++) {
-		hipFree(c->dimg[i]);
+		(void)hipFree(c->dimg[i]);
 		for (int j = 0; j < kImgUsers; j++)
-			hipEventDestroy(c->users[i].ev[j]);
+			(void)hipEventDestroy(c->users[i].ev[j]);
 	}
-	hipHostFree(c->staging);
-	hipEventDestroy(c->staging_free);
-	hipEventDestroy(c->tables_ready);
-	hipFree(c->sched);
+	(void)hipHostFree(c->staging);
+	(void)hipEventDestroy(c->staging_free);
+	(void)hipEventDestroy(c->tables_ready);
+	(void)hipFree(c->sched);
 	for (int i = 0; i < GCL_SCHED_SLOTS; i++)
-		hipEventDestroy(c->sched_ev[i]);
+		(void)hipEventDestroy(c->sched_ev[i]);
 	for (int i = 0; i < c->e2e.nstreams; i++) {
-		hipStreamDestroy(c->e2e.st[i]);
-		hipFree(c->e2e.slab[i]);
-		hipFree(c->e2e.side[i]);
-		hipFree(c->e2e.verd[i]);
+		(void)hipStreamDestroy(c->e2e.st[i]);
+		(void)hipFree(c->e2e.slab[i]);
+		(void)hipFree(c->e2e.side[i]);
+		(void)hipFree(c->e2e.verd[i]);
 	}
-	hipFree(c->e2e.acc);
+	(void)hipFree(c->e2e.acc);
 	for (auto &pr : c->ev_pending) {
-		hipEventDestroy(pr.first);
-		hipEventDestroy(pr.second);
+		(void)hipEventDestroy(pr.first);
+		(void)hipEventDestroy(pr.second);
 	}
 	for (auto e : c->ev_pool)
-		hipEventDestroy(e);
+		(void)hipEventDestroy(e);
 	delete c;
 }
 
@@ -1399,9 +1417,8 @@ static hipEvent_t prof_event(gcl_ctx *c)
 		c->ev_pool.pop_back();
 		return e;
 	}
-	hipEvent_t e;
-	hipEventCreate(&e);
-	return e;
+	hipEvent_t e = nullptr;
+	return hipEventCreate(&e) == hipSuccess ? e : nullptr;
 }
 
 template <int MODE, bool TLDS, bool GENERAL, int DEPTH, int NT>
@@ -1415,8 +1432,11 @@ static hipError_t launch_t(KParams k, uint32_t lds, int num_cus, int bpc_cap, hi
 	if (lds > 64 * 1024) {
 		static bool raised = false;
 		if (!raised) {
-			hipFuncSetAttribute((const void *)classify_kernel<MODE, TLDS, GENERAL, DEPTH, NT>,
-			                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+			const hipError_t e = hipFuncSetAttribute(
+			        (const void *)classify_kernel<MODE, TLDS, GENERAL, DEPTH, NT>,
+			        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+			if (e != hipSuccess)
+				return e;
 			raised = true;
 		}
 	}
@@ -1534,23 +1554,23 @@ static Geometry choose_geometry(const gcl_ctx *c, uint32_t tab_lds, uint32_t his
 /* Note that a launch on @s reads the current image.  With more streams than
  * kImgUsers, the new stream takes over the oldest one's slot after waiting
  * for what that stream has queued so far, so the slot still covers it. */
-static void image_used(gcl_ctx *c, hipStream_t s)
+static int image_used(gcl_ctx *c, hipStream_t s)
 {
 	gcl_ctx::ImgUsers &u = c->users[c->cur];
 	for (int i = 0; i < u.n; i++)
 		if (u.st[i] == s)
-			return;
+			return 0;
 	if (u.n == kImgUsers) {
-		hipEventRecord(u.ev[0], u.st[0]);
-		hipStreamWaitEvent(s, u.ev[0], 0);
+		HipErr he;
+		he(hipEventRecord(u.ev[0], u.st[0]));
+		he(hipStreamWaitEvent(s, u.ev[0], 0));
 		u.st[0] = s;
-		return;
+		return he.bad() ? -EIO : 0;
 	}
 	u.st[u.n++] = s;
+	return 0;
 }
 
-/* Upload a new table snapshot on @s if anything changed; launches on other
- * streams wait for c->tables_ready before reading the image. */
 static uint32_t verdict_bytes(const gcl_ctx *c)
 {
 	return (c->cfg.flags & GCL_CFG_VERDICT2) ? 2 : (c->cfg.flags & GCL_CFG_VERDICT4) ? 4 : 8;
@@ -1562,11 +1582,16 @@ static uint32_t kernel_cflags(const gcl_ctx *c)
 	return (c->cfg.flags & 0xFFFFFFu) | (uint32_t)c->cfg.thread_bits << 24;
 }
 
+/* Upload a new table snapshot on @s if anything changed; launches on other
+ * streams wait for c->tables_ready before reading the image. */
 static int upload_tables(gcl_ctx *c, hipStream_t s)
 {
 	if (!c->dirty)
 		return 0;
-	hipEventSynchronize(c->staging_free);
+	HipErr he;
+	he(hipEventSynchronize(c->staging_free));
+	if (he.bad())
+		return -EIO;
 	uint32_t bytes = build_image(c);
 	if (!bytes)
 		return -ENOSPC;
@@ -1576,18 +1601,19 @@ static int upload_tables(gcl_ctx *c, hipStream_t s)
 	if (old.retired)
 		for (int i = 0; i < old.n; i++)
 			if (old.st[i] != s)
-				hipStreamWaitEvent(s, old.ev[i], 0);
+				he(hipStreamWaitEvent(s, old.ev[i], 0));
 	old.n = 0;
 	old.retired = false;
 	/* the image going out of use: mark where each of its streams is */
 	gcl_ctx::ImgUsers &cur = c->users[c->cur];
 	for (int i = 0; i < cur.n; i++)
-		hipEventRecord(cur.ev[i], cur.st[i]);
+		he(hipEventRecord(cur.ev[i], cur.st[i]));
 	cur.retired = true;
-	if (hipMemcpyAsync(c->dimg[nxt], c->staging, bytes, hipMemcpyHostToDevice, s) != hipSuccess)
-		return -EIO;
-	hipEventRecord(c->staging_free, s);
-	hipEventRecord(c->tables_ready, s);
+	he(hipMemcpyAsync(c->dimg[nxt], c->staging, bytes, hipMemcpyHostToDevice, s));
+	he(hipEventRecord(c->staging_free, s));
+	he(hipEventRecord(c->tables_ready, s));
+	if (he.bad())
+		return -EIO; /* dirty stays set: the next call uploads again */
 	c->tables_stream = s;
 	c->tables_done = false;
 	c->cur = nxt;
@@ -1597,15 +1623,15 @@ static int upload_tables(gcl_ctx *c, hipStream_t s)
 
 /* Order a launch on @s after the last table upload: free on the upload's own
  * stream, and skipped once the upload is known to have completed. */
-static void wait_tables(gcl_ctx *c, hipStream_t s)
+static int wait_tables(gcl_ctx *c, hipStream_t s)
 {
 	if (c->tables_done || s == c->tables_stream)
-		return;
+		return 0;
 	if (hipEventQuery(c->tables_ready) == hipSuccess) {
 		c->tables_done = true;
-		return;
+		return 0;
 	}
-	hipStreamWaitEvent(s, c->tables_ready, 0);
+	return hipStreamWaitEvent(s, c->tables_ready, 0) == hipSuccess ? 0 : -EIO;
 }
 
 extern "C" int gcl_classify(struct gcl_ctx *c, const struct gcl_batch *b,
@@ -1634,12 +1660,14 @@ extern "C" int gcl_classify_ex(struct gcl_ctx *c, const struct gcl_batch *b,
 	 * it below) cannot wrap */
 	if (!verdicts || b->n > (1ull << 40))
 		return -EINVAL;
-	hipSetDevice(c->device);
+	if (hipSetDevice(c->device) != hipSuccess)
+		return -ENODEV;
 
 	const int up = upload_tables(c, s);
 	if (up)
 		return up;
-	wait_tables(c, s);
+	if (wait_tables(c, s))
+		return -EIO;
 
 	KParams k = {};
 	k.frames = b->frames;
@@ -1684,11 +1712,12 @@ extern "C" int gcl_classify_ex(struct gcl_ctx *c, const struct gcl_batch *b,
 	k.tables_lds_bytes = tlds ? tab_bytes : 0;
 	Geometry geo = choose_geometry(c, tlds ? tab_bytes : 0, hist_bytes);
 
+	HipErr he;
 	int slot = -1;
 	if (c->tune_sched && geo.depth == 1) {
 		slot = (int)(c->sched_seq++ % GCL_SCHED_SLOTS);
 		if (c->sched_used[slot])
-			hipStreamWaitEvent(s, c->sched_ev[slot], 0);
+			he(hipStreamWaitEvent(s, c->sched_ev[slot], 0));
 		k.sched = c->sched + (size_t)slot * GCL_SCHED_WORDS;
 	}
 
@@ -1696,7 +1725,15 @@ extern "C" int gcl_classify_ex(struct gcl_ctx *c, const struct gcl_batch *b,
 	if ((c->cfg.flags & GCL_CFG_PROFILE) && c->prof_seq++ % c->prof_every == 0) {
 		e0 = prof_event(c);
 		e1 = prof_event(c);
-		hipEventRecord(e0, s);
+		if (!e0 || !e1) { /* no timing for this launch */
+			if (e0)
+				c->ev_pool.push_back(e0);
+			if (e1)
+				c->ev_pool.push_back(e1);
+			e0 = e1 = nullptr;
+		} else {
+			he(hipEventRecord(e0, s));
+		}
 	}
 	hipError_t err;
 	switch (c->cfg.hash_mode) {
@@ -1714,23 +1751,29 @@ extern "C" int gcl_classify_ex(struct gcl_ctx *c, const struct gcl_batch *b,
 		break;
 	}
 	if (e0) {
-		hipEventRecord(e1, s);
-		c->ev_pending.push_back({e0, e1});
+		he(hipEventRecord(e1, s));
+		if (he.bad()) { /* an unusable timing pair: back to the pool */
+			c->ev_pool.push_back(e0);
+			c->ev_pool.push_back(e1);
+		} else {
+			c->ev_pending.push_back({e0, e1});
+		}
 	}
-	image_used(c, s);
+	const int iu = image_used(c, s);
 	if (slot >= 0) {
-		hipEventRecord(c->sched_ev[slot], s);
+		he(hipEventRecord(c->sched_ev[slot], s));
 		c->sched_used[slot] = true;
 	}
 	c->last_stream = s;
-	return err == hipSuccess ? 0 : -EIO;
+	return err == hipSuccess && !he.bad() && !iu ? 0 : -EIO;
 }
 
 extern "C" int gcl_sync(struct gcl_ctx *c)
 {
 	if (!c)
 		return -EINVAL;
-	hipSetDevice(c->device);
+	if (hipSetDevice(c->device) != hipSuccess)
+		return -ENODEV;
 	return hipStreamSynchronize(c->last_stream) == hipSuccess ? 0 : -EIO;
 }
 
@@ -1747,13 +1790,15 @@ extern "C" int gcl_kernel_time(struct gcl_ctx *c, double *ms, uint64_t *launches
 {
 	if (!c)
 		return -EINVAL;
-	hipSetDevice(c->device);
+	if (hipSetDevice(c->device) != hipSuccess)
+		return -ENODEV;
 	for (auto &pr : c->ev_pending) {
 		float f = 0;
-		hipEventSynchronize(pr.second);
-		hipEventElapsedTime(&f, pr.first, pr.second);
-		c->prof_ms += f;
-		c->prof_launches++;
+		if (hipEventSynchronize(pr.second) == hipSuccess &&
+		    hipEventElapsedTime(&f, pr.first, pr.second) == hipSuccess) {
+			c->prof_ms += f;
+			c->prof_launches++;
+		}
 		c->ev_pool.push_back(pr.first);
 		c->ev_pool.push_back(pr.second);
 	}
@@ -1912,8 +1957,10 @@ extern "C" int gcl_dev_alloc_paired(int hip_device, size_t bytes, const void *pa
 	hipEvent_t e0, e1;
 	if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess)
 		return -EIO;
-	hipEventCreate(&e0);
-	hipEventCreate(&e1);
+	if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) {
+		(void)hipStreamDestroy(s);
+		return -EIO;
+	}
 	const bool dbg = getenv("GCL_PAIR_DEBUG") != nullptr;
 	std::vector<std::pair<void *, double>> cand;
 	std::vector<void *> spacers;
@@ -1939,7 +1986,7 @@ extern "C" int gcl_dev_alloc_paired(int hip_device, size_t bytes, const void *pa
 		if (dbg)
 			fprintf(stderr, "gcl_dev_alloc_paired: candidate %d %p probe %.2f us\n", i, p, us);
 		if (us < 0) {
-			hipFree(p);
+			(void)hipFree(p);
 			ret = -EIO;
 			break;
 		}
@@ -1961,12 +2008,12 @@ extern "C" int gcl_dev_alloc_paired(int hip_device, size_t bytes, const void *pa
 	}
 	for (size_t i = 0; i < cand.size(); i++)
 		if (ret || i != best)
-			hipFree(cand[i].first);
+			(void)hipFree(cand[i].first);
 	for (void *sp : spacers)
-		hipFree(sp);
-	hipEventDestroy(e0);
-	hipEventDestroy(e1);
-	hipStreamDestroy(s);
+		(void)hipFree(sp);
+	(void)hipEventDestroy(e0);
+	(void)hipEventDestroy(e1);
+	(void)hipStreamDestroy(s);
 	if (ret)
 		return ret;
 	if (cand.empty())
@@ -2001,10 +2048,10 @@ static int e2e_setup(gcl_ctx *c, int nstreams, uint64_t chunk)
 	if (e.nstreams == nstreams && e.chunk == chunk)
 		return 0;
 	for (int i = 0; i < e.nstreams; i++) {
-		hipStreamDestroy(e.st[i]);
-		hipFree(e.slab[i]);
-		hipFree(e.side[i]);
-		hipFree(e.verd[i]);
+		(void)hipStreamDestroy(e.st[i]);
+		(void)hipFree(e.slab[i]);
+		(void)hipFree(e.side[i]);
+		(void)hipFree(e.verd[i]);
 	}
 	if (!e.acc && hipMalloc(&e.acc, (GCL_MAX_PROC + GCL_NR_STATS) * 8) != hipSuccess)
 		return -ENOMEM;
@@ -2042,7 +2089,8 @@ extern "C" int gcl_classify_host(struct gcl_ctx *c, const struct gcl_batch *hb,
 		return -EINVAL;
 	if (hb->n == 0)
 		return 0;
-	hipSetDevice(c->device);
+	if (hipSetDevice(c->device) != hipSuccess)
+		return -ENODEV;
 	const uint32_t max_rt = c->cfg.max_runtimes;
 	const uint64_t vsize = verdict_bytes(c);
 	int nst = o->nstreams ? (int)o->nstreams : 2;
@@ -2054,14 +2102,16 @@ extern "C" int gcl_classify_host(struct gcl_ctx *c, const struct gcl_batch *hb,
 		return ret;
 	gcl_ctx::E2E &e = c->e2e;
 	hipStream_t s0 = e.st[0];
-	hipMemsetAsync(e.acc, 0, (max_rt + GCL_NR_STATS) * 8, s0);
+	HipErr he; /* every asynchronous step below; checked after the final sync */
+	he(hipMemsetAsync(e.acc, 0, (max_rt + GCL_NR_STATS) * 8, s0));
 	if (upload_tables(c, s0))
 		return -EIO;
 	hipEvent_t ready;
-	hipEventCreateWithFlags(&ready, hipEventDisableTiming);
-	hipEventRecord(ready, s0);
+	if (hipEventCreateWithFlags(&ready, hipEventDisableTiming) != hipSuccess)
+		return -EIO;
+	he(hipEventRecord(ready, s0));
 	for (int i = 1; i < nst; i++)
-		hipStreamWaitEvent(e.st[i], ready, 0);
+		he(hipStreamWaitEvent(e.st[i], ready, 0));
 
 	uint64_t *dcounts = e.acc, *dstats = e.acc + max_rt;
 	if (o->mode == GCL_E2E_ZEROCOPY) {
@@ -2078,13 +2128,13 @@ extern "C" int gcl_classify_host(struct gcl_ctx *c, const struct gcl_batch *hb,
 		if (!db.frames || !dv || (hb->offs && !db.offs) || (hb->olflags && !db.olflags) ||
 		    (hb->rss && !db.rss) || (hb->fdir_hi && !db.fdir_hi) ||
 		    (hb->dst_hint && !db.dst_hint)) {
-			hipEventDestroy(ready);
+			(void)hipEventDestroy(ready);
 			return -EFAULT; /* not pinned/registered: see gcl_host_register */
 		}
 		ret = gcl_classify(c, &db, dv, dcounts, dstats, s0);
 	} else {
 		if (hb->offs || (hb->stride & 15) || hb->stride < GCL_HDR_GRANULE) {
-			hipEventDestroy(ready);
+			(void)hipEventDestroy(ready);
 			return -EINVAL; /* the copy path gathers fixed-stride header granules */
 		}
 		for (uint64_t s = 0, ci = 0; s < hb->n && !ret; s += chunk, ci++) {
@@ -2099,10 +2149,10 @@ extern "C" int gcl_classify_host(struct gcl_ctx *c, const struct gcl_batch *hb,
 				break;
 			}
 			if (hb->stride == GCL_HDR_GRANULE)
-				hipMemcpyAsync(e.slab[i], src, m * GCL_HDR_GRANULE, hipMemcpyHostToDevice, st);
+				he(hipMemcpyAsync(e.slab[i], src, m * GCL_HDR_GRANULE, hipMemcpyHostToDevice, st));
 			else
-				hipMemcpy2DAsync(e.slab[i], GCL_HDR_GRANULE, src, hb->stride, GCL_HDR_GRANULE, m,
-				                 hipMemcpyHostToDevice, st);
+				he(hipMemcpy2DAsync(e.slab[i], GCL_HDR_GRANULE, src, hb->stride, GCL_HDR_GRANULE, m,
+				                    hipMemcpyHostToDevice, st));
 			struct gcl_batch db = {};
 			db.frames = e.slab[i];
 			db.frames_len = m * GCL_HDR_GRANULE;
@@ -2110,36 +2160,38 @@ extern "C" int gcl_classify_host(struct gcl_ctx *c, const struct gcl_batch *hb,
 			db.n = m;
 			uint8_t *side = e.side[i];
 			if (hb->olflags) {
-				hipMemcpyAsync(side, hb->olflags + s, m, hipMemcpyHostToDevice, st);
+				he(hipMemcpyAsync(side, hb->olflags + s, m, hipMemcpyHostToDevice, st));
 				db.olflags = side;
 			}
 			if (hb->rss) {
-				hipMemcpyAsync(side + chunk, hb->rss + s, m * 4, hipMemcpyHostToDevice, st);
+				he(hipMemcpyAsync(side + chunk, hb->rss + s, m * 4, hipMemcpyHostToDevice, st));
 				db.rss = (const uint32_t *)(side + chunk);
 			}
 			if (hb->fdir_hi) {
-				hipMemcpyAsync(side + 5 * chunk, hb->fdir_hi + s, m * 4, hipMemcpyHostToDevice, st);
+				he(hipMemcpyAsync(side + 5 * chunk, hb->fdir_hi + s, m * 4, hipMemcpyHostToDevice, st));
 				db.fdir_hi = (const uint32_t *)(side + 5 * chunk);
 			}
 			if (hb->dst_hint) {
-				hipMemcpyAsync(side + 9 * chunk, hb->dst_hint + s, m * 4, hipMemcpyHostToDevice, st);
+				he(hipMemcpyAsync(side + 9 * chunk, hb->dst_hint + s, m * 4, hipMemcpyHostToDevice, st));
 				db.dst_hint = (const uint32_t *)(side + 9 * chunk);
 			}
 			ret = gcl_classify(c, &db, e.verd[i], dcounts, dstats, st);
-			hipMemcpyAsync((uint8_t *)host_verdicts + s * vsize, e.verd[i], m * vsize,
-			               hipMemcpyDeviceToHost, st);
+			he(hipMemcpyAsync((uint8_t *)host_verdicts + s * vsize, e.verd[i], m * vsize,
+			                  hipMemcpyDeviceToHost, st));
 		}
 		for (int i = 1; i < nst; i++) {
-			hipEventRecord(ready, e.st[i]);
-			hipStreamWaitEvent(s0, ready, 0);
+			he(hipEventRecord(ready, e.st[i]));
+			he(hipStreamWaitEvent(s0, ready, 0));
 		}
 	}
 	uint64_t tmp[GCL_MAX_PROC + GCL_NR_STATS];
-	hipMemcpyAsync(tmp, e.acc, (max_rt + GCL_NR_STATS) * 8, hipMemcpyDeviceToHost, s0);
+	he(hipMemcpyAsync(tmp, e.acc, (max_rt + GCL_NR_STATS) * 8, hipMemcpyDeviceToHost, s0));
 	hipError_t err = hipStreamSynchronize(s0);
-	hipEventDestroy(ready);
+	(void)hipEventDestroy(ready);
 	if (ret)
 		return ret;
+	if (he.bad())
+		return -EIO;
 	if (err != hipSuccess)
 		return -EIO;
 	if (host_counts)
@@ -2237,7 +2289,8 @@ static bool ticket_done(gcl_rxloop *L, uint64_t t)
 static int loop_write_image(gcl_rxloop *L, int i)
 {
 	gcl_ctx *c = L->c;
-	hipEventSynchronize(c->staging_free);
+	if (hipEventSynchronize(c->staging_free) != hipSuccess)
+		return -EIO;
 	const uint32_t bytes = build_image(c);
 	if (!bytes)
 		return -ENOSPC;
@@ -2259,9 +2312,13 @@ static int loop_write_image(gcl_rxloop *L, int i)
 template <int MODE>
 static hipError_t loop_launch(const LoopParams &lp, uint32_t lds, hipStream_t s)
 {
-	if (lds > 64 * 1024)
-		hipFuncSetAttribute((const void *)rxloop_kernel<MODE>,
-		                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+	if (lds > 64 * 1024) {
+		const hipError_t e = hipFuncSetAttribute((const void *)rxloop_kernel<MODE>,
+		                                         hipFuncAttributeMaxDynamicSharedMemorySize,
+		                                         160 * 1024);
+		if (e != hipSuccess)
+			return e;
+	}
 	hipLaunchKernelGGL(rxloop_kernel<MODE>, dim3(lp.workers), dim3(256), lds, s, lp);
 	return hipGetLastError();
 }
@@ -2355,7 +2412,7 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 		             : c->cfg.hash_mode == GCL_HASH_JENKINS ? loop_launch<GCL_HASH_JENKINS>(lp, lds, L->st)
 		             : loop_launch<GCL_HASH_TOEPLITZ>(lp, lds, L->st);
 		if (e != hipSuccess) {
-			hipStreamDestroy(L->st);
+			(void)hipStreamDestroy(L->st);
 			L->st = nullptr;
 			goto fail;
 		}
@@ -2364,10 +2421,10 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 	*out = L;
 	return 0;
 fail:
-	hipHostFree(L->slots);
-	hipHostFree(L->img[0]);
-	hipHostFree(L->img[1]);
-	hipHostFree(L->ctl);
+	(void)hipHostFree(L->slots);
+	(void)hipHostFree(L->img[0]);
+	(void)hipHostFree(L->img[1]);
+	(void)hipHostFree(L->ctl);
 	delete L;
 	return ret;
 }
@@ -2488,11 +2545,11 @@ extern "C" int gcl_rxloop_stop(struct gcl_rxloop *L)
 				fprintf(stderr, " %u", L->ctl[8 + b] - 1);
 		fprintf(stderr, "\n");
 	}
-	hipStreamDestroy(L->st);
-	hipHostFree(L->slots);
-	hipHostFree(L->img[0]);
-	hipHostFree(L->img[1]);
-	hipHostFree(L->ctl);
+	(void)hipStreamDestroy(L->st);
+	(void)hipHostFree(L->slots);
+	(void)hipHostFree(L->img[0]);
+	(void)hipHostFree(L->img[1]);
+	(void)hipHostFree(L->ctl);
 	if (L->c->loop == L)
 		L->c->loop = nullptr;
 	delete L;
