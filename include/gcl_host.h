@@ -116,7 +116,8 @@ struct gcl_verdict4 gcl_verdict2_to4(uint16_t v, uint8_t thread_bits);
 
 /*
  * gcl_host_deliver2 - gcl_host_deliver4 over 2-byte verdicts: the same
- * replay, packet by packet, of @v widened by gcl_verdict2_to4.  The DELIVER
+ * replay of rx_send_pkt_to_runtime / rx_send_to_runtime (rx.c:50-92),
+ * packet by packet, of @v widened by gcl_verdict2_to4.  The DELIVER
  * fast path reads the destination ring straight from the queue index.
  */
 uint64_t gcl_host_deliver2(struct gcl_host_proc *const *clients_by_id, uint32_t max_runtimes,
