@@ -53,6 +53,9 @@ WORKLOADS = {
 # verdict of GCL_CFG_VERDICT2) (DESIGN.md "Roofline"); tables and counters
 # amortise to ~0.
 HDR_BYTES = 64
+# the bench default is the 4-byte verdict: the 2-byte queue verdict is
+# 1-4.5 % faster (profiles/r01_verdict_width_ab.jsonl) but carries 2 B/pkt
+# less, so its roofline fraction is no higher
 VERDICT_BYTES = 4
 VERDICT_NAMES = {8: "gcl_verdict, 8 B", 4: "gcl_verdict4, 4 B",
                  2: "queue verdict (GCL_CFG_VERDICT2), 2 B"}

@@ -91,7 +91,7 @@ def main(rnd):
         cal = calib(base)
         with open(os.path.join(prof, f"{rnd}_calibration.json"), "w") as f:
             json.dump({"note": __doc__.strip().split("\n\n")[2], "patterns": cal}, f, indent=1)
-    for wl, vb in [(w, v) for w in PKTS for v in (4, 8)]:
+    for wl, vb in [(w, v) for w in PKTS for v in (2, 4, 8)]:
         tag = f"{wl}_v{vb}"
         tdir = os.path.join(base, f"{tag}_trace")
         if not os.path.isdir(tdir):
@@ -133,7 +133,7 @@ def main(rnd):
             out.update(req)
             out["traffic_over_algorithmic_from_requests"] = round(req["hbm_bytes_from_requests"] / algo, 4)
             out["requests_per_pkt"] = round((req["req_reads"] + req["req_writes"]) / PKTS[wl], 4)
-        with open(os.path.join(prof, f"pmc_{wl}{'_v4' if vb == 4 else ''}.json"), "w") as f:
+        with open(os.path.join(prof, f"pmc_{wl}{'' if vb == 8 else f'_v{vb}'}.json"), "w") as f:
             json.dump(out, f, indent=1)
         print(json.dumps(out))
 

@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 R=${ROUND:-r01}
 OUT=gpurun_out/prof_$R
 mkdir -p $OUT
-for vb in ${VBS:-4 8}; do
+for vb in ${VBS:-2 4 8}; do
 for wl in ${WLS:-udp64 tcp1500}; do
   A="--workload $wl --verdict-bytes $vb --no-cpu --no-secondary --no-e2e"
   D=$OUT/${wl}_v${vb}
