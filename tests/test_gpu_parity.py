@@ -331,6 +331,42 @@ def test_gpu_table_images_across_streams(g, orc):
         assert_same(v.cpu().numpy().view(g.VERDICT_DTYPE), ve, f"launch {i}")
 
 
+def test_gpu_table_images_many_streams(g, orc):
+    """More streams than an image tracks readers for (8): launches on 10
+    streams read one image, the later ones taking over the oldest slot after
+    waiting for it; then two table changes overwrite that image, and every
+    launch must still see the tables current when it was submitted."""
+    n, R = 20000, 16
+    frames, _, _ = orc.generate(0, n, 64, R)
+    t = orc.Tables(R, 1, 0, 0x09)
+    clf = g.Classifier(0, R, 1)
+    for r in range(R):
+        t.runtime_set(r, orc.runtime_ip(r), 4, 4, [0, 1, 2, 3])
+        clf.runtime_set(r, g.runtime_ip(r), 4, 4, [0, 1, 2, 3])
+    f = dev(frames)
+    streams = [torch.cuda.Stream() for _ in range(10)]
+    bufs = [torch.zeros(n * 8, dtype=torch.uint8, device="cuda") for _ in range(13)]
+    torch.cuda.synchronize()
+    with torch.cuda.stream(streams[0]):
+        torch.cuda._sleep(100_000_000)  # hold the first reader back
+    for i, st in enumerate(streams):
+        clf.classify(f, n, 64, verdicts=bufs[i], stream=st.cuda_stream)       # v0
+    clf.runtime_set(2, g.runtime_ip(2), 5, 3, orc.steer_flows(5, [4, 0, 2]))
+    clf.classify(f, n, 64, verdicts=bufs[10], stream=streams[3].cuda_stream)  # v1
+    clf.runtime_set(7, g.runtime_ip(7), 2, 0, None)
+    clf.classify(f, n, 64, verdicts=bufs[11], stream=streams[9].cuda_stream)  # v2: image of v0
+    clf.classify(f, n, 64, verdicts=bufs[12], stream=streams[0].cuda_stream)  # v2
+    torch.cuda.synchronize()
+    v0 = t.classify(frames, n, 64)[0]
+    t.runtime_set(2, orc.runtime_ip(2), 5, 3, orc.steer_flows(5, [4, 0, 2]))
+    v1 = t.classify(frames, n, 64)[0]
+    t.runtime_set(7, orc.runtime_ip(7), 2, 0, None)
+    v2 = t.classify(frames, n, 64)[0]
+    assert not (v0 == v1).all() and not (v1 == v2).all()
+    for i, (v, ve) in enumerate(zip(bufs, [v0] * 10 + [v1, v2, v2])):
+        assert_same(v.cpu().numpy().view(g.VERDICT_DTYPE), ve, f"launch {i}")
+
+
 def test_gpu_counts_accumulate_and_edge_sizes(g, orc):
     """Counters accumulate across calls; n = 1, ragged tails, empty batch."""
     R = 16
