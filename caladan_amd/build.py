@@ -5,7 +5,6 @@ host-side C (csrc/gcl_host.c); hipcc links both into caladan_amd/libgclassify.so
 The .so is git-ignored but travels to the GPU box with the gpurun snapshot.
 """
 import os
-import shutil
 import subprocess
 import sys
 
