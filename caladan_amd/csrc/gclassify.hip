@@ -136,6 +136,23 @@ __device__ __forceinline__ uint64_t frame_off(const KParams &k, uint64_t idx)
 	return idx * k.stride;
 }
 
+/*
+ * Header bytes staged for a frame at @off: the 64-B granule, cut at the end of
+ * its first 128-B line when that line still holds bytes [0, 40) -- Ethernet,
+ * an IHL-5 IPv4 header and the L4 ports, all the common case reads.  An
+ * 8-B-aligned frame starting in the last 40-63 bytes of a line (mbuf data at
+ * element + 344 in the reference's 9408-B ingress elements lands at 88 mod
+ * 128 every other slot, defs.h:503-506) then costs one line, not two; the
+ * rare packets that need more (ARP's target IP at 38-41, IPv4 options) read
+ * the rest directly (classify_one).  Returns 64 (whole granule) or 40/48/56.
+ */
+__device__ __forceinline__ uint32_t hdr_avail(const KParams &k, uint64_t off)
+{
+	const uint64_t A = (uint64_t)(uintptr_t)k.frames + off;
+	const uint32_t E = 128u - (uint32_t)(A & 127);
+	return ((A & 7) == 0 && E >= 40 && E < 64) ? E : 64u;
+}
+
 template <bool GENERAL, int NT>
 __device__ __forceinline__ void load_tile(const KParams &k, uint64_t tile, uint4 r[4])
 {
@@ -157,8 +174,28 @@ __device__ __forceinline__ void load_tile(const KParams &k, uint64_t tile, uint4
 		uint64_t idx = tile * NT + (uint64_t)(c >> 2);
 		uint4 v = make_uint4(0, 0, 0, 0);
 		if (idx < k.n) {
-			uint64_t a = frame_off<GENERAL>(k, idx) + (uint64_t)(c & 3) * 16;
-			if (!GENERAL || (a + 16 <= k.frames_len && (a & 15) == 0)) {
+			const uint64_t off = frame_off<GENERAL>(k, idx);
+			const uint32_t q16 = (uint32_t)(c & 3) * 16;
+			const uint32_t e = GENERAL ? hdr_avail(k, off) : 64u;
+			uint64_t a = off + q16;
+			if (GENERAL && q16 >= e) {
+				/* past the frame's first line: left 0, read on demand */
+			} else if (GENERAL && q16 + 16 > e) {
+				/* the 8 bytes before the line end (e = q16 + 8) */
+				if (a + 8 <= k.frames_len) {
+					const gcl::u32x2v lo =
+					        __builtin_nontemporal_load((const gcl::u32x2v *)(k.frames + a));
+					v = make_uint4(lo.x, lo.y, 0, 0);
+				} else {
+					uint32_t w[2];
+					for (int b = 0; b < 2; b++)
+						w[b] = frame_byte(k, a + 4 * b) |
+						       frame_byte(k, a + 4 * b + 1) << 8 |
+						       frame_byte(k, a + 4 * b + 2) << 16 |
+						       (uint32_t)frame_byte(k, a + 4 * b + 3) << 24;
+					v = make_uint4(w[0], w[1], 0, 0);
+				}
+			} else if (!GENERAL || (a + 16 <= k.frames_len && (a & 15) == 0)) {
 				v = gcl::load16_nt(k.frames + a);
 			} else if (a + 16 <= k.frames_len && (a & 7) == 0) {
 				/* mbuf data in the reference's ingress pool sits at
@@ -268,9 +305,15 @@ __device__ __forceinline__ void classify_one(const KParams &k, const uint4 *tile
 	const uint32_t proto = d5 >> 24;
 	const uint32_t saddr = gcl::bswap32(gcl::mid32(d6, d7));
 	const uint32_t daddr = gcl::bswap32(gcl::mid32(d7, d8));     /* rx.c:157-159 */
-	const uint32_t arp_tip = gcl::bswap32(gcl::mid32(d9, d10));  /* rx.c:165-167 */
+	uint32_t arp_tip = gcl::bswap32(gcl::mid32(d9, d10));        /* rx.c:165-167 */
 	const uint32_t flags = (GENERAL && k.olflags) ? k.olflags[idx] : k.default_flags;
 	const bool is_ip = et == GCL_ETHTYPE_IP, is_arp = et == GCL_ETHTYPE_ARP;
+	if (GENERAL && !SYS && is_arp && hdr_avail(k, frame_off<GENERAL>(k, idx)) < 44) {
+		/* bytes 40-41 are past the staged line (load_tile) */
+		const uint64_t a = frame_off<GENERAL>(k, idx) + 38;
+		arp_tip = (uint32_t)frame_byte(k, a) << 24 | (uint32_t)frame_byte(k, a + 1) << 16 |
+		          (uint32_t)frame_byte(k, a + 2) << 8 | frame_byte(k, a + 3);
+	}
 	const bool azure = k.cflags & GCL_CFG_AZURE_ARP;
 
 	/* steering hash (gclassify.h: NIC / JENKINS / TOEPLITZ) */
@@ -285,11 +328,12 @@ __device__ __forceinline__ void classify_one(const KParams &k, const uint4 *tile
 		                      (proto == 6 || proto == 17);
 		uint32_t sport = gcl::bswap16(d8 >> 16), dport = gcl::bswap16(d9 & 0xFFFF);
 		if (hashable && ihl != 5) {
-			if (ihl <= 11) {
+			if (ihl <= 11 && (!GENERAL || SYS ||
+			                  20 + 4 * ihl <= hdr_avail(k, frame_off<GENERAL>(k, idx)))) {
 				const int o = 14 + 4 * (int)ihl;
 				sport = gcl::bswap16(tile_dword(tile, tid, o - 2) >> 16);
 				dport = gcl::bswap16(tile_dword(tile, tid, o + 2) & 0xFFFF);
-			} else { /* past the staged granule */
+			} else { /* past the staged header bytes */
 				const uint64_t a = frame_off<GENERAL>(k, idx) + 14 + 4 * ihl;
 				sport = (uint32_t)fbyte<SYS>(k, a) << 8 | fbyte<SYS>(k, a + 1);
 				dport = (uint32_t)fbyte<SYS>(k, a + 2) << 8 | fbyte<SYS>(k, a + 3);

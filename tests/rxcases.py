@@ -97,7 +97,9 @@ def fuzz_batch(rng, n, runtimes, max_runtimes, slot=128, tail_runts=True, misali
     """Random frames hitting every branch; 16-B aligned shuffled offsets, the
     last frames straddling the end of the buffer (reads past it see 0).
     misalign: None, "mbuf" (every frame at +8, like mbuf data in the
-    reference's ingress pool) or "mixed" (shifts of 0..15 bytes)."""
+    reference's ingress pool), "mixed" (shifts of 0..15 bytes) or "lineend"
+    (shifts of up to 92 bytes, most putting a 128-B line end 40-56 bytes
+    into the frame; needs slot >= 256)."""
     ips = [r["ip"] for r in runtimes] or [0x0A000001]
     buf_slots = n + 8
     frames = np.zeros(buf_slots * slot, dtype=np.uint8)
@@ -107,6 +109,10 @@ def fuzz_batch(rng, n, runtimes, max_runtimes, slot=128, tail_runts=True, misali
         offs += np.uint64(8)
     elif misalign == "mixed":
         offs += rng.choice([0, 8, 8, 4, 12, 1, 2, 3, 5, 15], size=n).astype(np.uint64)
+    elif misalign == "lineend":
+        # first 128-B line ends 40, 48 or 56 bytes into the frame (staged
+        # header cut at the line, the rest read on demand), or later
+        offs += rng.choice([88, 80, 72, 88, 80, 72, 8, 40, 84, 92], size=n).astype(np.uint64)
     olflags = rng.integers(0, 16, size=n, dtype=np.uint8)
     rss = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
     fdir = np.where(rng.random(n) < 0.7,
@@ -138,7 +144,7 @@ def fuzz_batch(rng, n, runtimes, max_runtimes, slot=128, tail_runts=True, misali
             fr = eth + b"\x81\x00\x00\x05\x08\x00" + bytes(rng.integers(0, 256, size=40, dtype=np.uint8))
         else:
             fr = bytes(rng.integers(0, 256, size=int(rng.integers(14, slot)), dtype=np.uint8))
-        fr = fr[:slot - (16 if misalign else 0)]
+        fr = fr[:slot - (96 if misalign == "lineend" else 16 if misalign else 0)]
         o = int(offs[i])
         frames[o:o + len(fr)] = np.frombuffer(fr, dtype=np.uint8)
     # loopback hints (tx_pktmbuf_priv.dst_ip): none, a registered IP, or a miss
@@ -152,6 +158,10 @@ def fuzz_batch(rng, n, runtimes, max_runtimes, slot=128, tail_runts=True, misali
         for j, cut in enumerate((20, 36, 60)):
             offs[n - 1 - j] = last + 16 * j
         frames_len = last + 16 * 2 + 40
+        if misalign == "lineend":
+            # the line-end cut (8 bytes at last + 120) straddling frames_len
+            offs[n - 3] = last + 88
+            frames_len = last + 124
     return frames, frames_len, offs, olflags, rss, fdir, hint
 
 

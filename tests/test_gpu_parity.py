@@ -110,16 +110,19 @@ def test_gpu_fuzz_vs_oracle(g, orc, mode, flags, max_rt):
     assert (st == se).all(), (st, se)
 
 
-@pytest.mark.parametrize("misalign", ["mbuf", "mixed"])
+@pytest.mark.parametrize("misalign", ["mbuf", "mixed", "lineend"])
 @pytest.mark.parametrize("mode", [0, 1])
 def test_gpu_fuzz_misaligned_offsets(g, orc, misalign, mode):
     """Frame offsets that are not 16-B aligned: 8-B aligned like mbuf data in
-    the reference's ingress pool (element + 344, iokernel/defs.h:503-506), and
-    arbitrary byte shifts."""
-    rng = np.random.default_rng(9100 + 10 * mode + (misalign == "mixed"))
+    the reference's ingress pool (element + 344, iokernel/defs.h:503-506),
+    arbitrary byte shifts, and frames whose first 128-B line ends 40-56 bytes
+    in (header staged up to the line end; ARP's target IP and IPv4 options
+    read past it)."""
+    rng = np.random.default_rng(9100 + 10 * mode + (misalign == "mixed") + 2 * (misalign == "lineend"))
     rts = random_runtimes(rng, 1024, 300)
     n = 5000
-    frames, flen, offs, olf, rss, fdir, hint = fuzz_batch(rng, n, rts, 1024, misalign=misalign)
+    frames, flen, offs, olf, rss, fdir, hint = fuzz_batch(
+        rng, n, rts, 1024, slot=256 if misalign == "lineend" else 128, misalign=misalign)
     t = orc.Tables(1024, mode, g.CFG_TRANS_HASH, 0x09)
     apply_runtimes(t, rts)
     clf = g.Classifier(0, 1024, mode, g.CFG_TRANS_HASH, 0x09)
