@@ -137,25 +137,51 @@ __device__ __forceinline__ uint64_t frame_off(const KParams &k, uint64_t idx)
 }
 
 /*
- * Header bytes staged for a frame at @off: the 64-B granule, cut at the end of
- * its first 128-B line when that line still holds bytes [0, 40) -- Ethernet,
- * an IHL-5 IPv4 header and the L4 ports, all the common case reads.  An
- * 8-B-aligned frame starting in the last 40-63 bytes of a line (mbuf data at
- * element + 344 in the reference's 9408-B ingress elements lands at 88 mod
- * 128 every other slot, defs.h:503-506) then costs one line, not two; the
- * rare packets that need more (ARP's target IP at 38-41, IPv4 options) read
- * the rest directly (classify_one).  Returns 64 (whole granule) or 40/48/56.
+ * Where a frame's header is staged from (frames at per-packet offsets, or at
+ * a stride that is not a multiple of 16).  A 4-B-aligned frame is read as the
+ * 16-B-aligned 64-B window that starts @return (0-12) bytes before it: four
+ * 16-B loads instead of the eight or sixteen narrower ones an 8- or
+ * 4-B-aligned granule needs (mbuf data at element + 344 in the reference's
+ * ingress pool, defs.h:503-506, is 8-B aligned: 275 -> 216 us for 8 Mi random
+ * mbufs, profiles/r01_ingress_ab.jsonl).  The window is cut at the end of its
+ * first 128-B line (@cut < 64) when that line still holds frame bytes
+ * [0, 40) -- Ethernet, an IHL-5 IPv4 header and the L4 ports, all the common
+ * case reads -- so such a frame costs one line, not two; the rare packets
+ * that need more (ARP's target IP at 38-41, IPv4 options) read it directly
+ * (classify_one).  Frame bytes [0, @cut - @return) are staged.  Any other
+ * frame (@return 0xFF) is read bytewise from its own start, all 64 bytes.
  */
-__device__ __forceinline__ uint32_t hdr_avail(const KParams &k, uint64_t off)
+constexpr uint32_t kSpanFull = 64u << 8; /* no shift, 64 frame bytes staged */
+
+__device__ __forceinline__ uint32_t hdr_window(const KParams &k, uint64_t off, uint32_t &cut)
 {
 	const uint64_t A = (uint64_t)(uintptr_t)k.frames + off;
-	const uint32_t E = 128u - (uint32_t)(A & 127);
-	return ((A & 7) == 0 && E >= 40 && E < 64) ? E : 64u;
+	const uint32_t s = (uint32_t)(A & 15);
+	cut = 64;
+	if ((A & 3) != 0 || off < s)
+		return 0xFF;
+	const uint32_t Ew = 128u - (uint32_t)((A - s) & 127);
+	if (Ew < 64 && Ew >= s + 40)
+		cut = Ew;
+	return s;
 }
 
 template <bool GENERAL, int NT>
-__device__ __forceinline__ void load_tile(const KParams &k, uint64_t tile, uint4 r[4])
+__device__ __forceinline__ void load_tile(const KParams &k, uint64_t tile, uint4 r[4],
+                                          uint32_t &span)
 {
+	/* where this lane's own packet of the tile sits in its staged row
+	 * (hdr_window): shift | staged frame bytes << 8, for classify_one */
+	span = kSpanFull;
+	if (GENERAL) {
+		const uint64_t me = tile * NT + threadIdx.x;
+		if (me < k.n) {
+			uint32_t cut;
+			const uint32_t sh = hdr_window(k, frame_off<GENERAL>(k, me), cut);
+			if (sh != 0xFF)
+				span = sh | (cut - sh) << 8;
+		}
+	}
 	if (!GENERAL && (tile + 1) * NT <= k.n) {
 		/* full tile, every granule in range (checked on the host): no
 		 * per-lane predicate, four back-to-back 16-B loads per lane */
@@ -176,34 +202,27 @@ __device__ __forceinline__ void load_tile(const KParams &k, uint64_t tile, uint4
 		if (idx < k.n) {
 			const uint64_t off = frame_off<GENERAL>(k, idx);
 			const uint32_t q16 = (uint32_t)(c & 3) * 16;
-			const uint32_t e = GENERAL ? hdr_avail(k, off) : 64u;
-			uint64_t a = off + q16;
-			if (GENERAL && q16 >= e) {
-				/* past the frame's first line: left 0, read on demand */
-			} else if (GENERAL && q16 + 16 > e) {
-				/* the 8 bytes before the line end (e = q16 + 8) */
-				if (a + 8 <= k.frames_len) {
-					const gcl::u32x2v lo =
-					        __builtin_nontemporal_load((const gcl::u32x2v *)(k.frames + a));
-					v = make_uint4(lo.x, lo.y, 0, 0);
+			uint32_t cut = 64;
+			const uint32_t sh = GENERAL ? hdr_window(k, off, cut) : 0u;
+			if (!GENERAL) {
+				v = gcl::load16_nt(k.frames + off + q16);
+			} else if (sh != 0xFF) {
+				const uint64_t a = off - sh + q16; /* 16-B aligned */
+				if (q16 >= cut) {
+					/* past the first line: left 0, read on demand */
+				} else if (a + 16 <= k.frames_len) {
+					v = gcl::load16_nt(k.frames + a);
 				} else {
-					uint32_t w[2];
-					for (int b = 0; b < 2; b++)
+					uint32_t w[4];
+					for (int b = 0; b < 4; b++)
 						w[b] = frame_byte(k, a + 4 * b) |
 						       frame_byte(k, a + 4 * b + 1) << 8 |
 						       frame_byte(k, a + 4 * b + 2) << 16 |
 						       (uint32_t)frame_byte(k, a + 4 * b + 3) << 24;
-					v = make_uint4(w[0], w[1], 0, 0);
+					v = make_uint4(w[0], w[1], w[2], w[3]);
 				}
-			} else if (!GENERAL || (a + 16 <= k.frames_len && (a & 15) == 0)) {
-				v = gcl::load16_nt(k.frames + a);
-			} else if (a + 16 <= k.frames_len && (a & 7) == 0) {
-				/* mbuf data in the reference's ingress pool sits at
-				 * element + 344 (defs.h:503-506): 8-B aligned */
-				v = gcl::load16_a8(k.frames + a);
-			} else if (a + 16 <= k.frames_len && (a & 3) == 0) {
-				v = gcl::load16_a4(k.frames + a);
 			} else {
+				const uint64_t a = off + q16;
 				uint32_t w[4];
 				for (int b = 0; b < 4; b++)
 					w[b] = frame_byte(k, a + 4 * b) | frame_byte(k, a + 4 * b + 1) << 8 |
@@ -291,13 +310,28 @@ __device__ __forceinline__ uint32_t toeplitz_lut(const uint32_t *toep, uint32_t 
 template <int MODE, bool GENERAL, bool SYS = false>
 __device__ __forceinline__ void classify_one(const KParams &k, const uint4 *tile, int tid,
                                              uint64_t idx, const Tables &tb, uint32_t *hist,
-                                             Counters &cnt)
+                                             Counters &cnt, uint32_t span = kSpanFull)
 {
-	const uint4 w0 = tile[tile_slot(tid, 0)];
-	const uint4 w1 = tile[tile_slot(tid, 1)];
-	const uint4 w2 = tile[tile_slot(tid, 2)];
-	const uint32_t d3 = w0.w, d5 = w1.y, d6 = w1.z, d7 = w1.w;
-	const uint32_t d8 = w2.x, d9 = w2.y, d10 = w2.z;
+	/* frame byte b of this lane's header sits at tile byte b + sh, and frame
+	 * bytes [0, avail) are staged (hdr_window) */
+	const uint32_t sh = (GENERAL && !SYS) ? (span & 0xFF) : 0u;
+	const uint32_t avail = (GENERAL && !SYS) ? (span >> 8) : 64u;
+	uint32_t d3, d5, d6, d7, d8, d9, d10;
+	if (GENERAL && !SYS && sh != 0) {
+		d3 = tile_dword(tile, tid, 12 + sh);
+		d5 = tile_dword(tile, tid, 20 + sh);
+		d6 = tile_dword(tile, tid, 24 + sh);
+		d7 = tile_dword(tile, tid, 28 + sh);
+		d8 = tile_dword(tile, tid, 32 + sh);
+		d9 = tile_dword(tile, tid, 36 + sh);
+		d10 = tile_dword(tile, tid, 40 + sh);
+	} else {
+		const uint4 w0 = tile[tile_slot(tid, 0)];
+		const uint4 w1 = tile[tile_slot(tid, 1)];
+		const uint4 w2 = tile[tile_slot(tid, 2)];
+		d3 = w0.w, d5 = w1.y, d6 = w1.z, d7 = w1.w;
+		d8 = w2.x, d9 = w2.y, d10 = w2.z;
+	}
 
 	const uint32_t et = gcl::bswap16(d3 & 0xFFFF);              /* rx.c:154 */
 	const uint32_t ihl = (d3 >> 16) & 0xF;
@@ -308,7 +342,7 @@ __device__ __forceinline__ void classify_one(const KParams &k, const uint4 *tile
 	uint32_t arp_tip = gcl::bswap32(gcl::mid32(d9, d10));        /* rx.c:165-167 */
 	const uint32_t flags = (GENERAL && k.olflags) ? k.olflags[idx] : k.default_flags;
 	const bool is_ip = et == GCL_ETHTYPE_IP, is_arp = et == GCL_ETHTYPE_ARP;
-	if (GENERAL && !SYS && is_arp && hdr_avail(k, frame_off<GENERAL>(k, idx)) < 44) {
+	if (GENERAL && !SYS && is_arp && avail < 44) {
 		/* bytes 40-41 are past the staged line (load_tile) */
 		const uint64_t a = frame_off<GENERAL>(k, idx) + 38;
 		arp_tip = (uint32_t)frame_byte(k, a) << 24 | (uint32_t)frame_byte(k, a + 1) << 16 |
@@ -328,9 +362,8 @@ __device__ __forceinline__ void classify_one(const KParams &k, const uint4 *tile
 		                      (proto == 6 || proto == 17);
 		uint32_t sport = gcl::bswap16(d8 >> 16), dport = gcl::bswap16(d9 & 0xFFFF);
 		if (hashable && ihl != 5) {
-			if (ihl <= 11 && (!GENERAL || SYS ||
-			                  20 + 4 * ihl <= hdr_avail(k, frame_off<GENERAL>(k, idx)))) {
-				const int o = 14 + 4 * (int)ihl;
+			if (20 + 4 * ihl <= avail) { /* ihl <= 11 when avail == 64 */
+				const int o = 14 + 4 * (int)ihl + (int)sh;
 				sport = gcl::bswap16(tile_dword(tile, tid, o - 2) >> 16);
 				dport = gcl::bswap16(tile_dword(tile, tid, o + 2) & 0xFFFF);
 			} else { /* past the staged header bytes */
@@ -546,6 +579,7 @@ classify_kernel(KParams k)
 	const uint32_t x0 = blockIdx.x & (GCL_SCHED_XCD - 1);
 	uint32_t xs = x0; /* head this block dequeues from (thread 0 only) */
 	uint4 ra[4], rb[4];
+	uint32_t spa = kSpanFull, spb = kSpanFull;
 	uint64_t t = blockIdx.x;
 	/* static walk: tiles t, t + step, ... below t_end.  Default: tiles dealt
 	 * round-robin, so the whole chip sweeps one 16 MiB window of the batch.
@@ -570,9 +604,9 @@ classify_kernel(KParams k)
 			got = atomicAdd(&k.sched[x0 * GCL_SCHED_LINE], 1u);
 	}
 	if (t < t_end)
-		load_tile<GENERAL, NT>(k, t, ra);
+		load_tile<GENERAL, NT>(k, t, ra, spa);
 	if (DEPTH == 2 && t + step < t_end)
-		load_tile<GENERAL, NT>(k, t + step, rb);
+		load_tile<GENERAL, NT>(k, t + step, rb, spb);
 	if (dyn && tid == 0)
 		s_next[0] = t < k.ntiles ? sched_resolve(k.sched, k.ntiles, (uint32_t)G, x0, xs, got)
 		                         : k.ntiles;
@@ -580,6 +614,7 @@ classify_kernel(KParams k)
 
 	while (t < t_end) {
 		stage_tile<NT>(tile, ra);
+		const uint32_t sp = spa;
 		__syncthreads();
 		uint64_t nxt = t + DEPTH * step;
 		if (dyn) {
@@ -590,12 +625,12 @@ classify_kernel(KParams k)
 				got = atomicAdd(&k.sched[xs * GCL_SCHED_LINE], 1u);
 		}
 		if (nxt < t_end)
-			load_tile<GENERAL, NT>(k, nxt, ra); /* in flight while parsing */
+			load_tile<GENERAL, NT>(k, nxt, ra, spa); /* in flight while parsing */
 		if (k.ablate & 16) { /* timing only: the membench tile_v0 body */
 			const uint4 a = tile[tile_slot(tid, 0)], b = tile[tile_slot(tid, 1)];
 			*(u32x2 *)&k.verdicts[t * NT + tid] = u32x2{b.z ^ a.x, a.w ^ b.y};
 		} else if (t * NT + tid < k.n)
-			classify_one<MODE, GENERAL>(k, tile, tid, t * NT + tid, tb, hist, cnt);
+			classify_one<MODE, GENERAL>(k, tile, tid, t * NT + tid, tb, hist, cnt, sp);
 		if (dyn && tid == 0)
 			s_next[par ^ 1] = nxt < k.ntiles ? sched_resolve(k.sched, k.ntiles, (uint32_t)G,
 			                                                 x0, xs, got)
@@ -611,11 +646,12 @@ classify_kernel(KParams k)
 			if (t >= t_end)
 				break;
 			stage_tile<NT>(tile, rb);
+			const uint32_t sp2 = spb;
 			__syncthreads();
 			if (t + 2 * step < t_end)
-				load_tile<GENERAL, NT>(k, t + 2 * step, rb);
+				load_tile<GENERAL, NT>(k, t + 2 * step, rb, spb);
 			if (t * NT + tid < k.n)
-				classify_one<MODE, GENERAL>(k, tile, tid, t * NT + tid, tb, hist, cnt);
+				classify_one<MODE, GENERAL>(k, tile, tid, t * NT + tid, tb, hist, cnt, sp2);
 			__syncthreads();
 			t += step;
 		}

@@ -10,6 +10,7 @@ interleaved, so the difference between the rows is the access pattern alone:
   pool       the pool in address order, 64 times (sequential mbufs)
   sub16k     random over the first 16384 mbufs (154 MB, fits the MALL)
   sub1k      random over the first 1024 mbufs (9.6 MB, fits L2)
+  *_a16      the same, frames at element + 336 (16-B aligned loads)
 
     python tools/ingress_ab.py > gpurun_out/ingress_ab.jsonl
 """
@@ -35,6 +36,9 @@ def main(cycles=64, reps=10, rounds=3):
     pool_offs = torch.from_numpy(g.mbuf_data_offsets(P).view(np.int64)).to(dev)
     region = torch.zeros(g.mbuf_region_bytes(P), dtype=torch.uint8, device=dev)
     region[(pool_offs[:, None] + torch.arange(64, device=dev)).view(-1)] = hdr
+    # the same frames 8 bytes earlier (element + 336): 16-B aligned
+    region16 = torch.zeros_like(region)
+    region16[(pool_offs[:, None] - 8 + torch.arange(64, device=dev)).view(-1)] = hdr
     del hdr
     gen = torch.Generator(device="cpu").manual_seed(SEED)
     n = P * cycles
@@ -44,7 +48,9 @@ def main(cycles=64, reps=10, rounds=3):
         "sub16k": torch.randint(0, 16384, (n,), generator=gen),
         "sub1k": torch.randint(0, 1024, (n,), generator=gen),
     }
-    offs = {k: pool_offs[v.to(dev)].contiguous() for k, v in orders.items()}
+    offs = {k: (region, pool_offs[v.to(dev)].contiguous()) for k, v in orders.items()}
+    for k in ("random", "sub1k"):
+        offs[k + "_a16"] = (region16, offs[k][1] - 8)
     clf = classifier(dev, R, T, 4)
     setup_tables(clf, R, T)
     cnt = torch.zeros(R + g.NR_STATS, dtype=torch.int64, device=dev)
@@ -52,12 +58,12 @@ def main(cycles=64, reps=10, rounds=3):
     st = torch.cuda.current_stream().cuda_stream
     res = {k: [] for k in offs}
     for rnd in range(rounds):
-        for k, o in offs.items():
-            clf.classify(region, n, 0, verdicts=dv, counts=cnt[:R], stats=cnt[R:], offs=o, stream=st)
+        for k, (reg, o) in offs.items():
+            clf.classify(reg, n, 0, verdicts=dv, counts=cnt[:R], stats=cnt[R:], offs=o, stream=st)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for _ in range(reps):
-                clf.classify(region, n, 0, verdicts=dv, counts=cnt[:R], stats=cnt[R:], offs=o,
+                clf.classify(reg, n, 0, verdicts=dv, counts=cnt[:R], stats=cnt[R:], offs=o,
                              stream=st)
             torch.cuda.synchronize()
             res[k].append((time.perf_counter() - t0) / reps)
