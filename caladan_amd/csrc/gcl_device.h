@@ -19,24 +19,6 @@ __device__ __forceinline__ uint4 load16_nt(const void *p)
 	return make_uint4(v.x, v.y, v.z, v.w);
 }
 
-typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
-
-/* 16 bytes at an address that is only known to be @align-byte aligned
- * (align = 8 or 4), as naturally aligned narrower loads */
-__device__ __forceinline__ uint4 load16_a8(const void *p)
-{
-	const u32x2v a = __builtin_nontemporal_load((const u32x2v *)p);
-	const u32x2v b = __builtin_nontemporal_load((const u32x2v *)p + 1);
-	return make_uint4(a.x, a.y, b.x, b.y);
-}
-
-__device__ __forceinline__ uint4 load16_a4(const void *p)
-{
-	const uint32_t *q = (const uint32_t *)p;
-	return make_uint4(__builtin_nontemporal_load(q), __builtin_nontemporal_load(q + 1),
-	                  __builtin_nontemporal_load(q + 2), __builtin_nontemporal_load(q + 3));
-}
-
 /* System-scope (sc0 sc1) accesses for host memory the CPU rewrites while a
  * persistent kernel runs (the rx loop's burst slots, table images and the
  * frames of a recycled mbuf pool): they miss in every GPU cache, so a line
