@@ -519,6 +519,43 @@ def test_gpu_end_to_end_verdict2(g, orc, mode):
     assert (counts == ce).all() and (stats == se).all()
 
 
+@pytest.mark.parametrize("base", [4, 8, 12])
+def test_gpu_frames_base_misaligned(g, orc, base):
+    """A frames pointer that is itself only 4-B aligned: the staging window
+    (hdr_window) is placed by address, not by offset; frames within @base
+    bytes of the buffer start fall back to bytewise reads, and the window's
+    cut at a line end moves with the address."""
+    rng = np.random.default_rng(9300 + base)
+    rts = random_runtimes(rng, 1024, 300)
+    n = 4000
+    frames, flen, offs, olf, rss, fdir, hint = fuzz_batch(rng, n, rts, 1024, slot=256,
+                                                          misalign="lineend")
+    offs[0], offs[1], offs[2] = 0, 4, 8  # before any 16-B-aligned window start
+    t = orc.Tables(1024, 1, g.CFG_TRANS_HASH, 0x09)
+    apply_runtimes(t, rts)
+    clf = g.Classifier(0, 1024, 1, g.CFG_TRANS_HASH, 0x09)
+    apply_runtimes(clf, rts)
+    ve, ce, se, tre = t.classify(frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir_hi=fdir,
+                                 frames_len=flen, dst_hint=hint, trans=True)
+    big = torch.zeros(frames.nbytes + 64, dtype=torch.uint8, device="cuda")
+    big[base:base + frames.nbytes] = torch.from_numpy(frames).cuda()
+    f = big[base:base + frames.nbytes]
+    assert f.data_ptr() % 16 == base
+    v = torch.zeros(n * clf.vbytes, dtype=torch.uint8, device="cuda")
+    c = torch.zeros(clf.max_runtimes, dtype=torch.int64, device="cuda")
+    st = torch.zeros(g.NR_STATS, dtype=torch.int64, device="cuda")
+    tr = torch.zeros(n * 8, dtype=torch.uint8, device="cuda")
+    clf.classify(f, n, 0, verdicts=v, counts=c, stats=st, offs=dev(offs.astype(np.int64)),
+                 olflags=dev(olf), trans=tr, rss=dev(rss.view(np.int32)),
+                 fdir_hi=dev(fdir.astype(np.int32)), frames_len=flen,
+                 dst_hint=dev(hint.view(np.int32)))
+    torch.cuda.synchronize()
+    assert_same(v.cpu().numpy().view(g.verdict_dtype(clf.vbytes)), ve, f"base={base}")
+    assert (tr.cpu().numpy().view(g.TRANS_DTYPE) == tre).all()
+    assert (c.cpu().numpy().astype(np.uint64) == ce).all()
+    assert (st.cpu().numpy().astype(np.uint64) == se).all()
+
+
 def test_gpu_ingress_pool_geometry(g, orc):
     """Frames at their real place in the reference's ingress mbuf pool
     (9408-B elements, 222 per 2 MiB page, data at element + 344, so 8-B
