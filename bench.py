@@ -5,15 +5,17 @@ already resident in HBM (the rx_one_pkt loop of iokernel/rx.c:281-287 for a
 whole batch), plus -- with more than one GPU -- an RCCL all_gather of every
 rank's per-runtime packet counts and rx counters over xGMI.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling weak|strong]
     torchrun --nproc-per-node N bench.py --gpus N ...
 
 Rank 0 prints one JSON line.  Workload (configs[1] of BASELINE.json): 32 Mi
 synthetic 64-B Eth/IPv4/UDP frames per GPU, uniform 5-tuples, 16 runtimes x 8
 kthreads, JENKINS flow hash; packets are sharded round-robin across ranks in
-64 Ki-packet blocks (weak scaling: per-GPU work is fixed).  At N=1 the
-secondary config (1500-B TCP, Zipf-0.99 flows, 1024 runtimes) and the CPU
-baseline (the oracle's restatement of rx.c on this host's cores) are added.
+64 Ki-packet blocks.  --scaling weak (default) keeps 32 Mi packets per GPU;
+--scaling strong splits SURVEY §8(e)'s 256 Mi-packet batch (config 4) over
+the ranks.  At N=1 the secondary config (1500-B TCP, Zipf-0.99 flows, 1024
+runtimes), the integrated ingress-pool shape and the CPU baseline (the
+oracle's restatement of rx.c on this host's cores) are added.
 """
 import argparse
 import json
@@ -57,6 +59,8 @@ HDR_BYTES = 64
 # 1-4.5 % faster (profiles/r01_verdict_width_ab.jsonl) but carries 2 B/pkt
 # less, so its roofline fraction is no higher
 VERDICT_BYTES = 4
+# the secondary (config 3, 1500-B TCP) line's verdict: the 2-byte queue verdict
+SECONDARY_VERDICT_BYTES = 2
 VERDICT_NAMES = {8: "gcl_verdict, 8 B", 4: "gcl_verdict4, 4 B",
                  2: "queue verdict (GCL_CFG_VERDICT2), 2 B"}
 
@@ -69,9 +73,9 @@ def verdict_cfg(vbytes, R, T):
     return (g.CFG_VERDICT4 if vbytes == 4 else 0), 0
 
 
-def classifier(device, R, T, vbytes, extra_flags=0):
+def classifier(device, R, T, vbytes, extra_flags=0, hash_mode=g.HASH_JENKINS):
     fl, tb = verdict_cfg(vbytes, R, T)
-    return g.Classifier(device.index or 0, R, g.HASH_JENKINS, fl | extra_flags, thread_bits=tb)
+    return g.Classifier(device.index or 0, R, hash_mode, fl | extra_flags, thread_bits=tb)
 
 
 def log(*a):
@@ -123,8 +127,10 @@ def zero_fill(buf):
 
 
 class Workload:
-    def __init__(self, name, rank, world, device, hash_mode=g.HASH_JENKINS, vbytes=VERDICT_BYTES):
-        wl, n, stride, R, T, desc = WORKLOADS[name]
+    def __init__(self, name, rank, world, device, hash_mode=g.HASH_JENKINS, vbytes=VERDICT_BYTES,
+                 n=None):
+        wl, n_default, stride, R, T, desc = WORKLOADS[name]
+        n = n_default if n is None else n
         self.name, self.wl, self.n, self.stride, self.R, self.T, self.desc = name, wl, n, stride, R, T, desc
         self.vbytes = vbytes
         self.bytes_per_pkt = HDR_BYTES + vbytes
@@ -151,7 +157,7 @@ class Workload:
         g.generate(wl, n, stride, R, self.frames, seed=SEED, rank=rank, world=world,
                    shard_block=SHARD_BLOCK, zipf_cdf_dev=cdf_dev, nflows=nflows)
         fl, tb = verdict_cfg(vbytes, R, T)
-        self.clf = g.Classifier(device.index or 0, R, hash_mode, g.CFG_PROFILE | fl, thread_bits=tb)
+        self.clf = g.Classifier(device.index or 0, R, hash_mode, fl, thread_bits=tb)
         self.tables = setup_tables(self.clf, R, T)
         torch.cuda.synchronize()
 
@@ -160,8 +166,6 @@ class Workload:
                           counts=self.counts[:self.R], stats=self.counts[self.R:], stream=stream)
 
 
-# classify launches timed with HIP events: one in PROFILE_EVERY (gcl_profile_sample)
-PROFILE_EVERY = 5
 # steps per multi-GPU counts exchange: 8 udp64 steps = 3.5 ms, far fresher than
 # the iokernel's once-a-second stats dump, and the exchange's cross-stream
 # event packets (~13 us each on the compute queue) amortise to <0.5%
@@ -227,14 +231,20 @@ class Exchange:
         cur.wait_stream(self.comm)
 
 
-def run_timed(w, steps, warmup, world, ex=None, profile_every=PROFILE_EVERY):
-    stream = torch.cuda.current_stream().cuda_stream
+def run_timed(w, steps, warmup, world, ex=None):
+    """Warm up, then time exactly `steps` steps between a barrier +
+    synchronize on both sides.  Returns (wall seconds, max over ranks;
+    GPU ms per step, max over ranks): the second is a HIP event pair on the
+    launch stream around the timed steps, so it is the classify kernels'
+    back-to-back time (launch gaps included) and never exceeds the wall
+    time of a step."""
+    stream = torch.cuda.current_stream()
 
     def one():
         if ex is not None:
             ex.step(w)
         else:
-            w.step(stream)
+            w.step(stream.cuda_stream)
 
     for _ in range(warmup):
         one()
@@ -244,54 +254,78 @@ def run_timed(w, steps, warmup, world, ex=None, profile_every=PROFILE_EVERY):
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
-    w.clf.kernel_time(reset=True)
-    # HIP events around one launch in `profile_every` (the first one timed):
-    # a timed event pair costs the stream ~10 us, 2% of a udp64 step
-    w.clf.profile_sample(profile_every)
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    e0.record(stream)
     for _ in range(steps):
         one()
     if ex is not None:
         ex.drain()
+    e1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    kms, nl = w.clf.kernel_time(reset=True)
-    kms = kms / max(nl, 1)
-    if world > 1:  # the slowest rank's wall time and mean kernel time
-        t = torch.tensor([el, kms], dtype=torch.float64)
+    gpu_ms = e0.elapsed_time(e1) / steps
+    if world > 1:  # the slowest rank's wall time and GPU step time
+        t = torch.tensor([el, gpu_ms], dtype=torch.float64)
         if torch.distributed.get_backend() == "nccl":
             t = t.cuda()
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        el, kms = float(t[0].item()), float(t[1].item())
-    return el, kms
+        el, gpu_ms = float(t[0].item()), float(t[1].item())
+    return el, gpu_ms
+
+
+def pmc_traffic(name, vbytes):
+    """HBM bytes per launch from the committed PMC passes (profiles/pmc_*.json,
+    tools/prof_summary.py: FETCH_SIZE + WRITE_SIZE, gfx950-corrected)."""
+    prof = os.path.join(ROOT, "profiles", f"pmc_{name}{'' if vbytes == 8 else f'_v{vbytes}'}.json")
+    if not os.path.exists(prof):
+        return None
+    try:
+        with open(prof) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def roofline_obj(bytes_per_launch, kernel_ms, traffic, extra=None):
+    achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
+    r = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+         "kernel_ms": round(kernel_ms, 4)}
+    if extra:
+        r.update(extra)
+    if traffic:
+        moved = traffic / (kernel_ms * 1e-3) / 1e9
+        r["moved"] = {"achieved": round(moved, 1), "frac": round(moved / HBM_PEAK_GBS, 4),
+                      "what": "HBM bytes moved per launch (PMC traffic) / kernel time"}
+    return r
 
 
 def roofline(w, kernel_ms):
-    bytes_per_launch = w.n * w.bytes_per_pkt
-    achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
-    traffic = None
-    prof = os.path.join(ROOT, "profiles", f"pmc_{w.name}{'' if w.vbytes == 8 else f'_v{w.vbytes}'}.json")
-    if os.path.exists(prof):
-        try:
-            with open(prof) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            traffic = None
-    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "bytes_per_pkt": w.bytes_per_pkt, "kernel_ms": round(kernel_ms, 4)}
+    """The roofline object of one workload's classify launch.  The committed
+    PMC passes were taken at the workload's default batch size, so their
+    bytes are scaled per packet to this launch's (strong scaling)."""
+    traffic = pmc_traffic(w.name, w.vbytes)
+    if traffic is not None:
+        traffic = traffic / WORKLOADS[w.name][1] * w.n
+    return roofline_obj(w.n * w.bytes_per_pkt, kernel_ms, traffic,
+                        {"bytes_per_pkt": w.bytes_per_pkt})
 
 
 def placement(w):
-    """How the frame pool was placed against the verdict ring."""
-    pu = getattr(w.frames, "probe_us", None)
-    if pu is None:
+    """How the frame pool was placed against the verdict ring
+    (gcl_dev_alloc_paired: DESIGN.md §4 "Buffer placement")."""
+    info = getattr(w.frames, "pair_info", None)
+    if info is None:
         return {"policy": "plain hipMalloc"}
     return {"policy": "gcl_dev_alloc_paired (frame pool placed against the verdict ring)",
-            "probe_us_chosen": round(pu[0], 2), "probe_us_worst": round(pu[1], 2)}
+            **info,
+            "class_chosen": ("fast (cross-class pair: both classes seen)" if info["classes_seen"] == 2
+                             else "unknown (one class in every candidate)")}
 
 
 def e2e_bench(device, vbytes=VERDICT_BYTES, reps=3):
@@ -340,13 +374,13 @@ def e2e_bench(device, vbytes=VERDICT_BYTES, reps=3):
     return out
 
 
-def e2e_multi(device, rank, world, vbytes, reps=3):
+def e2e_multi(device, rank, world, vbytes, reps=3, n=256 << 10, keep=None):
     """Config 5 on N GPUs: every rank classifies its round-robin shard of the
     mixed jumbo trace from pinned host memory, PCIe zero-copy and header
     DMA-gather; barrier + max-over-ranks timing, RX_PULLED summed over ranks
-    as the accounting check.  PCIe-inclusive: never `value`."""
+    as the accounting check.  PCIe-inclusive: never `value`.  `keep` (a dict,
+    tests) receives this rank's last verdicts and its accumulated stats."""
     wl, _, stride, R, T, _ = WORKLOADS["mixed"]
-    n = 256 << 10
     dfr = torch.zeros(n * stride, dtype=torch.uint8, device=device)
     g.generate(wl, n, stride, R, dfr, seed=SEED, rank=rank, world=world, shard_block=SHARD_BLOCK)
     hfr = torch.empty(n * stride, dtype=torch.uint8).pin_memory()
@@ -379,6 +413,8 @@ def e2e_multi(device, rank, world, vbytes, reps=3):
     torch.distributed.all_reduce(pulled)
     res["rx_pulled_check"] = "ok" if int(pulled.item()) == world * n * calls else \
         f"MISMATCH {int(pulled.item())} != {world * n * calls}"
+    if keep is not None:
+        keep.update(verdicts=hv.numpy().copy(), stats=stats.copy(), calls=calls, n=n)
     del hfr, hv, clf
     torch.cuda.empty_cache()
     return res
@@ -458,17 +494,44 @@ def rxloop_bench(device, vbytes, iters=2000):
     return out
 
 
+def timed_launches(fn, reps):
+    """(wall s, GPU ms) per call of `fn` over `reps` back-to-back calls on the
+    current stream, after one untimed call."""
+    fn()
+    torch.cuda.synchronize()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / reps, e0.elapsed_time(e1) / reps
+
+
+# Algorithmic bytes of the integrated rx_burst shape (INTEGRATION.md §4), per
+# packet: the 64-B header granule + the descriptor's u64 offset into the mbuf
+# pool + u8 ol_flags + u32 hash.rss + the verdict.
+INGRESS_DESC_BYTES = 8 + 1 + 4
+
+
 def ingress_pool_bench(device, vbytes, cycles=64, reps=10):
     """Frames where the reference keeps them (§8f-2): the 131072-mbuf ingress
     pool, 9408-B elements, 222 per 2 MiB page, frame data at element + 344
     (8-B aligned; iokernel/defs.h:70, :503-523).  A batch is `cycles` random
     passes over the pool (descriptor i -> offs[i], like rte_eth_rx_burst
-    handing back recycled mbufs).  Device-resident (pool in HBM) and PCIe
-    zero-copy (pool in pinned host memory, as the shm region would be)."""
+    handing back recycled mbufs), each descriptor with the mbuf's ol_flags
+    and hash.rss, classified in GCL_HASH_NIC mode -- the integrated rx_burst
+    replacement of INTEGRATION.md §4.  Device-resident (pool in HBM, with a
+    roofline) and PCIe zero-copy (pool in pinned host memory, as the shm
+    region would be).  The JENKINS row with offsets only is kept beside it."""
     wl, _, _, R, T, _ = WORKLOADS["udp64"]
     P = g.IOKERNEL_NUM_MBUFS
     hdr = torch.zeros(P * 64, dtype=torch.uint8, device=device)
-    g.generate(wl, P, 64, R, hdr, seed=SEED)
+    olf_p = torch.zeros(P, dtype=torch.uint8, device=device)
+    rss_p = torch.zeros(P, dtype=torch.int32, device=device)
+    g.generate(wl, P, 64, R, hdr, olflags=olf_p, rss=rss_p, seed=SEED)
     pool_offs = torch.from_numpy(g.mbuf_data_offsets(P).view(np.int64)).to(device)
     region = torch.zeros(g.mbuf_region_bytes(P), dtype=torch.uint8, device=device)
     region[(pool_offs[:, None] + torch.arange(64, device=device)).view(-1)] = hdr
@@ -476,40 +539,57 @@ def ingress_pool_bench(device, vbytes, cycles=64, reps=10):
     gen = torch.Generator(device="cpu").manual_seed(SEED)
     order = torch.cat([torch.randperm(P, generator=gen) for _ in range(cycles)]).to(device)
     offs = pool_offs[order].contiguous()
+    olf = olf_p[order].contiguous()
+    rss = rss_p[order].contiguous()
     n = offs.numel()
-    clf = classifier(device, R, T, vbytes)
-    setup_tables(clf, R, T)
+    out = {"mbufs": P, "pkts_per_batch": n, "frame_data_offset": "element + 344 (8-B aligned)",
+           "descriptor_order": f"{cycles} random permutations of the pool"}
     cnt = torch.zeros(R + g.NR_STATS, dtype=torch.int64, device=device)
     dv = torch.empty(n * vbytes, dtype=torch.uint8, device=device)
     st = torch.cuda.current_stream().cuda_stream
+    nic = classifier(device, R, T, vbytes, hash_mode=g.HASH_NIC)
+    setup_tables(nic, R, T)
 
-    def dev_step():
-        clf.classify(region, n, 0, verdicts=dv, counts=cnt[:R], stats=cnt[R:], offs=offs, stream=st)
+    def nic_step():
+        nic.classify(region, n, 0, verdicts=dv, counts=cnt[:R], stats=cnt[R:], offs=offs,
+                     olflags=olf, rss=rss, stream=st)
 
-    dev_step()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        dev_step()
-    torch.cuda.synchronize()
-    dt_dev = (time.perf_counter() - t0) / reps
+    wall, gms = timed_launches(nic_step, reps)
     ok = int(cnt[:R].sum().item()) == n * (reps + 1)
+    bpp = HDR_BYTES + INGRESS_DESC_BYTES + vbytes
+    out["integrated_nic"] = {
+        "what": "offs[] + ol_flags[] + hash.rss[] per descriptor, GCL_HASH_NIC (INTEGRATION.md §4)",
+        "device_resident_mpps": round(n / wall / 1e6, 1), "counts_check": "ok" if ok else "MISMATCH",
+        "roofline": roofline_obj(n * bpp, gms, pmc_traffic("ingress_nic", vbytes),
+                                 {"bytes_per_pkt": bpp})}
+    cnt.zero_()
+    jen = classifier(device, R, T, vbytes)
+    setup_tables(jen, R, T)
+
+    def jen_step():
+        jen.classify(region, n, 0, verdicts=dv, counts=cnt[:R], stats=cnt[R:], offs=offs, stream=st)
+
+    wall_j, gms_j = timed_launches(jen_step, reps)
+    okj = int(cnt[:R].sum().item()) == n * (reps + 1)
+    out["jenkins_offs_only"] = {"device_resident_mpps": round(n / wall_j / 1e6, 1),
+                                "kernel_ms": round(gms_j, 4), "counts_check": "ok" if okj else "MISMATCH"}
     # zero-copy: the pool in pinned host memory, descriptors and verdicts too
     hreg = torch.empty(region.numel(), dtype=torch.uint8).pin_memory()
     hreg.copy_(region)
     del region
     hoffs = offs.cpu().pin_memory()
+    holf = olf.cpu().pin_memory()
+    hrss = rss.cpu().pin_memory()
     hv = torch.empty(n * vbytes, dtype=torch.uint8).pin_memory()
-    clf.classify_host(hreg, n, 0, verdicts=hv, offs=hoffs, mode=g.E2E_ZEROCOPY)
+    kw = dict(verdicts=hv, offs=hoffs, olflags=holf, rss=hrss, mode=g.E2E_ZEROCOPY)
+    nic.classify_host(hreg, n, 0, **kw)
     t0 = time.perf_counter()
     for _ in range(3):
-        clf.classify_host(hreg, n, 0, verdicts=hv, offs=hoffs, mode=g.E2E_ZEROCOPY)
-    dt_zc = (time.perf_counter() - t0) / 3
-    del hreg, hoffs, hv, offs, dv, clf
+        nic.classify_host(hreg, n, 0, **kw)
+    out["integrated_nic"]["zerocopy_mpps"] = round(n / ((time.perf_counter() - t0) / 3) / 1e6, 1)
+    del hreg, hoffs, holf, hrss, hv, offs, olf, rss, dv, nic, jen
     torch.cuda.empty_cache()
-    return {"mbufs": P, "pkts_per_batch": n, "frame_data_offset": "element + 344 (8-B aligned)",
-            "device_resident_mpps": round(n / dt_dev / 1e6, 1), "counts_check": "ok" if ok else "MISMATCH",
-            "zerocopy_mpps": round(n / dt_zc / 1e6, 1)}
+    return out
 
 
 def trace_replay(device, n=64 << 10, reps=3):
@@ -555,10 +635,22 @@ def trace_replay(device, n=64 << 10, reps=3):
             "wire_bytes_rate_GBs": round(float(pl.astype(np.float64).sum()) / dt / 1e9, 1)}
 
 
+# The GPU box's CPU share for one GPU (the pool's rule for worker pools;
+# os.cpu_count() there reports the whole host)
+BOX_CPU_SHARE = 16
+
+
 def cpu_baseline(budget_s=12.0):
-    """The oracle's rx.c restatement on this host (TEST INFRASTRUCTURE as the
-    checker/baseline only).  Sample: the first 2 Mi packets of the udp64
-    stream (identical bytes to the GPU's), bursts of 64, prefetch stride 2."""
+    """rx.c's per-packet work on this host's cores, timed on the oracle's
+    restatement (TEST INFRASTRUCTURE, used here only as the baseline):
+    rx_one_pkt with rx.c's direct header-struct loads (rx.c:127-167), bursts
+    of 64 with prefetch stride 2 (rx.c:281-287), -O3 -march=native.
+      nic_mode     hash.rss from the NIC (rx.c:83) -- what rx.c computes per
+                   packet, the `value`;
+      jenkins_mode the 13-B lookup3 flow hash computed on the CPU, the same
+                   work as the GPU headline.
+    Sample: the first 2 Mi packets of the udp64 stream (identical bytes to
+    the GPU's) with the generator's ol_flags and NIC hashes."""
     from oracle import orc
     try:
         orc.build(native=True)
@@ -568,23 +660,40 @@ def cpu_baseline(budget_s=12.0):
         native = False
     wl, _, stride, R, T, _ = WORKLOADS["udp64"]
     n = 2 << 20
-    frames, _, _ = orc.generate(wl, n, stride, R, seed=SEED, native=native)
-    t = orc.Tables(R, g.HASH_JENKINS, 0, g.F_RSS_HASH | g.F_IP_CKSUM_GOOD, native=native)
-    rng = np.random.default_rng(SEED)
-    for r in range(R):
-        act = int(rng.integers(1, T + 1))
-        idx = [int(x) for x in rng.choice(T, size=act, replace=False)]
-        t.runtime_set(r, orc.runtime_ip(r), T, act, orc.steer_flows(T, idx))
-    probe = t.bench(frames, n, stride, threads=1, passes=1)
-    passes = max(1, int(budget_s * 0.45 / max(probe, 1e-6)))
-    s1 = t.bench(frames, n, stride, threads=1, passes=passes)
-    rate1 = n * passes / s1 / 1e6
-    s_l = t.bench(frames, n, stride, threads=1, passes=max(1, passes // 2), lrpc=True)
-    rate_l = n * max(1, passes // 2) / s_l / 1e6
-    threads = min(16, os.cpu_count() or 1)
-    pm = max(1, int(budget_s * 0.25 / max(probe / threads, 1e-6)))
-    sm = t.bench(frames, n, stride, threads=threads, passes=pm)
-    rate_m = n * pm / sm / 1e6
+    frames, olf, rss = orc.generate(wl, n, stride, R, seed=SEED, native=native)
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        avail = os.cpu_count() or 1
+    threads = max(1, min(BOX_CPU_SHARE, avail))
+
+    def tables(mode):
+        t = orc.Tables(R, mode, 0, g.F_RSS_HASH | g.F_IP_CKSUM_GOOD, native=native)
+        rng = np.random.default_rng(SEED)
+        for r in range(R):
+            act = int(rng.integers(1, T + 1))
+            idx = [int(x) for x in rng.choice(T, size=act, replace=False)]
+            t.runtime_set(r, orc.runtime_ip(r), T, act, orc.steer_flows(T, idx))
+        return t
+
+    spent = 0.0
+    res = {}
+    for name, mode, share in (("nic_mode", g.HASH_NIC, 0.5), ("jenkins_mode", g.HASH_JENKINS, 0.5)):
+        t = tables(mode)
+        kw = dict(olflags=olf, rss=rss, direct=True)
+        probe = t.bench(frames, n, stride, threads=1, passes=1, **kw)
+        budget = budget_s * share
+        p1 = max(1, int(budget * 0.45 / max(probe, 1e-6)))
+        s1 = t.bench(frames, n, stride, threads=1, passes=p1, **kw)
+        pl = max(1, p1 // 2)
+        sl = t.bench(frames, n, stride, threads=1, passes=pl, lrpc=True, **kw)
+        pm = max(1, int(budget * 0.3 / max(probe / threads, 1e-6)))
+        sm = t.bench(frames, n, stride, threads=threads, passes=pm, **kw)
+        spent += probe + s1 + sl + sm
+        res[name] = {"1core_mpps": round(n * p1 / s1 / 1e6, 2),
+                     "1core_lrpc_mpps": round(n * pl / sl / 1e6, 2),
+                     "all_cores_mpps": round(n * pm / sm / 1e6, 2), "all_cores": threads,
+                     "passes": [p1, pl, pm]}
     cpu_model = ""
     try:
         with open("/proc/cpuinfo") as f:
@@ -595,14 +704,35 @@ def cpu_baseline(budget_s=12.0):
     except OSError:
         pass
     return {
-        "value": round(rate1, 2), "unit": "Mpkt/s", "cores": 1, "kind": "port",
-        "sample": f"first {n} pkts of the udp64 stream x {passes} passes, classify-only "
-                  f"(rx_one_pkt restatement, bursts of 64, -O3 -march={'native' if native else 'x86-64-v2'})",
-        "lrpc_1core_mpps": round(rate_l, 2),
-        "all_cores": {"value": round(rate_m, 2), "cores": threads, "passes": pm},
-        "cpu_model": cpu_model, "nproc": os.cpu_count(),
-        "seconds": round(probe + s1 + s_l + sm, 2),
+        "value": res["nic_mode"]["1core_mpps"], "unit": "Mpkt/s", "cores": 1, "kind": "port",
+        "sample": (f"first {n} pkts of the udp64 stream, classify-only rx_one_pkt restatement with "
+                   f"rx.c's direct header loads and the NIC's hash.rss (rx.c:83), bursts of 64, "
+                   f"prefetch stride 2, -O3 -march={'native' if native else 'x86-64-v2'}"),
+        "nic_mode": res["nic_mode"], "jenkins_mode": res["jenkins_mode"],
+        "all_cores_note": (f"{threads} threads: the GPU box's CPU share for one GPU "
+                           f"(min({BOX_CPU_SHARE}, {avail} CPUs in this process's affinity mask)); "
+                           f"the host reports nproc={os.cpu_count()}"),
+        "cpu_model": cpu_model, "nproc": os.cpu_count(), "seconds": round(spent, 2),
     }
+
+
+STRONG_TOTAL_PKTS = 256 << 20
+
+
+def pick_device(local, world, allow_shared):
+    """One process per GPU: rank -> LOCAL_RANK's device.  More ranks than
+    visible GPUs is refused (two ranks on one GPU would halve each one's
+    bandwidth and read as bad scaling) unless --allow-shared-gpu, which only
+    the single-GPU rehearsals (gloo) use."""
+    ndev = torch.cuda.device_count()
+    if ndev == 0:
+        raise SystemExit("bench.py: no GPU visible")
+    if local >= ndev:
+        if not allow_shared:
+            raise SystemExit(f"bench.py: LOCAL_RANK {local} but only {ndev} GPU(s) visible; "
+                             f"refusing to put two ranks on one GPU (--allow-shared-gpu to rehearse)")
+        return local % ndev
+    return local
 
 
 def main():
@@ -611,14 +741,18 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="udp64", choices=sorted(WORKLOADS))
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak: 32 Mi packets per GPU; strong: --total-pkts split over the ranks")
+    ap.add_argument("--total-pkts", type=int, default=STRONG_TOTAL_PKTS,
+                    help="strong scaling: packets per step over all ranks (default 256 Mi)")
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo only to rehearse N>1 on one GPU")
-    ap.add_argument("--profile-every", type=int, default=PROFILE_EVERY,
-                    help="time one classify launch in N with HIP events (roofline.kernel_ms)")
+    ap.add_argument("--allow-shared-gpu", action="store_true",
+                    help="rehearsal only: let several ranks share a GPU")
     ap.add_argument("--exchange-every", type=int, default=EXCHANGE_EVERY,
                     help="steps per counts all_gather (multi-GPU exchange period)")
     ap.add_argument("--verdict-bytes", type=int, default=VERDICT_BYTES, choices=[2, 4, 8],
@@ -632,18 +766,23 @@ def main():
     rank, world, local = shard.dist_env()
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    ndev = torch.cuda.device_count()
-    dev_index = local % ndev
+    dev_index = pick_device(local, world, args.allow_shared_gpu)
     torch.cuda.set_device(dev_index)
     device = torch.device("cuda", dev_index)
     dist_on = world > 1 or args.force_exchange
     if dist_on:
-        shard.init(rank, world, backend=args.dist_backend)
+        shard.init(rank, world, backend=args.dist_backend, device=device)
 
     vb = args.verdict_bytes
-    w = Workload(args.workload, rank, world, device, vbytes=vb)
+    n_rank = None
+    if args.scaling == "strong":
+        if args.total_pkts % (world * SHARD_BLOCK):
+            raise SystemExit(f"bench.py: --total-pkts {args.total_pkts} is not a multiple of "
+                             f"{world} ranks x {SHARD_BLOCK}-packet shard blocks")
+        n_rank = args.total_pkts // world
+    w = Workload(args.workload, rank, world, device, vbytes=vb, n=n_rank)
     ex = Exchange(w, world, device, args.exchange_every) if dist_on else None
-    el, kms = run_timed(w, args.steps, args.warmup, world, ex, max(1, args.profile_every))
+    el, gms = run_timed(w, args.steps, args.warmup, world, ex)
     total_pkts = w.n * world * args.steps
     value = total_pkts / el / 1e6
     # correctness spot check: every packet of every step was accounted for
@@ -653,7 +792,16 @@ def main():
     else:
         tot = w.counts[:w.R].sum().item()
         expect = w.n * (args.steps + args.warmup)
+    counts_ok = tot == expect
+    # kernel-only next to the exchange-inclusive step: the same
+    # steps without the all_gather, barrier + max-over-ranks timed
+    if ex is not None:
+        el_k, gms_k = run_timed(w, args.steps, 2, world, None)
+    else:
+        el_k, gms_k = el, gms
     w_n = w.n
+    scaling_desc = (f"weak: {w.n} pkts per GPU" if args.scaling == "weak" else
+                    f"strong: {args.total_pkts} pkts per step over {world} GPU(s), {w.n} per GPU")
     result = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -663,70 +811,78 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(el / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic",
         "config": {"workload": f"{args.workload}: {w.desc}", "pkts_per_gpu": w.n,
                    "slot_stride": w.stride, "runtimes": w.R, "kthreads": w.T,
                    "hash": "jenkins (lookup3 13-B 5-tuple)",
-                   "verdict": VERDICT_NAMES[vb],
+                   "verdict": VERDICT_NAMES[vb], "scaling": scaling_desc,
                    "parallelism": (f"dp{world}: round-robin 64Ki-pkt shards, {args.dist_backend} "
                                    f"all_gather of per-runtime counts every {args.exchange_every} step(s), overlapped"
                                    if dist_on else "single GPU")},
-        "roofline": roofline(w, kms),
+        "roofline": roofline(w, gms_k),
+        "kernel_only": {
+            "value": round(w_n * world * args.steps / el_k / 1e6, 1), "unit": "Mpkt/s",
+            "ms_per_step": round(el_k / args.steps * 1e3, 4), "gpu_ms_per_step": round(gms_k, 4),
+            "what": ("the same classify steps without the counts all_gather, barrier + "
+                     "max-over-ranks timed" if ex is not None else
+                     "N=1 without an exchange: the step is the classify launch")},
         "placement": placement(w),
-        "counts_check": "ok" if tot == expect else f"MISMATCH {tot} != {expect}",
+        "counts_check": "ok" if counts_ok else f"MISMATCH {tot} != {expect}",
     }
-    del w
+    if ex is not None:
+        result["exchange"] = {"gpu_ms_per_step": round(gms, 4), "period_steps": args.exchange_every,
+                              "periods": ex.k}
+    del w, ex
     torch.cuda.empty_cache()
 
-    if world == 1 and not args.no_secondary and args.workload == "udp64":
+    if world == 1 and not args.no_secondary and args.workload == "udp64" and args.scaling == "weak":
         # the same udp64 step with the other verdict formats
         other = []
         for ob in (b for b in (8, 4, 2) if b != vb):
             w4 = Workload(args.workload, rank, world, device, vbytes=ob)
-            el4, kms4 = run_timed(w4, args.steps, 3, 1)
+            el4, gms4 = run_timed(w4, args.steps, 3, 1)
             other.append({"verdict": VERDICT_NAMES[ob],
                           "value": round(w4.n * args.steps / el4 / 1e6, 1), "unit": "Mpkt/s",
-                          "ms_per_step": round(el4 / args.steps * 1e3, 4), "roofline": roofline(w4, kms4),
+                          "ms_per_step": round(el4 / args.steps * 1e3, 4), "roofline": roofline(w4, gms4),
                           "placement": placement(w4)})
             del w4
             torch.cuda.empty_cache()
-        w2 = Workload("tcp1500", rank, world, device, vbytes=vb)
-        el2, kms2 = run_timed(w2, max(20, args.steps // 2), 3, 1)
         steps2 = max(20, args.steps // 2)
+        sec = {}
+        # config 3 leads with the 2-byte queue verdict (1024 runtimes x 4
+        # kthreads fit thread_bits 2): 174 vs 180 us for the 4-byte one on
+        # the same buffers (profiles/r02_defer_ab.jsonl)
+        for vb2 in (SECONDARY_VERDICT_BYTES,) + tuple(b for b in (vb,) if b != SECONDARY_VERDICT_BYTES):
+            w2 = Workload("tcp1500", rank, world, device, vbytes=vb2)
+            el2, gms2 = run_timed(w2, steps2, 3, 1)
+            sec[vb2] = {"verdict": VERDICT_NAMES[vb2],
+                        "value": round(w2.n * steps2 / el2 / 1e6, 1), "unit": "Mpkt/s",
+                        "ms_per_step": round(el2 / steps2 * 1e3, 4), "steps": steps2,
+                        "roofline": roofline(w2, gms2), "placement": placement(w2),
+                        "frame_bytes_rate_GBs": round(w2.n * 1500 / (gms2 * 1e-3) / 1e9, 1)}
+            del w2
+            torch.cuda.empty_cache()
         w3 = Workload("tcp1500_hsplit", rank, world, device, vbytes=vb)
-        el3, kms3 = run_timed(w3, steps2, 2, 1)
+        el3, gms3 = run_timed(w3, steps2, 2, 1)
         hsplit = {"workload": f"tcp1500_hsplit: {w3.desc}",
                   "value": round(w3.n * steps2 / el3 / 1e6, 1), "unit": "Mpkt/s",
-                  "roofline": roofline(w3, kms3), "placement": placement(w3)}
+                  "roofline": roofline(w3, gms3), "placement": placement(w3)}
         del w3
-        result["secondary"] = {
-            "workload": f"tcp1500: {w2.desc}",
-            "value": round(w2.n * steps2 / el2 / 1e6, 1), "unit": "Mpkt/s",
-            "ms_per_step": round(el2 / steps2 * 1e3, 4), "steps": steps2,
-            "roofline": roofline(w2, kms2),
-            "placement": placement(w2),
-            "frame_bytes_rate_GBs": round(w2.n * 1500 / (kms2 * 1e-3) / 1e9, 1),
-            "header_split_layout": hsplit,
-            "udp64_other_verdicts": other,
-        }
-        del w2
         torch.cuda.empty_cache()
+        result["secondary"] = {"workload": f"tcp1500: {WORKLOADS['tcp1500'][5]}",
+                               **sec[SECONDARY_VERDICT_BYTES],
+                               "other_verdicts": [sec[b] for b in sec if b != SECONDARY_VERDICT_BYTES],
+                               "header_split_layout": hsplit, "udp64_other_verdicts": other}
 
-    if world == 1 and not args.no_e2e and args.workload == "udp64":
+    if world == 1 and not args.no_e2e and args.workload == "udp64" and args.scaling == "weak":
         result["e2e"] = e2e_bench(device, vb)
 
     if world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(args.cpu_budget)
-    if dist_on:
-        # kernel-only next to kernel + all_gather (= value)
-        result["kernel_only"] = {
-            "value": round(w_n * world / (kms * 1e-3) / 1e6, 1), "unit": "Mpkt/s",
-            "what": ("all ranks' packets per step / the slowest rank's mean classify kernel "
-                     "time, HIP-event timed (1 launch in --profile-every; the event pair adds "
-                     "~10 us, so this can read below value at N=1)")}
+        result["cpu_baseline"]["gpu_over_1core_nic"] = round(value / result["cpu_baseline"]["value"], 1)
     if world > 1 and not args.no_e2e:
         result["e2e_multi"] = e2e_multi(device, rank, world, vb)
     if dist_on:

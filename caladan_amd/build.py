@@ -61,5 +61,30 @@ def build(force=False, verbose_resources=False):
     return OUT
 
 
+SANITIZE_FLAGS = ["-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+                  "-fno-omit-frame-pointer", "-static-libasan", "-g", "-O1"]
+
+
+def build_sanitized(out_dir=None):
+    """Host-only CPU build of the C that parses untrusted input -- the pcap
+    loader (csrc/gcl_pcap.c), the verdict post-pass (csrc/gcl_host.c) and the
+    oracle's classifier (oracle/orc.c, test infrastructure) -- under ASan +
+    UBSan, linked into the fuzz driver tests/fuzz/host_fuzz.c.  No HIP code is
+    compiled: GPU code is never built with sanitizers here.  Returns the
+    driver's path."""
+    out_dir = out_dir or os.path.join(ROOT, "build", "sanitize")
+    os.makedirs(out_dir, exist_ok=True)
+    exe = os.path.join(out_dir, "host_fuzz")
+    srcs = [os.path.join(ROOT, "tests", "fuzz", "host_fuzz.c"), os.path.join(CSRC, "gcl_host.c"),
+            os.path.join(CSRC, "gcl_pcap.c"), os.path.join(ROOT, "oracle", "orc.c")]
+    if _stale(exe, srcs + [os.path.join(CSRC, d) for d in DEPS]):
+        _run(["gcc", "-std=gnu11", "-Wall", "-Wno-unused-parameter", *SANITIZE_FLAGS,
+              "-o", exe, *srcs, "-lm", "-lpthread"])
+    return exe
+
+
 if __name__ == "__main__":
-    build(force="--force" in sys.argv, verbose_resources="--resources" in sys.argv)
+    if "--sanitize" in sys.argv:
+        print(build_sanitized())
+    else:
+        build(force="--force" in sys.argv, verbose_resources="--resources" in sys.argv)

@@ -209,8 +209,15 @@ static bool send_to_runtime(struct gcl_host_proc *p, uint32_t hash, int slot, in
 {
 	int th;
 
+	/* verdicts come from device memory: a thread or flow_tbl slot outside
+	 * the runtime's thread_count (a stale or corrupted verdict) is refused
+	 * like a full ring, never used as an index */
+	if (p->thread_count == 0 || p->thread_count > GCL_NCPU)
+		return false;
 	if (slot < 0)
-		slot = p->thread_count ? (int)(hash % p->thread_count) : 0;
+		slot = (int)(hash % p->thread_count);
+	else if (slot >= p->thread_count)
+		return false;
 	if (gpu_thread >= 0) {
 		th = gpu_thread;
 	} else if (p->active_thread_count > 0) {

@@ -14,12 +14,16 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/stat.h>
 
 #include "../../include/gcl_pcap.h"
 
 #define PCAP_MAGIC_US 0xA1B2C3D4u
 #define PCAP_MAGIC_NS 0xA1B23C4Du
 #define LINKTYPE_ETHERNET 1
+/* largest capture accepted: pkt_len is the u16 rte_pktmbuf_pkt_len, and the
+ * largest frame the reference handles is ETH_MAX_LEN_JUMBO (inc/net/ethernet.h:18) */
+#define PCAP_MAX_INCL 0xFFFFu
 
 struct pcap_file_hdr {
 	uint32_t magic;
@@ -73,10 +77,10 @@ int gcl_pcap_load(const char *path, struct gcl_trace *t, uint64_t max_pkts)
 {
 	struct pcap_file_hdr fh;
 	struct pcap_rec_hdr rh;
+	struct stat st;
 	FILE *f;
 	int swap, ns, ret = 0;
-	uint64_t n = 0, bytes = 0, cap_pkts, cap_bytes;
-	long data_start;
+	uint64_t n = 0, bytes = 0, cap_pkts, cap_bytes, pos, fsize;
 
 	if (!path || !t)
 		return -EINVAL;
@@ -84,9 +88,14 @@ int gcl_pcap_load(const char *path, struct gcl_trace *t, uint64_t max_pkts)
 	f = fopen(path, "rb");
 	if (!f)
 		return -errno;
-	if (fread(&fh, sizeof(fh), 1, f) != 1) {
+	if (fstat(fileno(f), &st) || !S_ISREG(st.st_mode)) {
 		fclose(f);
 		return -EINVAL;
+	}
+	fsize = (uint64_t)st.st_size;
+	if (fread(&fh, sizeof(fh), 1, f) != 1) {
+		fclose(f);
+		return -EPROTO;
 	}
 	swap = fh.magic == bswap32_(PCAP_MAGIC_US) || fh.magic == bswap32_(PCAP_MAGIC_NS);
 	if (swap) {
@@ -100,17 +109,24 @@ int gcl_pcap_load(const char *path, struct gcl_trace *t, uint64_t max_pkts)
 		return -EPROTO;
 	}
 	ns = fh.magic == PCAP_MAGIC_NS;
-	data_start = ftell(f);
+	pos = sizeof(fh);
 
-	/* pass 1: size the packed buffer */
-	while (fread(&rh, sizeof(rh), 1, f) == 1 && (!max_pkts || n < max_pkts)) {
+	/* pass 1: size the packed buffer; every record must lie inside the file
+	 * (fseek past EOF succeeds, so the bound is checked against its size) */
+	while ((!max_pkts || n < max_pkts) && fread(&rh, sizeof(rh), 1, f) == 1) {
 		uint32_t incl = swap ? bswap32_(rh.incl_len) : rh.incl_len;
-		if (incl > 0x40000 || fseek(f, incl, SEEK_CUR)) {
+		pos += sizeof(rh);
+		if (incl > PCAP_MAX_INCL || incl > fsize - pos || fseeko(f, incl, SEEK_CUR)) {
 			fclose(f);
 			return -EPROTO;
 		}
+		pos += incl;
 		bytes += align_up(incl ? incl : 1, 16);
 		n++;
+	}
+	if ((!max_pkts || n < max_pkts) && pos != fsize) { /* a cut-off record header */
+		fclose(f);
+		return -EPROTO;
 	}
 	cap_pkts = n ? n : 1;
 	cap_bytes = bytes + GCL_PCAP_TAIL_PAD;
@@ -126,8 +142,14 @@ int gcl_pcap_load(const char *path, struct gcl_trace *t, uint64_t max_pkts)
 	t->alloc_len = align_up(cap_bytes, 1 << 21);
 	memset(t->frames, 0, t->alloc_len);
 
-	/* pass 2: copy frames to 16-B-aligned offsets */
-	fseek(f, data_start, SEEK_SET);
+	/* pass 2: copy frames to 16-B-aligned offsets.  The records are re-read,
+	 * so each one is bounded again against the buffer pass 1 sized: a file
+	 * rewritten in between gives -EPROTO, never a write past the buffer. */
+	if (fseeko(f, sizeof(fh), SEEK_SET)) {
+		fclose(f);
+		gcl_pcap_free(t);
+		return -EIO;
+	}
 	uint64_t off = 0;
 	for (uint64_t i = 0; i < n; i++) {
 		if (fread(&rh, sizeof(rh), 1, f) != 1) {
@@ -138,15 +160,20 @@ int gcl_pcap_load(const char *path, struct gcl_trace *t, uint64_t max_pkts)
 		uint32_t orig = swap ? bswap32_(rh.orig_len) : rh.orig_len;
 		uint32_t sec = swap ? bswap32_(rh.ts_sec) : rh.ts_sec;
 		uint32_t frac = swap ? bswap32_(rh.ts_frac) : rh.ts_frac;
+		uint64_t sz = align_up(incl ? incl : 1, 16);
+		if (incl > PCAP_MAX_INCL || sz > bytes - off) {
+			ret = -EPROTO;
+			break;
+		}
 		if (incl && fread(t->frames + off, 1, incl, f) != incl) {
 			ret = -EIO;
 			break;
 		}
 		t->offs[i] = off;
-		t->pkt_len[i] = (uint16_t)(incl > 0xFFFF ? 0xFFFF : incl);
+		t->pkt_len[i] = (uint16_t)incl;
 		t->orig_len[i] = orig;
 		t->ts_ns[i] = (uint64_t)sec * 1000000000ull + (ns ? frac : (uint64_t)frac * 1000ull);
-		off += align_up(incl ? incl : 1, 16);
+		off += sz;
 	}
 	fclose(f);
 	if (ret) {

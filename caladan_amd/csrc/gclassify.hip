@@ -56,6 +56,12 @@ constexpr int kDefaultXcdMap = 0; /* GCL_TUNE_XCD_MAP default: round-robin tiles
  * verdict widths, tcp1500 2-2.4 %, the header-split layout unchanged
  * (profiles/r01_verdict_store_ab.jsonl) */
 constexpr int kDefaultVerdictStore = 2;
+/* GCL_TUNE_DEFER default: verdicts stored at the end of their own tile.
+ * Issuing them one tile late (before the next tile's loads, 1) measured
+ * udp64 1-3 % slower and tcp1500 0.4 % faster, same buffers, one process
+ * (profiles/r02_defer_ab.jsonl), so the store latency is not what the
+ * verdict stream costs */
+constexpr int kDefaultDefer = 0;
 
 /* tuning knobs for experiments (GCL_TUNE_BLOCKS_PER_CU caps the grid) */
 static int g_tune_bpc = 0;
@@ -95,6 +101,7 @@ struct KParams {
 	uint32_t off_seed, off_crc;
 	uint32_t *sched; /* tile queue slot (SchedSlot) or NULL = static persistent grid */
 	uint32_t xcd_map; /* static grid: 1 = each XCD walks one contiguous eighth of the tiles */
+	uint32_t defer;   /* 1: a tile's verdicts are stored after the next tile's barrier */
 };
 
 /* Dynamic tile queue of one launch: tiles are dealt per XCD (tile t belongs
@@ -137,8 +144,9 @@ __device__ __forceinline__ uint64_t frame_off(const KParams &k, uint64_t idx)
 }
 
 /*
- * Where a frame's header is staged from (frames at per-packet offsets, or at
- * a stride that is not a multiple of 16).  A 4-B-aligned frame is read as the
+ * Where a frame's header is staged from (frames at per-packet offsets; a
+ * slot stride is always a multiple of 16, gcl_classify_ex refuses any
+ * other).  A 4-B-aligned frame is read as the
  * 16-B-aligned 64-B window that starts @return (0-12) bytes before it: four
  * 16-B loads instead of the eight or sixteen narrower ones an 8- or
  * 4-B-aligned granule needs (mbuf data at element + 344 in the reference's
@@ -308,9 +316,9 @@ __device__ __forceinline__ uint32_t toeplitz_lut(const uint32_t *toep, uint32_t 
  * probe chain longer than one slot -- take a divergent branch.
  */
 template <int MODE, bool GENERAL, bool SYS = false>
-__device__ __forceinline__ void classify_one(const KParams &k, const uint4 *tile, int tid,
-                                             uint64_t idx, const Tables &tb, uint32_t *hist,
-                                             Counters &cnt, uint32_t span = kSpanFull)
+__device__ __forceinline__ uint64_t classify_one(const KParams &k, const uint4 *tile, int tid,
+                                                 uint64_t idx, const Tables &tb, uint32_t *hist,
+                                                 Counters &cnt, uint32_t span = kSpanFull)
 {
 	/* frame byte b of this lane's header sits at tile byte b + sh, and frame
 	 * bytes [0, avail) are staged (hdr_window) */
@@ -472,24 +480,34 @@ __device__ __forceinline__ void classify_one(const KParams &k, const uint4 *tile
 		/* q = uniqid << thread_bits | thread (thread_bits in cflags[31:24]) */
 		const uint32_t a = action & GCL_ACT_MASK;
 		const uint32_t q = uniq << (k.cflags >> 24) | thr;
-		const uint32_t v2 = a == GCL_ACT_DELIVER ? q
-		                  : a == GCL_ACT_WAKE ? GCL_V2_WAKE | q : GCL_V2_OTHER | a;
+		return a == GCL_ACT_DELIVER ? q : a == GCL_ACT_WAKE ? GCL_V2_WAKE | q : GCL_V2_OTHER | a;
+	}
+	if (k.cflags & GCL_CFG_VERDICT4)
+		return vlo;
+	return (uint64_t)vlo << 32 | hash;
+}
+
+/* Store verdict word @w (classify_one) of packet @idx in the context's
+ * verdict format and store policy. */
+__device__ __forceinline__ void put_verdict(const KParams &k, uint64_t idx, uint64_t w)
+{
+	if (k.cflags & GCL_CFG_VERDICT2) {
 		if (k.nt_store == 2)
-			__hip_atomic_store((uint16_t *)k.verdicts + idx, (uint16_t)v2, __ATOMIC_RELAXED,
+			__hip_atomic_store((uint16_t *)k.verdicts + idx, (uint16_t)w, __ATOMIC_RELAXED,
 			                   __HIP_MEMORY_SCOPE_SYSTEM);
 		else
-			((uint16_t *)k.verdicts)[idx] = (uint16_t)v2;
+			((uint16_t *)k.verdicts)[idx] = (uint16_t)w;
 	} else if (k.cflags & GCL_CFG_VERDICT4) {
 		if (k.nt_store == 2) /* write-through (sc0 sc1), kDefaultVerdictStore */
-			__hip_atomic_store((uint32_t *)k.verdicts + idx, vlo, __ATOMIC_RELAXED,
+			__hip_atomic_store((uint32_t *)k.verdicts + idx, (uint32_t)w, __ATOMIC_RELAXED,
 			                   __HIP_MEMORY_SCOPE_SYSTEM);
 		else
-			((uint32_t *)k.verdicts)[idx] = vlo;
+			((uint32_t *)k.verdicts)[idx] = (uint32_t)w;
 	} else {
-		const u32x2 vd = {hash, vlo};
+		const u32x2 vd = {(uint32_t)w, (uint32_t)(w >> 32)};
 		if (k.nt_store == 2)
-			__hip_atomic_store((uint64_t *)k.verdicts + idx, (uint64_t)vlo << 32 | hash,
-			                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+			__hip_atomic_store((uint64_t *)k.verdicts + idx, w, __ATOMIC_RELAXED,
+			                   __HIP_MEMORY_SCOPE_SYSTEM);
 		else if (k.nt_store)
 			__builtin_nontemporal_store(vd, (u32x2 *)&k.verdicts[idx]);
 		else
@@ -611,11 +629,32 @@ classify_kernel(KParams k)
 		s_next[0] = t < k.ntiles ? sched_resolve(k.sched, k.ntiles, (uint32_t)G, x0, xs, got)
 		                         : k.ntiles;
 	int par = 0;
+	/* Deferred verdict stores (k.defer, GCL_TUNE_DEFER=1): on gfx950 stores
+	 * count in vmcnt, and the compiler waits vmcnt(0) for the next tile's
+	 * loads at the top of the loop, so a verdict store issued at the end of a
+	 * tile is waited for right away.  Held in a register and issued after the
+	 * next tile's barrier, before that tile's loads, it completes while the
+	 * tile is parsed.  Measured no faster (kDefaultDefer), kept as a knob. */
+	uint64_t pend_w = 0, pend_i = ~0ull;
+	auto flush = [&]() {
+		if (pend_i != ~0ull)
+			put_verdict(k, pend_i, pend_w);
+		pend_i = ~0ull;
+	};
+	auto verdict = [&](uint64_t idx, uint64_t w) {
+		if (k.defer) {
+			pend_w = w;
+			pend_i = idx;
+		} else {
+			put_verdict(k, idx, w);
+		}
+	};
 
 	while (t < t_end) {
 		stage_tile<NT>(tile, ra);
 		const uint32_t sp = spa;
 		__syncthreads();
+		flush();
 		uint64_t nxt = t + DEPTH * step;
 		if (dyn) {
 			nxt = s_next[par];
@@ -630,7 +669,8 @@ classify_kernel(KParams k)
 			const uint4 a = tile[tile_slot(tid, 0)], b = tile[tile_slot(tid, 1)];
 			*(u32x2 *)&k.verdicts[t * NT + tid] = u32x2{b.z ^ a.x, a.w ^ b.y};
 		} else if (t * NT + tid < k.n)
-			classify_one<MODE, GENERAL>(k, tile, tid, t * NT + tid, tb, hist, cnt, sp);
+			verdict(t * NT + tid, classify_one<MODE, GENERAL>(k, tile, tid, t * NT + tid, tb, hist,
+			                                                  cnt, sp));
 		if (dyn && tid == 0)
 			s_next[par ^ 1] = nxt < k.ntiles ? sched_resolve(k.sched, k.ntiles, (uint32_t)G,
 			                                                 x0, xs, got)
@@ -648,14 +688,17 @@ classify_kernel(KParams k)
 			stage_tile<NT>(tile, rb);
 			const uint32_t sp2 = spb;
 			__syncthreads();
+			flush();
 			if (t + 2 * step < t_end)
 				load_tile<GENERAL, NT>(k, t + 2 * step, rb, spb);
 			if (t * NT + tid < k.n)
-				classify_one<MODE, GENERAL>(k, tile, tid, t * NT + tid, tb, hist, cnt, sp2);
+				verdict(t * NT + tid, classify_one<MODE, GENERAL>(k, tile, tid, t * NT + tid, tb,
+				                                                  hist, cnt, sp2));
 			__syncthreads();
 			t += step;
 		}
 	}
+	flush();
 	uint32_t n_flowtag = cnt.flowtag, n_hashmiss = cnt.hashmiss;
 	uint32_t n_unreg = cnt.unreg, n_unhandled = cnt.unhandled;
 
@@ -910,7 +953,8 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 			k.fdir = (fl & GCL_LOOP_F_FDIR) ? cur.fdir : nullptr;
 			k.dst_hint = (fl & GCL_LOOP_F_HINT) ? cur.hint : nullptr;
 			if ((uint32_t)tid < m) {
-				classify_one<MODE, true, true>(k, tile, tid, (uint64_t)tid, tb, hist, cnt);
+				put_verdict(k, (uint64_t)tid,
+				            classify_one<MODE, true, true>(k, tile, tid, (uint64_t)tid, tb, hist, cnt));
 				const bool v4 = L.cflags & GCL_CFG_VERDICT4, v2 = L.cflags & GCL_CFG_VERDICT2;
 				const uint32_t hsh = v4 || v2 ? 0u : s_verd[tid].x;
 				const uint32_t vlo = v2 ? ((const uint16_t *)s_verd)[tid]
@@ -1163,6 +1207,7 @@ struct gcl_ctx {
 	int tune_ablate;   /* GCL_TUNE_ABLATE bitmask (timing experiments only) */
 	int tune_sched;    /* GCL_TUNE_SCHED: 0 static persistent grid, 1 dynamic tile queue */
 	int tune_xcd_map;  /* GCL_TUNE_XCD_MAP: 1 contiguous eighth per XCD, 0 round-robin tiles */
+	int tune_defer;    /* GCL_TUNE_DEFER: 1 verdict stores one tile late, 0 at once (default) */
 	/* dynamic tile queue: one slot per launch in flight, reused in turn; a
 	 * launch waits for the previous user of its slot (same or other stream) */
 	uint32_t *sched;
@@ -1246,6 +1291,8 @@ extern "C" int gcl_open(int hip_device, const struct gcl_cfg *cfg, struct gcl_ct
 		c->tune_sched = e ? atoi(e) : kDefaultSched;
 		e = getenv("GCL_TUNE_XCD_MAP");
 		c->tune_xcd_map = e ? atoi(e) : kDefaultXcdMap;
+		e = getenv("GCL_TUNE_DEFER");
+		c->tune_defer = e ? atoi(e) : kDefaultDefer;
 	}
 	c->dimg[0] = c->dimg[1] = nullptr;
 	c->sched = nullptr;
@@ -1794,6 +1841,7 @@ extern "C" int gcl_classify_ex(struct gcl_ctx *c, const struct gcl_batch *b,
 	k.nt_store = c->tune_nt_store;
 	k.ablate = c->tune_ablate;
 	k.xcd_map = c->tune_xcd_map;
+	k.defer = c->tune_defer;
 
 	/* the specialised fast path needs every header granule in range */
 	bool general = b->offs || b->olflags || b->fdir_hi || b->dst_hint ||
@@ -2004,6 +2052,9 @@ __global__ void __launch_bounds__(256) pair_probe_kernel(const uint8_t *rd, uint
 	}
 }
 
+/* the probe stores to at most this much of the written side */
+constexpr size_t kPairProbeWriteMax = 256ull << 20;
+
 /* min over 3 timed launches of the probe (after one untimed), microseconds;
  * negative on a HIP error */
 double pair_probe(const uint8_t *rd, size_t rd_bytes, uint32_t *wr, size_t wr_bytes, hipStream_t s,
@@ -2013,7 +2064,7 @@ double pair_probe(const uint8_t *rd, size_t rd_bytes, uint32_t *wr, size_t wr_by
 	 * pool against a 128 MiB verdict ring is 0.35-0.4 ms): a probe of the
 	 * first 512 MiB against the first 32 MiB missed the class on some boxes */
 	const uint64_t ntiles = std::min<size_t>(rd_bytes, 4ull << 30) / (256 * 64);
-	const uint64_t wtiles = std::min<size_t>(wr_bytes, 256ull << 20) / (256 * 4);
+	const uint64_t wtiles = std::min<size_t>(wr_bytes, kPairProbeWriteMax) / (256 * 4);
 	if (!ntiles || !wtiles)
 		return -1;
 	double best = 1e30;
@@ -2042,14 +2093,19 @@ double pair_probe(const uint8_t *rd, size_t rd_bytes, uint32_t *wr, size_t wr_by
 
 } /* namespace */
 
-/* The class gap: same-class pairs measured 13-18% slower than cross-class
- * ones (406 vs 343 us classify, 390 vs 354 us in the probe's shape at full
- * size); run-to-run noise of one probe is under 1.5%. */
+/* The class gap: same-class pairs measured 12-18% slower than cross-class
+ * ones (406 vs 343 us classify; 375-382 vs 330-341 us in the probe's shape at
+ * full size, profiles/r02_classmap.jsonl); run-to-run noise of one probe is
+ * under 1.5%. */
 constexpr double kPairGap = 0.06;
+/* Of the free device memory at entry, at most this share is held by
+ * candidates and spacers while searching (all but the kept buffer are freed
+ * before returning). */
+constexpr double kPairHoldShare = 0.6;
 
 extern "C" int gcl_dev_alloc_paired(int hip_device, size_t bytes, const void *partner,
                                     size_t partner_bytes, uint32_t flags, void **out,
-                                    double *probe_us)
+                                    struct gcl_pair_info *info)
 {
 	const bool new_reads = flags == GCL_PAIR_NEW_READS;
 	if (!out || !bytes || !partner || !partner_bytes ||
@@ -2064,6 +2120,10 @@ extern "C" int gcl_dev_alloc_paired(int hip_device, size_t bytes, const void *pa
 	int cus = 0;
 	if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, hip_device) != hipSuccess)
 		return -ENODEV;
+	size_t free_b = 0, total_b = 0;
+	if (hipMemGetInfo(&free_b, &total_b) != hipSuccess)
+		return -ENODEV;
+	const size_t hold_cap = (size_t)((double)free_b * kPairHoldShare);
 	hipStream_t s;
 	hipEvent_t e0, e1;
 	if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess)
@@ -2075,22 +2135,36 @@ extern "C" int gcl_dev_alloc_paired(int hip_device, size_t bytes, const void *pa
 	const bool dbg = getenv("GCL_PAIR_DEBUG") != nullptr;
 	std::vector<std::pair<void *, double>> cand;
 	std::vector<void *> spacers;
-	int ret = 0;
+	size_t held = 0, spacer_held = 0;
+	int ret = 0, nspacers = 0, classes = 1;
 	for (int i = 0; i < GCL_PAIR_TRIES; i++) {
 		void *p = nullptr;
-		if (i && i % GCL_PAIR_RUN == 0) { /* one class so far: step past the run */
+		if (i && i % GCL_PAIR_RUN == 0) {
+			/* one class so far: step past the run.  Runs of one class span
+			 * 4-34 GiB of consecutive allocations (profiles/r02_classmap.jsonl),
+			 * so the spacer grows: 2, 4, 8, then 16 x @bytes */
+			size_t sp_bytes = bytes * (2ull << std::min(nspacers, 3));
+			if (held + sp_bytes + bytes > hold_cap)
+				sp_bytes = hold_cap > held + 2 * bytes ? hold_cap - held - bytes : 0;
 			void *sp = nullptr;
-			if (hipMalloc(&sp, 2 * bytes) == hipSuccess)
+			if (sp_bytes && hipMalloc(&sp, sp_bytes) == hipSuccess) {
 				spacers.push_back(sp);
-			else
+				held += sp_bytes;
+				spacer_held += sp_bytes;
+				nspacers++;
+			} else {
 				(void)hipGetLastError();
+			}
 			if (dbg)
-				fprintf(stderr, "gcl_dev_alloc_paired: spacer %p\n", sp);
+				fprintf(stderr, "gcl_dev_alloc_paired: spacer %p (%zu MiB)\n", sp, sp_bytes >> 20);
 		}
+		if (held + bytes > hold_cap && !cand.empty())
+			break;
 		if (hipMalloc(&p, bytes) != hipSuccess) {
 			(void)hipGetLastError();
 			break;
 		}
+		held += bytes;
 		const double us = new_reads
 		        ? pair_probe((const uint8_t *)p, rd_bytes, (uint32_t *)partner, wr_bytes, s, e0, e1, cus)
 		        : pair_probe((const uint8_t *)partner, rd_bytes, (uint32_t *)p, wr_bytes, s, e0, e1, cus);
@@ -2107,8 +2181,10 @@ extern "C" int gcl_dev_alloc_paired(int hip_device, size_t bytes, const void *pa
 			lo = std::min(lo, c.second);
 			hi = std::max(hi, c.second);
 		}
-		if (hi > lo * (1 + kPairGap))
+		if (hi > lo * (1 + kPairGap)) {
+			classes = 2;
 			break; /* both classes seen */
+		}
 	}
 	size_t best = 0;
 	double worst = 0;
@@ -2130,9 +2206,18 @@ extern "C" int gcl_dev_alloc_paired(int hip_device, size_t bytes, const void *pa
 	if (cand.empty())
 		return -ENOMEM;
 	*out = cand[best].first;
-	if (probe_us) {
-		probe_us[0] = cand[best].second;
-		probe_us[1] = worst;
+	if (classes == 1 && !getenv("GCL_PAIR_QUIET"))
+		fprintf(stderr, "gcl_dev_alloc_paired: warning: one placement class in %zu candidates "
+		        "(%.1f-%.1f us, %zu MiB of spacers); the pair may be the slow one\n",
+		        cand.size(), cand[best].second, worst, spacer_held >> 20);
+	if (info) {
+		memset(info, 0, sizeof(*info));
+		info->chosen_us = cand[best].second;
+		info->worst_us = worst;
+		info->candidates = (uint32_t)cand.size();
+		info->classes = (uint32_t)classes;
+		info->spacer_bytes = spacer_held;
+		info->probe_write_bytes = std::min<size_t>(wr_bytes, kPairProbeWriteMax);
 	}
 	return 0;
 }
@@ -2572,13 +2657,12 @@ extern "C" int64_t gcl_rxloop_submit(struct gcl_rxloop *L, uint32_t n, const uin
 		uint8_t *hd = s + L->lp.off_hdr;
 		for (uint32_t i = 0; i < n; i++, hd += GCL_HDR_GRANULE) {
 			const uint64_t o = offs[i];
-			if (o + GCL_HDR_GRANULE <= L->region_len) {
-				memcpy(hd, L->region + o, GCL_HDR_GRANULE);
-			} else {
-				const uint64_t k = o < L->region_len ? L->region_len - o : 0;
+			/* no o + granule: an offset near UINT64_MAX must not wrap past the check */
+			const uint64_t k = o < L->region_len ? std::min<uint64_t>(L->region_len - o, GCL_HDR_GRANULE) : 0;
+			if (k)
 				memcpy(hd, L->region + o, k);
+			if (k < GCL_HDR_GRANULE)
 				memset(hd + k, 0, GCL_HDR_GRANULE - k);
-			}
 		}
 	}
 	if (olflags) {

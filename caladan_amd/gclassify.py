@@ -28,7 +28,7 @@ CFG_AZURE_ARP, CFG_HASH16, CFG_PROFILE, CFG_TRANS_HASH, CFG_VERDICT4 = 0x1, 0x2,
 CFG_VERDICT2 = 0x20
 # GCL_CFG_VERDICT2: u16 q = uniqid << thread_bits | thread; kind in the top two bits
 V2_Q_MASK, V2_KIND, V2_DELIVER, V2_WAKE, V2_OTHER, V2_QUEUES = 0x3FFF, 0xC000, 0, 0x4000, 0xC000, 0x4000
-PAIR_NEW_READS, PAIR_NEW_WRITES, PAIR_TRIES, PAIR_RUN = 0x1, 0x2, 12, 3
+PAIR_NEW_READS, PAIR_NEW_WRITES, PAIR_TRIES, PAIR_RUN = 0x1, 0x2, 24, 2
 
 F_RSS_HASH, F_FDIR_ID = 0x01, 0x02
 F_IP_CKSUM_MASK, F_IP_CKSUM_UNKNOWN, F_IP_CKSUM_BAD = 0x0C, 0x00, 0x04
@@ -105,6 +105,12 @@ class GclE2eOpts(ctypes.Structure):
 
 
 E2E_COPY, E2E_ZEROCOPY = 0, 1
+
+
+class GclPairInfo(ctypes.Structure):
+    _fields_ = [("chosen_us", ctypes.c_double), ("worst_us", ctypes.c_double),
+                ("candidates", ctypes.c_uint32), ("classes", ctypes.c_uint32),
+                ("spacer_bytes", ctypes.c_uint64), ("probe_write_bytes", ctypes.c_uint64)]
 
 
 class GclRxloopCfg(ctypes.Structure):
@@ -199,7 +205,7 @@ def _load():
         "gcl_rxloop_stop": (i32, [vp]),
         "gcl_rxloop_drive": (i32, [vp, u32, vp, u32, u32, vp, ctypes.POINTER(u64)]),
         "gcl_dev_alloc_paired": (i32, [i32, ctypes.c_size_t, vp, ctypes.c_size_t, u32,
-                                       ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_double)]),
+                                       ctypes.POINTER(vp), ctypes.POINTER(GclPairInfo)]),
         "gcl_host_unregister": (i32, [vp]),
         "gcl_pcap_write": (i32, [ctypes.c_char_p, vp, u64, vp, vp, vp, u64, u32]),
         "gcl_pcap_load": (i32, [ctypes.c_char_p, ctypes.POINTER(GclTrace), u64]),
@@ -247,6 +253,18 @@ def _nbytes(x):
     return x.nbytes
 
 
+def _frames_len(frames, frames_len):
+    """The readable length the kernel is given: the whole buffer, or a
+    caller's shorter limit -- never more than the buffer holds (the kernel
+    trusts it as the bound of every frame read)."""
+    size = _nbytes(frames)
+    if frames_len is None:
+        return size
+    if frames_len < 0 or frames_len > size:
+        raise ValueError(f"frames_len {frames_len} exceeds the {size}-byte frame buffer")
+    return frames_len
+
+
 def jenkins_hash(key: bytes) -> int:
     return lib.gcl_jenkins_hash(key, len(key))
 
@@ -290,14 +308,20 @@ class DeviceBuffer:
         new_reads: the new buffer is the frame (read) side."""
         p = ctypes.c_void_p()
         self.probe_us = None
+        self.pair_info = None
         if partner is None:
             _check(lib.gcl_dev_alloc(device, nbytes, ctypes.byref(p)), "gcl_dev_alloc")
         else:
-            us = (ctypes.c_double * 2)()
+            info = GclPairInfo()
             _check(lib.gcl_dev_alloc_paired(device, nbytes, _ptr(partner), _nbytes(partner),
                                             PAIR_NEW_READS if new_reads else PAIR_NEW_WRITES,
-                                            ctypes.byref(p), us), "gcl_dev_alloc_paired")
-            self.probe_us = (us[0], us[1])
+                                            ctypes.byref(p), ctypes.byref(info)), "gcl_dev_alloc_paired")
+            self.probe_us = (info.chosen_us, info.worst_us)
+            self.pair_info = {"probe_us_chosen": round(info.chosen_us, 2),
+                              "probe_us_worst": round(info.worst_us, 2),
+                              "candidates": info.candidates, "classes_seen": info.classes,
+                              "spacer_MiB": info.spacer_bytes >> 20,
+                              "probe_write_bytes": info.probe_write_bytes}
         self.ptr, self.nbytes = p.value, nbytes
 
     def data_ptr(self):
@@ -492,7 +516,7 @@ class Classifier:
             if arr is not None and _nbytes(arr) < w * n:
                 raise ValueError("per-packet array too small")
         b = GclBatch(frames=_ptr(frames),
-                     frames_len=_nbytes(frames) if frames_len is None else frames_len,
+                     frames_len=_frames_len(frames, frames_len),
                      stride=stride, offs=_ptr(offs), olflags=_ptr(olflags), rss=_ptr(rss),
                      fdir_hi=_ptr(fdir_hi), pkt_len=None, n=n, dst_hint=_ptr(dst_hint))
         if trans is not None and _nbytes(trans) < 8 * n:
@@ -509,7 +533,7 @@ class Classifier:
         if verdicts is not None and _nbytes(verdicts) < self.vbytes * n:
             raise ValueError("verdict buffer too small")
         b = GclBatch(frames=_ptr(frames),
-                     frames_len=_nbytes(frames) if frames_len is None else frames_len,
+                     frames_len=_frames_len(frames, frames_len),
                      stride=stride, offs=_ptr(offs), olflags=_ptr(olflags), rss=_ptr(rss),
                      fdir_hi=_ptr(fdir_hi), pkt_len=None, n=n, dst_hint=_ptr(dst_hint))
         o = GclE2eOpts(mode=mode, nstreams=nstreams, chunk=chunk)

@@ -20,10 +20,13 @@ def dist_env():
     return rank, world, local
 
 
-def init(rank, world, backend="nccl"):
+def init(rank, world, backend="nccl", device=None):
+    """Join the process group.  With nccl (RCCL) the rank's GPU is bound at
+    init (`device`), so barriers and collectives use it, never a guess."""
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29511")
-    dist.init_process_group(backend, rank=rank, world_size=world)
+    kw = {"device_id": device} if backend == "nccl" and device is not None else {}
+    dist.init_process_group(backend, rank=rank, world_size=world, **kw)
 
 
 def finish():

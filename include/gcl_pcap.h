@@ -28,8 +28,11 @@ struct gcl_trace {
 /*
  * gcl_pcap_load - read a classic pcap file (either byte order, micro- or
  * nanosecond timestamps, LINKTYPE_ETHERNET) into @t; at most @max_pkts
- * packets (0 = all).  Returns 0, -EPROTO (not an Ethernet pcap), -ENOMEM,
- * -EIO or -errno from fopen.
+ * packets (0 = all).  Returns 0, -EPROTO (not an Ethernet pcap, a record
+ * running past the end of the file, a cut-off record header, or a capture
+ * longer than 65535 bytes -- pkt_len is a u16, and the largest frame the
+ * reference handles is ETH_MAX_LEN_JUMBO), -EINVAL (not a regular file),
+ * -ENOMEM, -EIO or -errno from fopen.
  */
 int gcl_pcap_load(const char *path, struct gcl_trace *t, uint64_t max_pkts);
 void gcl_pcap_free(struct gcl_trace *t);

@@ -109,9 +109,14 @@ struct gcl_batch {
 	uint64_t        frames_len; /* readable bytes at frames; reads past it see 0 */
 	uint64_t        stride;     /* slot stride when offs == NULL (multiple of 16) */
 	const uint64_t *offs;       /* optional u64[n] frame start offsets, any alignment:
-	                               16-B aligned is one 16-B load per granule chunk,
-	                               8-B aligned (the reference's mbuf data, element
-	                               + 344, iokernel/defs.h:503-506) two 8-B loads */
+	                               a 4-B-aligned frame (16-B aligned, or the
+	                               reference's mbuf data at element + 344,
+	                               iokernel/defs.h:503-506) is staged as the
+	                               16-B-aligned 64-B window starting up to 12 B
+	                               before it (four 16-B loads), cut at the first
+	                               128-B line end when that line holds frame
+	                               bytes 0-39; any other alignment is read byte
+	                               by byte */
 	const uint8_t  *olflags;    /* optional u8[n]  GCL_F_* per packet */
 	const uint32_t *rss;        /* optional u32[n] buf->hash.rss (NIC mode) */
 	const uint32_t *fdir_hi;    /* optional u32[n] buf->hash.fdir.hi (FDIR mark) */
@@ -422,27 +427,39 @@ int gcl_dev_free(void *p);
  * The class cannot be read from a virtual address, so this allocates a
  * candidate, times a read+write probe of the classify kernel's access shape
  * over the whole of both buffers (up to 4 GiB read, 256 MiB written) against
- * @partner, and keeps the first candidate whose probe differs
- * from an earlier one by more than the class gap (the faster of the two),
- * trying at most GCL_PAIR_TRIES candidates; losers are freed.  Classes come
- * in runs of consecutive allocations (up to six 2-GiB buffers in a row were
- * measured), so after every GCL_PAIR_RUN candidates of one class a spacer
- * of twice @bytes is allocated to step past the run; spacers are freed too.
+ * @partner, and keeps the first candidate whose probe differs from an
+ * earlier one by more than the class gap (the faster of the two), trying at
+ * most GCL_PAIR_TRIES candidates; losers are freed.  Classes come in runs of
+ * consecutive allocations (4-34 GiB of 2-GiB pools in a row were measured,
+ * profiles/r02_classmap.jsonl), so after every GCL_PAIR_RUN candidates of one
+ * class a spacer of 2, 4, 8, then 16 x @bytes is allocated to step past the
+ * run.  Candidates and spacers together hold at most 60% of the free device
+ * memory; all but the kept buffer are freed before returning.  When no second
+ * class shows up the fastest candidate is kept, @info->classes is 1 and a
+ * warning goes to stderr (GCL_PAIR_QUIET silences it).
  *
  * GCL_PAIR_NEW_READS: the new buffer is the one stream-read (frames) and
  *                     @partner the one written (verdicts);
  * GCL_PAIR_NEW_WRITES: the reverse.
- * The probe WRITES to the written side's first min(bytes, 256 MiB): call it
- * before that buffer holds data.  @probe_us (optional, 2 doubles) returns the
- * chosen and the slowest probe time in microseconds.
+ * The probe WRITES to the written side's first min(bytes, 256 MiB)
+ * (@info->probe_write_bytes) and nothing past it: call it before that buffer
+ * holds data.  @info may be NULL.
  * Returns 0, -EINVAL, -ENODEV, -ENOMEM or -EIO.
  */
 #define GCL_PAIR_NEW_READS  0x1
 #define GCL_PAIR_NEW_WRITES 0x2
-#define GCL_PAIR_TRIES      12
-#define GCL_PAIR_RUN        3
+#define GCL_PAIR_TRIES      24
+#define GCL_PAIR_RUN        2
+struct gcl_pair_info {
+	double   chosen_us;         /* probe time of the buffer kept */
+	double   worst_us;          /* slowest candidate probed */
+	uint32_t candidates;        /* candidates probed */
+	uint32_t classes;           /* placement classes seen: 2, or 1 (kept one may be slow) */
+	uint64_t spacer_bytes;      /* spacer memory held during the search */
+	uint64_t probe_write_bytes; /* bytes of the written side the probe stored to */
+};
 int gcl_dev_alloc_paired(int hip_device, size_t bytes, const void *partner, size_t partner_bytes,
-                         uint32_t flags, void **out, double *probe_us);
+                         uint32_t flags, void **out, struct gcl_pair_info *info);
 
 /*
  * Persistent rx loop: the classifier at the reference's own granularity, one

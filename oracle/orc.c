@@ -506,7 +506,155 @@ deliver:
 		v->action |= GCL_ACT_F_TRANS;
 }
 
+/*
+ * rx_one_pkt as rx.c:116-233 writes it, for the CPU BASELINE only: header
+ * fields loaded straight through header structs at the frame pointer
+ * (rte_pktmbuf_mtod + ether_type / iphdr->dst_addr / arp_tip, rx.c:127-167),
+ * no per-byte bounds test, and in GCL_HASH_NIC mode the NIC's hash.rss
+ * (rx.c:83) -- what the dataplane core really does per packet.  The caller
+ * guarantees every frame's first 42 bytes (54 with L4 ports) lie inside the
+ * buffer, as an mbuf's data does.  Same verdicts as orc_rx_one_pkt for such
+ * batches without loopback hints (tests/test_oracle_scenarios.py).
+ */
+struct rb_eth { uint8_t dst[6], src[6]; uint16_t type; } __attribute__((packed));
+struct rb_ip {
+	uint8_t vihl, tos;
+	uint16_t len, id, off;
+	uint8_t ttl, proto;
+	uint16_t csum;
+	uint32_t saddr, daddr;
+} __attribute__((packed));
+struct rb_arp {
+	uint16_t htype, ptype;
+	uint8_t hlen, plen;
+	uint16_t op;
+	uint8_t sha[6];
+	uint32_t sip;
+	uint8_t tha[6];
+	uint32_t tip;
+} __attribute__((packed));
+
+static inline uint32_t rb_flow_hash(const struct orc_tables *t, const uint8_t *f)
+{
+	const struct rb_ip *ip = (const struct rb_ip *)(f + sizeof(struct rb_eth));
+	const unsigned ihl = ip->vihl & 0xF;
+	uint8_t key[13];
+	uint32_t saddr, daddr;
+	uint16_t sport, dport, ports[2];
+
+	if (__builtin_bswap16(((const struct rb_eth *)f)->type) != GCL_ETHTYPE_IP || ihl < 5 ||
+	    (__builtin_bswap16(ip->off) & 0x3FFF) || (ip->proto != 6 && ip->proto != 17))
+		return 0;
+	memcpy(ports, f + sizeof(struct rb_eth) + 4 * ihl, 4);
+	saddr = __builtin_bswap32(ip->saddr);
+	daddr = __builtin_bswap32(ip->daddr);
+	sport = __builtin_bswap16(ports[0]);
+	dport = __builtin_bswap16(ports[1]);
+	if (t->hash_mode == GCL_HASH_TOEPLITZ)
+		return orc_do_toeplitz(t->rss_key, saddr, daddr, sport, dport);
+	memcpy(key, &saddr, 4);
+	memcpy(key + 4, &daddr, 4);
+	memcpy(key + 8, &dport, 2);
+	memcpy(key + 10, &sport, 2);
+	key[12] = ip->proto;
+	return orc_jhash(key, 13);
+}
+
+static inline void rx_one_pkt_direct(const struct orc_tables *t, const struct gcl_batch *b,
+                                     uint64_t i, struct gcl_verdict *v, uint64_t *counts,
+                                     uint64_t *stats)
+{
+	const uint8_t *f = b->frames + (b->offs ? b->offs[i] : i * b->stride);
+	const struct rb_eth *eh = (const struct rb_eth *)f;
+	const uint8_t flags = b->olflags ? b->olflags[i] : t->default_olflags;
+	uint32_t hash, dst_ip;
+	uint16_t et;
+	int p;
+
+	hash = t->hash_mode == GCL_HASH_NIC ? (b->rss ? b->rss[i] : 0) : rb_flow_hash(t, f);
+	if (t->flags & GCL_CFG_HASH16)
+		hash &= 0xFFFF;
+	v->hash = hash;
+	v->uniqid = GCL_NO_RUNTIME;
+	v->thread = GCL_NO_THREAD;
+	if (flags & GCL_F_FDIR_ID) { /* rx.c:131-146 */
+		const uint32_t mark = b->fdir_hi ? b->fdir_hi[i] : 0;
+		stats[GCL_RX_FLOW_TAG_MATCH]++;
+		if (mark < t->max_runtimes && t->rt[mark].present) {
+			p = (int)mark;
+			goto deliver_fdir;
+		}
+	}
+	et = __builtin_bswap16(eh->type); /* rx.c:154 */
+	if (__builtin_expect(et == GCL_ETHTYPE_IP, 1)) {
+		const struct rb_ip *ip = (const struct rb_ip *)(f + sizeof(*eh));
+		dst_ip = __builtin_bswap32(ip->daddr); /* rx.c:157-159 */
+		if (!(flags & GCL_F_RSS_HASH))
+			stats[GCL_RX_HASH_MISSING]++;
+	} else if (et == GCL_ETHTYPE_ARP) {
+		const struct rb_arp *ah = (const struct rb_arp *)(f + sizeof(*eh));
+		dst_ip = __builtin_bswap32(ah->tip); /* rx.c:165-167 */
+		if ((t->flags & GCL_CFG_AZURE_ARP) && __builtin_bswap16(ah->op) == GCL_ARP_OP_REPLY) {
+			v->action = GCL_ACT_BROADCAST;
+			return;
+		}
+	} else {
+		v->action = GCL_ACT_DROP_ETHERTYPE; /* rx.c:191-194 */
+		stats[GCL_RX_UNHANDLED]++;
+		return;
+	}
+	p = iptab_lookup(t, dst_ip); /* rx.c:197 */
+	if (__builtin_expect(p < 0, 0)) {
+		if ((t->flags & GCL_CFG_AZURE_ARP) && et == GCL_ETHTYPE_ARP &&
+		    __builtin_bswap16(((const struct rb_arp *)(f + sizeof(*eh)))->op) ==
+		            GCL_ARP_OP_REQUEST) {
+			v->action = GCL_ACT_ARP_RESPOND;
+			return;
+		}
+		stats[GCL_RX_UNREGISTERED_MAC]++;
+		stats[GCL_RX_UNHANDLED]++;
+		v->action = GCL_ACT_DROP_UNREG;
+		return;
+	}
+	v->uniqid = (uint16_t)p;
+	counts[p]++;
+	if (t->rt[p].active > 0) { /* rx.c:55-59 */
+		v->thread = (uint8_t)t->rt[p].flow_tbl[hash % t->rt[p].thread_count];
+		v->action = GCL_ACT_DELIVER;
+	} else {
+		v->action = GCL_ACT_WAKE;
+	}
+	return;
+deliver_fdir:
+	v->uniqid = (uint16_t)p;
+	counts[p]++;
+	if (t->rt[p].active > 0) {
+		v->thread = (uint8_t)t->rt[p].flow_tbl[hash % t->rt[p].thread_count];
+		v->action = GCL_ACT_DELIVER | GCL_ACT_F_FDIR;
+	} else {
+		v->action = GCL_ACT_WAKE | GCL_ACT_F_FDIR;
+	}
+}
+
 #define RX_PREFETCH_STRIDE 2 /* rx.c:22 */
+
+static void classify_range_direct(const struct orc_tables *t, const struct gcl_batch *b,
+                                  uint64_t lo, uint64_t hi, struct gcl_verdict *v,
+                                  uint64_t *counts, uint64_t *stats)
+{
+	/* rx_burst, rx.c:270-290, over rx_one_pkt_direct */
+	for (uint64_t s = lo; s < hi; s += GCL_RX_BURST_SIZE) {
+		uint64_t nb = hi - s < GCL_RX_BURST_SIZE ? hi - s : GCL_RX_BURST_SIZE;
+		stats[GCL_RX_PULLED] += nb;
+		for (uint64_t i = 0; i < nb; i++) {
+			if (i + RX_PREFETCH_STRIDE < nb) {
+				uint64_t j = s + i + RX_PREFETCH_STRIDE;
+				__builtin_prefetch(b->frames + (b->offs ? b->offs[j] : j * b->stride));
+			}
+			rx_one_pkt_direct(t, b, s + i, &v[s + i - lo], counts, stats);
+		}
+	}
+}
 
 static void classify_range(const struct orc_tables *t, const struct gcl_batch *b,
                            uint64_t lo, uint64_t hi, struct gcl_verdict *v,
@@ -533,6 +681,12 @@ void orc_classify(const struct orc_tables *t, const struct gcl_batch *b,
                   struct gcl_verdict *v, uint64_t *counts, uint64_t *stats)
 {
 	classify_range(t, b, 0, b->n, v, counts, stats, NULL);
+}
+
+void orc_classify_direct(const struct orc_tables *t, const struct gcl_batch *b,
+                         struct gcl_verdict *v, uint64_t *counts, uint64_t *stats)
+{
+	classify_range_direct(t, b, 0, b->n, v, counts, stats);
 }
 
 void orc_classify_ex(const struct orc_tables *t, const struct gcl_batch *b,
@@ -581,7 +735,7 @@ static struct orc_lrpc *ring_of(struct lrpc_set *s, uint32_t p, uint32_t th)
 static void classify_range_lrpc(const struct orc_tables *t, const struct gcl_batch *b,
                                 uint64_t lo, uint64_t hi, struct gcl_verdict *v,
                                 uint64_t *counts, uint64_t *stats,
-                                struct lrpc_set *rs)
+                                struct lrpc_set *rs, int direct)
 {
 	for (uint64_t s = lo; s < hi; s += GCL_RX_BURST_SIZE) {
 		uint64_t nb = hi - s < GCL_RX_BURST_SIZE ? hi - s : GCL_RX_BURST_SIZE;
@@ -595,7 +749,10 @@ static void classify_range_lrpc(const struct orc_tables *t, const struct gcl_bat
 				if (off < b->frames_len)
 					__builtin_prefetch(b->frames + off);
 			}
-			orc_rx_one_pkt(t, b, k, vk, counts, stats, NULL);
+			if (direct)
+				rx_one_pkt_direct(t, b, k, vk, counts, stats);
+			else
+				orc_rx_one_pkt(t, b, k, vk, counts, stats, NULL);
 			if ((vk->action & GCL_ACT_MASK) == GCL_ACT_DELIVER) {
 				/* rx_make_cmd, rx.c:24-38 */
 				uint8_t fl = b->olflags ? b->olflags[k] : t->default_olflags;
@@ -647,7 +804,7 @@ void orc_classify_lrpc(const struct orc_tables *t, const struct gcl_batch *b,
 {
 	struct lrpc_set rs;
 	lrpc_set_init(&rs, t);
-	classify_range_lrpc(t, b, 0, b->n, v, counts, stats, &rs);
+	classify_range_lrpc(t, b, 0, b->n, v, counts, stats, &rs, 0);
 	lrpc_set_free(&rs, t);
 }
 
@@ -658,7 +815,7 @@ struct bench_arg {
 	const struct orc_tables *t;
 	const struct gcl_batch *b;
 	uint64_t lo, hi;
-	int passes, with_lrpc;
+	int passes, with_lrpc, direct;
 	pthread_barrier_t *bar;
 };
 
@@ -669,7 +826,7 @@ static void *bench_thread(void *arg)
 	struct gcl_verdict *v = malloc((n ? n : 1) * sizeof(*v));
 	uint64_t *counts = calloc(a->t->max_runtimes, sizeof(uint64_t));
 	uint64_t stats[GCL_NR_STATS] = { 0 };
-	struct lrpc_set rs;
+	struct lrpc_set rs = { 0 };
 
 	if (a->with_lrpc)
 		lrpc_set_init(&rs, a->t);
@@ -678,7 +835,9 @@ static void *bench_thread(void *arg)
 	pthread_barrier_wait(a->bar);
 	for (int p = 0; p < a->passes; p++) {
 		if (a->with_lrpc)
-			classify_range_lrpc(a->t, a->b, a->lo, a->hi, v, counts, stats, &rs);
+			classify_range_lrpc(a->t, a->b, a->lo, a->hi, v, counts, stats, &rs, a->direct);
+		else if (a->direct)
+			classify_range_direct(a->t, a->b, a->lo, a->hi, v, counts, stats);
 		else
 			classify_range(a->t, a->b, a->lo, a->hi, v, counts, stats, NULL);
 	}
@@ -692,6 +851,12 @@ static void *bench_thread(void *arg)
 
 double orc_bench(const struct orc_tables *t, const struct gcl_batch *b,
                  int threads, int passes, int with_lrpc)
+{
+	return orc_bench_ex(t, b, threads, passes, with_lrpc ? ORC_BENCH_LRPC : 0);
+}
+
+double orc_bench_ex(const struct orc_tables *t, const struct gcl_batch *b,
+                    int threads, int passes, unsigned int flags)
 {
 	pthread_t tid[256];
 	struct bench_arg arg[256];
@@ -709,7 +874,8 @@ double orc_bench(const struct orc_tables *t, const struct gcl_batch *b,
 		arg[i].lo = b->n * (uint64_t)i / (uint64_t)threads;
 		arg[i].hi = b->n * (uint64_t)(i + 1) / (uint64_t)threads;
 		arg[i].passes = passes;
-		arg[i].with_lrpc = with_lrpc;
+		arg[i].with_lrpc = !!(flags & ORC_BENCH_LRPC);
+		arg[i].direct = !!(flags & ORC_BENCH_DIRECT);
 		arg[i].bar = &bar;
 		pthread_create(&tid[i], NULL, bench_thread, &arg[i]);
 	}

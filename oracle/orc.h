@@ -12,6 +12,8 @@
  *   orc_steer_flows   iokernel/sched.c:122-147
  *   orc_rx_burst      iokernel/rx.c:270-290 (bursts of 64, prefetch stride 2)
  *   orc_rx_one_pkt    iokernel/rx.c:116-233 (+ rx_send_to_runtime :50-73)
+ *   rx_one_pkt_direct the same, as the CPU baseline: rx.c's direct header
+ *                     struct loads and the NIC hash (orc_bench_ex DIRECT)
  *   orc_crc32c_u64    crc32q, inc/asm/ops.h:77-80 (hash_crc32c_one/two)
  *   orc_trans         trans_hash_5tuple/3tuple, runtime/net/transport.c:29-42
  *   orc_iptab_*       the ip_to_proc rte_hash (iokernel/dp_clients.c:349-363),
@@ -96,6 +98,19 @@ void orc_classify_lrpc(const struct orc_tables *t, const struct gcl_batch *b,
  * wall seconds. */
 double orc_bench(const struct orc_tables *t, const struct gcl_batch *b,
                  int threads, int passes, int with_lrpc);
+
+/* orc_bench with options: ORC_BENCH_LRPC adds the lrpc_send of every
+ * delivered packet; ORC_BENCH_DIRECT classifies with rx.c's direct header
+ * loads (no bounds test: every frame's first 54 bytes must be in range). */
+#define ORC_BENCH_LRPC   0x1
+#define ORC_BENCH_DIRECT 0x2
+double orc_bench_ex(const struct orc_tables *t, const struct gcl_batch *b,
+                    int threads, int passes, unsigned int flags);
+
+/* orc_classify through the CPU-baseline form (direct header loads, same
+ * preconditions as ORC_BENCH_DIRECT; dst_hint is ignored). */
+void orc_classify_direct(const struct orc_tables *t, const struct gcl_batch *b,
+                         struct gcl_verdict *v, uint64_t *counts, uint64_t *stats);
 
 /* Synthetic generator: the same streams as gcl_generate, written on the CPU.
  * frames must hold n*stride bytes (pre-zeroed by the caller). */

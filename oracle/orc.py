@@ -67,6 +67,8 @@ def _bind(path):
         "orc_crc32c_u64": (u32, [u32, u64]),
         "orc_runtime_set_trans_seed": (i32, [vp, u16, u32]),
         "orc_bench": (ctypes.c_double, [vp, ctypes.POINTER(Batch), i32, i32, i32]),
+        "orc_bench_ex": (ctypes.c_double, [vp, ctypes.POINTER(Batch), i32, i32, u32]),
+        "orc_classify_direct": (None, [vp, ctypes.POINTER(Batch), vp, vp, vp]),
         "orc_generate": (i32, [ctypes.POINTER(GenParams), vp, vp, vp, vp]),
         "orc_runtime_ip": (u32, [u32]),
         "orc_zipf_cdf": (i32, [u32, ctypes.c_double, vp]),
@@ -231,10 +233,30 @@ class Tables:
         fn(self.h, ctypes.byref(b), v.ctypes.data, counts.ctypes.data, stats.ctypes.data)
         return v, counts, stats
 
+    def classify_direct(self, frames, n, stride=0, offs=None, olflags=None, rss=None,
+                        fdir_hi=None):
+        """The CPU-baseline form (rx.c's direct header loads): every frame's
+        first 54 bytes must lie inside `frames`."""
+        last = (int(offs.max()) if offs is not None and n else (n - 1) * stride) + 54
+        if n and last > frames.nbytes:
+            raise ValueError("classify_direct: a frame's header runs past the buffer")
+        b = self._batch(frames, n, stride, offs, olflags, rss, fdir_hi, None, None)
+        v = np.zeros(n, dtype=VERDICT_DTYPE)
+        counts = np.zeros(self.max_runtimes, dtype=np.uint64)
+        stats = np.zeros(NR_STATS, dtype=np.uint64)
+        self._lib.orc_classify_direct(self.h, ctypes.byref(b), v.ctypes.data, counts.ctypes.data,
+                                      stats.ctypes.data)
+        return v, counts, stats
+
     def bench(self, frames, n, stride, threads=1, passes=1, lrpc=False, offs=None, olflags=None,
-              rss=None, fdir_hi=None, pkt_len=None):
+              rss=None, fdir_hi=None, pkt_len=None, direct=False):
+        """Wall seconds of `passes` classifications on `threads` threads
+        (contiguous shards); direct=True times rx.c's direct-load form."""
+        if direct and n and (n - 1) * stride + 54 > frames.nbytes and offs is None:
+            raise ValueError("direct bench: a frame's header runs past the buffer")
         b = self._batch(frames, n, stride, offs, olflags, rss, fdir_hi, pkt_len, None)
-        return self._lib.orc_bench(self.h, ctypes.byref(b), threads, passes, int(lrpc))
+        flags = (1 if lrpc else 0) | (2 if direct else 0)
+        return self._lib.orc_bench_ex(self.h, ctypes.byref(b), threads, passes, flags)
 
 
 def generate(workload, n, stride, nruntimes, seed=0xCA1ADA4, rank=0, world=1, shard_block=0,

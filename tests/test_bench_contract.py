@@ -58,3 +58,36 @@ def test_workloads_match_baseline_configs(bench):
     assert (n, stride, R) == (32 << 20, 64, 16)
     wl, n, stride, R, T, _ = bench.WORKLOADS["tcp1500"]
     assert (stride, R) == (1536, 1024) and n == 8 << 20
+
+
+def test_pick_device_refuses_ranks_past_gpus(bench, monkeypatch):
+    """One process per GPU: a LOCAL_RANK past the visible GPUs is refused
+    (two ranks on one GPU would read as bad scaling), unless the rehearsal
+    flag asks for it."""
+    monkeypatch.setattr(bench.torch.cuda, "device_count", lambda: 2)
+    assert bench.pick_device(1, 2, False) == 1
+    with pytest.raises(SystemExit):
+        bench.pick_device(2, 4, False)
+    assert bench.pick_device(3, 4, True) == 1
+    monkeypatch.setattr(bench.torch.cuda, "device_count", lambda: 0)
+    with pytest.raises(SystemExit):
+        bench.pick_device(0, 1, False)
+
+
+def test_strong_scaling_split(bench):
+    """Config 4: 256 Mi packets split evenly over 1, 2, 4 and 8 ranks in whole
+    64 Ki-packet shard blocks (32 Mi per GPU at 8)."""
+    for world in (1, 2, 4, 8):
+        assert bench.STRONG_TOTAL_PKTS % (world * bench.SHARD_BLOCK) == 0
+    assert bench.STRONG_TOTAL_PKTS // 8 == bench.WORKLOADS["udp64"][1]
+
+
+def test_roofline_traffic_scales_with_batch(bench):
+    """The committed PMC bytes (taken at 32 Mi packets) scale per packet to a
+    strong-scaling launch's batch."""
+    import types
+    w = types.SimpleNamespace(name="udp64", n=256 << 20, vbytes=4, bytes_per_pkt=68)
+    r = bench.roofline(w, 2.9)
+    if r["traffic"] is not None:
+        assert abs(r["traffic"] / (w.n * 68) - 1) < 0.01
+        assert abs(r["moved"]["frac"] - r["frac"]) < 0.01

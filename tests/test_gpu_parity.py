@@ -446,6 +446,47 @@ def test_gpu_full_size_properties(g, orc):
     assert_same(vv[sample], ve, "sample")
 
 
+def test_gpu_full_size_tcp1500_properties(g, orc):
+    """Config 3 at full size (8 Mi x 1536-B slots, Zipf-0.99 over 1 Mi flows,
+    1024 runtimes x 4 kthreads): every packet is accounted for per runtime,
+    each runtime gets exactly the flows `flow % R` maps to it, and a
+    65536-packet random sample matches the oracle bit for bit (hash,
+    runtime, kthread, action)."""
+    n, R, T, stride, F = 8 << 20, 1024, 4, 1536, 1 << 20
+    frames = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
+    cdf = g.zipf_cdf(F, 0.99)
+    g.generate(g.WL_TCP1500_ZIPF, n, stride, R, frames,
+               zipf_cdf_dev=torch.from_numpy(cdf.view(np.int64)).cuda(), nflows=F)
+    clf = g.Classifier(0, R, 1)
+    t = orc.Tables(R, 1, 0, 0x09)
+    rng = np.random.default_rng(9)
+    for r in range(R):
+        act = int(rng.integers(1, T + 1))
+        fl = orc.steer_flows(T, [int(x) for x in rng.choice(T, size=act, replace=False)])
+        clf.runtime_set(r, g.runtime_ip(r), T, act, fl)
+        t.runtime_set(r, orc.runtime_ip(r), T, act, fl)
+    v = torch.zeros(n * 8, dtype=torch.uint8, device="cuda")
+    c = torch.zeros(R, dtype=torch.int64, device="cuda")
+    s = torch.zeros(8, dtype=torch.int64, device="cuda")
+    clf.classify(frames, n, stride, verdicts=v, counts=c, stats=s)
+    torch.cuda.synchronize()
+    vv = v.view(torch.int64).cpu().numpy().view(g.VERDICT_DTYPE)
+    cc = c.cpu().numpy()
+    ss = s.cpu().numpy()
+    assert cc.sum() == n and ss[g.RX_PULLED] == n and ss[g.RX_UNHANDLED] == 0
+    assert ss[g.RX_UNREGISTERED_MAC] == 0 and ss[g.RX_HASH_MISSING] == 0
+    assert (np.bincount(vv["uniqid"], minlength=R)[:R] == cc).all()
+    assert ((vv["action"] & 0x3F) == 0).all() and (vv["thread"] < T).all()
+    # Zipf skew survives: the top runtime (flow 0's) carries the most packets
+    assert cc.argmax() == 0 and cc[0] > 4 * np.median(cc)
+    sample = np.sort(rng.choice(n, size=65536, replace=False))
+    fr = frames.view(n, stride)[torch.from_numpy(sample).cuda(), :64].cpu().numpy().reshape(-1)
+    del frames
+    torch.cuda.empty_cache()
+    ve, _, _ = t.classify(fr, len(sample), 64)
+    assert_same(vv[sample], ve, "tcp1500 sample")
+
+
 @pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("wl,stride,R,T,arrays", [(0, 64, 16, 8, False), (1, 1536, 1024, 4, False),
                                                    (2, 9216, 16, 8, True)])
@@ -618,6 +659,32 @@ def test_gpu_trace_replay_zero_copy(g, orc, tmp_path):
             g.host_unregister(a)
     assert_same(hv, ve, "trace replay")
     assert (counts == ce).all() and (stats == se).all()
+
+
+@pytest.mark.parametrize("partner_mib", [24, 300])
+def test_gpu_pair_probe_write_bound(g, partner_mib):
+    """gcl_dev_alloc_paired's probe stores into the written side (the partner
+    verdict ring here) only within min(partner_bytes, 256 MiB): a guard area
+    past partner_bytes, and the ring's bytes past 256 MiB, keep their
+    pattern.  The returned info names the bound and the classes seen."""
+    import ctypes
+    pb = partner_mib << 20
+    guard = 4 << 20
+    buf = torch.full((pb + guard,), 0xA5, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    out = ctypes.c_void_p()
+    info = g.GclPairInfo()
+    assert g.lib.gcl_dev_alloc_paired(0, 64 << 20, buf.data_ptr(), pb, g.PAIR_NEW_READS,
+                                      ctypes.byref(out), ctypes.byref(info)) == 0
+    try:
+        wb = min(pb, 256 << 20)
+        assert info.probe_write_bytes == wb
+        assert 1 <= info.candidates <= g.PAIR_TRIES and info.classes in (1, 2)
+        assert 0 < info.chosen_us <= info.worst_us
+        tail = buf[wb:].cpu()
+        assert bool((tail == 0xA5).all()), "probe wrote past min(partner_bytes, 256 MiB)"
+    finally:
+        g.lib.gcl_dev_free(out)
 
 
 def test_gpu_dev_alloc_paired(g, orc):

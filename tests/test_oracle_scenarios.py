@@ -78,3 +78,44 @@ def test_crc32c_golden_from_reference(orc):
         for _ in range(5000):
             s, a = rnd.getrandbits(32), rnd.getrandbits(64)
             assert ref.ref_crc32c_one(s, a) == orc.crc32c_u64(s, a)
+
+
+@pytest.mark.parametrize("s", SETS, ids=[s["name"] for s in SETS])
+def test_direct_form_matches_scenarios(orc, s):
+    """The CPU-baseline form (rx.c's direct header loads, bench.py
+    cpu_baseline) gives the fixtures' verdicts, counts and counters too --
+    for the sets it covers: no loopback hints, and the transport pre-hash flag
+    (a runtime-side extra, not rx.c's work) masked off."""
+    cfg = s["cfg"]
+    frames, olflags, rss, fdir, exp, hint = scenario_batch(s)
+    if hint is not None and hint.any():
+        pytest.skip("loopback hints are rx_loopback's, not rx_one_pkt's")
+    t = orc.Tables(cfg["max_runtimes"], cfg["hash_mode"], cfg["flags"], cfg["default_olflags"],
+                   bytes.fromhex(cfg["rss_key"]))
+    apply_runtimes(t, s["runtimes"])
+    n = len(exp)
+    v, counts, stats = t.classify_direct(frames, n, 128, olflags=olflags, rss=rss, fdir_hi=fdir)
+    for i in range(n):
+        got, want = tuple(v[i]), tuple(exp[i])
+        assert got[:3] == want[:3] and int(got[3]) == int(want[3]) & 0xBF, (s["packets"][i]["cite"], got, want)
+    assert list(stats) == s["expect_stats"]
+    assert list(counts) == s["expect_counts"]
+
+
+@pytest.mark.parametrize("wl,stride,R", [(0, 64, 16), (1, 1536, 1024), (2, 9216, 16)])
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_direct_form_matches_oracle_on_workloads(orc, wl, stride, R, mode):
+    """Direct form == bounds-checked form on the three bench streams, with the
+    generator's ol_flags and NIC hashes, in all three hash modes."""
+    n = 3000
+    cdf = orc.zipf_cdf(1 << 12) if wl == 1 else None
+    frames, olf, rss = orc.generate(wl, n, stride, R, cdf=cdf)
+    t = orc.Tables(R, mode, 0, 0x09, rss_key=bytes(range(40)))
+    rng = np.random.default_rng(7)
+    for r in range(R):
+        act = int(rng.integers(0, 5))
+        t.runtime_set(r, orc.runtime_ip(r), 4, act, orc.steer_flows(4, list(range(act))) if act else None)
+    a = t.classify(frames, n, stride, olflags=olf, rss=rss)
+    b = t.classify_direct(frames, n, stride, olflags=olf, rss=rss)
+    for x, y in zip(a, b):
+        assert (x == y).all()

@@ -4,7 +4,8 @@
 //   cbench <workload> <steps> [cfg ...]
 // (env CBENCH_N, CBENCH_STRIDE, CBENCH_R override the workload's shape)
 //
-// Each cfg is "ABLATE:GRID:DEPTH:THREADS:BPC:SCHED:V4[:NT]" (NT = GCL_TUNE_NT_STORE) (GCL_TUNE_* knobs, 0 = default;
+// Each cfg is "ABLATE:GRID:DEPTH:THREADS:BPC:SCHED:V4[:NT[:DEFER]]" (NT = GCL_TUNE_NT_STORE,
+// DEFER = GCL_TUNE_DEFER, -1 or absent = library default) (GCL_TUNE_* knobs, 0 = default;
 // V4=1 classifies into 4-byte verdicts, GCL_CFG_VERDICT4; V4=2 into 2-byte queue
 // verdicts, GCL_CFG_VERDICT2).
 // CBENCH_NOISE_US=X co-runs, on a second stream, 32 one-wave blocks that each
@@ -80,7 +81,7 @@ __global__ void noise_kernel(unsigned us, unsigned long long *sink)
 
 struct Cfg {
 	std::string name;
-	int ablate, grid, depth, threads, bpc, sched, v4, nt;
+	int ablate, grid, depth, threads, bpc, sched, v4, nt, defer;
 	bool ref;
 	std::vector<double> us, wall;
 };
@@ -102,15 +103,15 @@ int main(int argc, char **argv)
 		return 1;
 	}
 	std::vector<Cfg> cfgs;
-	cfgs.push_back({"ref", 0, 0, 0, 0, 0, 0, 0, 0, true, {}, {}});
+	cfgs.push_back({"ref", 0, 0, 0, 0, 0, 0, 0, 0, -1, true, {}, {}});
 	for (int i = 3; i < argc; i++) {
-		Cfg c = {argv[i], 0, 0, 0, 0, 0, 0, 0, 0, false, {}, {}};
-		sscanf(argv[i], "%d:%d:%d:%d:%d:%d:%d:%d", &c.ablate, &c.grid, &c.depth, &c.threads, &c.bpc,
-		       &c.sched, &c.v4, &c.nt);
+		Cfg c = {argv[i], 0, 0, 0, 0, 0, 0, 0, 0, -1, false, {}, {}};
+		sscanf(argv[i], "%d:%d:%d:%d:%d:%d:%d:%d:%d", &c.ablate, &c.grid, &c.depth, &c.threads, &c.bpc,
+		       &c.sched, &c.v4, &c.nt, &c.defer);
 		cfgs.push_back(c);
 	}
 	if (cfgs.size() == 1)
-		cfgs.push_back({"default", 0, 0, 0, 0, 0, 0, 0, 0, false, {}, {}});
+		cfgs.push_back({"default", 0, 0, 0, 0, 0, 0, 0, 0, -1, false, {}, {}});
 	const char *pe = getenv("CBENCH_PROFILE");
 	const bool profile = !pe || atoi(pe) != 0; /* 0: no per-launch events, wall time only */
 	const char *ne = getenv("CBENCH_NOISE_US");
@@ -130,12 +131,13 @@ int main(int argc, char **argv)
 	uint64_t *acc, *zipf = nullptr;
 	CHECK(hipMalloc(&v, n * sizeof(*v)));
 	if (getenv("CBENCH_PAIRED")) { /* frame pool placed against the verdict ring */
-		double pu[2];
-		if (gcl_dev_alloc_paired(0, n * stride, v, n * 4, GCL_PAIR_NEW_READS, (void **)&frames, pu)) {
+		struct gcl_pair_info pi;
+		if (gcl_dev_alloc_paired(0, n * stride, v, n * 4, GCL_PAIR_NEW_READS, (void **)&frames, &pi)) {
 			fprintf(stderr, "gcl_dev_alloc_paired failed\n");
 			return 1;
 		}
-		fprintf(stderr, "paired: probe %.2f us (worst %.2f)\n", pu[0], pu[1]);
+		fprintf(stderr, "paired: probe %.2f us (worst %.2f, %u candidates, %u classes)\n",
+		        pi.chosen_us, pi.worst_us, pi.candidates, pi.classes);
 	} else {
 		CHECK(hipMalloc(&frames, n * stride));
 	}
@@ -206,6 +208,12 @@ int main(int argc, char **argv)
 			setenv("GCL_TUNE_SCHED", buf, 1);
 			snprintf(buf, sizeof(buf), "%d", c.nt);
 			setenv("GCL_TUNE_NT_STORE", buf, 1);
+			if (c.defer >= 0) {
+				snprintf(buf, sizeof(buf), "%d", c.defer);
+				setenv("GCL_TUNE_DEFER", buf, 1);
+			} else {
+				unsetenv("GCL_TUNE_DEFER");
+			}
 			struct gcl_cfg cfg = {};
 			cfg.max_runtimes = R;
 			cfg.hash_mode = GCL_HASH_JENKINS;

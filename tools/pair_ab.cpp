@@ -130,9 +130,15 @@ int main(int argc, char **argv)
 	cfg.hash_mode = GCL_HASH_JENKINS;
 	cfg.flags = GCL_CFG_VERDICT4;
 	cfg.default_olflags = GCL_F_RSS_HASH | GCL_F_IP_CKSUM_GOOD;
-	struct gcl_ctx *ctx;
+	/* ctx: the library default; ctx2: GCL_TUNE_DEFER=0 (verdict stores at the
+	 * end of their tile) for the deferred-store A/B */
+	struct gcl_ctx *ctx, *ctx2;
 	if (gcl_open(0, &cfg, &ctx))
 		return 1;
+	setenv("GCL_TUNE_DEFER", "0", 1);
+	if (gcl_open(0, &cfg, &ctx2))
+		return 1;
+	unsetenv("GCL_TUNE_DEFER");
 	uint16_t act[GCL_NCPU], flow[GCL_NCPU];
 	for (uint32_t r = 0; r < R; r++) {
 		uint16_t na = (uint16_t)(r % T + 1);
@@ -140,13 +146,14 @@ int main(int argc, char **argv)
 			act[i] = i;
 		gcl_steer_flows((uint16_t)T, act, na, flow);
 		gcl_runtime_set(ctx, (uint16_t)r, gcl_runtime_ip(r), (uint16_t)T, na, flow);
+		gcl_runtime_set(ctx2, (uint16_t)r, gcl_runtime_ip(r), (uint16_t)T, na, flow);
 	}
 	int cus = 0;
 	CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
 	hipEvent_t e0, e1;
 	CHECK(hipEventCreate(&e0));
 	CHECK(hipEventCreate(&e1));
-	std::vector<std::vector<double>> cl(NF * NV), tk(NF * NV);
+	std::vector<std::vector<double>> cl(NF * NV), tk(NF * NV), c2(NF * NV);
 	for (int round = 0; round < 3; round++)
 		for (int f = 0; f < NF; f++)
 			for (int v = 0; v < NV; v++) {
@@ -164,6 +171,14 @@ int main(int argc, char **argv)
 				float ms;
 				CHECK(hipEventElapsedTime(&ms, e0, e1));
 				cl[f * NV + v].push_back(ms * 1e3 / steps);
+				gcl_classify(ctx2, &bt, vb[v], acc, acc + R, nullptr);
+				CHECK(hipEventRecord(e0, nullptr));
+				for (int s = 0; s < steps; s++)
+					gcl_classify(ctx2, &bt, vb[v], acc, acc + R, nullptr);
+				CHECK(hipEventRecord(e1, nullptr));
+				CHECK(hipEventSynchronize(e1));
+				CHECK(hipEventElapsedTime(&ms, e0, e1));
+				c2[f * NV + v].push_back(ms * 1e3 / steps);
 				CHECK(hipEventRecord(e0, nullptr));
 				for (int s = 0; s < steps; s++)
 					hipLaunchKernelGGL(tile_kernel<0>, dim3(cus * 4), dim3(256), 0, nullptr, fb[f],
@@ -190,6 +205,8 @@ int main(int argc, char **argv)
 	};
 	for (int f : {0, NF / 2, NF - 1})
 		for (int v : {0, NV / 2, NV - 1}) {
+			if (!getenv("PAIR_AB_EXTRA"))
+				break;
 			auto go = [&](auto kern) {
 				return tm([&] { hipLaunchKernelGGL(kern, dim3(cus * 4), dim3(256), 0, nullptr, fb[f],
 				                                   (unsigned long long)(n / 256), vb[v]); });
@@ -207,13 +224,15 @@ int main(int argc, char **argv)
 		                                   (unsigned long long)(n / 256), vb[v]); }));
 	for (int f = 0; f < NF; f++)
 		for (int v = 0; v < NV; v++) {
-			auto &a = cl[f * NV + v], &b = tk[f * NV + v];
+			auto &a = cl[f * NV + v], &b = tk[f * NV + v], &c = c2[f * NV + v];
 			std::sort(a.begin(), a.end());
 			std::sort(b.begin(), b.end());
+			std::sort(c.begin(), c.end());
 			printf("{\"f\": %d, \"v\": %d, \"fva\": \"%p\", \"vva\": \"%p\", \"classify_us\": %.2f, "
-			       "\"tile_us\": %.2f}\n", f, v, (void *)fb[f], (void *)vb[v], a[a.size() / 2],
-			       b[b.size() / 2]);
+			       "\"classify_defer0_us\": %.2f, \"tile_us\": %.2f}\n", f, v, (void *)fb[f], (void *)vb[v],
+			       a[a.size() / 2], c[c.size() / 2], b[b.size() / 2]);
 		}
 	gcl_close(ctx);
+	gcl_close(ctx2);
 	return 0;
 }
