@@ -55,11 +55,15 @@ WORKLOADS = {
 # verdict of GCL_CFG_VERDICT2) (DESIGN.md "Roofline"); tables and counters
 # amortise to ~0.
 HDR_BYTES = 64
-# the bench default is the 4-byte verdict: the 2-byte queue verdict is
-# 1-4.5 % faster (profiles/r01_verdict_width_ab.jsonl) but carries 2 B/pkt
-# less, so its roofline fraction is no higher
-VERDICT_BYTES = 4
-# the secondary (config 3, 1500-B TCP) line's verdict: the 2-byte queue verdict
+# the bench default is the 2-byte queue verdict (GCL_CFG_VERDICT2): the flat
+# kthread-queue index q = uniqid << thread_bits | thread that the lrpc
+# post-pass (gcl_host_deliver2) indexes its rings with, a wake's flow_tbl
+# slot, or a tagged drop/broadcast action -- everything rx_send_pkt_to_runtime
+# needs.  It halves the write requests of the 4-byte form: 331 vs 342 us for
+# udp64 and 174 vs 180 us for tcp1500 on the same buffers
+# (profiles/r02_defer_ab.jsonl).  The 4- and 8-byte forms stay as rows.
+VERDICT_BYTES = 2
+# the secondary (config 3, 1500-B TCP) line's verdict
 SECONDARY_VERDICT_BYTES = 2
 VERDICT_NAMES = {8: "gcl_verdict, 8 B", 4: "gcl_verdict4, 4 B",
                  2: "queue verdict (GCL_CFG_VERDICT2), 2 B"}
@@ -126,6 +130,14 @@ def zero_fill(buf):
     hip.hipDeviceSynchronize()
 
 
+# start-up placement check (Workload.check_placement): the kernel over the
+# chosen pair must run within this factor of the probe's time, else the pool
+# is placed again, at most PLACEMENT_TRIES times.  Fast pairs measured
+# kernel/probe 1.00-1.06, slow ones >= 1.16 (profiles/r02_pair_check.jsonl)
+PLACEMENT_SLACK = 1.10
+PLACEMENT_TRIES = 3
+
+
 class Workload:
     def __init__(self, name, rank, world, device, hash_mode=g.HASH_JENKINS, vbytes=VERDICT_BYTES,
                  n=None):
@@ -134,6 +146,8 @@ class Workload:
         self.name, self.wl, self.n, self.stride, self.R, self.T, self.desc = name, wl, n, stride, R, T, desc
         self.vbytes = vbytes
         self.bytes_per_pkt = HDR_BYTES + vbytes
+        self.device = device
+        self.placement_checks = []
         if os.environ.get("GCL_BENCH_TORCH_ALLOC") == "1":
             self.frames = torch.zeros(n * stride, dtype=torch.uint8, device=device)
             self.verdicts = torch.empty(n * vbytes, dtype=torch.uint8, device=device)
@@ -142,24 +156,76 @@ class Workload:
             # (gcl_dev_alloc_paired: DESIGN.md §4 "Buffer placement");
             # GCL_BENCH_PLACEMENT=0 allocates both plainly, for the A/B
             self.verdicts = g.DeviceBuffer(n * vbytes, device.index or 0)
-            paired = os.environ.get("GCL_BENCH_PLACEMENT", "1") != "0"
-            self.frames = g.DeviceBuffer(n * stride, device.index or 0,
-                                         partner=self.verdicts if paired else None)
-            torch.cuda.synchronize()
-            zero_fill(self.frames)
+            self.paired = os.environ.get("GCL_BENCH_PLACEMENT", "1") != "0"
+            self.frames = self._new_pool()
         self.counts = torch.zeros(R + g.NR_STATS, dtype=torch.int64, device=device)
 
-        cdf_dev = None
-        nflows = 0
+        self.cdf_dev = None
+        self.nflows = 0
         if wl == g.WL_TCP1500_ZIPF:
-            nflows = 1 << 20
-            cdf_dev = torch.from_numpy(g.zipf_cdf(nflows, 0.99).view(np.int64)).to(device)
-        g.generate(wl, n, stride, R, self.frames, seed=SEED, rank=rank, world=world,
-                   shard_block=SHARD_BLOCK, zipf_cdf_dev=cdf_dev, nflows=nflows)
+            self.nflows = 1 << 20
+            self.cdf_dev = torch.from_numpy(g.zipf_cdf(self.nflows, 0.99).view(np.int64)).to(device)
+        self.rank, self.world = rank, world
+        self._fill(self.frames)
         fl, tb = verdict_cfg(vbytes, R, T)
         self.clf = g.Classifier(device.index or 0, R, hash_mode, fl, thread_bits=tb)
         self.tables = setup_tables(self.clf, R, T)
         torch.cuda.synchronize()
+        if getattr(self, "paired", False) and stride == HDR_BYTES:
+            self.check_placement()
+
+    def _new_pool(self):
+        buf = g.DeviceBuffer(self.n * self.stride, self.device.index or 0,
+                             partner=self.verdicts if self.paired else None, vbytes=self.vbytes)
+        torch.cuda.synchronize()
+        zero_fill(buf)
+        return buf
+
+    def _fill(self, buf):
+        g.generate(self.wl, self.n, self.stride, self.R, buf, seed=SEED, rank=self.rank,
+                   world=self.world, shard_block=SHARD_BLOCK, zipf_cdf_dev=self.cdf_dev,
+                   nflows=self.nflows)
+
+    def kernel_us(self, reps=5):
+        """Mean classify launch time over this pair, into scratch counters."""
+        scratch = torch.zeros_like(self.counts)
+        st = torch.cuda.current_stream()
+
+        def go():
+            self.clf.classify(self.frames, self.n, self.stride, verdicts=self.verdicts,
+                              counts=scratch[:self.R], stats=scratch[self.R:], stream=st.cuda_stream)
+        go()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(reps):
+            go()
+        e1.record(st)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps * 1e3
+
+    def check_placement(self, tries=PLACEMENT_TRIES):
+        """Keep the frame pool only if the classify kernel itself runs in the
+        fast class over it: its launch time within PLACEMENT_SLACK of the
+        probe's chosen time (scaled to the probe's 4 GiB read cap).  A pool
+        that fails is placed again against the same ring (the old one held
+        while the search runs, so the next lands elsewhere), regenerated,
+        and checked again -- a start-up placement, like the iokernel's
+        (iokernel/rx.c:398-415)."""
+        for k in range(tries + 1):
+            info = self.frames.pair_info
+            scale = self.n * self.stride / min(self.n * self.stride, 4 << 30)
+            us = self.kernel_us()
+            ok = us <= info["probe_us_chosen"] * scale * PLACEMENT_SLACK
+            self.placement_checks.append({"kernel_us": round(us, 2), "probe_us_chosen":
+                                          info["probe_us_chosen"], "classes_seen": info["classes_seen"],
+                                          "kept": ok or k == tries})
+            if ok or k == tries:
+                return
+            old = self.frames
+            self.frames = self._new_pool()
+            old.free()
+            self._fill(self.frames)
+            torch.cuda.synchronize()
 
     def step(self, stream):
         self.clf.classify(self.frames, self.n, self.stride, verdicts=self.verdicts,
@@ -322,10 +388,12 @@ def placement(w):
     info = getattr(w.frames, "pair_info", None)
     if info is None:
         return {"policy": "plain hipMalloc"}
+    checks = getattr(w, "placement_checks", [])
     return {"policy": "gcl_dev_alloc_paired (frame pool placed against the verdict ring)",
             **info,
             "class_chosen": ("fast (cross-class pair: both classes seen)" if info["classes_seen"] == 2
-                             else "unknown (one class in every candidate)")}
+                             else "unknown (one class in every candidate)"),
+            "kernel_checks": checks, "replaced": max(0, len(checks) - 1)}
 
 
 def e2e_bench(device, vbytes=VERDICT_BYTES, reps=3):
@@ -516,7 +584,7 @@ def timed_launches(fn, reps):
 INGRESS_DESC_BYTES = 8 + 1 + 4
 
 
-def ingress_pool_bench(device, vbytes, cycles=64, reps=10):
+def ingress_pool_bench(device, vbytes, cycles=64, reps=10, zerocopy=True):
     """Frames where the reference keeps them (§8f-2): the 131072-mbuf ingress
     pool, 9408-B elements, 222 per 2 MiB page, frame data at element + 344
     (8-B aligned; iokernel/defs.h:70, :503-523).  A batch is `cycles` random
@@ -573,6 +641,10 @@ def ingress_pool_bench(device, vbytes, cycles=64, reps=10):
     okj = int(cnt[:R].sum().item()) == n * (reps + 1)
     out["jenkins_offs_only"] = {"device_resident_mpps": round(n / wall_j / 1e6, 1),
                                 "kernel_ms": round(gms_j, 4), "counts_check": "ok" if okj else "MISMATCH"}
+    if not zerocopy:
+        del region, offs, olf, rss, dv, nic, jen
+        torch.cuda.empty_cache()
+        return out
     # zero-copy: the pool in pinned host memory, descriptors and verdicts too
     hreg = torch.empty(region.numel(), dtype=torch.uint8).pin_memory()
     hreg.copy_(region)

@@ -2011,11 +2011,11 @@ extern "C" int gcl_dev_free(void *p)
 namespace {
 
 /* The classify kernel's memory shape without its compute: 256-packet tiles of
- * 64-B granules read with four nt 16-B loads per lane, one 4-B store per
+ * 64-B granules read with four nt 16-B loads per lane, one VB-byte store per
  * packet (tile t writes slot t % wtiles of the write side). */
-template <bool WT>
+template <bool WT, int VB>
 __global__ void __launch_bounds__(256) pair_probe_kernel(const uint8_t *rd, uint64_t ntiles,
-                                                         uint32_t *wr, uint64_t wtiles)
+                                                         uint8_t *wr, uint64_t wtiles)
 {
 	__shared__ uint4 tile[1024];
 	uint64_t t = blockIdx.x;
@@ -2042,11 +2042,27 @@ __global__ void __launch_bounds__(256) pair_probe_kernel(const uint8_t *rd, uint
 		const int p = threadIdx.x;
 		const uint4 a = tile[tile_slot(p, 0)], b = tile[tile_slot(p, 1)];
 		const uint32_t v = a.x ^ a.w ^ b.y ^ b.z;
-		if (WT) /* the classify kernel's default verdict store (kDefaultVerdictStore) */
-			__hip_atomic_store(&wr[(t % wtiles) * 256 + p], v, __ATOMIC_RELAXED,
-			                   __HIP_MEMORY_SCOPE_SYSTEM);
-		else
-			wr[(t % wtiles) * 256 + p] = v;
+		const uint64_t i = (t % wtiles) * 256 + p;
+		/* WT: the classify kernel's default verdict store (kDefaultVerdictStore) */
+		if (VB == 2) {
+			if (WT)
+				__hip_atomic_store((uint16_t *)wr + i, (uint16_t)v, __ATOMIC_RELAXED,
+				                   __HIP_MEMORY_SCOPE_SYSTEM);
+			else
+				((uint16_t *)wr)[i] = (uint16_t)v;
+		} else if (VB == 8) {
+			if (WT)
+				__hip_atomic_store((uint64_t *)wr + i, (uint64_t)v * 0x100000001ull,
+				                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+			else
+				((uint64_t *)wr)[i] = (uint64_t)v * 0x100000001ull;
+		} else {
+			if (WT)
+				__hip_atomic_store((uint32_t *)wr + i, v, __ATOMIC_RELAXED,
+				                   __HIP_MEMORY_SCOPE_SYSTEM);
+			else
+				((uint32_t *)wr)[i] = v;
+		}
 		__syncthreads();
 		t = nx;
 	}
@@ -2057,29 +2073,42 @@ constexpr size_t kPairProbeWriteMax = 256ull << 20;
 
 /* min over 3 timed launches of the probe (after one untimed), microseconds;
  * negative on a HIP error */
-double pair_probe(const uint8_t *rd, size_t rd_bytes, uint32_t *wr, size_t wr_bytes, hipStream_t s,
-                  hipEvent_t e0, hipEvent_t e1, int cus)
+double pair_probe(const uint8_t *rd, size_t rd_bytes, uint8_t *wr, size_t wr_bytes, int vb,
+                  hipStream_t s, hipEvent_t e0, hipEvent_t e1, int cus)
 {
 	/* the whole of both buffers, as the kernel walks them (a 2 GiB frame
 	 * pool against a 128 MiB verdict ring is 0.35-0.4 ms): a probe of the
 	 * first 512 MiB against the first 32 MiB missed the class on some boxes */
 	const uint64_t ntiles = std::min<size_t>(rd_bytes, 4ull << 30) / (256 * 64);
-	const uint64_t wtiles = std::min<size_t>(wr_bytes, kPairProbeWriteMax) / (256 * 4);
+	const uint64_t wtiles = std::min<size_t>(wr_bytes, kPairProbeWriteMax) / (256 * (size_t)vb);
 	if (!ntiles || !wtiles)
 		return -1;
+	/* the store policy decides which pairs collide: probe with the one the
+	 * classify kernel will use (GCL_TUNE_NT_STORE, as gcl_open) */
+	const char *e = getenv("GCL_TUNE_NT_STORE");
+	const bool wt = (e ? atoi(e) : kDefaultVerdictStore) == 2;
+	auto launch = [&]() {
+		const dim3 g(cus * 4), b(256);
+#define GCL_PROBE(W, V) hipLaunchKernelGGL((pair_probe_kernel<W, V>), g, b, 0, s, rd, ntiles, wr, wtiles)
+		if (vb == 2 && wt)
+			GCL_PROBE(true, 2);
+		else if (vb == 2)
+			GCL_PROBE(false, 2);
+		else if (vb == 8 && wt)
+			GCL_PROBE(true, 8);
+		else if (vb == 8)
+			GCL_PROBE(false, 8);
+		else if (wt)
+			GCL_PROBE(true, 4);
+		else
+			GCL_PROBE(false, 4);
+#undef GCL_PROBE
+	};
 	double best = 1e30;
 	for (int i = 0; i < 4; i++) {
 		if (hipEventRecord(e0, s) != hipSuccess)
 			return -1;
-		/* the store policy decides which pairs collide: probe with the one
-		 * the classify kernel will use (GCL_TUNE_NT_STORE, as gcl_open) */
-		const char *e = getenv("GCL_TUNE_NT_STORE");
-		if ((e ? atoi(e) : kDefaultVerdictStore) == 2)
-			hipLaunchKernelGGL(pair_probe_kernel<true>, dim3(cus * 4), dim3(256), 0, s, rd, ntiles, wr,
-			                   wtiles);
-		else
-			hipLaunchKernelGGL(pair_probe_kernel<false>, dim3(cus * 4), dim3(256), 0, s, rd, ntiles, wr,
-			                   wtiles);
+		launch();
 		if (hipEventRecord(e1, s) != hipSuccess || hipEventSynchronize(e1) != hipSuccess)
 			return -1;
 		float ms = 0;
@@ -2107,13 +2136,16 @@ extern "C" int gcl_dev_alloc_paired(int hip_device, size_t bytes, const void *pa
                                     size_t partner_bytes, uint32_t flags, void **out,
                                     struct gcl_pair_info *info)
 {
-	const bool new_reads = flags == GCL_PAIR_NEW_READS;
+	const uint32_t dir = flags & 0xFF;
+	const int vb = GCL_PAIR_VBYTES_OF(flags) ? (int)GCL_PAIR_VBYTES_OF(flags) : 4;
+	const bool new_reads = dir == GCL_PAIR_NEW_READS;
 	if (!out || !bytes || !partner || !partner_bytes ||
-	    (flags != GCL_PAIR_NEW_READS && flags != GCL_PAIR_NEW_WRITES))
+	    (dir != GCL_PAIR_NEW_READS && dir != GCL_PAIR_NEW_WRITES) ||
+	    (vb != 2 && vb != 4 && vb != 8) || (flags >> 16))
 		return -EINVAL;
 	const size_t rd_bytes = new_reads ? bytes : partner_bytes;
 	const size_t wr_bytes = new_reads ? partner_bytes : bytes;
-	if (rd_bytes < 256 * 64 || wr_bytes < 256 * 4)
+	if (rd_bytes < 256 * 64 || wr_bytes < 256 * (size_t)vb)
 		return -EINVAL;
 	if (hipSetDevice(hip_device) != hipSuccess)
 		return -ENODEV;
@@ -2166,8 +2198,8 @@ extern "C" int gcl_dev_alloc_paired(int hip_device, size_t bytes, const void *pa
 		}
 		held += bytes;
 		const double us = new_reads
-		        ? pair_probe((const uint8_t *)p, rd_bytes, (uint32_t *)partner, wr_bytes, s, e0, e1, cus)
-		        : pair_probe((const uint8_t *)partner, rd_bytes, (uint32_t *)p, wr_bytes, s, e0, e1, cus);
+		        ? pair_probe((const uint8_t *)p, rd_bytes, (uint8_t *)partner, wr_bytes, vb, s, e0, e1, cus)
+		        : pair_probe((const uint8_t *)partner, rd_bytes, (uint8_t *)p, wr_bytes, vb, s, e0, e1, cus);
 		if (dbg)
 			fprintf(stderr, "gcl_dev_alloc_paired: candidate %d %p probe %.2f us\n", i, p, us);
 		if (us < 0) {
@@ -2217,7 +2249,7 @@ extern "C" int gcl_dev_alloc_paired(int hip_device, size_t bytes, const void *pa
 		info->candidates = (uint32_t)cand.size();
 		info->classes = (uint32_t)classes;
 		info->spacer_bytes = spacer_held;
-		info->probe_write_bytes = std::min<size_t>(wr_bytes, kPairProbeWriteMax);
+		info->probe_write_bytes = std::min<size_t>(wr_bytes, kPairProbeWriteMax) / (256 * vb) * (256 * vb);
 	}
 	return 0;
 }

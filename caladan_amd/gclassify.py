@@ -301,11 +301,12 @@ class DeviceBuffer:
     address with the duck-typed interface the binding accepts (data_ptr,
     numel, element_size)."""
 
-    def __init__(self, nbytes, device=0, partner=None, new_reads=True):
+    def __init__(self, nbytes, device=0, partner=None, new_reads=True, vbytes=4):
         """partner: another buffer (data_ptr/numel); the new one is then placed
         by gcl_dev_alloc_paired so that reading the frame side while writing
         the verdict side does not hit the same-placement-class slowdown.
-        new_reads: the new buffer is the frame (read) side."""
+        new_reads: the new buffer is the frame (read) side.
+        vbytes: the verdict width the classifier will write (2, 4 or 8)."""
         p = ctypes.c_void_p()
         self.probe_us = None
         self.pair_info = None
@@ -314,7 +315,8 @@ class DeviceBuffer:
         else:
             info = GclPairInfo()
             _check(lib.gcl_dev_alloc_paired(device, nbytes, _ptr(partner), _nbytes(partner),
-                                            PAIR_NEW_READS if new_reads else PAIR_NEW_WRITES,
+                                            (PAIR_NEW_READS if new_reads else PAIR_NEW_WRITES) |
+                                            vbytes << 8,
                                             ctypes.byref(p), ctypes.byref(info)), "gcl_dev_alloc_paired")
             self.probe_us = (info.chosen_us, info.worst_us)
             self.pair_info = {"probe_us_chosen": round(info.chosen_us, 2),

@@ -441,13 +441,18 @@ int gcl_dev_free(void *p);
  * GCL_PAIR_NEW_READS: the new buffer is the one stream-read (frames) and
  *                     @partner the one written (verdicts);
  * GCL_PAIR_NEW_WRITES: the reverse.
- * The probe WRITES to the written side's first min(bytes, 256 MiB)
- * (@info->probe_write_bytes) and nothing past it: call it before that buffer
+ * OR in GCL_PAIR_VBYTES(2|4|8), the verdict width the kernel will write
+ * (default 4): the probe stores the same width, so its time tracks the
+ * kernel's for every format.
+ * The probe WRITES to the written side's first min(bytes, 256 MiB), rounded
+ * down to whole 256-verdict tiles (@info->probe_write_bytes), and nothing past it: call it before that buffer
  * holds data.  @info may be NULL.
  * Returns 0, -EINVAL, -ENODEV, -ENOMEM or -EIO.
  */
 #define GCL_PAIR_NEW_READS  0x1
 #define GCL_PAIR_NEW_WRITES 0x2
+#define GCL_PAIR_VBYTES(b)  ((uint32_t)(b) << 8)
+#define GCL_PAIR_VBYTES_OF(f) (((f) >> 8) & 0xFF)
 #define GCL_PAIR_TRIES      24
 #define GCL_PAIR_RUN        2
 struct gcl_pair_info {

@@ -1,0 +1,21 @@
+"""bench.py's integrated ingress-pool leg alone (device-resident part), for
+rocprofv3: 8 Mi descriptors into the reference's mbuf pool geometry with
+ol_flags and hash.rss, GCL_HASH_NIC (classify_kernel<0, ...>), then the
+JENKINS offsets-only row (classify_kernel<1, ...>).
+
+    python tools/ingress_run.py [reps]
+"""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+
+if __name__ == "__main__":
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    print(json.dumps(bench.ingress_pool_bench(dev, bench.VERDICT_BYTES, reps=reps, zerocopy=False)))

@@ -20,7 +20,17 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HDR_BYTES = 64
-PKTS = {"udp64": 32 << 20, "tcp1500": 8 << 20, "mixed": 1 << 20}
+PKTS = {"udp64": 32 << 20, "tcp1500": 8 << 20, "mixed": 1 << 20, "ingress_nic": 8 << 20}
+# per-packet bytes besides the 64-B header and the verdict: the integrated
+# ingress shape reads a u64 offset, u8 ol_flags and u32 hash.rss per descriptor
+EXTRA = {"ingress_nic": 8 + 1 + 4}
+# which classify_kernel instance is the workload's: the ingress run also
+# launches the JENKINS (MODE 1) row; its NIC launches are MODE 0
+KNAME = {"ingress_nic": "classify_kernel<0,"}
+
+
+def is_kernel(wl, name):
+    return KNAME.get(wl, "classify_kernel") in name.replace(" ", "")
 
 
 def rows(path):
@@ -51,7 +61,7 @@ def calib(base):
     return out
 
 
-def request_bytes(base, tag):
+def request_bytes(base, tag, wl):
     """Fabric request counts per classify launch (TCC_EA0_RDREQ / _32B,
     TCC_BUBBLE, TCC_EA0_WRREQ / _64B).  rocprof-compute's gfx950 'HBM
     Bandwidth' formula prices reads as 128 x TCC_BUBBLE + 32 x RDREQ_32B + 64 x
@@ -68,7 +78,7 @@ def request_bytes(base, tag):
     for path in (d1, d2):
         launches = {}
         for r in rows(path):
-            if "classify_kernel" in r["Kernel_Name"]:
+            if is_kernel(wl, r["Kernel_Name"]):
                 launches.setdefault(r["Dispatch_Id"], {})[r["Counter_Name"].replace("_sum", "")] = \
                     float(r["Counter_Value"])
         for c in {k for v in launches.values() for k in v}:
@@ -98,16 +108,16 @@ def main(rnd):
             continue
         shutil.copy(os.path.join(tdir, "run_kernel_stats.csv"),
                     os.path.join(prof, f"{rnd}_{tag}_kernel_stats.csv"))
-        st = [r for r in rows(os.path.join(tdir, "run_kernel_stats.csv")) if "classify_kernel" in r["Name"]]
+        st = [r for r in rows(os.path.join(tdir, "run_kernel_stats.csv")) if is_kernel(wl, r["Name"])]
         pm = {}
         for c in ("FETCH_SIZE", "WRITE_SIZE"):
             vals = [float(r["Counter_Value"]) for r in
                     rows(os.path.join(base, f"{tag}_{c}", "run_counter_collection.csv"))
-                    if "classify_kernel" in r["Kernel_Name"]]
+                    if is_kernel(wl, r["Kernel_Name"])]
             pm[c] = sum(vals) / len(vals)
         hbm_read = 2.0 * pm["FETCH_SIZE"] * 1024
         hbm_write = pm["WRITE_SIZE"] * 1024
-        algo = PKTS[wl] * (HDR_BYTES + vb)
+        algo = PKTS[wl] * (HDR_BYTES + EXTRA.get(wl, 0) + vb)
         avg_ns = float(st[0]["AverageNs"])
         out = {
             "workload": wl,
@@ -128,7 +138,7 @@ def main(rnd):
             "algorithmic_GBs": round(algo / (avg_ns * 1e-9) / 1e9, 1),
             "source": f"gpurun_out/prof_{rnd}/{tag}_{{trace,FETCH_SIZE,WRITE_SIZE}} (rocprofv3)",
         }
-        req = request_bytes(base, tag)
+        req = request_bytes(base, tag, wl)
         if req:
             out.update(req)
             out["traffic_over_algorithmic_from_requests"] = round(req["hbm_bytes_from_requests"] / algo, 4)
