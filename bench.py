@@ -297,6 +297,10 @@ class Exchange:
         cur.wait_stream(self.comm)
 
 
+# GPU time of continuous steps (warmup + settle) before the timed region
+SETTLE_MS = 30.0
+
+
 def run_timed(w, steps, warmup, world, ex=None):
     """Warm up, then time exactly `steps` steps between a barrier +
     synchronize on both sides.  Returns (wall seconds, max over ranks;
@@ -312,14 +316,39 @@ def run_timed(w, steps, warmup, world, ex=None):
         else:
             w.step(stream.cuda_stream)
 
+    # settle: the kernel reaches its steady launch time only after ~40
+    # back-to-back launches (~15 ms) following any pause -- 359 -> 343 -> 336
+    # us per launch over the first 60 udp64 launches, then flat
+    # (profiles/r02_drift_v2.jsonl) -- so the timed steps start after at
+    # least SETTLE_MS of continuous steps, warmup included.  The step time is
+    # estimated from the warmup (one settle step when there is none), and all
+    # ranks run the same number of settle steps (the counts check needs it).
+    t_w = time.perf_counter()
     for _ in range(warmup):
         one()
+    pre = 0
+    if warmup == 0 and SETTLE_MS > 0:
+        one()
+        pre = 1
+    torch.cuda.synchronize()
+    step_ms = (time.perf_counter() - t_w) * 1e3 / max(warmup + pre, 1)
+    settle = max(0, int(SETTLE_MS / max(step_ms, 1e-3)) + 1 - warmup - pre) if SETTLE_MS > 0 else 0
+    if world > 1:
+        t = torch.tensor([settle], dtype=torch.int64)
+        if torch.distributed.get_backend() == "nccl":
+            t = t.cuda()
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        settle = int(t.item())
+    for _ in range(settle):
+        one()
+    settle += pre
     if ex is not None:
         ex.drain()
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
+    run_timed.last_settle = settle
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
@@ -855,15 +884,16 @@ def main():
     w = Workload(args.workload, rank, world, device, vbytes=vb, n=n_rank)
     ex = Exchange(w, world, device, args.exchange_every) if dist_on else None
     el, gms = run_timed(w, args.steps, args.warmup, world, ex)
+    settle_steps = run_timed.last_settle
     total_pkts = w.n * world * args.steps
     value = total_pkts / el / 1e6
     # correctness spot check: every packet of every step was accounted for
     if ex is not None:
         tot = ex.acc[:w.R].sum().item()
-        expect = w.n * world * (args.steps + args.warmup)
+        expect = w.n * world * (args.steps + args.warmup + settle_steps)
     else:
         tot = w.counts[:w.R].sum().item()
-        expect = w.n * (args.steps + args.warmup)
+        expect = w.n * (args.steps + args.warmup + settle_steps)
     counts_ok = tot == expect
     # kernel-only next to the exchange-inclusive step: the same
     # steps without the all_gather, barrier + max-over-ranks timed
@@ -903,6 +933,9 @@ def main():
                      "N=1 without an exchange: the step is the classify launch")},
         "placement": placement(w),
         "counts_check": "ok" if counts_ok else f"MISMATCH {tot} != {expect}",
+        "settle": {"steps": settle_steps, "ms_target": SETTLE_MS,
+                   "what": ("untimed steps after the warmup, so the timed steps start after "
+                            ">= ms_target of continuous launches (DESIGN.md §5)")},
     }
     if ex is not None:
         result["exchange"] = {"gpu_ms_per_step": round(gms, 4), "period_steps": args.exchange_every,

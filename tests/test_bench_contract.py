@@ -91,3 +91,17 @@ def test_roofline_traffic_scales_with_batch(bench):
     if r["traffic"] is not None:
         assert abs(r["traffic"] / (w.n * 68) - 1) < 0.01
         assert abs(r["moved"]["frac"] - r["frac"]) < 0.01
+
+
+def test_frames_len_bounded_by_buffer():
+    """The binding refuses a frames_len past the frame buffer (the kernel
+    trusts it as the bound of every frame read)."""
+    import numpy as np
+    from caladan_amd import gclassify as g
+    buf = np.zeros(4096, dtype=np.uint8)
+    assert g._frames_len(buf, None) == 4096
+    assert g._frames_len(buf, 100) == 100
+    with pytest.raises(ValueError):
+        g._frames_len(buf, 4097)
+    with pytest.raises(ValueError):
+        g._frames_len(buf, -1)
