@@ -629,6 +629,37 @@ def test_gpu_ingress_pool_geometry(g, orc):
     assert (counts == ce).all() and (stats == se).all()
 
 
+def test_gpu_ingress_integrated_nic_verdict2(g, orc):
+    """The bench's integrated ingress shape (e2e.ingress_pool.integrated_nic,
+    INTEGRATION.md §4): descriptors into the reference's mbuf pool geometry
+    in random pool order, each with its mbuf's ol_flags and hash.rss,
+    GCL_HASH_NIC, 2-byte queue verdicts -- bit-exact against the oracle."""
+    n, R, T, P = 60000, 16, 8, 8192
+    hdr, olf_p, rss_p = orc.generate(0, P, 64, R)
+    rng = np.random.default_rng(17)
+    pool = g.mbuf_data_offsets(P)
+    order = np.concatenate([rng.permutation(P) for _ in range(-(-n // P))])[:n]
+    offs = pool[order]
+    olf = np.ascontiguousarray(olf_p[order])
+    rss = np.ascontiguousarray(rss_p[order])
+    olf[::7] &= ~np.uint8(g.F_RSS_HASH)  # some frames without the NIC's hash flag
+    region = np.zeros(g.mbuf_region_bytes(P), dtype=np.uint8)
+    region[pool[:, None].astype(np.int64) + np.arange(64)] = hdr.reshape(P, 64)
+    tb = g.thread_bits_for(R, T)
+    t = orc.Tables(R, g.HASH_NIC, 0, 0x09)
+    clf = g.Classifier(0, R, g.HASH_NIC, g.CFG_VERDICT2, 0x09, thread_bits=tb)
+    for r in range(R):
+        act = (r * 5) % (T + 1)  # includes runtimes with no active kthread (WAKE)
+        fl = orc.steer_flows(T, list(range(act))) if act else None
+        t.runtime_set(r, orc.runtime_ip(r), T, act, fl)
+        clf.runtime_set(r, g.runtime_ip(r), T, act, fl)
+    ve, ce, se = t.classify(region, n, 0, offs=offs, olflags=olf, rss=rss)
+    v, c, st = gpu_run(g, clf, region, n, 0, offs=offs, olflags=olf, rss=rss)
+    assert ((ve["action"] & 0x3F) == g.ACT_WAKE).any() and se[g.RX_HASH_MISSING] > 0
+    assert_same(v, to_verdict2(ve, [T] * R, tb), "integrated ingress shape")
+    assert (c == ce).all() and (st == se).all()
+
+
 def test_gpu_trace_replay_zero_copy(g, orc, tmp_path):
     """Config 5's path: a pcap trace loaded into host memory, registered, and
     classified by the kernel straight over PCIe (gcl_classify_host ZEROCOPY)."""
