@@ -102,11 +102,6 @@ struct KParams {
 	uint32_t *sched; /* tile queue slot (SchedSlot) or NULL = static persistent grid */
 	uint32_t xcd_map; /* static grid: 1 = each XCD walks one contiguous eighth of the tiles */
 	uint32_t defer;   /* 1: a tile's verdicts are stored after the next tile's barrier */
-	/* slotted verdict bursts (GCL_TUNE_WSLOT): verdicts of up to wslots tiles
-	 * wait in LDS (wbuf_off) and are written when the GPU clock is inside the
-	 * first wwindow ticks of every wperiod (100 MHz), or when the buffer is
-	 * full; 0 = off */
-	uint32_t wslots, wperiod, wwindow, wbuf_off;
 };
 
 /* Dynamic tile queue of one launch: tiles are dealt per XCD (tile t belongs
@@ -646,67 +641,13 @@ classify_kernel(KParams k)
 			put_verdict(k, pend_i, pend_w);
 		pend_i = ~0ull;
 	};
-	/* slotted bursts: wbuf holds wslots tiles of verdicts (vb bytes each),
-	 * wtile their tile numbers, then one u32 flag */
-	const uint32_t vb = (k.cflags & GCL_CFG_VERDICT2) ? 2u : (k.cflags & GCL_CFG_VERDICT4) ? 4u : 8u;
-	uint8_t *wbuf = (uint8_t *)smem + k.wbuf_off;
-	uint64_t *wtile = (uint64_t *)(wbuf + (size_t)k.wslots * NT * vb);
-	uint32_t *s_wflag = (uint32_t *)(wtile + k.wslots);
-	uint32_t nsl = 0; /* tiles waiting in wbuf (block-uniform) */
 	auto verdict = [&](uint64_t idx, uint64_t w) {
-		if (k.wslots) {
-			uint8_t *d = wbuf + ((size_t)nsl * NT + tid) * vb;
-			if (vb == 2)
-				*(uint16_t *)d = (uint16_t)w;
-			else if (vb == 4)
-				*(uint32_t *)d = (uint32_t)w;
-			else
-				*(uint64_t *)d = w;
-		} else if (k.defer) {
+		if (k.defer) {
 			pend_w = w;
 			pend_i = idx;
 		} else {
 			put_verdict(k, idx, w);
 		}
-	};
-	/* before the end-of-tile barrier: note the tile, decide whether to burst */
-	auto slot_note = [&](uint64_t tt) {
-		if (!k.wslots)
-			return;
-		if (tid == 0) {
-			wtile[nsl] = tt;
-			const uint64_t now = __builtin_amdgcn_s_memrealtime();
-			*s_wflag = (nsl + 1 == k.wslots) || (now % k.wperiod) < k.wwindow;
-		}
-		nsl++;
-	};
-	/* after the barrier: write the waiting tiles out, 16 B per lane */
-	auto slot_burst = [&](bool force) {
-		if (!k.wslots || !nsl || !(force || *s_wflag))
-			return;
-		const uint32_t cps = NT * vb / 16; /* 16-B chunks per tile */
-		const uint64_t vbytes_total = k.n * vb;
-		for (uint32_t c = tid; c < nsl * cps; c += NT) {
-			const uint32_t i = c / cps, o = (c % cps) * 16;
-			const uint64_t g = wtile[i] * NT * vb + o;
-			const uint4 x = *(const uint4 *)(wbuf + (size_t)i * NT * vb + o);
-			uint8_t *dst = (uint8_t *)k.verdicts + g;
-			if (g + 16 <= vbytes_total) {
-				if (k.nt_store == 2) {
-					__hip_atomic_store((uint64_t *)dst, (uint64_t)x.y << 32 | x.x, __ATOMIC_RELAXED,
-					                   __HIP_MEMORY_SCOPE_SYSTEM);
-					__hip_atomic_store((uint64_t *)dst + 1, (uint64_t)x.w << 32 | x.z,
-					                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-				} else {
-					*(uint4 *)dst = x;
-				}
-			} else {
-				const uint8_t *sb = (const uint8_t *)&x;
-				for (uint32_t b = 0; b < 16 && g + b < vbytes_total; b++)
-					dst[b] = sb[b];
-			}
-		}
-		nsl = 0;
 	};
 
 	while (t < t_end) {
@@ -734,9 +675,7 @@ classify_kernel(KParams k)
 			s_next[par ^ 1] = nxt < k.ntiles ? sched_resolve(k.sched, k.ntiles, (uint32_t)G,
 			                                                 x0, xs, got)
 			                                 : k.ntiles;
-		slot_note(t);
 		__syncthreads();
-		slot_burst(false);
 		if (dyn) {
 			t = nxt;
 			par ^= 1;
@@ -755,14 +694,11 @@ classify_kernel(KParams k)
 			if (t * NT + tid < k.n)
 				verdict(t * NT + tid, classify_one<MODE, GENERAL>(k, tile, tid, t * NT + tid, tb,
 				                                                  hist, cnt, sp2));
-			slot_note(t);
 			__syncthreads();
-			slot_burst(false);
 			t += step;
 		}
 	}
 	flush();
-	slot_burst(true);
 	uint32_t n_flowtag = cnt.flowtag, n_hashmiss = cnt.hashmiss;
 	uint32_t n_unreg = cnt.unreg, n_unhandled = cnt.unhandled;
 
@@ -1272,7 +1208,6 @@ struct gcl_ctx {
 	int tune_sched;    /* GCL_TUNE_SCHED: 0 static persistent grid, 1 dynamic tile queue */
 	int tune_xcd_map;  /* GCL_TUNE_XCD_MAP: 1 contiguous eighth per XCD, 0 round-robin tiles */
 	int tune_defer;    /* GCL_TUNE_DEFER: 1 verdict stores one tile late, 0 at once (default) */
-	uint32_t tune_wslots, tune_wperiod, tune_wwindow; /* GCL_TUNE_WSLOT "slots:period:window" */
 	/* dynamic tile queue: one slot per launch in flight, reused in turn; a
 	 * launch waits for the previous user of its slot (same or other stream) */
 	uint32_t *sched;
@@ -1358,16 +1293,6 @@ extern "C" int gcl_open(int hip_device, const struct gcl_cfg *cfg, struct gcl_ct
 		c->tune_xcd_map = e ? atoi(e) : kDefaultXcdMap;
 		e = getenv("GCL_TUNE_DEFER");
 		c->tune_defer = e ? atoi(e) : kDefaultDefer;
-		c->tune_wslots = c->tune_wperiod = c->tune_wwindow = 0;
-		e = getenv("GCL_TUNE_WSLOT");
-		if (e) {
-			unsigned a = 0, b = 0, w = 0;
-			if (sscanf(e, "%u:%u:%u", &a, &b, &w) == 3 && a >= 1 && a <= 64 && b >= 1 && w <= b) {
-				c->tune_wslots = a;
-				c->tune_wperiod = b;
-				c->tune_wwindow = w;
-			}
-		}
 	}
 	c->dimg[0] = c->dimg[1] = nullptr;
 	c->sched = nullptr;
@@ -1709,24 +1634,11 @@ struct Geometry {
 	int bpc_cap;  /* blocks per CU */
 };
 
-static uint32_t kernel_cflags(const gcl_ctx *c);
-
-/* LDS of the slotted verdict bursts (GCL_TUNE_WSLOT) for @nt-lane tiles */
-static uint32_t wslot_lds(uint32_t wslots, uint32_t nt, uint32_t cflags)
-{
-	const uint32_t vb = (cflags & GCL_CFG_VERDICT2) ? 2u : (cflags & GCL_CFG_VERDICT4) ? 4u : 8u;
-	return wslots ? wslots * (nt * vb + 8) + 16 : 0;
-}
-
 template <int MODE>
-static hipError_t launch_mode(const KParams &k0, bool tlds, bool general, const Geometry &geo,
+static hipError_t launch_mode(const KParams &k, bool tlds, bool general, const Geometry &geo,
                               uint32_t tab_lds, uint32_t hist_bytes, int num_cus, hipStream_t s)
 {
-	KParams k = k0;
-	uint32_t lds = (uint32_t)geo.threads * 64 + kLdsQueueBytes + hist_bytes + tab_lds;
-	lds = (lds + 15) & ~15u;
-	k.wbuf_off = lds;
-	lds += wslot_lds(k.wslots, (uint32_t)geo.threads, k.cflags);
+	const uint32_t lds = (uint32_t)geo.threads * 64 + kLdsQueueBytes + hist_bytes + tab_lds;
 #define GCL_LAUNCH(D, T) \
 	return launch_nt<MODE, D, T>(k, tlds, general, lds, num_cus, geo.bpc_cap, s)
 	if (geo.depth == 2) {
@@ -1756,8 +1668,7 @@ static Geometry choose_geometry(const gcl_ctx *c, uint32_t tab_lds, uint32_t his
 	g.depth = 1;
 	g.threads = 0;
 	for (int nt = 256; nt <= 1024 && !g.threads; nt *= 2) {
-		uint32_t per_block = (uint32_t)nt * 64 + kLdsQueueBytes + hist_bytes + tab_lds + 16 +
-		                     wslot_lds(c->tune_wslots, (uint32_t)nt, kernel_cflags(c));
+		uint32_t per_block = (uint32_t)nt * 64 + kLdsQueueBytes + hist_bytes + tab_lds;
 		if ((lanes_cu / nt) * per_block <= lds_cu) {
 			g.threads = nt;
 			g.bpc_cap = (int)(lanes_cu / (uint32_t)nt);
@@ -1765,8 +1676,7 @@ static Geometry choose_geometry(const gcl_ctx *c, uint32_t tab_lds, uint32_t his
 	}
 	if (!g.threads) { /* big tables: as many 256-lane blocks as LDS admits */
 		g.threads = 256;
-		g.bpc_cap = (int)(lds_cu / (256u * 64 + kLdsQueueBytes + hist_bytes + tab_lds + 16 +
-		                            wslot_lds(c->tune_wslots, 256, kernel_cflags(c))));
+		g.bpc_cap = (int)(lds_cu / (256u * 64 + kLdsQueueBytes + hist_bytes + tab_lds));
 		if (g.bpc_cap < 1)
 			g.bpc_cap = 1;
 	} else if (g.threads <= 512 && !c->tune_sched) {
@@ -1932,9 +1842,6 @@ extern "C" int gcl_classify_ex(struct gcl_ctx *c, const struct gcl_batch *b,
 	k.ablate = c->tune_ablate;
 	k.xcd_map = c->tune_xcd_map;
 	k.defer = c->tune_defer;
-	k.wslots = c->tune_wslots;
-	k.wperiod = c->tune_wperiod;
-	k.wwindow = c->tune_wwindow;
 
 	/* the specialised fast path needs every header granule in range */
 	bool general = b->offs || b->olflags || b->fdir_hi || b->dst_hint ||

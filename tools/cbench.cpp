@@ -5,8 +5,7 @@
 // (env CBENCH_N, CBENCH_STRIDE, CBENCH_R override the workload's shape)
 //
 // Each cfg is "ABLATE:GRID:DEPTH:THREADS:BPC:SCHED:V4[:NT[:DEFER]]" (NT = GCL_TUNE_NT_STORE,
-// DEFER = GCL_TUNE_DEFER, -1 or absent = library default; a suffix "@S/P/W" sets
-// GCL_TUNE_WSLOT=S:P:W for that cfg) (GCL_TUNE_* knobs, 0 = default;
+// DEFER = GCL_TUNE_DEFER, -1 or absent = library default) (GCL_TUNE_* knobs, 0 = default;
 // V4=1 classifies into 4-byte verdicts, GCL_CFG_VERDICT4; V4=2 into 2-byte queue
 // verdicts, GCL_CFG_VERDICT2).
 // CBENCH_NOISE_US=X co-runs, on a second stream, 32 one-wave blocks that each
@@ -209,18 +208,6 @@ int main(int argc, char **argv)
 			setenv("GCL_TUNE_SCHED", buf, 1);
 			snprintf(buf, sizeof(buf), "%d", c.nt);
 			setenv("GCL_TUNE_NT_STORE", buf, 1);
-			{ /* "cfg@slots/period/window": GCL_TUNE_WSLOT for this cfg */
-				const size_t at = c.name.find('@');
-				if (at != std::string::npos) {
-					std::string w = c.name.substr(at + 1);
-					for (char &ch : w)
-						if (ch == '/')
-							ch = ':';
-					setenv("GCL_TUNE_WSLOT", w.c_str(), 1);
-				} else {
-					unsetenv("GCL_TUNE_WSLOT");
-				}
-			}
 			if (c.defer >= 0) {
 				snprintf(buf, sizeof(buf), "%d", c.defer);
 				setenv("GCL_TUNE_DEFER", buf, 1);
