@@ -102,6 +102,7 @@ struct KParams {
 	uint32_t *sched; /* tile queue slot (SchedSlot) or NULL = static persistent grid */
 	uint32_t xcd_map; /* static grid: 1 = each XCD walks one contiguous eighth of the tiles */
 	uint32_t defer;   /* 1: a tile's verdicts are stored after the next tile's barrier */
+	uint32_t offs_lds; /* 1: per-frame offsets shared through LDS (NT u64 after the tables) */
 };
 
 /* Dynamic tile queue of one launch: tiles are dealt per XCD (tile t belongs
@@ -174,9 +175,16 @@ __device__ __forceinline__ uint32_t hdr_window(const KParams &k, uint64_t off, u
 	return s;
 }
 
+/*
+ * @s_off (GENERAL with per-frame offsets, classify_kernel): the tile's frame
+ * offsets already in LDS, one per packet, and @my_off this lane's own; the
+ * four chunk loads then wait on LDS reads instead of four dependent global
+ * loads of offs[].  NULL: offsets read from global memory here.
+ */
 template <bool GENERAL, int NT>
 __device__ __forceinline__ void load_tile(const KParams &k, uint64_t tile, uint4 r[4],
-                                          uint32_t &span)
+                                          uint32_t &span, const uint64_t *s_off = nullptr,
+                                          uint64_t my_off = 0)
 {
 	/* where this lane's own packet of the tile sits in its staged row
 	 * (hdr_window): shift | staged frame bytes << 8, for classify_one */
@@ -185,7 +193,7 @@ __device__ __forceinline__ void load_tile(const KParams &k, uint64_t tile, uint4
 		const uint64_t me = tile * NT + threadIdx.x;
 		if (me < k.n) {
 			uint32_t cut;
-			const uint32_t sh = hdr_window(k, frame_off<GENERAL>(k, me), cut);
+			const uint32_t sh = hdr_window(k, s_off ? my_off : frame_off<GENERAL>(k, me), cut);
 			if (sh != 0xFF)
 				span = sh | (cut - sh) << 8;
 		}
@@ -208,7 +216,7 @@ __device__ __forceinline__ void load_tile(const KParams &k, uint64_t tile, uint4
 		uint64_t idx = tile * NT + (uint64_t)(c >> 2);
 		uint4 v = make_uint4(0, 0, 0, 0);
 		if (idx < k.n) {
-			const uint64_t off = frame_off<GENERAL>(k, idx);
+			const uint64_t off = (GENERAL && s_off) ? s_off[c >> 2] : frame_off<GENERAL>(k, idx);
 			const uint32_t q16 = (uint32_t)(c & 3) * 16;
 			uint32_t cut = 64;
 			const uint32_t sh = GENERAL ? hdr_window(k, off, cut) : 0u;
@@ -561,7 +569,9 @@ __device__ __forceinline__ uint64_t sched_resolve(uint32_t *sched, uint64_t ntil
  * is parsed.
  */
 template <int MODE, bool TLDS, bool GENERAL, int DEPTH, int NT>
-__global__ void __launch_bounds__(NT)
+/* 4 waves per SIMD (<= 128 VGPRs): the 1024 resident lanes per CU the
+ * geometry policy plans for, at every tile size */
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4)))
 classify_kernel(KParams k)
 {
 	extern __shared__ uint4 smem[];
@@ -625,6 +635,24 @@ classify_kernel(KParams k)
 		load_tile<GENERAL, NT>(k, t, ra, spa);
 	if (DEPTH == 2 && t + step < t_end)
 		load_tile<GENERAL, NT>(k, t + step, rb, spb);
+	/* Per-frame offsets go through LDS (GENERAL, offs[], static walk): each
+	 * lane loads only its own packet's offset, DEPTH tiles ahead of the tile
+	 * whose frames it is for (offa/offb, coalesced), publishes it in s_off
+	 * before the stage barrier, and the chunk loads after the barrier read
+	 * their packets' offsets from LDS -- no dependent global offs[] loads on
+	 * the way to the frame loads (k.offs_lds). */
+	const bool goffs = GENERAL && k.offs && !dyn && k.offs_lds;
+	uint64_t *s_off = (uint64_t *)(lds_tab + k.tables_lds_bytes);
+	auto my_off = [&](uint64_t tt) -> uint64_t {
+		const uint64_t i = tt * NT + tid;
+		return (tt < t_end && i < k.n) ? k.offs[i] : 0;
+	};
+	uint64_t offa = 0, offb = 0;
+	if (goffs) {
+		offa = my_off(t + DEPTH * step);
+		if (DEPTH == 2)
+			offb = my_off(t + 3 * step);
+	}
 	if (dyn && tid == 0)
 		s_next[0] = t < k.ntiles ? sched_resolve(k.sched, k.ntiles, (uint32_t)G, x0, xs, got)
 		                         : k.ntiles;
@@ -653,6 +681,8 @@ classify_kernel(KParams k)
 	while (t < t_end) {
 		stage_tile<NT>(tile, ra);
 		const uint32_t sp = spa;
+		if (goffs)
+			s_off[tid] = offa;
 		__syncthreads();
 		flush();
 		uint64_t nxt = t + DEPTH * step;
@@ -663,8 +693,14 @@ classify_kernel(KParams k)
 			if (tid == 0 && nxt < k.ntiles)
 				got = atomicAdd(&k.sched[xs * GCL_SCHED_LINE], 1u);
 		}
-		if (nxt < t_end)
-			load_tile<GENERAL, NT>(k, nxt, ra, spa); /* in flight while parsing */
+		if (nxt < t_end) { /* in flight while parsing */
+			if (goffs)
+				load_tile<GENERAL, NT>(k, nxt, ra, spa, s_off, offa);
+			else
+				load_tile<GENERAL, NT>(k, nxt, ra, spa);
+		}
+		if (goffs)
+			offa = my_off(nxt + DEPTH * step);
 		if (k.ablate & 16) { /* timing only: the membench tile_v0 body */
 			const uint4 a = tile[tile_slot(tid, 0)], b = tile[tile_slot(tid, 1)];
 			*(u32x2 *)&k.verdicts[t * NT + tid] = u32x2{b.z ^ a.x, a.w ^ b.y};
@@ -687,10 +723,18 @@ classify_kernel(KParams k)
 				break;
 			stage_tile<NT>(tile, rb);
 			const uint32_t sp2 = spb;
+			if (goffs)
+				s_off[tid] = offb;
 			__syncthreads();
 			flush();
-			if (t + 2 * step < t_end)
-				load_tile<GENERAL, NT>(k, t + 2 * step, rb, spb);
+			if (t + 2 * step < t_end) {
+				if (goffs)
+					load_tile<GENERAL, NT>(k, t + 2 * step, rb, spb, s_off, offb);
+				else
+					load_tile<GENERAL, NT>(k, t + 2 * step, rb, spb);
+			}
+			if (goffs)
+				offb = my_off(t + 4 * step);
 			if (t * NT + tid < k.n)
 				verdict(t * NT + tid, classify_one<MODE, GENERAL>(k, tile, tid, t * NT + tid, tb,
 				                                                  hist, cnt, sp2));
@@ -1208,6 +1252,7 @@ struct gcl_ctx {
 	int tune_sched;    /* GCL_TUNE_SCHED: 0 static persistent grid, 1 dynamic tile queue */
 	int tune_xcd_map;  /* GCL_TUNE_XCD_MAP: 1 contiguous eighth per XCD, 0 round-robin tiles */
 	int tune_defer;    /* GCL_TUNE_DEFER: 1 verdict stores one tile late, 0 at once (default) */
+	int tune_offs_lds; /* GCL_TUNE_OFFS_LDS: 1 per-frame offsets shared through LDS (default) */
 	/* dynamic tile queue: one slot per launch in flight, reused in turn; a
 	 * launch waits for the previous user of its slot (same or other stream) */
 	uint32_t *sched;
@@ -1293,6 +1338,8 @@ extern "C" int gcl_open(int hip_device, const struct gcl_cfg *cfg, struct gcl_ct
 		c->tune_xcd_map = e ? atoi(e) : kDefaultXcdMap;
 		e = getenv("GCL_TUNE_DEFER");
 		c->tune_defer = e ? atoi(e) : kDefaultDefer;
+		e = getenv("GCL_TUNE_OFFS_LDS");
+		c->tune_offs_lds = e ? atoi(e) : 1;
 	}
 	c->dimg[0] = c->dimg[1] = nullptr;
 	c->sched = nullptr;
@@ -1634,11 +1681,18 @@ struct Geometry {
 	int bpc_cap;  /* blocks per CU */
 };
 
+/* LDS for the tile's frame offsets when they are shared through LDS */
+static uint32_t offs_lds_bytes(bool offs_lds, uint32_t nt)
+{
+	return offs_lds ? nt * 8 : 0;
+}
+
 template <int MODE>
 static hipError_t launch_mode(const KParams &k, bool tlds, bool general, const Geometry &geo,
                               uint32_t tab_lds, uint32_t hist_bytes, int num_cus, hipStream_t s)
 {
-	const uint32_t lds = (uint32_t)geo.threads * 64 + kLdsQueueBytes + hist_bytes + tab_lds;
+	const uint32_t lds = (uint32_t)geo.threads * 64 + kLdsQueueBytes + hist_bytes + tab_lds +
+	                     offs_lds_bytes(k.offs_lds, (uint32_t)geo.threads);
 #define GCL_LAUNCH(D, T) \
 	return launch_nt<MODE, D, T>(k, tlds, general, lds, num_cus, geo.bpc_cap, s)
 	if (geo.depth == 2) {
@@ -1661,14 +1715,16 @@ static hipError_t launch_mode(const KParams &k, bool tlds, bool general, const G
  * tables serves twice the packets (tcp1500: 234 -> 206 us).  More resident
  * waves than that only add contention (udp64: 446 us at 8 x 256).
  */
-static Geometry choose_geometry(const gcl_ctx *c, uint32_t tab_lds, uint32_t hist_bytes)
+static Geometry choose_geometry(const gcl_ctx *c, uint32_t tab_lds, uint32_t hist_bytes,
+                                bool offs_lds)
 {
 	const uint32_t lds_cu = 160 * 1024, lanes_cu = 1024;
 	Geometry g;
 	g.depth = 1;
 	g.threads = 0;
 	for (int nt = 256; nt <= 1024 && !g.threads; nt *= 2) {
-		uint32_t per_block = (uint32_t)nt * 64 + kLdsQueueBytes + hist_bytes + tab_lds;
+		uint32_t per_block = (uint32_t)nt * 64 + kLdsQueueBytes + hist_bytes + tab_lds +
+		                     offs_lds_bytes(offs_lds, (uint32_t)nt);
 		if ((lanes_cu / nt) * per_block <= lds_cu) {
 			g.threads = nt;
 			g.bpc_cap = (int)(lanes_cu / (uint32_t)nt);
@@ -1676,7 +1732,8 @@ static Geometry choose_geometry(const gcl_ctx *c, uint32_t tab_lds, uint32_t his
 	}
 	if (!g.threads) { /* big tables: as many 256-lane blocks as LDS admits */
 		g.threads = 256;
-		g.bpc_cap = (int)(lds_cu / (256u * 64 + kLdsQueueBytes + hist_bytes + tab_lds));
+		g.bpc_cap = (int)(lds_cu / (256u * 64 + kLdsQueueBytes + hist_bytes + tab_lds +
+		                            offs_lds_bytes(offs_lds, 256)));
 		if (g.bpc_cap < 1)
 			g.bpc_cap = 1;
 	} else if (g.threads <= 512 && !c->tune_sched) {
@@ -1855,7 +1912,8 @@ extern "C" int gcl_classify_ex(struct gcl_ctx *c, const struct gcl_batch *b,
 	else if (c->tune_tables == 2)
 		tlds = tab_bytes <= kLdsTableBudget;
 	k.tables_lds_bytes = tlds ? tab_bytes : 0;
-	Geometry geo = choose_geometry(c, tlds ? tab_bytes : 0, hist_bytes);
+	k.offs_lds = general && b->offs && c->tune_offs_lds;
+	Geometry geo = choose_geometry(c, tlds ? tab_bytes : 0, hist_bytes, k.offs_lds);
 
 	HipErr he;
 	int slot = -1;

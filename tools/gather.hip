@@ -8,6 +8,7 @@
 //   random    64 random permutations of the pool (the bench's order)
 //   address   the pool in address order, 64 times
 //   dense     a dense 64-B slot array of the same packet count (udp64 shape)
+//   working_set_4096  a random 4096-mbuf subset of the pool in random order
 // Prints the kernel time and packets/s per order.
 // Build: hipcc --offload-arch=gfx950 -O3 -o tools/gather tools/gather.hip
 #include <hip/hip_runtime.h>
@@ -45,7 +46,7 @@ int main(int argc, char **argv)
 	const unsigned long long P = 131072, per_page = 222, elt = 9408, data = 344, cycles = 64;
 	const unsigned long long region = (P + per_page - 1) / per_page * (2ull << 20);
 	const unsigned long long n = P * cycles;
-	std::vector<unsigned long long> pool(P), rnd(n), adr(n), dense(n);
+	std::vector<unsigned long long> pool(P), rnd(n), adr(n), dense(n), wset(n);
 	for (unsigned long long i = 0; i < P; i++)
 		pool[i] = (i / per_page) * (2ull << 20) + (i % per_page) * elt + data;
 	std::mt19937_64 rng(0xCA1ADA4);
@@ -61,6 +62,18 @@ int main(int argc, char **argv)
 	}
 	for (unsigned long long i = 0; i < n; i++)
 		dense[i] = i * 64;
+	{ /* a 4096-mbuf working set in random order (RX ring + mempool cache) */
+		const unsigned long long W = 4096;
+		for (unsigned long long i = 0; i < P; i++)
+			perm[i] = i;
+		std::shuffle(perm.begin(), perm.end(), rng);
+		std::vector<unsigned long long> sub(perm.begin(), perm.begin() + W);
+		for (unsigned long long c = 0; c < n / W; c++) {
+			std::shuffle(sub.begin(), sub.end(), rng);
+			for (unsigned long long i = 0; i < W; i++)
+				wset[c * W + i] = pool[sub[i]];
+		}
+	}
 	const unsigned long long bytes = std::max(region, n * 64);
 	unsigned char *buf;
 	unsigned long long *d_offs;
@@ -75,7 +88,7 @@ int main(int argc, char **argv)
 	CHECK(hipEventCreate(&a));
 	CHECK(hipEventCreate(&b));
 	const struct { const char *name; std::vector<unsigned long long> *o; } orders[] = {
-		{"random", &rnd}, {"address", &adr}, {"dense", &dense}};
+		{"random", &rnd}, {"address", &adr}, {"dense", &dense}, {"working_set_4096", &wset}};
 	for (auto &ord : orders) {
 		CHECK(hipMemcpy(d_offs, ord.o->data(), n * 8, hipMemcpyHostToDevice));
 		for (int g : {cus * 4, cus * 8, cus * 16}) {
