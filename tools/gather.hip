@@ -9,7 +9,9 @@
 //   address   the pool in address order, 64 times
 //   dense     a dense 64-B slot array of the same packet count (udp64 shape)
 //   working_set_4096  a random 4096-mbuf subset of the pool in random order
-// Prints the kernel time and packets/s per order.
+// Two kernels: `gather` (one 16-B chunk per lane, its descriptor loaded
+// right before it) and `gather_lds` (the classify kernel's form: descriptors
+// shared through LDS, one tile ahead).  Prints the kernel time and packets/s.
 // Build: hipcc --offload-arch=gfx950 -O3 -o tools/gather tools/gather.hip
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -35,6 +37,41 @@ __global__ void __launch_bounds__(256) gather_kernel(const unsigned char *pool, 
 		const unsigned long long o = (__builtin_nontemporal_load(offs + (c >> 2)) & ~15ull) + (c & 3) * 16;
 		const u32x4 v = __builtin_nontemporal_load((const u32x4 *)(pool + o));
 		acc ^= v.x ^ v.y ^ v.z ^ v.w;
+	}
+	if (acc == 0x9E3779B9u)
+		out[blockIdx.x] = acc;
+}
+
+// the classify kernel's decoupled form: a 256-lane block takes 256
+// descriptors per tile, each lane loading its own packet's descriptor one
+// tile ahead; after a barrier the descriptors come from LDS and the four
+// lanes of each 64-B window issue their 16-B loads (coalesced), two tiles of
+// loads in flight
+__global__ void __launch_bounds__(256) gather_lds_kernel(const unsigned char *pool,
+                                                         const unsigned long long *offs,
+                                                         unsigned long long n, unsigned *out)
+{
+	__shared__ unsigned long long s_off[2][256];
+	unsigned acc = 0;
+	const unsigned long long ntiles = n / 256, G = gridDim.x;
+	unsigned long long t = blockIdx.x;
+	unsigned long long mine = t < ntiles ? __builtin_nontemporal_load(offs + t * 256 + threadIdx.x) : 0;
+	int par = 0;
+	for (; t < ntiles; t += G, par ^= 1) {
+		s_off[par][threadIdx.x] = mine;
+		__syncthreads();
+		if (t + G < ntiles)
+			mine = __builtin_nontemporal_load(offs + (t + G) * 256 + threadIdx.x);
+		u32x4 v[4];
+#pragma unroll
+		for (int j = 0; j < 4; j++) {
+			const int c = j * 256 + (int)threadIdx.x;
+			v[j] = __builtin_nontemporal_load(
+			        (const u32x4 *)(pool + (s_off[par][c >> 2] & ~15ull) + (c & 3) * 16));
+		}
+#pragma unroll
+		for (int j = 0; j < 4; j++)
+			acc ^= v[j].x ^ v[j].y ^ v[j].z ^ v[j].w;
 	}
 	if (acc == 0x9E3779B9u)
 		out[blockIdx.x] = acc;
@@ -101,9 +138,24 @@ int main(int argc, char **argv)
 			float ms = 0;
 			CHECK(hipEventElapsedTime(&ms, a, b));
 			const double us = ms * 1e3 / reps;
-			printf("{\"order\": \"%s\", \"blocks\": %d, \"pkts\": %llu, \"us\": %.2f, \"Mpkts\": %.1f, "
-			       "\"desc_plus_window_GBs\": %.1f}\n", ord.name, g, n, us, n / us,
+			printf("{\"order\": \"%s\", \"kernel\": \"gather\", \"blocks\": %d, \"pkts\": %llu, \"us\": %.2f, "
+			       "\"Mpkts\": %.1f, \"desc_plus_window_GBs\": %.1f}\n", ord.name, g, n, us, n / us,
 			       n * 72.0 / (us * 1e-6) / 1e9);
+			fflush(stdout);
+		}
+		for (int g : {cus * 4, cus * 8, cus * 16}) {
+			hipLaunchKernelGGL(gather_lds_kernel, dim3(g), dim3(256), 0, 0, buf, d_offs, n, out);
+			CHECK(hipEventRecord(a, 0));
+			for (int r = 0; r < reps; r++)
+				hipLaunchKernelGGL(gather_lds_kernel, dim3(g), dim3(256), 0, 0, buf, d_offs, n, out);
+			CHECK(hipEventRecord(b, 0));
+			CHECK(hipEventSynchronize(b));
+			float ms = 0;
+			CHECK(hipEventElapsedTime(&ms, a, b));
+			const double us = ms * 1e3 / reps;
+			printf("{\"order\": \"%s\", \"kernel\": \"gather_lds\", \"blocks\": %d, \"pkts\": %llu, "
+			       "\"us\": %.2f, \"Mpkts\": %.1f, \"desc_plus_window_GBs\": %.1f}\n", ord.name, g, n, us,
+			       n / us, n * 72.0 / (us * 1e-6) / 1e9);
 			fflush(stdout);
 		}
 	}
