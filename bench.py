@@ -622,7 +622,8 @@ INGRESS_DESC_BYTES = 8 + 1 + 4
 INGRESS_WORKING_SET = 4096
 
 
-def ingress_pool_bench(device, vbytes, cycles=64, reps=10, zerocopy=True):
+def ingress_pool_bench(device, vbytes, cycles=64, reps=10, zerocopy=True,
+                       rows=("nic", "jenkins", "working_set")):
     """Frames where the reference keeps them (§8f-2): the 131072-mbuf ingress
     pool, 9408-B elements, 222 per 2 MiB page, frame data at element + 344
     (8-B aligned; iokernel/defs.h:70, :503-523).  A batch is `cycles` random
@@ -668,6 +669,10 @@ def ingress_pool_bench(device, vbytes, cycles=64, reps=10, zerocopy=True):
         "device_resident_mpps": round(n / wall / 1e6, 1), "counts_check": "ok" if ok else "MISMATCH",
         "roofline": roofline_obj(n * bpp, gms, pmc_traffic("ingress_nic", vbytes),
                                  {"bytes_per_pkt": bpp})}
+    if rows == ("nic",):  # rocprof of the random-pool row alone (tools/ingress_run.py)
+        del region, offs, olf, rss, dv, nic
+        torch.cuda.empty_cache()
+        return out
     cnt.zero_()
     jen = classifier(device, R, T, vbytes)
     setup_tables(jen, R, T)

@@ -12,7 +12,7 @@ OUT=gpurun_out/prof_$R
 mkdir -p $OUT
 run_cmd() { # workload, vbytes, steps -> the program and its arguments
   if [ "$1" = ingress_nic ]; then
-    echo "python3 tools/ingress_run.py $3"
+    echo "python3 tools/ingress_run.py $3 --nic-only"
   else
     echo "python3 bench.py --workload $1 --verdict-bytes $2 --no-cpu --no-secondary --no-e2e --steps $3 --warmup 1"
   fi
