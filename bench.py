@@ -656,58 +656,66 @@ def ingress_pool_bench(device, vbytes, cycles=64, reps=10, zerocopy=True,
     st = torch.cuda.current_stream().cuda_stream
     nic = classifier(device, R, T, vbytes, hash_mode=g.HASH_NIC)
     setup_tables(nic, R, T)
-
-    def nic_step():
-        nic.classify(region, n, 0, verdicts=dv, counts=cnt[:R], stats=cnt[R:], offs=offs,
-                     olflags=olf, rss=rss, stream=st)
-
-    wall, gms = timed_launches(nic_step, reps)
-    ok = int(cnt[:R].sum().item()) % n == 0 and int(cnt[R + g.RX_PULLED].item()) == int(cnt[:R].sum().item())
     bpp = HDR_BYTES + INGRESS_DESC_BYTES + vbytes
-    out["integrated_nic"] = {
-        "what": "offs[] + ol_flags[] + hash.rss[] per descriptor, GCL_HASH_NIC (INTEGRATION.md §4)",
-        "device_resident_mpps": round(n / wall / 1e6, 1), "counts_check": "ok" if ok else "MISMATCH",
-        "roofline": roofline_obj(n * bpp, gms, pmc_traffic("ingress_nic", vbytes),
-                                 {"bytes_per_pkt": bpp})}
-    if rows == ("nic",):  # rocprof of the random-pool row alone (tools/ingress_run.py)
-        del region, offs, olf, rss, dv, nic
-        torch.cuda.empty_cache()
-        return out
-    cnt.zero_()
-    jen = classifier(device, R, T, vbytes)
-    setup_tables(jen, R, T)
 
-    def jen_step():
-        jen.classify(region, n, 0, verdicts=dv, counts=cnt[:R], stats=cnt[R:], offs=offs, stream=st)
+    def counts_ok():
+        tot = int(cnt[:R].sum().item())
+        return tot % n == 0 and int(cnt[R + g.RX_PULLED].item()) == tot
 
-    wall_j, gms_j = timed_launches(jen_step, reps)
-    okj = int(cnt[:R].sum().item()) % n == 0 and int(cnt[R + g.RX_PULLED].item()) == int(cnt[:R].sum().item())
-    out["jenkins_offs_only"] = {"device_resident_mpps": round(n / wall_j / 1e6, 1),
-                                "kernel_ms": round(gms_j, 4), "counts_check": "ok" if okj else "MISMATCH"}
-    # the working set the reference really cycles: mbufs come back through the
-    # iokernel lcore's LIFO mempool cache (MBUF_CACHE_SIZE 250, rx.c:21) into
-    # an RX ring of 256 / 2048 descriptors (dpdk.c:50-53), so a few thousand
-    # mbufs are in rotation, not the whole 131072-mbuf pool
-    ws = INGRESS_WORKING_SET
-    sub = torch.randperm(P, generator=gen)[:ws]
-    order_ws = torch.cat([sub[torch.randperm(ws, generator=gen)] for _ in range(n // ws)]).to(device)
-    offs_w, olf_w, rss_w = (pool_offs[order_ws].contiguous(), olf_p[order_ws].contiguous(),
-                            rss_p[order_ws].contiguous())
-    cnt.zero_()
+    if "nic" in rows:
+        cnt.zero_()
 
-    def ws_step():
-        nic.classify(region, n, 0, verdicts=dv, counts=cnt[:R], stats=cnt[R:], offs=offs_w,
-                     olflags=olf_w, rss=rss_w, stream=st)
+        def nic_step():
+            nic.classify(region, n, 0, verdicts=dv, counts=cnt[:R], stats=cnt[R:], offs=offs,
+                         olflags=olf, rss=rss, stream=st)
 
-    wall_w, gms_w = timed_launches(ws_step, reps)
-    okw = int(cnt[:R].sum().item()) % n == 0 and int(cnt[R + g.RX_PULLED].item()) == int(cnt[:R].sum().item())
-    out["integrated_nic_working_set"] = {
-        "what": (f"as integrated_nic, descriptors drawn from a working set of {ws} mbufs in random "
-                 f"order (RX ring 2048 + mempool cache 250 + in flight)"),
-        "device_resident_mpps": round(n / wall_w / 1e6, 1), "counts_check": "ok" if okw else "MISMATCH",
-        "roofline": roofline_obj(n * bpp, gms_w, None, {"bytes_per_pkt": bpp})}
-    del offs_w, olf_w, rss_w, order_ws
-    if not zerocopy:
+        wall, gms = timed_launches(nic_step, reps)
+        out["integrated_nic"] = {
+            "what": "offs[] + ol_flags[] + hash.rss[] per descriptor, GCL_HASH_NIC (INTEGRATION.md §4)",
+            "device_resident_mpps": round(n / wall / 1e6, 1),
+            "counts_check": "ok" if counts_ok() else "MISMATCH",
+            "roofline": roofline_obj(n * bpp, gms, pmc_traffic("ingress_nic", vbytes),
+                                     {"bytes_per_pkt": bpp})}
+    jen = None
+    if "jenkins" in rows:
+        cnt.zero_()
+        jen = classifier(device, R, T, vbytes)
+        setup_tables(jen, R, T)
+
+        def jen_step():
+            jen.classify(region, n, 0, verdicts=dv, counts=cnt[:R], stats=cnt[R:], offs=offs,
+                         stream=st)
+
+        wall_j, gms_j = timed_launches(jen_step, reps)
+        out["jenkins_offs_only"] = {"device_resident_mpps": round(n / wall_j / 1e6, 1),
+                                    "kernel_ms": round(gms_j, 4),
+                                    "counts_check": "ok" if counts_ok() else "MISMATCH"}
+    if "working_set" in rows:
+        # the working set the reference really cycles: mbufs come back through
+        # the iokernel lcore's LIFO mempool cache (MBUF_CACHE_SIZE 250, rx.c:21)
+        # into an RX ring of 256 / 2048 descriptors (dpdk.c:50-53), so a few
+        # thousand mbufs are in rotation, not the whole 131072-mbuf pool
+        ws = INGRESS_WORKING_SET
+        sub = torch.randperm(P, generator=gen)[:ws]
+        order_ws = torch.cat([sub[torch.randperm(ws, generator=gen)] for _ in range(n // ws)]).to(device)
+        offs_w, olf_w, rss_w = (pool_offs[order_ws].contiguous(), olf_p[order_ws].contiguous(),
+                                rss_p[order_ws].contiguous())
+        cnt.zero_()
+
+        def ws_step():
+            nic.classify(region, n, 0, verdicts=dv, counts=cnt[:R], stats=cnt[R:], offs=offs_w,
+                         olflags=olf_w, rss=rss_w, stream=st)
+
+        wall_w, gms_w = timed_launches(ws_step, reps)
+        out["integrated_nic_working_set"] = {
+            "what": (f"as integrated_nic, descriptors drawn from a working set of {ws} mbufs in random "
+                     f"order (RX ring 2048 + mempool cache 250 + in flight)"),
+            "device_resident_mpps": round(n / wall_w / 1e6, 1),
+            "counts_check": "ok" if counts_ok() else "MISMATCH",
+            "roofline": roofline_obj(n * bpp, gms_w, pmc_traffic("ingress_ws", vbytes),
+                                     {"bytes_per_pkt": bpp})}
+        del offs_w, olf_w, rss_w, order_ws
+    if not zerocopy or "nic" not in rows:
         del region, offs, olf, rss, dv, nic, jen
         torch.cuda.empty_cache()
         return out

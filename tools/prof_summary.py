@@ -20,13 +20,14 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HDR_BYTES = 64
-PKTS = {"udp64": 32 << 20, "tcp1500": 8 << 20, "mixed": 1 << 20, "ingress_nic": 8 << 20}
+PKTS = {"udp64": 32 << 20, "tcp1500": 8 << 20, "mixed": 1 << 20, "ingress_nic": 8 << 20,
+        "ingress_ws": 8 << 20}
 # per-packet bytes besides the 64-B header and the verdict: the integrated
 # ingress shape reads a u64 offset, u8 ol_flags and u32 hash.rss per descriptor
-EXTRA = {"ingress_nic": 8 + 1 + 4}
+EXTRA = {"ingress_nic": 8 + 1 + 4, "ingress_ws": 8 + 1 + 4}
 # which classify_kernel instance is the workload's: the ingress run also
 # launches the JENKINS (MODE 1) row; its NIC launches are MODE 0
-KNAME = {"ingress_nic": "classify_kernel<0,"}
+KNAME = {"ingress_nic": "classify_kernel<0,", "ingress_ws": "classify_kernel<0,"}
 
 
 def is_kernel(wl, name):

@@ -13,6 +13,8 @@ mkdir -p $OUT
 run_cmd() { # workload, vbytes, steps -> the program and its arguments
   if [ "$1" = ingress_nic ]; then
     echo "python3 tools/ingress_run.py $3 --nic-only"
+  elif [ "$1" = ingress_ws ]; then
+    echo "python3 tools/ingress_run.py $3 --ws-only"
   else
     echo "python3 bench.py --workload $1 --verdict-bytes $2 --no-cpu --no-secondary --no-e2e --steps $3 --warmup 1"
   fi
