@@ -176,24 +176,89 @@ __device__ __forceinline__ uint32_t hdr_window(const KParams &k, uint64_t off, u
 }
 
 /*
- * @s_off (GENERAL with per-frame offsets, classify_kernel): the tile's frame
- * offsets already in LDS, one per packet, and @my_off this lane's own; the
- * four chunk loads then wait on LDS reads instead of four dependent global
- * loads of offs[].  NULL: offsets read from global memory here.
+ * Where the chunk loads of a packet at frame offset @off read from, as
+ * published in LDS by the packet's own lane (classify_kernel's offs_lds
+ * path): {base lo, base hi, w, 0} with
+ *   w = shift | cut << 8 (> 0xFF)  the hdr_window, base = off - shift, and
+ *                                  the window's [0, cut) inside frames_len
+ *   w = 0xFF                       bytewise from base = off (unaligned frame,
+ *                                  or a window running past frames_len)
+ *   w = 0                          no packet (@off == kNoOff, past the batch)
+ * so a chunk load is one LDS read, a compare and a 64-bit add.
+ */
+constexpr uint64_t kNoOff = ~0ull;
+
+__device__ __forceinline__ uint4 hdr_src(const KParams &k, uint64_t off)
+{
+	if (off == kNoOff)
+		return make_uint4(0, 0, 0, 0);
+	uint32_t cut;
+	const uint32_t sh = hdr_window(k, off, cut);
+	uint64_t base = off;
+	uint32_t w = 0xFF;
+	if (sh != 0xFF && off - sh + cut <= k.frames_len) {
+		base = off - sh;
+		w = sh | cut << 8;
+	}
+	return make_uint4((uint32_t)base, (uint32_t)(base >> 32), w, 0);
+}
+
+/* 16 frame bytes from @a, bytewise (frame_byte: zero past frames_len) */
+__device__ __forceinline__ uint4 load16_bytes(const KParams &k, uint64_t a)
+{
+	uint32_t w[4];
+	for (int b = 0; b < 4; b++)
+		w[b] = frame_byte(k, a + 4 * b) | frame_byte(k, a + 4 * b + 1) << 8 |
+		       frame_byte(k, a + 4 * b + 2) << 16 | (uint32_t)frame_byte(k, a + 4 * b + 3) << 24;
+	return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+/*
+ * @s_src (GENERAL with per-frame offsets, classify_kernel): the tile's
+ * packets' hdr_src entries already in LDS, so the four chunk loads wait on
+ * one LDS read each instead of dependent global loads of offs[], and the
+ * window arithmetic and bounds checks ran once per packet, not per chunk.
+ * NULL: offsets read from global memory here.
  */
 template <bool GENERAL, int NT>
 __device__ __forceinline__ void load_tile(const KParams &k, uint64_t tile, uint4 r[4],
-                                          uint32_t &span, const uint64_t *s_off = nullptr,
-                                          uint64_t my_off = 0)
+                                          uint32_t &span, const uint4 *s_src = nullptr)
 {
 	/* where this lane's own packet of the tile sits in its staged row
 	 * (hdr_window): shift | staged frame bytes << 8, for classify_one */
 	span = kSpanFull;
+	if (GENERAL && s_src) {
+		const uint32_t me = s_src[threadIdx.x].z;
+		if (me > 0xFF)
+			span = (me & 0xFF) | ((me >> 8) - (me & 0xFF)) << 8;
+		bool bytewise = false;
+#pragma unroll
+		for (int j = 0; j < 4; j++) {
+			const int c = j * NT + (int)threadIdx.x;
+			const uint4 s = s_src[c >> 2];
+			const uint32_t q16 = (uint32_t)(c & 3) * 16;
+			uint4 v = make_uint4(0, 0, 0, 0);
+			/* past the first line (q16 >= cut): left 0, read on demand */
+			if (s.z > 0xFF && q16 < (s.z >> 8))
+				v = gcl::load16_nt(k.frames + ((uint64_t)s.y << 32 | s.x) + q16);
+			bytewise |= s.z == 0xFF;
+			r[j] = v;
+		}
+		if (bytewise) { /* rare: unaligned frames, the end of the buffer */
+			for (int j = 0; j < 4; j++) {
+				const int c = j * NT + (int)threadIdx.x;
+				const uint4 s = s_src[c >> 2];
+				if (s.z == 0xFF)
+					r[j] = load16_bytes(k, ((uint64_t)s.y << 32 | s.x) + (uint32_t)(c & 3) * 16);
+			}
+		}
+		return;
+	}
 	if (GENERAL) {
 		const uint64_t me = tile * NT + threadIdx.x;
 		if (me < k.n) {
 			uint32_t cut;
-			const uint32_t sh = hdr_window(k, s_off ? my_off : frame_off<GENERAL>(k, me), cut);
+			const uint32_t sh = hdr_window(k, frame_off<GENERAL>(k, me), cut);
 			if (sh != 0xFF)
 				span = sh | (cut - sh) << 8;
 		}
@@ -216,7 +281,7 @@ __device__ __forceinline__ void load_tile(const KParams &k, uint64_t tile, uint4
 		uint64_t idx = tile * NT + (uint64_t)(c >> 2);
 		uint4 v = make_uint4(0, 0, 0, 0);
 		if (idx < k.n) {
-			const uint64_t off = (GENERAL && s_off) ? s_off[c >> 2] : frame_off<GENERAL>(k, idx);
+			const uint64_t off = frame_off<GENERAL>(k, idx);
 			const uint32_t q16 = (uint32_t)(c & 3) * 16;
 			uint32_t cut = 64;
 			const uint32_t sh = GENERAL ? hdr_window(k, off, cut) : 0u;
@@ -229,22 +294,10 @@ __device__ __forceinline__ void load_tile(const KParams &k, uint64_t tile, uint4
 				} else if (a + 16 <= k.frames_len) {
 					v = gcl::load16_nt(k.frames + a);
 				} else {
-					uint32_t w[4];
-					for (int b = 0; b < 4; b++)
-						w[b] = frame_byte(k, a + 4 * b) |
-						       frame_byte(k, a + 4 * b + 1) << 8 |
-						       frame_byte(k, a + 4 * b + 2) << 16 |
-						       (uint32_t)frame_byte(k, a + 4 * b + 3) << 24;
-					v = make_uint4(w[0], w[1], w[2], w[3]);
+					v = load16_bytes(k, a);
 				}
 			} else {
-				const uint64_t a = off + q16;
-				uint32_t w[4];
-				for (int b = 0; b < 4; b++)
-					w[b] = frame_byte(k, a + 4 * b) | frame_byte(k, a + 4 * b + 1) << 8 |
-					       frame_byte(k, a + 4 * b + 2) << 16 |
-					       (uint32_t)frame_byte(k, a + 4 * b + 3) << 24;
-				v = make_uint4(w[0], w[1], w[2], w[3]);
+				v = load16_bytes(k, off + q16);
 			}
 		}
 		r[j] = v;
@@ -637,15 +690,15 @@ classify_kernel(KParams k)
 		load_tile<GENERAL, NT>(k, t + step, rb, spb);
 	/* Per-frame offsets go through LDS (GENERAL, offs[], static walk): each
 	 * lane loads only its own packet's offset, DEPTH tiles ahead of the tile
-	 * whose frames it is for (offa/offb, coalesced), publishes it in s_off
-	 * before the stage barrier, and the chunk loads after the barrier read
-	 * their packets' offsets from LDS -- no dependent global offs[] loads on
-	 * the way to the frame loads (k.offs_lds). */
+	 * whose frames it is for (offa/offb, coalesced), publishes its hdr_src
+	 * in s_src before the stage barrier, and the chunk loads after the
+	 * barrier read their packets' sources from LDS -- no dependent global
+	 * offs[] loads on the way to the frame loads (k.offs_lds). */
 	const bool goffs = GENERAL && k.offs && !dyn && k.offs_lds;
-	uint64_t *s_off = (uint64_t *)(lds_tab + k.tables_lds_bytes);
+	uint4 *s_src = (uint4 *)(lds_tab + k.tables_lds_bytes);
 	auto my_off = [&](uint64_t tt) -> uint64_t {
 		const uint64_t i = tt * NT + tid;
-		return (tt < t_end && i < k.n) ? k.offs[i] : 0;
+		return (tt < t_end && i < k.n) ? k.offs[i] : kNoOff;
 	};
 	uint64_t offa = 0, offb = 0;
 	if (goffs) {
@@ -682,7 +735,7 @@ classify_kernel(KParams k)
 		stage_tile<NT>(tile, ra);
 		const uint32_t sp = spa;
 		if (goffs)
-			s_off[tid] = offa;
+			s_src[tid] = hdr_src(k, offa);
 		__syncthreads();
 		flush();
 		uint64_t nxt = t + DEPTH * step;
@@ -695,7 +748,7 @@ classify_kernel(KParams k)
 		}
 		if (nxt < t_end) { /* in flight while parsing */
 			if (goffs)
-				load_tile<GENERAL, NT>(k, nxt, ra, spa, s_off, offa);
+				load_tile<GENERAL, NT>(k, nxt, ra, spa, s_src);
 			else
 				load_tile<GENERAL, NT>(k, nxt, ra, spa);
 		}
@@ -724,12 +777,12 @@ classify_kernel(KParams k)
 			stage_tile<NT>(tile, rb);
 			const uint32_t sp2 = spb;
 			if (goffs)
-				s_off[tid] = offb;
+				s_src[tid] = hdr_src(k, offb);
 			__syncthreads();
 			flush();
 			if (t + 2 * step < t_end) {
 				if (goffs)
-					load_tile<GENERAL, NT>(k, t + 2 * step, rb, spb, s_off, offb);
+					load_tile<GENERAL, NT>(k, t + 2 * step, rb, spb, s_src);
 				else
 					load_tile<GENERAL, NT>(k, t + 2 * step, rb, spb);
 			}
@@ -1684,7 +1737,7 @@ struct Geometry {
 /* LDS for the tile's frame offsets when they are shared through LDS */
 static uint32_t offs_lds_bytes(bool offs_lds, uint32_t nt)
 {
-	return offs_lds ? nt * 8 : 0;
+	return offs_lds ? nt * 16 : 0; /* s_src: one hdr_src uint4 per packet */
 }
 
 template <int MODE>
