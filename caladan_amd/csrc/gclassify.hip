@@ -56,12 +56,10 @@ constexpr int kDefaultXcdMap = 0; /* GCL_TUNE_XCD_MAP default: round-robin tiles
  * verdict widths, tcp1500 2-2.4 %, the header-split layout unchanged
  * (profiles/r01_verdict_store_ab.jsonl) */
 constexpr int kDefaultVerdictStore = 2;
-/* GCL_TUNE_DEFER default: verdicts stored at the end of their own tile.
- * Issuing them one tile late (before the next tile's loads, 1) measured
- * udp64 1-3 % slower and tcp1500 0.4 % faster, same buffers, one process
- * (profiles/r02_defer_ab.jsonl), so the store latency is not what the
- * verdict stream costs */
-constexpr int kDefaultDefer = 0;
+/* Verdicts are stored at the end of their own tile.  Issuing them one tile
+ * late (the former GCL_TUNE_DEFER=1) measured udp64 1-3 % slower and tcp1500
+ * 0.4 % faster (profiles/r02_defer_ab.jsonl); the knob was removed for the
+ * registers it held. */
 
 /* tuning knobs for experiments (GCL_TUNE_BLOCKS_PER_CU caps the grid) */
 static int g_tune_bpc = 0;
@@ -101,8 +99,6 @@ struct KParams {
 	uint32_t off_seed, off_crc;
 	uint32_t *sched; /* tile queue slot (SchedSlot) or NULL = static persistent grid */
 	uint32_t xcd_map; /* static grid: 1 = each XCD walks one contiguous eighth of the tiles */
-	uint32_t defer;   /* 1: a tile's verdicts are stored after the next tile's barrier */
-	uint32_t offs_lds; /* 1: per-frame offsets shared through LDS (NT u64 after the tables) */
 };
 
 /* Dynamic tile queue of one launch: tiles are dealt per XCD (tile t belongs
@@ -177,8 +173,8 @@ __device__ __forceinline__ uint32_t hdr_window(const KParams &k, uint64_t off, u
 
 /*
  * Where the chunk loads of a packet at frame offset @off read from, as
- * published in LDS by the packet's own lane (classify_kernel's offs_lds
- * path): {base lo, base hi, w, 0} with
+ * published in LDS by the packet's own lane (classify_kernel, GENERAL
+ * with DEPTH 2): {base lo, base hi, w, 0} with
  *   w = shift | cut << 8 (> 0xFF)  the hdr_window, base = off - shift, and
  *                                  the window's [0, cut) inside frames_len
  *   w = 0xFF                       bytewise from base = off (unaligned frame,
@@ -214,93 +210,74 @@ __device__ __forceinline__ uint4 load16_bytes(const KParams &k, uint64_t a)
 }
 
 /*
- * @s_src (GENERAL with per-frame offsets, classify_kernel): the tile's
- * packets' hdr_src entries already in LDS, so the four chunk loads wait on
- * one LDS read each instead of dependent global loads of offs[], and the
- * window arithmetic and bounds checks ran once per packet, not per chunk.
- * NULL: offsets read from global memory here.
+ * Issue the four 16-B chunk loads of this lane for @tile (staged by
+ * stage_tile after the loads land).  Every lane issues all four loads on
+ * every path -- a chunk with nothing to read (past the batch, past the
+ * first line, !@live, a bytewise frame) loads 16 B of the table image
+ * instead and is never looked at -- and nothing here consumes a loaded
+ * value.  Loads retire in order and the compiler's wait before staging a
+ * tile counts the loads issued after that tile's on every path through
+ * the loop, so with a fixed count it waits for this tile alone and the
+ * next tile's loads stay in flight (DEPTH 2); one conditional load path
+ * makes it wait for everything.
+ *
+ * @s_src (GENERAL, SRC: classify_kernel at DEPTH 2): the tile's
+ * packets' hdr_src entries already in LDS, so a chunk load is one LDS read,
+ * a compare and a 64-bit add.  !SRC: offsets read here (dependent loads).
+ * @span: where this lane's own packet sits in its staged row (hdr_window):
+ * shift | staged frame bytes << 8, for classify_one; bits 16-19 flag this
+ * lane's chunks of bytewise frames, which patch_tile fills in after staging.
  */
-template <bool GENERAL, int NT>
-__device__ __forceinline__ void load_tile(const KParams &k, uint64_t tile, uint4 r[4],
+template <bool GENERAL, int NT, bool SRC = false>
+__device__ __forceinline__ void load_tile(const KParams &k, uint64_t tile, bool live, uint4 r[4],
                                           uint32_t &span, const uint4 *s_src = nullptr)
 {
-	/* where this lane's own packet of the tile sits in its staged row
-	 * (hdr_window): shift | staged frame bytes << 8, for classify_one */
+	const uint8_t *dummy = k.tables; /* device table image: >= 16 B, always mapped */
 	span = kSpanFull;
-	if (GENERAL && s_src) {
-		const uint32_t me = s_src[threadIdx.x].z;
-		if (me > 0xFF)
-			span = (me & 0xFF) | ((me >> 8) - (me & 0xFF)) << 8;
-		bool bytewise = false;
+	if (!GENERAL) {
+		const uint64_t t0 = tile * NT;
+		const uint32_t lim = (!live || t0 >= k.n) ? 0u : k.n - t0 < NT ? (uint32_t)(k.n - t0) : NT;
+		const uint8_t *base = k.frames + t0 * k.stride;
 #pragma unroll
 		for (int j = 0; j < 4; j++) {
-			const int c = j * NT + (int)threadIdx.x;
-			const uint4 s = s_src[c >> 2];
-			const uint32_t q16 = (uint32_t)(c & 3) * 16;
-			uint4 v = make_uint4(0, 0, 0, 0);
-			/* past the first line (q16 >= cut): left 0, read on demand */
-			if (s.z > 0xFF && q16 < (s.z >> 8))
-				v = gcl::load16_nt(k.frames + ((uint64_t)s.y << 32 | s.x) + q16);
-			bytewise |= s.z == 0xFF;
-			r[j] = v;
-		}
-		if (bytewise) { /* rare: unaligned frames, the end of the buffer */
-			for (int j = 0; j < 4; j++) {
-				const int c = j * NT + (int)threadIdx.x;
-				const uint4 s = s_src[c >> 2];
-				if (s.z == 0xFF)
-					r[j] = load16_bytes(k, ((uint64_t)s.y << 32 | s.x) + (uint32_t)(c & 3) * 16);
-			}
+			const uint32_t c = j * NT + threadIdx.x, p = c >> 2;
+			const uint8_t *a = p < lim ? base + (p * (uint32_t)k.stride + (c & 3) * 16) : dummy;
+			r[j] = gcl::load16_nt(a);
 		}
 		return;
 	}
-	if (GENERAL) {
-		const uint64_t me = tile * NT + threadIdx.x;
-		if (me < k.n) {
-			uint32_t cut;
-			const uint32_t sh = hdr_window(k, frame_off<GENERAL>(k, me), cut);
-			if (sh != 0xFF)
-				span = sh | (cut - sh) << 8;
-		}
-	}
-	if (!GENERAL && (tile + 1) * NT <= k.n) {
-		/* full tile, every granule in range (checked on the host): no
-		 * per-lane predicate, four back-to-back 16-B loads per lane */
-		const uint8_t *base = k.frames + tile * NT * k.stride;
-#pragma unroll
-		for (int j = 0; j < 4; j++) {
-			int c = j * NT + (int)threadIdx.x;
-			r[j] = gcl::load16_nt(base + ((uint32_t)(c >> 2) * (uint32_t)k.stride +
-			                              (uint32_t)(c & 3) * 16));
-		}
-		return;
-	}
+	auto src = [&](uint32_t p) -> uint4 {
+		if (SRC)
+			return s_src[p];
+		const uint64_t idx = tile * NT + p;
+		return hdr_src(k, live && idx < k.n ? frame_off<GENERAL>(k, idx) : kNoOff);
+	};
+	const uint32_t me = src(threadIdx.x).z;
+	if (me > 0xFF)
+		span = (me & 0xFF) | ((me >> 8) - (me & 0xFF)) << 8;
 #pragma unroll
 	for (int j = 0; j < 4; j++) {
-		int c = j * NT + (int)threadIdx.x;
-		uint64_t idx = tile * NT + (uint64_t)(c >> 2);
-		uint4 v = make_uint4(0, 0, 0, 0);
-		if (idx < k.n) {
-			const uint64_t off = frame_off<GENERAL>(k, idx);
-			const uint32_t q16 = (uint32_t)(c & 3) * 16;
-			uint32_t cut = 64;
-			const uint32_t sh = GENERAL ? hdr_window(k, off, cut) : 0u;
-			if (!GENERAL) {
-				v = gcl::load16_nt(k.frames + off + q16);
-			} else if (sh != 0xFF) {
-				const uint64_t a = off - sh + q16; /* 16-B aligned */
-				if (q16 >= cut) {
-					/* past the first line: left 0, read on demand */
-				} else if (a + 16 <= k.frames_len) {
-					v = gcl::load16_nt(k.frames + a);
-				} else {
-					v = load16_bytes(k, a);
-				}
-			} else {
-				v = load16_bytes(k, off + q16);
-			}
-		}
-		r[j] = v;
+		const uint32_t c = j * NT + threadIdx.x, q16 = (c & 3) * 16;
+		const uint4 e = src(c >> 2);
+		/* past the first line (q16 >= cut): not staged, read on demand */
+		const bool use = e.z > 0xFF && q16 < (e.z >> 8);
+		r[j] = gcl::load16_nt(use ? k.frames + (((uint64_t)e.y << 32 | e.x) + q16) : dummy);
+		span |= (uint32_t)(e.z == 0xFF) << (16 + j);
+	}
+}
+
+/* After stage_tile: this lane's chunks of @tile that load_tile flagged
+ * bytewise (@mask, span bits 16-19: unaligned frames, the end of the
+ * buffer), read byte by byte from the frame start into their tile slots.
+ * Rare, and out of load_tile, so that its loads are not on the common path. */
+template <int NT>
+__device__ __forceinline__ void patch_tile(const KParams &k, uint4 *tile, uint64_t t, uint32_t mask)
+{
+	for (int j = 0; j < 4; j++) {
+		const uint32_t c = j * NT + threadIdx.x;
+		if (mask >> j & 1)
+			tile[tile_slot(c >> 2, c & 3)] =
+			        load16_bytes(k, frame_off<true>(k, t * NT + (c >> 2)) + (c & 3) * 16);
 	}
 }
 
@@ -371,6 +348,19 @@ __device__ __forceinline__ uint32_t toeplitz_lut(const uint32_t *toep, uint32_t 
 }
 
 /*
+ * Dense slots (!GENERAL): wait for the tile just requested before parsing
+ * the staged one, so each wave has one tile of loads in flight at a time and
+ * the latency hides behind the other resident waves.  Keeping the loads in
+ * flight across the parse (the GENERAL pipelining) measured udp64 91.4 vs
+ * 101 Gpkt/s: the HBM stream is fastest with fewer requests outstanding per
+ * wave (profiles/r02_dense_depth_ab.jsonl).
+ */
+__device__ __forceinline__ void dense_drain()
+{
+	__builtin_amdgcn_s_waitcnt(0x0F70); /* vmcnt(0), expcnt / lgkmcnt untouched */
+}
+
+/*
  * rx_one_pkt for the packet staged in row `tid` of the tile (rx.c:116-233).
  * Written as straight-line selects: every lane runs the same instruction
  * stream (hash, probe, steer), and only the rare cases -- IHL != 5 ports, a
@@ -379,12 +369,13 @@ __device__ __forceinline__ uint32_t toeplitz_lut(const uint32_t *toep, uint32_t 
 template <int MODE, bool GENERAL, bool SYS = false>
 __device__ __forceinline__ uint64_t classify_one(const KParams &k, const uint4 *tile, int tid,
                                                  uint64_t idx, const Tables &tb, uint32_t *hist,
-                                                 Counters &cnt, uint32_t span = kSpanFull)
+                                                 Counters &cnt, uint32_t span = kSpanFull,
+                                                 const uint32_t *pre = nullptr)
 {
 	/* frame byte b of this lane's header sits at tile byte b + sh, and frame
 	 * bytes [0, avail) are staged (hdr_window) */
 	const uint32_t sh = (GENERAL && !SYS) ? (span & 0xFF) : 0u;
-	const uint32_t avail = (GENERAL && !SYS) ? (span >> 8) : 64u;
+	const uint32_t avail = (GENERAL && !SYS) ? (span >> 8 & 0xFF) : 64u;
 	uint32_t d3, d5, d6, d7, d8, d9, d10;
 	if (GENERAL && !SYS && sh != 0) {
 		d3 = tile_dword(tile, tid, 12 + sh);
@@ -409,7 +400,10 @@ __device__ __forceinline__ uint64_t classify_one(const KParams &k, const uint4 *
 	const uint32_t saddr = gcl::bswap32(gcl::mid32(d6, d7));
 	const uint32_t daddr = gcl::bswap32(gcl::mid32(d7, d8));     /* rx.c:157-159 */
 	uint32_t arp_tip = gcl::bswap32(gcl::mid32(d9, d10));        /* rx.c:165-167 */
-	const uint32_t flags = (GENERAL && k.olflags) ? k.olflags[idx] : k.default_flags;
+	/* @pre: {ol_flags, hash.rss} as loaded a tile ahead by classify_kernel
+	 * (raw: the table image stands in for a missing array) */
+	const uint32_t flags = !(GENERAL && k.olflags) ? k.default_flags
+	                       : pre ? pre[0] & 0xFF : k.olflags[idx];
 	const bool is_ip = et == GCL_ETHTYPE_IP, is_arp = et == GCL_ETHTYPE_ARP;
 	if (GENERAL && !SYS && is_arp && avail < 44) {
 		/* bytes 40-41 are past the staged line (load_tile) */
@@ -425,7 +419,7 @@ __device__ __forceinline__ uint64_t classify_one(const KParams &k, const uint4 *
 		hash = daddr;
 	} else if (MODE == GCL_HASH_NIC) {
 		if (k.rss)
-			hash = k.rss[idx];
+			hash = pre ? pre[1] : k.rss[idx];
 	} else {
 		const bool hashable = is_ip && ihl >= 5 && (frag & 0x3FFF) == 0 &&
 		                      (proto == 6 || proto == 17);
@@ -479,6 +473,8 @@ __device__ __forceinline__ uint64_t classify_one(const KParams &k, const uint4 *
 	cnt.hashmiss += parse && is_ip && !(flags & GCL_F_RSS_HASH); /* rx.c:160-163 */
 	const uint32_t dst = is_ip ? daddr : arp_tip;
 
+	if constexpr (!GENERAL && !SYS)
+		dense_drain();
 	/* ip_to_proc: open addressing keyed by rte_jhash(&ip, 4, 0), rx.c:197 */
 	if (k.ablate & 2) {
 		if (lookup)
@@ -637,13 +633,16 @@ classify_kernel(KParams k)
 	/* stage tables and zero the histogram */
 	for (uint32_t i = tid; i < k.max_rt; i += NT)
 		hist[i] = 0;
-	const uint8_t *tab = k.tables;
-	if (TLDS && !(k.ablate & 32)) {
+	/* @tab is LDS or global by the template argument alone: a pointer that
+	 * may be either compiles to flat loads, which count against the vector
+	 * memory counter too, so every table lookup would wait for the frame
+	 * loads in flight */
+	const uint8_t *tab = TLDS ? lds_tab : k.tables;
+	if (TLDS) {
 		const uint4 *src = (const uint4 *)k.tables;
 		uint4 *dst = (uint4 *)lds_tab;
 		for (uint32_t i = tid; i < k.tables_lds_bytes / 16; i += NT)
 			dst[i] = src[i];
-		tab = lds_tab;
 	}
 	Tables tb;
 	tb.ipt = (const uint2 *)tab;
@@ -661,6 +660,12 @@ classify_kernel(KParams k)
 	uint32_t xs = x0; /* head this block dequeues from (thread 0 only) */
 	uint4 ra[4], rb[4];
 	uint32_t spa = kSpanFull, spb = kSpanFull;
+	/* GENERAL, DEPTH 2: the descriptors' ol_flags and hash.rss, loaded a
+	 * tile ahead -- right after the previous use of the same registers, so
+	 * that no copy of an in-flight value (which waits for it) is needed --
+	 * and not looked at until the tile is parsed (loaded in classify_one,
+	 * they would wait for the next tile's loads issued before them) */
+	uint32_t pra[2] = {0, 0}, prb[2] = {0, 0};
 	uint64_t t = blockIdx.x;
 	/* static walk: tiles t, t + step, ... below t_end.  Default: tiles dealt
 	 * round-robin, so the whole chip sweeps one 16 MiB window of the batch.
@@ -684,60 +689,78 @@ classify_kernel(KParams k)
 		if (tid == 0 && t < k.ntiles)
 			got = atomicAdd(&k.sched[x0 * GCL_SCHED_LINE], 1u);
 	}
-	if (t < t_end)
-		load_tile<GENERAL, NT>(k, t, ra, spa);
-	if (DEPTH == 2 && t + step < t_end)
-		load_tile<GENERAL, NT>(k, t + step, rb, spb);
-	/* Per-frame offsets go through LDS (GENERAL, offs[], static walk): each
+	/* GENERAL, DEPTH 2 (a static walk): frame offsets go through LDS.  Each
 	 * lane loads only its own packet's offset, DEPTH tiles ahead of the tile
-	 * whose frames it is for (offa/offb, coalesced), publishes its hdr_src
-	 * in s_src before the stage barrier, and the chunk loads after the
-	 * barrier read their packets' sources from LDS -- no dependent global
-	 * offs[] loads on the way to the frame loads (k.offs_lds). */
-	const bool goffs = GENERAL && k.offs && !dyn && k.offs_lds;
+	 * whose frames it is for (offa/offb, coalesced), publishes its hdr_src in
+	 * s_src before the stage barrier, and the chunk loads after the barrier
+	 * read their packets' sources from LDS -- no dependent global offs[]
+	 * loads on the way to the frame loads, and the same load count on every
+	 * path (load_tile). */
+	constexpr bool goffs = GENERAL && DEPTH == 2;
 	uint4 *s_src = (uint4 *)(lds_tab + k.tables_lds_bytes);
+	/* offs[] of this lane's packet of tile tt, loaded unconditionally (the
+	 * table image stands in without offs[]); whether there is a packet is
+	 * my_ok(tt), applied by pub() when the offset is published, after the
+	 * load has landed */
+	const uint64_t *offs_src = k.offs ? k.offs : (const uint64_t *)k.tables;
+	auto my_ok = [&](uint64_t tt) { return tt < t_end && tt * NT + tid < k.n; };
 	auto my_off = [&](uint64_t tt) -> uint64_t {
+		return offs_src[k.offs && my_ok(tt) ? tt * NT + tid : 0];
+	};
+	auto pref = [&](uint64_t tt, uint32_t pr[2]) {
+		if constexpr (goffs) {
+			const uint64_t i = my_ok(tt) ? tt * NT + tid : 0;
+			pr[0] = (k.olflags ? k.olflags : k.tables)[k.olflags ? i : 0];
+			if (MODE == GCL_HASH_NIC)
+				pr[1] = (k.rss ? k.rss : (const uint32_t *)k.tables)[k.rss ? i : 0];
+		}
+	};
+	auto pub = [&](uint64_t tt, uint64_t raw) {
 		const uint64_t i = tt * NT + tid;
-		return (tt < t_end && i < k.n) ? k.offs[i] : kNoOff;
+		s_src[tid] = hdr_src(k, !my_ok(tt) ? kNoOff : k.offs ? raw : i * k.stride);
 	};
 	uint64_t offa = 0, offb = 0;
 	if (goffs) {
-		offa = my_off(t + DEPTH * step);
+		/* the loop's waits count the loads issued after each one on
+		 * every path, this prologue included: offa and offb go out
+		 * before rb's loads, so waiting for them leaves rb in flight */
+		pub(t, my_off(t));
+		const uint64_t o1 = my_off(t + step);
+		__syncthreads();
+		load_tile<GENERAL, NT, goffs>(k, t, t < t_end, ra, spa, s_src);
+		pref(t, pra);
+		__syncthreads();
+		pub(t + step, o1);
+		offa = my_off(t + 2 * step);
+		offb = my_off(t + 3 * step);
+		__syncthreads();
+		load_tile<GENERAL, NT, goffs>(k, t + step, t + step < t_end, rb, spb, s_src);
+		pref(t + step, prb);
+		__syncthreads();
+	} else {
+		if (t < t_end)
+			load_tile<GENERAL, NT>(k, t, true, ra, spa);
 		if (DEPTH == 2)
-			offb = my_off(t + 3 * step);
+			load_tile<GENERAL, NT>(k, t + step, t + step < t_end, rb, spb);
 	}
 	if (dyn && tid == 0)
 		s_next[0] = t < k.ntiles ? sched_resolve(k.sched, k.ntiles, (uint32_t)G, x0, xs, got)
 		                         : k.ntiles;
 	int par = 0;
-	/* Deferred verdict stores (k.defer, GCL_TUNE_DEFER=1): on gfx950 stores
-	 * count in vmcnt, and the compiler waits vmcnt(0) for the next tile's
-	 * loads at the top of the loop, so a verdict store issued at the end of a
-	 * tile is waited for right away.  Held in a register and issued after the
-	 * next tile's barrier, before that tile's loads, it completes while the
-	 * tile is parsed.  Measured no faster (kDefaultDefer), kept as a knob. */
-	uint64_t pend_w = 0, pend_i = ~0ull;
-	auto flush = [&]() {
-		if (pend_i != ~0ull)
-			put_verdict(k, pend_i, pend_w);
-		pend_i = ~0ull;
-	};
-	auto verdict = [&](uint64_t idx, uint64_t w) {
-		if (k.defer) {
-			pend_w = w;
-			pend_i = idx;
-		} else {
-			put_verdict(k, idx, w);
-		}
-	};
 
 	while (t < t_end) {
+		/* t opaque to the loop optimiser: without it every per-packet
+		 * address (offs, olflags, rss, fdir, verdicts, ...) becomes its
+		 * own 64-bit induction variable, held in VGPRs and spilled */
+		if constexpr (DEPTH == 2) /* (DEPTH 1 may take t from LDS: a VGPR) */
+			asm volatile("" : "+s"(t));
 		stage_tile<NT>(tile, ra);
 		const uint32_t sp = spa;
+		if (GENERAL && (sp >> 16))
+			patch_tile<NT>(k, tile, t, sp >> 16);
 		if (goffs)
-			s_src[tid] = hdr_src(k, offa);
+			pub(t + DEPTH * step, offa);
 		__syncthreads();
-		flush();
 		uint64_t nxt = t + DEPTH * step;
 		if (dyn) {
 			nxt = s_next[par];
@@ -746,20 +769,18 @@ classify_kernel(KParams k)
 			if (tid == 0 && nxt < k.ntiles)
 				got = atomicAdd(&k.sched[xs * GCL_SCHED_LINE], 1u);
 		}
-		if (nxt < t_end) { /* in flight while parsing */
-			if (goffs)
-				load_tile<GENERAL, NT>(k, nxt, ra, spa, s_src);
-			else
-				load_tile<GENERAL, NT>(k, nxt, ra, spa);
-		}
+		/* in flight while parsing */
+		load_tile<GENERAL, NT, goffs>(k, nxt, nxt < t_end, ra, spa, s_src);
 		if (goffs)
 			offa = my_off(nxt + DEPTH * step);
 		if (k.ablate & 16) { /* timing only: the membench tile_v0 body */
 			const uint4 a = tile[tile_slot(tid, 0)], b = tile[tile_slot(tid, 1)];
 			*(u32x2 *)&k.verdicts[t * NT + tid] = u32x2{b.z ^ a.x, a.w ^ b.y};
-		} else if (t * NT + tid < k.n)
-			verdict(t * NT + tid, classify_one<MODE, GENERAL>(k, tile, tid, t * NT + tid, tb, hist,
-			                                                  cnt, sp));
+		} else if (t * NT + tid < k.n) {
+			put_verdict(k, t * NT + tid, classify_one<MODE, GENERAL>(k, tile, tid, t * NT + tid, tb,
+			                                                         hist, cnt, sp, goffs ? pra : nullptr));
+		}
+		pref(nxt, pra);
 		if (dyn && tid == 0)
 			s_next[par ^ 1] = nxt < k.ntiles ? sched_resolve(k.sched, k.ntiles, (uint32_t)G,
 			                                                 x0, xs, got)
@@ -772,30 +793,29 @@ classify_kernel(KParams k)
 		}
 		t += step;
 		if (DEPTH == 2) {
-			if (t >= t_end)
-				break;
+			/* runs past t_end too (an empty tile: dummy loads, nothing
+			 * classified) rather than leaving the loop here: a path out of
+			 * the middle of the body, without the rb loads below, would
+			 * make the wait before staging ra wait for everything */
 			stage_tile<NT>(tile, rb);
 			const uint32_t sp2 = spb;
+			if (GENERAL && (sp2 >> 16))
+				patch_tile<NT>(k, tile, t, sp2 >> 16);
 			if (goffs)
-				s_src[tid] = hdr_src(k, offb);
+				pub(t + 2 * step, offb);
 			__syncthreads();
-			flush();
-			if (t + 2 * step < t_end) {
-				if (goffs)
-					load_tile<GENERAL, NT>(k, t + 2 * step, rb, spb, s_src);
-				else
-					load_tile<GENERAL, NT>(k, t + 2 * step, rb, spb);
-			}
+			load_tile<GENERAL, NT, goffs>(k, t + 2 * step, t + 2 * step < t_end, rb, spb, s_src);
 			if (goffs)
 				offb = my_off(t + 4 * step);
-			if (t * NT + tid < k.n)
-				verdict(t * NT + tid, classify_one<MODE, GENERAL>(k, tile, tid, t * NT + tid, tb,
-				                                                  hist, cnt, sp2));
+			if (t < t_end && t * NT + tid < k.n)
+				put_verdict(k, t * NT + tid, classify_one<MODE, GENERAL>(k, tile, tid, t * NT + tid,
+				                                                         tb, hist, cnt, sp2,
+				                                                         goffs ? prb : nullptr));
+			pref(t + 2 * step, prb);
 			__syncthreads();
 			t += step;
 		}
 	}
-	flush();
 	uint32_t n_flowtag = cnt.flowtag, n_hashmiss = cnt.hashmiss;
 	uint32_t n_unreg = cnt.unreg, n_unhandled = cnt.unhandled;
 
@@ -1304,8 +1324,6 @@ struct gcl_ctx {
 	int tune_ablate;   /* GCL_TUNE_ABLATE bitmask (timing experiments only) */
 	int tune_sched;    /* GCL_TUNE_SCHED: 0 static persistent grid, 1 dynamic tile queue */
 	int tune_xcd_map;  /* GCL_TUNE_XCD_MAP: 1 contiguous eighth per XCD, 0 round-robin tiles */
-	int tune_defer;    /* GCL_TUNE_DEFER: 1 verdict stores one tile late, 0 at once (default) */
-	int tune_offs_lds; /* GCL_TUNE_OFFS_LDS: 1 per-frame offsets shared through LDS (default) */
 	/* dynamic tile queue: one slot per launch in flight, reused in turn; a
 	 * launch waits for the previous user of its slot (same or other stream) */
 	uint32_t *sched;
@@ -1389,10 +1407,6 @@ extern "C" int gcl_open(int hip_device, const struct gcl_cfg *cfg, struct gcl_ct
 		c->tune_sched = e ? atoi(e) : kDefaultSched;
 		e = getenv("GCL_TUNE_XCD_MAP");
 		c->tune_xcd_map = e ? atoi(e) : kDefaultXcdMap;
-		e = getenv("GCL_TUNE_DEFER");
-		c->tune_defer = e ? atoi(e) : kDefaultDefer;
-		e = getenv("GCL_TUNE_OFFS_LDS");
-		c->tune_offs_lds = e ? atoi(e) : 1;
 	}
 	c->dimg[0] = c->dimg[1] = nullptr;
 	c->sched = nullptr;
@@ -1734,10 +1748,10 @@ struct Geometry {
 	int bpc_cap;  /* blocks per CU */
 };
 
-/* LDS for the tile's frame offsets when they are shared through LDS */
-static uint32_t offs_lds_bytes(bool offs_lds, uint32_t nt)
+/* LDS for the tile's header sources (s_src, classify_kernel): GENERAL */
+static uint32_t offs_lds_bytes(bool general, uint32_t nt)
 {
-	return offs_lds ? nt * 16 : 0; /* s_src: one hdr_src uint4 per packet */
+	return general ? nt * 16 : 0; /* one hdr_src uint4 per packet */
 }
 
 template <int MODE>
@@ -1745,7 +1759,7 @@ static hipError_t launch_mode(const KParams &k, bool tlds, bool general, const G
                               uint32_t tab_lds, uint32_t hist_bytes, int num_cus, hipStream_t s)
 {
 	const uint32_t lds = (uint32_t)geo.threads * 64 + kLdsQueueBytes + hist_bytes + tab_lds +
-	                     offs_lds_bytes(k.offs_lds, (uint32_t)geo.threads);
+	                     offs_lds_bytes(general, (uint32_t)geo.threads);
 #define GCL_LAUNCH(D, T) \
 	return launch_nt<MODE, D, T>(k, tlds, general, lds, num_cus, geo.bpc_cap, s)
 	if (geo.depth == 2) {
@@ -1769,7 +1783,7 @@ static hipError_t launch_mode(const KParams &k, bool tlds, bool general, const G
  * waves than that only add contention (udp64: 446 us at 8 x 256).
  */
 static Geometry choose_geometry(const gcl_ctx *c, uint32_t tab_lds, uint32_t hist_bytes,
-                                bool offs_lds)
+                                bool general)
 {
 	const uint32_t lds_cu = 160 * 1024, lanes_cu = 1024;
 	Geometry g;
@@ -1777,7 +1791,7 @@ static Geometry choose_geometry(const gcl_ctx *c, uint32_t tab_lds, uint32_t his
 	g.threads = 0;
 	for (int nt = 256; nt <= 1024 && !g.threads; nt *= 2) {
 		uint32_t per_block = (uint32_t)nt * 64 + kLdsQueueBytes + hist_bytes + tab_lds +
-		                     offs_lds_bytes(offs_lds, (uint32_t)nt);
+		                     offs_lds_bytes(general, (uint32_t)nt);
 		if ((lanes_cu / nt) * per_block <= lds_cu) {
 			g.threads = nt;
 			g.bpc_cap = (int)(lanes_cu / (uint32_t)nt);
@@ -1786,7 +1800,7 @@ static Geometry choose_geometry(const gcl_ctx *c, uint32_t tab_lds, uint32_t his
 	if (!g.threads) { /* big tables: as many 256-lane blocks as LDS admits */
 		g.threads = 256;
 		g.bpc_cap = (int)(lds_cu / (256u * 64 + kLdsQueueBytes + hist_bytes + tab_lds +
-		                            offs_lds_bytes(offs_lds, 256)));
+		                            offs_lds_bytes(general, 256)));
 		if (g.bpc_cap < 1)
 			g.bpc_cap = 1;
 	} else if (g.threads <= 512 && !c->tune_sched) {
@@ -1951,7 +1965,6 @@ extern "C" int gcl_classify_ex(struct gcl_ctx *c, const struct gcl_batch *b,
 	k.nt_store = c->tune_nt_store;
 	k.ablate = c->tune_ablate;
 	k.xcd_map = c->tune_xcd_map;
-	k.defer = c->tune_defer;
 
 	/* the specialised fast path needs every header granule in range */
 	bool general = b->offs || b->olflags || b->fdir_hi || b->dst_hint ||
@@ -1965,8 +1978,7 @@ extern "C" int gcl_classify_ex(struct gcl_ctx *c, const struct gcl_batch *b,
 	else if (c->tune_tables == 2)
 		tlds = tab_bytes <= kLdsTableBudget;
 	k.tables_lds_bytes = tlds ? tab_bytes : 0;
-	k.offs_lds = general && b->offs && c->tune_offs_lds;
-	Geometry geo = choose_geometry(c, tlds ? tab_bytes : 0, hist_bytes, k.offs_lds);
+	Geometry geo = choose_geometry(c, tlds ? tab_bytes : 0, hist_bytes, general);
 
 	HipErr he;
 	int slot = -1;

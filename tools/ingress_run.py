@@ -3,7 +3,7 @@ rocprofv3: 8 Mi descriptors into the reference's mbuf pool geometry with
 ol_flags and hash.rss, GCL_HASH_NIC (classify_kernel<0, ...>), then the
 JENKINS offsets-only row (classify_kernel<1, ...>).
 
-    python tools/ingress_run.py [reps] [--nic-only | --ws-only]
+    python tools/ingress_run.py [reps] [--nic-only | --ws-only] [--vbytes N]
 
 --nic-only / --ws-only: the random-pool or the working-set NIC row alone, so
 its classify_kernel<0, ...> launches are the only ones in a rocprof pass (both
@@ -24,5 +24,6 @@ if __name__ == "__main__":
     torch.cuda.set_device(dev)
     rows = (("nic",) if "--nic-only" in sys.argv else ("working_set",) if "--ws-only" in sys.argv
             else ("nic", "jenkins", "working_set"))
-    print(json.dumps(bench.ingress_pool_bench(dev, bench.VERDICT_BYTES, reps=reps, zerocopy=False,
+    vb = int(sys.argv[sys.argv.index("--vbytes") + 1]) if "--vbytes" in sys.argv else bench.VERDICT_BYTES
+    print(json.dumps(bench.ingress_pool_bench(dev, vb, reps=reps, zerocopy=False,
                                               rows=rows)))

@@ -1,11 +1,11 @@
-# A/B of the packed-window LDS publish (s_win): new / old / new libraries,
-# each running the ingress rows (random pool + working set) and the
+# A/B of kernel builds (tools/_ab/libgclassify_<variant>.so, a trailing 2
+# reruns the variant; VARIANTS picks them, default new / old / new2), each running the ingress rows (random pool + working set) and the
 # tcp1500 / udp64 kernel-only bench lines in a fresh process.
 set -o pipefail
 O=gpurun_out/r02ac; mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 400 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/gpu_tests.log 2>&1 || exit $?
-for v in new old new2; do
+for v in ${VARIANTS:-new old new2}; do
   src=tools/_ab/libgclassify_${v%2}.so
   cp $src caladan_amd/libgclassify.so || exit 1
   timeout -k 10 240 python3 tools/ingress_run.py 10 > $O/ingress_$v.json 2> $O/ingress_$v.err || exit $?
