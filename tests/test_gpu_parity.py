@@ -806,6 +806,57 @@ def test_gpu_tables_in_hbm_forced(g, orc, monkeypatch):
     assert (c == ce).all() and (st == se).all()
 
 
+LOOP_GEOMETRIES = [
+    {},
+    {"GCL_TUNE_GRID": "3"},
+    {"GCL_TUNE_GRID": "16", "GCL_TUNE_XCD_MAP": "1"},
+    {"GCL_TUNE_GRID": "24", "GCL_TUNE_XCD_MAP": "1", "GCL_TUNE_THREADS": "512"},
+    {"GCL_TUNE_DEPTH": "1", "GCL_TUNE_GRID": "5"},
+    {"GCL_TUNE_SCHED": "1"},
+    {"GCL_TUNE_THREADS": "1024", "GCL_TUNE_GRID": "7"},
+]
+
+
+@pytest.mark.parametrize("geo", range(len(LOOP_GEOMETRIES)))
+@pytest.mark.parametrize("general", [False, True])
+def test_gpu_loop_geometries(g, orc, monkeypatch, geo, general):
+    """The tile loop's edges under every launch shape the knobs allow: few
+    blocks walking many tiles (odd counts per block, so the second half of the
+    DEPTH-2 loop runs past the end as an empty tile), the per-XCD contiguous
+    walk (a block's walk ends inside the batch), DEPTH 1, the dynamic tile
+    queue and 512/1024-lane tiles; dense slots and per-frame offsets with
+    ol_flags / hash.rss (NIC mode), ragged n.  Same verdicts, counts, stats."""
+    env = LOOP_GEOMETRIES[geo]
+    rng = np.random.default_rng(9700 + 10 * geo + general)
+    R = 64
+    rts = random_runtimes(rng, R, 40)
+    mode = 0 if general else 1
+    t = orc.Tables(R, mode, 0, 0x09)
+    apply_runtimes(t, rts)
+    for kk, vv in env.items():
+        monkeypatch.setenv(kk, vv)
+    try:
+        clf = g.Classifier(0, R, mode, 0, 0x09)
+    finally:
+        for kk in env:
+            monkeypatch.delenv(kk)
+    apply_runtimes(clf, rts)
+    if general:
+        n = 20011
+        frames, flen, offs, olf, rss, fdir, hint = fuzz_batch(rng, n, rts, R, misalign="mixed")
+        ve, ce, se = t.classify(frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir_hi=fdir,
+                                frames_len=flen)
+        v, c, st = gpu_run(g, clf, frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir=fdir,
+                           frames_len=flen)
+    else:
+        n = 50001
+        frames, _, _ = orc.generate(0, n, 64, R)
+        ve, ce, se = t.classify(frames, n, 64)
+        v, c, st = gpu_run(g, clf, frames, n, 64)
+    assert_same(v, ve, f"geometry {env} general={general}")
+    assert (c == ce).all() and (st == se).all()
+
+
 def test_gpu_reference_struct_frames(g, orc):
     """Frames written through the reference's own inc/net structs
     (oracle/_ref/libhost_ref.so, see tests/test_ref_host.py) classify on the
