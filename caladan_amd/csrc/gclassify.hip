@@ -348,12 +348,16 @@ __device__ __forceinline__ uint32_t toeplitz_lut(const uint32_t *toep, uint32_t 
 }
 
 /*
- * Dense slots (!GENERAL): wait for the tile just requested before parsing
- * the staged one, so each wave has one tile of loads in flight at a time and
- * the latency hides behind the other resident waves.  Keeping the loads in
- * flight across the parse (the GENERAL pipelining) measured udp64 91.4 vs
- * 101 Gpkt/s: the HBM stream is fastest with fewer requests outstanding per
- * wave (profiles/r02_dense_depth_ab.jsonl).
+ * Dense slots (!GENERAL): wait for everything outstanding -- the tile just
+ * requested and the wave's verdict stores -- before the IP lookup of every
+ * tile and before staging the first tile of each loop iteration, so a wave
+ * has at most about one tile of requests in flight and the latency hides
+ * behind the other resident waves.  Keeping the loads in flight across the
+ * parse (the GENERAL pipelining) measured udp64 91.4 against 101 Gpkt/s, the
+ * lookup drain alone 99.2-99.8 (8-B verdicts 85.9-87.3 against 92.7-93.9),
+ * both drains 100.8-101.0 (92.5-92.8), a drain before both stages 86.7: the
+ * HBM stream runs best with few requests outstanding per wave
+ * (profiles/r02_dense_depth_ab.jsonl).
  */
 __device__ __forceinline__ void dense_drain()
 {
@@ -754,6 +758,8 @@ classify_kernel(KParams k)
 		 * own 64-bit induction variable, held in VGPRs and spilled */
 		if constexpr (DEPTH == 2) /* (DEPTH 1 may take t from LDS: a VGPR) */
 			asm volatile("" : "+s"(t));
+		if constexpr (!GENERAL) /* dense_drain: once per loop iteration too */
+			dense_drain();
 		stage_tile<NT>(tile, ra);
 		const uint32_t sp = spa;
 		if (GENERAL && (sp >> 16))
