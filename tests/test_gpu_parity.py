@@ -818,30 +818,41 @@ LOOP_GEOMETRIES = [
 
 
 @pytest.mark.parametrize("geo", range(len(LOOP_GEOMETRIES)))
-@pytest.mark.parametrize("general", [False, True])
+@pytest.mark.parametrize("general", [False, True, "stride"])
 def test_gpu_loop_geometries(g, orc, monkeypatch, geo, general):
     """The tile loop's edges under every launch shape the knobs allow: few
     blocks walking many tiles (odd counts per block, so the second half of the
     DEPTH-2 loop runs past the end as an empty tile), the per-XCD contiguous
     walk (a block's walk ends inside the batch), DEPTH 1, the dynamic tile
-    queue and 512/1024-lane tiles; dense slots and per-frame offsets with
-    ol_flags / hash.rss (NIC mode), ragged n.  Same verdicts, counts, stats."""
+    queue and 512/1024-lane tiles; dense slots, per-frame offsets with
+    ol_flags / hash.rss (NIC mode), and fixed slots with ol_flags / hash.rss
+    and a buffer ending inside the last frame ("stride": the GENERAL path
+    without offs[]), ragged n.  Same verdicts, counts, stats."""
     env = LOOP_GEOMETRIES[geo]
-    rng = np.random.default_rng(9700 + 10 * geo + general)
+    rng = np.random.default_rng(9700 + 10 * geo + {False: 0, True: 1, "stride": 2}[general])
     R = 64
     rts = random_runtimes(rng, R, 40)
-    mode = 0 if general else 1
-    t = orc.Tables(R, mode, 0, 0x09)
+    mode = 0 if general is True else 1 if general is False else 2
+    key = bytes(rng.integers(0, 256, size=40, dtype=np.uint8))
+    t = orc.Tables(R, mode, 0, 0x09, key)
     apply_runtimes(t, rts)
     for kk, vv in env.items():
         monkeypatch.setenv(kk, vv)
     try:
-        clf = g.Classifier(0, R, mode, 0, 0x09)
+        clf = g.Classifier(0, R, mode, 0, 0x09, key)
     finally:
         for kk in env:
             monkeypatch.delenv(kk)
     apply_runtimes(clf, rts)
-    if general:
+    if general == "stride":
+        n = 30011
+        frames, _, _ = orc.generate(0, n, 64, R)
+        olf = rng.integers(0, 16, size=n, dtype=np.uint8)
+        rss = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
+        flen = (n - 1) * 64 + 37  # the last frame cut inside its header
+        ve, ce, se = t.classify(frames, n, 64, olflags=olf, rss=rss, frames_len=flen)
+        v, c, st = gpu_run(g, clf, frames, n, 64, olflags=olf, rss=rss, frames_len=flen)
+    elif general:
         n = 20011
         frames, flen, offs, olf, rss, fdir, hint = fuzz_batch(rng, n, rts, R, misalign="mixed")
         ve, ce, se = t.classify(frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir_hi=fdir,
