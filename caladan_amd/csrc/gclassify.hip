@@ -94,7 +94,10 @@ struct KParams {
 	uint32_t cflags;
 	uint32_t default_flags;
 	uint32_t nt_store;
-	uint32_t ablate; /* GCL_TUNE_ABLATE: timing-only experiments, wrong results */
+	/* GCL_TUNE_ABLATE, timing-only experiments with wrong results: 1 hash =
+	 * daddr, 2 no IP lookup, 4 no histogram add, 8 no flow_tbl read, 16 no
+	 * classification (the membench tile body), 64 no counter flush */
+	uint32_t ablate;
 	uint2 *trans;    /* struct gcl_trans[n] or NULL */
 	uint32_t off_seed, off_crc;
 	uint32_t *sched; /* tile queue slot (SchedSlot) or NULL = static persistent grid */
@@ -781,7 +784,8 @@ classify_kernel(KParams k)
 			offa = my_off(nxt + DEPTH * step);
 		if (k.ablate & 16) { /* timing only: the membench tile_v0 body */
 			const uint4 a = tile[tile_slot(tid, 0)], b = tile[tile_slot(tid, 1)];
-			*(u32x2 *)&k.verdicts[t * NT + tid] = u32x2{b.z ^ a.x, a.w ^ b.y};
+			if (t * NT + tid < k.n) /* in the verdict format: never past the buffer */
+				put_verdict(k, t * NT + tid, (uint64_t)(a.w ^ b.y) << 32 | (b.z ^ a.x));
 		} else if (t * NT + tid < k.n) {
 			put_verdict(k, t * NT + tid, classify_one<MODE, GENERAL>(k, tile, tid, t * NT + tid, tb,
 			                                                         hist, cnt, sp, goffs ? pra : nullptr));
