@@ -1000,6 +1000,18 @@ def main():
                           "placement": placement(w4)})
             del w4
             torch.cuda.empty_cache()
+        # the same udp64 step in the NIC-fidelity hash mode: bit-exact
+        # do_toeplitz (runtime/net/core.c:120-139) with the 40-B RSS key,
+        # 12 LDS LUT reads per packet instead of lookup3
+        wt = Workload(args.workload, rank, world, device, hash_mode=g.HASH_TOEPLITZ, vbytes=vb)
+        elt, gmst = run_timed(wt, args.steps, 3, 1)
+        toeplitz = {"hash": "toeplitz (GCL_HASH_TOEPLITZ, Caladan's RSS key)",
+                    "verdict": VERDICT_NAMES[vb],
+                    "value": round(wt.n * args.steps / elt / 1e6, 1), "unit": "Mpkt/s",
+                    "ms_per_step": round(elt / args.steps * 1e3, 4), "roofline": roofline(wt, gmst),
+                    "placement": placement(wt)}
+        del wt
+        torch.cuda.empty_cache()
         steps2 = max(20, args.steps // 2)
         sec = {}
         # config 3 leads with the 2-byte queue verdict (1024 runtimes x 4
@@ -1025,7 +1037,8 @@ def main():
         result["secondary"] = {"workload": f"tcp1500: {WORKLOADS['tcp1500'][5]}",
                                **sec[SECONDARY_VERDICT_BYTES],
                                "other_verdicts": [sec[b] for b in sec if b != SECONDARY_VERDICT_BYTES],
-                               "header_split_layout": hsplit, "udp64_other_verdicts": other}
+                               "header_split_layout": hsplit, "udp64_other_verdicts": other,
+                               "udp64_toeplitz": toeplitz}
 
     if world == 1 and not args.no_e2e and args.workload == "udp64" and args.scaling == "weak":
         result["e2e"] = e2e_bench(device, vb)
