@@ -20,8 +20,11 @@
 #include <string.h>
 
 #include <algorithm>
+#include <map>
 #include <mutex>
 #include <new>
+#include <set>
+#include <utility>
 #include <vector>
 
 #include "../../include/gclassify.h"
@@ -36,6 +39,10 @@ constexpr uint32_t kToepBytes = 12 * 256 * 4;
 constexpr uint32_t kCrcBytes = 8 * 256 * 4;
 constexpr uint32_t kLdsTableBudget = 96 * 1024;
 constexpr int kImgUsers = 8;             /* streams tracked per table image */
+/* GCL_TUNE_QUAD default: GENERAL batches on classify_kernel.  The
+ * register-header classify_quad_kernel measured equal or 1-3 % slower on the
+ * ingress rows (profiles/r02_quad_ab.jsonl), so it stays an experiment. */
+constexpr int kDefaultQuad = 0;
 constexpr uint32_t kLdsQueueBytes = 16; /* s_next[2] after the header tile */
 
 /* The first failure of a sequence of HIP calls whose outcome is checked
@@ -96,7 +103,9 @@ struct KParams {
 	uint32_t nt_store;
 	/* GCL_TUNE_ABLATE, timing-only experiments with wrong results: 1 hash =
 	 * daddr, 2 no IP lookup, 4 no histogram add, 8 no flow_tbl read, 16 no
-	 * classification (the membench tile body), 64 no counter flush */
+	 * classification (the membench tile body), 64 no counter flush, 128 no
+	 * rx_one_pkt in classify_quad_kernel (the register loop alone), 256
+	 * dummy loads on one shared address (side_dummy) */
 	uint32_t ablate;
 	uint2 *trans;    /* struct gcl_trans[n] or NULL */
 	uint32_t off_seed, off_crc;
@@ -264,7 +273,8 @@ __device__ __forceinline__ void load_tile(const KParams &k, uint64_t tile, bool 
 		const uint4 e = src(c >> 2);
 		/* past the first line (q16 >= cut): not staged, read on demand */
 		const bool use = e.z > 0xFF && q16 < (e.z >> 8);
-		r[j] = gcl::load16_nt(use ? k.frames + (((uint64_t)e.y << 32 | e.x) + q16) : dummy);
+		const uint64_t a = ((uint64_t)e.y << 32 | e.x) + (use ? q16 : 0);
+		r[j] = gcl::load16_nt(e.z > 0xFF && !(k.ablate & 256) ? k.frames + a : use ? k.frames + a : dummy);
 		span |= (uint32_t)(e.z == 0xFF) << (16 + j);
 	}
 }
@@ -282,6 +292,19 @@ __device__ __forceinline__ void patch_tile(const KParams &k, uint4 *tile, uint64
 			tile[tile_slot(c >> 2, c & 3)] =
 			        load16_bytes(k, frame_off<true>(k, t * NT + (c >> 2)) + (c & 3) * 16);
 	}
+}
+
+/*
+ * What a lane loads in place of an absent per-packet array (the loop keeps
+ * one load count on every path): packet @i's own offs[] entry, a line the
+ * kernel has already fetched, else the table image.  One address shared by
+ * every lane of the chip (the table image) puts all these loads on one L2
+ * channel; GCL_TUNE_ABLATE 256 restores that for the A/B.
+ */
+template <typename T>
+__device__ __forceinline__ const T *side_dummy(const KParams &k, uint64_t i)
+{
+	return (const T *)(k.offs && !(k.ablate & 256) ? (const uint8_t *)(k.offs + i) : k.tables);
 }
 
 /* dword at byte offset b (4-aligned, < 64) of this lane's staged header */
@@ -373,33 +396,26 @@ __device__ __forceinline__ void dense_drain()
  * stream (hash, probe, steer), and only the rare cases -- IHL != 5 ports, a
  * probe chain longer than one slot -- take a divergent branch.
  */
-template <int MODE, bool GENERAL, bool SYS = false>
-__device__ __forceinline__ uint64_t classify_one(const KParams &k, const uint4 *tile, int tid,
-                                                 uint64_t idx, const Tables &tb, uint32_t *hist,
-                                                 Counters &cnt, uint32_t span = kSpanFull,
-                                                 const uint32_t *pre = nullptr)
-{
-	/* frame byte b of this lane's header sits at tile byte b + sh, and frame
-	 * bytes [0, avail) are staged (hdr_window) */
-	const uint32_t sh = (GENERAL && !SYS) ? (span & 0xFF) : 0u;
-	const uint32_t avail = (GENERAL && !SYS) ? (span >> 8 & 0xFF) : 64u;
+/* The header dwords rx_one_pkt's decision reads: frame bytes 12-15 and 20-43
+ * (Ethertype + IHL, frag/proto or ARP opcode, saddr, daddr, L4 ports, ARP
+ * target IP) as little-endian dwords. */
+struct HdrWords {
 	uint32_t d3, d5, d6, d7, d8, d9, d10;
-	if (GENERAL && !SYS && sh != 0) {
-		d3 = tile_dword(tile, tid, 12 + sh);
-		d5 = tile_dword(tile, tid, 20 + sh);
-		d6 = tile_dword(tile, tid, 24 + sh);
-		d7 = tile_dword(tile, tid, 28 + sh);
-		d8 = tile_dword(tile, tid, 32 + sh);
-		d9 = tile_dword(tile, tid, 36 + sh);
-		d10 = tile_dword(tile, tid, 40 + sh);
-	} else {
-		const uint4 w0 = tile[tile_slot(tid, 0)];
-		const uint4 w1 = tile[tile_slot(tid, 1)];
-		const uint4 w2 = tile[tile_slot(tid, 2)];
-		d3 = w0.w, d5 = w1.y, d6 = w1.z, d7 = w1.w;
-		d8 = w2.x, d9 = w2.y, d10 = w2.z;
-	}
+};
 
+/*
+ * rx_one_pkt on the header dwords @h of packet @idx (rx.c:116-233).  Frame
+ * bytes [0, @avail) were staged with shift @sh (hdr_window); @tile (REG
+ * false) holds them in row @tid for the IHL != 5 port reads, which REG
+ * (classify_quad_kernel: headers in registers) reads from the frame instead.
+ */
+template <int MODE, bool GENERAL, bool SYS, bool REG>
+__device__ __forceinline__ uint64_t classify_core(const KParams &k, const HdrWords &h,
+                                                  const uint4 *tile, int tid, uint64_t idx,
+                                                  const Tables &tb, uint32_t *hist, Counters &cnt,
+                                                  uint32_t sh, uint32_t avail, const uint32_t *pre)
+{
+	const uint32_t d3 = h.d3, d5 = h.d5, d6 = h.d6, d7 = h.d7, d8 = h.d8, d9 = h.d9, d10 = h.d10;
 	const uint32_t et = gcl::bswap16(d3 & 0xFFFF);              /* rx.c:154 */
 	const uint32_t ihl = (d3 >> 16) & 0xF;
 	const uint32_t frag = gcl::bswap16(d5 & 0xFFFF);            /* ARP: opcode */
@@ -432,7 +448,7 @@ __device__ __forceinline__ uint64_t classify_one(const KParams &k, const uint4 *
 		                      (proto == 6 || proto == 17);
 		uint32_t sport = gcl::bswap16(d8 >> 16), dport = gcl::bswap16(d9 & 0xFFFF);
 		if (hashable && ihl != 5) {
-			if (20 + 4 * ihl <= avail) { /* ihl <= 11 when avail == 64 */
+			if (!REG && 20 + 4 * ihl <= avail) { /* ihl <= 11 when avail == 64 */
 				const int o = 14 + 4 * (int)ihl + (int)sh;
 				sport = gcl::bswap16(tile_dword(tile, tid, o - 2) >> 16);
 				dport = gcl::bswap16(tile_dword(tile, tid, o + 2) & 0xFFFF);
@@ -551,6 +567,37 @@ __device__ __forceinline__ uint64_t classify_one(const KParams &k, const uint4 *
 	return (uint64_t)vlo << 32 | hash;
 }
 
+/* rx_one_pkt for the packet staged in row `tid` of the LDS tile */
+template <int MODE, bool GENERAL, bool SYS = false>
+__device__ __forceinline__ uint64_t classify_one(const KParams &k, const uint4 *tile, int tid,
+                                                 uint64_t idx, const Tables &tb, uint32_t *hist,
+                                                 Counters &cnt, uint32_t span = kSpanFull,
+                                                 const uint32_t *pre = nullptr)
+{
+	/* frame byte b of this lane's header sits at tile byte b + sh, and frame
+	 * bytes [0, avail) are staged (hdr_window) */
+	const uint32_t sh = (GENERAL && !SYS) ? (span & 0xFF) : 0u;
+	const uint32_t avail = (GENERAL && !SYS) ? (span >> 8 & 0xFF) : 64u;
+	HdrWords h;
+	if (GENERAL && !SYS && sh != 0) {
+		h.d3 = tile_dword(tile, tid, 12 + sh);
+		h.d5 = tile_dword(tile, tid, 20 + sh);
+		h.d6 = tile_dword(tile, tid, 24 + sh);
+		h.d7 = tile_dword(tile, tid, 28 + sh);
+		h.d8 = tile_dword(tile, tid, 32 + sh);
+		h.d9 = tile_dword(tile, tid, 36 + sh);
+		h.d10 = tile_dword(tile, tid, 40 + sh);
+	} else {
+		const uint4 w0 = tile[tile_slot(tid, 0)];
+		const uint4 w1 = tile[tile_slot(tid, 1)];
+		const uint4 w2 = tile[tile_slot(tid, 2)];
+		h.d3 = w0.w, h.d5 = w1.y, h.d6 = w1.z, h.d7 = w1.w;
+		h.d8 = w2.x, h.d9 = w2.y, h.d10 = w2.z;
+	}
+	return classify_core<MODE, GENERAL, SYS, false>(k, h, tile, tid, idx, tb, hist, cnt, sh, avail,
+	                                                 pre);
+}
+
 /* Store verdict word @w (classify_one) of packet @idx in the context's
  * verdict format and store policy. */
 __device__ __forceinline__ void put_verdict(const KParams &k, uint64_t idx, uint64_t w)
@@ -586,6 +633,44 @@ __device__ __forceinline__ void stage_tile(uint4 *tile, const uint4 r[4])
 	for (int j = 0; j < 4; j++) {
 		int c = j * NT + (int)threadIdx.x;
 		tile[tile_slot(c >> 2, c & 3)] = r[j];
+	}
+}
+
+/* End of a classify launch: the block's histogram (all its waves' adds
+ * done) and every wave's counters into the device totals. */
+template <int NT>
+__device__ __forceinline__ void flush_counters(const KParams &k, const uint32_t *hist,
+                                               const Counters &cnt)
+{
+	if (k.ablate & 64)
+		return;
+	const int tid = threadIdx.x;
+	for (uint32_t i = tid; i < k.max_rt; i += NT) {
+		uint32_t v = hist[i];
+		if (v && k.counts)
+			atomicAdd(&k.counts[i], (unsigned long long)v);
+	}
+	if (k.stats) {
+		uint32_t n_flowtag = cnt.flowtag, n_hashmiss = cnt.hashmiss;
+		uint32_t n_unreg = cnt.unreg, n_unhandled = cnt.unhandled;
+		for (int off = 32; off > 0; off >>= 1) {
+			n_flowtag += __shfl_xor(n_flowtag, off);
+			n_hashmiss += __shfl_xor(n_hashmiss, off);
+			n_unreg += __shfl_xor(n_unreg, off);
+			n_unhandled += __shfl_xor(n_unhandled, off);
+		}
+		if ((tid & 63) == 0) {
+			if (n_flowtag)
+				atomicAdd(&k.stats[GCL_RX_FLOW_TAG_MATCH], (unsigned long long)n_flowtag);
+			if (n_hashmiss)
+				atomicAdd(&k.stats[GCL_RX_HASH_MISSING], (unsigned long long)n_hashmiss);
+			if (n_unreg)
+				atomicAdd(&k.stats[GCL_RX_UNREGISTERED_MAC], (unsigned long long)n_unreg);
+			if (n_unhandled)
+				atomicAdd(&k.stats[GCL_RX_UNHANDLED], (unsigned long long)n_unhandled);
+		}
+		if (blockIdx.x == 0 && tid == 0)
+			atomicAdd(&k.stats[GCL_RX_PULLED], (unsigned long long)k.n);
 	}
 }
 
@@ -717,9 +802,9 @@ classify_kernel(KParams k)
 	auto pref = [&](uint64_t tt, uint32_t pr[2]) {
 		if constexpr (goffs) {
 			const uint64_t i = my_ok(tt) ? tt * NT + tid : 0;
-			pr[0] = (k.olflags ? k.olflags : k.tables)[k.olflags ? i : 0];
+			pr[0] = *(k.olflags ? k.olflags + i : side_dummy<uint8_t>(k, i));
 			if (MODE == GCL_HASH_NIC)
-				pr[1] = (k.rss ? k.rss : (const uint32_t *)k.tables)[k.rss ? i : 0];
+				pr[1] = *(k.rss ? k.rss + i : side_dummy<uint32_t>(k, i));
 		}
 	};
 	auto pub = [&](uint64_t tt, uint64_t raw) {
@@ -826,9 +911,6 @@ classify_kernel(KParams k)
 			t += step;
 		}
 	}
-	uint32_t n_flowtag = cnt.flowtag, n_hashmiss = cnt.hashmiss;
-	uint32_t n_unreg = cnt.unreg, n_unhandled = cnt.unhandled;
-
 	/* every dequeue of this block has returned; the last block out rewinds */
 	if (dyn && tid == 0) {
 		uint32_t *done = &k.sched[GCL_SCHED_XCD * GCL_SCHED_LINE];
@@ -840,34 +922,203 @@ classify_kernel(KParams k)
 		}
 	}
 
-	/* flush per-block counters */
-	if (k.ablate & 64)
-		return;
-	for (uint32_t i = tid; i < k.max_rt; i += NT) {
-		uint32_t v = hist[i];
-		if (v && k.counts)
-			atomicAdd(&k.counts[i], (unsigned long long)v);
+	flush_counters<NT>(k, hist, cnt);
+}
+
+/* ------------------------------------------------------------------------
+ * classify_quad_kernel: the GENERAL path (frames at per-packet offsets) with
+ * the headers kept in registers.  Each wave owns 64 packets of every tile
+ * and never waits for the other waves: no LDS header tile, no barriers.
+ *
+ * Lane l of a wave classifies packet l.  The header loads stay coalesced per
+ * frame: load j of lane l reads 16-B chunk (l & 3) of packet (l & ~3) + j,
+ * so each quad of lanes reads one whole 64-B window per load.  A 4 x 4
+ * transpose inside the quad (two DPP exchange steps) then gives every lane
+ * its own packet's four chunks.  The quad learns where its packets' windows
+ * are from each lane's hdr_src by DPP broadcast.  Offsets, ol_flags and
+ * hash.rss are loaded DEPTH (2) tiles / one tile ahead, every load on every
+ * path (dummy addresses for what is absent), so each wait counts exactly
+ * the loads issued after the ones it needs (classify_kernel's rule).
+ */
+template <int CTRL>
+__device__ __forceinline__ uint32_t qdpp(uint32_t v)
+{
+	return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+
+template <int CTRL>
+__device__ __forceinline__ uint4 qdpp4(const uint4 &v)
+{
+	return make_uint4(qdpp<CTRL>(v.x), qdpp<CTRL>(v.y), qdpp<CTRL>(v.z), qdpp<CTRL>(v.w));
+}
+
+__device__ __forceinline__ uint4 sel4(bool c, const uint4 &a, const uint4 &b)
+{
+	return make_uint4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
+}
+
+/* r[j] = chunk (lane & 3) of quad packet j  ->  r[c] = chunk c of packet (lane & 3) */
+__device__ __forceinline__ void quad_transpose(uint4 r[4])
+{
+	const bool odd = threadIdx.x & 1, hi = threadIdx.x & 2;
+	/* quad_perm [1,0,3,2]: exchange with lane ^ 1 */
+	const uint4 x0 = qdpp4<0xB1>(sel4(odd, r[0], r[1]));
+	const uint4 x1 = qdpp4<0xB1>(sel4(odd, r[2], r[3]));
+	r[0] = sel4(odd, x0, r[0]);
+	r[1] = sel4(odd, r[1], x0);
+	r[2] = sel4(odd, x1, r[2]);
+	r[3] = sel4(odd, r[3], x1);
+	/* quad_perm [2,3,0,1]: exchange with lane ^ 2 */
+	const uint4 y0 = qdpp4<0x4E>(sel4(hi, r[0], r[2]));
+	const uint4 y1 = qdpp4<0x4E>(sel4(hi, r[1], r[3]));
+	r[0] = sel4(hi, y0, r[0]);
+	r[2] = sel4(hi, r[2], y0);
+	r[1] = sel4(hi, y1, r[1]);
+	r[3] = sel4(hi, r[3], y1);
+}
+
+/* load j of this lane: chunk (lane & 3) of the quad's packet j, whose
+ * hdr_src lane j of the quad holds in @my */
+template <int J>
+__device__ __forceinline__ uint4 quad_chunk_load(const KParams &k, const uint4 &my)
+{
+	constexpr int B = J * 0x55; /* quad_perm [J,J,J,J]: broadcast */
+	const uint32_t bx = qdpp<B>(my.x), by = qdpp<B>(my.y), bw = qdpp<B>(my.z);
+	const uint32_t q16 = (threadIdx.x & 3) * 16;
+	const bool use = bw > 0xFF && q16 < (bw >> 8);
+	const uint64_t a = ((uint64_t)by << 32 | bx) + (use ? q16 : 0);
+	return gcl::load16_nt(bw > 0xFF && !(k.ablate & 256) ? k.frames + a : use ? k.frames + a : k.tables);
+}
+
+/* the header dwords of frame bytes 12 + 4i (+ 4 @ds dwords of window shift) */
+template <int I>
+__device__ __forceinline__ uint32_t hdr_word(const uint32_t w[16], uint32_t ds)
+{
+	return ds == 0 ? w[I] : ds == 1 ? w[I + 1] : ds == 2 ? w[I + 2] : w[I + 3];
+}
+
+template <int MODE, bool TLDS, int NT>
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4)))
+classify_quad_kernel(KParams k)
+{
+	extern __shared__ uint4 smem[];
+	uint32_t *hist = (uint32_t *)smem;
+	uint8_t *lds_tab = (uint8_t *)(hist + ((k.max_rt + 3) & ~3u));
+	const int tid = threadIdx.x;
+	for (uint32_t i = tid; i < k.max_rt; i += NT)
+		hist[i] = 0;
+	const uint8_t *tab = TLDS ? lds_tab : k.tables;
+	if (TLDS) {
+		const uint4 *src = (const uint4 *)k.tables;
+		uint4 *dst = (uint4 *)lds_tab;
+		for (uint32_t i = tid; i < k.tables_lds_bytes / 16; i += NT)
+			dst[i] = src[i];
 	}
-	if (k.stats) {
-		for (int off = 32; off > 0; off >>= 1) {
-			n_flowtag += __shfl_xor(n_flowtag, off);
-			n_hashmiss += __shfl_xor(n_hashmiss, off);
-			n_unreg += __shfl_xor(n_unreg, off);
-			n_unhandled += __shfl_xor(n_unhandled, off);
+	Tables tb;
+	tb.ipt = (const uint2 *)tab;
+	tb.rtab = (const RtEntry *)(tab + k.off_rt);
+	tb.flow = tab + k.off_flow;
+	tb.toep = (const uint32_t *)(tab + k.off_toep);
+	tb.seed = (const uint32_t *)(tab + k.off_seed);
+	tb.crc = (const uint32_t *)(tab + k.off_crc);
+	__syncthreads();
+
+	Counters cnt = {0, 0, 0, 0};
+	const uint64_t step = gridDim.x;
+	const uint64_t *offs_src = k.offs ? k.offs : (const uint64_t *)k.tables;
+	auto ok = [&](uint64_t tt) { return tt < k.ntiles && tt * NT + tid < k.n; };
+	auto ld_off = [&](uint64_t tt) -> uint64_t {
+		return offs_src[k.offs && ok(tt) ? tt * NT + tid : 0];
+	};
+	auto src_of = [&](uint64_t tt, uint64_t raw) -> uint4 {
+		return hdr_src(k, !ok(tt) ? kNoOff : k.offs ? raw : (tt * NT + tid) * k.stride);
+	};
+	auto pref = [&](uint64_t tt, uint32_t pr[2]) {
+		const uint64_t i = ok(tt) ? tt * NT + tid : 0;
+		pr[0] = *(k.olflags ? k.olflags + i : side_dummy<uint8_t>(k, i));
+		if (MODE == GCL_HASH_NIC)
+			pr[1] = *(k.rss ? k.rss + i : side_dummy<uint32_t>(k, i));
+	};
+	auto issue = [&](const uint4 &my, uint4 r[4]) {
+		r[0] = quad_chunk_load<0>(k, my);
+		r[1] = quad_chunk_load<1>(k, my);
+		r[2] = quad_chunk_load<2>(k, my);
+		r[3] = quad_chunk_load<3>(k, my);
+	};
+	/* the landed chunks of the tile whose own hdr_src is @my -> this lane's
+	 * header dwords, staged shift and staged byte count */
+	auto unpack = [&](uint4 r[4], const uint4 &my, HdrWords &h, uint32_t &sh, uint32_t &avail) {
+		quad_transpose(r);
+		sh = 0;
+		avail = 64;
+		if (my.z > 0xFF) {
+			sh = my.z & 0xFF;
+			avail = (my.z >> 8) - sh;
+		} else if (my.z == 0xFF) { /* bytewise frame (rare): all 64 bytes from its start */
+			const uint64_t off = (uint64_t)my.y << 32 | my.x;
+			for (int c = 0; c < 4; c++)
+				r[c] = load16_bytes(k, off + 16 * c);
 		}
-		if ((tid & 63) == 0) {
-			if (n_flowtag)
-				atomicAdd(&k.stats[GCL_RX_FLOW_TAG_MATCH], (unsigned long long)n_flowtag);
-			if (n_hashmiss)
-				atomicAdd(&k.stats[GCL_RX_HASH_MISSING], (unsigned long long)n_hashmiss);
-			if (n_unreg)
-				atomicAdd(&k.stats[GCL_RX_UNREGISTERED_MAC], (unsigned long long)n_unreg);
-			if (n_unhandled)
-				atomicAdd(&k.stats[GCL_RX_UNHANDLED], (unsigned long long)n_unhandled);
+		const uint32_t w[16] = {r[0].x, r[0].y, r[0].z, r[0].w, r[1].x, r[1].y, r[1].z, r[1].w,
+		                        r[2].x, r[2].y, r[2].z, r[2].w, r[3].x, r[3].y, r[3].z, r[3].w};
+		const uint32_t ds = sh >> 2; /* a window shift is 0, 4, 8 or 12 bytes */
+		h.d3 = hdr_word<3>(w, ds);
+		h.d5 = hdr_word<5>(w, ds);
+		h.d6 = hdr_word<6>(w, ds);
+		h.d7 = hdr_word<7>(w, ds);
+		h.d8 = hdr_word<8>(w, ds);
+		h.d9 = hdr_word<9>(w, ds);
+		h.d10 = hdr_word<10>(w, ds);
+	};
+	auto classify = [&](uint64_t tt, const HdrWords &h, uint32_t sh, uint32_t avail,
+	                    const uint32_t pr[2]) {
+		if (ok(tt)) {
+			const uint64_t i = tt * NT + tid;
+			if (k.ablate & 128) /* timing only: the loop without rx_one_pkt */
+				put_verdict(k, i, h.d3 ^ h.d7 ^ h.d10 ^ pr[0] ^ pr[1] ^ sh ^ avail);
+			else
+				put_verdict(k, i, classify_core<MODE, true, false, true>(k, h, nullptr, tid, i,
+				                                                          tb, hist, cnt, sh,
+				                                                          avail, pr));
 		}
-		if (blockIdx.x == 0 && tid == 0)
-			atomicAdd(&k.stats[GCL_RX_PULLED], (unsigned long long)k.n);
+	};
+
+	uint64_t t = blockIdx.x;
+	uint4 ra[4], rb[4];
+	uint32_t pra[2] = {0, 0}, prb[2] = {0, 0};
+	/* prologue: tiles t and t + step in flight, offsets of the two after */
+	uint64_t oa = ld_off(t), ob = ld_off(t + step);
+	uint4 sa = src_of(t, oa);
+	issue(sa, ra);
+	pref(t, pra);
+	oa = ld_off(t + 2 * step);
+	uint4 sb = src_of(t + step, ob);
+	issue(sb, rb);
+	pref(t + step, prb);
+	ob = ld_off(t + 3 * step);
+	while (t < k.ntiles) {
+		asm volatile("" : "+s"(t));
+		HdrWords h;
+		uint32_t sh, avail;
+		unpack(ra, sa, h, sh, avail);
+		sa = src_of(t + 2 * step, oa);
+		issue(sa, ra);
+		classify(t, h, sh, avail, pra);
+		pref(t + 2 * step, pra);
+		oa = ld_off(t + 4 * step);
+		t += step;
+		/* runs past ntiles too (dummy loads, nothing classified): a path
+		 * out of the middle would change the wait counts (classify_kernel) */
+		unpack(rb, sb, h, sh, avail);
+		sb = src_of(t + 2 * step, ob);
+		issue(sb, rb);
+		classify(t, h, sh, avail, prb);
+		pref(t + 2 * step, prb);
+		ob = ld_off(t + 4 * step);
+		t += step;
 	}
+	__syncthreads(); /* every wave's histogram adds are in */
+	flush_counters<NT>(k, hist, cnt);
 }
 
 /* ------------------------------------------------------------------------
@@ -1334,6 +1585,7 @@ struct gcl_ctx {
 	int tune_ablate;   /* GCL_TUNE_ABLATE bitmask (timing experiments only) */
 	int tune_sched;    /* GCL_TUNE_SCHED: 0 static persistent grid, 1 dynamic tile queue */
 	int tune_xcd_map;  /* GCL_TUNE_XCD_MAP: 1 contiguous eighth per XCD, 0 round-robin tiles */
+	int tune_quad;     /* GCL_TUNE_QUAD: 1 GENERAL batches on classify_quad_kernel, 0 classify_kernel */
 	/* dynamic tile queue: one slot per launch in flight, reused in turn; a
 	 * launch waits for the previous user of its slot (same or other stream) */
 	uint32_t *sched;
@@ -1417,6 +1669,8 @@ extern "C" int gcl_open(int hip_device, const struct gcl_cfg *cfg, struct gcl_ct
 		c->tune_sched = e ? atoi(e) : kDefaultSched;
 		e = getenv("GCL_TUNE_XCD_MAP");
 		c->tune_xcd_map = e ? atoi(e) : kDefaultXcdMap;
+		e = getenv("GCL_TUNE_QUAD");
+		c->tune_quad = e ? atoi(e) : kDefaultQuad;
 	}
 	c->dimg[0] = c->dimg[1] = nullptr;
 	c->sched = nullptr;
@@ -1689,43 +1943,41 @@ static hipEvent_t prof_event(gcl_ctx *c)
 	return hipEventCreate(&e) == hipSuccess ? e : nullptr;
 }
 
-template <int MODE, bool TLDS, bool GENERAL, int DEPTH, int NT>
-static hipError_t launch_t(KParams k, uint32_t lds, int num_cus, int bpc_cap, hipStream_t s)
+typedef void (*ClassifyFn)(KParams);
+
+/* Persistent grid of @fn (@nt-lane blocks, @lds bytes of LDS each): as many
+ * blocks per CU as fit, capped at @bpc_cap, never more than tiles. */
+static hipError_t launch_fn(ClassifyFn fn, int nt, KParams k, uint32_t lds, int num_cus,
+                            int bpc_cap, hipStream_t s)
 {
 	static std::mutex mu;
-	static int occ_cache[64];
-	static uint32_t occ_lds[64];
-	int slot = (lds / 1024) & 63;
+	static std::map<std::pair<const void *, uint32_t>, int> occ_cache;
+	static std::set<const void *> raised;
 	int occ;
-	if (lds > 64 * 1024) {
-		static bool raised = false;
-		if (!raised) {
-			const hipError_t e = hipFuncSetAttribute(
-			        (const void *)classify_kernel<MODE, TLDS, GENERAL, DEPTH, NT>,
-			        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-			if (e != hipSuccess)
-				return e;
-			raised = true;
-		}
-	}
 	{
 		std::lock_guard<std::mutex> g(mu);
-		if (occ_lds[slot] != lds + 1) {
-			int o = 0;
-			if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-			        &o, classify_kernel<MODE, TLDS, GENERAL, DEPTH, NT>, NT, lds) != hipSuccess ||
-			    o < 1)
-				o = 1;
-			occ_cache[slot] = o;
-			occ_lds[slot] = lds + 1;
+		if (lds > 64 * 1024 && !raised.count((const void *)fn)) {
+			const hipError_t e = hipFuncSetAttribute(
+			        (const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+			if (e != hipSuccess)
+				return e;
+			raised.insert((const void *)fn);
 		}
-		occ = occ_cache[slot];
+		const auto key = std::make_pair((const void *)fn, lds);
+		auto it = occ_cache.find(key);
+		if (it == occ_cache.end()) {
+			int o = 0;
+			if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, fn, nt, lds) != hipSuccess || o < 1)
+				o = 1;
+			it = occ_cache.emplace(key, o).first;
+		}
+		occ = it->second;
 	}
 	if (bpc_cap > 0 && bpc_cap < occ)
 		occ = bpc_cap;
 	if (g_tune_bpc > 0 && g_tune_bpc < occ)
 		occ = g_tune_bpc;
-	k.ntiles = (k.n + NT - 1) / NT;
+	k.ntiles = (k.n + nt - 1) / nt;
 	uint64_t grid = (uint64_t)num_cus * (uint64_t)occ;
 	if (g_tune_grid > 0)
 		grid = (uint64_t)g_tune_grid;
@@ -1735,8 +1987,7 @@ static hipError_t launch_t(KParams k, uint32_t lds, int num_cus, int bpc_cap, hi
 		grid = 1;
 	if (grid % GCL_SCHED_XCD) /* the per-XCD walk needs whole rows of 8 blocks */
 		k.xcd_map = 0;
-	hipLaunchKernelGGL((classify_kernel<MODE, TLDS, GENERAL, DEPTH, NT>), dim3((unsigned)grid),
-	                   dim3(NT), lds, s, k);
+	hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(nt), lds, s, k);
 	return hipGetLastError();
 }
 
@@ -1744,11 +1995,20 @@ template <int MODE, int DEPTH, int NT>
 static hipError_t launch_nt(const KParams &k, bool tlds, bool general, uint32_t lds,
                             int num_cus, int bpc_cap, hipStream_t s)
 {
-	if (tlds)
-		return general ? launch_t<MODE, true, true, DEPTH, NT>(k, lds, num_cus, bpc_cap, s)
-		               : launch_t<MODE, true, false, DEPTH, NT>(k, lds, num_cus, bpc_cap, s);
-	return general ? launch_t<MODE, false, true, DEPTH, NT>(k, lds, num_cus, bpc_cap, s)
-	               : launch_t<MODE, false, false, DEPTH, NT>(k, lds, num_cus, bpc_cap, s);
+	const ClassifyFn fn = tlds ? (general ? classify_kernel<MODE, true, true, DEPTH, NT>
+	                                      : classify_kernel<MODE, true, false, DEPTH, NT>)
+	                           : (general ? classify_kernel<MODE, false, true, DEPTH, NT>
+	                                      : classify_kernel<MODE, false, false, DEPTH, NT>);
+	return launch_fn(fn, NT, k, lds, num_cus, bpc_cap, s);
+}
+
+template <int MODE, int NT>
+static hipError_t launch_quad(const KParams &k, bool tlds, uint32_t lds, int num_cus, int bpc_cap,
+                              hipStream_t s)
+{
+	const ClassifyFn fn = tlds ? classify_quad_kernel<MODE, true, NT>
+	                           : classify_quad_kernel<MODE, false, NT>;
+	return launch_fn(fn, NT, k, lds, num_cus, bpc_cap, s);
 }
 
 /* Launch geometry (measured on MI355X, tools/cbench.cpp): */
@@ -1756,6 +2016,7 @@ struct Geometry {
 	int threads;  /* packets per tile = lanes per block */
 	int depth;    /* tiles in flight per block */
 	int bpc_cap;  /* blocks per CU */
+	bool quad;    /* classify_quad_kernel (GENERAL batches): no LDS header tile */
 };
 
 /* LDS for the tile's header sources (s_src, classify_kernel): GENERAL */
@@ -1768,6 +2029,14 @@ template <int MODE>
 static hipError_t launch_mode(const KParams &k, bool tlds, bool general, const Geometry &geo,
                               uint32_t tab_lds, uint32_t hist_bytes, int num_cus, hipStream_t s)
 {
+	if (geo.quad) {
+		const uint32_t lds = hist_bytes + tab_lds;
+		if (geo.threads == 1024)
+			return launch_quad<MODE, 1024>(k, tlds, lds, num_cus, geo.bpc_cap, s);
+		if (geo.threads == 512)
+			return launch_quad<MODE, 512>(k, tlds, lds, num_cus, geo.bpc_cap, s);
+		return launch_quad<MODE, 256>(k, tlds, lds, num_cus, geo.bpc_cap, s);
+	}
 	const uint32_t lds = (uint32_t)geo.threads * 64 + kLdsQueueBytes + hist_bytes + tab_lds +
 	                     offs_lds_bytes(general, (uint32_t)geo.threads);
 #define GCL_LAUNCH(D, T) \
@@ -1799,18 +2068,26 @@ static Geometry choose_geometry(const gcl_ctx *c, uint32_t tab_lds, uint32_t his
 	Geometry g;
 	g.depth = 1;
 	g.threads = 0;
+	/* GENERAL batches take the register-header kernel unless an experiment
+	 * knob asks for the tile kernel's own shapes (GCL_TUNE_QUAD=0, the tile
+	 * queue, depth 1, the membench body) */
+	g.quad = general && c->tune_quad && !c->tune_sched && c->tune_depth != 1 &&
+	         !(c->tune_ablate & 16);
+	auto per_block = [&](uint32_t nt) -> uint32_t {
+		if (g.quad)
+			return hist_bytes + tab_lds;
+		return nt * 64 + kLdsQueueBytes + hist_bytes + tab_lds + offs_lds_bytes(general, nt);
+	};
 	for (int nt = 256; nt <= 1024 && !g.threads; nt *= 2) {
-		uint32_t per_block = (uint32_t)nt * 64 + kLdsQueueBytes + hist_bytes + tab_lds +
-		                     offs_lds_bytes(general, (uint32_t)nt);
-		if ((lanes_cu / nt) * per_block <= lds_cu) {
+		const uint32_t pb = per_block((uint32_t)nt);
+		if ((lanes_cu / nt) * pb <= lds_cu) {
 			g.threads = nt;
 			g.bpc_cap = (int)(lanes_cu / (uint32_t)nt);
 		}
 	}
 	if (!g.threads) { /* big tables: as many 256-lane blocks as LDS admits */
 		g.threads = 256;
-		g.bpc_cap = (int)(lds_cu / (256u * 64 + kLdsQueueBytes + hist_bytes + tab_lds +
-		                            offs_lds_bytes(general, 256)));
+		g.bpc_cap = (int)(lds_cu / per_block(256));
 		if (g.bpc_cap < 1)
 			g.bpc_cap = 1;
 	} else if (g.threads <= 512 && !c->tune_sched) {

@@ -135,6 +135,36 @@ def test_gpu_fuzz_misaligned_offsets(g, orc, misalign, mode):
     assert (tr == tre).all() and (c == ce).all() and (st == se).all()
 
 
+@pytest.mark.parametrize("misalign", ["mbuf", "mixed", "lineend"])
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_gpu_quad_kernel_fuzz(g, orc, monkeypatch, misalign, mode):
+    """The register-header GENERAL kernel (classify_quad_kernel,
+    GCL_TUNE_QUAD=1) on the misaligned-offset fuzz: window shifts of 0-12
+    bytes selected in registers, bytewise frames, headers cut at the first
+    line end, IHL > 5 ports and ARP target IPs read from the frame, loopback
+    hints, FDIR marks and the transport pre-hash, in all three hash modes."""
+    rng = np.random.default_rng(9300 + 10 * mode + {"mbuf": 0, "mixed": 1, "lineend": 2}[misalign])
+    rts = random_runtimes(rng, 1024, 300)
+    n = 7001
+    frames, flen, offs, olf, rss, fdir, hint = fuzz_batch(
+        rng, n, rts, 1024, slot=256 if misalign == "lineend" else 128, misalign=misalign)
+    key = bytes(rng.integers(0, 256, size=40, dtype=np.uint8))
+    t = orc.Tables(1024, mode, g.CFG_TRANS_HASH, 0x09, key)
+    apply_runtimes(t, rts)
+    monkeypatch.setenv("GCL_TUNE_QUAD", "1")
+    try:
+        clf = g.Classifier(0, 1024, mode, g.CFG_TRANS_HASH, 0x09, key)
+    finally:
+        monkeypatch.delenv("GCL_TUNE_QUAD")
+    apply_runtimes(clf, rts)
+    ve, ce, se, tre = t.classify(frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir_hi=fdir,
+                                 frames_len=flen, dst_hint=hint, trans=True)
+    v, c, st, tr = gpu_run(g, clf, frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir=fdir,
+                           frames_len=flen, hint=hint, trans=True)
+    assert_same(v, ve, f"quad misalign={misalign} mode={mode}")
+    assert (tr == tre).all() and (c == ce).all() and (st == se).all()
+
+
 @pytest.mark.parametrize("mode", [0, 1, 2])
 @pytest.mark.parametrize("flags", [1, 2])
 @pytest.mark.parametrize("max_rt", [16, 1024])
@@ -814,6 +844,10 @@ LOOP_GEOMETRIES = [
     {"GCL_TUNE_DEPTH": "1", "GCL_TUNE_GRID": "5"},
     {"GCL_TUNE_SCHED": "1"},
     {"GCL_TUNE_THREADS": "1024", "GCL_TUNE_GRID": "7"},
+    {"GCL_TUNE_QUAD": "1"},
+    {"GCL_TUNE_QUAD": "1", "GCL_TUNE_GRID": "3"},
+    {"GCL_TUNE_QUAD": "1", "GCL_TUNE_THREADS": "512", "GCL_TUNE_GRID": "5"},
+    {"GCL_TUNE_QUAD": "1", "GCL_TUNE_THREADS": "1024", "GCL_TUNE_GRID": "7"},
 ]
 
 
@@ -824,7 +858,8 @@ def test_gpu_loop_geometries(g, orc, monkeypatch, geo, general):
     blocks walking many tiles (odd counts per block, so the second half of the
     DEPTH-2 loop runs past the end as an empty tile), the per-XCD contiguous
     walk (a block's walk ends inside the batch), DEPTH 1, the dynamic tile
-    queue and 512/1024-lane tiles; dense slots, per-frame offsets with
+    queue, 512/1024-lane tiles and the register-header GENERAL kernel
+    (GCL_TUNE_QUAD=1, dense slots keep the tile kernel); dense slots, per-frame offsets with
     ol_flags / hash.rss (NIC mode), and fixed slots with ol_flags / hash.rss
     and a buffer ending inside the last frame ("stride": the GENERAL path
     without offs[]), ragged n.  Same verdicts, counts, stats."""
