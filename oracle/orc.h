@@ -21,8 +21,9 @@
  *
  * Pinning: orc_jhash is checked against base/jenkins_hash.c compiled from the
  * reference tree (oracle/_ref, see oracle/Makefile) and the published lookup3
- * KATs; orc_do_toeplitz against the Microsoft RSS verification vectors, which
- * the survey ran through the reference's do_toeplitz; orc_rx_one_pkt against
+ * KATs; orc_do_toeplitz against the reference's own do_toeplitz, compiled in
+ * place (oracle/ref_toeplitz.c, tests/golden/toeplitz_ref.json), and the
+ * Microsoft RSS verification vectors; orc_rx_one_pkt against
  * hand-derived scenario fixtures (tests/golden/rx_scenarios.json) that cite
  * rx.c line by line.  iokernel/rx.c itself needs DPDK headers that are not in
  * this image, so it is not compiled here, and the reference ships no tests or

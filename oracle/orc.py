@@ -15,6 +15,7 @@ LIB_NATIVE = os.path.join(HERE, "build", "liborc_native.so")
 REF_JHASH = os.path.join(HERE, "_ref", "libjhash_ref.so")
 REF_CRC = os.path.join(HERE, "_ref", "libcrc_ref.so")
 REF_HOST = os.path.join(HERE, "_ref", "libhost_ref.so")
+REF_TOEPLITZ = os.path.join(HERE, "_ref", "libtoeplitz_ref.so")
 TRANS_DTYPE = np.dtype([("h5", "<u4"), ("h3", "<u4")])
 
 NR_STATS = 8
@@ -112,6 +113,20 @@ def ref_crc():
     l.ref_crc32c_two.restype = ctypes.c_uint32
     l.ref_crc32c_two.argtypes = [ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64]
     return l
+
+
+def ref_toeplitz():
+    """The reference's own do_toeplitz (runtime/net/core.c:120-139, compiled in
+    place into oracle/_ref/libtoeplitz_ref.so by oracle/ref_toeplitz.c), as
+    f(key, saddr, daddr, sport, dport), or None."""
+    if not os.path.exists(REF_TOEPLITZ):
+        return None
+    l = ctypes.CDLL(REF_TOEPLITZ)
+    f = l.ref_do_toeplitz
+    f.restype = ctypes.c_uint32
+    f.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                  ctypes.c_uint16, ctypes.c_uint16]
+    return lambda key, s, d, sp, dp: f(bytes(key), len(key), s, d, sp, dp)
 
 
 def ref_host():

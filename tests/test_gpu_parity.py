@@ -937,3 +937,26 @@ def test_gpu_rejects_oversized_batch(g):
     b = g.GclBatch(frames=f.data_ptr(), frames_len=4096, stride=64, n=(1 << 40) + 1)
     o = g.GclOut(verdicts=v.data_ptr())
     assert g.lib.gcl_classify_ex(clf._ctx, ctypes.byref(b), ctypes.byref(o), None) == -22
+
+
+def test_gpu_toeplitz_reference_vectors(g):
+    """TOEPLITZ mode on the GPU reproduces the reference's own do_toeplitz
+    outputs (tests/golden/toeplitz_ref.json, generated by the reference
+    compiled in place): one Eth/IPv4/TCP frame per vector, every key of the
+    fixture in its own context, the hash read from the 8-B verdict."""
+    import struct
+    from tests.rxcases import load_json
+    d = load_json("toeplitz_ref.json")
+    for ki, khex in enumerate(d["keys"]):
+        vecs = [v for v in d["vectors"] if v["key"] == ki]
+        n = len(vecs)
+        frames = np.zeros(n * 64, dtype=np.uint8)
+        for i, v in enumerate(vecs):
+            ip = struct.pack("!BBHHHBBHII", 0x45, 0, 40, 1, 0, 64, 6, 0, v["saddr"], v["daddr"])
+            fr = bytes(12) + b"\x08\x00" + ip + struct.pack("!HH", v["sport"], v["dport"])
+            frames[64 * i:64 * i + len(fr)] = np.frombuffer(fr, dtype=np.uint8)
+        clf = g.Classifier(0, 16, g.HASH_TOEPLITZ, 0, 0x09, bytes.fromhex(khex))
+        ver, _, _ = gpu_run(g, clf, frames, n, 64)
+        want = np.array([v["hash"] for v in vecs], dtype=np.uint32)
+        bad = np.nonzero(ver["hash"] != want)[0]
+        assert len(bad) == 0, f"key {ki}: {len(bad)} hashes differ, first {vecs[bad[0]]} gpu={ver['hash'][bad[0]]:#x}"

@@ -71,3 +71,34 @@ def test_toeplitz_do_vs_bytes_random(orc):
         h = orc.do_toeplitz(key, s, d, sp, dp)
         assert h == orc.toeplitz_bytes(key, tup)
         assert h == g.toeplitz(key, tup)
+
+
+def test_toeplitz_golden_from_reference(orc):
+    """tests/golden/toeplitz_ref.json was produced by the reference's own
+    do_toeplitz (runtime/net/core.c:120-139, compiled in place by
+    oracle/ref_toeplitz.c; tests/golden/make_toeplitz_ref.py): Caladan's RSS
+    key and random keys over random and edge 4-tuples."""
+    from caladan_amd import gclassify as g
+    d = load_json("toeplitz_ref.json")
+    keys = [bytes.fromhex(k) for k in d["keys"]]
+    assert keys[0] == g.CALADAN_RSS_KEY and len(d["vectors"]) > 900
+    for v in d["vectors"]:
+        key = keys[v["key"]]
+        s, dd, sp, dp = v["saddr"], v["daddr"], v["sport"], v["dport"]
+        assert orc.do_toeplitz(key, s, dd, sp, dp) == v["hash"], v
+        assert g.toeplitz(key, struct.pack("!IIHH", s, dd, sp, dp)) == v["hash"], v
+
+
+def test_toeplitz_live_reference(orc):
+    """When oracle/_ref is built (reference tree mounted), compare the oracle
+    with the reference's do_toeplitz live on fresh random keys and tuples."""
+    import random
+    ref = orc.ref_toeplitz()
+    if ref is None:
+        pytest.skip("oracle/_ref/libtoeplitz_ref.so not built")
+    rnd = random.Random(os.getpid())
+    for _ in range(20):
+        key = bytes(rnd.getrandbits(8) for _ in range(40))
+        for _ in range(200):
+            t = (rnd.getrandbits(32), rnd.getrandbits(32), rnd.getrandbits(16), rnd.getrandbits(16))
+            assert orc.do_toeplitz(key, *t) == ref(key, *t), (key.hex(), t)
