@@ -16,6 +16,7 @@ REF_JHASH = os.path.join(HERE, "_ref", "libjhash_ref.so")
 REF_CRC = os.path.join(HERE, "_ref", "libcrc_ref.so")
 REF_HOST = os.path.join(HERE, "_ref", "libhost_ref.so")
 REF_TOEPLITZ = os.path.join(HERE, "_ref", "libtoeplitz_ref.so")
+REF_TRANS = os.path.join(HERE, "_ref", "libtrans_ref.so")
 TRANS_DTYPE = np.dtype([("h5", "<u4"), ("h3", "<u4")])
 
 NR_STATS = 8
@@ -127,6 +128,26 @@ def ref_toeplitz():
     f.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                   ctypes.c_uint16, ctypes.c_uint16]
     return lambda key, s, d, sp, dp: f(bytes(key), len(key), s, d, sp, dp)
+
+
+def ref_trans():
+    """The reference's own trans_hash_5tuple/3tuple (runtime/net/transport.c:29-42,
+    compiled in place into oracle/_ref/libtrans_ref.so by oracle/ref_trans.c),
+    as f(seed, proto, lip, lport, rip, rport) -> (h5, h3), or None."""
+    if not os.path.exists(REF_TRANS):
+        return None
+    l = ctypes.CDLL(REF_TRANS)
+    f = l.ref_trans_hash
+    f.restype = None
+    u32 = ctypes.c_uint32
+    f.argtypes = [u32, ctypes.c_uint8, u32, ctypes.c_uint16, u32, ctypes.c_uint16,
+                  ctypes.POINTER(u32 * 2)]
+
+    def call(seed, proto, lip, lport, rip, rport):
+        out = (u32 * 2)()
+        f(seed, proto, lip, lport, rip, rport, ctypes.byref(out))
+        return out[0], out[1]
+    return call
 
 
 def ref_host():

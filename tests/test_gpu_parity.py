@@ -960,3 +960,29 @@ def test_gpu_toeplitz_reference_vectors(g):
         want = np.array([v["hash"] for v in vecs], dtype=np.uint32)
         bad = np.nonzero(ver["hash"] != want)[0]
         assert len(bad) == 0, f"key {ki}: {len(bad)} hashes differ, first {vecs[bad[0]]} gpu={ver['hash'][bad[0]]:#x}"
+
+
+def test_gpu_trans_hash_reference_vectors(g):
+    """The transport demux pre-hash on the GPU (GCL_CFG_TRANS_HASH) equals
+    the reference's own trans_hash_5tuple/3tuple (tests/golden/trans_ref.json,
+    generated by runtime/net/transport.c compiled in place) for IPv4 TCP/UDP
+    frames delivered to 16 runtimes, each with its own trans_seed."""
+    import struct
+    from tests.rxcases import load_json
+    d = load_json("trans_ref.json")
+    vecs = d["frames"]
+    n = len(vecs)
+    frames = np.zeros(n * 64, dtype=np.uint8)
+    for i, v in enumerate(vecs):
+        ip = struct.pack("!BBHHHBBHII", 0x45, 0, 40, 1, 0x4000, 64, v["proto"], 0, v["saddr"],
+                         d["runtime_ips"][v["runtime"]])
+        fr = bytes(12) + b"\x08\x00" + ip + struct.pack("!HH", v["sport"], v["dport"])
+        frames[64 * i:64 * i + len(fr)] = np.frombuffer(fr, dtype=np.uint8)
+    clf = g.Classifier(0, 16, g.HASH_NIC, g.CFG_TRANS_HASH, 0x09)
+    for r, (ip, seed) in enumerate(zip(d["runtime_ips"], d["trans_seeds"])):
+        clf.runtime_set(r, ip, 4, 4, [0, 1, 2, 3])
+        clf.set_trans_seed(r, seed)
+    ver, _, _, tr = gpu_run(g, clf, frames, n, 64, trans=True)
+    assert (ver["uniqid"] == np.array([v["runtime"] for v in vecs])).all()
+    assert (tr["h5"] == np.array([v["h5"] for v in vecs], dtype=np.uint32)).all()
+    assert (tr["h3"] == np.array([v["h3"] for v in vecs], dtype=np.uint32)).all()

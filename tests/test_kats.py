@@ -102,3 +102,35 @@ def test_toeplitz_live_reference(orc):
         for _ in range(200):
             t = (rnd.getrandbits(32), rnd.getrandbits(32), rnd.getrandbits(16), rnd.getrandbits(16))
             assert orc.do_toeplitz(key, *t) == ref(key, *t), (key.hex(), t)
+
+
+def test_trans_hash_golden_from_reference():
+    """tests/golden/trans_ref.json was produced by the reference's own
+    trans_hash_5tuple/3tuple (runtime/net/transport.c:29-42, compiled in
+    place by oracle/ref_trans.c): the product's host gcl_trans_hash equals
+    it on received-frame tuples and on arbitrary inputs."""
+    from caladan_amd import gclassify as g
+    d = load_json("trans_ref.json")
+    for v in d["frames"]:
+        r = v["runtime"]
+        got = g.trans_hash(d["trans_seeds"][r], v["proto"], d["runtime_ips"][r], v["dport"],
+                           v["saddr"], v["sport"])
+        assert tuple(got) == (v["h5"], v["h3"]), v
+    for v in d["random"]:
+        got = g.trans_hash(v["seed"], v["proto"], v["lip"], v["lport"], v["rip"], v["rport"])
+        assert tuple(got) == (v["h5"], v["h3"]), v
+
+
+def test_trans_hash_live_reference(orc):
+    """When oracle/_ref is built, the product's host transport hashes equal
+    the reference's trans_hash_5tuple/3tuple live on fresh random inputs."""
+    import random
+    from caladan_amd import gclassify as g
+    ref = orc.ref_trans()
+    if ref is None:
+        pytest.skip("oracle/_ref/libtrans_ref.so not built")
+    rnd = random.Random(os.getpid())
+    for _ in range(5000):
+        a = (rnd.getrandbits(32), rnd.getrandbits(8), rnd.getrandbits(32), rnd.getrandbits(16),
+             rnd.getrandbits(32), rnd.getrandbits(16))
+        assert ref(*a) == tuple(g.trans_hash(*a)), a
