@@ -22,7 +22,7 @@
  * Pinning: orc_jhash is checked against base/jenkins_hash.c compiled from the
  * reference tree (oracle/_ref, see oracle/Makefile) and the published lookup3
  * KATs; orc_do_toeplitz against the reference's own do_toeplitz, compiled in
- * place (oracle/ref_toeplitz.c, tests/golden/toeplitz_ref.json), and the
+ * place (oracle/ref_core.c, tests/golden/toeplitz_ref.json), and the
  * Microsoft RSS verification vectors; orc_rx_one_pkt against
  * hand-derived scenario fixtures (tests/golden/rx_scenarios.json) that cite
  * rx.c line by line.  iokernel/rx.c itself needs DPDK headers that are not in

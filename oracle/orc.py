@@ -15,7 +15,7 @@ LIB_NATIVE = os.path.join(HERE, "build", "liborc_native.so")
 REF_JHASH = os.path.join(HERE, "_ref", "libjhash_ref.so")
 REF_CRC = os.path.join(HERE, "_ref", "libcrc_ref.so")
 REF_HOST = os.path.join(HERE, "_ref", "libhost_ref.so")
-REF_TOEPLITZ = os.path.join(HERE, "_ref", "libtoeplitz_ref.so")
+REF_CORE = os.path.join(HERE, "_ref", "libcore_ref.so")
 REF_TRANS = os.path.join(HERE, "_ref", "libtrans_ref.so")
 TRANS_DTYPE = np.dtype([("h5", "<u4"), ("h3", "<u4")])
 
@@ -118,16 +118,27 @@ def ref_crc():
 
 def ref_toeplitz():
     """The reference's own do_toeplitz (runtime/net/core.c:120-139, compiled in
-    place into oracle/_ref/libtoeplitz_ref.so by oracle/ref_toeplitz.c), as
+    place into oracle/_ref/libcore_ref.so by oracle/ref_core.c), as
     f(key, saddr, daddr, sport, dport), or None."""
-    if not os.path.exists(REF_TOEPLITZ):
+    if not os.path.exists(REF_CORE):
         return None
-    l = ctypes.CDLL(REF_TOEPLITZ)
+    l = ctypes.CDLL(REF_CORE)
     f = l.ref_do_toeplitz
     f.restype = ctypes.c_uint32
     f.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                   ctypes.c_uint16, ctypes.c_uint16]
     return lambda key, s, d, sp, dp: f(bytes(key), len(key), s, d, sp, dp)
+
+
+def ref_ip_hdr_supported():
+    """The reference's own ip_hdr_supported (runtime/net/core.c:203-209,
+    oracle/_ref/libcore_ref.so) as f(20-byte wire header) -> bool, or None."""
+    if not os.path.exists(REF_CORE):
+        return None
+    f = ctypes.CDLL(REF_CORE).ref_ip_hdr_supported
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_char_p]
+    return lambda hdr: bool(f(bytes(hdr)))
 
 
 def ref_trans():

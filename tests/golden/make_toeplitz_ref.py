@@ -1,6 +1,6 @@
 """Generate tests/golden/toeplitz_ref.json from the REFERENCE's own
 do_toeplitz (runtime/net/core.c:120-139), compiled in place into
-oracle/_ref/libtoeplitz_ref.so by oracle/Makefile (oracle/ref_toeplitz.c).
+oracle/_ref/libcore_ref.so by oracle/Makefile (oracle/ref_core.c).
 
 Run where /root/reference exists (after `make -C oracle ref`):
     python tests/golden/make_toeplitz_ref.py
@@ -24,7 +24,7 @@ from oracle import orc  # noqa: E402
 def main():
     ref = orc.ref_toeplitz()
     if ref is None:
-        raise SystemExit("oracle/_ref/libtoeplitz_ref.so not built (make -C oracle ref)")
+        raise SystemExit("oracle/_ref/libcore_ref.so not built (make -C oracle ref)")
     rnd = random.Random(0x7E0B)
     keys = [CALADAN_RSS_KEY] + [bytes(rnd.getrandbits(8) for _ in range(40)) for _ in range(7)]
     vecs = []
@@ -38,7 +38,7 @@ def main():
         for s, d, sp, dp in tuples:
             vecs.append({"key": ki, "saddr": s, "daddr": d, "sport": sp, "dport": dp,
                          "hash": ref(key, s, d, sp, dp)})
-    out = {"source": "reference do_toeplitz (runtime/net/core.c:120-139) via oracle/_ref/libtoeplitz_ref.so",
+    out = {"source": "reference do_toeplitz (runtime/net/core.c:120-139) via oracle/_ref/libcore_ref.so",
            "keys": [k.hex() for k in keys], "vectors": vecs}
     with open(os.path.join(HERE, "toeplitz_ref.json"), "w") as f:
         json.dump(out, f, indent=0)

@@ -986,3 +986,21 @@ def test_gpu_trans_hash_reference_vectors(g):
     assert (ver["uniqid"] == np.array([v["runtime"] for v in vecs])).all()
     assert (tr["h5"] == np.array([v["h5"] for v in vecs], dtype=np.uint32)).all()
     assert (tr["h3"] == np.array([v["h3"] for v in vecs], dtype=np.uint32)).all()
+
+
+def test_gpu_ip_hdr_supported_reference(g):
+    """The GPU sets the transport pre-hash (GCL_ACT_F_TRANS) exactly on the
+    frames the reference's own ip_hdr_supported accepts
+    (tests/golden/iphdr_ref.json: 256 version/IHL bytes x 10 fragment
+    fields, generated by runtime/net/core.c compiled in place)."""
+    from tests.rxcases import load_json
+    from tests.test_kats import _iphdr_frames
+    d = load_json("iphdr_ref.json")
+    ip = 0x0A000001
+    clf = g.Classifier(0, 16, g.HASH_NIC, g.CFG_TRANS_HASH, 0x09)
+    clf.runtime_set(0, ip, 4, 4, [0, 1, 2, 3])
+    n = len(d["headers"])
+    v, _, _, _ = gpu_run(g, clf, _iphdr_frames(d, ip), n, 64, trans=True)
+    got = (v["action"] & g.ACT_F_TRANS) != 0
+    want = np.array([h["supported"] for h in d["headers"]])
+    assert (got == want).all(), np.nonzero(got != want)[0][:5]

@@ -76,7 +76,7 @@ def test_toeplitz_do_vs_bytes_random(orc):
 def test_toeplitz_golden_from_reference(orc):
     """tests/golden/toeplitz_ref.json was produced by the reference's own
     do_toeplitz (runtime/net/core.c:120-139, compiled in place by
-    oracle/ref_toeplitz.c; tests/golden/make_toeplitz_ref.py): Caladan's RSS
+    oracle/ref_core.c; tests/golden/make_toeplitz_ref.py): Caladan's RSS
     key and random keys over random and edge 4-tuples."""
     from caladan_amd import gclassify as g
     d = load_json("toeplitz_ref.json")
@@ -95,7 +95,7 @@ def test_toeplitz_live_reference(orc):
     import random
     ref = orc.ref_toeplitz()
     if ref is None:
-        pytest.skip("oracle/_ref/libtoeplitz_ref.so not built")
+        pytest.skip("oracle/_ref/libcore_ref.so not built")
     rnd = random.Random(os.getpid())
     for _ in range(20):
         key = bytes(rnd.getrandbits(8) for _ in range(40))
@@ -134,3 +134,50 @@ def test_trans_hash_live_reference(orc):
         a = (rnd.getrandbits(32), rnd.getrandbits(8), rnd.getrandbits(32), rnd.getrandbits(16),
              rnd.getrandbits(32), rnd.getrandbits(16))
         assert ref(*a) == tuple(g.trans_hash(*a)), a
+
+
+def _iphdr_frames(d, ip):
+    import numpy as np
+    hdrs = d["headers"]
+    frames = np.zeros(len(hdrs) * 64, dtype=np.uint8)
+    for i, v in enumerate(hdrs):
+        h = bytearray.fromhex(v["hdr"])
+        h[16:20] = struct.pack("!I", ip)  # to the registered runtime; not part of the predicate
+        fr = bytes(12) + b"\x08\x00" + bytes(h) + struct.pack("!HH", 1000 + i, 80)
+        frames[64 * i:64 * i + len(fr)] = np.frombuffer(fr, dtype=np.uint8)
+    return frames
+
+
+def test_ip_hdr_supported_golden_from_reference(orc):
+    """Which delivered frames get the transport demux pre-hash follows the
+    reference's own ip_hdr_supported (runtime/net/core.c:203-209, quirk
+    included: IP_MF tested on the network-order field), per
+    tests/golden/iphdr_ref.json (generated by core.c compiled in place): all
+    256 version/IHL bytes x 10 fragment fields through the oracle."""
+    import numpy as np
+    from caladan_amd import gclassify as g
+    d = load_json("iphdr_ref.json")
+    ip = 0x0A000001
+    t = orc.Tables(16, g.HASH_NIC, g.CFG_TRANS_HASH, 0x09)
+    t.runtime_set(0, ip, 4, 4, [0, 1, 2, 3])
+    n = len(d["headers"])
+    v, _, _, _ = t.classify(_iphdr_frames(d, ip), n, 64, trans=True)
+    got = (v["action"] & g.ACT_F_TRANS) != 0
+    want = np.array([h["supported"] for h in d["headers"]])
+    assert want.sum() == 7 and (got == want).all(), np.nonzero(got != want)[0][:5]
+
+
+def test_ip_hdr_supported_live_reference(orc):
+    """The same against the reference live, on random headers."""
+    import random
+    ref = orc.ref_ip_hdr_supported()
+    if ref is None:
+        pytest.skip("oracle/_ref/libcore_ref.so not built")
+    d = load_json("iphdr_ref.json")
+    for h in d["headers"]:
+        assert ref(bytes.fromhex(h["hdr"])) == h["supported"]
+    rnd = random.Random(os.getpid())
+    for _ in range(2000):
+        hdr = bytes(rnd.getrandbits(8) for _ in range(20))
+        vihl, frag = hdr[0], hdr[6] | hdr[7] << 8
+        assert ref(hdr) == (vihl == 0x45 and not (frag & 0x2000)), hdr.hex()
