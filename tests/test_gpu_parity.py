@@ -135,15 +135,18 @@ def test_gpu_fuzz_misaligned_offsets(g, orc, misalign, mode):
     assert (tr == tre).all() and (c == ce).all() and (st == se).all()
 
 
+@pytest.mark.parametrize("tables", ["lds", "global"])
 @pytest.mark.parametrize("misalign", ["mbuf", "mixed", "lineend"])
 @pytest.mark.parametrize("mode", [0, 1, 2])
-def test_gpu_quad_kernel_fuzz(g, orc, monkeypatch, misalign, mode):
+def test_gpu_quad_kernel_fuzz(g, orc, monkeypatch, misalign, mode, tables):
     """The register-header GENERAL kernel (classify_quad_kernel,
     GCL_TUNE_QUAD=1) on the misaligned-offset fuzz: window shifts of 0-12
     bytes selected in registers, bytewise frames, headers cut at the first
     line end, IHL > 5 ports and ARP target IPs read from the frame, loopback
-    hints, FDIR marks and the transport pre-hash, in all three hash modes."""
-    rng = np.random.default_rng(9300 + 10 * mode + {"mbuf": 0, "mixed": 1, "lineend": 2}[misalign])
+    hints, FDIR marks and the transport pre-hash, in all three hash modes,
+    with the tables in LDS and forced to global memory (GCL_TUNE_TABLES=1)."""
+    rng = np.random.default_rng(9300 + 10 * mode + {"mbuf": 0, "mixed": 1, "lineend": 2}[misalign]
+                                + 100 * (tables == "global"))
     rts = random_runtimes(rng, 1024, 300)
     n = 7001
     frames, flen, offs, olf, rss, fdir, hint = fuzz_batch(
@@ -151,11 +154,14 @@ def test_gpu_quad_kernel_fuzz(g, orc, monkeypatch, misalign, mode):
     key = bytes(rng.integers(0, 256, size=40, dtype=np.uint8))
     t = orc.Tables(1024, mode, g.CFG_TRANS_HASH, 0x09, key)
     apply_runtimes(t, rts)
-    monkeypatch.setenv("GCL_TUNE_QUAD", "1")
+    env = {"GCL_TUNE_QUAD": "1", **({"GCL_TUNE_TABLES": "1"} if tables == "global" else {})}
+    for kk, vv in env.items():
+        monkeypatch.setenv(kk, vv)
     try:
         clf = g.Classifier(0, 1024, mode, g.CFG_TRANS_HASH, 0x09, key)
     finally:
-        monkeypatch.delenv("GCL_TUNE_QUAD")
+        for kk in env:
+            monkeypatch.delenv(kk)
     apply_runtimes(clf, rts)
     ve, ce, se, tre = t.classify(frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir_hi=fdir,
                                  frames_len=flen, dst_hint=hint, trans=True)
