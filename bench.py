@@ -130,6 +130,18 @@ def zero_fill(buf):
     hip.hipDeviceSynchronize()
 
 
+def hip_copy(dst, src, nbytes):
+    """hipMemcpy (kind default: direction from the pointers) between tensors
+    and DeviceBuffers, synchronous."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    for b in (dst, src):
+        assert nbytes <= b.numel() * b.element_size()
+    assert hip.hipMemcpy(dst.data_ptr(), src.data_ptr(), nbytes, 4) == 0  # hipMemcpyDefault
+    hip.hipDeviceSynchronize()
+
+
 # start-up placement check (Workload.check_placement): the kernel over the
 # chosen pair must run within this factor of the probe's time (per verdict
 # width), else the pool is placed again, at most PLACEMENT_TRIES times.  Fast
@@ -652,7 +664,19 @@ def ingress_pool_bench(device, vbytes, cycles=64, reps=10, zerocopy=True,
     out = {"mbufs": P, "pkts_per_batch": n, "frame_data_offset": "element + 344 (8-B aligned)",
            "descriptor_order": f"{cycles} random permutations of the pool"}
     cnt = torch.zeros(R + g.NR_STATS, dtype=torch.int64, device=device)
-    dv = torch.empty(n * vbytes, dtype=torch.uint8, device=device)
+    if os.environ.get("GCL_BENCH_PLACEMENT", "1") != "0":
+        # the device-resident pool placed against the verdict ring, as the
+        # udp64 frame pool is (gcl_dev_alloc_paired, DESIGN.md §4 "Buffer
+        # placement"): the iokernel places its ingress region once at start-up
+        dv = g.DeviceBuffer(n * vbytes, device.index or 0)
+        placed = g.DeviceBuffer(region.numel(), device.index or 0, partner=dv, vbytes=vbytes)
+        torch.cuda.synchronize()
+        hip_copy(placed, region, region.numel())
+        del region
+        region = placed
+        out["placement"] = placed.pair_info
+    else:
+        dv = torch.empty(n * vbytes, dtype=torch.uint8, device=device)
     st = torch.cuda.current_stream().cuda_stream
     nic = classifier(device, R, T, vbytes, hash_mode=g.HASH_NIC)
     setup_tables(nic, R, T)
@@ -721,7 +745,7 @@ def ingress_pool_bench(device, vbytes, cycles=64, reps=10, zerocopy=True,
         return out
     # zero-copy: the pool in pinned host memory, descriptors and verdicts too
     hreg = torch.empty(region.numel(), dtype=torch.uint8).pin_memory()
-    hreg.copy_(region)
+    hip_copy(hreg, region, region.numel())
     del region
     hoffs = offs.cpu().pin_memory()
     holf = olf.cpu().pin_memory()
