@@ -312,7 +312,7 @@ class Exchange:
 
 
 # GPU time of continuous steps (warmup + settle) before the timed region
-SETTLE_MS = 30.0
+SETTLE_MS = float(os.environ.get("GCL_BENCH_SETTLE_MS", "30"))
 
 
 def run_timed(w, steps, warmup, world, ex=None):
