@@ -387,6 +387,62 @@ def run_timed(w, steps, warmup, world, ex=None):
     return el, gpu_ms
 
 
+def group_bench(w, steps, warmup, device_index, period=EXCHANGE_EVERY):
+    """The multi-GPU step as the single-process iokernel links it
+    (include/gcl_group.h): a gcl_group over this process's GPUs (one here)
+    classifying the headline batch on the group's own stream, with the
+    per-runtime counts and rx counters all-gathered through RCCL
+    (ncclCommInitAll + ncclAllGather) every `period` steps on a side stream.
+    Same buffers as the headline; timed like run_timed (settle, then K steps
+    between synchronisations), the node-wide counts read back and checked."""
+    fl, tb = verdict_cfg(w.vbytes, w.R, w.T)
+    grp = g.Group([device_index], w.R, g.HASH_JENKINS, flags=fl, thread_bits=tb,
+                  exchange=g.XCHG_RCCL)
+    try:
+        for (r, ip, T, act, fl_tbl) in w.tables:
+            grp.runtime_set(r, ip, T, act, fl_tbl)
+        st = torch.cuda.ExternalStream(grp.stream(0), device=w.device)
+        shard_d = {"frames": w.frames, "n": w.n, "stride": w.stride}
+        k = [0]
+
+        def one():
+            grp.classify([shard_d], [w.verdicts])
+            k[0] += 1
+            if k[0] % period == 0:
+                grp.exchange()
+
+        t0 = time.perf_counter()
+        for _ in range(max(warmup, 1)):
+            one()
+        grp.sync()
+        step_ms = (time.perf_counter() - t0) * 1e3 / max(warmup, 1)
+        for _ in range(int(SETTLE_MS / max(step_ms, 1e-3)) + 1):
+            one()
+        grp.sync()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        e0.record(st)
+        for _ in range(steps):
+            one()
+        e1.record(st)
+        grp.sync()
+        el = time.perf_counter() - t0
+        grp.exchange()
+        c, s, per = grp.read()
+        ok = int(c.sum()) == w.n * k[0] and int(s[g.RX_PULLED]) == w.n * k[0]
+        return {"what": ("gcl_group (include/gcl_group.h): one process driving this node's GPUs, "
+                         "round-robin shards, RCCL ncclAllGather of u64[R+8] every "
+                         f"{period} steps on a side stream; the headline buffers"),
+                "n_gpus": grp.n, "exchange": "rccl",
+                "value": round(w.n * grp.n * steps / el / 1e6, 1), "unit": "Mpkt/s",
+                "ms_per_step": round(el / steps * 1e3, 4),
+                "gpu_ms_per_step": round(e0.elapsed_time(e1) / steps, 4),
+                "exchanges": int(k[0] // period) + 1,
+                "counts_check": "ok" if ok else f"MISMATCH {int(c.sum())} != {w.n * k[0]}"}
+    finally:
+        grp.close()
+
+
 def pmc_traffic(name, vbytes):
     """HBM bytes per launch from the committed PMC passes (profiles/pmc_*.json,
     tools/prof_summary.py: FETCH_SIZE + WRITE_SIZE, gfx950-corrected)."""
@@ -918,6 +974,8 @@ def main():
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-group", action="store_true",
+                    help="skip the gcl_group (C ABI + RCCL) line at N=1")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo only to rehearse N>1 on one GPU")
@@ -1009,6 +1067,11 @@ def main():
     if ex is not None:
         result["exchange"] = {"gpu_ms_per_step": round(gms, 4), "period_steps": args.exchange_every,
                               "periods": ex.k}
+    if world == 1 and not args.no_group:
+        try:
+            result["group"] = group_bench(w, args.steps, args.warmup, dev_index, args.exchange_every)
+        except (OSError, ImportError) as e:  # reported, never silently dropped
+            result["group"] = {"error": str(e)}
     del w, ex
     torch.cuda.empty_cache()
 

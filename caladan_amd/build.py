@@ -1,8 +1,12 @@
-"""Build the product shared library libgclassify.so in-tree for gfx950.
+"""Build the product shared libraries in-tree for gfx950.
 
 hipcc compiles the HIP kernels + C ABI (csrc/gclassify.hip); gcc compiles the
-host-side C (csrc/gcl_host.c); hipcc links both into caladan_amd/libgclassify.so.
-The .so is git-ignored but travels to the GPU box with the gpurun snapshot.
+host-side C (csrc/gcl_host.c, csrc/gcl_pcap.c); hipcc links them into
+caladan_amd/libgclassify.so.  The multi-GPU group (csrc/gcl_group.hip,
+include/gcl_group.h) is its own library, caladan_amd/libgclgroup.so, linked
+against libgclassify.so and RCCL, so that a single-GPU dataplane does not
+load RCCL.  The .so files are git-ignored but travel to the GPU box with the
+gpurun snapshot.
 """
 import os
 import subprocess
@@ -12,6 +16,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libgclassify.so")
+OUT_GROUP = os.path.join(HERE, "libgclgroup.so")
 OBJ = os.path.join(HERE, "_obj")
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -21,6 +26,8 @@ SOURCES_HIP = ["gclassify.hip"]
 SOURCES_C = ["gcl_host.c", "gcl_pcap.c"]
 DEPS = ["gcl_device.h", "../../include/gclassify.h", "../../include/gcl_host.h",
         "../../include/gcl_pcap.h"]
+SOURCE_GROUP = "gcl_group.hip"
+DEPS_GROUP = ["../../include/gclassify.h", "../../include/gcl_group.h"]
 
 
 def _run(cmd):
@@ -58,7 +65,23 @@ def build(force=False, verbose_resources=False):
         objs.append(o)
     if force or _stale(OUT, objs):
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT] + objs + ["-lm"])
+    build_group(force)
     return OUT
+
+
+def build_group(force=False):
+    """libgclgroup.so: the multi-GPU group over libgclassify.so + RCCL."""
+    s = os.path.join(CSRC, SOURCE_GROUP)
+    o = os.path.join(OBJ, SOURCE_GROUP + ".o")
+    deps = [s, os.path.abspath(__file__)] + [os.path.join(CSRC, d) for d in DEPS_GROUP]
+    if force or _stale(o, deps):
+        _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
+              "-c", s, "-o", o])
+    if force or _stale(OUT_GROUP, [o, OUT]):
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT_GROUP, o,
+              "-L" + HERE, "-lgclassify", "-L/opt/rocm/lib", "-lrccl",
+              "-Wl,-rpath,$ORIGIN", "-Wl,--no-undefined"])
+    return OUT_GROUP
 
 
 SANITIZE_FLAGS = ["-fsanitize=address,undefined", "-fno-sanitize-recover=all",

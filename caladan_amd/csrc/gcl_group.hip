@@ -1,0 +1,608 @@
+/*
+ * gcl_group.hip - the multi-GPU step behind the C ABI (include/gcl_group.h).
+ *
+ * One process, one dataplane thread (iokernel/dpdk.c:276-280,
+ * iokernel/main.c:144-150), every GPU of the node: one gcl_ctx per GPU with
+ * replicated tables, batches split round-robin in blocks, and the
+ * per-runtime counts + rx counters (iokernel/defs.h:417-460) all-gathered
+ * with RCCL over xGMI.
+ *
+ * Counters.  Every GPU accumulates u64[R + 8] ([counts | stats]) in its own
+ * `acc` with the classify kernels' atomics.  An exchange first snapshots
+ * `acc` on the GPU's compute stream (a 1-8 KiB D2D copy, in order with the
+ * launches before it), so launches enqueued after the exchange never race
+ * the gather; the gather and the sum then run on a side stream per GPU and
+ * overlap the next batches.  Snapshots rotate over kSlots buffers, each
+ * guarded by the event that ends its exchange.
+ */
+#include <errno.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <new>
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include "../../include/gcl_group.h"
+#include "../../include/gclassify.h"
+
+namespace {
+
+constexpr int kSlots = 4; /* exchanges in flight */
+
+struct HipErr {
+	hipError_t e = hipSuccess;
+	void operator()(hipError_t r)
+	{
+		if (r != hipSuccess && e == hipSuccess)
+			e = r;
+	}
+	bool bad() const { return e != hipSuccess; }
+};
+
+/* out[i] = sum over the @rows gathered vectors of element i */
+__global__ void __launch_bounds__(256) sum_rows_kernel(const unsigned long long *rows, int nrows,
+                                                       int len, unsigned long long *out)
+{
+	const int i = blockIdx.x * 256 + threadIdx.x;
+	if (i >= len)
+		return;
+	unsigned long long s = 0;
+	for (int r = 0; r < nrows; r++)
+		s += rows[(size_t)r * len + i];
+	out[i] = s;
+}
+
+uint32_t verdict_size(uint32_t flags)
+{
+	return (flags & GCL_CFG_VERDICT2) ? 2 : (flags & GCL_CFG_VERDICT4) ? 4 : 8;
+}
+
+} // namespace
+
+struct gcl_group {
+	int n;
+	uint32_t R, L;      /* runtimes; vector length R + GCL_NR_STATS */
+	uint64_t block;
+	uint32_t xchg;
+	uint32_t vsize;
+	int nst;            /* work streams per GPU (host batches) */
+	struct Dev {
+		int dev;
+		gcl_ctx *ctx;
+		hipStream_t st[GCL_GROUP_MAX_STREAMS]; /* st[0]: device-resident launches */
+		hipEvent_t st_ev[GCL_GROUP_MAX_STREAMS];
+		hipStream_t xs;                        /* exchange stream */
+		uint64_t *acc;                         /* u64[L] */
+		uint64_t *snap;                        /* u64[kSlots][L] */
+		uint64_t *gath;                        /* u64[kSlots][n * L] */
+		uint64_t *node;                        /* u64[kSlots][L] */
+		hipEvent_t snap_ev[kSlots];
+		hipEvent_t done_ev[kSlots];
+		bool pending[kSlots];
+		/* COPY staging per work stream, sized for one block */
+		uint8_t *slab[GCL_GROUP_MAX_STREAMS];
+		uint8_t *side[GCL_GROUP_MAX_STREAMS];
+		uint8_t *verd[GCL_GROUP_MAX_STREAMS];
+		ncclComm_t comm;
+	} d[GCL_GROUP_MAX_DEV];
+	uint64_t *host_node; /* pinned u64[kSlots][L]: GPU 0's node vector */
+	uint64_t *host_gath; /* pinned u64[kSlots][n * L]: GPU 0's gathered vectors */
+	uint64_t seq;        /* exchanges enqueued */
+	int last;            /* slot of the last exchange, -1 = none */
+};
+
+extern "C" uint64_t gcl_shard_count(uint64_t n, uint32_t world, uint32_t rank, uint64_t block)
+{
+	if (world <= 1 || block == 0)
+		return rank == 0 ? n : 0;
+	if (rank >= world)
+		return 0;
+	const uint64_t full = n / block, tail = n % block;
+	/* blocks rank, rank + world, ... below full, plus the ragged last block */
+	uint64_t c = (full > rank ? (full - rank + world - 1) / world : 0) * block;
+	if (tail && full % world == rank)
+		c += tail;
+	return c;
+}
+
+extern "C" uint64_t gcl_shard_global(uint64_t j, uint32_t world, uint32_t rank, uint64_t block)
+{
+	if (world <= 1 || block == 0)
+		return j;
+	return ((j / block) * world + rank) * block + j % block;
+}
+
+static void free_dev(gcl_group::Dev &D, bool rccl)
+{
+	if (D.dev < 0)
+		return;
+	(void)hipSetDevice(D.dev);
+	if (rccl && D.comm)
+		(void)ncclCommDestroy(D.comm);
+	for (int i = 0; i < GCL_GROUP_MAX_STREAMS; i++) {
+		if (D.st[i])
+			(void)hipStreamDestroy(D.st[i]);
+		if (D.st_ev[i])
+			(void)hipEventDestroy(D.st_ev[i]);
+		if (D.slab[i])
+			(void)hipFree(D.slab[i]);
+		if (D.side[i])
+			(void)hipFree(D.side[i]);
+		if (D.verd[i])
+			(void)hipFree(D.verd[i]);
+	}
+	if (D.xs)
+		(void)hipStreamDestroy(D.xs);
+	for (int s = 0; s < kSlots; s++) {
+		if (D.snap_ev[s])
+			(void)hipEventDestroy(D.snap_ev[s]);
+		if (D.done_ev[s])
+			(void)hipEventDestroy(D.done_ev[s]);
+	}
+	for (uint64_t *p : {D.acc, D.snap, D.gath, D.node})
+		if (p)
+			(void)hipFree(p);
+	if (D.ctx)
+		gcl_close(D.ctx);
+}
+
+extern "C" void gcl_group_close(struct gcl_group *g)
+{
+	if (!g)
+		return;
+	(void)gcl_group_sync(g);
+	for (int i = 0; i < g->n; i++)
+		free_dev(g->d[i], g->xchg == GCL_XCHG_RCCL);
+	if (g->host_node)
+		(void)hipHostFree(g->host_node);
+	if (g->host_gath)
+		(void)hipHostFree(g->host_gath);
+	delete g;
+}
+
+extern "C" int gcl_group_open(int ndev, const int *devs, const struct gcl_cfg *cfg,
+                              const struct gcl_group_cfg *gcfg, struct gcl_group **out)
+{
+	if (!out || !devs || !cfg || ndev < 1 || ndev > GCL_GROUP_MAX_DEV)
+		return -EINVAL;
+	*out = nullptr;
+	const uint64_t block = gcfg && gcfg->block ? gcfg->block : GCL_GROUP_BLOCK;
+	const uint32_t xchg = gcfg ? gcfg->exchange : GCL_XCHG_RCCL;
+	const uint32_t nst = gcfg && gcfg->nstreams ? gcfg->nstreams : 2;
+	if ((block & 255) || block > (1ull << 32) || xchg > GCL_XCHG_HOST ||
+	    nst > GCL_GROUP_MAX_STREAMS)
+		return -EINVAL;
+	int visible = 0;
+	if (hipGetDeviceCount(&visible) != hipSuccess)
+		return -ENODEV;
+	for (int i = 0; i < ndev; i++) {
+		if (devs[i] < 0 || devs[i] >= visible)
+			return -ENODEV;
+		for (int j = 0; j < i && xchg == GCL_XCHG_RCCL; j++)
+			if (devs[j] == devs[i])
+				return -EINVAL; /* one communicator rank per GPU */
+	}
+
+	gcl_group *g = new (std::nothrow) gcl_group();
+	if (!g)
+		return -ENOMEM;
+	g->n = ndev;
+	g->R = cfg->max_runtimes;
+	g->L = cfg->max_runtimes + GCL_NR_STATS;
+	g->block = block;
+	g->xchg = xchg;
+	g->vsize = verdict_size(cfg->flags);
+	g->nst = (int)nst;
+	g->seq = 0;
+	g->last = -1;
+	for (int i = 0; i < GCL_GROUP_MAX_DEV; i++)
+		g->d[i].dev = -1;
+	const size_t L8 = (size_t)g->L * 8;
+	int ret = 0;
+	for (int i = 0; i < ndev && !ret; i++) {
+		gcl_group::Dev &D = g->d[i];
+		D.dev = devs[i];
+		ret = gcl_open(devs[i], cfg, &D.ctx);
+		if (ret)
+			break;
+		HipErr he;
+		he(hipSetDevice(D.dev));
+		for (int s = 0; s < g->nst; s++) {
+			he(hipStreamCreateWithFlags(&D.st[s], hipStreamNonBlocking));
+			he(hipEventCreateWithFlags(&D.st_ev[s], hipEventDisableTiming));
+		}
+		he(hipStreamCreateWithFlags(&D.xs, hipStreamNonBlocking));
+		for (int s = 0; s < kSlots; s++) {
+			he(hipEventCreateWithFlags(&D.snap_ev[s], hipEventDisableTiming));
+			he(hipEventCreateWithFlags(&D.done_ev[s], hipEventDisableTiming));
+		}
+		he(hipMalloc(&D.acc, L8));
+		he(hipMalloc(&D.snap, L8 * kSlots));
+		he(hipMalloc(&D.gath, L8 * kSlots * ndev));
+		he(hipMalloc(&D.node, L8 * kSlots));
+		if (!he.bad())
+			he(hipMemset(D.acc, 0, L8));
+		if (he.bad())
+			ret = he.e == hipErrorOutOfMemory ? -ENOMEM : -EIO;
+	}
+	if (!ret) {
+		HipErr he;
+		he(hipHostMalloc(&g->host_node, L8 * kSlots, hipHostMallocDefault));
+		he(hipHostMalloc(&g->host_gath, L8 * kSlots * ndev, hipHostMallocDefault));
+		if (he.bad())
+			ret = -ENOMEM;
+	}
+	if (!ret && xchg == GCL_XCHG_RCCL) {
+		ncclComm_t comms[GCL_GROUP_MAX_DEV] = {};
+		if (ncclCommInitAll(comms, ndev, devs) != ncclSuccess)
+			ret = -EIO;
+		else
+			for (int i = 0; i < ndev; i++)
+				g->d[i].comm = comms[i];
+	}
+	if (ret) {
+		gcl_group_close(g);
+		return ret;
+	}
+	*out = g;
+	return 0;
+}
+
+extern "C" int gcl_group_size(const struct gcl_group *g) { return g ? g->n : -EINVAL; }
+
+extern "C" struct gcl_ctx *gcl_group_ctx(struct gcl_group *g, int i)
+{
+	return g && i >= 0 && i < g->n ? g->d[i].ctx : nullptr;
+}
+
+extern "C" void *gcl_group_stream(struct gcl_group *g, int i)
+{
+	return g && i >= 0 && i < g->n ? (void *)g->d[i].st[0] : nullptr;
+}
+
+extern "C" int gcl_group_runtime_set(struct gcl_group *g, uint16_t uniqid, uint32_t ip_host,
+                                     uint16_t thread_count, uint16_t active_count,
+                                     const uint16_t *flow_tbl)
+{
+	if (!g)
+		return -EINVAL;
+	const int r0 = gcl_runtime_set(g->d[0].ctx, uniqid, ip_host, thread_count, active_count, flow_tbl);
+	if (r0)
+		return r0;
+	for (int i = 1; i < g->n; i++)
+		if (gcl_runtime_set(g->d[i].ctx, uniqid, ip_host, thread_count, active_count, flow_tbl))
+			return -EIO; /* replicas hold the same tables: cannot differ */
+	return 0;
+}
+
+extern "C" int gcl_group_runtime_del(struct gcl_group *g, uint16_t uniqid)
+{
+	if (!g)
+		return -EINVAL;
+	const int r0 = gcl_runtime_del(g->d[0].ctx, uniqid);
+	if (r0)
+		return r0;
+	for (int i = 1; i < g->n; i++)
+		if (gcl_runtime_del(g->d[i].ctx, uniqid))
+			return -EIO;
+	return 0;
+}
+
+extern "C" int gcl_group_runtime_set_trans_seed(struct gcl_group *g, uint16_t uniqid, uint32_t seed)
+{
+	if (!g)
+		return -EINVAL;
+	const int r0 = gcl_runtime_set_trans_seed(g->d[0].ctx, uniqid, seed);
+	if (r0)
+		return r0;
+	for (int i = 1; i < g->n; i++)
+		if (gcl_runtime_set_trans_seed(g->d[i].ctx, uniqid, seed))
+			return -EIO;
+	return 0;
+}
+
+extern "C" int gcl_group_classify(struct gcl_group *g, const struct gcl_batch *shards,
+                                  void *const *verdicts)
+{
+	if (!g || !shards || !verdicts)
+		return -EINVAL;
+	for (int i = 0; i < g->n; i++) {
+		gcl_group::Dev &D = g->d[i];
+		const int r = gcl_classify(D.ctx, &shards[i], verdicts[i], D.acc, D.acc + g->R, D.st[0]);
+		if (r)
+			return r;
+	}
+	return 0;
+}
+
+/* device address of registered host memory on the current device, or NULL */
+static void *mapped(const void *h)
+{
+	void *d = nullptr;
+	if (!h)
+		return nullptr;
+	if (hipHostGetDevicePointer(&d, (void *)h, 0) != hipSuccess) {
+		(void)hipGetLastError();
+		return nullptr;
+	}
+	return d;
+}
+
+static int ensure_staging(gcl_group *g, gcl_group::Dev &D, int nst)
+{
+	if (hipSetDevice(D.dev) != hipSuccess)
+		return -ENODEV;
+	for (int s = 0; s < nst; s++) {
+		if (D.slab[s])
+			continue;
+		if (hipMalloc(&D.slab[s], g->block * GCL_HDR_GRANULE) != hipSuccess ||
+		    hipMalloc(&D.side[s], g->block * 13) != hipSuccess ||
+		    hipMalloc(&D.verd[s], g->block * 8) != hipSuccess)
+			return -ENOMEM;
+	}
+	return 0;
+}
+
+/* Sub-batch of block @b: packets [b * block, min(n, (b + 1) * block)). */
+static gcl_batch block_batch(const gcl_batch &hb, uint64_t b, uint64_t block)
+{
+	gcl_batch s = hb;
+	const uint64_t i0 = b * block;
+	s.n = hb.n - i0 < block ? hb.n - i0 : block;
+	if (hb.offs) {
+		s.offs = hb.offs + i0;
+	} else {
+		const uint64_t o = i0 * hb.stride;
+		s.frames = hb.frames + o;
+		s.frames_len = hb.frames_len > o ? hb.frames_len - o : 0;
+	}
+	if (hb.olflags)
+		s.olflags = hb.olflags + i0;
+	if (hb.rss)
+		s.rss = hb.rss + i0;
+	if (hb.fdir_hi)
+		s.fdir_hi = hb.fdir_hi + i0;
+	if (hb.dst_hint)
+		s.dst_hint = hb.dst_hint + i0;
+	if (hb.pkt_len)
+		s.pkt_len = hb.pkt_len + i0;
+	return s;
+}
+
+extern "C" int gcl_group_classify_host(struct gcl_group *g, const struct gcl_batch *hb,
+                                       void *host_verdicts, const struct gcl_e2e_opts *o)
+{
+	if (!g || !hb || !host_verdicts || !o || o->mode > GCL_E2E_ZEROCOPY ||
+	    o->nstreams > GCL_GROUP_MAX_STREAMS)
+		return -EINVAL;
+	if (hb->n == 0)
+		return 0;
+	if (!hb->frames || (!hb->offs && (hb->stride < 16 || (hb->stride & 15))))
+		return -EINVAL;
+	const int nst = o->nstreams ? (int)o->nstreams : g->nst;
+	const int G = g->n;
+	const uint64_t nb = (hb->n + g->block - 1) / g->block;
+	int ret = 0;
+	HipErr he;
+	if (o->mode == GCL_E2E_ZEROCOPY) {
+		/* every GPU reads its blocks straight out of registered host
+		 * memory and writes their verdicts back in place */
+		gcl_batch db[GCL_GROUP_MAX_DEV];
+		uint8_t *dv[GCL_GROUP_MAX_DEV];
+		for (int i = 0; i < G; i++) {
+			if (hipSetDevice(g->d[i].dev) != hipSuccess)
+				return -ENODEV;
+			db[i] = *hb;
+			db[i].frames = (const uint8_t *)mapped(hb->frames);
+			db[i].offs = (const uint64_t *)mapped(hb->offs);
+			db[i].olflags = (const uint8_t *)mapped(hb->olflags);
+			db[i].rss = (const uint32_t *)mapped(hb->rss);
+			db[i].fdir_hi = (const uint32_t *)mapped(hb->fdir_hi);
+			db[i].dst_hint = (const uint32_t *)mapped(hb->dst_hint);
+			db[i].pkt_len = nullptr;
+			dv[i] = (uint8_t *)mapped(host_verdicts);
+			if (!db[i].frames || !dv[i] || (hb->offs && !db[i].offs) ||
+			    (hb->olflags && !db[i].olflags) || (hb->rss && !db[i].rss) ||
+			    (hb->fdir_hi && !db[i].fdir_hi) || (hb->dst_hint && !db[i].dst_hint))
+				return -EFAULT; /* not registered: gcl_host_register */
+		}
+		/* blocks in batch order, so every GPU has work from the start */
+		for (uint64_t b = 0; b < nb && !ret; b++) {
+			const int i = (int)(b % G);
+			gcl_group::Dev &D = g->d[i];
+			const gcl_batch s = block_batch(db[i], b, g->block);
+			ret = gcl_classify(D.ctx, &s, dv[i] + b * g->block * g->vsize, D.acc, D.acc + g->R,
+			                   D.st[(b / G) % nst]);
+		}
+	} else {
+		if (hb->offs || hb->stride < GCL_HDR_GRANULE)
+			return -EINVAL; /* the copy path gathers fixed-stride header granules */
+		if (hb->frames_len < (hb->n - 1) * hb->stride + GCL_HDR_GRANULE)
+			return -EINVAL;
+		for (int i = 0; i < G; i++)
+			if ((ret = ensure_staging(g, g->d[i], nst)))
+				return ret;
+		for (uint64_t b = 0; b < nb && !ret; b++) {
+			const int i = (int)(b % G);
+			gcl_group::Dev &D = g->d[i];
+			const int si = (int)((b / G) % nst);
+			hipStream_t st = D.st[si];
+			const gcl_batch s = block_batch(*hb, b, g->block);
+			const uint64_t m = s.n, B = g->block;
+			if (hipSetDevice(D.dev) != hipSuccess)
+				return -ENODEV;
+			/* H2D of only the 64-B header granule of every slot (2D DMA) */
+			if (hb->stride == GCL_HDR_GRANULE)
+				he(hipMemcpyAsync(D.slab[si], s.frames, m * GCL_HDR_GRANULE, hipMemcpyHostToDevice, st));
+			else
+				he(hipMemcpy2DAsync(D.slab[si], GCL_HDR_GRANULE, s.frames, hb->stride,
+				                    GCL_HDR_GRANULE, m, hipMemcpyHostToDevice, st));
+			gcl_batch db = {};
+			db.frames = D.slab[si];
+			db.frames_len = m * GCL_HDR_GRANULE;
+			db.stride = GCL_HDR_GRANULE;
+			db.n = m;
+			uint8_t *side = D.side[si];
+			if (s.olflags) {
+				he(hipMemcpyAsync(side, s.olflags, m, hipMemcpyHostToDevice, st));
+				db.olflags = side;
+			}
+			if (s.rss) {
+				he(hipMemcpyAsync(side + B, s.rss, m * 4, hipMemcpyHostToDevice, st));
+				db.rss = (const uint32_t *)(side + B);
+			}
+			if (s.fdir_hi) {
+				he(hipMemcpyAsync(side + 5 * B, s.fdir_hi, m * 4, hipMemcpyHostToDevice, st));
+				db.fdir_hi = (const uint32_t *)(side + 5 * B);
+			}
+			if (s.dst_hint) {
+				he(hipMemcpyAsync(side + 9 * B, s.dst_hint, m * 4, hipMemcpyHostToDevice, st));
+				db.dst_hint = (const uint32_t *)(side + 9 * B);
+			}
+			ret = gcl_classify(D.ctx, &db, D.verd[si], D.acc, D.acc + g->R, st);
+			he(hipMemcpyAsync((uint8_t *)host_verdicts + b * B * g->vsize, D.verd[si],
+			                  m * g->vsize, hipMemcpyDeviceToHost, st));
+		}
+	}
+	const int sr = gcl_group_sync(g);
+	if (ret)
+		return ret;
+	return he.bad() ? -EIO : sr;
+}
+
+extern "C" int gcl_group_exchange(struct gcl_group *g)
+{
+	if (!g)
+		return -EINVAL;
+	const int b = (int)(g->seq % kSlots);
+	const size_t L = g->L, L8 = L * 8;
+	HipErr he;
+	for (int i = 0; i < g->n; i++) {
+		gcl_group::Dev &D = g->d[i];
+		he(hipSetDevice(D.dev));
+		hipStream_t c = D.st[0];
+		/* the snapshot follows every launch enqueued so far, on every
+		 * work stream of this GPU */
+		for (int s = 1; s < g->nst; s++) {
+			he(hipEventRecord(D.st_ev[s], D.st[s]));
+			he(hipStreamWaitEvent(c, D.st_ev[s], 0));
+		}
+		if (D.pending[b]) /* slot b's previous exchange must be done with it */
+			he(hipStreamWaitEvent(c, D.done_ev[b], 0));
+		he(hipMemcpyAsync(D.snap + b * L, D.acc, L8, hipMemcpyDeviceToDevice, c));
+		he(hipEventRecord(D.snap_ev[b], c));
+		he(hipStreamWaitEvent(D.xs, D.snap_ev[b], 0));
+	}
+	if (he.bad())
+		return -EIO;
+	if (g->xchg == GCL_XCHG_RCCL) {
+		bool ok = ncclGroupStart() == ncclSuccess;
+		for (int i = 0; i < g->n && ok; i++) {
+			gcl_group::Dev &D = g->d[i];
+			ok = ncclAllGather(D.snap + b * L, D.gath + b * L * g->n, L, ncclUint64, D.comm,
+			                   D.xs) == ncclSuccess;
+		}
+		ok = ncclGroupEnd() == ncclSuccess && ok;
+		if (!ok)
+			return -EIO;
+		for (int i = 0; i < g->n; i++) {
+			gcl_group::Dev &D = g->d[i];
+			he(hipSetDevice(D.dev));
+			hipLaunchKernelGGL(sum_rows_kernel, dim3((unsigned)((L + 255) / 256)), dim3(256), 0, D.xs,
+			                   (const unsigned long long *)(D.gath + b * L * g->n), g->n, (int)L,
+			                   (unsigned long long *)(D.node + b * L));
+			he(hipGetLastError());
+			if (i == 0) {
+				he(hipMemcpyAsync(g->host_node + b * L, D.node + b * L, L8, hipMemcpyDeviceToHost, D.xs));
+				he(hipMemcpyAsync(g->host_gath + b * L * g->n, D.gath + b * L * g->n, L8 * g->n,
+				                  hipMemcpyDeviceToHost, D.xs));
+			}
+		}
+	} else {
+		for (int i = 0; i < g->n; i++) {
+			gcl_group::Dev &D = g->d[i];
+			he(hipSetDevice(D.dev));
+			he(hipMemcpyAsync(g->host_gath + (b * g->n + i) * L, D.snap + b * L, L8,
+			                  hipMemcpyDeviceToHost, D.xs));
+		}
+	}
+	for (int i = 0; i < g->n; i++) {
+		gcl_group::Dev &D = g->d[i];
+		he(hipSetDevice(D.dev));
+		he(hipEventRecord(D.done_ev[b], D.xs));
+		D.pending[b] = true;
+	}
+	g->last = b;
+	g->seq++;
+	return he.bad() ? -EIO : 0;
+}
+
+extern "C" int gcl_group_read(struct gcl_group *g, uint64_t *node_counts, uint64_t *node_stats,
+                              uint64_t *per_gpu)
+{
+	if (!g)
+		return -EINVAL;
+	if (g->last < 0)
+		return -ENODATA;
+	const int b = g->last;
+	const size_t L = g->L;
+	for (int i = 0; i < g->n; i++) {
+		gcl_group::Dev &D = g->d[i];
+		if (hipSetDevice(D.dev) != hipSuccess || hipEventSynchronize(D.done_ev[b]) != hipSuccess)
+			return -EIO;
+	}
+	const uint64_t *rows = g->host_gath + b * L * g->n;
+	for (size_t k = 0; k < L; k++) {
+		uint64_t v;
+		if (g->xchg == GCL_XCHG_RCCL) {
+			v = g->host_node[b * L + k];
+		} else {
+			v = 0;
+			for (int i = 0; i < g->n; i++)
+				v += rows[i * L + k];
+		}
+		if (k < g->R) {
+			if (node_counts)
+				node_counts[k] = v;
+		} else if (node_stats) {
+			node_stats[k - g->R] = v;
+		}
+	}
+	if (per_gpu)
+		memcpy(per_gpu, rows, L * 8 * g->n);
+	return 0;
+}
+
+extern "C" int gcl_group_sync(struct gcl_group *g)
+{
+	if (!g)
+		return -EINVAL;
+	int ret = 0;
+	for (int i = 0; i < g->n; i++) {
+		gcl_group::Dev &D = g->d[i];
+		if (D.dev < 0 || hipSetDevice(D.dev) != hipSuccess)
+			continue;
+		for (int s = 0; s < g->nst; s++)
+			if (D.st[s] && hipStreamSynchronize(D.st[s]) != hipSuccess)
+				ret = -EIO;
+		if (D.xs && hipStreamSynchronize(D.xs) != hipSuccess)
+			ret = -EIO;
+	}
+	return ret;
+}
+
+extern "C" int gcl_group_reset(struct gcl_group *g)
+{
+	if (!g)
+		return -EINVAL;
+	int ret = gcl_group_sync(g);
+	for (int i = 0; i < g->n && !ret; i++) {
+		gcl_group::Dev &D = g->d[i];
+		if (hipSetDevice(D.dev) != hipSuccess || hipMemset(D.acc, 0, (size_t)g->L * 8) != hipSuccess)
+			ret = -EIO;
+	}
+	return ret;
+}

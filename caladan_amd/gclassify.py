@@ -567,6 +567,167 @@ def version():
     return lib.gcl_version().decode()
 
 
+# ------------------------------------------------------------- multi-GPU group
+GROUP_LIB_PATH = os.path.join(HERE, "libgclgroup.so")
+GROUP_BLOCK = 64 << 10
+XCHG_RCCL, XCHG_HOST = 0, 1
+
+
+class GclGroupCfg(ctypes.Structure):
+    _fields_ = [("block", ctypes.c_uint64), ("exchange", ctypes.c_uint32),
+                ("nstreams", ctypes.c_uint32)]
+
+
+_glib = None
+
+
+def group_lib():
+    """libgclgroup.so (include/gcl_group.h), loaded on first use: the
+    single-GPU binding never pulls in RCCL."""
+    global _glib
+    if _glib is not None:
+        return _glib
+    if not os.path.exists(GROUP_LIB_PATH):
+        raise ImportError(f"{GROUP_LIB_PATH} missing: run `python caladan_amd/build.py`")
+    gl = ctypes.CDLL(GROUP_LIB_PATH)
+    vp, u16, u32, u64, i32 = ctypes.c_void_p, ctypes.c_uint16, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+    sig = {
+        "gcl_group_open": (i32, [i32, ctypes.POINTER(i32), ctypes.POINTER(GclCfg),
+                                 ctypes.POINTER(GclGroupCfg), ctypes.POINTER(vp)]),
+        "gcl_group_close": (None, [vp]),
+        "gcl_group_size": (i32, [vp]),
+        "gcl_group_ctx": (vp, [vp, i32]),
+        "gcl_group_stream": (vp, [vp, i32]),
+        "gcl_group_runtime_set": (i32, [vp, u16, u32, u16, u16, ctypes.POINTER(u16)]),
+        "gcl_group_runtime_del": (i32, [vp, u16]),
+        "gcl_group_runtime_set_trans_seed": (i32, [vp, u16, u32]),
+        "gcl_shard_count": (u64, [u64, u32, u32, u64]),
+        "gcl_shard_global": (u64, [u64, u32, u32, u64]),
+        "gcl_group_classify": (i32, [vp, ctypes.POINTER(GclBatch), ctypes.POINTER(vp)]),
+        "gcl_group_classify_host": (i32, [vp, ctypes.POINTER(GclBatch), vp, ctypes.POINTER(GclE2eOpts)]),
+        "gcl_group_exchange": (i32, [vp]),
+        "gcl_group_read": (i32, [vp, vp, vp, vp]),
+        "gcl_group_reset": (i32, [vp]),
+        "gcl_group_sync": (i32, [vp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(gl, name)
+        f.restype = res
+        f.argtypes = args
+    _glib = gl
+    return gl
+
+
+def shard_count(n, world, rank, block=GROUP_BLOCK):
+    return group_lib().gcl_shard_count(n, world, rank, block)
+
+
+def shard_global(j, world, rank, block=GROUP_BLOCK):
+    return group_lib().gcl_shard_global(j, world, rank, block)
+
+
+class Group:
+    """gcl_group: one dataplane driving several GPUs (include/gcl_group.h) --
+    a gcl_ctx per GPU, round-robin block shards, RCCL all-gather of the
+    per-runtime counts and rx counters."""
+
+    def __init__(self, devices, max_runtimes=16, hash_mode=HASH_JENKINS, flags=0,
+                 default_olflags=F_RSS_HASH | F_IP_CKSUM_GOOD, rss_key=CALADAN_RSS_KEY,
+                 thread_bits=0, block=GROUP_BLOCK, exchange=XCHG_RCCL, nstreams=2):
+        gl = group_lib()
+        if isinstance(hash_mode, str):
+            hash_mode = HASH_MODES[hash_mode]
+        cfg = GclCfg(max_runtimes=max_runtimes, hash_mode=hash_mode, flags=flags,
+                     default_olflags=default_olflags, thread_bits=thread_bits)
+        key = bytes(rss_key)[:40].ljust(40, b"\0")
+        for i in range(40):
+            cfg.rss_key[i] = key[i]
+        self.devices = list(devices)
+        self.n = len(self.devices)
+        self.max_runtimes = max_runtimes
+        self.vbytes = verdict_bytes(flags)
+        self.block = block
+        devs = (ctypes.c_int * self.n)(*self.devices)
+        gc = GclGroupCfg(block=block, exchange=exchange, nstreams=nstreams)
+        self._g = ctypes.c_void_p()
+        _check(gl.gcl_group_open(self.n, devs, ctypes.byref(cfg), ctypes.byref(gc), ctypes.byref(self._g)),
+               "gcl_group_open")
+
+    def close(self):
+        if self._g:
+            group_lib().gcl_group_close(self._g)
+            self._g = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def stream(self, i=0):
+        return group_lib().gcl_group_stream(self._g, i)
+
+    def runtime_set(self, uniqid, ip, thread_count, active_count, flow_tbl=None):
+        tbl = None
+        if flow_tbl is not None:
+            tbl = (ctypes.c_uint16 * max(len(flow_tbl), 1))(*flow_tbl)
+        return _check(group_lib().gcl_group_runtime_set(self._g, uniqid, ip, thread_count, active_count, tbl),
+                      "gcl_group_runtime_set")
+
+    def runtime_del(self, uniqid):
+        return _check(group_lib().gcl_group_runtime_del(self._g, uniqid), "gcl_group_runtime_del")
+
+    def classify(self, shards, verdicts):
+        """shards: one dict per GPU (frames, n, stride, and optional offs,
+        olflags, rss, fdir_hi, dst_hint, frames_len) of device buffers on that
+        GPU; verdicts: one device buffer per GPU.  Asynchronous."""
+        if len(shards) != self.n or len(verdicts) != self.n:
+            raise ValueError("one shard and one verdict buffer per GPU")
+        bs = (GclBatch * self.n)()
+        vs = (ctypes.c_void_p * self.n)()
+        for i, (s, v) in enumerate(zip(shards, verdicts)):
+            if _nbytes(v) < self.vbytes * s["n"]:
+                raise ValueError("verdict buffer too small")
+            bs[i] = GclBatch(frames=_ptr(s["frames"]), frames_len=_frames_len(s["frames"], s.get("frames_len")),
+                             stride=s.get("stride", 0), offs=_ptr(s.get("offs")),
+                             olflags=_ptr(s.get("olflags")), rss=_ptr(s.get("rss")),
+                             fdir_hi=_ptr(s.get("fdir_hi")), pkt_len=None, n=s["n"],
+                             dst_hint=_ptr(s.get("dst_hint")))
+            vs[i] = _ptr(v)
+        return _check(group_lib().gcl_group_classify(self._g, bs, vs), "gcl_group_classify")
+
+    def classify_host(self, frames, n, stride=0, verdicts=None, offs=None, olflags=None, rss=None,
+                      fdir_hi=None, dst_hint=None, frames_len=None, mode=E2E_ZEROCOPY, nstreams=0):
+        """One host batch split round-robin over the GPUs (synchronous)."""
+        if verdicts is None or _nbytes(verdicts) < self.vbytes * n:
+            raise ValueError("verdict buffer too small")
+        b = GclBatch(frames=_ptr(frames), frames_len=_frames_len(frames, frames_len), stride=stride,
+                     offs=_ptr(offs), olflags=_ptr(olflags), rss=_ptr(rss), fdir_hi=_ptr(fdir_hi),
+                     pkt_len=None, n=n, dst_hint=_ptr(dst_hint))
+        o = GclE2eOpts(mode=mode, nstreams=nstreams, chunk=0)
+        return _check(group_lib().gcl_group_classify_host(self._g, ctypes.byref(b), _ptr(verdicts),
+                                                          ctypes.byref(o)), "gcl_group_classify_host")
+
+    def exchange(self):
+        return _check(group_lib().gcl_group_exchange(self._g), "gcl_group_exchange")
+
+    def read(self):
+        """(node counts u64[R], node stats u64[8], per-GPU vectors u64[n, R + 8])
+        of the last exchange."""
+        c = np.zeros(self.max_runtimes, dtype=np.uint64)
+        s = np.zeros(NR_STATS, dtype=np.uint64)
+        p = np.zeros((self.n, self.max_runtimes + NR_STATS), dtype=np.uint64)
+        _check(group_lib().gcl_group_read(self._g, c.ctypes.data, s.ctypes.data, p.ctypes.data),
+               "gcl_group_read")
+        return c, s, p
+
+    def reset(self):
+        return _check(group_lib().gcl_group_reset(self._g), "gcl_group_reset")
+
+    def sync(self):
+        return _check(group_lib().gcl_group_sync(self._g), "gcl_group_sync")
+
+
 __all__ = [n for n in dir() if not n.startswith("_")]
 
 

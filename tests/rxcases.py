@@ -188,6 +188,14 @@ def to_verdict2(v, thread_count, thread_bits):
     return out.astype(np.uint16)
 
 
+def load_struct_frames():
+    """tests/golden/struct_frames_ref.npz (make_struct_frames.py): (ips,
+    frames[n, 64], uniqid, hash, hit), frames written by the reference's
+    inc/net structs, hashes by the reference's jenkins_hash."""
+    with np.load(os.path.join(GOLDEN, "struct_frames_ref.npz"), allow_pickle=False) as z:
+        return z["ips"], z["frames"], z["uniqid"], z["hash"], z["hit"]
+
+
 def ref_struct_batch(ref, orc, rng, n, R):
     """@n 64-B frames written by the reference's own inc/net structs
     (oracle/ref_host.c ref_build_frame): IPv4 UDP/TCP with IHL 5..11 and

@@ -223,3 +223,38 @@ def test_parse_offsets_match_reference_structs(g, ref, orc):
             assert int(v["thread"][i]) == h % 4, i
         else:
             assert int(v["action"][i]) & 0x3F == g.ACT_DROP_UNREG, i
+
+
+def test_struct_frames_fixture_matches_oracle(g, orc):
+    """The committed struct-frame fixture (tests/golden/struct_frames_ref.npz,
+    frames from the reference's inc/net structs, hashes from its
+    jenkins_hash) classifies on the oracle as it records: what the GPU test
+    checks without loading anything built from reference sources."""
+    from tests.rxcases import load_struct_frames
+    ips, frames, uniq, hashes, hit = load_struct_frames()
+    R, n = 64, len(frames)
+    t = orc.Tables(R, 1, 0, 0x09)
+    for u, ip in enumerate(ips):
+        assert t.runtime_set(u, int(ip), 4, 4, [0, 1, 2, 3]) == 0
+    v, _, _ = t.classify(frames.reshape(-1), n, 64)
+    assert (v["uniqid"] == uniq).all()
+    assert (v["hash"][hit] == hashes[hit]).all()
+    assert (v["thread"][hit] == hashes[hit] % 4).all()
+    assert ((v["action"][~hit] & 0x3F) == g.ACT_DROP_UNREG).all()
+
+
+def test_struct_frames_fixture_regenerates(ref, orc):
+    """With the reference mounted, make_struct_frames.py's recipe reproduces
+    the committed fixture exactly."""
+    import types
+    from tests.rxcases import load_struct_frames, ref_struct_batch
+    rj = orc.ref_jhash()
+    if rj is None:
+        pytest.skip("oracle/_ref/libjhash_ref.so not built")
+    refj = types.SimpleNamespace(jhash=lambda b: int(rj.jenkins_hash(b, len(b))))
+    ips, frames, want = ref_struct_batch(ref, refj, np.random.default_rng(17), 3000, 64)
+    f_ips, f_frames, f_uniq, f_hash, f_hit = load_struct_frames()
+    assert (np.array(ips, dtype=np.uint32) == f_ips).all()
+    assert (frames == f_frames).all()
+    assert [w[0] for w in want] == f_uniq.tolist()
+    assert [w[1] for w in want] == f_hash.tolist()
