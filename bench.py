@@ -150,6 +150,13 @@ def hip_copy(dst, src, nbytes):
 # r02_bench_spread_settle.jsonl, gpurun_out/r02c, r02g)
 PLACEMENT_SLACK = {2: 1.07, 4: 1.10, 8: 1.10}
 PLACEMENT_TRIES = 3
+# the slack above was calibrated on 16-runtime udp64 pairs only; with 1024
+# runtimes the kernel's time is not predicted by the probe's read+write
+# shape (the header-split pool ran 96 us against an 81-83 us probe on every
+# placement, BENCH_r02.json), so those pools keep the probe's choice and the
+# kernel check is recorded as skipped instead of re-placing them
+PLACEMENT_CHECK_RUNTIMES = (16,)
+PROBE_READ_CAP = 4 << 30  # gcl_dev_alloc_paired's probe reads at most this much
 
 
 class Workload:
@@ -186,7 +193,11 @@ class Workload:
         self.tables = setup_tables(self.clf, R, T)
         torch.cuda.synchronize()
         if getattr(self, "paired", False) and stride == HDR_BYTES:
-            self.check_placement()
+            if R in PLACEMENT_CHECK_RUNTIMES:
+                self.check_placement()
+            else:
+                self.placement_checks.append({"skipped": f"kernel check calibrated for {PLACEMENT_CHECK_RUNTIMES} "
+                                                         f"runtimes only; {R} here: the probe's choice is kept"})
 
     def _new_pool(self):
         buf = g.DeviceBuffer(self.n * self.stride, self.device.index or 0,
@@ -227,12 +238,19 @@ class Workload:
         (iokernel/rx.c:398-415)."""
         for k in range(tries + 1):
             info = self.frames.pair_info
-            scale = self.n * self.stride / min(self.n * self.stride, 4 << 30)
+            # the probe read min(pool, 4 GiB) and wrote probe_write_bytes of
+            # the ring: scale its time to the kernel's whole read + write
+            rd, wr = self.n * self.stride, self.n * self.vbytes
+            probed = min(rd, PROBE_READ_CAP) + max(1, min(wr, info["probe_write_bytes"] or wr))
+            scale = (rd + wr) / probed
             us = self.kernel_us()
-            ok = us <= info["probe_us_chosen"] * scale * PLACEMENT_SLACK[self.vbytes]
+            limit = info["probe_us_chosen"] * scale * PLACEMENT_SLACK[self.vbytes]
+            ok = us <= limit
             self.placement_checks.append({"kernel_us": round(us, 2), "probe_us_chosen":
-                                          info["probe_us_chosen"], "classes_seen": info["classes_seen"],
-                                          "kept": ok or k == tries})
+                                          info["probe_us_chosen"], "limit_us": round(limit, 2),
+                                          "classes_seen": info["classes_seen"], "passed": ok,
+                                          **({"kept": True} if ok else
+                                             {"kept_failed": True} if k == tries else {})})
             if ok or k == tries:
                 return
             old = self.frames
@@ -492,7 +510,8 @@ def placement(w):
             **info,
             "class_chosen": ("fast (cross-class pair: both classes seen)" if info["classes_seen"] == 2
                              else "unknown (one class in every candidate)"),
-            "kernel_checks": checks, "replaced": max(0, len(checks) - 1)}
+            "kernel_checks": checks, "replaced": sum(1 for c in checks if c.get("passed") is False
+                                                     and not c.get("kept_failed"))}
 
 
 def e2e_bench(device, vbytes=VERDICT_BYTES, reps=3):
@@ -598,7 +617,12 @@ def rxpipe_bench():
     if not os.access(exe, os.X_OK):
         return {"skipped": "tools/rxpipe not built (python -c 'import __graft_entry__ as g; g.build()')"}
     rows = []
-    for cfg in (("64", "1", "1", "20000"), ("64", "4", "8", "20000"), ("256", "4", "8", "10000"),
+    # burst 64 is the reference's own (IOKERNEL_RX_BURST_SIZE, defs.h:75):
+    # throughput there is workers / round trip, so it is run at 1, 4, 8 and
+    # 16 workers; verdicts are read in place in the slot (gcl_rxloop_peek),
+    # and once copied out (the round-2 form) for comparison
+    for cfg in (("64", "1", "1", "20000"), ("64", "4", "8", "20000"), ("64", "4", "8", "20000", "copy"),
+                ("64", "8", "16", "40000"), ("64", "16", "32", "40000"), ("256", "4", "8", "10000"),
                 ("1024", "8", "16", "4000"), ("4096", "16", "16", "1000")):
         try:
             r = subprocess.run([exe, *cfg], capture_output=True, text=True, timeout=120)

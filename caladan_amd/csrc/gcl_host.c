@@ -358,7 +358,7 @@ deliver_compact(struct gcl_host_proc *const *clients_by_id, uint32_t max_runtime
                 const struct gcl_verdict4 *v4, const uint16_t *v2, uint8_t thread_bits,
                 const uint32_t *bcast_hash, const uint16_t *pkt_len, const uint8_t *olflags,
                 uint8_t default_olflags, const uint64_t *shmptr, uint64_t n,
-                const struct gcl_host_ops *ops, uint64_t *stats)
+                const struct gcl_host_ops *ops, uint64_t *stats, size_t vstride)
 {
 	const uint64_t csum_def = (default_olflags & GCL_F_IP_CKSUM_MASK) == GCL_F_IP_CKSUM_GOOD;
 	void (*const enable_poll)(void *, struct gcl_host_proc *, unsigned int) =
@@ -373,13 +373,18 @@ deliver_compact(struct gcl_host_proc *const *clients_by_id, uint32_t max_runtime
 		uint32_t uniqid, thread;
 		bool fast;
 
+		/* verdict i sits @vstride bytes after verdict i - 1: packed
+		 * arrays, or the rx loop's 16-B records read in place */
+		const uint16_t *v2i = v2 ? (const uint16_t *)((const char *)v2 + i * vstride) : NULL;
+		const struct gcl_verdict4 *v4i =
+			v4 ? (const struct gcl_verdict4 *)((const char *)v4 + i * vstride) : NULL;
 		if (v2) {
-			const uint16_t x = v2[i];
+			const uint16_t x = *v2i;
 			uniqid = (x & GCL_V2_Q_MASK) >> thread_bits;
 			thread = x & tmask;
 			fast = (x & GCL_V2_KIND) == GCL_V2_DELIVER;
 		} else {
-			const struct gcl_verdict4 x = v4[i];
+			const struct gcl_verdict4 x = *v4i;
 			uniqid = x.uniqid;
 			thread = x.thread;
 			fast = (x.action & GCL_ACT_MASK) == GCL_ACT_DELIVER;
@@ -387,7 +392,7 @@ deliver_compact(struct gcl_host_proc *const *clients_by_id, uint32_t max_runtime
 		if (!fast || uniqid >= max_runtimes || !(p = clients_by_id[uniqid]) ||
 		    thread >= p->thread_count || !(chan = p->rxq[thread]) ||
 		    chan->send_head - chan->send_tail >= chan->size) {
-			const struct gcl_verdict4 w = v2 ? gcl_verdict2_to4(v2[i], thread_bits) : v4[i];
+			const struct gcl_verdict4 w = v2 ? gcl_verdict2_to4(*v2i, thread_bits) : *v4i;
 			delivered += deliver(clients_by_id, max_runtimes, clients, nr_clients, NULL, &w,
 			                     bcast_hash ? bcast_hash + i : NULL, pkt_len ? pkt_len + i : NULL,
 			                     olflags ? olflags + i : NULL, default_olflags,
@@ -419,7 +424,8 @@ uint64_t gcl_host_deliver4(struct gcl_host_proc *const *clients_by_id, uint32_t 
                            const struct gcl_host_ops *ops, uint64_t *stats)
 {
 	return deliver_compact(clients_by_id, max_runtimes, clients, nr_clients, v, NULL, 0,
-	                       bcast_hash, pkt_len, olflags, default_olflags, shmptr, n, ops, stats);
+	                       bcast_hash, pkt_len, olflags, default_olflags, shmptr, n, ops, stats,
+	                       sizeof(*v));
 }
 
 uint64_t gcl_host_deliver2(struct gcl_host_proc *const *clients_by_id, uint32_t max_runtimes,
@@ -433,5 +439,40 @@ uint64_t gcl_host_deliver2(struct gcl_host_proc *const *clients_by_id, uint32_t 
 		return 0;
 	return deliver_compact(clients_by_id, max_runtimes, clients, nr_clients, NULL, v,
 	                       thread_bits, bcast_hash, pkt_len, olflags, default_olflags, shmptr,
-	                       n, ops, stats);
+	                       n, ops, stats, sizeof(*v));
+}
+
+uint64_t gcl_host_deliver_recs(struct gcl_host_proc *const *clients_by_id, uint32_t max_runtimes,
+                               struct gcl_host_proc *const *clients, int nr_clients,
+                               const struct gcl_loop_rec *recs, uint8_t vbytes,
+                               uint8_t thread_bits, const uint32_t *bcast_hash,
+                               const uint16_t *pkt_len, const uint8_t *olflags,
+                               uint8_t default_olflags, const uint64_t *shmptr, uint64_t n,
+                               const struct gcl_host_ops *ops, uint64_t *stats)
+{
+	uint64_t delivered = 0;
+
+	if (!recs || thread_bits > 8)
+		return 0;
+	if (vbytes == 4)
+		return deliver_compact(clients_by_id, max_runtimes, clients, nr_clients,
+		                       (const struct gcl_verdict4 *)&recs[0].verdict, NULL, 0, bcast_hash,
+		                       pkt_len, olflags, default_olflags, shmptr, n, ops, stats,
+		                       sizeof(*recs));
+	if (vbytes == 2)
+		return deliver_compact(clients_by_id, max_runtimes, clients, nr_clients, NULL,
+		                       (const uint16_t *)&recs[0].verdict, thread_bits, bcast_hash,
+		                       pkt_len, olflags, default_olflags, shmptr, n, ops, stats,
+		                       sizeof(*recs));
+	if (vbytes != 8)
+		return 0;
+	/* 8-byte contexts: a record's first 8 bytes are the struct gcl_verdict */
+	for (uint64_t i = 0; i < n; i++) {
+		struct gcl_verdict v;
+		memcpy(&v, &recs[i], sizeof(v));
+		delivered += deliver(clients_by_id, max_runtimes, clients, nr_clients, &v, NULL, NULL,
+		                     pkt_len ? pkt_len + i : NULL, olflags ? olflags + i : NULL,
+		                     default_olflags, shmptr ? shmptr + i : NULL, 1, ops, i, stats);
+	}
+	return delivered;
 }

@@ -1146,7 +1146,7 @@ struct LoopRec {
 	uint32_t hash, vlo;
 	uint64_t ticket;
 };
-static_assert(sizeof(LoopRec) == 16, "LoopRec");
+static_assert(sizeof(LoopRec) == 16 && sizeof(LoopRec) == sizeof(gcl_loop_rec), "LoopRec");
 __host__ __device__ constexpr uint64_t loop_word(uint64_t t, uint32_t n, uint32_t fl, uint32_t img,
                                                  uint32_t iseq)
 {
@@ -3129,15 +3129,9 @@ extern "C" int64_t gcl_rxloop_submit(struct gcl_rxloop *L, uint32_t n, const uin
 	return (int64_t)t;
 }
 
-extern "C" int gcl_rxloop_wait(struct gcl_rxloop *L, int64_t ticket, void *verdicts_out,
-                               uint64_t spin_ns)
+/* spin up to @spin_ns for ticket @t's burst: 0, -EAGAIN or -ESHUTDOWN */
+static int loop_await(gcl_rxloop *L, uint64_t t, uint64_t spin_ns)
 {
-	if (!L || ticket < 1 || (uint64_t)ticket > L->next)
-		return -EINVAL;
-	const uint64_t t = (uint64_t)ticket;
-	if (t + L->lp.nslots <= L->next)
-		return -ESTALE;
-	LoopSlotHdr *h = loop_slot(L, t);
 	const uint64_t t0 = spin_ns ? now_ns() : 0;
 	uint32_t k = 0;
 	while (!burst_complete(L, t)) {
@@ -3149,6 +3143,51 @@ extern "C" int gcl_rxloop_wait(struct gcl_rxloop *L, int64_t ticket, void *verdi
 		}
 		__builtin_ia32_pause();
 	}
+	return 0;
+}
+
+extern "C" int gcl_rxloop_peek(struct gcl_rxloop *L, int64_t ticket, uint64_t spin_ns,
+                               const struct gcl_loop_rec **recs, uint32_t *n)
+{
+	if (!L || !recs || !n || ticket < 1 || (uint64_t)ticket > L->next)
+		return -EINVAL;
+	const uint64_t t = (uint64_t)ticket;
+	if (t + L->lp.nslots <= L->next)
+		return -ESTALE;
+	const int r = loop_await(L, t, spin_ns);
+	if (r)
+		return r;
+	LoopSlotHdr *h = loop_slot(L, t);
+	*n = (uint32_t)(h->word >> 11) & 0x1FFF;
+	*recs = (const struct gcl_loop_rec *)loop_recs(L, h);
+	return 0;
+}
+
+extern "C" int gcl_rxloop_release(struct gcl_rxloop *L, int64_t ticket)
+{
+	if (!L || ticket < 1 || (uint64_t)ticket > L->next)
+		return -EINVAL;
+	const uint64_t t = (uint64_t)ticket;
+	if (t + L->lp.nslots <= L->next)
+		return -ESTALE;
+	uint64_t &r = L->retired[(t - 1) % L->lp.nslots];
+	if (r < t)
+		r = t;
+	return 0;
+}
+
+extern "C" int gcl_rxloop_wait(struct gcl_rxloop *L, int64_t ticket, void *verdicts_out,
+                               uint64_t spin_ns)
+{
+	if (!L || ticket < 1 || (uint64_t)ticket > L->next)
+		return -EINVAL;
+	const uint64_t t = (uint64_t)ticket;
+	if (t + L->lp.nslots <= L->next)
+		return -ESTALE;
+	LoopSlotHdr *h = loop_slot(L, t);
+	const int aw = loop_await(L, t, spin_ns);
+	if (aw)
+		return aw;
 	if (verdicts_out) {
 		const uint32_t n = (uint32_t)(h->word >> 11) & 0x1FFF;
 		const LoopRec *r = loop_recs(L, h);

@@ -58,6 +58,8 @@ VERDICT_DTYPE = np.dtype([("hash", "<u4"), ("uniqid", "<u2"), ("thread", "u1"), 
 # GCL_CFG_VERDICT4: WAKE verdicts carry the flow_tbl slot (hash % thread_count) in `thread`
 VERDICT4_DTYPE = np.dtype([("uniqid", "<u2"), ("thread", "u1"), ("action", "u1")])
 TRANS_DTYPE = np.dtype([("h5", "<u4"), ("h3", "<u4")])
+# struct gcl_loop_rec: one persistent-loop verdict record (gcl_rxloop_peek)
+LOOP_REC_DTYPE = np.dtype([("hash", "<u4"), ("verdict", "<u4"), ("ticket", "<u8")])
 
 
 class GclCfg(ctypes.Structure):
@@ -217,6 +219,10 @@ def _load():
         "gcl_host_deliver2": (u64, [vp, u32, vp, i32, vp, ctypes.c_uint8, vp, vp, vp,
                                     ctypes.c_uint8, vp, u64, ctypes.POINTER(GclHostOps), vp]),
         "gcl_verdict2_to4": (ctypes.c_uint32, [ctypes.c_uint16, ctypes.c_uint8]),
+        "gcl_host_deliver_recs": (u64, [vp, u32, vp, i32, vp, ctypes.c_uint8, ctypes.c_uint8, vp, vp,
+                                        vp, ctypes.c_uint8, vp, u64, ctypes.POINTER(GclHostOps), vp]),
+        "gcl_rxloop_peek": (i32, [vp, ctypes.c_int64, u64, ctypes.POINTER(vp), ctypes.POINTER(u32)]),
+        "gcl_rxloop_release": (i32, [vp, ctypes.c_int64]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -762,6 +768,20 @@ class RxLoop:
         if ret:
             raise OSError(-ret, f"gcl_rxloop_wait: {os.strerror(-ret)}")
         return out
+
+    def peek(self, ticket, spin_ns=2_000_000_000):
+        """The burst's verdict records in place in the ring slot (a numpy
+        view of LOOP_REC_DTYPE, valid until release(ticket))."""
+        p = ctypes.c_void_p()
+        n = ctypes.c_uint32()
+        ret = lib.gcl_rxloop_peek(self._h, ticket, spin_ns, ctypes.byref(p), ctypes.byref(n))
+        if ret:
+            raise OSError(-ret, f"gcl_rxloop_peek: {os.strerror(-ret)}")
+        buf = (ctypes.c_uint8 * (16 * n.value)).from_address(p.value)
+        return np.frombuffer(buf, dtype=LOOP_REC_DTYPE)
+
+    def release(self, ticket):
+        return _check(lib.gcl_rxloop_release(self._h, ticket), "gcl_rxloop_release")
 
     def drive(self, offs, iters, depth=1):
         offs = np.ascontiguousarray(offs, dtype=np.uint64)

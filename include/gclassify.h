@@ -519,6 +519,24 @@ int64_t gcl_rxloop_submit(struct gcl_rxloop *loop, uint32_t n, const uint64_t *o
                           const uint8_t *olflags, const uint32_t *rss, const uint32_t *fdir_hi,
                           const uint32_t *dst_hint);
 int gcl_rxloop_wait(struct gcl_rxloop *loop, int64_t ticket, void *verdicts_out, uint64_t spin_ns);
+/*
+ * gcl_rxloop_peek - gcl_rxloop_wait without the copy: on 0, *@recs points at
+ * the burst's @*n verdict records in the ring slot itself (one 16-B record per
+ * packet, written by the kernel with one store; @verdict holds the verdict in
+ * the context's width -- gcl_verdict4 bytes, the 2-byte queue verdict in the
+ * low half, or with 8-byte verdicts {hash, verdict} is the struct gcl_verdict).
+ * The records stay valid, and the slot is not reused, until
+ * gcl_rxloop_release(@ticket): the post-pass (gcl_host_deliver_recs) reads
+ * them in place.  Errors as gcl_rxloop_wait.
+ */
+struct gcl_loop_rec {
+	uint32_t hash;
+	uint32_t verdict;
+	uint64_t ticket;
+};
+int gcl_rxloop_peek(struct gcl_rxloop *loop, int64_t ticket, uint64_t spin_ns,
+                    const struct gcl_loop_rec **recs, uint32_t *n);
+int gcl_rxloop_release(struct gcl_rxloop *loop, int64_t ticket);
 int gcl_rxloop_stop(struct gcl_rxloop *loop);
 int gcl_rxloop_drive(struct gcl_rxloop *loop, uint32_t n, const uint64_t *offs, uint32_t iters,
                      uint32_t depth, uint64_t *lat_ns, uint64_t *elapsed_ns);

@@ -706,8 +706,13 @@ static int lrpc_send(struct orc_lrpc *c, uint64_t cmd, uint64_t payload)
 {
 	uint64_t *dst;
 
-	if (c->send_head - c->send_tail >= c->size)
-		return 0; /* ring full: RX_UNICAST_FAIL */
+	if (c->send_head - c->send_tail >= c->size) {
+		/* __lrpc_send's refresh from recv_head_wb (base/lrpc.c:16-19):
+		 * the emulated runtime consumes instantly, so its head is ours */
+		c->send_tail = c->send_head;
+		if (c->send_head - c->send_tail >= c->size)
+			return 0; /* ring full: RX_UNICAST_FAIL */
+	}
 	dst = &c->tbl[2 * (c->send_head & (c->size - 1))];
 	cmd |= (c->send_head++ & c->size) ? 0 : (1ull << 63);
 	dst[1] = payload;
@@ -766,14 +771,8 @@ static void classify_range_lrpc(const struct orc_tables *t, const struct gcl_bat
 				}
 			}
 		}
-		/* the runtimes drain their rings between bursts */
-		for (uint64_t i = 0; i < nb; i++) {
-			struct gcl_verdict *vk = &v[s + i - lo];
-			if ((vk->action & GCL_ACT_MASK) == GCL_ACT_DELIVER) {
-				struct orc_lrpc *r = ring_of(rs, vk->uniqid, vk->thread);
-				r->send_tail = r->send_head;
-			}
-		}
+		/* the runtimes drain their rings: seen lazily, when a ring looks
+		 * full (lrpc_send), as the GPU pipeline's rings (tools/rxpipe.cpp) */
 	}
 }
 

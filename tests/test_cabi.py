@@ -301,6 +301,17 @@ def test_host_deliver4_matches_deliver(g, orc):
     shm = offs.astype(np.uint64)
     bhash = rss.astype(np.uint32)  # NIC mode: the hash is hash.rss whatever the flags
 
+    def recs(vb):
+        """the rx loop's 16-B records (struct gcl_loop_rec) of these verdicts"""
+        r = np.zeros(n, dtype=g.LOOP_REC_DTYPE)
+        r["ticket"] = 7
+        if vb == 8:
+            r["hash"], r["verdict"] = v.view(np.uint64) & 0xFFFFFFFF, v.view(np.uint64) >> 32
+        else:
+            r["hash"] = 0xDEADBEEF  # unused in the compact forms
+            r["verdict"] = v4.view(np.uint32) if vb == 4 else v2.astype(np.uint32)
+        return r
+
     def run(compact):
         procs, rings, keep = _host_procs(g, rts, 8)
         by_id = (ctypes.c_void_p * R)()
@@ -343,7 +354,14 @@ def test_host_deliver4_matches_deliver(g, orc):
         ops.sched_add_core, ops.free_pkt, ops.refcnt_update = add_core, free_pkt, refcnt
         ops.owned, ops.enable_poll, ops.arp_respond = owned, poll, arp
         stats = np.zeros(8, dtype=np.uint64)
-        if compact == 2:
+        if isinstance(compact, str):  # "recs<vb>": the records read in place
+            vb = int(compact[4:])
+            rr = recs(vb)
+            d = g.lib.gcl_host_deliver_recs(by_id, R, clients, len(procs), rr.ctypes.data, vb, 3,
+                                            bhash.ctypes.data if vb != 8 else None,
+                                            pkt_len.ctypes.data, olf.ctypes.data, 0x09,
+                                            shm.ctypes.data, n, ctypes.byref(ops), stats.ctypes.data)
+        elif compact == 2:
             d = g.lib.gcl_host_deliver2(by_id, R, clients, len(procs), v2.ctypes.data, 3,
                                         bhash.ctypes.data, pkt_len.ctypes.data, olf.ctypes.data,
                                         0x09, shm.ctypes.data, n, ctypes.byref(ops),
@@ -364,6 +382,8 @@ def test_host_deliver4_matches_deliver(g, orc):
     assert full[0] > 0 and {"wake", "own", "poll", "free", "ref", "arp"} <= kinds, kinds
     assert full == compact
     assert full == compact2
+    for vb in (4, 2, 8):
+        assert full == run(f"recs{vb}"), vb
 
 
 @pytest.mark.parametrize("meta", ["all", "no_olflags", "none"])
@@ -401,7 +421,13 @@ def test_host_deliver4_fast_path(g, orc, meta):
             by_id[u] = ctypes.addressof(p)
         clients = (ctypes.c_void_p * len(procs))(*[ctypes.addressof(p) for p in procs.values()])
         stats = np.zeros(8, dtype=np.uint64)
-        if compact:
+        if compact == "recs":  # the fast path over 16-B loop records, in place
+            rr = np.zeros(n, dtype=g.LOOP_REC_DTYPE)
+            rr["verdict"] = v4.view(np.uint32)
+            d = g.lib.gcl_host_deliver_recs(by_id, R, clients, len(procs), rr.ctypes.data, 4, 0,
+                                            bhash.ctypes.data, pl, of, 0x09, sp, n, None,
+                                            stats.ctypes.data)
+        elif compact:
             d = g.lib.gcl_host_deliver4(by_id, R, clients, len(procs), v4.ctypes.data,
                                         bhash.ctypes.data, pl, of, 0x09, sp, n, None,
                                         stats.ctypes.data)
@@ -413,6 +439,7 @@ def test_host_deliver4_fast_path(g, orc, meta):
     full, compact = run(False), run(True)
     assert full[0] > 0 and full[1][1] > 0  # deliveries and ring-full failures both happen
     assert full == compact
+    assert full == run("recs")
 
 
 def test_dev_alloc_paired_rejects_bad_args(g):

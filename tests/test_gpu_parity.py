@@ -523,6 +523,51 @@ def test_gpu_full_size_tcp1500_properties(g, orc):
     assert_same(vv[sample], ve, "tcp1500 sample")
 
 
+@pytest.mark.parametrize("name", ["udp64", "tcp1500", "tcp1500_hsplit"])
+def test_gpu_full_size_bench_format(g, orc, name):
+    """The bench lines' own instances at full size, in exactly the format and
+    allocation they time: bench.Workload (frame pool placed against the
+    verdict ring by gcl_dev_alloc_paired, 2-byte queue verdicts with
+    thread_bits 3 for 16 x 8 and 2 for 1024 x 4, the bench's seeded tables)
+    stepped once.  Every verdict is a DELIVER to a queue of a registered
+    runtime, the queue histogram equals the device counts, and a
+    65536-packet random sample decodes (to_verdict2) to the oracle's
+    verdicts bit for bit."""
+    import bench
+    from tests.rxcases import to_verdict2
+    dev = torch.device("cuda", 0)
+    w = bench.Workload(name, 0, 1, dev, vbytes=2)
+    assert w.vbytes == 2 and w.clf.vbytes == 2
+    tb = w.clf.thread_bits
+    assert tb == {16: 3, 1024: 2}[w.R]
+    w.step(torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    n, R = w.n, w.R
+    hv = torch.empty(n * 2, dtype=torch.uint8).pin_memory()
+    bench.hip_copy(hv, w.verdicts, n * 2)
+    q = hv.numpy().view(np.uint16)
+    cc = w.counts[:R].cpu().numpy()
+    ss = w.counts[R:].cpu().numpy()
+    assert cc.sum() == n and ss[g.RX_PULLED] == n and ss[g.RX_UNHANDLED] == 0
+    assert ((q & g.V2_KIND) == g.V2_DELIVER).all()
+    assert (np.bincount(q >> tb, minlength=R)[:R] == cc).all()
+    # the sample: the same bytes from the CPU generator, classified by the oracle
+    t = orc.Tables(R, 1, 0, 0x09)
+    for (r, ip, T, act, fl) in w.tables:
+        assert t.runtime_set(r, ip, T, act, fl) == 0
+    rng = np.random.default_rng(21)
+    sample = np.sort(rng.choice(n, size=65536, replace=False))
+    fr_dev = torch.empty(n * w.stride, dtype=torch.uint8, device=dev)
+    bench.hip_copy(fr_dev, w.frames, n * w.stride)
+    fr = fr_dev.view(n, w.stride)[torch.from_numpy(sample).cuda(), :64].cpu().numpy().reshape(-1)
+    del fr_dev
+    ve, _, _ = t.classify(fr, len(sample), 64)
+    want = to_verdict2(ve, {r: T for (r, _, T, _, _) in w.tables}, tb)
+    assert_same(q[sample], want, f"{name} 2-B sample")
+    del w
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("wl,stride,R,T,arrays", [(0, 64, 16, 8, False), (1, 1536, 1024, 4, False),
                                                    (2, 9216, 16, 8, True)])

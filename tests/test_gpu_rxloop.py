@@ -70,10 +70,23 @@ def test_rxloop_fuzz_vs_oracle(g, orc, mode, vb, flags, inline):
                       flags=g.LOOP_INLINE_HDRS if inline else 0)
     try:
         got = []
-        for a, b in bursts(n):
+        for k, (a, b) in enumerate(bursts(n)):
             tk = loop.submit(offs[a:b], olf[a:b], rss[a:b], fdir[a:b], hint[a:b])
             assert tk > 0
-            got.append(loop.wait(tk, b - a))
+            if k % 2 == 0:
+                got.append(loop.wait(tk, b - a))
+                continue
+            # every other burst read in place (gcl_rxloop_peek) and released
+            rec = loop.peek(tk)
+            assert len(rec) == b - a and (rec["ticket"] == tk).all()
+            if vb == 8:
+                x = (rec["verdict"].astype(np.uint64) << np.uint64(32)) | rec["hash"].astype(np.uint64)
+                got.append(x.view(g.VERDICT_DTYPE))
+            elif vb == 4:
+                got.append(rec["verdict"].copy().view(g.VERDICT4_DTYPE))
+            else:
+                got.append(rec["verdict"].astype(np.uint16))
+            loop.release(tk)
         got = np.concatenate(got)
     finally:
         loop.stop()
@@ -146,6 +159,11 @@ def test_rxloop_workers_pipelined_and_full_ring(g, orc):
         tks = [loop.submit(offs[a:b], olf[a:b]) for a, b in bs[:8]]
         assert all(x > 0 for x in tks)
         assert loop.submit(offs[:64], olf[:64]) == -11  # -EAGAIN
+        # a peeked burst holds its slot until released
+        rec = loop.peek(tks[0])
+        assert (rec["verdict"].copy().view(g.VERDICT4_DTYPE) == w[:64]).all()
+        assert loop.submit(offs[:64], olf[:64]) == -11
+        assert g.lib.gcl_rxloop_release(loop._h, tks[-1] + 5) == -22
         got = [loop.wait(tk, 64) for tk in tks]
         for a, b in bs[8:]:
             tk = loop.submit(offs[a:b], olf[a:b])

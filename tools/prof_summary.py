@@ -94,6 +94,49 @@ def request_bytes(base, tag, wl):
             "hbm_write_bytes_from_requests": wbytes, "hbm_bytes_from_requests": rbytes + wbytes}
 
 
+TIMED_DEFAULT = 20  # tools/profile.sh's trace pass: --steps 20 / 20 ingress reps
+
+
+def timed_dispatches(tdir, wl, tag, bench_json):
+    """Average only the TIMED dispatches of the workload's kernel: the last K
+    of the trace pass, K = the bench line's `steps` (its timed steps come
+    last: placement checks, warmup and settle launch the same kernel before
+    them, and --no-group keeps anything after them out of the pass).  The
+    whole-run average of run_kernel_stats.csv mixes in the ramp (the first
+    ~40 launches run up to 19 % slower), so this is the figure
+    the bench line's roofline is checked against."""
+    path = os.path.join(tdir, "run_kernel_trace.csv")
+    if not os.path.exists(path):
+        return None
+    line = {}
+    if bench_json and os.path.exists(bench_json):
+        with open(bench_json) as f:
+            txt = [ln for ln in f.read().splitlines() if ln.startswith("{")]
+        line = json.loads(txt[-1]) if txt else {}
+    k = int(line.get("steps", TIMED_DEFAULT))
+    ds = sorted((r for r in rows(path) if is_kernel(wl, r["Kernel_Name"])),
+                key=lambda r: int(r["Start_Timestamp"]))
+    kept = ds[-k:]
+    durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in kept]
+    avg = sum(durs) / len(durs)
+    out = {"workload": wl, "tag": tag, "kernel": kept[0]["Kernel_Name"],
+           "dispatches_in_trace": len(ds), "timed_kept": len(kept),
+           "kept_dispatch_ids": [int(r["Dispatch_Id"]) for r in kept],
+           "kept_positions": [len(ds) - len(kept), len(ds) - 1],
+           "avg_ns": round(avg, 1), "min_ns": min(durs), "max_ns": max(durs),
+           "whole_trace_avg_ns": round(sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+                                           for r in ds) / len(ds), 1)}
+    rl = line.get("roofline") or {}
+    if wl in ("udp64", "tcp1500") and rl.get("bytes_per_pkt"):
+        algo = line["config"]["pkts_per_gpu"] * rl["bytes_per_pkt"]
+        frac = algo / (avg * 1e-9) / 1e9 / rl["peak"]
+        out.update({"algorithmic_bytes_per_launch": algo, "frac_from_timed_dispatches": round(frac, 4),
+                    "bench_line_under_rocprof": {"frac": rl.get("frac"), "kernel_ms": rl.get("kernel_ms"),
+                                                 "ms_per_step": line.get("ms_per_step")},
+                    "frac_rel_diff": round(frac / rl["frac"] - 1, 4) if rl.get("frac") else None})
+    return out
+
+
 def main(rnd):
     base = os.path.join(ROOT, "gpurun_out", f"prof_{rnd}")
     prof = os.path.join(ROOT, "profiles")
@@ -109,6 +152,13 @@ def main(rnd):
             continue
         shutil.copy(os.path.join(tdir, "run_kernel_stats.csv"),
                     os.path.join(prof, f"{rnd}_{tag}_kernel_stats.csv"))
+        td = timed_dispatches(tdir, wl, tag, os.path.join(base, f"{tag}_bench.json"))
+        if td:
+            with open(os.path.join(prof, f"{rnd}_{tag}_timed.json"), "w") as f:
+                json.dump(td, f, indent=1)
+            print(json.dumps({k: v for k, v in td.items() if k != "kept_dispatch_ids"}))
+        if not os.path.isdir(os.path.join(base, f"{tag}_FETCH_SIZE")):
+            continue
         st = [r for r in rows(os.path.join(tdir, "run_kernel_stats.csv")) if is_kernel(wl, r["Name"])]
         pm = {}
         for c in ("FETCH_SIZE", "WRITE_SIZE"):

@@ -6,11 +6,17 @@
 // sustains with the GPU classifying, to set beside the reference's own
 // classify + lrpc_send rate on one core (bench.py cpu_baseline.lrpc_1core_mpps).
 //
-//   rxpipe <burst> <workers> <depth> <bursts>    -> one JSON line
+//   rxpipe <burst> <workers> <depth> <bursts> [copy]   -> one JSON line
 //
-// Runtime consumers are emulated as infinitely fast (each ring's consumer
-// position is set to its producer position after every burst), as in the CPU
-// baseline's lrpc variant.
+// Each burst's verdicts are read in place in the loop's ring slot
+// (gcl_rxloop_peek + gcl_host_deliver_recs, then gcl_rxloop_release); with
+// the fifth argument `copy` they are copied out first (gcl_rxloop_wait +
+// gcl_host_deliver4), the round-2 form.
+// Runtime consumers are emulated as infinitely fast and are never touched by
+// the dataplane loop: each ring's recv_head_wb points at its own send_head,
+// so when a ring looks full the producer's refresh (__lrpc_send,
+// base/lrpc.c:16-19) finds it drained -- the reference's own path, taken
+// once per 4096 messages per ring, as in the CPU baseline's lrpc variant.
 // Build: hipcc --offload-arch=gfx950 -O2 -Iinclude -o tools/rxpipe tools/rxpipe.cpp \
 //          -Lcaladan_amd -lgclassify -Wl,-rpath,'$ORIGIN/../caladan_amd'
 #include <hip/hip_runtime.h>
@@ -41,6 +47,7 @@ int main(int argc, char **argv)
 	const uint32_t workers = argc > 2 ? (uint32_t)atoi(argv[2]) : 1;
 	const uint32_t depth = argc > 3 ? (uint32_t)atoi(argv[3]) : 1;
 	const uint32_t nbursts = argc > 4 ? (uint32_t)atoi(argv[4]) : 20000;
+	const bool copy_out = argc > 5 && !strcmp(argv[5], "copy");
 	const uint32_t R = 16, T = 8, RING = 4096;
 	const uint64_t nframes = 1 << 16, stride = 64;
 	if (!burst || burst > 4096 || !workers || workers > 16 || !depth || depth > 64) {
@@ -79,7 +86,7 @@ int main(int argc, char **argv)
 	std::vector<gcl_host_proc *> by_id(R), clients(R);
 	std::vector<gcl_lrpc_chan_out> chans(R * T);
 	std::vector<gcl_lrpc_msg> msgs((size_t)R * T * RING);
-	std::vector<uint32_t> heads(R * T, 0);
+
 	for (uint32_t r = 0; r < R; r++) {
 		const uint16_t na = (uint16_t)(r % T + 1);
 		uint16_t act[GCL_NCPU];
@@ -93,8 +100,8 @@ int main(int argc, char **argv)
 		p.idle_top = -1;
 		gcl_steer_flows((uint16_t)T, act, na, p.flow_tbl);
 		for (uint32_t t = 0; t < T; t++) {
-			gcl_lrpc_init_out(&chans[r * T + t], &msgs[(size_t)(r * T + t) * RING], RING,
-			                  &heads[r * T + t]);
+			gcl_lrpc_chan_out *ch = &chans[r * T + t];
+			gcl_lrpc_init_out(ch, &msgs[(size_t)(r * T + t) * RING], RING, &ch->send_head);
 			p.rxq[t] = &chans[r * T + t];
 		}
 		by_id[r] = clients[r] = &p;
@@ -143,19 +150,35 @@ int main(int argc, char **argv)
 				tk[head % depth] = r;
 				head++;
 			}
-			const int w = gcl_rxloop_wait(loop, tk[tail % depth], v.data(), 1000000000ull);
-			if (w) {
-				fprintf(stderr, "wait: %d\n", w);
-				exit(1);
-			}
 			const uint32_t b = (uint32_t)((seq + tail) % nb);
-			const uint64_t d0 = now_ns();
-			delivered += gcl_host_deliver4(by_id.data(), R, clients.data(), (int)R, v.data(),
-			                               nullptr, len.data(), nullptr, cfg.default_olflags,
-			                               &offs[(size_t)b * burst], burst, nullptr, stats);
-			for (uint32_t i = 0; i < R * T; i++) /* the runtimes drained their rings */
-				heads[i] = chans[i].send_head;
-			const uint64_t d1 = now_ns();
+			const int64_t t = tk[tail % depth];
+			uint64_t d0, d1;
+			if (copy_out) {
+				const int w = gcl_rxloop_wait(loop, t, v.data(), 1000000000ull);
+				if (w) {
+					fprintf(stderr, "wait: %d\n", w);
+					exit(1);
+				}
+				d0 = now_ns();
+				delivered += gcl_host_deliver4(by_id.data(), R, clients.data(), (int)R, v.data(),
+				                               nullptr, len.data(), nullptr, cfg.default_olflags,
+				                               &offs[(size_t)b * burst], burst, nullptr, stats);
+				d1 = now_ns();
+			} else {
+				const gcl_loop_rec *recs;
+				uint32_t n = 0;
+				const int w = gcl_rxloop_peek(loop, t, 1000000000ull, &recs, &n);
+				if (w || n != burst) {
+					fprintf(stderr, "peek: %d (n %u)\n", w, n);
+					exit(1);
+				}
+				d0 = now_ns();
+				delivered += gcl_host_deliver_recs(by_id.data(), R, clients.data(), (int)R, recs, 4, 0,
+				                                   nullptr, len.data(), nullptr, cfg.default_olflags,
+				                                   &offs[(size_t)b * burst], burst, nullptr, stats);
+				d1 = now_ns();
+				gcl_rxloop_release(loop, t);
+			}
 			if (timed) {
 				t_deliver += d1 - d0;
 				lat.push_back(d1 - t_sub[tail % depth]);
@@ -172,10 +195,11 @@ int main(int argc, char **argv)
 	gcl_rxloop_stop(loop);
 	std::sort(lat.begin(), lat.end());
 	const double pkts = (double)burst * nbursts;
-	printf("{\"burst\": %u, \"workers\": %u, \"depth\": %u, \"bursts\": %u, \"mpps_one_core\": %.2f, "
+	printf("{\"burst\": %u, \"workers\": %u, \"depth\": %u, \"bursts\": %u, \"verdicts\": \"%s\", "
+	       "\"mpps_one_core\": %.2f, "
 	       "\"burst_latency_p50_us\": %.2f, \"burst_latency_p99_us\": %.2f, "
 	       "\"deliver_ns_per_pkt\": %.2f, \"delivered_check\": \"%s\", \"unicast_fail\": %llu}\n",
-	       burst, workers, depth, nbursts, pkts / (el * 1e-3), lat[lat.size() / 2] * 1e-3,
+	       burst, workers, depth, nbursts, copy_out ? "copied out" : "read in place", pkts / (el * 1e-3), lat[lat.size() / 2] * 1e-3,
 	       lat[lat.size() * 99 / 100] * 1e-3, t_deliver / pkts,
 	       delivered == (uint64_t)burst * (nbursts + warm) ? "ok" : "MISMATCH",
 	       (unsigned long long)stats[GCL_RX_UNICAST_FAIL]);
