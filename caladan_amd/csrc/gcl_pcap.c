@@ -21,8 +21,10 @@
 #define PCAP_MAGIC_US 0xA1B2C3D4u
 #define PCAP_MAGIC_NS 0xA1B23C4Du
 #define LINKTYPE_ETHERNET 1
-/* largest capture accepted: pkt_len is the u16 rte_pktmbuf_pkt_len, and the
- * largest frame the reference handles is ETH_MAX_LEN_JUMBO (inc/net/ethernet.h:18) */
+/* largest capture loaded: pkt_len is the u16 rte_pktmbuf_pkt_len, and the
+ * largest frame the reference handles is ETH_MAX_LEN_JUMBO (inc/net/ethernet.h:18).
+ * Longer records (captures on lo, MTU 65536, or of GRO/TSO super-frames with
+ * snaplen 262144) are skipped and counted in gcl_trace.skipped, not loaded. */
 #define PCAP_MAX_INCL 0xFFFFu
 
 struct pcap_file_hdr {
@@ -113,14 +115,19 @@ int gcl_pcap_load(const char *path, struct gcl_trace *t, uint64_t max_pkts)
 
 	/* pass 1: size the packed buffer; every record must lie inside the file
 	 * (fseek past EOF succeeds, so the bound is checked against its size) */
+	uint64_t skipped = 0;
 	while ((!max_pkts || n < max_pkts) && fread(&rh, sizeof(rh), 1, f) == 1) {
 		uint32_t incl = swap ? bswap32_(rh.incl_len) : rh.incl_len;
 		pos += sizeof(rh);
-		if (incl > PCAP_MAX_INCL || incl > fsize - pos || fseeko(f, incl, SEEK_CUR)) {
+		if (incl > fsize - pos || fseeko(f, incl, SEEK_CUR)) {
 			fclose(f);
 			return -EPROTO;
 		}
 		pos += incl;
+		if (incl > PCAP_MAX_INCL) { /* too long for a u16 pkt_len: skipped */
+			skipped++;
+			continue;
+		}
 		bytes += align_up(incl ? incl : 1, 16);
 		n++;
 	}
@@ -151,12 +158,19 @@ int gcl_pcap_load(const char *path, struct gcl_trace *t, uint64_t max_pkts)
 		return -EIO;
 	}
 	uint64_t off = 0;
-	for (uint64_t i = 0; i < n; i++) {
+	for (uint64_t i = 0; i < n;) {
 		if (fread(&rh, sizeof(rh), 1, f) != 1) {
 			ret = -EIO;
 			break;
 		}
 		uint32_t incl = swap ? bswap32_(rh.incl_len) : rh.incl_len;
+		if (incl > PCAP_MAX_INCL) { /* skipped in pass 1 too */
+			if (fseeko(f, incl, SEEK_CUR)) {
+				ret = -EIO;
+				break;
+			}
+			continue;
+		}
 		uint32_t orig = swap ? bswap32_(rh.orig_len) : rh.orig_len;
 		uint32_t sec = swap ? bswap32_(rh.ts_sec) : rh.ts_sec;
 		uint32_t frac = swap ? bswap32_(rh.ts_frac) : rh.ts_frac;
@@ -174,6 +188,7 @@ int gcl_pcap_load(const char *path, struct gcl_trace *t, uint64_t max_pkts)
 		t->orig_len[i] = orig;
 		t->ts_ns[i] = (uint64_t)sec * 1000000000ull + (ns ? frac : (uint64_t)frac * 1000ull);
 		off += sz;
+		i++;
 	}
 	fclose(f);
 	if (ret) {
@@ -181,6 +196,7 @@ int gcl_pcap_load(const char *path, struct gcl_trace *t, uint64_t max_pkts)
 		return ret;
 	}
 	t->n = n;
+	t->skipped = skipped;
 	t->frames_len = off + GCL_PCAP_TAIL_PAD;
 	return 0;
 }

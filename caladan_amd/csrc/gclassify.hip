@@ -2068,9 +2068,11 @@ static Geometry choose_geometry(const gcl_ctx *c, uint32_t tab_lds, uint32_t his
 	Geometry g;
 	g.depth = 1;
 	g.threads = 0;
-	/* GENERAL batches take the register-header kernel unless an experiment
-	 * knob asks for the tile kernel's own shapes (GCL_TUNE_QUAD=0, the tile
-	 * queue, depth 1, the membench body) */
+	/* GENERAL batches run on the LDS-tile classify_kernel by default
+	 * (kDefaultQuad 0).  The register-header classify_quad_kernel runs only
+	 * with GCL_TUNE_QUAD=1, and even then the tile kernel is kept when the
+	 * dynamic tile queue (GCL_TUNE_SCHED), depth 1 (GCL_TUNE_DEPTH=1) or the
+	 * membench body (GCL_TUNE_ABLATE bit 16) is asked for */
 	g.quad = general && c->tune_quad && !c->tune_sched && c->tune_depth != 1 &&
 	         !(c->tune_ablate & 16);
 	auto per_block = [&](uint32_t nt) -> uint32_t {

@@ -99,7 +99,7 @@ class GclTrace(ctypes.Structure):
     _fields_ = [("frames", ctypes.c_void_p), ("frames_len", ctypes.c_uint64),
                 ("alloc_len", ctypes.c_uint64), ("offs", ctypes.c_void_p),
                 ("pkt_len", ctypes.c_void_p), ("orig_len", ctypes.c_void_p),
-                ("ts_ns", ctypes.c_void_p), ("n", ctypes.c_uint64)]
+                ("ts_ns", ctypes.c_void_p), ("n", ctypes.c_uint64), ("skipped", ctypes.c_uint64)]
 
 
 class GclE2eOpts(ctypes.Structure):
@@ -362,6 +362,7 @@ class Trace:
         _check(lib.gcl_pcap_load(os.fsencode(path), ctypes.byref(self.t), max_pkts), "gcl_pcap_load")
         n = self.t.n
         self.n = n
+        self.skipped = self.t.skipped  # records longer than 65535 bytes, not loaded
 
         def view(ptr, ctype, count, dtype):
             if not count:

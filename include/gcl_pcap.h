@@ -23,16 +23,19 @@ struct gcl_trace {
 	uint32_t *orig_len;   /* u32[n] length on the wire */
 	uint64_t *ts_ns;      /* u64[n] capture time */
 	uint64_t  n;
+	uint64_t  skipped;    /* records not loaded: captures longer than 65535 bytes */
 };
 
 /*
  * gcl_pcap_load - read a classic pcap file (either byte order, micro- or
  * nanosecond timestamps, LINKTYPE_ETHERNET) into @t; at most @max_pkts
- * packets (0 = all).  Returns 0, -EPROTO (not an Ethernet pcap, a record
- * running past the end of the file, a cut-off record header, or a capture
- * longer than 65535 bytes -- pkt_len is a u16, and the largest frame the
- * reference handles is ETH_MAX_LEN_JUMBO), -EINVAL (not a regular file),
- * -ENOMEM, -EIO or -errno from fopen.
+ * packets (0 = all).  A record whose capture is longer than 65535 bytes
+ * (pkt_len is a u16, and the largest frame the reference handles is
+ * ETH_MAX_LEN_JUMBO; such records come from captures on lo or of GRO/TSO
+ * super-frames) is skipped and counted in @t->skipped.  Returns 0, -EPROTO
+ * (not an Ethernet pcap, a record running past the end of the file, or a
+ * cut-off record header), -EINVAL (not a regular file), -ENOMEM, -EIO or
+ * -errno from fopen.
  */
 int gcl_pcap_load(const char *path, struct gcl_trace *t, uint64_t max_pkts);
 void gcl_pcap_free(struct gcl_trace *t);

@@ -4,7 +4,7 @@
  * caladan_amd/build.py --sanitize (tests/test_sanitize.py runs it).
  *
  *   host_fuzz pcap FILE...        gcl_pcap_load each file; print its return
- *                                 code and packet count, and touch every
+ *                                 code, packet and skipped counts, and touch every
  *                                 captured byte it reports
  *   host_fuzz deliver SEED ITERS  random verdict streams (8-, 4- and 2-byte)
  *                                 through gcl_host_deliver{,4,2}: uniqids past
@@ -52,8 +52,8 @@ static int fuzz_pcap(int argc, char **argv)
 					sum += t.frames[t.offs[k] + b];
 			}
 		}
-		printf("%s %d %llu %llu\n", argv[i], r, (unsigned long long)(r ? 0 : t.n),
-		       (unsigned long long)sum);
+		printf("%s %d %llu %llu %llu\n", argv[i], r, (unsigned long long)(r ? 0 : t.n),
+		       (unsigned long long)(r ? 0 : t.skipped), (unsigned long long)sum);
 		if (r == 0)
 			gcl_pcap_free(&t);
 	}

@@ -65,6 +65,26 @@ def test_pcap_foreign_byte_order_and_usec(g, tmp_path):
         assert bytes(t.frames[o:o + len(fr)]) == fr
 
 
+def test_pcap_skips_oversized_records(g, tmp_path):
+    """Records longer than 65535 bytes (a capture on lo, or GRO/TSO
+    super-frames with snaplen 262144) are skipped and counted, the rest of
+    the trace loads."""
+    path = tmp_path / "lo.pcap"
+    small = [bytes(range(64)), bytes(range(64, 164))]
+    with open(path, "wb") as f:
+        f.write(struct.pack("<IHHiIII", 0xA1B23C4D, 2, 4, 0, 0, 262144, 1))
+        for i, fr in enumerate([small[0], b"\x07" * 65536, b"\x08" * 200000, small[1]]):
+            f.write(struct.pack("<IIII", i, 0, len(fr), len(fr)) + fr)
+    t = g.Trace(str(path))
+    assert t.n == 2 and t.skipped == 2
+    assert list(t.pkt_len) == [64, 100] and list(t.ts_ns) == [0, 3 * 10**9]
+    for i, fr in enumerate(small):
+        o = int(t.offs[i])
+        assert bytes(t.frames[o:o + len(fr)]) == fr
+    t1 = g.Trace(str(path), max_pkts=1)
+    assert t1.n == 1 and t1.skipped == 0
+
+
 def test_pcap_errors(g, tmp_path):
     with pytest.raises(OSError) as e:
         g.Trace(str(tmp_path / "missing.pcap"))

@@ -47,21 +47,29 @@ def test_pcap_malformed_files(fuzz_exe, tmp_path):
     rng = np.random.default_rng(5)
     fr = [bytes(rng.integers(0, 256, size=k, dtype=np.uint8)) for k in (60, 1514, 9014, 65535)]
     cases = {
-        "ok_le": (_hdr() + b"".join(_rec("<", f) for f in fr), 0, 4),
-        "ok_be_usec": (_hdr(">", 0xA1B2C3D4) + b"".join(_rec(">", f) for f in fr), 0, 4),
-        "header_only": (_hdr(), 0, 0),
-        "empty": (b"", -EPROTO, 0),
-        "short_header": (_hdr()[:20], -EPROTO, 0),
-        "truncated_data": (_hdr() + _rec("<", fr[0]) + _rec("<", fr[1])[:-7], -EPROTO, 0),
-        "cut_record_header": (_hdr() + _rec("<", fr[0]) + b"\x01\x02\x03", -EPROTO, 0),
-        "incl_65536": (_hdr() + _rec("<", b"\0" * 65536), -EPROTO, 0),
-        "incl_huge": (_hdr() + struct.pack("<IIII", 1, 2, 0xFFFFFFF0, 60) + b"\0" * 64, -EPROTO, 0),
-        "incl_past_eof": (_hdr() + struct.pack("<IIII", 1, 2, 4000, 4000) + b"\0" * 100, -EPROTO, 0),
-        "zero_len_record": (_hdr() + _rec("<", b"") + _rec("<", fr[0]), 0, 2),
-        "not_ethernet": (_hdr(linktype=101) + _rec("<", fr[0]), -EPROTO, 0),
+        # name: (file, return code, packets loaded, records skipped)
+        "ok_le": (_hdr() + b"".join(_rec("<", f) for f in fr), 0, 4, 0),
+        "ok_be_usec": (_hdr(">", 0xA1B2C3D4) + b"".join(_rec(">", f) for f in fr), 0, 4, 0),
+        "header_only": (_hdr(), 0, 0, 0),
+        "empty": (b"", -EPROTO, 0, 0),
+        "short_header": (_hdr()[:20], -EPROTO, 0, 0),
+        "truncated_data": (_hdr() + _rec("<", fr[0]) + _rec("<", fr[1])[:-7], -EPROTO, 0, 0),
+        "cut_record_header": (_hdr() + _rec("<", fr[0]) + b"\x01\x02\x03", -EPROTO, 0, 0),
+        # a capture longer than a u16 pkt_len (lo MTU 65536, GRO/TSO): skipped, counted
+        "incl_65536": (_hdr() + _rec("<", b"\0" * 65536), 0, 0, 1),
+        "oversize_between": (_hdr() + _rec("<", fr[0]) + _rec("<", b"\1" * 70000) + _rec("<", fr[1]),
+                             0, 2, 1),
+        "oversize_be": (_hdr(">", 0xA1B2C3D4) + _rec(">", b"\2" * 262144) + _rec(">", fr[2]), 0, 1, 1),
+        # ... but one running past the end of the file is still refused
+        "incl_huge": (_hdr() + struct.pack("<IIII", 1, 2, 0xFFFFFFF0, 60) + b"\0" * 64, -EPROTO, 0, 0),
+        "incl_past_eof": (_hdr() + struct.pack("<IIII", 1, 2, 4000, 4000) + b"\0" * 100, -EPROTO, 0, 0),
+        "oversize_past_eof": (_hdr() + _rec("<", fr[0]) + struct.pack("<IIII", 1, 2, 70000, 70000)
+                              + b"\0" * 1000, -EPROTO, 0, 0),
+        "zero_len_record": (_hdr() + _rec("<", b"") + _rec("<", fr[0]), 0, 2, 0),
+        "not_ethernet": (_hdr(linktype=101) + _rec("<", fr[0]), -EPROTO, 0, 0),
     }
     paths = []
-    for name, (data, _, _) in cases.items():
+    for name, (data, _, _, _) in cases.items():
         p = tmp_path / f"{name}.pcap"
         p.write_bytes(data)
         paths.append(p)
@@ -73,10 +81,10 @@ def test_pcap_malformed_files(fuzz_exe, tmp_path):
     out = run(fuzz_exe, "pcap", *paths)
     got = {}
     for line in out.splitlines():
-        path, rc, n, _ = line.rsplit(" ", 3)
-        got[os.path.basename(path)[:-5]] = (int(rc), int(n))
-    for name, (_, rc, n) in cases.items():
-        assert got[name] == (rc, n), (name, got[name])
+        path, rc, n, sk, _ = line.rsplit(" ", 4)
+        got[os.path.basename(path)[:-5]] = (int(rc), int(n), int(sk))
+    for name, (_, rc, n, sk) in cases.items():
+        assert got[name] == (rc, n, sk), (name, got[name])
     for k in range(40):
         assert got[f"garbage{k}"][0] in (0, -EPROTO)
 

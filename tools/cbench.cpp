@@ -4,8 +4,8 @@
 //   cbench <workload> <steps> [cfg ...]
 // (env CBENCH_N, CBENCH_STRIDE, CBENCH_R override the workload's shape)
 //
-// Each cfg is "ABLATE:GRID:DEPTH:THREADS:BPC:SCHED:V4[:NT[:DEFER]]" (NT = GCL_TUNE_NT_STORE,
-// DEFER = GCL_TUNE_DEFER, -1 or absent = library default) (GCL_TUNE_* knobs, 0 = default;
+// Each cfg is "ABLATE:GRID:DEPTH:THREADS:BPC:SCHED:V4[:NT]" (NT = GCL_TUNE_NT_STORE;
+// a ninth field, the removed GCL_TUNE_DEFER knob, is refused) (GCL_TUNE_* knobs, 0 = default;
 // V4=1 classifies into 4-byte verdicts, GCL_CFG_VERDICT4; V4=2 into 2-byte queue
 // verdicts, GCL_CFG_VERDICT2).
 // CBENCH_NOISE_US=X co-runs, on a second stream, 32 one-wave blocks that each
@@ -81,7 +81,7 @@ __global__ void noise_kernel(unsigned us, unsigned long long *sink)
 
 struct Cfg {
 	std::string name;
-	int ablate, grid, depth, threads, bpc, sched, v4, nt, defer;
+	int ablate, grid, depth, threads, bpc, sched, v4, nt, defer; /* defer: must stay -1 */
 	bool ref;
 	std::vector<double> us, wall;
 };
@@ -108,6 +108,10 @@ int main(int argc, char **argv)
 		Cfg c = {argv[i], 0, 0, 0, 0, 0, 0, 0, 0, -1, false, {}, {}};
 		sscanf(argv[i], "%d:%d:%d:%d:%d:%d:%d:%d:%d", &c.ablate, &c.grid, &c.depth, &c.threads, &c.bpc,
 		       &c.sched, &c.v4, &c.nt, &c.defer);
+		if (c.defer != -1) {
+			fprintf(stderr, "cfg %s: GCL_TUNE_DEFER was removed from the library\n", argv[i]);
+			return 1;
+		}
 		cfgs.push_back(c);
 	}
 	if (cfgs.size() == 1)
@@ -208,12 +212,6 @@ int main(int argc, char **argv)
 			setenv("GCL_TUNE_SCHED", buf, 1);
 			snprintf(buf, sizeof(buf), "%d", c.nt);
 			setenv("GCL_TUNE_NT_STORE", buf, 1);
-			if (c.defer >= 0) {
-				snprintf(buf, sizeof(buf), "%d", c.defer);
-				setenv("GCL_TUNE_DEFER", buf, 1);
-			} else {
-				unsetenv("GCL_TUNE_DEFER");
-			}
 			struct gcl_cfg cfg = {};
 			cfg.max_runtimes = R;
 			cfg.hash_mode = GCL_HASH_JENKINS;

@@ -130,15 +130,11 @@ int main(int argc, char **argv)
 	cfg.hash_mode = GCL_HASH_JENKINS;
 	cfg.flags = GCL_CFG_VERDICT4;
 	cfg.default_olflags = GCL_F_RSS_HASH | GCL_F_IP_CKSUM_GOOD;
-	/* ctx: the library default; ctx2: GCL_TUNE_DEFER=0 (verdict stores at the
-	 * end of their tile) for the deferred-store A/B */
-	struct gcl_ctx *ctx, *ctx2;
+	/* the library default (the former GCL_TUNE_DEFER A/B context is gone
+	 * with the knob, gclassify.hip kDefaultVerdictStore notes) */
+	struct gcl_ctx *ctx;
 	if (gcl_open(0, &cfg, &ctx))
 		return 1;
-	setenv("GCL_TUNE_DEFER", "0", 1);
-	if (gcl_open(0, &cfg, &ctx2))
-		return 1;
-	unsetenv("GCL_TUNE_DEFER");
 	uint16_t act[GCL_NCPU], flow[GCL_NCPU];
 	for (uint32_t r = 0; r < R; r++) {
 		uint16_t na = (uint16_t)(r % T + 1);
@@ -146,14 +142,13 @@ int main(int argc, char **argv)
 			act[i] = i;
 		gcl_steer_flows((uint16_t)T, act, na, flow);
 		gcl_runtime_set(ctx, (uint16_t)r, gcl_runtime_ip(r), (uint16_t)T, na, flow);
-		gcl_runtime_set(ctx2, (uint16_t)r, gcl_runtime_ip(r), (uint16_t)T, na, flow);
 	}
 	int cus = 0;
 	CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
 	hipEvent_t e0, e1;
 	CHECK(hipEventCreate(&e0));
 	CHECK(hipEventCreate(&e1));
-	std::vector<std::vector<double>> cl(NF * NV), tk(NF * NV), c2(NF * NV);
+	std::vector<std::vector<double>> cl(NF * NV), tk(NF * NV);
 	for (int round = 0; round < 3; round++)
 		for (int f = 0; f < NF; f++)
 			for (int v = 0; v < NV; v++) {
@@ -171,14 +166,6 @@ int main(int argc, char **argv)
 				float ms;
 				CHECK(hipEventElapsedTime(&ms, e0, e1));
 				cl[f * NV + v].push_back(ms * 1e3 / steps);
-				gcl_classify(ctx2, &bt, vb[v], acc, acc + R, nullptr);
-				CHECK(hipEventRecord(e0, nullptr));
-				for (int s = 0; s < steps; s++)
-					gcl_classify(ctx2, &bt, vb[v], acc, acc + R, nullptr);
-				CHECK(hipEventRecord(e1, nullptr));
-				CHECK(hipEventSynchronize(e1));
-				CHECK(hipEventElapsedTime(&ms, e0, e1));
-				c2[f * NV + v].push_back(ms * 1e3 / steps);
 				CHECK(hipEventRecord(e0, nullptr));
 				for (int s = 0; s < steps; s++)
 					hipLaunchKernelGGL(tile_kernel<0>, dim3(cus * 4), dim3(256), 0, nullptr, fb[f],
@@ -224,15 +211,13 @@ int main(int argc, char **argv)
 		                                   (unsigned long long)(n / 256), vb[v]); }));
 	for (int f = 0; f < NF; f++)
 		for (int v = 0; v < NV; v++) {
-			auto &a = cl[f * NV + v], &b = tk[f * NV + v], &c = c2[f * NV + v];
+			auto &a = cl[f * NV + v], &b = tk[f * NV + v];
 			std::sort(a.begin(), a.end());
 			std::sort(b.begin(), b.end());
-			std::sort(c.begin(), c.end());
 			printf("{\"f\": %d, \"v\": %d, \"fva\": \"%p\", \"vva\": \"%p\", \"classify_us\": %.2f, "
-			       "\"classify_defer0_us\": %.2f, \"tile_us\": %.2f}\n", f, v, (void *)fb[f], (void *)vb[v],
-			       a[a.size() / 2], c[c.size() / 2], b[b.size() / 2]);
+			       "\"tile_us\": %.2f}\n", f, v, (void *)fb[f], (void *)vb[v],
+			       a[a.size() / 2], b[b.size() / 2]);
 		}
 	gcl_close(ctx);
-	gcl_close(ctx2);
 	return 0;
 }
