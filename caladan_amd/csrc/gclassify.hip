@@ -43,6 +43,15 @@ constexpr int kImgUsers = 8;             /* streams tracked per table image */
  * register-header classify_quad_kernel measured equal or 1-3 % slower on the
  * ingress rows (profiles/r02_quad_ab.jsonl), so it stays an experiment. */
 constexpr int kDefaultQuad = 0;
+/* GCL_TUNE_PAIR default: GENERAL batches on classify_pair_kernel.  Against
+ * the LDS-tile classify_kernel, alternating in one process
+ * (profiles/r03_general_ab.jsonl, r03_ws_ab.jsonl): the cache-resident
+ * working-set row 107.4-109.5 -> 95.4-98.4 us, the random pool, the
+ * JENKINS offsets-only row, PCIe zero-copy and the pcap replay within
+ * +-1 %; 23 % fewer VALU instructions per wave (SQ counters,
+ * profiles/r03_sq_ingress_ws_*.json).  GCL_TUNE_PAIR=0 restores the tile
+ * kernel, =2 runs the pair kernel at 2048 lanes per CU. */
+constexpr int kDefaultPair = 1;
 constexpr uint32_t kLdsQueueBytes = 16; /* s_next[2] after the header tile */
 
 /* The first failure of a sequence of HIP calls whose outcome is checked
@@ -413,7 +422,8 @@ template <int MODE, bool GENERAL, bool SYS, bool REG>
 __device__ __forceinline__ uint64_t classify_core(const KParams &k, const HdrWords &h,
                                                   const uint4 *tile, int tid, uint64_t idx,
                                                   const Tables &tb, uint32_t *hist, Counters &cnt,
-                                                  uint32_t sh, uint32_t avail, const uint32_t *pre)
+                                                  uint32_t sh, uint32_t avail, const uint32_t *pre,
+                                                  uint64_t foff = kNoOff)
 {
 	const uint32_t d3 = h.d3, d5 = h.d5, d6 = h.d6, d7 = h.d7, d8 = h.d8, d9 = h.d9, d10 = h.d10;
 	const uint32_t et = gcl::bswap16(d3 & 0xFFFF);              /* rx.c:154 */
@@ -429,10 +439,18 @@ __device__ __forceinline__ uint64_t classify_core(const KParams &k, const HdrWor
 	                       : pre ? pre[0] & 0xFF : k.olflags[idx];
 	const bool is_ip = et == GCL_ETHTYPE_IP, is_arp = et == GCL_ETHTYPE_ARP;
 	if (GENERAL && !SYS && is_arp && avail < 44) {
-		/* bytes 40-41 are past the staged line (load_tile) */
-		const uint64_t a = frame_off<GENERAL>(k, idx) + 38;
-		arp_tip = (uint32_t)frame_byte(k, a) << 24 | (uint32_t)frame_byte(k, a + 1) << 16 |
-		          (uint32_t)frame_byte(k, a + 2) << 8 | frame_byte(k, a + 3);
+		/* bytes 40-41 are past the staged bytes: one dword load when it is
+		 * aligned and inside frames_len, else byte by byte (@foff: the frame
+		 * offset when the caller has it, saving the offs[] reload) */
+		const uint64_t o = foff != kNoOff ? foff : frame_off<GENERAL>(k, idx);
+		const uint64_t A = (uint64_t)(uintptr_t)k.frames + o + 40;
+		if (o < k.frames_len && k.frames_len - o >= 44 && (A & 3) == 0) {
+			arp_tip = gcl::bswap32(gcl::mid32(d9, *(const uint32_t *)(k.frames + o + 40)));
+		} else {
+			const uint64_t a = o + 38;
+			arp_tip = (uint32_t)frame_byte(k, a) << 24 | (uint32_t)frame_byte(k, a + 1) << 16 |
+			          (uint32_t)frame_byte(k, a + 2) << 8 | frame_byte(k, a + 3);
+		}
 	}
 	const bool azure = k.cflags & GCL_CFG_AZURE_ARP;
 
@@ -1122,6 +1140,188 @@ classify_quad_kernel(KParams k)
 }
 
 /* ------------------------------------------------------------------------
+ * classify_pair_kernel: the GENERAL path (frames at per-packet offsets, or
+ * per-packet side arrays) without a staged window.  rx_one_pkt reads frame
+ * bytes 12-39 of every IPv4 packet (Ethertype, IHL, fragment field, proto,
+ * saddr, daddr and -- for the computed hashes -- the L4 ports, rx.c:127-167)
+ * and bytes 38-41 of an ARP packet, so each packet's header is fetched as the
+ * 32 bytes [8, 40): one 128-B line for every frame that starts at least 40
+ * bytes before a line end, which is every frame of the reference's ingress
+ * pool (element + 344 of 9408-B elements, iokernel/defs.h:503-506).  A PAIR of
+ * lanes loads it with one 16-B load each -- lane 2i bytes 8-23, lane 2i+1
+ * bytes 24-39, of packet 2i and then of packet 2i+1 -- and one DPP exchange
+ * gives each lane both halves of its own packet: no LDS header tile, no
+ * barriers and no window arithmetic, about half the VALU work per packet of
+ * the tile kernel's GENERAL loop, which is issue-bound on cache-resident
+ * frames (SQ counters).  The ARP target (bytes 40-41) and the
+ * ports behind IPv4 options are read from the frame when needed (REG path of
+ * classify_core), as are frames that are not 4-B aligned or end past
+ * frames_len (bytewise, zero past it).  Offsets, ol_flags and hash.rss are
+ * loaded tiles ahead with a fixed load count on every path (the tile
+ * kernel's rule for the waits).
+ */
+constexpr uint64_t kPairBytewise = 1ull << 63;
+
+/* DPP move with no "old" operand: a quad_perm never leaves a lane without
+ * a source, so the exchange needs no register of zeros */
+template <int CTRL>
+__device__ __forceinline__ uint32_t mdpp(uint32_t v)
+{
+	return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
+}
+
+/* Where packet @off's bytes [8, 40) come from: off + 8 when one aligned
+ * pair of 16-B loads inside frames_len can read them; kPairBytewise | o
+ * (o = off, or frames_len when off is past it, so every byte reads 0) when
+ * they must be read byte by byte; kNoOff when there is no packet. */
+__device__ __forceinline__ uint64_t pair_src(const KParams &k, uint64_t off)
+{
+	/* straight-line selects: every lane runs the same instructions */
+	const bool in = off < k.frames_len;
+	const bool fits = in && k.frames_len - off >= 40 &&
+	                  (((uint32_t)(uintptr_t)k.frames + (uint32_t)off) & 3) == 0;
+	const uint64_t bw = kPairBytewise | (in ? off : k.frames_len);
+	return off == kNoOff ? kNoOff : fits ? off + 8 : bw;
+}
+
+typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+
+/* load J of this lane: half (lane & 1) of the pair's packet J, whose
+ * pair_src lane J of the pair holds in @my (quad_perm broadcast) */
+template <int J>
+__device__ __forceinline__ uint4 pair_load(const KParams &k, uint64_t my)
+{
+	constexpr int B = J ? 0xF5 : 0xA0; /* quad_perm [1,1,3,3] : [0,0,2,2] */
+	const uint32_t lo = mdpp<B>((uint32_t)my), hi = mdpp<B>((uint32_t)(my >> 32));
+	const uint64_t s = (uint64_t)hi << 32 | lo;
+	const uint8_t *a = (hi >> 31) ? k.tables : k.frames + s + 16 * (threadIdx.x & 1);
+	const u32x4a4 v = __builtin_nontemporal_load((const u32x4a4 *)a);
+	return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+/* r[j] = half (lane & 1) of pair packet j  ->  r[h] = half h of this lane's packet */
+__device__ __forceinline__ void pair_exchange(uint4 r[2])
+{
+	const bool odd = threadIdx.x & 1;
+	/* quad_perm [1,0,3,2]: the odd lane sends the even packet's second
+	 * half, the even lane the odd packet's first half */
+	const uint4 x = sel4(odd, r[0], r[1]);
+	const uint4 y = make_uint4(mdpp<0xB1>(x.x), mdpp<0xB1>(x.y), mdpp<0xB1>(x.z), mdpp<0xB1>(x.w));
+	r[0] = sel4(odd, y, r[0]);
+	r[1] = sel4(odd, r[1], y);
+}
+
+template <int MODE, bool TLDS, int NT>
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4)))
+classify_pair_kernel(KParams k)
+{
+	extern __shared__ uint4 smem[];
+	uint32_t *hist = (uint32_t *)smem;
+	uint8_t *lds_tab = (uint8_t *)(hist + ((k.max_rt + 3) & ~3u));
+	const int tid = threadIdx.x;
+	for (uint32_t i = tid; i < k.max_rt; i += NT)
+		hist[i] = 0;
+	const uint8_t *tab = TLDS ? lds_tab : k.tables;
+	if (TLDS) {
+		const uint4 *src = (const uint4 *)k.tables;
+		uint4 *dst = (uint4 *)lds_tab;
+		for (uint32_t i = tid; i < k.tables_lds_bytes / 16; i += NT)
+			dst[i] = src[i];
+	}
+	Tables tb;
+	tb.ipt = (const uint2 *)tab;
+	tb.rtab = (const RtEntry *)(tab + k.off_rt);
+	tb.flow = tab + k.off_flow;
+	tb.toep = (const uint32_t *)(tab + k.off_toep);
+	tb.seed = (const uint32_t *)(tab + k.off_seed);
+	tb.crc = (const uint32_t *)(tab + k.off_crc);
+	__syncthreads();
+
+	Counters cnt = {0, 0, 0, 0};
+	const uint64_t step = gridDim.x;
+	const uint64_t *offs_src = k.offs ? k.offs : (const uint64_t *)k.tables;
+	auto ok = [&](uint64_t tt) { return tt < k.ntiles && tt * NT + tid < k.n; };
+	auto ld_off = [&](uint64_t tt) -> uint64_t {
+		return offs_src[k.offs && ok(tt) ? tt * NT + tid : 0];
+	};
+	auto src_of = [&](uint64_t tt, uint64_t raw) -> uint64_t {
+		return pair_src(k, !ok(tt) ? kNoOff : k.offs ? raw : (tt * NT + tid) * k.stride);
+	};
+	auto pref = [&](uint64_t tt, uint32_t pr[2]) {
+		const uint64_t i = ok(tt) ? tt * NT + tid : 0;
+		pr[0] = *(k.olflags ? k.olflags + i : side_dummy<uint8_t>(k, i));
+		if (MODE == GCL_HASH_NIC)
+			pr[1] = *(k.rss ? k.rss + i : side_dummy<uint32_t>(k, i));
+	};
+	auto issue = [&](uint64_t my, uint4 r[2]) {
+		r[0] = pair_load<0>(k, my);
+		r[1] = pair_load<1>(k, my);
+	};
+	/* the landed halves -> this lane's header dwords (frame bytes 12-39;
+	 * d10, bytes 40-43, is not fetched: avail 40 sends ARP to the frame) */
+	auto unpack = [&](uint4 r[2], uint64_t my, HdrWords &h) {
+		pair_exchange(r);
+		if ((my >> 63) && my != kNoOff) { /* bytewise (rare) */
+			const uint64_t off = my & ~kPairBytewise;
+			r[0] = load16_bytes(k, off + 8);
+			r[1] = load16_bytes(k, off + 24);
+		}
+		h.d3 = r[0].y, h.d5 = r[0].w, h.d6 = r[1].x, h.d7 = r[1].y;
+		h.d8 = r[1].z, h.d9 = r[1].w, h.d10 = 0;
+	};
+	auto classify = [&](uint64_t tt, const HdrWords &h, const uint32_t pr[2], uint64_t my) {
+		if (ok(tt)) {
+			const uint64_t i = tt * NT + tid;
+			/* this packet's frame offset, for the ARP target's extra read */
+			const uint64_t foff = (my >> 63) ? (my & ~kPairBytewise) : my - 8;
+			if (k.ablate & 128) /* timing only: the loop without rx_one_pkt */
+				put_verdict(k, i, h.d3 ^ h.d7 ^ h.d9 ^ pr[0] ^ pr[1]);
+			else
+				put_verdict(k, i, classify_core<MODE, true, false, true>(k, h, nullptr, tid, i, tb,
+				                                                          hist, cnt, 0, 40, pr, foff));
+		}
+	};
+
+	uint64_t t = blockIdx.x;
+	uint4 ra[2], rb[2];
+	uint32_t pra[2] = {0, 0}, prb[2] = {0, 0};
+	/* prologue: tiles t and t + step in flight, offsets of the two after */
+	uint64_t oa = ld_off(t), ob = ld_off(t + step);
+	uint64_t sa = src_of(t, oa);
+	issue(sa, ra);
+	pref(t, pra);
+	oa = ld_off(t + 2 * step);
+	uint64_t sb = src_of(t + step, ob);
+	issue(sb, rb);
+	pref(t + step, prb);
+	ob = ld_off(t + 3 * step);
+	while (t < k.ntiles) {
+		asm volatile("" : "+s"(t));
+		HdrWords h;
+		unpack(ra, sa, h);
+		uint64_t my = sa;
+		sa = src_of(t + 2 * step, oa);
+		issue(sa, ra);
+		classify(t, h, pra, my);
+		pref(t + 2 * step, pra);
+		oa = ld_off(t + 4 * step);
+		t += step;
+		/* runs past ntiles too (dummy loads, nothing classified): a path
+		 * out of the middle would change the wait counts (classify_kernel) */
+		unpack(rb, sb, h);
+		my = sb;
+		sb = src_of(t + 2 * step, ob);
+		issue(sb, rb);
+		classify(t, h, prb, my);
+		pref(t + 2 * step, prb);
+		ob = ld_off(t + 4 * step);
+		t += step;
+	}
+	__syncthreads(); /* every wave's histogram adds are in */
+	flush_counters<NT>(k, hist, cnt);
+}
+
+/* ------------------------------------------------------------------------
  * Persistent rx loop (gcl_rxloop_*): a burst-at-a-time classifier for the
  * reference's own granularity, rx_burst's <= 64 mbufs (iokernel/rx.c:270-290).
  * Each of `workers` 256-lane blocks owns tickets w+1, w+1+W, ...: it polls
@@ -1586,6 +1786,7 @@ struct gcl_ctx {
 	int tune_sched;    /* GCL_TUNE_SCHED: 0 static persistent grid, 1 dynamic tile queue */
 	int tune_xcd_map;  /* GCL_TUNE_XCD_MAP: 1 contiguous eighth per XCD, 0 round-robin tiles */
 	int tune_quad;     /* GCL_TUNE_QUAD: 1 GENERAL batches on classify_quad_kernel, 0 classify_kernel */
+	int tune_pair;     /* GCL_TUNE_PAIR: 1 GENERAL batches on classify_pair_kernel */
 	/* dynamic tile queue: one slot per launch in flight, reused in turn; a
 	 * launch waits for the previous user of its slot (same or other stream) */
 	uint32_t *sched;
@@ -1671,6 +1872,8 @@ extern "C" int gcl_open(int hip_device, const struct gcl_cfg *cfg, struct gcl_ct
 		c->tune_xcd_map = e ? atoi(e) : kDefaultXcdMap;
 		e = getenv("GCL_TUNE_QUAD");
 		c->tune_quad = e ? atoi(e) : kDefaultQuad;
+		e = getenv("GCL_TUNE_PAIR");
+		c->tune_pair = e ? atoi(e) : kDefaultPair;
 	}
 	c->dimg[0] = c->dimg[1] = nullptr;
 	c->sched = nullptr;
@@ -2011,12 +2214,22 @@ static hipError_t launch_quad(const KParams &k, bool tlds, uint32_t lds, int num
 	return launch_fn(fn, NT, k, lds, num_cus, bpc_cap, s);
 }
 
+template <int MODE, int NT>
+static hipError_t launch_pair(const KParams &k, bool tlds, uint32_t lds, int num_cus, int bpc_cap,
+                              hipStream_t s)
+{
+	const ClassifyFn fn = tlds ? classify_pair_kernel<MODE, true, NT>
+	                           : classify_pair_kernel<MODE, false, NT>;
+	return launch_fn(fn, NT, k, lds, num_cus, bpc_cap, s);
+}
+
 /* Launch geometry (measured on MI355X, tools/cbench.cpp): */
 struct Geometry {
 	int threads;  /* packets per tile = lanes per block */
 	int depth;    /* tiles in flight per block */
 	int bpc_cap;  /* blocks per CU */
 	bool quad;    /* classify_quad_kernel (GENERAL batches): no LDS header tile */
+	bool pair;    /* classify_pair_kernel (GENERAL batches): [8, 40) per packet by lane pairs */
 };
 
 /* LDS for the tile's header sources (s_src, classify_kernel): GENERAL */
@@ -2029,6 +2242,14 @@ template <int MODE>
 static hipError_t launch_mode(const KParams &k, bool tlds, bool general, const Geometry &geo,
                               uint32_t tab_lds, uint32_t hist_bytes, int num_cus, hipStream_t s)
 {
+	if (geo.pair) {
+		const uint32_t lds = hist_bytes + tab_lds;
+		if (geo.threads == 1024)
+			return launch_pair<MODE, 1024>(k, tlds, lds, num_cus, geo.bpc_cap, s);
+		if (geo.threads == 512)
+			return launch_pair<MODE, 512>(k, tlds, lds, num_cus, geo.bpc_cap, s);
+		return launch_pair<MODE, 256>(k, tlds, lds, num_cus, geo.bpc_cap, s);
+	}
 	if (geo.quad) {
 		const uint32_t lds = hist_bytes + tab_lds;
 		if (geo.threads == 1024)
@@ -2068,15 +2289,18 @@ static Geometry choose_geometry(const gcl_ctx *c, uint32_t tab_lds, uint32_t his
 	Geometry g;
 	g.depth = 1;
 	g.threads = 0;
-	/* GENERAL batches run on the LDS-tile classify_kernel by default
-	 * (kDefaultQuad 0).  The register-header classify_quad_kernel runs only
-	 * with GCL_TUNE_QUAD=1, and even then the tile kernel is kept when the
-	 * dynamic tile queue (GCL_TUNE_SCHED), depth 1 (GCL_TUNE_DEPTH=1) or the
-	 * membench body (GCL_TUNE_ABLATE bit 16) is asked for */
+	/* GENERAL batches run on the lane-pair classify_pair_kernel by default
+	 * (kDefaultPair 1), on the register-header classify_quad_kernel with
+	 * GCL_TUNE_QUAD=1, and on the LDS-tile classify_kernel with
+	 * GCL_TUNE_PAIR=0 -- or whenever the dynamic tile queue
+	 * (GCL_TUNE_SCHED), depth 1 (GCL_TUNE_DEPTH=1) or the membench body
+	 * (GCL_TUNE_ABLATE bit 16) is asked for, which only it implements */
 	g.quad = general && c->tune_quad && !c->tune_sched && c->tune_depth != 1 &&
 	         !(c->tune_ablate & 16);
+	g.pair = general && !g.quad && c->tune_pair && !c->tune_sched && c->tune_depth != 1 &&
+	         !(c->tune_ablate & 16);
 	auto per_block = [&](uint32_t nt) -> uint32_t {
-		if (g.quad)
+		if (g.quad || g.pair)
 			return hist_bytes + tab_lds;
 		return nt * 64 + kLdsQueueBytes + hist_bytes + tab_lds + offs_lds_bytes(general, nt);
 	};
@@ -2098,6 +2322,11 @@ static Geometry choose_geometry(const gcl_ctx *c, uint32_t tab_lds, uint32_t his
 		 * 1024-runtime tables) 1 % on the 8 Mi header-split layout, 3.4 % at
 		 * 32 Mi, and no change on tcp1500 (profiles/r01_hsplit_geometry.jsonl) */
 		g.depth = 2;
+	}
+	if (g.pair && c->tune_pair == 2) { /* experiment: 2048 resident lanes per CU */
+		const uint32_t pb = per_block((uint32_t)g.threads);
+		if ((uint32_t)(2 * g.bpc_cap) * pb <= lds_cu)
+			g.bpc_cap *= 2;
 	}
 	if (c->tune_threads)
 		g.threads = c->tune_threads;

@@ -135,18 +135,22 @@ def test_gpu_fuzz_misaligned_offsets(g, orc, misalign, mode):
     assert (tr == tre).all() and (c == ce).all() and (st == se).all()
 
 
+@pytest.mark.parametrize("kernel", ["quad", "tile", "pair"])
 @pytest.mark.parametrize("tables", ["lds", "global"])
 @pytest.mark.parametrize("misalign", ["mbuf", "mixed", "lineend"])
 @pytest.mark.parametrize("mode", [0, 1, 2])
-def test_gpu_quad_kernel_fuzz(g, orc, monkeypatch, misalign, mode, tables):
-    """The register-header GENERAL kernel (classify_quad_kernel,
-    GCL_TUNE_QUAD=1) on the misaligned-offset fuzz: window shifts of 0-12
-    bytes selected in registers, bytewise frames, headers cut at the first
-    line end, IHL > 5 ports and ARP target IPs read from the frame, loopback
-    hints, FDIR marks and the transport pre-hash, in all three hash modes,
-    with the tables in LDS and forced to global memory (GCL_TUNE_TABLES=1)."""
+def test_gpu_general_kernels_fuzz(g, orc, monkeypatch, misalign, mode, tables, kernel):
+    """Every GENERAL kernel on the misaligned-offset fuzz, each forced by its
+    knob: the lane-pair kernel (classify_pair_kernel, the default), the
+    LDS-tile kernel (classify_kernel, GCL_TUNE_PAIR=0) and the register-header
+    kernel (classify_quad_kernel, GCL_TUNE_QUAD=1).  Window shifts of 0-12
+    bytes, frames that are not 4-B aligned (bytewise), headers cut at the
+    first line end, frames straddling frames_len, IHL > 5 ports and ARP
+    target IPs read from the frame, loopback hints, FDIR marks and the
+    transport pre-hash, in all three hash modes, an odd packet count, with
+    the tables in LDS and forced to global memory (GCL_TUNE_TABLES=1)."""
     rng = np.random.default_rng(9300 + 10 * mode + {"mbuf": 0, "mixed": 1, "lineend": 2}[misalign]
-                                + 100 * (tables == "global"))
+                                + 100 * (tables == "global") + 1000 * ["quad", "tile", "pair"].index(kernel))
     rts = random_runtimes(rng, 1024, 300)
     n = 7001
     frames, flen, offs, olf, rss, fdir, hint = fuzz_batch(
@@ -154,7 +158,8 @@ def test_gpu_quad_kernel_fuzz(g, orc, monkeypatch, misalign, mode, tables):
     key = bytes(rng.integers(0, 256, size=40, dtype=np.uint8))
     t = orc.Tables(1024, mode, g.CFG_TRANS_HASH, 0x09, key)
     apply_runtimes(t, rts)
-    env = {"GCL_TUNE_QUAD": "1", **({"GCL_TUNE_TABLES": "1"} if tables == "global" else {})}
+    env = {{"quad": "GCL_TUNE_QUAD", "tile": "GCL_TUNE_PAIR", "pair": "GCL_TUNE_PAIR"}[kernel]:
+           "0" if kernel == "tile" else "1", **({"GCL_TUNE_TABLES": "1"} if tables == "global" else {})}
     for kk, vv in env.items():
         monkeypatch.setenv(kk, vv)
     try:
@@ -167,7 +172,7 @@ def test_gpu_quad_kernel_fuzz(g, orc, monkeypatch, misalign, mode, tables):
                                  frames_len=flen, dst_hint=hint, trans=True)
     v, c, st, tr = gpu_run(g, clf, frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir=fdir,
                            frames_len=flen, hint=hint, trans=True)
-    assert_same(v, ve, f"quad misalign={misalign} mode={mode}")
+    assert_same(v, ve, f"{kernel} misalign={misalign} mode={mode}")
     assert (tr == tre).all() and (c == ce).all() and (st == se).all()
 
 
