@@ -405,14 +405,17 @@ def run_timed(w, steps, warmup, world, ex=None):
     return el, gpu_ms
 
 
-def group_bench(w, steps, warmup, device_index, period=EXCHANGE_EVERY):
+def group_bench(w, steps, warmup, device_index, period=EXCHANGE_EVERY, settle=None):
     """The multi-GPU step as the single-process iokernel links it
     (include/gcl_group.h): a gcl_group over this process's GPUs (one here)
     classifying the headline batch on the group's own stream, with the
     per-runtime counts and rx counters all-gathered through RCCL
     (ncclCommInitAll + ncclAllGather) every `period` steps on a side stream.
     Same buffers as the headline; timed like run_timed (settle, then K steps
-    between synchronisations), the node-wide counts read back and checked."""
+    between synchronisations), the node-wide counts read back and checked.
+    `settle`: untimed steps before the timed ones (the headline's own count:
+    a settle sized from the warmup's wall time, which includes the group's
+    first table upload, can leave the timed steps in the launch-time ramp)."""
     fl, tb = verdict_cfg(w.vbytes, w.R, w.T)
     grp = g.Group([device_index], w.R, g.HASH_JENKINS, flags=fl, thread_bits=tb,
                   exchange=g.XCHG_RCCL)
@@ -434,7 +437,9 @@ def group_bench(w, steps, warmup, device_index, period=EXCHANGE_EVERY):
             one()
         grp.sync()
         step_ms = (time.perf_counter() - t0) * 1e3 / max(warmup, 1)
-        for _ in range(int(SETTLE_MS / max(step_ms, 1e-3)) + 1):
+        if settle is None:
+            settle = int(SETTLE_MS / max(step_ms, 1e-3)) + 1
+        for _ in range(settle):
             one()
         grp.sync()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -455,7 +460,7 @@ def group_bench(w, steps, warmup, device_index, period=EXCHANGE_EVERY):
                 "value": round(w.n * grp.n * steps / el / 1e6, 1), "unit": "Mpkt/s",
                 "ms_per_step": round(el / steps * 1e3, 4),
                 "gpu_ms_per_step": round(e0.elapsed_time(e1) / steps, 4),
-                "exchanges": int(k[0] // period) + 1,
+                "exchanges": int(k[0] // period) + 1, "settle_steps": settle,
                 "counts_check": "ok" if ok else f"MISMATCH {int(c.sum())} != {w.n * k[0]}"}
     finally:
         grp.close()
@@ -1093,7 +1098,8 @@ def main():
                               "periods": ex.k}
     if world == 1 and not args.no_group:
         try:
-            result["group"] = group_bench(w, args.steps, args.warmup, dev_index, args.exchange_every)
+            result["group"] = group_bench(w, args.steps, args.warmup, dev_index, args.exchange_every,
+                                          settle=settle_steps)
         except (OSError, ImportError) as e:  # reported, never silently dropped
             result["group"] = {"error": str(e)}
     del w, ex
