@@ -627,7 +627,8 @@ def rxpipe_bench():
     # 16 workers; verdicts are read in place in the slot (gcl_rxloop_peek),
     # and once copied out (the round-2 form) for comparison
     for cfg in (("64", "1", "1", "20000"), ("64", "4", "8", "20000"), ("64", "4", "8", "20000", "copy"),
-                ("64", "8", "16", "40000"), ("64", "16", "32", "40000"), ("256", "4", "8", "10000"),
+                ("64", "8", "16", "40000"), ("64", "16", "32", "40000"), ("64", "8", "16", "40000", "inline"),
+                ("64", "16", "32", "40000", "inline"), ("256", "4", "8", "10000"),
                 ("1024", "8", "16", "4000"), ("4096", "16", "16", "1000")):
         try:
             r = subprocess.run([exe, *cfg], capture_output=True, text=True, timeout=120)

@@ -418,7 +418,9 @@ struct HdrWords {
  * false) holds them in row @tid for the IHL != 5 port reads, which REG
  * (classify_quad_kernel: headers in registers) reads from the frame instead.
  */
-template <int MODE, bool GENERAL, bool SYS, bool REG>
+/* VF: the verdict format when known at compile time (2: GCL_CFG_VERDICT2,
+ * which excludes the transport pre-hash), 0: read from k.cflags */
+template <int MODE, bool GENERAL, bool SYS, bool REG, int VF = 0>
 __device__ __forceinline__ uint64_t classify_core(const KParams &k, const HdrWords &h,
                                                   const uint4 *tile, int tid, uint64_t idx,
                                                   const Tables &tb, uint32_t *hist, Counters &cnt,
@@ -426,6 +428,8 @@ __device__ __forceinline__ uint64_t classify_core(const KParams &k, const HdrWor
                                                   uint64_t foff = kNoOff)
 {
 	const uint32_t d3 = h.d3, d5 = h.d5, d6 = h.d6, d7 = h.d7, d8 = h.d8, d9 = h.d9, d10 = h.d10;
+	/* timing-only ablations: never in a format-specialised (VF) kernel */
+	const uint32_t ablate = VF ? 0u : k.ablate;
 	const uint32_t et = gcl::bswap16(d3 & 0xFFFF);              /* rx.c:154 */
 	const uint32_t ihl = (d3 >> 16) & 0xF;
 	const uint32_t frag = gcl::bswap16(d5 & 0xFFFF);            /* ARP: opcode */
@@ -456,7 +460,7 @@ __device__ __forceinline__ uint64_t classify_core(const KParams &k, const HdrWor
 
 	/* steering hash (gclassify.h: NIC / JENKINS / TOEPLITZ) */
 	uint32_t hash = 0;
-	if (k.ablate & 1) {
+	if (ablate & 1) {
 		hash = daddr;
 	} else if (MODE == GCL_HASH_NIC) {
 		if (k.rss)
@@ -517,7 +521,7 @@ __device__ __forceinline__ uint64_t classify_core(const KParams &k, const HdrWor
 	if constexpr (!GENERAL && !SYS)
 		dense_drain();
 	/* ip_to_proc: open addressing keyed by rte_jhash(&ip, 4, 0), rx.c:197 */
-	if (k.ablate & 2) {
+	if (ablate & 2) {
 		if (lookup)
 			p = (int)(dst & 15);
 	} else if (lookup) {
@@ -539,7 +543,7 @@ __device__ __forceinline__ uint64_t classify_core(const KParams &k, const HdrWor
 	if (p >= 0) {
 		const RtEntry re = tb.rtab[p];
 		uniq = (uint32_t)p;
-		if (k.ablate & 8) {
+		if (ablate & 8) {
 			thr = hash & 7;
 		} else {
 			const uint64_t M = (uint64_t)re.m_hi << 32 | re.m_lo;
@@ -552,10 +556,10 @@ __device__ __forceinline__ uint64_t classify_core(const KParams &k, const HdrWor
 					thr = slot; /* the host replays flow_tbl[slot] */
 			}
 		}
-		if (!(k.ablate & 4))
+		if (!(ablate & 4))
 			atomicAdd(&hist[p], 1u);
 	}
-	if (k.trans) {
+	if (VF != 2 && k.trans) {
 		/* trans_lookup's hashes with runtime p's trans_seed
 		 * (transport.c:29-42, :366-375), for the packets net_rx_one passes
 		 * to net_rx_trans (core.c:203-209, :281-300) */
@@ -574,7 +578,7 @@ __device__ __forceinline__ uint64_t classify_core(const KParams &k, const HdrWor
 		k.trans[idx] = tr;
 	}
 	const uint32_t vlo = uniq | thr << 16 | action << 24;
-	if (k.cflags & GCL_CFG_VERDICT2) {
+	if (VF == 2 || (VF == 0 && (k.cflags & GCL_CFG_VERDICT2))) {
 		/* q = uniqid << thread_bits | thread (thread_bits in cflags[31:24]) */
 		const uint32_t a = action & GCL_ACT_MASK;
 		const uint32_t q = uniq << (k.cflags >> 24) | thr;
@@ -618,6 +622,20 @@ __device__ __forceinline__ uint64_t classify_one(const KParams &k, const uint4 *
 
 /* Store verdict word @w (classify_one) of packet @idx in the context's
  * verdict format and store policy. */
+__device__ __forceinline__ void put_verdict(const KParams &k, uint64_t idx, uint64_t w);
+
+/* put_verdict with the format known at compile time: VF 2 is the 2-byte
+ * verdict with the default write-through store (kDefaultVerdictStore) */
+template <int VF>
+__device__ __forceinline__ void put_verdict_vf(const KParams &k, uint64_t idx, uint64_t w)
+{
+	if (VF == 2)
+		__hip_atomic_store((uint16_t *)k.verdicts + idx, (uint16_t)w, __ATOMIC_RELAXED,
+		                   __HIP_MEMORY_SCOPE_SYSTEM);
+	else
+		put_verdict(k, idx, w);
+}
+
 __device__ __forceinline__ void put_verdict(const KParams &k, uint64_t idx, uint64_t w)
 {
 	if (k.cflags & GCL_CFG_VERDICT2) {
@@ -1211,7 +1229,7 @@ __device__ __forceinline__ void pair_exchange(uint4 r[2])
 	r[1] = sel4(odd, r[1], y);
 }
 
-template <int MODE, bool TLDS, int NT>
+template <int MODE, bool TLDS, int NT, int VF>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4)))
 classify_pair_kernel(KParams k)
 {
@@ -1274,11 +1292,11 @@ classify_pair_kernel(KParams k)
 			const uint64_t i = tt * NT + tid;
 			/* this packet's frame offset, for the ARP target's extra read */
 			const uint64_t foff = (my >> 63) ? (my & ~kPairBytewise) : my - 8;
-			if (k.ablate & 128) /* timing only: the loop without rx_one_pkt */
-				put_verdict(k, i, h.d3 ^ h.d7 ^ h.d9 ^ pr[0] ^ pr[1]);
+			if (!VF && (k.ablate & 128)) /* timing only: the loop without rx_one_pkt */
+				put_verdict_vf<VF>(k, i, h.d3 ^ h.d7 ^ h.d9 ^ pr[0] ^ pr[1]);
 			else
-				put_verdict(k, i, classify_core<MODE, true, false, true>(k, h, nullptr, tid, i, tb,
-				                                                          hist, cnt, 0, 40, pr, foff));
+				put_verdict_vf<VF>(k, i, classify_core<MODE, true, false, true, VF>(
+				                                 k, h, nullptr, tid, i, tb, hist, cnt, 0, 40, pr, foff));
 		}
 	};
 
@@ -2218,8 +2236,16 @@ template <int MODE, int NT>
 static hipError_t launch_pair(const KParams &k, bool tlds, uint32_t lds, int num_cus, int bpc_cap,
                               hipStream_t s)
 {
-	const ClassifyFn fn = tlds ? classify_pair_kernel<MODE, true, NT>
-	                           : classify_pair_kernel<MODE, false, NT>;
+	/* the bench's and the iokernel's format, 2-byte verdicts stored
+	 * write-through, compiled in; every other format (and the timing-only
+	 * ablations) reads k.cflags.  25 % fewer static VALU instructions and
+	 * SGPR spills 27 -> 8, but the working-set row is unchanged (96.5-97.3
+	 * us, profiles/r03_ws_ab_vf2.jsonl): the loop is not bound by them */
+	const bool v2 = (k.cflags & GCL_CFG_VERDICT2) && k.nt_store == 2 && !k.ablate;
+	const ClassifyFn fn = v2 ? (tlds ? classify_pair_kernel<MODE, true, NT, 2>
+	                                 : classify_pair_kernel<MODE, false, NT, 2>)
+	                         : (tlds ? classify_pair_kernel<MODE, true, NT, 0>
+	                                 : classify_pair_kernel<MODE, false, NT, 0>);
 	return launch_fn(fn, NT, k, lds, num_cus, bpc_cap, s);
 }
 

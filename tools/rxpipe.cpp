@@ -6,12 +6,15 @@
 // sustains with the GPU classifying, to set beside the reference's own
 // classify + lrpc_send rate on one core (bench.py cpu_baseline.lrpc_1core_mpps).
 //
-//   rxpipe <burst> <workers> <depth> <bursts> [copy]   -> one JSON line
+//   rxpipe <burst> <workers> <depth> <bursts> [copy|inline]   -> one JSON line
 //
 // Each burst's verdicts are read in place in the loop's ring slot
 // (gcl_rxloop_peek + gcl_host_deliver_recs, then gcl_rxloop_release); with
 // the fifth argument `copy` they are copied out first (gcl_rxloop_wait +
-// gcl_host_deliver4), the round-2 form.
+// gcl_host_deliver4), the round-2 form; with `inline` the submitting core
+// copies each frame's 64-B header granule into the slot
+// (GCL_LOOP_INLINE_HDRS: the core reads the headers, as rx_one_pkt does, and
+// the kernel saves a PCIe round trip).
 // Runtime consumers are emulated as infinitely fast and are never touched by
 // the dataplane loop: each ring's recv_head_wb points at its own send_head,
 // so when a ring looks full the producer's refresh (__lrpc_send,
@@ -48,6 +51,7 @@ int main(int argc, char **argv)
 	const uint32_t depth = argc > 3 ? (uint32_t)atoi(argv[3]) : 1;
 	const uint32_t nbursts = argc > 4 ? (uint32_t)atoi(argv[4]) : 20000;
 	const bool copy_out = argc > 5 && !strcmp(argv[5], "copy");
+	const bool inline_hdrs = argc > 5 && !strcmp(argv[5], "inline");
 	const uint32_t R = 16, T = 8, RING = 4096;
 	const uint64_t nframes = 1 << 16, stride = 64;
 	if (!burst || burst > 4096 || !workers || workers > 16 || !depth || depth > 64) {
@@ -115,6 +119,7 @@ int main(int argc, char **argv)
 	lc.lifetime_ms = 60000;
 	lc.region = region;
 	lc.region_len = nframes * stride;
+	lc.flags = inline_hdrs ? GCL_LOOP_INLINE_HDRS : 0;
 	struct gcl_rxloop *loop;
 	int ret = gcl_rxloop_start(ctx, &lc, &loop);
 	if (ret) {
@@ -199,7 +204,9 @@ int main(int argc, char **argv)
 	       "\"mpps_one_core\": %.2f, "
 	       "\"burst_latency_p50_us\": %.2f, \"burst_latency_p99_us\": %.2f, "
 	       "\"deliver_ns_per_pkt\": %.2f, \"delivered_check\": \"%s\", \"unicast_fail\": %llu}\n",
-	       burst, workers, depth, nbursts, copy_out ? "copied out" : "read in place", pkts / (el * 1e-3), lat[lat.size() / 2] * 1e-3,
+	       burst, workers, depth, nbursts,
+	       copy_out ? "copied out" : inline_hdrs ? "read in place, headers inlined in the slot" : "read in place",
+	       pkts / (el * 1e-3), lat[lat.size() / 2] * 1e-3,
 	       lat[lat.size() * 99 / 100] * 1e-3, t_deliver / pkts,
 	       delivered == (uint64_t)burst * (nbursts + warm) ? "ok" : "MISMATCH",
 	       (unsigned long long)stats[GCL_RX_UNICAST_FAIL]);
