@@ -114,7 +114,8 @@ struct KParams {
 	 * daddr, 2 no IP lookup, 4 no histogram add, 8 no flow_tbl read, 16 no
 	 * classification (the membench tile body), 64 no counter flush, 128 no
 	 * rx_one_pkt in classify_quad_kernel (the register loop alone), 256
-	 * dummy loads on one shared address (side_dummy) */
+	 * dummy loads on one shared address (side_dummy), 512 no verdict
+	 * stores (classify_pair_kernel) */
 	uint32_t ablate;
 	uint2 *trans;    /* struct gcl_trans[n] or NULL */
 	uint32_t off_seed, off_crc;
@@ -1292,11 +1293,16 @@ classify_pair_kernel(KParams k)
 			const uint64_t i = tt * NT + tid;
 			/* this packet's frame offset, for the ARP target's extra read */
 			const uint64_t foff = (my >> 63) ? (my & ~kPairBytewise) : my - 8;
-			if (!VF && (k.ablate & 128)) /* timing only: the loop without rx_one_pkt */
+			if (!VF && (k.ablate & 128)) { /* timing only: the loop without rx_one_pkt */
 				put_verdict_vf<VF>(k, i, h.d3 ^ h.d7 ^ h.d9 ^ pr[0] ^ pr[1]);
-			else
-				put_verdict_vf<VF>(k, i, classify_core<MODE, true, false, true, VF>(
-				                                 k, h, nullptr, tid, i, tb, hist, cnt, 0, 40, pr, foff));
+			} else {
+				const uint64_t w = classify_core<MODE, true, false, true, VF>(
+				        k, h, nullptr, tid, i, tb, hist, cnt, 0, 40, pr, foff);
+				if (VF || !(k.ablate & 512)) /* 512: timing only, no verdict stores */
+					put_verdict_vf<VF>(k, i, w);
+				else
+					cnt.flowtag += (uint32_t)w == 0xFFFFFFFFu; /* keep w live */
+			}
 		}
 	};
 
