@@ -151,9 +151,10 @@ def test_gpu_group_shards_two_contexts(g, orc, vbytes):
     grp.close()
 
 
+@pytest.mark.parametrize("nstreams", [1, 4])
 @pytest.mark.parametrize("mode", ["zerocopy", "copy"])
 @pytest.mark.parametrize("layout", ["slots1536", "offs"])
-def test_gpu_group_classify_host_split(g, orc, mode, layout):
+def test_gpu_group_classify_host_split(g, orc, mode, layout, nstreams):
     """One host batch split round-robin by the C splitter over two contexts:
     the verdicts land at their batch positions and equal the oracle's; the
     node-wide counts and counters equal the oracle's (NIC mode with ol_flags
@@ -177,7 +178,7 @@ def test_gpu_group_classify_host_split(g, orc, mode, layout):
             o = int(offs[i])
             frames[o:o + 64] = hdr[i * 64:(i + 1) * 64]
     hv = pinned(np.zeros(n, dtype=g.VERDICT_DTYPE))
-    grp = g.Group([0, 0], R, g.HASH_NIC, block=B, exchange=g.XCHG_HOST)
+    grp = g.Group([0, 0], R, g.HASH_NIC, block=B, exchange=g.XCHG_HOST, nstreams=nstreams)
     tables(grp)
     grp.classify_host(pinned(frames), n, stride, verdicts=hv,
                       offs=None if offs is None else pinned(offs), olflags=pinned(olf),

@@ -1057,3 +1057,54 @@ def test_gpu_ip_hdr_supported_reference(g):
     got = (v["action"] & g.ACT_F_TRANS) != 0
     want = np.array([h["supported"] for h in d["headers"]])
     assert (got == want).all(), np.nonzero(got != want)[0][:5]
+
+
+@pytest.mark.parametrize("pattern", ["arp", "ipv4"])
+@pytest.mark.parametrize("kernel", ["pair", "tile", "quad"])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_gpu_general_frames_at_the_end(g, orc, monkeypatch, kernel, mode, pattern):
+    """Frames at every byte offset from 80 bytes before frames_len to 8
+    past it, over a tail whose bytes repeat 08 06 (ARP) or 08 00 (IPv4), so
+    every other offset parses as that Ethertype and its destination (the ARP
+    target at bytes 38-41, daddr at 30-33) is a registered runtime -- until
+    the bytes it needs run past frames_len and read 0 (the build's rule; the
+    bytes behind frames_len hold 0xEE).  This walks the pair kernel from its
+    16-B loads of [8, 40) to bytewise reads, the ARP target from one dword
+    load to bytewise, and the other GENERAL kernels' windows and line cuts,
+    each against the oracle."""
+    rng = np.random.default_rng(4400 + mode + 10 * ["pair", "tile", "quad"].index(kernel)
+                                + 100 * (pattern == "ipv4"))
+    R = 16
+    unit = b"\x08\x06" if pattern == "arp" else b"\x08\x00"
+    word = int.from_bytes(unit * 2, "big")  # the IP the pattern reads as, host order
+    ips = [word, int.from_bytes(unit[::-1] * 2, "big")] + [0x0A000001 + r for r in range(R - 2)]
+    flen = 4096 + 37
+    frames = np.full(flen + 256, 0xEE, dtype=np.uint8)
+    frames[:flen] = rng.integers(0, 256, size=flen, dtype=np.uint8)
+    frames[flen - 96:flen] = np.frombuffer(unit * 48, dtype=np.uint8)
+    offs = np.arange(flen - 80, flen + 8, dtype=np.uint64)
+    offs = np.concatenate([offs, offs[::-1]])
+    n = len(offs)
+    olf = rng.integers(0, 16, size=n, dtype=np.uint8)
+    rss = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
+    t = orc.Tables(R, mode, 0, 0x09)
+    for r, ip in enumerate(ips):
+        assert t.runtime_set(r, ip, 4, 4, [0, 1, 2, 3]) == 0
+    env = {"pair": {"GCL_TUNE_PAIR": "1"}, "tile": {"GCL_TUNE_PAIR": "0"},
+           "quad": {"GCL_TUNE_QUAD": "1"}}[kernel]
+    for kk, vv in env.items():
+        monkeypatch.setenv(kk, vv)
+    try:
+        clf = g.Classifier(0, R, mode, 0, 0x09)
+    finally:
+        for kk in env:
+            monkeypatch.delenv(kk)
+    for r, ip in enumerate(ips):
+        clf.runtime_set(r, ip, 4, 4, [0, 1, 2, 3])
+    ve, ce, se = t.classify(frames, n, 0, offs=offs, olflags=olf, rss=rss, frames_len=flen)
+    v, c, st = gpu_run(g, clf, frames, n, 0, offs=offs, olflags=olf, rss=rss, frames_len=flen)
+    assert_same(v, ve, f"{kernel} mode={mode} {pattern} at the end")
+    assert (c == ce).all() and (st == se).all()
+    acts = ve["action"] & 0x3F
+    # both outcomes occur: registered destinations, and ones cut by frames_len
+    assert (acts == g.ACT_DELIVER).sum() > 10 and (acts == g.ACT_DROP_UNREG).sum() > 4
