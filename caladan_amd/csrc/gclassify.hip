@@ -39,10 +39,6 @@ constexpr uint32_t kToepBytes = 12 * 256 * 4;
 constexpr uint32_t kCrcBytes = 8 * 256 * 4;
 constexpr uint32_t kLdsTableBudget = 96 * 1024;
 constexpr int kImgUsers = 8;             /* streams tracked per table image */
-/* GCL_TUNE_QUAD default: GENERAL batches on classify_kernel.  The
- * register-header classify_quad_kernel measured equal or 1-3 % slower on the
- * ingress rows (profiles/r02_quad_ab.jsonl), so it stays an experiment. */
-constexpr int kDefaultQuad = 0;
 /* GCL_TUNE_PAIR default: GENERAL batches on classify_pair_kernel.  Against
  * the LDS-tile classify_kernel, alternating in one process
  * (profiles/r03_general_ab.jsonl, r03_ws_ab.jsonl): the cache-resident
@@ -113,7 +109,7 @@ struct KParams {
 	/* GCL_TUNE_ABLATE, timing-only experiments with wrong results: 1 hash =
 	 * daddr, 2 no IP lookup, 4 no histogram add, 8 no flow_tbl read, 16 no
 	 * classification (the membench tile body), 64 no counter flush, 128 no
-	 * rx_one_pkt in classify_quad_kernel (the register loop alone), 256
+	 * rx_one_pkt in classify_pair_kernel (the register loop alone), 256
 	 * dummy loads on one shared address (side_dummy), 512 no verdict
 	 * stores (classify_pair_kernel) */
 	uint32_t ablate;
@@ -417,7 +413,7 @@ struct HdrWords {
  * rx_one_pkt on the header dwords @h of packet @idx (rx.c:116-233).  Frame
  * bytes [0, @avail) were staged with shift @sh (hdr_window); @tile (REG
  * false) holds them in row @tid for the IHL != 5 port reads, which REG
- * (classify_quad_kernel: headers in registers) reads from the frame instead.
+ * (classify_pair_kernel: headers in registers) reads from the frame instead.
  */
 /* VF: the verdict format when known at compile time (2: GCL_CFG_VERDICT2,
  * which excludes the transport pre-hash), 0: read from k.cflags */
@@ -962,200 +958,10 @@ classify_kernel(KParams k)
 	flush_counters<NT>(k, hist, cnt);
 }
 
-/* ------------------------------------------------------------------------
- * classify_quad_kernel: the GENERAL path (frames at per-packet offsets) with
- * the headers kept in registers.  Each wave owns 64 packets of every tile
- * and never waits for the other waves: no LDS header tile, no barriers.
- *
- * Lane l of a wave classifies packet l.  The header loads stay coalesced per
- * frame: load j of lane l reads 16-B chunk (l & 3) of packet (l & ~3) + j,
- * so each quad of lanes reads one whole 64-B window per load.  A 4 x 4
- * transpose inside the quad (two DPP exchange steps) then gives every lane
- * its own packet's four chunks.  The quad learns where its packets' windows
- * are from each lane's hdr_src by DPP broadcast.  Offsets, ol_flags and
- * hash.rss are loaded DEPTH (2) tiles / one tile ahead, every load on every
- * path (dummy addresses for what is absent), so each wait counts exactly
- * the loads issued after the ones it needs (classify_kernel's rule).
- */
-template <int CTRL>
-__device__ __forceinline__ uint32_t qdpp(uint32_t v)
-{
-	return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
-}
-
-template <int CTRL>
-__device__ __forceinline__ uint4 qdpp4(const uint4 &v)
-{
-	return make_uint4(qdpp<CTRL>(v.x), qdpp<CTRL>(v.y), qdpp<CTRL>(v.z), qdpp<CTRL>(v.w));
-}
-
+/* Lane-wise select of two 16-B values (classify_pair_kernel's exchange). */
 __device__ __forceinline__ uint4 sel4(bool c, const uint4 &a, const uint4 &b)
 {
 	return make_uint4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
-}
-
-/* r[j] = chunk (lane & 3) of quad packet j  ->  r[c] = chunk c of packet (lane & 3) */
-__device__ __forceinline__ void quad_transpose(uint4 r[4])
-{
-	const bool odd = threadIdx.x & 1, hi = threadIdx.x & 2;
-	/* quad_perm [1,0,3,2]: exchange with lane ^ 1 */
-	const uint4 x0 = qdpp4<0xB1>(sel4(odd, r[0], r[1]));
-	const uint4 x1 = qdpp4<0xB1>(sel4(odd, r[2], r[3]));
-	r[0] = sel4(odd, x0, r[0]);
-	r[1] = sel4(odd, r[1], x0);
-	r[2] = sel4(odd, x1, r[2]);
-	r[3] = sel4(odd, r[3], x1);
-	/* quad_perm [2,3,0,1]: exchange with lane ^ 2 */
-	const uint4 y0 = qdpp4<0x4E>(sel4(hi, r[0], r[2]));
-	const uint4 y1 = qdpp4<0x4E>(sel4(hi, r[1], r[3]));
-	r[0] = sel4(hi, y0, r[0]);
-	r[2] = sel4(hi, r[2], y0);
-	r[1] = sel4(hi, y1, r[1]);
-	r[3] = sel4(hi, r[3], y1);
-}
-
-/* load j of this lane: chunk (lane & 3) of the quad's packet j, whose
- * hdr_src lane j of the quad holds in @my */
-template <int J>
-__device__ __forceinline__ uint4 quad_chunk_load(const KParams &k, const uint4 &my)
-{
-	constexpr int B = J * 0x55; /* quad_perm [J,J,J,J]: broadcast */
-	const uint32_t bx = qdpp<B>(my.x), by = qdpp<B>(my.y), bw = qdpp<B>(my.z);
-	const uint32_t q16 = (threadIdx.x & 3) * 16;
-	const bool use = bw > 0xFF && q16 < (bw >> 8);
-	const uint64_t a = ((uint64_t)by << 32 | bx) + (use ? q16 : 0);
-	return gcl::load16_nt(bw > 0xFF && !(k.ablate & 256) ? k.frames + a : use ? k.frames + a : k.tables);
-}
-
-/* the header dwords of frame bytes 12 + 4i (+ 4 @ds dwords of window shift) */
-template <int I>
-__device__ __forceinline__ uint32_t hdr_word(const uint32_t w[16], uint32_t ds)
-{
-	return ds == 0 ? w[I] : ds == 1 ? w[I + 1] : ds == 2 ? w[I + 2] : w[I + 3];
-}
-
-template <int MODE, bool TLDS, int NT>
-__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4)))
-classify_quad_kernel(KParams k)
-{
-	extern __shared__ uint4 smem[];
-	uint32_t *hist = (uint32_t *)smem;
-	uint8_t *lds_tab = (uint8_t *)(hist + ((k.max_rt + 3) & ~3u));
-	const int tid = threadIdx.x;
-	for (uint32_t i = tid; i < k.max_rt; i += NT)
-		hist[i] = 0;
-	const uint8_t *tab = TLDS ? lds_tab : k.tables;
-	if (TLDS) {
-		const uint4 *src = (const uint4 *)k.tables;
-		uint4 *dst = (uint4 *)lds_tab;
-		for (uint32_t i = tid; i < k.tables_lds_bytes / 16; i += NT)
-			dst[i] = src[i];
-	}
-	Tables tb;
-	tb.ipt = (const uint2 *)tab;
-	tb.rtab = (const RtEntry *)(tab + k.off_rt);
-	tb.flow = tab + k.off_flow;
-	tb.toep = (const uint32_t *)(tab + k.off_toep);
-	tb.seed = (const uint32_t *)(tab + k.off_seed);
-	tb.crc = (const uint32_t *)(tab + k.off_crc);
-	__syncthreads();
-
-	Counters cnt = {0, 0, 0, 0};
-	const uint64_t step = gridDim.x;
-	const uint64_t *offs_src = k.offs ? k.offs : (const uint64_t *)k.tables;
-	auto ok = [&](uint64_t tt) { return tt < k.ntiles && tt * NT + tid < k.n; };
-	auto ld_off = [&](uint64_t tt) -> uint64_t {
-		return offs_src[k.offs && ok(tt) ? tt * NT + tid : 0];
-	};
-	auto src_of = [&](uint64_t tt, uint64_t raw) -> uint4 {
-		return hdr_src(k, !ok(tt) ? kNoOff : k.offs ? raw : (tt * NT + tid) * k.stride);
-	};
-	auto pref = [&](uint64_t tt, uint32_t pr[2]) {
-		const uint64_t i = ok(tt) ? tt * NT + tid : 0;
-		pr[0] = *(k.olflags ? k.olflags + i : side_dummy<uint8_t>(k, i));
-		if (MODE == GCL_HASH_NIC)
-			pr[1] = *(k.rss ? k.rss + i : side_dummy<uint32_t>(k, i));
-	};
-	auto issue = [&](const uint4 &my, uint4 r[4]) {
-		r[0] = quad_chunk_load<0>(k, my);
-		r[1] = quad_chunk_load<1>(k, my);
-		r[2] = quad_chunk_load<2>(k, my);
-		r[3] = quad_chunk_load<3>(k, my);
-	};
-	/* the landed chunks of the tile whose own hdr_src is @my -> this lane's
-	 * header dwords, staged shift and staged byte count */
-	auto unpack = [&](uint4 r[4], const uint4 &my, HdrWords &h, uint32_t &sh, uint32_t &avail) {
-		quad_transpose(r);
-		sh = 0;
-		avail = 64;
-		if (my.z > 0xFF) {
-			sh = my.z & 0xFF;
-			avail = (my.z >> 8) - sh;
-		} else if (my.z == 0xFF) { /* bytewise frame (rare): all 64 bytes from its start */
-			const uint64_t off = (uint64_t)my.y << 32 | my.x;
-			for (int c = 0; c < 4; c++)
-				r[c] = load16_bytes(k, off + 16 * c);
-		}
-		const uint32_t w[16] = {r[0].x, r[0].y, r[0].z, r[0].w, r[1].x, r[1].y, r[1].z, r[1].w,
-		                        r[2].x, r[2].y, r[2].z, r[2].w, r[3].x, r[3].y, r[3].z, r[3].w};
-		const uint32_t ds = sh >> 2; /* a window shift is 0, 4, 8 or 12 bytes */
-		h.d3 = hdr_word<3>(w, ds);
-		h.d5 = hdr_word<5>(w, ds);
-		h.d6 = hdr_word<6>(w, ds);
-		h.d7 = hdr_word<7>(w, ds);
-		h.d8 = hdr_word<8>(w, ds);
-		h.d9 = hdr_word<9>(w, ds);
-		h.d10 = hdr_word<10>(w, ds);
-	};
-	auto classify = [&](uint64_t tt, const HdrWords &h, uint32_t sh, uint32_t avail,
-	                    const uint32_t pr[2]) {
-		if (ok(tt)) {
-			const uint64_t i = tt * NT + tid;
-			if (k.ablate & 128) /* timing only: the loop without rx_one_pkt */
-				put_verdict(k, i, h.d3 ^ h.d7 ^ h.d10 ^ pr[0] ^ pr[1] ^ sh ^ avail);
-			else
-				put_verdict(k, i, classify_core<MODE, true, false, true>(k, h, nullptr, tid, i,
-				                                                          tb, hist, cnt, sh,
-				                                                          avail, pr));
-		}
-	};
-
-	uint64_t t = blockIdx.x;
-	uint4 ra[4], rb[4];
-	uint32_t pra[2] = {0, 0}, prb[2] = {0, 0};
-	/* prologue: tiles t and t + step in flight, offsets of the two after */
-	uint64_t oa = ld_off(t), ob = ld_off(t + step);
-	uint4 sa = src_of(t, oa);
-	issue(sa, ra);
-	pref(t, pra);
-	oa = ld_off(t + 2 * step);
-	uint4 sb = src_of(t + step, ob);
-	issue(sb, rb);
-	pref(t + step, prb);
-	ob = ld_off(t + 3 * step);
-	while (t < k.ntiles) {
-		asm volatile("" : "+s"(t));
-		HdrWords h;
-		uint32_t sh, avail;
-		unpack(ra, sa, h, sh, avail);
-		sa = src_of(t + 2 * step, oa);
-		issue(sa, ra);
-		classify(t, h, sh, avail, pra);
-		pref(t + 2 * step, pra);
-		oa = ld_off(t + 4 * step);
-		t += step;
-		/* runs past ntiles too (dummy loads, nothing classified): a path
-		 * out of the middle would change the wait counts (classify_kernel) */
-		unpack(rb, sb, h, sh, avail);
-		sb = src_of(t + 2 * step, ob);
-		issue(sb, rb);
-		classify(t, h, sh, avail, prb);
-		pref(t + 2 * step, prb);
-		ob = ld_off(t + 4 * step);
-		t += step;
-	}
-	__syncthreads(); /* every wave's histogram adds are in */
-	flush_counters<NT>(k, hist, cnt);
 }
 
 /* ------------------------------------------------------------------------
@@ -1809,7 +1615,6 @@ struct gcl_ctx {
 	int tune_ablate;   /* GCL_TUNE_ABLATE bitmask (timing experiments only) */
 	int tune_sched;    /* GCL_TUNE_SCHED: 0 static persistent grid, 1 dynamic tile queue */
 	int tune_xcd_map;  /* GCL_TUNE_XCD_MAP: 1 contiguous eighth per XCD, 0 round-robin tiles */
-	int tune_quad;     /* GCL_TUNE_QUAD: 1 GENERAL batches on classify_quad_kernel, 0 classify_kernel */
 	int tune_pair;     /* GCL_TUNE_PAIR: 1 GENERAL batches on classify_pair_kernel */
 	/* dynamic tile queue: one slot per launch in flight, reused in turn; a
 	 * launch waits for the previous user of its slot (same or other stream) */
@@ -1894,8 +1699,6 @@ extern "C" int gcl_open(int hip_device, const struct gcl_cfg *cfg, struct gcl_ct
 		c->tune_sched = e ? atoi(e) : kDefaultSched;
 		e = getenv("GCL_TUNE_XCD_MAP");
 		c->tune_xcd_map = e ? atoi(e) : kDefaultXcdMap;
-		e = getenv("GCL_TUNE_QUAD");
-		c->tune_quad = e ? atoi(e) : kDefaultQuad;
 		e = getenv("GCL_TUNE_PAIR");
 		c->tune_pair = e ? atoi(e) : kDefaultPair;
 	}
@@ -2230,15 +2033,6 @@ static hipError_t launch_nt(const KParams &k, bool tlds, bool general, uint32_t 
 }
 
 template <int MODE, int NT>
-static hipError_t launch_quad(const KParams &k, bool tlds, uint32_t lds, int num_cus, int bpc_cap,
-                              hipStream_t s)
-{
-	const ClassifyFn fn = tlds ? classify_quad_kernel<MODE, true, NT>
-	                           : classify_quad_kernel<MODE, false, NT>;
-	return launch_fn(fn, NT, k, lds, num_cus, bpc_cap, s);
-}
-
-template <int MODE, int NT>
 static hipError_t launch_pair(const KParams &k, bool tlds, uint32_t lds, int num_cus, int bpc_cap,
                               hipStream_t s)
 {
@@ -2260,7 +2054,6 @@ struct Geometry {
 	int threads;  /* packets per tile = lanes per block */
 	int depth;    /* tiles in flight per block */
 	int bpc_cap;  /* blocks per CU */
-	bool quad;    /* classify_quad_kernel (GENERAL batches): no LDS header tile */
 	bool pair;    /* classify_pair_kernel (GENERAL batches): [8, 40) per packet by lane pairs */
 };
 
@@ -2281,14 +2074,6 @@ static hipError_t launch_mode(const KParams &k, bool tlds, bool general, const G
 		if (geo.threads == 512)
 			return launch_pair<MODE, 512>(k, tlds, lds, num_cus, geo.bpc_cap, s);
 		return launch_pair<MODE, 256>(k, tlds, lds, num_cus, geo.bpc_cap, s);
-	}
-	if (geo.quad) {
-		const uint32_t lds = hist_bytes + tab_lds;
-		if (geo.threads == 1024)
-			return launch_quad<MODE, 1024>(k, tlds, lds, num_cus, geo.bpc_cap, s);
-		if (geo.threads == 512)
-			return launch_quad<MODE, 512>(k, tlds, lds, num_cus, geo.bpc_cap, s);
-		return launch_quad<MODE, 256>(k, tlds, lds, num_cus, geo.bpc_cap, s);
 	}
 	const uint32_t lds = (uint32_t)geo.threads * 64 + kLdsQueueBytes + hist_bytes + tab_lds +
 	                     offs_lds_bytes(general, (uint32_t)geo.threads);
@@ -2322,17 +2107,19 @@ static Geometry choose_geometry(const gcl_ctx *c, uint32_t tab_lds, uint32_t his
 	g.depth = 1;
 	g.threads = 0;
 	/* GENERAL batches run on the lane-pair classify_pair_kernel by default
-	 * (kDefaultPair 1), on the register-header classify_quad_kernel with
-	 * GCL_TUNE_QUAD=1, and on the LDS-tile classify_kernel with
+	 * (kDefaultPair 1), and on the LDS-tile classify_kernel with
 	 * GCL_TUNE_PAIR=0 -- or whenever the dynamic tile queue
 	 * (GCL_TUNE_SCHED), depth 1 (GCL_TUNE_DEPTH=1) or the membench body
-	 * (GCL_TUNE_ABLATE bit 16) is asked for, which only it implements */
-	g.quad = general && c->tune_quad && !c->tune_sched && c->tune_depth != 1 &&
-	         !(c->tune_ablate & 16);
-	g.pair = general && !g.quad && c->tune_pair && !c->tune_sched && c->tune_depth != 1 &&
+	 * (GCL_TUNE_ABLATE bit 16) is asked for, which only it implements.
+	 * (Round 2's register-header classify_quad_kernel, 64-B windows
+	 * transposed across lane quads, was removed in round 3: the pair kernel
+	 * does the same without the window, and beat it on every row --
+	 * working set 96 vs 109-111 us, random pool 181 vs 189,
+	 * profiles/r03_ws_ab.jsonl.) */
+	g.pair = general && c->tune_pair && !c->tune_sched && c->tune_depth != 1 &&
 	         !(c->tune_ablate & 16);
 	auto per_block = [&](uint32_t nt) -> uint32_t {
-		if (g.quad || g.pair)
+		if (g.pair)
 			return hist_bytes + tab_lds;
 		return nt * 64 + kLdsQueueBytes + hist_bytes + tab_lds + offs_lds_bytes(general, nt);
 	};

@@ -135,15 +135,14 @@ def test_gpu_fuzz_misaligned_offsets(g, orc, misalign, mode):
     assert (tr == tre).all() and (c == ce).all() and (st == se).all()
 
 
-@pytest.mark.parametrize("kernel", ["quad", "tile", "pair"])
+@pytest.mark.parametrize("kernel", ["tile", "pair"])
 @pytest.mark.parametrize("tables", ["lds", "global"])
 @pytest.mark.parametrize("misalign", ["mbuf", "mixed", "lineend"])
 @pytest.mark.parametrize("mode", [0, 1, 2])
 def test_gpu_general_kernels_fuzz(g, orc, monkeypatch, misalign, mode, tables, kernel):
     """Every GENERAL kernel on the misaligned-offset fuzz, each forced by its
-    knob: the lane-pair kernel (classify_pair_kernel, the default), the
-    LDS-tile kernel (classify_kernel, GCL_TUNE_PAIR=0) and the register-header
-    kernel (classify_quad_kernel, GCL_TUNE_QUAD=1).  Window shifts of 0-12
+    knob: the lane-pair kernel (classify_pair_kernel, the default) and the
+    LDS-tile kernel (classify_kernel, GCL_TUNE_PAIR=0).  Window shifts of 0-12
     bytes, frames that are not 4-B aligned (bytewise), headers cut at the
     first line end, frames straddling frames_len, IHL > 5 ports and ARP
     target IPs read from the frame, loopback hints, FDIR marks and the
@@ -158,8 +157,8 @@ def test_gpu_general_kernels_fuzz(g, orc, monkeypatch, misalign, mode, tables, k
     key = bytes(rng.integers(0, 256, size=40, dtype=np.uint8))
     t = orc.Tables(1024, mode, g.CFG_TRANS_HASH, 0x09, key)
     apply_runtimes(t, rts)
-    env = {{"quad": "GCL_TUNE_QUAD", "tile": "GCL_TUNE_PAIR", "pair": "GCL_TUNE_PAIR"}[kernel]:
-           "0" if kernel == "tile" else "1", **({"GCL_TUNE_TABLES": "1"} if tables == "global" else {})}
+    env = {"GCL_TUNE_PAIR": "0" if kernel == "tile" else "1",
+           **({"GCL_TUNE_TABLES": "1"} if tables == "global" else {})}
     for kk, vv in env.items():
         monkeypatch.setenv(kk, vv)
     try:
@@ -900,10 +899,10 @@ LOOP_GEOMETRIES = [
     {"GCL_TUNE_DEPTH": "1", "GCL_TUNE_GRID": "5"},
     {"GCL_TUNE_SCHED": "1"},
     {"GCL_TUNE_THREADS": "1024", "GCL_TUNE_GRID": "7"},
-    {"GCL_TUNE_QUAD": "1"},
-    {"GCL_TUNE_QUAD": "1", "GCL_TUNE_GRID": "3"},
-    {"GCL_TUNE_QUAD": "1", "GCL_TUNE_THREADS": "512", "GCL_TUNE_GRID": "5"},
-    {"GCL_TUNE_QUAD": "1", "GCL_TUNE_THREADS": "1024", "GCL_TUNE_GRID": "7"},
+    {"GCL_TUNE_PAIR": "0"},
+    {"GCL_TUNE_PAIR": "0", "GCL_TUNE_GRID": "3"},
+    {"GCL_TUNE_PAIR": "0", "GCL_TUNE_THREADS": "512", "GCL_TUNE_GRID": "5"},
+    {"GCL_TUNE_PAIR": "2", "GCL_TUNE_GRID": "7"},
 ]
 
 
@@ -914,8 +913,9 @@ def test_gpu_loop_geometries(g, orc, monkeypatch, geo, general):
     blocks walking many tiles (odd counts per block, so the second half of the
     DEPTH-2 loop runs past the end as an empty tile), the per-XCD contiguous
     walk (a block's walk ends inside the batch), DEPTH 1, the dynamic tile
-    queue, 512/1024-lane tiles and the register-header GENERAL kernel
-    (GCL_TUNE_QUAD=1, dense slots keep the tile kernel); dense slots, per-frame offsets with
+    queue, 512/1024-lane tiles, the lane-pair GENERAL kernel (the default)
+    and the LDS-tile one (GCL_TUNE_PAIR=0; dense slots keep the dense tile
+    kernel either way); dense slots, per-frame offsets with
     ol_flags / hash.rss (NIC mode), and fixed slots with ol_flags / hash.rss
     and a buffer ending inside the last frame ("stride": the GENERAL path
     without offs[]), ragged n.  Same verdicts, counts, stats."""
@@ -1060,7 +1060,7 @@ def test_gpu_ip_hdr_supported_reference(g):
 
 
 @pytest.mark.parametrize("pattern", ["arp", "ipv4"])
-@pytest.mark.parametrize("kernel", ["pair", "tile", "quad"])
+@pytest.mark.parametrize("kernel", ["pair", "tile"])
 @pytest.mark.parametrize("mode", [0, 1])
 def test_gpu_general_frames_at_the_end(g, orc, monkeypatch, kernel, mode, pattern):
     """Frames at every byte offset from 80 bytes before frames_len to 8
@@ -1090,8 +1090,7 @@ def test_gpu_general_frames_at_the_end(g, orc, monkeypatch, kernel, mode, patter
     t = orc.Tables(R, mode, 0, 0x09)
     for r, ip in enumerate(ips):
         assert t.runtime_set(r, ip, 4, 4, [0, 1, 2, 3]) == 0
-    env = {"pair": {"GCL_TUNE_PAIR": "1"}, "tile": {"GCL_TUNE_PAIR": "0"},
-           "quad": {"GCL_TUNE_QUAD": "1"}}[kernel]
+    env = {"pair": {"GCL_TUNE_PAIR": "1"}, "tile": {"GCL_TUNE_PAIR": "0"}}[kernel]
     for kk, vv in env.items():
         monkeypatch.setenv(kk, vv)
     try:

@@ -12,7 +12,6 @@ opened with different GCL_TUNE_* knobs, one process, interleaved rounds:
                      header windows and LDS staging; no classification
   no_lookups         GCL_TUNE_ABLATE=2|4|8: no IP lookup, histogram, flow_tbl
   no_flush           GCL_TUNE_ABLATE=64: no counter flush at the end
-  quad               GCL_TUNE_QUAD=1: the register-header kernel
   extra rows from argv as name=ENV:VAL,ENV:VAL
 
 Timing-only rows (ablations) give wrong verdicts on purpose.
@@ -30,8 +29,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from bench import SEED, WORKLOADS, g, setup_tables, timed_launches  # noqa: E402
 
 ROWS = [("default", {}), ("tile", {"GCL_TUNE_PAIR": "0"}), ("loads_only", {"GCL_TUNE_ABLATE": "16"}),
-        ("no_lookups", {"GCL_TUNE_ABLATE": "14"}), ("no_flush", {"GCL_TUNE_ABLATE": "64"}),
-        ("quad", {"GCL_TUNE_QUAD": "1"})]
+        ("no_lookups", {"GCL_TUNE_ABLATE": "14"}), ("no_flush", {"GCL_TUNE_ABLATE": "64"})]
 
 
 def main(rounds=3, extra=()):
