@@ -25,9 +25,10 @@ PKTS = {"udp64": 32 << 20, "tcp1500": 8 << 20, "mixed": 1 << 20, "ingress_nic": 
 # per-packet bytes besides the 64-B header and the verdict: the integrated
 # ingress shape reads a u64 offset, u8 ol_flags and u32 hash.rss per descriptor
 EXTRA = {"ingress_nic": 8 + 1 + 4, "ingress_ws": 8 + 1 + 4}
-# which classify_kernel instance is the workload's: the ingress run also
-# launches the JENKINS (MODE 1) row; its NIC launches are MODE 0
-KNAME = {"ingress_nic": "classify_kernel<0,", "ingress_ws": "classify_kernel<0,"}
+# which kernel instance is the workload's: the ingress rows run NIC mode (MODE
+# 0) on the GENERAL kernel -- classify_pair_kernel<0, ...> since round 3,
+# classify_kernel<0, ...> before -- and tools/ingress_run.py launches one row
+KNAME = {"ingress_nic": "_kernel<0,", "ingress_ws": "_kernel<0,"}
 
 
 def is_kernel(wl, name):
