@@ -246,6 +246,19 @@ __device__ __forceinline__ uint4 load16_bytes(const KParams &k, uint64_t a)
  * shift | staged frame bytes << 8, for classify_one; bits 16-19 flag this
  * lane's chunks of bytewise frames, which patch_tile fills in after staging.
  */
+/* The tile kernel's 16-B frame loads: with the streaming hint (measured
+ * faster for the dense HBM stream); GCL_TILE_LOAD_PLAIN builds
+ * the plain-load variant for A/B runs (tools/dense_ab.sh). */
+__device__ __forceinline__ uint4 tile_load(const void *p)
+{
+#ifdef GCL_TILE_LOAD_PLAIN
+	const uint4 v = *(const uint4 *)p;
+	return v;
+#else
+	return gcl::load16_nt(p);
+#endif
+}
+
 template <bool GENERAL, int NT, bool SRC = false>
 __device__ __forceinline__ void load_tile(const KParams &k, uint64_t tile, bool live, uint4 r[4],
                                           uint32_t &span, const uint4 *s_src = nullptr)
@@ -260,7 +273,7 @@ __device__ __forceinline__ void load_tile(const KParams &k, uint64_t tile, bool 
 		for (int j = 0; j < 4; j++) {
 			const uint32_t c = j * NT + threadIdx.x, p = c >> 2;
 			const uint8_t *a = p < lim ? base + (p * (uint32_t)k.stride + (c & 3) * 16) : dummy;
-			r[j] = gcl::load16_nt(a);
+			r[j] = tile_load(a);
 		}
 		return;
 	}
@@ -280,7 +293,7 @@ __device__ __forceinline__ void load_tile(const KParams &k, uint64_t tile, bool 
 		/* past the first line (q16 >= cut): not staged, read on demand */
 		const bool use = e.z > 0xFF && q16 < (e.z >> 8);
 		const uint64_t a = ((uint64_t)e.y << 32 | e.x) + (use ? q16 : 0);
-		r[j] = gcl::load16_nt(e.z > 0xFF && !(k.ablate & 256) ? k.frames + a : use ? k.frames + a : dummy);
+		r[j] = tile_load(e.z > 0xFF && !(k.ablate & 256) ? k.frames + a : use ? k.frames + a : dummy);
 		span |= (uint32_t)(e.z == 0xFF) << (16 + j);
 	}
 }
@@ -1013,14 +1026,16 @@ typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 
 /* load J of this lane: half (lane & 1) of the pair's packet J, whose
  * pair_src lane J of the pair holds in @my (quad_perm broadcast) */
-template <int J>
+template <int J, bool NTL>
 __device__ __forceinline__ uint4 pair_load(const KParams &k, uint64_t my)
 {
 	constexpr int B = J ? 0xF5 : 0xA0; /* quad_perm [1,1,3,3] : [0,0,2,2] */
 	const uint32_t lo = mdpp<B>((uint32_t)my), hi = mdpp<B>((uint32_t)(my >> 32));
 	const uint64_t s = (uint64_t)hi << 32 | lo;
 	const uint8_t *a = (hi >> 31) ? k.tables : k.frames + s + 16 * (threadIdx.x & 1);
-	const u32x4a4 v = __builtin_nontemporal_load((const u32x4a4 *)a);
+	/* plain loads: the frames stay in L2 for the next use of the same mbuf;
+	 * NTL (GCL_TUNE_PAIR_LOADS=1, experiment) adds the streaming hint */
+	const u32x4a4 v = NTL ? __builtin_nontemporal_load((const u32x4a4 *)a) : *(const u32x4a4 *)a;
 	return make_uint4(v.x, v.y, v.z, v.w);
 }
 
@@ -1036,7 +1051,7 @@ __device__ __forceinline__ void pair_exchange(uint4 r[2])
 	r[1] = sel4(odd, r[1], y);
 }
 
-template <int MODE, bool TLDS, int NT, int VF>
+template <int MODE, bool TLDS, int NT, int VF, bool NTL = false>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4)))
 classify_pair_kernel(KParams k)
 {
@@ -1079,8 +1094,8 @@ classify_pair_kernel(KParams k)
 			pr[1] = *(k.rss ? k.rss + i : side_dummy<uint32_t>(k, i));
 	};
 	auto issue = [&](uint64_t my, uint4 r[2]) {
-		r[0] = pair_load<0>(k, my);
-		r[1] = pair_load<1>(k, my);
+		r[0] = pair_load<0, NTL>(k, my);
+		r[1] = pair_load<1, NTL>(k, my);
 	};
 	/* the landed halves -> this lane's header dwords (frame bytes 12-39;
 	 * d10, bytes 40-43, is not fetched: avail 40 sends ARP to the frame) */
@@ -1616,6 +1631,7 @@ struct gcl_ctx {
 	int tune_sched;    /* GCL_TUNE_SCHED: 0 static persistent grid, 1 dynamic tile queue */
 	int tune_xcd_map;  /* GCL_TUNE_XCD_MAP: 1 contiguous eighth per XCD, 0 round-robin tiles */
 	int tune_pair;     /* GCL_TUNE_PAIR: 1 GENERAL batches on classify_pair_kernel */
+	int tune_pair_loads; /* GCL_TUNE_PAIR_LOADS: 1 = the pair kernel's frame loads non-temporal (experiment) */
 	/* dynamic tile queue: one slot per launch in flight, reused in turn; a
 	 * launch waits for the previous user of its slot (same or other stream) */
 	uint32_t *sched;
@@ -1701,6 +1717,8 @@ extern "C" int gcl_open(int hip_device, const struct gcl_cfg *cfg, struct gcl_ct
 		c->tune_xcd_map = e ? atoi(e) : kDefaultXcdMap;
 		e = getenv("GCL_TUNE_PAIR");
 		c->tune_pair = e ? atoi(e) : kDefaultPair;
+		e = getenv("GCL_TUNE_PAIR_LOADS");
+		c->tune_pair_loads = e ? atoi(e) : 0;
 	}
 	c->dimg[0] = c->dimg[1] = nullptr;
 	c->sched = nullptr;
@@ -2034,7 +2052,7 @@ static hipError_t launch_nt(const KParams &k, bool tlds, bool general, uint32_t 
 
 template <int MODE, int NT>
 static hipError_t launch_pair(const KParams &k, bool tlds, uint32_t lds, int num_cus, int bpc_cap,
-                              hipStream_t s)
+                              bool ntl, hipStream_t s)
 {
 	/* the bench's and the iokernel's format, 2-byte verdicts stored
 	 * write-through, compiled in; every other format (and the timing-only
@@ -2042,10 +2060,12 @@ static hipError_t launch_pair(const KParams &k, bool tlds, uint32_t lds, int num
 	 * SGPR spills 27 -> 8, but the working-set row is unchanged (96.5-97.3
 	 * us, profiles/r03_ws_ab_vf2.jsonl): the loop is not bound by them */
 	const bool v2 = (k.cflags & GCL_CFG_VERDICT2) && k.nt_store == 2 && !k.ablate;
-	const ClassifyFn fn = v2 ? (tlds ? classify_pair_kernel<MODE, true, NT, 2>
-	                                 : classify_pair_kernel<MODE, false, NT, 2>)
-	                         : (tlds ? classify_pair_kernel<MODE, true, NT, 0>
-	                                 : classify_pair_kernel<MODE, false, NT, 0>);
+	ClassifyFn fn = v2 ? (tlds ? classify_pair_kernel<MODE, true, NT, 2>
+	                           : classify_pair_kernel<MODE, false, NT, 2>)
+	                   : (tlds ? classify_pair_kernel<MODE, true, NT, 0>
+	                           : classify_pair_kernel<MODE, false, NT, 0>);
+	if (ntl && v2 && tlds && NT == 256) /* the streaming-hint experiment */
+		fn = classify_pair_kernel<MODE, true, NT, 2, true>;
 	return launch_fn(fn, NT, k, lds, num_cus, bpc_cap, s);
 }
 
@@ -2055,6 +2075,7 @@ struct Geometry {
 	int depth;    /* tiles in flight per block */
 	int bpc_cap;  /* blocks per CU */
 	bool pair;    /* classify_pair_kernel (GENERAL batches): [8, 40) per packet by lane pairs */
+	bool ntl;     /* its frame loads with the streaming hint (GCL_TUNE_PAIR_LOADS=1) */
 };
 
 /* LDS for the tile's header sources (s_src, classify_kernel): GENERAL */
@@ -2070,10 +2091,10 @@ static hipError_t launch_mode(const KParams &k, bool tlds, bool general, const G
 	if (geo.pair) {
 		const uint32_t lds = hist_bytes + tab_lds;
 		if (geo.threads == 1024)
-			return launch_pair<MODE, 1024>(k, tlds, lds, num_cus, geo.bpc_cap, s);
+			return launch_pair<MODE, 1024>(k, tlds, lds, num_cus, geo.bpc_cap, geo.ntl, s);
 		if (geo.threads == 512)
-			return launch_pair<MODE, 512>(k, tlds, lds, num_cus, geo.bpc_cap, s);
-		return launch_pair<MODE, 256>(k, tlds, lds, num_cus, geo.bpc_cap, s);
+			return launch_pair<MODE, 512>(k, tlds, lds, num_cus, geo.bpc_cap, geo.ntl, s);
+		return launch_pair<MODE, 256>(k, tlds, lds, num_cus, geo.bpc_cap, geo.ntl, s);
 	}
 	const uint32_t lds = (uint32_t)geo.threads * 64 + kLdsQueueBytes + hist_bytes + tab_lds +
 	                     offs_lds_bytes(general, (uint32_t)geo.threads);
@@ -2118,6 +2139,7 @@ static Geometry choose_geometry(const gcl_ctx *c, uint32_t tab_lds, uint32_t his
 	 * profiles/r03_ws_ab.jsonl.) */
 	g.pair = general && c->tune_pair && !c->tune_sched && c->tune_depth != 1 &&
 	         !(c->tune_ablate & 16);
+	g.ntl = c->tune_pair_loads & 1;
 	auto per_block = [&](uint32_t nt) -> uint32_t {
 		if (g.pair)
 			return hist_bytes + tab_lds;
