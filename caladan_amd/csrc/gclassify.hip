@@ -246,17 +246,14 @@ __device__ __forceinline__ uint4 load16_bytes(const KParams &k, uint64_t a)
  * shift | staged frame bytes << 8, for classify_one; bits 16-19 flag this
  * lane's chunks of bytewise frames, which patch_tile fills in after staging.
  */
-/* The tile kernel's 16-B frame loads: with the streaming hint (measured
- * faster for the dense HBM stream); GCL_TILE_LOAD_PLAIN builds
- * the plain-load variant for A/B runs (tools/dense_ab.sh). */
+/* The tile kernel's 16-B frame loads carry the streaming hint: plain loads
+ * measured 11 % slower on udp64 (88.7-89.6 vs 99.8-100.7 Gpkt/s) and 13 % on
+ * tcp1500, alternating fresh processes on one box
+ * (profiles/r03_dense_load_hint_ab.jsonl) -- the opposite of the pair
+ * kernel, whose frames are reused from L2. */
 __device__ __forceinline__ uint4 tile_load(const void *p)
 {
-#ifdef GCL_TILE_LOAD_PLAIN
-	const uint4 v = *(const uint4 *)p;
-	return v;
-#else
 	return gcl::load16_nt(p);
-#endif
 }
 
 template <bool GENERAL, int NT, bool SRC = false>

@@ -15,8 +15,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# GCL_LIB: another build of the library, for A/B runs only (tools/dense_ab.sh)
-LIB_PATH = os.environ.get("GCL_LIB") or os.path.join(HERE, "libgclassify.so")
+LIB_PATH = os.path.join(HERE, "libgclassify.so")
 
 GCL_MAX_PROC = 4096
 GCL_NCPU = 256
