@@ -1629,6 +1629,8 @@ struct gcl_ctx {
 	int tune_xcd_map;  /* GCL_TUNE_XCD_MAP: 1 contiguous eighth per XCD, 0 round-robin tiles */
 	int tune_pair;     /* GCL_TUNE_PAIR: 1 GENERAL batches on classify_pair_kernel */
 	int tune_pair_loads; /* GCL_TUNE_PAIR_LOADS: 1 = the pair kernel's frame loads non-temporal (experiment) */
+	int tune_general;  /* GCL_TUNE_GENERAL: 1 = fixed-slot batches on the GENERAL path too
+	                      (experiment: the pair kernel over host memory) */
 	/* dynamic tile queue: one slot per launch in flight, reused in turn; a
 	 * launch waits for the previous user of its slot (same or other stream) */
 	uint32_t *sched;
@@ -1716,6 +1718,8 @@ extern "C" int gcl_open(int hip_device, const struct gcl_cfg *cfg, struct gcl_ct
 		c->tune_pair = e ? atoi(e) : kDefaultPair;
 		e = getenv("GCL_TUNE_PAIR_LOADS");
 		c->tune_pair_loads = e ? atoi(e) : 0;
+		e = getenv("GCL_TUNE_GENERAL");
+		c->tune_general = e ? atoi(e) : 0;
 	}
 	c->dimg[0] = c->dimg[1] = nullptr;
 	c->sched = nullptr;
@@ -2325,7 +2329,7 @@ extern "C" int gcl_classify_ex(struct gcl_ctx *c, const struct gcl_batch *b,
 	/* the specialised fast path needs every header granule in range */
 	bool general = b->offs || b->olflags || b->fdir_hi || b->dst_hint ||
 	               (c->cfg.default_olflags & GCL_F_FDIR_ID) ||
-	               b->frames_len < (b->n - 1) * b->stride + GCL_HDR_GRANULE;
+	               b->frames_len < (b->n - 1) * b->stride + GCL_HDR_GRANULE || c->tune_general;
 	uint32_t tab_bytes = c->image_bytes;
 	uint32_t hist_bytes = ((c->cfg.max_runtimes + 3) & ~3u) * 4;
 	bool tlds = tab_bytes <= kLdsTableBudget;

@@ -268,3 +268,32 @@ def test_gpu_torch_nccl_one_rank_exchange(g):
         assert torch.equal(shard.global_counts(gathered, 1), local)
     finally:
         dist.destroy_process_group()
+
+
+def test_gpu_group_errors(g):
+    """The group's error returns, as the reference's init paths fail:
+    RCCL with one GPU twice (-EINVAL), a read before any exchange
+    (-ENODATA), a zero-copy batch in memory that is not registered
+    (-EFAULT), and the binding's shape checks."""
+    with pytest.raises(OSError) as e:
+        g.Group([0, 0], R, g.HASH_JENKINS, exchange=g.XCHG_RCCL)
+    assert e.value.errno == 22
+    grp = g.Group([0], R, g.HASH_JENKINS)
+    try:
+        tables(grp)
+        with pytest.raises(OSError) as e:
+            grp.read()
+        assert e.value.errno == 61  # ENODATA
+        frames = np.zeros(4096 * 64, dtype=np.uint8)  # pageable, not registered
+        hv = np.zeros(4096 * 8, dtype=np.uint8)
+        with pytest.raises(OSError) as e:
+            grp.classify_host(frames, 4096, 64, verdicts=hv, mode=g.E2E_ZEROCOPY)
+        assert e.value.errno == 14  # EFAULT
+        with pytest.raises(ValueError):
+            grp.classify([], [])
+        # the host batch was refused before any launch: nothing was counted
+        grp.exchange()
+        c, s, _ = grp.read()
+        assert not c.any() and not s.any()
+    finally:
+        grp.close()
