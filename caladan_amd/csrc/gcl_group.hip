@@ -331,6 +331,24 @@ static void *mapped(const void *h)
 	return d;
 }
 
+/* Work streams 0 .. @nst - 1 on every GPU (a host batch may ask for more
+ * than the group opened with); exchanges and syncs cover all of them. */
+static int grow_streams(gcl_group *g, int nst)
+{
+	for (int i = 0; i < g->n && nst > g->nst; i++) {
+		gcl_group::Dev &D = g->d[i];
+		if (hipSetDevice(D.dev) != hipSuccess)
+			return -ENODEV;
+		for (int s = g->nst; s < nst; s++)
+			if (!D.st[s] && (hipStreamCreateWithFlags(&D.st[s], hipStreamNonBlocking) != hipSuccess ||
+			                 hipEventCreateWithFlags(&D.st_ev[s], hipEventDisableTiming) != hipSuccess))
+				return -ENOMEM;
+	}
+	if (nst > g->nst)
+		g->nst = nst;
+	return 0;
+}
+
 static int ensure_staging(gcl_group *g, gcl_group::Dev &D, int nst)
 {
 	if (hipSetDevice(D.dev) != hipSuccess)
@@ -385,7 +403,9 @@ extern "C" int gcl_group_classify_host(struct gcl_group *g, const struct gcl_bat
 	const int nst = o->nstreams ? (int)o->nstreams : g->nst;
 	const int G = g->n;
 	const uint64_t nb = (hb->n + g->block - 1) / g->block;
-	int ret = 0;
+	int ret = grow_streams(g, nst);
+	if (ret)
+		return ret;
 	HipErr he;
 	if (o->mode == GCL_E2E_ZEROCOPY) {
 		/* every GPU reads its blocks straight out of registered host

@@ -100,8 +100,8 @@ int gcl_group_classify(struct gcl_group *g, const struct gcl_batch *shards,
  * blocks' 64-B header granules DMA-gathered into HBM, fixed-stride slots
  * only) and writes their verdicts at their batch positions of
  * @host_verdicts.  All GPUs run at once from this one thread; synchronous.
- * @o->chunk is ignored (the block is the unit); @o->nstreams overrides the
- * group's streams when non-zero.  Counts accumulate on the GPUs as with
+ * @o->chunk is ignored (the block is the unit); @o->nstreams (1..4) overrides
+ * the group's streams per GPU when non-zero.  Counts accumulate on the GPUs as with
  * gcl_group_classify.  -EFAULT when a ZEROCOPY buffer is not registered.
  */
 int gcl_group_classify_host(struct gcl_group *g, const struct gcl_batch *hb,

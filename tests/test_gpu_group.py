@@ -178,9 +178,10 @@ def test_gpu_group_classify_host_split(g, orc, mode, layout, nstreams):
             o = int(offs[i])
             frames[o:o + 64] = hdr[i * 64:(i + 1) * 64]
     hv = pinned(np.zeros(n, dtype=g.VERDICT_DTYPE))
-    grp = g.Group([0, 0], R, g.HASH_NIC, block=B, exchange=g.XCHG_HOST, nstreams=nstreams)
+    # opened with one stream per GPU; the batch asks for `nstreams`
+    grp = g.Group([0, 0], R, g.HASH_NIC, block=B, exchange=g.XCHG_HOST, nstreams=1)
     tables(grp)
-    grp.classify_host(pinned(frames), n, stride, verdicts=hv,
+    grp.classify_host(pinned(frames), n, stride, verdicts=hv, nstreams=nstreams,
                       offs=None if offs is None else pinned(offs), olflags=pinned(olf),
                       rss=pinned(rss), mode=g.E2E_ZEROCOPY if mode == "zerocopy" else g.E2E_COPY)
     grp.exchange()
