@@ -1107,3 +1107,68 @@ def test_gpu_general_frames_at_the_end(g, orc, monkeypatch, kernel, mode, patter
     acts = ve["action"] & 0x3F
     # both outcomes occur: registered destinations, and ones cut by frames_len
     assert (acts == g.ACT_DELIVER).sum() > 10 and (acts == g.ACT_DROP_UNREG).sum() > 4
+
+
+@pytest.mark.parametrize("order", ["random", "working_set"])
+def test_gpu_full_size_ingress_pool(g, orc, order):
+    """The integrated rx_burst shape at the bench's full size, on the GENERAL
+    path's default kernel (the lane-pair kernel): 8 Mi descriptors into the
+    reference's 131072-mbuf ingress pool (9408-B elements, frame data at
+    element + 344), each with its mbuf's ol_flags and hash.rss, NIC mode,
+    2-byte queue verdicts, the region placed against the verdict ring as
+    bench.ingress_pool_bench places it -- in random order over the whole
+    pool and over a 4096-mbuf working set.  Every packet is accounted for,
+    the queue histogram equals the device counts, and a 65536-descriptor
+    sample equals the oracle bit for bit."""
+    import bench
+    from tests.rxcases import to_verdict2
+    dev = torch.device("cuda", 0)
+    wl, _, _, R, T, _ = bench.WORKLOADS["udp64"]
+    P, n = g.IOKERNEL_NUM_MBUFS, 8 << 20
+    hdr = torch.zeros(P * 64, dtype=torch.uint8, device=dev)
+    olf_p = torch.zeros(P, dtype=torch.uint8, device=dev)
+    rss_p = torch.zeros(P, dtype=torch.int32, device=dev)
+    g.generate(wl, P, 64, R, hdr, olflags=olf_p, rss=rss_p, seed=bench.SEED)
+    pool_offs = torch.from_numpy(g.mbuf_data_offsets(P).view(np.int64)).to(dev)
+    region = torch.zeros(g.mbuf_region_bytes(P), dtype=torch.uint8, device=dev)
+    region[(pool_offs[:, None] + torch.arange(64, device=dev)).view(-1)] = hdr
+    gen = torch.Generator(device="cpu").manual_seed(bench.SEED + (order == "working_set"))
+    if order == "random":
+        sel = torch.cat([torch.randperm(P, generator=gen) for _ in range(n // P)])
+    else:
+        sub = torch.randperm(P, generator=gen)[:bench.INGRESS_WORKING_SET]
+        sel = torch.cat([sub[torch.randperm(len(sub), generator=gen)] for _ in range(n // len(sub))])
+    sel = sel.to(dev)
+    offs, olf, rss = pool_offs[sel].contiguous(), olf_p[sel].contiguous(), rss_p[sel].contiguous()
+    dv = g.DeviceBuffer(n * 2, 0)
+    placed = g.DeviceBuffer(region.numel(), 0, partner=dv, vbytes=2)
+    torch.cuda.synchronize()
+    bench.hip_copy(placed, region, region.numel())
+    clf = bench.classifier(dev, R, T, 2, hash_mode=g.HASH_NIC)
+    tables = bench.setup_tables(clf, R, T)
+    assert clf.thread_bits == 3
+    cnt = torch.zeros(R + g.NR_STATS, dtype=torch.int64, device=dev)
+    clf.classify(placed, n, 0, verdicts=dv, counts=cnt[:R], stats=cnt[R:], offs=offs, olflags=olf,
+                 rss=rss, stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    hv = torch.empty(n * 2, dtype=torch.uint8).pin_memory()
+    bench.hip_copy(hv, dv, n * 2)
+    q = hv.numpy().view(np.uint16)
+    cc, ss = cnt[:R].cpu().numpy(), cnt[R:].cpu().numpy()
+    assert cc.sum() == n and ss[g.RX_PULLED] == n and ss[g.RX_UNHANDLED] == 0
+    assert ((q & g.V2_KIND) == g.V2_DELIVER).all()
+    assert (np.bincount(q >> 3, minlength=R)[:R] == cc).all()
+    rng = np.random.default_rng(77)
+    sample = np.sort(rng.choice(n, size=65536, replace=False))
+    sidx = torch.from_numpy(sample).to(dev)
+    so = offs[sidx]
+    fr = region[(so[:, None] + torch.arange(64, device=dev)).view(-1)].cpu().numpy()
+    t = orc.Tables(R, g.HASH_NIC, 0, 0x09)
+    for (r, ip, TT, act, fl) in tables:
+        assert t.runtime_set(r, ip, TT, act, fl) == 0
+    ve, _, _ = t.classify(fr, len(sample), 64, olflags=olf[sidx].cpu().numpy(),
+                          rss=rss[sidx].cpu().numpy().view(np.uint32))
+    want = to_verdict2(ve, {r: TT for (r, _, TT, _, _) in tables}, 3)
+    assert_same(q[sample], want, f"ingress pool {order} sample")
+    del region, placed, dv
+    torch.cuda.empty_cache()
