@@ -466,6 +466,92 @@ def group_bench(w, steps, warmup, device_index, period=EXCHANGE_EVERY, settle=No
         grp.close()
 
 
+def group_node_bench(ndev, steps, warmup, period=EXCHANGE_EVERY, vbytes=VERDICT_BYTES):
+    """The single-process multi-GPU step over `ndev` GPUs of this node (run in
+    a child process by group_node_line): the udp64 workload sharded
+    round-robin in 64 Ki-packet blocks, each GPU's 32 Mi-packet shard
+    generated in its own HBM (a frame pool placed against its verdict ring),
+    one gcl_group over all of them classifying every GPU's shard per step and
+    all-gathering the counts through RCCL (ncclCommInitAll) every `period`
+    steps.  Wall time between full synchronisations of every GPU; the
+    node-wide counts read back through the exchange and checked."""
+    wl, n, stride, R, T, _ = WORKLOADS["udp64"]
+    fl, tb = verdict_cfg(vbytes, R, T)
+    devs = list(range(ndev))
+    frames, verdicts = [], []
+    for d in devs:
+        with torch.cuda.device(d):
+            v = g.DeviceBuffer(n * vbytes, d)
+            f = g.DeviceBuffer(n * stride, d, partner=v, vbytes=vbytes)
+            torch.cuda.synchronize()
+            zero_fill(f)
+            g.generate(wl, n, stride, R, f, seed=SEED, rank=d, world=ndev, shard_block=SHARD_BLOCK)
+            torch.cuda.synchronize()
+            frames.append(f)
+            verdicts.append(v)
+    grp = g.Group(devs, R, g.HASH_JENKINS, flags=fl, thread_bits=tb, exchange=g.XCHG_RCCL)
+    try:
+        rng = np.random.default_rng(SEED)
+        for r in range(R):
+            act = int(rng.integers(1, T + 1))
+            idx = [int(x) for x in rng.choice(T, size=act, replace=False)]
+            grp.runtime_set(r, g.runtime_ip(r), T, act, g.steer_flows(T, idx))
+        shards = [{"frames": f, "n": n, "stride": stride} for f in frames]
+        k = [0]
+
+        def one():
+            grp.classify(shards, verdicts)
+            k[0] += 1
+            if k[0] % period == 0:
+                grp.exchange()
+
+        t0 = time.perf_counter()
+        for _ in range(max(warmup, 1)):
+            one()
+        grp.sync()
+        step_ms = (time.perf_counter() - t0) * 1e3 / max(warmup, 1)
+        for _ in range(int(SETTLE_MS / max(step_ms, 1e-3)) + 1):
+            one()
+        grp.sync()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            one()
+        grp.sync()
+        el = time.perf_counter() - t0
+        grp.exchange()
+        c, s, per = grp.read()
+        ok = (int(c.sum()) == n * ndev * k[0] and int(s[g.RX_PULLED]) == n * ndev * k[0] and
+              all(int(per[i, R + g.RX_PULLED]) == n * k[0] for i in range(ndev)))
+        return {"what": (f"gcl_group over {ndev} GPU(s) from one process: round-robin 64Ki-pkt shards, "
+                         f"{n} pkts per GPU per step, RCCL ncclAllGather of u64[R+8] every {period} steps"),
+                "n_gpus": ndev, "value": round(n * ndev * steps / el / 1e6, 1), "unit": "Mpkt/s",
+                "ms_per_step": round(el / steps * 1e3, 4), "steps": steps,
+                "exchanges": int(k[0] // period) + 1,
+                "counts_check": "ok" if ok else "MISMATCH"}
+    finally:
+        grp.close()
+
+
+def group_node_line(args):
+    """group_node_bench over every visible GPU, in a child process with its
+    own time limit (an RCCL or driver stall there cannot take the bench line
+    down with it).  Only when this node shows more than one GPU."""
+    import subprocess
+    ndev = min(torch.cuda.device_count(), 16)
+    if ndev < 2 and not args.group_node_force:
+        return None
+    cmd = [sys.executable, os.path.abspath(__file__), "--group-child", str(max(ndev, 1)),
+           "--steps", str(args.steps), "--warmup", str(args.warmup)]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    except subprocess.TimeoutExpired:
+        return {"n_gpus": ndev, "error": "timeout (300 s)"}
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"n_gpus": ndev, "error": (r.stderr.strip()[-300:] or f"rc {r.returncode}")}
+    return json.loads(lines[-1])
+
+
 def pmc_traffic(name, vbytes):
     """HBM bytes per launch from the committed PMC passes (profiles/pmc_*.json,
     tools/prof_summary.py: FETCH_SIZE + WRITE_SIZE, gfx950-corrected)."""
@@ -1005,7 +1091,10 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-group", action="store_true",
-                    help="skip the gcl_group (C ABI + RCCL) line at N=1")
+                    help="skip the gcl_group (C ABI + RCCL) lines at N=1")
+    ap.add_argument("--group-node-force", action="store_true",
+                    help="run the all-GPU group line even with one GPU visible")
+    ap.add_argument("--group-child", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo only to rehearse N>1 on one GPU")
@@ -1020,6 +1109,9 @@ def main():
                     help="run the multi-GPU step (RCCL all_gather on a side stream) even at N=1")
     args = ap.parse_args()
     _claim_stdout()
+    if args.group_child:  # group_node_line's child: one JSON line, nothing else
+        emit_json(group_node_bench(args.group_child, args.steps, args.warmup, args.exchange_every))
+        return
 
     rank, world, local = shard.dist_env()
     if world != args.gpus:
@@ -1104,6 +1196,11 @@ def main():
         except (OSError, ImportError) as e:  # reported, never silently dropped
             result["group"] = {"error": str(e)}
     del w, ex
+    torch.cuda.empty_cache()
+    if world == 1 and not args.no_group:
+        node = group_node_line(args)
+        if node is not None:
+            result["group_node"] = node
     torch.cuda.empty_cache()
 
     if world == 1 and not args.no_secondary and args.workload == "udp64" and args.scaling == "weak":
