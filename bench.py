@@ -549,7 +549,26 @@ def group_node_line(args):
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     if r.returncode != 0 or not lines:
         return {"n_gpus": ndev, "error": (r.stderr.strip()[-300:] or f"rc {r.returncode}")}
-    return json.loads(lines[-1])
+    out = json.loads(lines[-1])
+    out["host_ingress_c"] = grouppipe_run(ndev)
+    return out
+
+
+def grouppipe_run(ndev, n=8 << 20, iters=5):
+    """tools/grouppipe: the same group driven from C over a host-memory
+    ingress batch (n udp64 frames in pinned memory split over the GPUs,
+    zero-copy and header DMA-gather); PCIe-inclusive, never `value`."""
+    import subprocess
+    exe = os.path.join(ROOT, "tools", "grouppipe")
+    if not os.access(exe, os.X_OK):
+        return {"skipped": "tools/grouppipe not built"}
+    try:
+        r = subprocess.run([exe, str(ndev), str(n), str(iters)], capture_output=True, text=True, timeout=180)
+    except subprocess.TimeoutExpired:
+        return {"error": "timeout (180 s)"}
+    if r.returncode != 0:
+        return {"error": r.stderr.strip()[-300:] or f"rc {r.returncode}"}
+    return json.loads(r.stdout.strip().splitlines()[-1])
 
 
 def pmc_traffic(name, vbytes):

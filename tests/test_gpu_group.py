@@ -213,6 +213,26 @@ def test_gpu_group_rccl_classify_host(g, orc):
     grp.close()
 
 
+def test_gpu_grouppipe_c_driver(g):
+    """tools/grouppipe (the group driven from C, as the iokernel would link
+    it): a ragged 1 Mi + 77 packet host batch over every visible GPU, both
+    transports; it checks the last batch's verdicts against one context and the
+    RCCL-gathered counts against the packets submitted, and exits 2 on a
+    mismatch."""
+    import json
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "grouppipe")
+    if not os.access(exe, os.X_OK):
+        pytest.fail("tools/grouppipe not built (python -c 'import __graft_entry__ as g; g.build()')")
+    ndev = min(torch.cuda.device_count(), 16)
+    r = subprocess.run([exe, str(ndev), str((1 << 20) + 77), "2"], capture_output=True, text=True,
+                       timeout=100)
+    assert r.returncode == 0, r.stderr[-500:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["counts_check"] == "ok" and out["verdicts_check"] == "ok" and out["n_gpus"] == ndev
+    assert out["zerocopy_mpps"] > 0 and out["copy_hdr_mpps"] > 0
+
+
 def test_gpu_group_table_fanout(g):
     """Table changes reach every context; the first one decides errors."""
     grp = g.Group([0, 0], R, g.HASH_JENKINS, exchange=g.XCHG_HOST)

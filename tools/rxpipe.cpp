@@ -23,6 +23,8 @@
 // Build: hipcc --offload-arch=gfx950 -O2 -Iinclude -o tools/rxpipe tools/rxpipe.cpp \
 //          -Lcaladan_amd -lgclassify -Wl,-rpath,'$ORIGIN/../caladan_amd'
 #include <hip/hip_runtime.h>
+#include <ctype.h>
+#include <sched.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -42,6 +44,52 @@ static uint64_t now_ns()
 	struct timespec ts;
 	clock_gettime(CLOCK_MONOTONIC, &ts);
 	return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
+/* Pin this thread to one CPU, as the iokernel pins its dataplane lcore
+ * (iokernel/dpdk.c:276-280): the LAST CPU of our affinity mask that is local
+ * to GPU @dev's PCIe node (sysfs local_cpulist), else the last one of the
+ * mask -- away from CPU 0, where housekeeping and interrupts tend to land.
+ * RXPIPE_PIN=0 in the environment leaves the thread unpinned.  Returns the
+ * CPU, or -1. */
+static int pin_near_gpu(int dev)
+{
+	const char *env = getenv("RXPIPE_PIN");
+	if (env && !strcmp(env, "0"))
+		return -1;
+	cpu_set_t allowed;
+	if (sched_getaffinity(0, sizeof(allowed), &allowed))
+		return -1;
+	int pick = -1;
+	char bus[64] = {0}, path[160];
+	if (hipDeviceGetPCIBusId(bus, sizeof(bus), dev) == hipSuccess) {
+		for (char *c = bus; *c; c++)
+			*c = (char)tolower(*c);
+		snprintf(path, sizeof(path), "/sys/bus/pci/devices/%s/local_cpulist", bus);
+		FILE *f = fopen(path, "r");
+		if (f) {
+			int lo, hi;
+			char sep;
+			while (fscanf(f, "%d", &lo) == 1) {
+				hi = lo;
+				if (fscanf(f, "%c", &sep) == 1 && sep == '-' && fscanf(f, "%d", &hi) == 1)
+					(void)fscanf(f, "%c", &sep);
+				for (int cpu = lo; cpu <= hi; cpu++)
+					if (cpu < CPU_SETSIZE && CPU_ISSET(cpu, &allowed))
+						pick = cpu;
+			}
+			fclose(f);
+		}
+	}
+	for (int cpu = CPU_SETSIZE - 1; cpu >= 0 && pick < 0; cpu--)
+		if (CPU_ISSET(cpu, &allowed))
+			pick = cpu;
+	if (pick < 0)
+		return -1;
+	cpu_set_t one;
+	CPU_ZERO(&one);
+	CPU_SET(pick, &one);
+	return sched_setaffinity(0, sizeof(one), &one) ? -1 : pick;
 }
 
 int main(int argc, char **argv)
@@ -192,6 +240,8 @@ int main(int argc, char **argv)
 		}
 		seq += count;
 	};
+	/* pinned after the runtime's own threads exist (they keep their masks) */
+	const int cpu = pin_near_gpu(0);
 	const uint32_t warm = 200;
 	pump(warm, false);
 	const uint64_t t0 = now_ns();
@@ -203,13 +253,14 @@ int main(int argc, char **argv)
 	printf("{\"burst\": %u, \"workers\": %u, \"depth\": %u, \"bursts\": %u, \"verdicts\": \"%s\", "
 	       "\"mpps_one_core\": %.2f, "
 	       "\"burst_latency_p50_us\": %.2f, \"burst_latency_p99_us\": %.2f, "
-	       "\"deliver_ns_per_pkt\": %.2f, \"delivered_check\": \"%s\", \"unicast_fail\": %llu}\n",
+	       "\"deliver_ns_per_pkt\": %.2f, \"delivered_check\": \"%s\", \"unicast_fail\": %llu, "
+	       "\"host_cpu\": %d}\n",
 	       burst, workers, depth, nbursts,
 	       copy_out ? "copied out" : inline_hdrs ? "read in place, headers inlined in the slot" : "read in place",
 	       pkts / (el * 1e-3), lat[lat.size() / 2] * 1e-3,
 	       lat[lat.size() * 99 / 100] * 1e-3, t_deliver / pkts,
 	       delivered == (uint64_t)burst * (nbursts + warm) ? "ok" : "MISMATCH",
-	       (unsigned long long)stats[GCL_RX_UNICAST_FAIL]);
+	       (unsigned long long)stats[GCL_RX_UNICAST_FAIL], cpu);
 	gcl_close(ctx);
 	CHECK(hipHostFree(region));
 	return 0;
