@@ -159,8 +159,6 @@ def test_gpu_group_classify_host_split(g, orc, mode, layout, nstreams):
     the verdicts land at their batch positions and equal the oracle's; the
     node-wide counts and counters equal the oracle's (NIC mode with ol_flags
     and hash.rss, a ragged last block)."""
-    if mode == "copy" and layout == "offs":
-        pytest.skip("the header DMA-gather path takes fixed-stride slots only")
     B = 4096
     n = 5 * B + 77
     rng = np.random.default_rng(3)
@@ -181,9 +179,18 @@ def test_gpu_group_classify_host_split(g, orc, mode, layout, nstreams):
     # opened with one stream per GPU; the batch asks for `nstreams`
     grp = g.Group([0, 0], R, g.HASH_NIC, block=B, exchange=g.XCHG_HOST, nstreams=1)
     tables(grp)
-    grp.classify_host(pinned(frames), n, stride, verdicts=hv, nstreams=nstreams,
-                      offs=None if offs is None else pinned(offs), olflags=pinned(olf),
-                      rss=pinned(rss), mode=g.E2E_ZEROCOPY if mode == "zerocopy" else g.E2E_COPY)
+    kw = dict(verdicts=hv, nstreams=nstreams, offs=None if offs is None else pinned(offs),
+              olflags=pinned(olf), rss=pinned(rss),
+              mode=g.E2E_ZEROCOPY if mode == "zerocopy" else g.E2E_COPY)
+    if mode == "copy" and layout == "offs":
+        # the header DMA-gather copies fixed-stride granules (one 2D DMA per
+        # block); descriptors at arbitrary offsets are refused, not gathered
+        with pytest.raises(OSError) as e:
+            grp.classify_host(pinned(frames), n, stride, **kw)
+        assert e.value.errno == 22
+        grp.close()
+        return
+    grp.classify_host(pinned(frames), n, stride, **kw)
     grp.exchange()
     c, s, per = grp.read()
     t = orc.Tables(R, 0, 0, 0x09)
