@@ -1197,6 +1197,25 @@ __host__ __device__ constexpr uint64_t loop_word(uint64_t t, uint32_t n, uint32_
 }
 static_assert(sizeof(LoopSlotHdr) == 64, "LoopSlotHdr");
 
+/* Offsets in a ring slot carry the slot's use count in their top 24 bits
+ * (offsets themselves are < 2^40: the ingress region is bounded at start).
+ * An 8-B entry is written and read whole, so a lane that reads its entry
+ * while polling knows by the stamp whether it holds this burst's offset or a
+ * stale one: the offsets arrive with the poll that sees the burst, one PCIe
+ * round trip sooner.  Entries past a burst's n keep older stamps; every
+ * kLoopRefresh uses of a slot the host rewrites all of them, so no entry is
+ * ever 2^24 uses stale and a stamp never aliases. */
+constexpr int kLoopStampShift = 40;
+constexpr uint64_t kLoopOffMask = (1ull << kLoopStampShift) - 1;
+constexpr uint64_t kLoopRefresh = 256;
+/* s_memrealtime ticks (100 MHz) a wait polls the offsets with the word: a
+ * burst that arrives later costs the offsets' round trip after the word */
+constexpr uint64_t kLoopSpecTicks = 400;
+__host__ __device__ constexpr uint64_t loop_stamp(uint64_t t, uint32_t nslots)
+{
+	return (((t - 1) / nslots + 1) & 0xFFFFFF) << kLoopStampShift;
+}
+
 struct LoopImgHdr {        /* first 64 B of a table image buffer */
 	uint32_t bytes, ipt_mask, off_rt, off_flow, off_toep, ipt_seed, pad[10];
 };
@@ -1221,6 +1240,7 @@ struct LoopParams {
 	unsigned long long *counts, *stats;
 	uint32_t max_rt, cflags, default_flags;
 	uint32_t off_hdr;          /* GCL_LOOP_INLINE_HDRS: 64-B granules in the slot; else 0 */
+	uint32_t spec_offs;        /* poll the stamped offsets too (bursts <= 64, no inline headers) */
 };
 
 /* header tile + 2 x side arrays (offs, rss, fdir, hint, olflags) + verdicts + ctl */
@@ -1236,14 +1256,16 @@ struct LoopSide {
 	__device__ LoopSide(uint8_t *b)
 	    : offs((uint64_t *)b), rss((uint32_t *)(b + 2048)), fdir(rss + 256), hint(fdir + 256),
 	      olf((uint8_t *)(hint + 256)) {}
-	/* packets [base, base + m) of the burst in @slot, one per lane */
+	/* packets [base, base + m) of the burst in @slot, one per lane (the
+	 * offsets too unless the poll already brought them) */
 	__device__ void load(const uint8_t *slot, const LoopParams &L, uint32_t fl, uint32_t base,
-	                     uint32_t m, int tid)
+	                     uint32_t m, int tid, bool with_offs = true)
 	{
 		if ((uint32_t)tid >= m)
 			return;
 		const uint32_t i = base + tid;
-		offs[tid] = gcl::ld_sys64(slot + L.off_offs + 8 * i);
+		if (with_offs)
+			offs[tid] = gcl::ld_sys64(slot + L.off_offs + 8 * i) & kLoopOffMask;
 		if (fl & GCL_LOOP_F_OLF)
 			olf[tid] = (uint8_t)(gcl::ld_sys32(slot + L.off_olf + (i & ~3u)) >> (8 * (i & 3)));
 		if (fl & GCL_LOOP_F_RSS)
@@ -1288,27 +1310,60 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 		uint8_t *slot = L.slots + ((t - 1) % L.nslots) * L.slot_bytes;
 		LoopSlotHdr *h = (LoopSlotHdr *)slot;
 		const __amdgpu_buffer_rsrc_t srs = gcl::host_rsrc(slot, L.slot_bytes);
-		if (tid == 0) {
-			uint64_t w = 0;
-			for (;;) { /* one system-scope load per poll carries the whole burst header */
-				w = gcl::ld_sys64(&h->word);
-				if ((w >> 24) == (t & ((1ull << 40) - 1)))
+		if (tid < 64) {
+			/* wave 0 polls.  One system-scope load of the slot word carries
+			 * the whole burst header, and without inline headers each lane
+			 * also reads its stamped offset entry, so a burst of <= 64
+			 * packets has its offsets when the word shows it.  (The stop flag is read beside every 8th poll,
+			 * never after one: that made each poll two round trips.)  The
+			 * offsets are polled only for the first kLoopSpecTicks of a wait:
+			 * a worker that waits longer (many workers, deep queues) polls
+			 * the word alone, so idle polls do not crowd the PCIe requests
+			 * of the workers that are reading frames */
+			const bool spec = L.spec_offs;
+			const uint64_t stamp = loop_stamp(t, L.nslots);
+			const uint64_t spec_end = __builtin_amdgcn_s_memrealtime() + kLoopSpecTicks;
+			uint64_t w = 0, e = 0;
+			for (uint32_t k = 0;; k++) {
+				const bool sp = spec && __builtin_amdgcn_s_memrealtime() < spec_end;
+				const uint64_t ev = sp ? gcl::ld_sys64(slot + L.off_offs + 8 * tid) : 0;
+				uint64_t wv = 0;
+				uint32_t sv = 0;
+				if (tid == 0) {
+					wv = gcl::ld_sys64(&h->word);
+					if ((k & 7) == 7) /* a stop waits for up to 8 polls */
+						sv = gcl::ld_sys32(L.stop);
+				}
+				wv = __shfl(wv, 0);
+				sv = __shfl(sv, 0);
+				if ((wv >> 24) == (t & ((1ull << 40) - 1))) {
+					w = wv;
+					e = ev;
 					break;
-				w = 0;
-				if (gcl::ld_sys32(L.stop) || __builtin_amdgcn_s_memrealtime() > t_end)
+				}
+				if (sv || __builtin_amdgcn_s_memrealtime() > t_end)
 					break;
 				__builtin_amdgcn_s_sleep(1);
 			}
-			s_ctl[0] = w != 0;
-			s_ctl[1] = (uint32_t)(w >> 11) & 0x1FFF;
-			s_ctl[2] = (uint32_t)(w >> 7) & 0xF;
-			s_ctl[3] = (uint32_t)(w >> 6) & 1;
-			s_ctl[4] = (uint32_t)w & 63;
+			const uint32_t nw = (uint32_t)(w >> 11) & 0x1FFF;
+			const bool fresh = (uint32_t)tid >= nw || (e & ~kLoopOffMask) == stamp;
+			const bool early = spec && w && nw <= 64 && __all(fresh);
+			if (early && (uint32_t)tid < nw)
+				side(0).offs[tid] = e & kLoopOffMask;
+			if (tid == 0) {
+				s_ctl[0] = w != 0;
+				s_ctl[1] = nw;
+				s_ctl[2] = (uint32_t)(w >> 7) & 0xF;
+				s_ctl[3] = (uint32_t)(w >> 6) & 1;
+				s_ctl[4] = (uint32_t)w & 63;
+				s_ctl[5] = early;
+			}
 		}
 		__syncthreads();
 		if (!s_ctl[0])
 			break;
 		const uint32_t n = s_ctl[1], fl = s_ctl[2], img = s_ctl[3], img_seq = s_ctl[4];
+		const bool early_offs = s_ctl[5];
 		if (img_seq != cur_seq) { /* a new table snapshot: copy it into LDS */
 			const uint8_t *ib = L.img[img];
 			const uint32_t bytes = gcl::ld_sys32(ib);
@@ -1347,11 +1402,13 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 				}
 			}
 		};
-		if (L.off_hdr) /* the granules do not wait for the offsets */
+		/* the granules do not wait for the offsets, nor do frames whose
+		 * offsets came with the poll */
+		if (L.off_hdr || early_offs)
 			load_frames(side(0), 0, chunk_m(0));
-		side(0).load(slot, L, fl, 0, chunk_m(0), tid);
+		side(0).load(slot, L, fl, 0, chunk_m(0), tid, !early_offs);
 		__syncthreads();
-		if (!L.off_hdr)
+		if (!L.off_hdr && !early_offs)
 			load_frames(side(0), 0, chunk_m(0));
 		for (uint32_t c = 0; c < nch; c++) {
 			const uint32_t m = chunk_m(c), base = 256 * c;
@@ -3046,6 +3103,8 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 		return -ENOTSUP;
 	if (cfg->flags & ~(uint32_t)GCL_LOOP_INLINE_HDRS)
 		return -EINVAL;
+	if (cfg->region_len > kLoopOffMask - GCL_HDR_GRANULE)
+		return -EINVAL; /* offsets share their slot entry with a stamp */
 	if (c->loop)
 		return -EBUSY;
 	if (hipSetDevice(c->device) != hipSuccess)
@@ -3071,6 +3130,7 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 	lp.off_hint = lp.off_fdir + 4 * mb;
 	lp.off_verd = lp.off_hint + 4 * mb;
 	lp.off_hdr = (cfg->flags & GCL_LOOP_INLINE_HDRS) ? lp.off_verd + sizeof(LoopRec) * mb : 0;
+	lp.spec_offs = !lp.off_hdr && cfg->max_burst <= 64;
 	lp.slot_bytes = (lp.off_verd + sizeof(LoopRec) * mb + (lp.off_hdr ? GCL_HDR_GRANULE * mb : 0) +
 	                 255) & ~255ull;
 	lp.nslots = cfg->slots;
@@ -3167,7 +3227,15 @@ extern "C" int64_t gcl_rxloop_submit(struct gcl_rxloop *L, uint32_t n, const uin
 	LoopSlotHdr *h = loop_slot(L, t);
 	uint8_t *s = (uint8_t *)h;
 	uint32_t fl = 0;
-	memcpy(s + L->lp.off_offs, offs, 8ull * n);
+	{ /* offsets stamped with the slot's use count (loop_stamp) */
+		uint64_t *so = (uint64_t *)(s + L->lp.off_offs);
+		const uint64_t st = loop_stamp(t, L->lp.nslots);
+		for (uint32_t i = 0; i < n; i++) /* past the region either way: reads 0 */
+			so[i] = std::min<uint64_t>(offs[i], kLoopOffMask) | st;
+		if ((((t - 1) / L->lp.nslots + 1) % kLoopRefresh) == 0)
+			for (uint32_t i = n; i < L->max_burst; i++)
+				so[i] = st;
+	}
 	if (L->lp.off_hdr) { /* the header granules ride in the slot; past the region: 0 */
 		uint8_t *hd = s + L->lp.off_hdr;
 		for (uint32_t i = 0; i < n; i++, hd += GCL_HDR_GRANULE) {

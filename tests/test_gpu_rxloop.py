@@ -182,6 +182,48 @@ def test_rxloop_workers_pipelined_and_full_ring(g, orc):
         g.host_unregister(frames)
 
 
+@pytest.mark.parametrize("max_burst,workers", [(64, 1), (64, 3), (256, 2)])
+def test_rxloop_stamped_offsets_ragged_bursts(g, orc, max_burst, workers):
+    """Offsets ride in the slot stamped with the slot's use count, and a
+    worker polling a burst of <= 64 takes them with the poll when every stamp
+    is current.  Two slots reused ~700 times each (past the periodic rewrite
+    of the entries beyond a burst's n), burst sizes drawn from 1..max_burst
+    so stale entries of longer bursts sit behind shorter ones, and offsets
+    at and past 2^40 (the stamp's bit) that read as frames past the region."""
+    rng = np.random.default_rng(7300 + max_burst + workers)
+    max_rt = 16
+    rts = random_runtimes(rng, max_rt, 12)
+    n = 4096
+    frames, flen, offs, olf, rss, fdir, hint = fuzz_batch(rng, n, rts, max_rt)
+    far = np.array([1 << 40, (1 << 40) - 1, (1 << 41) + 77, 1 << 50], dtype=np.uint64)
+    offs = np.concatenate([offs, far])
+    olf = np.concatenate([olf, np.full(len(far), 0x09, dtype=np.uint8)])
+    rss = np.concatenate([rss, rng.integers(0, 2**32, size=len(far), dtype=np.uint64).astype(np.uint32)])
+    t = orc.Tables(max_rt, 1, 0, 0x09)
+    apply_runtimes(t, rts)
+    ve, _, _ = t.classify(frames, len(offs), 0, offs=offs, olflags=olf, rss=rss, frames_len=flen)
+    assert (ve[n:]["action"] == ve[n]["action"]).all()  # zero frames: one drop verdict
+    clf = g.Classifier(0, max_rt, 1, 0, 0x09)
+    apply_runtimes(clf, rts)
+    g.host_register(frames)
+    loop = clf.rxloop(frames, slots=2, workers=workers, max_burst=max_burst, region_len=flen)
+    try:
+        nb = 1400
+        sizes = np.where(rng.random(nb) < 0.3, max_burst, rng.integers(1, max_burst + 1, size=nb))
+        for k, m in enumerate(sizes):
+            idx = rng.integers(0, len(offs), size=int(m))
+            if k % 50 == 0:
+                idx[-1] = n + k // 50 % len(far)  # an offset past 2^40
+            tk = loop.submit(offs[idx], olf[idx], rss[idx])
+            assert tk > 0
+            got = loop.wait(tk, int(m))
+            bad = np.nonzero(got != ve[idx])[0]
+            assert not len(bad), f"burst {k} (n {m}): packet {bad[0]} {got[bad[0]]} vs {ve[idx][bad[0]]}"
+    finally:
+        loop.stop()
+        g.host_unregister(frames)
+
+
 def test_rxloop_lifetime_and_errors(g):
     frames = np.zeros(1 << 16, dtype=np.uint8)
     clf = g.Classifier(0, 16, 1)
