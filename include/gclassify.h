@@ -479,7 +479,11 @@ int gcl_dev_alloc_paired(int hip_device, size_t bytes, const void *partner, size
  *   into it (mbuf data pointer - region base, like ptr_to_shmptr, shm.h:40-47).
  *   The kernel leaves by itself after @cfg->lifetime_ms.  Tables must fit in
  *   LDS (-E2BIG otherwise); GCL_CFG_TRANS_HASH is not supported (-ENOTSUP);
- *   one loop per context (-EBUSY).  Table changes made with gcl_runtime_set /
+ *   one loop per context (-EBUSY); the region must be shorter than 2^40 - 64
+ *   bytes (-EINVAL: offsets share their slot entry with a stamp, so a burst
+ *   of <= 64 packets has its offsets with the poll that finds it; offsets at
+ *   or past the region's end still read as frames of zeros).  Table changes
+ *   made with gcl_runtime_set /
  *   _del apply from the next submitted burst on (snapshot semantics).
  * gcl_rxloop_submit - publish one burst; returns its ticket (> 0), -EAGAIN
  *   when the ring is full (a slot is reused only after gcl_rxloop_wait has
@@ -511,7 +515,9 @@ struct gcl_rxloop_cfg {
 /* gcl_rxloop_submit copies each frame's first 64-B header granule into the
  * ring slot (the dataplane core reads the headers, as rx_one_pkt does), so
  * the kernel fetches them with the burst's side arrays instead of one PCIe
- * round trip later from the region: lower latency for CPU time. */
+ * round trip later from the region.  Since the offsets arrive with the poll
+ * the two forms take the same time for one burst; inlining saves the GPU's
+ * reads of the region when many workers keep PCIe busy. */
 #define GCL_LOOP_INLINE_HDRS 0x1
 int gcl_rxloop_start(struct gcl_ctx *ctx, const struct gcl_rxloop_cfg *cfg,
                      struct gcl_rxloop **out);
