@@ -728,12 +728,13 @@ def rxpipe_bench():
         return {"skipped": "tools/rxpipe not built (python -c 'import __graft_entry__ as g; g.build()')"}
     rows = []
     # burst 64 is the reference's own (IOKERNEL_RX_BURST_SIZE, defs.h:75):
-    # throughput there is workers / round trip, so it is run at 1, 4, 8 and
-    # 16 workers; verdicts are read in place in the slot (gcl_rxloop_peek),
-    # and once copied out (the round-2 form) for comparison
+    # throughput there is workers / round trip, so it is run at 1, 4, 8, 16
+    # and 32 workers; verdicts are read in place in the slot
+    # (gcl_rxloop_peek), and once copied out (the round-2 form) for comparison
     for cfg in (("64", "1", "1", "20000"), ("64", "4", "8", "20000"), ("64", "4", "8", "20000", "copy"),
-                ("64", "8", "16", "40000"), ("64", "16", "32", "40000"), ("64", "8", "16", "40000", "inline"),
-                ("64", "16", "32", "40000", "inline"), ("256", "4", "8", "10000"),
+                ("64", "8", "16", "40000"), ("64", "16", "32", "40000"), ("64", "32", "64", "60000"),
+                ("64", "8", "16", "40000", "inline"), ("64", "16", "32", "40000", "inline"),
+                ("256", "4", "8", "10000"),
                 ("1024", "8", "16", "4000"), ("4096", "16", "16", "1000")):
         try:
             r = subprocess.run([exe, *cfg], capture_output=True, text=True, timeout=120)

@@ -1234,6 +1234,7 @@ struct LoopParams {
 	const uint8_t *img[2];     /* device views of the two image buffers */
 	const uint32_t *stop;
 	uint32_t *where;           /* host words: XCC_ID + 1 of worker b at [b] (b < 8) */
+	uint32_t *exited;          /* host word: set by a worker that leaves */
 	uint64_t lifetime_ticks;   /* s_memrealtime ticks each block may run */
 	const uint8_t *frames;     /* device view of the registered region */
 	uint64_t frames_len;
@@ -1360,8 +1361,13 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 			}
 		}
 		__syncthreads();
-		if (!s_ctl[0])
+		if (!s_ctl[0]) {
+			/* the host stops publishing on this (one word it can read
+			 * without asking the HIP runtime per burst) */
+			if (tid == 0)
+				gcl::st_sys32(L.exited, 1);
 			break;
+		}
 		const uint32_t n = s_ctl[1], fl = s_ctl[2], img = s_ctl[3], img_seq = s_ctl[4];
 		const bool early_offs = s_ctl[5];
 		if (img_seq != cur_seq) { /* a new table snapshot: copy it into LDS */
@@ -3028,6 +3034,17 @@ static bool loop_ended(gcl_rxloop *L)
 	return L->ended;
 }
 
+/* loop_ended without a HIP call: a worker that leaves raises ctl[1].  Per
+ * burst on the submit path, where hipStreamQuery cost ~100 ns; a kernel that
+ * died without raising it is still caught by loop_await's periodic
+ * loop_ended. */
+static bool loop_left(gcl_rxloop *L)
+{
+	if (!L->ended && __atomic_load_n(&L->ctl[1], __ATOMIC_ACQUIRE))
+		L->ended = true;
+	return L->ended;
+}
+
 static const LoopRec *loop_recs(gcl_rxloop *L, LoopSlotHdr *h)
 {
 	return (const LoopRec *)((const uint8_t *)h + L->lp.off_verd);
@@ -3096,7 +3113,7 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 {
 	if (!c || !cfg || !out || !cfg->region || !cfg->region_len || cfg->slots < 2 ||
 	    cfg->slots > 1024 || (cfg->slots & (cfg->slots - 1)) || !cfg->max_burst ||
-	    cfg->max_burst > 4096 || !cfg->workers || cfg->workers > 16 || !cfg->lifetime_ms ||
+	    cfg->max_burst > 4096 || !cfg->workers || cfg->workers > 64 || !cfg->lifetime_ms ||
 	    cfg->lifetime_ms > 600000)
 		return -EINVAL;
 	if (c->cfg.flags & GCL_CFG_TRANS_HASH)
@@ -3175,6 +3192,7 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 		goto fail;
 	lp.stop = (const uint32_t *)d;
 	lp.where = (uint32_t *)d + 8;
+	lp.exited = (uint32_t *)d + 1;
 	if (hipStreamCreateWithFlags(&L->st, hipStreamNonBlocking) != hipSuccess)
 		goto fail;
 	{
@@ -3206,7 +3224,7 @@ extern "C" int64_t gcl_rxloop_submit(struct gcl_rxloop *L, uint32_t n, const uin
 {
 	if (!L || !n || n > L->max_burst || !offs)
 		return -EINVAL;
-	if (loop_ended(L))
+	if (loop_left(L))
 		return -ESHUTDOWN;
 	const uint64_t t = L->next + 1;
 	/* a slot is reused only after the host collected its previous burst */
@@ -3287,6 +3305,21 @@ static int loop_await(gcl_rxloop *L, uint64_t t, uint64_t spin_ns)
 	return 0;
 }
 
+/* Start the host's reads of the next ticket's verdict records while this
+ * burst is delivered: they are lines the GPU writes into host memory, so
+ * each costs a DRAM miss the first time (16 per 64-packet burst).  A line
+ * fetched before the GPU writes it is simply fetched again. */
+static void prefetch_next(gcl_rxloop *L, uint64_t t)
+{
+	if (t + 1 > L->next)
+		return;
+	const LoopSlotHdr *h = loop_slot(L, t + 1);
+	const uint32_t n = (uint32_t)(h->word >> 11) & 0x1FFF;
+	const uint8_t *r = (const uint8_t *)loop_recs(L, (LoopSlotHdr *)h);
+	for (uint32_t b = 0; b < n * (uint32_t)sizeof(LoopRec); b += 64)
+		__builtin_prefetch(r + b, 0, 3);
+}
+
 extern "C" int gcl_rxloop_peek(struct gcl_rxloop *L, int64_t ticket, uint64_t spin_ns,
                                const struct gcl_loop_rec **recs, uint32_t *n)
 {
@@ -3301,6 +3334,7 @@ extern "C" int gcl_rxloop_peek(struct gcl_rxloop *L, int64_t ticket, uint64_t sp
 	LoopSlotHdr *h = loop_slot(L, t);
 	*n = (uint32_t)(h->word >> 11) & 0x1FFF;
 	*recs = (const struct gcl_loop_rec *)loop_recs(L, h);
+	prefetch_next(L, t);
 	return 0;
 }
 
@@ -3329,6 +3363,7 @@ extern "C" int gcl_rxloop_wait(struct gcl_rxloop *L, int64_t ticket, void *verdi
 	const int aw = loop_await(L, t, spin_ns);
 	if (aw)
 		return aw;
+	prefetch_next(L, t);
 	if (verdicts_out) {
 		const uint32_t n = (uint32_t)(h->word >> 11) & 0x1FFF;
 		const LoopRec *r = loop_recs(L, h);

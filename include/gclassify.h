@@ -503,7 +503,7 @@ struct gcl_rxloop;
 struct gcl_rxloop_cfg {
 	uint32_t slots;        /* ring depth: power of two, 2..1024 */
 	uint32_t max_burst;    /* packets per burst: 1..4096 */
-	uint32_t workers;      /* polling workgroups: 1..16 */
+	uint32_t workers;      /* polling workgroups: 1..64 */
 	uint32_t lifetime_ms;  /* kernel lifetime bound: 1..600000 */
 	const void *region;    /* registered host region holding the frames */
 	uint64_t region_len;

@@ -102,7 +102,7 @@ int main(int argc, char **argv)
 	const bool inline_hdrs = argc > 5 && !strcmp(argv[5], "inline");
 	const uint32_t R = 16, T = 8, RING = 4096;
 	const uint64_t nframes = 1 << 16, stride = 64;
-	if (!burst || burst > 4096 || !workers || workers > 16 || !depth || depth > 64) {
+	if (!burst || burst > 4096 || !workers || workers > 64 || !depth || depth > 64) {
 		fprintf(stderr, "bad arguments\n");
 		return 1;
 	}
@@ -186,16 +186,19 @@ int main(int argc, char **argv)
 	std::vector<int64_t> tk(depth);
 	std::vector<uint64_t> t_sub(depth), lat;
 	lat.reserve(nbursts);
-	uint64_t delivered = 0, t_deliver = 0, seq = 0;
+	uint64_t delivered = 0, t_deliver = 0, t_submit = 0, t_wait = 0, seq = 0;
 	/* @count bursts with up to @depth in flight, in ticket order */
 	auto pump = [&](uint32_t count, bool timed) {
 		uint32_t head = 0, tail = 0;
 		while (tail < count) {
 			while (head < count && head - tail < depth) {
 				const uint32_t b = (uint32_t)((seq + head) % nb);
-				t_sub[head % depth] = now_ns();
+				const uint64_t ts = now_ns();
+				t_sub[head % depth] = ts;
 				const int64_t r = gcl_rxloop_submit(loop, burst, &offs[(size_t)b * burst], nullptr,
 				                                    nullptr, nullptr, nullptr);
+				if (timed)
+					t_submit += now_ns() - ts;
 				if (r < 0) {
 					fprintf(stderr, "submit: %lld\n", (long long)r);
 					exit(1);
@@ -205,6 +208,7 @@ int main(int argc, char **argv)
 			}
 			const uint32_t b = (uint32_t)((seq + tail) % nb);
 			const int64_t t = tk[tail % depth];
+			const uint64_t tw = now_ns();
 			uint64_t d0, d1;
 			if (copy_out) {
 				const int w = gcl_rxloop_wait(loop, t, v.data(), 1000000000ull);
@@ -234,6 +238,7 @@ int main(int argc, char **argv)
 			}
 			if (timed) {
 				t_deliver += d1 - d0;
+				t_wait += d0 - tw;
 				lat.push_back(d1 - t_sub[tail % depth]);
 			}
 			tail++;
@@ -253,12 +258,12 @@ int main(int argc, char **argv)
 	printf("{\"burst\": %u, \"workers\": %u, \"depth\": %u, \"bursts\": %u, \"verdicts\": \"%s\", "
 	       "\"mpps_one_core\": %.2f, "
 	       "\"burst_latency_p50_us\": %.2f, \"burst_latency_p99_us\": %.2f, "
-	       "\"deliver_ns_per_pkt\": %.2f, \"delivered_check\": \"%s\", \"unicast_fail\": %llu, "
-	       "\"host_cpu\": %d}\n",
+	       "\"deliver_ns_per_pkt\": %.2f, \"submit_ns_per_pkt\": %.2f, \"wait_ns_per_pkt\": %.2f, "
+	       "\"delivered_check\": \"%s\", \"unicast_fail\": %llu, \"host_cpu\": %d}\n",
 	       burst, workers, depth, nbursts,
 	       copy_out ? "copied out" : inline_hdrs ? "read in place, headers inlined in the slot" : "read in place",
 	       pkts / (el * 1e-3), lat[lat.size() / 2] * 1e-3,
-	       lat[lat.size() * 99 / 100] * 1e-3, t_deliver / pkts,
+	       lat[lat.size() * 99 / 100] * 1e-3, t_deliver / pkts, t_submit / pkts, t_wait / pkts,
 	       delivered == (uint64_t)burst * (nbursts + warm) ? "ok" : "MISMATCH",
 	       (unsigned long long)stats[GCL_RX_UNICAST_FAIL], cpu);
 	gcl_close(ctx);
