@@ -9,8 +9,8 @@
 //
 //   grouppipe <ndev> [pkts] [iters]   -> one JSON line
 //
-// Build: hipcc --offload-arch=gfx950 -O2 -Iinclude -o tools/grouppipe tools/grouppipe.cpp \
-//          -Lcaladan_amd -lgclgroup -lgclassify -Wl,-rpath,'$ORIGIN/../caladan_amd'
+// Build: hipcc --offload-arch=gfx950 -O2 -Iinclude -o tools/grouppipe tools/grouppipe.cpp
+//         -Lcaladan_amd -lgclgroup -lgclassify -Wl,-rpath,'$ORIGIN/../caladan_amd'
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>

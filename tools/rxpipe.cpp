@@ -20,8 +20,8 @@
 // so when a ring looks full the producer's refresh (__lrpc_send,
 // base/lrpc.c:16-19) finds it drained -- the reference's own path, taken
 // once per 4096 messages per ring, as in the CPU baseline's lrpc variant.
-// Build: hipcc --offload-arch=gfx950 -O2 -Iinclude -o tools/rxpipe tools/rxpipe.cpp \
-//          -Lcaladan_amd -lgclassify -Wl,-rpath,'$ORIGIN/../caladan_amd'
+// Build: hipcc --offload-arch=gfx950 -O2 -Iinclude -o tools/rxpipe tools/rxpipe.cpp
+//         -Lcaladan_amd -lgclassify -Wl,-rpath,'$ORIGIN/../caladan_amd'
 #include <hip/hip_runtime.h>
 #include <ctype.h>
 #include <sched.h>
