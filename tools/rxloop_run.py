@@ -1,6 +1,7 @@
 """bench.py's rx loop latency leg alone (e2e.rxloop): burst latency of the
-persistent loop at 64..1024-packet bursts, for A/Bs of the loop's knobs
-(GCL_LOOP_POLLERS, GCL_LOOP_STAGGER_NS) in fresh processes.
+persistent loop at 64..1024-packet bursts, one fresh process per call (the
+staggered-poller knobs it once compared are gone from the library,
+profiles/r02_loop_pollers_ab.jsonl).
 
     python tools/rxloop_run.py [iters]
 """
@@ -18,5 +19,4 @@ if __name__ == "__main__":
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     out = bench.rxloop_bench(dev, bench.VERDICT_BYTES, iters=iters)
-    out["env"] = {k: os.environ[k] for k in ("GCL_LOOP_POLLERS", "GCL_LOOP_STAGGER_NS") if k in os.environ}
     print(json.dumps(out))
