@@ -224,6 +224,25 @@ def test_rxloop_stamped_offsets_ragged_bursts(g, orc, max_burst, workers):
         g.host_unregister(frames)
 
 
+@pytest.mark.parametrize("cfg", [("200000", "1", "2", "1"), ("400000", "4", "4", "4"),
+                                 ("400000", "32", "64", "64")])
+def test_rxloop_soak_stamped_offsets(g, cfg):
+    """tools/loopsoak: random 1..64-packet bursts at random offsets into a
+    mixed-traffic region, few slots, a tight host loop with random pauses
+    racing the workers' polls; every verdict equal to the batch kernel's for
+    the same packet (exit 2 on a mismatch)."""
+    import json
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "loopsoak")
+    if not os.access(exe, os.X_OK):
+        pytest.fail("tools/loopsoak not built (python -c 'import __graft_entry__ as g; g.build()')")
+    r = subprocess.run([exe, *cfg], capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, (r.stdout[-300:], r.stderr[-300:])
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["mismatches"] == 0 and out["packets_checked"] > int(cfg[0]) * 30
+
+
 def test_rxloop_lifetime_and_errors(g):
     frames = np.zeros(1 << 16, dtype=np.uint8)
     clf = g.Classifier(0, 16, 1)
