@@ -735,6 +735,8 @@ def rxpipe_bench():
     for cfg in (("64", "1", "1", "20000"), ("64", "4", "8", "20000"), ("64", "4", "8", "20000", "copy"),
                 ("64", "8", "16", "40000"), ("64", "16", "32", "40000"), ("64", "32", "64", "60000"),
                 ("64", "8", "16", "40000", "inline"), ("64", "16", "32", "40000", "inline"),
+                ("64", "1", "1", "20000", "records"), ("64", "8", "16", "40000", "records"),
+                ("64", "16", "32", "40000", "records"),
                 ("256", "4", "8", "10000"),
                 ("1024", "8", "16", "4000"), ("4096", "16", "16", "1000")):
         try:
@@ -772,8 +774,10 @@ def rxloop_bench(device, vbytes, iters=2000):
                 "p99_us": round(float(us[int(len(us) * 0.99)]), 2),
                 "mean_us": round(float(us.mean()), 2)}
 
-    for burst, workers, depth, fl in ((64, 1, 1, 0), (64, 1, 1, g.LOOP_INLINE_HDRS), (256, 1, 1, 0),
-                                      (1024, 1, 1, 0), (64, 4, 8, 0), (1024, 8, 16, 0)):
+    for burst, workers, depth, fl in ((64, 1, 1, 0), (64, 1, 1, g.LOOP_INLINE_HDRS),
+                                      (64, 1, 1, g.LOOP_HDR_RECORDS), (256, 1, 1, 0),
+                                      (1024, 1, 1, 0), (64, 4, 8, 0), (64, 4, 8, g.LOOP_HDR_RECORDS),
+                                      (1024, 8, 16, 0)):
         loop = clf.rxloop(hfr, slots=16, max_burst=burst, workers=workers, lifetime_ms=30000,
                           flags=fl)
         try:
@@ -784,7 +788,8 @@ def rxloop_bench(device, vbytes, iters=2000):
             loop.stop()
         r = pct(lat)
         r["mpps"] = round(burst * iters / (el / 1e9) / 1e6, 2)
-        out[f"loop_burst{burst}_w{workers}_d{depth}" + ("_inline_hdrs" if fl else "")] = r
+        out[f"loop_burst{burst}_w{workers}_d{depth}" + {0: "", g.LOOP_INLINE_HDRS: "_inline_hdrs",
+                                                          g.LOOP_HDR_RECORDS: "_hdr_records"}[fl]] = r
     hv = torch.empty(64 * vbytes, dtype=torch.uint8).pin_memory()
     lat = []
     for i in range(iters // 4 + 20):

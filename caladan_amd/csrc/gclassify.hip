@@ -175,6 +175,9 @@ __device__ __forceinline__ uint64_t frame_off(const KParams &k, uint64_t idx)
  * frame (@return 0xFF) is read bytewise from its own start, all 64 bytes.
  */
 constexpr uint32_t kSpanFull = 64u << 8; /* no shift, 64 frame bytes staged */
+/* the rx loop's header records (GCL_LOOP_HDR_RECORDS) stage frame bytes 12-15
+ * and 20-43 only: ports past byte 43 (IHL >= 7) are read from the frame */
+constexpr uint32_t kSpanRec = 44u << 8;
 
 __device__ __forceinline__ uint32_t hdr_window(const KParams &k, uint64_t off, uint32_t &cut)
 {
@@ -606,7 +609,8 @@ __device__ __forceinline__ uint64_t classify_one(const KParams &k, const uint4 *
 	/* frame byte b of this lane's header sits at tile byte b + sh, and frame
 	 * bytes [0, avail) are staged (hdr_window) */
 	const uint32_t sh = (GENERAL && !SYS) ? (span & 0xFF) : 0u;
-	const uint32_t avail = (GENERAL && !SYS) ? (span >> 8 & 0xFF) : 64u;
+	/* SYS: 64, or 44 when the rx loop staged header records (kSpanRec) */
+	const uint32_t avail = GENERAL ? (span >> 8 & 0xFF) : 64u;
 	HdrWords h;
 	if (GENERAL && !SYS && sh != 0) {
 		h.d3 = tile_dword(tile, tid, 12 + sh);
@@ -1240,9 +1244,44 @@ struct LoopParams {
 	uint64_t frames_len;
 	unsigned long long *counts, *stats;
 	uint32_t max_rt, cflags, default_flags;
-	uint32_t off_hdr;          /* GCL_LOOP_INLINE_HDRS: 64-B granules in the slot; else 0 */
-	uint32_t spec_offs;        /* poll the stamped offsets too (bursts <= 64, no inline headers) */
+	uint32_t off_hdr;          /* GCL_LOOP_INLINE_HDRS: 64-B granules in the slot,
+	                              GCL_LOOP_HDR_RECORDS: 64-B header records; else 0 */
+	uint32_t spec;             /* bursts <= 64: poll the stamped offsets (or records) too */
+	uint32_t hdr_rec;          /* off_hdr holds header records (GCL_LOOP_HDR_RECORDS) */
+	uint32_t spec_ticks;       /* how long a wait polls them (s_memrealtime ticks) */
 };
+
+/* GCL_LOOP_HDR_RECORDS: the submitting core writes each packet as one 64-B
+ * record of four 16-B chunks, each stored whole and led by the slot's use
+ * count, so that a lane reading them while it polls knows whether all four
+ * are this burst's.  Together they carry everything rx_one_pkt reads:
+ *   q0 {stamp, d3, d5, d6}      frame dwords: bytes 12-15, 20-27
+ *   q1 {stamp, d7, d8, d9}      bytes 28-39
+ *   q2 {stamp, d10, rss, fdir}  bytes 40-43, hash.rss, hash.fdir.hi
+ *   q3 {stamp, off[31:0], off[39:32] | ol_flags << 8, dst_hint}
+ * (d4, total length and IP id, and the MAC addresses are never read.)  A burst
+ * of <= 64 packets then arrives whole with the poll that finds its word: one
+ * PCIe round trip per burst.  Ports past byte 43 (IHL >= 7) are read from the
+ * frame at the record's offset. */
+__host__ __device__ constexpr uint32_t loop_rec_stamp(uint64_t t, uint32_t nslots)
+{
+	return (uint32_t)((t - 1) / nslots + 1);
+}
+
+/* a record's four chunks -> the packet's tile row and side-array entries */
+__device__ __forceinline__ void rec_to_row(const uint4 *q, uint4 *tile, int p, uint64_t *offs,
+                                           uint8_t *olf, uint32_t *rss, uint32_t *fdir,
+                                           uint32_t *hint)
+{
+	tile[tile_slot(p, 0)] = make_uint4(0, 0, 0, q[0].y);
+	tile[tile_slot(p, 1)] = make_uint4(0, q[0].z, q[0].w, q[1].y);
+	tile[tile_slot(p, 2)] = make_uint4(q[1].z, q[1].w, q[2].y, 0);
+	offs[p] = (uint64_t)(q[3].z & 0xFF) << 32 | q[3].y;
+	olf[p] = (uint8_t)(q[3].z >> 8);
+	rss[p] = q[2].z;
+	fdir[p] = q[2].w;
+	hint[p] = q[3].w;
+}
 
 /* header tile + 2 x side arrays (offs, rss, fdir, hint, olflags) + verdicts + ctl */
 constexpr uint32_t kLoopSide = 256 * 8 + 3 * 256 * 4 + 256;
@@ -1321,13 +1360,24 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 			 * a worker that waits longer (many workers, deep queues) polls
 			 * the word alone, so idle polls do not crowd the PCIe requests
 			 * of the workers that are reading frames */
-			const bool spec = L.spec_offs;
+			const bool spec = L.spec, rec = L.hdr_rec;
 			const uint64_t stamp = loop_stamp(t, L.nslots);
-			const uint64_t spec_end = __builtin_amdgcn_s_memrealtime() + kLoopSpecTicks;
+			const uint32_t rstamp = loop_rec_stamp(t, L.nslots);
+			const uint64_t spec_end = __builtin_amdgcn_s_memrealtime() + L.spec_ticks;
 			uint64_t w = 0, e = 0;
+			bool rok = false;
+			uint4 q[4], qv[4]; /* header records: the lane's packet's chunks */
 			for (uint32_t k = 0;; k++) {
 				const bool sp = spec && __builtin_amdgcn_s_memrealtime() < spec_end;
-				const uint64_t ev = sp ? gcl::ld_sys64(slot + L.off_offs + 8 * tid) : 0;
+				const uint64_t ev = sp && !rec ? gcl::ld_sys64(slot + L.off_offs + 8 * tid) : 0;
+				if (sp && rec) {
+#pragma unroll
+					for (int j = 0; j < 4; j++) {
+						const auto v = __builtin_amdgcn_raw_buffer_load_b128(
+						        srs, (int)(L.off_hdr + 64 * tid + 16 * j), 0, gcl::kSysAux);
+						qv[j] = make_uint4(v[0], v[1], v[2], v[3]);
+					}
+				}
 				uint64_t wv = 0;
 				uint32_t sv = 0;
 				if (tid == 0) {
@@ -1340,6 +1390,11 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 				if ((wv >> 24) == (t & ((1ull << 40) - 1))) {
 					w = wv;
 					e = ev;
+					rok = sp && qv[0].x == rstamp && qv[1].x == rstamp && qv[2].x == rstamp &&
+					      qv[3].x == rstamp;
+#pragma unroll
+					for (int j = 0; j < 4; j++)
+						q[j] = qv[j];
 					break;
 				}
 				if (sv || __builtin_amdgcn_s_memrealtime() > t_end)
@@ -1347,10 +1402,15 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 				__builtin_amdgcn_s_sleep(1);
 			}
 			const uint32_t nw = (uint32_t)(w >> 11) & 0x1FFF;
-			const bool fresh = (uint32_t)tid >= nw || (e & ~kLoopOffMask) == stamp;
+			const bool fresh = (uint32_t)tid >= nw || (rec ? rok : (e & ~kLoopOffMask) == stamp);
 			const bool early = spec && w && nw <= 64 && __all(fresh);
-			if (early && (uint32_t)tid < nw)
-				side(0).offs[tid] = e & kLoopOffMask;
+			if (early && (uint32_t)tid < nw) {
+				const LoopSide s0 = side(0);
+				if (rec)
+					rec_to_row(q, tile, tid, s0.offs, s0.olf, s0.rss, s0.fdir, s0.hint);
+				else
+					s0.offs[tid] = e & kLoopOffMask;
+			}
 			if (tid == 0) {
 				s_ctl[0] = w != 0;
 				s_ctl[1] = nw;
@@ -1393,7 +1453,21 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 		const uint32_t nch = (n + 255) / 256;
 		uint4 r[4];
 		auto chunk_m = [&](uint32_t c) { return n - 256 * c < 256 ? n - 256 * c : 256u; };
+		const bool rec = L.hdr_rec;
 		auto load_frames = [&](const LoopSide &sd, uint32_t c0, uint32_t m) {
+			if (rec) { /* one packet per lane: its record's four chunks */
+#pragma unroll
+				for (int j = 0; j < 4; j++) {
+					if ((uint32_t)tid >= m) {
+						r[j] = make_uint4(0, 0, 0, 0);
+					} else {
+						const auto v = __builtin_amdgcn_raw_buffer_load_b128(
+						        srs, (int)(L.off_hdr + 64 * (256 * c0 + tid) + 16 * j), 0, gcl::kSysAux);
+						r[j] = make_uint4(v[0], v[1], v[2], v[3]);
+					}
+				}
+				return;
+			}
 #pragma unroll
 			for (int j = 0; j < 4; j++) {
 				const int c = j * 256 + tid, p = c >> 2, q = c & 3;
@@ -1410,21 +1484,33 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 		};
 		/* the granules do not wait for the offsets, nor do frames whose
 		 * offsets came with the poll */
-		if (L.off_hdr || early_offs)
-			load_frames(side(0), 0, chunk_m(0));
-		side(0).load(slot, L, fl, 0, chunk_m(0), tid, !early_offs);
-		__syncthreads();
-		if (!L.off_hdr && !early_offs)
-			load_frames(side(0), 0, chunk_m(0));
+		if (rec) {
+			/* the records carry the side arrays too; a burst that came
+			 * with the poll is already in the tile */
+			if (!early_offs)
+				load_frames(side(0), 0, chunk_m(0));
+		} else {
+			if (L.off_hdr || early_offs)
+				load_frames(side(0), 0, chunk_m(0));
+			side(0).load(slot, L, fl, 0, chunk_m(0), tid, !early_offs);
+			__syncthreads();
+			if (!L.off_hdr && !early_offs)
+				load_frames(side(0), 0, chunk_m(0));
+		}
 		for (uint32_t c = 0; c < nch; c++) {
 			const uint32_t m = chunk_m(c), base = 256 * c;
 			const LoopSide cur = side(c);
-			if (c + 1 < nch)
-				side(c + 1).load(slot, L, fl, base + 256, chunk_m(c + 1), tid);
+			if (rec) {
+				if ((c || !early_offs) && (uint32_t)tid < m)
+					rec_to_row(r, tile, tid, cur.offs, cur.olf, cur.rss, cur.fdir, cur.hint);
+			} else {
+				if (c + 1 < nch)
+					side(c + 1).load(slot, L, fl, base + 256, chunk_m(c + 1), tid);
 #pragma unroll
-			for (int j = 0; j < 4; j++) {
-				const int cc = j * 256 + tid;
-				tile[tile_slot(cc >> 2, cc & 3)] = r[j];
+				for (int j = 0; j < 4; j++) {
+					const int cc = j * 256 + tid;
+					tile[tile_slot(cc >> 2, cc & 3)] = r[j];
+				}
 			}
 			__syncthreads(); /* tile of c and side arrays of c + 1 in LDS */
 			if (c + 1 < nch)
@@ -1437,7 +1523,8 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 			k.dst_hint = (fl & GCL_LOOP_F_HINT) ? cur.hint : nullptr;
 			if ((uint32_t)tid < m) {
 				put_verdict(k, (uint64_t)tid,
-				            classify_one<MODE, true, true>(k, tile, tid, (uint64_t)tid, tb, hist, cnt));
+				            classify_one<MODE, true, true>(k, tile, tid, (uint64_t)tid, tb, hist, cnt,
+				                                           rec ? kSpanRec : kSpanFull));
 				const bool v4 = L.cflags & GCL_CFG_VERDICT4, v2 = L.cflags & GCL_CFG_VERDICT2;
 				const uint32_t hsh = v4 || v2 ? 0u : s_verd[tid].x;
 				const uint32_t vlo = v2 ? ((const uint16_t *)s_verd)[tid]
@@ -3118,7 +3205,8 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 		return -EINVAL;
 	if (c->cfg.flags & GCL_CFG_TRANS_HASH)
 		return -ENOTSUP;
-	if (cfg->flags & ~(uint32_t)GCL_LOOP_INLINE_HDRS)
+	if ((cfg->flags & ~(uint32_t)(GCL_LOOP_INLINE_HDRS | GCL_LOOP_HDR_RECORDS)) ||
+	    (cfg->flags & GCL_LOOP_INLINE_HDRS && cfg->flags & GCL_LOOP_HDR_RECORDS))
 		return -EINVAL;
 	if (cfg->region_len > kLoopOffMask - GCL_HDR_GRANULE)
 		return -EINVAL; /* offsets share their slot entry with a stamp */
@@ -3146,8 +3234,13 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 	lp.off_fdir = lp.off_rss + 4 * mb;
 	lp.off_hint = lp.off_fdir + 4 * mb;
 	lp.off_verd = lp.off_hint + 4 * mb;
-	lp.off_hdr = (cfg->flags & GCL_LOOP_INLINE_HDRS) ? lp.off_verd + sizeof(LoopRec) * mb : 0;
-	lp.spec_offs = !lp.off_hdr && cfg->max_burst <= 64;
+	lp.hdr_rec = (cfg->flags & GCL_LOOP_HDR_RECORDS) != 0;
+	lp.off_hdr = (cfg->flags & (GCL_LOOP_INLINE_HDRS | GCL_LOOP_HDR_RECORDS))
+	                     ? lp.off_verd + sizeof(LoopRec) * mb : 0;
+	lp.spec = (!lp.off_hdr || lp.hdr_rec) && cfg->max_burst <= 64;
+	lp.spec_ticks = kLoopSpecTicks;
+	if (const char *e = getenv("GCL_TUNE_LOOP_SPEC")) /* experiments: ticks of 10 ns */
+		lp.spec_ticks = (uint32_t)atoi(e);
 	lp.slot_bytes = (lp.off_verd + sizeof(LoopRec) * mb + (lp.off_hdr ? GCL_HDR_GRANULE * mb : 0) +
 	                 255) & ~255ull;
 	lp.nslots = cfg->slots;
@@ -3218,6 +3311,54 @@ fail:
 	return ret;
 }
 
+/* GCL_LOOP_HDR_RECORDS: packet i of ticket @t's burst as one stamped 64-B
+ * record (the layout above loop_rec_stamp), every 16-B chunk written by one aligned
+ * 16-B store so the GPU never sees a chunk half-written.  The core reads the
+ * header bytes rx_one_pkt reads, prefetching two frames ahead as rx_burst
+ * does (rx.c:281-285); bytes past the region read 0. */
+typedef uint32_t u32x4_h __attribute__((vector_size(16), aligned(16)));
+
+static void loop_write_records(gcl_rxloop *L, uint64_t t, uint8_t *dst, uint32_t n,
+                               const uint64_t *offs, const uint8_t *olflags, const uint32_t *rss,
+                               const uint32_t *fdir_hi, const uint32_t *dst_hint)
+{
+	const uint32_t S = loop_rec_stamp(t, L->lp.nslots);
+	volatile u32x4_h *q = (volatile u32x4_h *)dst;
+	for (uint32_t i = 0; i < n; i++, q += 4) {
+		if (i + 2 < n && offs[i + 2] < L->region_len)
+			__builtin_prefetch(L->region + offs[i + 2] + 12, 0, 3);
+		const uint64_t o = offs[i];
+		/* frame dwords 3-6 and 7-10 (bytes 12-43) in two registers, shuffled
+		 * into the chunks without a trip through memory */
+		u32x4_h v0, v1;
+		if (o < L->region_len && L->region_len - o >= 44) {
+			memcpy(&v0, L->region + o + 12, 16);
+			memcpy(&v1, L->region + o + 28, 16);
+		} else {
+			uint8_t b[32] = {0};
+			if (o < L->region_len && L->region_len - o > 12)
+				memcpy(b, L->region + o + 12, L->region_len - o - 12);
+			memcpy(&v0, b, 16);
+			memcpy(&v1, b + 16, 16);
+		}
+		const uint64_t off = std::min<uint64_t>(o, kLoopOffMask);
+		const uint32_t olf = olflags ? olflags[i] : 0;
+		const u32x4_h sv = {S, S, S, S};
+		const u32x4_h side = {S, 0, rss ? rss[i] : 0u, fdir_hi ? fdir_hi[i] : 0u};
+		q[0] = __builtin_shufflevector(v0, sv, 4, 0, 2, 3);   /* S d3 d5 d6 */
+		q[1] = __builtin_shufflevector(v1, sv, 4, 0, 1, 2);   /* S d7 d8 d9 */
+		q[2] = __builtin_shufflevector(side, v1, 0, 7, 2, 3); /* S d10 rss fdir */
+		q[3] = u32x4_h{S, (uint32_t)off, (uint32_t)(off >> 32) | olf << 8,
+		               dst_hint ? dst_hint[i] : 0u};
+	}
+	/* records past n keep older stamps; rewrite them now and then so that
+	 * none is ever 2^32 uses stale (loop_stamp's rule for the offsets) */
+	if (S % kLoopRefresh == 0)
+		for (uint32_t i = n; i < L->max_burst; i++, q += 4)
+			for (int j = 0; j < 4; j++)
+				q[j] = u32x4_h{S, 0, 0, 0};
+}
+
 extern "C" int64_t gcl_rxloop_submit(struct gcl_rxloop *L, uint32_t n, const uint64_t *offs,
                                      const uint8_t *olflags, const uint32_t *rss,
                                      const uint32_t *fdir_hi, const uint32_t *dst_hint)
@@ -3244,6 +3385,15 @@ extern "C" int64_t gcl_rxloop_submit(struct gcl_rxloop *L, uint32_t n, const uin
 	}
 	LoopSlotHdr *h = loop_slot(L, t);
 	uint8_t *s = (uint8_t *)h;
+	if (L->lp.hdr_rec) {
+		const uint32_t fl = (olflags ? GCL_LOOP_F_OLF : 0) | (rss ? GCL_LOOP_F_RSS : 0) |
+		                    (fdir_hi ? GCL_LOOP_F_FDIR : 0) | (dst_hint ? GCL_LOOP_F_HINT : 0);
+		loop_write_records(L, t, s + L->lp.off_hdr, n, offs, olflags, rss, fdir_hi, dst_hint);
+		__atomic_store_n(&h->word, loop_word(t, n, fl, L->cur_img, L->img_seq), __ATOMIC_RELEASE);
+		L->img_last[L->cur_img] = t;
+		L->next = t;
+		return (int64_t)t;
+	}
 	uint32_t fl = 0;
 	{ /* offsets stamped with the slot's use count (loop_stamp) */
 		uint64_t *so = (uint64_t *)(s + L->lp.off_offs);

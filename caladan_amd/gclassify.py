@@ -124,6 +124,7 @@ class GclRxloopCfg(ctypes.Structure):
 
 
 LOOP_INLINE_HDRS = 0x1
+LOOP_HDR_RECORDS = 0x2
 
 
 class GclVerdict(ctypes.Structure):

@@ -32,6 +32,9 @@ def want(ve, tc, vb, tb=4):
     return to_verdict2(ve, tc, tb) if vb == 2 else to_verdict4(ve, tc) if vb == 4 else ve
 
 
+LOOP_FLAGS = (lambda g: 0, lambda g: g.LOOP_INLINE_HDRS, lambda g: g.LOOP_HDR_RECORDS)
+
+
 def tc_map(rts, max_rt):
     tc = np.ones(max_rt, dtype=np.int64)
     for r in rts:
@@ -39,17 +42,19 @@ def tc_map(rts, max_rt):
     return tc
 
 
-LOOP_CASES = [(m, vb, 0, False) for m in (0, 1, 2) for vb in (8, 4, 2)] + \
-    [(m, 8, fl, False) for m in (0, 1, 2) for fl in (1, 2)] + \
-    [(0, 8, 1, True), (1, 4, 0, True), (2, 8, 2, True), (1, 2, 1, True)]
+LOOP_CASES = [(m, vb, 0, 0) for m in (0, 1, 2) for vb in (8, 4, 2)] + \
+    [(m, 8, fl, 0) for m in (0, 1, 2) for fl in (1, 2)] + \
+    [(0, 8, 1, 1), (1, 4, 0, 1), (2, 8, 2, 1), (1, 2, 1, 1)] + \
+    [(m, vb, 0, 2) for m in (0, 1, 2) for vb in (8, 4, 2)] + [(0, 8, 1, 2), (2, 8, 2, 2)]
 
 
 @pytest.mark.parametrize("mode,vb,flags,inline", LOOP_CASES)
 def test_rxloop_fuzz_vs_oracle(g, orc, mode, vb, flags, inline):
     """vb: verdict bytes (8 gcl_verdict, 4 VERDICT4, 2 VERDICT2);
     flags: 0 plain, 1 Azure ARP mode (GCL_CFG_AZURE_ARP), 2 16-bit hash;
-    inline: header granules copied into the ring slot (GCL_LOOP_INLINE_HDRS),
-    including the frames that straddle the end of the region."""
+    inline: 1 header granules copied into the ring slot (GCL_LOOP_INLINE_HDRS),
+    2 stamped header records (GCL_LOOP_HDR_RECORDS), including the frames that
+    straddle the end of the region and IPv4 options past byte 43."""
     rng = np.random.default_rng(7000 + 10 * mode + vb + 100 * flags + 1000 * inline)
     max_rt = 1024 if mode == 1 else 16
     rts = random_runtimes(rng, max_rt, 300 if max_rt == 1024 else 12)
@@ -67,7 +72,7 @@ def test_rxloop_fuzz_vs_oracle(g, orc, mode, vb, flags, inline):
     cnt = torch.zeros(max_rt, dtype=torch.int64, device="cuda")
     st = torch.zeros(g.NR_STATS, dtype=torch.int64, device="cuda")
     loop = clf.rxloop(frames, slots=8, counts=cnt, stats=st, region_len=flen,
-                      flags=g.LOOP_INLINE_HDRS if inline else 0)
+                      flags=LOOP_FLAGS[inline](g))
     try:
         got = []
         for k, (a, b) in enumerate(bursts(n)):
@@ -99,10 +104,12 @@ def test_rxloop_fuzz_vs_oracle(g, orc, mode, vb, flags, inline):
     assert (st.cpu().numpy().astype(np.uint64) == se).all()
 
 
-def test_rxloop_tables_and_recycled_mbufs(g, orc):
+@pytest.mark.parametrize("lflag", [0, 2])
+def test_rxloop_tables_and_recycled_mbufs(g, orc, lflag):
     """Table changes apply from the next burst on; frames rewritten in place
-    by the CPU between bursts are read fresh (system-scope loads)."""
-    rng = np.random.default_rng(7100)
+    by the CPU between bursts are read fresh (system-scope loads, or the
+    submitting core's header records)."""
+    rng = np.random.default_rng(7100 + lflag)
     max_rt = 64
     rts = random_runtimes(rng, max_rt, 20)
     n = 64
@@ -112,7 +119,7 @@ def test_rxloop_tables_and_recycled_mbufs(g, orc):
     clf = g.Classifier(0, max_rt, 1, 0, 0x09)
     apply_runtimes(clf, rts)
     g.host_register(frames)
-    loop = clf.rxloop(frames, slots=4)
+    loop = clf.rxloop(frames, slots=4, flags=LOOP_FLAGS[lflag](g))
     try:
         for rnd in range(6):
             tk = loop.submit(offs, olf, None, fdir, None)
@@ -182,15 +189,19 @@ def test_rxloop_workers_pipelined_and_full_ring(g, orc):
         g.host_unregister(frames)
 
 
-@pytest.mark.parametrize("max_burst,workers", [(64, 1), (64, 3), (256, 2)])
-def test_rxloop_stamped_offsets_ragged_bursts(g, orc, max_burst, workers):
+@pytest.mark.parametrize("max_burst,workers,lflag", [(64, 1, 0), (64, 3, 0), (256, 2, 0),
+                                                     (64, 1, 2), (64, 3, 2), (256, 2, 2),
+                                                     (1024, 2, 0), (1024, 2, 2)])
+def test_rxloop_stamped_offsets_ragged_bursts(g, orc, max_burst, workers, lflag):
     """Offsets ride in the slot stamped with the slot's use count, and a
     worker polling a burst of <= 64 takes them with the poll when every stamp
-    is current.  Two slots reused ~700 times each (past the periodic rewrite
-    of the entries beyond a burst's n), burst sizes drawn from 1..max_burst
-    so stale entries of longer bursts sit behind shorter ones, and offsets
-    at and past 2^40 (the stamp's bit) that read as frames past the region."""
-    rng = np.random.default_rng(7300 + max_burst + workers)
+    is current (lflag 2: whole header records, GCL_LOOP_HDR_RECORDS, each
+    16-B chunk stamped).  Two slots reused ~700 times each (past the periodic
+    rewrite of the entries beyond a burst's n), burst sizes drawn from
+    1..max_burst so stale entries of longer bursts sit behind shorter ones,
+    and offsets at and past 2^40 (the stamp's bit) that read as frames past
+    the region."""
+    rng = np.random.default_rng(7300 + max_burst + workers + 17 * lflag)
     max_rt = 16
     rts = random_runtimes(rng, max_rt, 12)
     n = 4096
@@ -206,7 +217,8 @@ def test_rxloop_stamped_offsets_ragged_bursts(g, orc, max_burst, workers):
     clf = g.Classifier(0, max_rt, 1, 0, 0x09)
     apply_runtimes(clf, rts)
     g.host_register(frames)
-    loop = clf.rxloop(frames, slots=2, workers=workers, max_burst=max_burst, region_len=flen)
+    loop = clf.rxloop(frames, slots=2, workers=workers, max_burst=max_burst, region_len=flen,
+                      flags=LOOP_FLAGS[lflag](g))
     try:
         nb = 1400
         sizes = np.where(rng.random(nb) < 0.3, max_burst, rng.integers(1, max_burst + 1, size=nb))
@@ -225,7 +237,9 @@ def test_rxloop_stamped_offsets_ragged_bursts(g, orc, max_burst, workers):
 
 
 @pytest.mark.parametrize("cfg", [("200000", "1", "2", "1"), ("400000", "4", "4", "4"),
-                                 ("400000", "32", "64", "64")])
+                                 ("400000", "32", "64", "64"), ("200000", "1", "2", "1", "records"),
+                                 ("400000", "4", "4", "4", "records"),
+                                 ("400000", "32", "64", "64", "records")])
 def test_rxloop_soak_stamped_offsets(g, cfg):
     """tools/loopsoak: random 1..64-packet bursts at random offsets into a
     mixed-traffic region, few slots, a tight host loop with random pauses
@@ -260,6 +274,10 @@ def test_rxloop_lifetime_and_errors(g):
         time.sleep(0.8)
         assert loop.submit(offs) == -108  # -ESHUTDOWN: the kernel left on its own
         loop.stop()
+        with pytest.raises(OSError):  # inline granules and header records exclude each other
+            clf.rxloop(frames, flags=g.LOOP_INLINE_HDRS | g.LOOP_HDR_RECORDS)
+        with pytest.raises(OSError):  # unknown flag
+            clf.rxloop(frames, flags=0x4)
         clf2 = g.Classifier(0, 16, 1, g.CFG_TRANS_HASH)
         with pytest.raises(OSError):
             clf2.rxloop(frames)

@@ -7,9 +7,11 @@
 // polls; every verdict is compared with the batch kernel's verdict for the
 // same packet (the batch path is the one the parity tests pin to the oracle).
 // A torn or stale offset that passed the stamp check would show as a
-// mismatch.
+// mismatch.  With a fifth argument `records` the bursts go in as stamped
+// header records (GCL_LOOP_HDR_RECORDS), whose 16-B chunks the workers read
+// with their polls: a torn or stale chunk that passed would show the same way.
 //
-//   loopsoak <bursts> <workers> <slots> <depth>   -> one JSON line, exit 2 on a mismatch
+//   loopsoak <bursts> <workers> <slots> <depth> [records]   -> one JSON line, exit 2 on a mismatch
 //
 // Build: hipcc --offload-arch=gfx950 -O2 -Iinclude -o tools/loopsoak tools/loopsoak.cpp
 //         -Lcaladan_amd -lgclassify -Wl,-rpath,'$ORIGIN/../caladan_amd'
@@ -44,6 +46,7 @@ int main(int argc, char **argv)
 	const uint32_t workers = argc > 2 ? (uint32_t)atoi(argv[2]) : 4;
 	const uint32_t slots = argc > 3 ? (uint32_t)atoi(argv[3]) : 4;
 	const uint32_t depth = argc > 4 ? (uint32_t)atoi(argv[4]) : 4;
+	const bool records = argc > 5 && !strcmp(argv[5], "records");
 	const uint32_t R = 16, T = 8, stride = 128;
 	const uint64_t n = 1 << 16;
 	if (!nbursts || !workers || workers > 64 || slots < 2 || slots > 1024 || (slots & (slots - 1)) ||
@@ -105,6 +108,7 @@ int main(int argc, char **argv)
 	lc.lifetime_ms = 600000;
 	lc.region = region;
 	lc.region_len = n * stride;
+	lc.flags = records ? GCL_LOOP_HDR_RECORDS : 0;
 	struct gcl_rxloop *loop;
 	GCHECK(gcl_rxloop_start(ctx, &lc, &loop));
 
@@ -151,9 +155,11 @@ int main(int argc, char **argv)
 	}
 	const double sec = (now_ns() - t0) * 1e-9;
 	gcl_rxloop_stop(loop);
-	printf("{\"bursts\": %llu, \"workers\": %u, \"slots\": %u, \"depth\": %u, \"packets_checked\": %llu, "
+	printf("{\"bursts\": %llu, \"workers\": %u, \"slots\": %u, \"depth\": %u, \"records\": %s, "
+	       "\"packets_checked\": %llu, "
 	       "\"mismatches\": %llu, \"first_mismatch_burst\": %lld, \"seconds\": %.1f, \"mpps\": %.1f}\n",
-	       (unsigned long long)nbursts, workers, slots, depth, (unsigned long long)checked,
+	       (unsigned long long)nbursts, workers, slots, depth, records ? "true" : "false",
+	       (unsigned long long)checked,
 	       (unsigned long long)bad, bad ? (long long)first_bad : -1LL, sec, checked / sec / 1e6);
 	gcl_close(ctx);
 	CHECK(hipHostFree(vref));

@@ -1,0 +1,17 @@
+# header records after the register-only record writer: against plain and inline loops,
+# burst 64 on one host core, alternating rounds
+set -o pipefail
+O=gpurun_out/r03zd
+mkdir -p $O
+for rnd in 1 2 3; do
+  for a in "1 1" "4 8" "8 16" "16 32"; do
+    for m in plain inline records; do
+      timeout -k 10 120 ./tools/rxpipe 64 $a 20000 $( [ $m = plain ] || echo $m ) | sed "s/^{/{\"mode\": \"$m\", \"round\": $rnd, /" >> $O/ab.jsonl || exit 1
+    done
+  done
+done
+python3 - <<'PY'
+import json
+for l in open('gpurun_out/r03zd/ab.jsonl'):
+    d=json.loads(l); print(d['round'], d['mode'], d['workers'], d['depth'], d['mpps_one_core'], d['burst_latency_p50_us'], d['burst_latency_p99_us'], d['submit_ns_per_pkt'], d['deliver_ns_per_pkt'])
+PY

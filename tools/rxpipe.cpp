@@ -6,7 +6,7 @@
 // sustains with the GPU classifying, to set beside the reference's own
 // classify + lrpc_send rate on one core (bench.py cpu_baseline.lrpc_1core_mpps).
 //
-//   rxpipe <burst> <workers> <depth> <bursts> [copy|inline]   -> one JSON line
+//   rxpipe <burst> <workers> <depth> <bursts> [copy|inline|records]   -> one JSON line
 //
 // Each burst's verdicts are read in place in the loop's ring slot
 // (gcl_rxloop_peek + gcl_host_deliver_recs, then gcl_rxloop_release); with
@@ -14,7 +14,9 @@
 // gcl_host_deliver4), the round-2 form; with `inline` the submitting core
 // copies each frame's 64-B header granule into the slot
 // (GCL_LOOP_INLINE_HDRS: the core reads the headers, as rx_one_pkt does, and
-// the kernel saves a PCIe round trip).
+// the kernel saves a PCIe round trip); with `records` it writes one stamped
+// 64-B header record per packet (GCL_LOOP_HDR_RECORDS), which a worker reads
+// with its poll: one PCIe round trip per burst of <= 64.
 // Runtime consumers are emulated as infinitely fast and are never touched by
 // the dataplane loop: each ring's recv_head_wb points at its own send_head,
 // so when a ring looks full the producer's refresh (__lrpc_send,
@@ -100,6 +102,7 @@ int main(int argc, char **argv)
 	const uint32_t nbursts = argc > 4 ? (uint32_t)atoi(argv[4]) : 20000;
 	const bool copy_out = argc > 5 && !strcmp(argv[5], "copy");
 	const bool inline_hdrs = argc > 5 && !strcmp(argv[5], "inline");
+	const bool hdr_records = argc > 5 && !strcmp(argv[5], "records");
 	const uint32_t R = 16, T = 8, RING = 4096;
 	const uint64_t nframes = 1 << 16, stride = 64;
 	if (!burst || burst > 4096 || !workers || workers > 64 || !depth || depth > 64) {
@@ -167,7 +170,7 @@ int main(int argc, char **argv)
 	lc.lifetime_ms = 60000;
 	lc.region = region;
 	lc.region_len = nframes * stride;
-	lc.flags = inline_hdrs ? GCL_LOOP_INLINE_HDRS : 0;
+	lc.flags = inline_hdrs ? GCL_LOOP_INLINE_HDRS : hdr_records ? GCL_LOOP_HDR_RECORDS : 0;
 	struct gcl_rxloop *loop;
 	int ret = gcl_rxloop_start(ctx, &lc, &loop);
 	if (ret) {
@@ -261,7 +264,8 @@ int main(int argc, char **argv)
 	       "\"deliver_ns_per_pkt\": %.2f, \"submit_ns_per_pkt\": %.2f, \"wait_ns_per_pkt\": %.2f, "
 	       "\"delivered_check\": \"%s\", \"unicast_fail\": %llu, \"host_cpu\": %d}\n",
 	       burst, workers, depth, nbursts,
-	       copy_out ? "copied out" : inline_hdrs ? "read in place, headers inlined in the slot" : "read in place",
+	       copy_out ? "copied out" : inline_hdrs ? "read in place, headers inlined in the slot"
+	       : hdr_records ? "read in place, stamped header records in the slot" : "read in place",
 	       pkts / (el * 1e-3), lat[lat.size() / 2] * 1e-3,
 	       lat[lat.size() * 99 / 100] * 1e-3, t_deliver / pkts, t_submit / pkts, t_wait / pkts,
 	       delivered == (uint64_t)burst * (nbursts + warm) ? "ok" : "MISMATCH",
