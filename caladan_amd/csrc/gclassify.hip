@@ -3324,6 +3324,8 @@ static void loop_write_records(gcl_rxloop *L, uint64_t t, uint8_t *dst, uint32_t
 {
 	const uint32_t S = loop_rec_stamp(t, L->lp.nslots);
 	volatile u32x4_h *q = (volatile u32x4_h *)dst;
+	/* (prefetching 6 ahead, or the record lines for ownership, measured
+	 * the same: profiles/r03_hdr_records_prefetch_ab.jsonl) */
 	for (uint32_t i = 0; i < n; i++, q += 4) {
 		if (i + 2 < n && offs[i + 2] < L->region_len)
 			__builtin_prefetch(L->region + offs[i + 2] + 12, 0, 3);
