@@ -1366,7 +1366,7 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 			const uint64_t spec_end = __builtin_amdgcn_s_memrealtime() + L.spec_ticks;
 			uint64_t w = 0, e = 0;
 			bool rok = false;
-			uint4 q[4], qv[4]; /* header records: the lane's packet's chunks */
+			uint4 q[4], qv[4] = {}; /* header records: the lane's packet's chunks */
 			for (uint32_t k = 0;; k++) {
 				const bool sp = spec && __builtin_amdgcn_s_memrealtime() < spec_end;
 				const uint64_t ev = sp && !rec ? gcl::ld_sys64(slot + L.off_offs + 8 * tid) : 0;
