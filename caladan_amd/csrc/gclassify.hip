@@ -1353,10 +1353,12 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 		if (tid < 64) {
 			/* wave 0 polls.  One system-scope load of the slot word carries
 			 * the whole burst header, and without inline headers each lane
-			 * also reads its stamped offset entry, so a burst of <= 64
-			 * packets has its offsets when the word shows it.  (The stop flag is read beside every 8th poll,
-			 * never after one: that made each poll two round trips.)  The
-			 * offsets are polled only for the first kLoopSpecTicks of a wait:
+			 * also reads its stamped offset entry (with header records, its
+			 * packet's four stamped chunks), so a burst of <= 64 packets has
+			 * its offsets (or all it needs) when the word shows it.  (The
+			 * stop flag is read beside every 8th poll, never after one: that
+			 * made each poll two round trips.)  The offsets or records are
+			 * polled only for the first L.spec_ticks of a wait:
 			 * a worker that waits longer (many workers, deep queues) polls
 			 * the word alone, so idle polls do not crowd the PCIe requests
 			 * of the workers that are reading frames */
