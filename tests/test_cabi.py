@@ -504,3 +504,19 @@ def test_open_rejects_bad_verdict2_cfg(g):
     assert g.thread_bits_for(16, 8) == 3 and g.thread_bits_for(1024, 4) == 2
     assert g.thread_bits_for(1024, 16) == 4 and g.thread_bits_for(1024, 17) is None
     assert g.thread_bits_for(16, 1) == 0 and g.thread_bits_for(16, 256) == 8
+
+
+def test_python_constants_match_header_defines(g):
+    """Every integer #define GCL_<NAME> in include/*.h that the ctypes
+    binding mirrors as gclassify.<NAME> (flags, modes, counters, loop and
+    group options) has the same value, so a flag added on one side only
+    cannot drift."""
+    defs = {}
+    for h in ("gclassify.h", "gcl_host.h", "gcl_pcap.h", "gcl_group.h"):
+        src = open(os.path.join(ROOT, "include", h)).read()
+        for m in re.finditer(r"^#define\s+GCL_(\w+)\s+\(?(0x[0-9A-Fa-f]+|\d+)u?\)?\s*(?:/\*.*)?$", src, re.M):
+            defs[m.group(1)] = int(m.group(2), 0)
+    mirrored = {k: v for k, v in defs.items() if hasattr(g, k)}
+    assert len(mirrored) >= 25 and "LOOP_HDR_RECORDS" in mirrored, sorted(mirrored)
+    bad = {k: (v, getattr(g, k)) for k, v in mirrored.items() if getattr(g, k) != v}
+    assert not bad, bad
