@@ -3363,6 +3363,43 @@ static void loop_write_records(gcl_rxloop *L, uint64_t t, uint8_t *dst, uint32_t
 				q[j] = u32x4_h{S, 0, 0, 0};
 }
 
+/* Ticket @t's burst into slot @s as stamped offsets, the optional header
+ * granules (GCL_LOOP_INLINE_HDRS) and the side arrays. */
+static void loop_write_arrays(gcl_rxloop *L, uint64_t t, uint8_t *s, uint32_t n,
+                              const uint64_t *offs, const uint8_t *olflags, const uint32_t *rss,
+                              const uint32_t *fdir_hi, const uint32_t *dst_hint)
+{
+	{ /* offsets stamped with the slot's use count (loop_stamp) */
+		uint64_t *so = (uint64_t *)(s + L->lp.off_offs);
+		const uint64_t st = loop_stamp(t, L->lp.nslots);
+		for (uint32_t i = 0; i < n; i++) /* past the region either way: reads 0 */
+			so[i] = std::min<uint64_t>(offs[i], kLoopOffMask) | st;
+		if ((((t - 1) / L->lp.nslots + 1) % kLoopRefresh) == 0)
+			for (uint32_t i = n; i < L->max_burst; i++)
+				so[i] = st;
+	}
+	if (L->lp.off_hdr) { /* the header granules ride in the slot; past the region: 0 */
+		uint8_t *hd = s + L->lp.off_hdr;
+		for (uint32_t i = 0; i < n; i++, hd += GCL_HDR_GRANULE) {
+			const uint64_t o = offs[i];
+			/* no o + granule: an offset near UINT64_MAX must not wrap past the check */
+			const uint64_t k = o < L->region_len ? std::min<uint64_t>(L->region_len - o, GCL_HDR_GRANULE) : 0;
+			if (k)
+				memcpy(hd, L->region + o, k);
+			if (k < GCL_HDR_GRANULE)
+				memset(hd + k, 0, GCL_HDR_GRANULE - k);
+		}
+	}
+	if (olflags)
+		memcpy(s + L->lp.off_olf, olflags, n);
+	if (rss)
+		memcpy(s + L->lp.off_rss, rss, 4ull * n);
+	if (fdir_hi)
+		memcpy(s + L->lp.off_fdir, fdir_hi, 4ull * n);
+	if (dst_hint)
+		memcpy(s + L->lp.off_hint, dst_hint, 4ull * n);
+}
+
 extern "C" int64_t gcl_rxloop_submit(struct gcl_rxloop *L, uint32_t n, const uint64_t *offs,
                                      const uint8_t *olflags, const uint32_t *rss,
                                      const uint32_t *fdir_hi, const uint32_t *dst_hint)
@@ -3389,53 +3426,12 @@ extern "C" int64_t gcl_rxloop_submit(struct gcl_rxloop *L, uint32_t n, const uin
 	}
 	LoopSlotHdr *h = loop_slot(L, t);
 	uint8_t *s = (uint8_t *)h;
-	if (L->lp.hdr_rec) {
-		const uint32_t fl = (olflags ? GCL_LOOP_F_OLF : 0) | (rss ? GCL_LOOP_F_RSS : 0) |
-		                    (fdir_hi ? GCL_LOOP_F_FDIR : 0) | (dst_hint ? GCL_LOOP_F_HINT : 0);
+	const uint32_t fl = (olflags ? GCL_LOOP_F_OLF : 0) | (rss ? GCL_LOOP_F_RSS : 0) |
+	                    (fdir_hi ? GCL_LOOP_F_FDIR : 0) | (dst_hint ? GCL_LOOP_F_HINT : 0);
+	if (L->lp.hdr_rec) /* everything rides in the records */
 		loop_write_records(L, t, s + L->lp.off_hdr, n, offs, olflags, rss, fdir_hi, dst_hint);
-		__atomic_store_n(&h->word, loop_word(t, n, fl, L->cur_img, L->img_seq), __ATOMIC_RELEASE);
-		L->img_last[L->cur_img] = t;
-		L->next = t;
-		return (int64_t)t;
-	}
-	uint32_t fl = 0;
-	{ /* offsets stamped with the slot's use count (loop_stamp) */
-		uint64_t *so = (uint64_t *)(s + L->lp.off_offs);
-		const uint64_t st = loop_stamp(t, L->lp.nslots);
-		for (uint32_t i = 0; i < n; i++) /* past the region either way: reads 0 */
-			so[i] = std::min<uint64_t>(offs[i], kLoopOffMask) | st;
-		if ((((t - 1) / L->lp.nslots + 1) % kLoopRefresh) == 0)
-			for (uint32_t i = n; i < L->max_burst; i++)
-				so[i] = st;
-	}
-	if (L->lp.off_hdr) { /* the header granules ride in the slot; past the region: 0 */
-		uint8_t *hd = s + L->lp.off_hdr;
-		for (uint32_t i = 0; i < n; i++, hd += GCL_HDR_GRANULE) {
-			const uint64_t o = offs[i];
-			/* no o + granule: an offset near UINT64_MAX must not wrap past the check */
-			const uint64_t k = o < L->region_len ? std::min<uint64_t>(L->region_len - o, GCL_HDR_GRANULE) : 0;
-			if (k)
-				memcpy(hd, L->region + o, k);
-			if (k < GCL_HDR_GRANULE)
-				memset(hd + k, 0, GCL_HDR_GRANULE - k);
-		}
-	}
-	if (olflags) {
-		memcpy(s + L->lp.off_olf, olflags, n);
-		fl |= GCL_LOOP_F_OLF;
-	}
-	if (rss) {
-		memcpy(s + L->lp.off_rss, rss, 4ull * n);
-		fl |= GCL_LOOP_F_RSS;
-	}
-	if (fdir_hi) {
-		memcpy(s + L->lp.off_fdir, fdir_hi, 4ull * n);
-		fl |= GCL_LOOP_F_FDIR;
-	}
-	if (dst_hint) {
-		memcpy(s + L->lp.off_hint, dst_hint, 4ull * n);
-		fl |= GCL_LOOP_F_HINT;
-	}
+	else
+		loop_write_arrays(L, t, s, n, offs, olflags, rss, fdir_hi, dst_hint);
 	__atomic_store_n(&h->word, loop_word(t, n, fl, L->cur_img, L->img_seq), __ATOMIC_RELEASE);
 	L->img_last[L->cur_img] = t;
 	L->next = t;
