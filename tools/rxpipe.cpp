@@ -172,7 +172,9 @@ int main(int argc, char **argv)
 	}
 
 	struct gcl_rxloop_cfg lc = {};
-	lc.slots = 64;
+	lc.slots = 64; /* RXPIPE_SLOTS overrides (a power of two >= 2 * depth) */
+	if (const char *e = getenv("RXPIPE_SLOTS"))
+		lc.slots = (uint32_t)atoi(e);
 	lc.max_burst = burst;
 	lc.workers = workers;
 	lc.lifetime_ms = 60000;
