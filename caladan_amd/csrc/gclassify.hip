@@ -1215,6 +1215,11 @@ constexpr uint64_t kLoopRefresh = 256;
 /* s_memrealtime ticks (100 MHz) a wait polls the offsets with the word: a
  * burst that arrives later costs the offsets' round trip after the word */
 constexpr uint64_t kLoopSpecTicks = 400;
+/* how a worker's bursts arrived (gcl_rxloop_poll_stats): with the poll that
+ * found the word; eligible for that, but an entry or record still stale so
+ * read after it; or after the word, the speculative window over or the
+ * burst too long for it */
+enum { kLoopPollEarly = 0, kLoopPollStale = 1, kLoopPollLate = 2 };
 __host__ __device__ constexpr uint64_t loop_stamp(uint64_t t, uint32_t nslots)
 {
 	return (((t - 1) / nslots + 1) & 0xFFFFFF) << kLoopStampShift;
@@ -1239,6 +1244,8 @@ struct LoopParams {
 	const uint32_t *stop;
 	uint32_t *where;           /* host words: XCC_ID + 1 of worker b at [b] (b < 8) */
 	uint32_t *exited;          /* host word: set by a worker that leaves */
+	uint32_t *polls;           /* host words: worker b's bursts at [4b + k] by how they
+	                              arrived (kLoopPollEarly / Stale / Late) */
 	uint64_t lifetime_ticks;   /* s_memrealtime ticks each block may run */
 	const uint8_t *frames;     /* device view of the registered region */
 	uint64_t frames_len;
@@ -1345,6 +1352,7 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 	k.default_flags = L.default_flags;
 	Tables tb = {};
 	uint32_t cur_seq = 0xFF; /* no image yet (versions are taken mod 64) */
+	uint32_t polls[3] = {0, 0, 0};
 
 	for (uint64_t t = blockIdx.x + 1;; t += L.workers) {
 		uint8_t *slot = L.slots + ((t - 1) % L.nslots) * L.slot_bytes;
@@ -1367,7 +1375,7 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 			const uint32_t rstamp = loop_rec_stamp(t, L.nslots);
 			const uint64_t spec_end = __builtin_amdgcn_s_memrealtime() + L.spec_ticks;
 			uint64_t w = 0, e = 0;
-			bool rok = false;
+			bool rok = false, sp_hit = false;
 			uint4 q[4], qv[4] = {}; /* header records: the lane's packet's chunks */
 			for (uint32_t k = 0;; k++) {
 				const bool sp = spec && __builtin_amdgcn_s_memrealtime() < spec_end;
@@ -1392,6 +1400,7 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 				if ((wv >> 24) == (t & ((1ull << 40) - 1))) {
 					w = wv;
 					e = ev;
+					sp_hit = sp;
 					rok = sp && qv[0].x == rstamp && qv[1].x == rstamp && qv[2].x == rstamp &&
 					      qv[3].x == rstamp;
 #pragma unroll
@@ -1412,6 +1421,12 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 					rec_to_row(q, tile, tid, s0.offs, s0.olf, s0.rss, s0.fdir, s0.hint);
 				else
 					s0.offs[tid] = e & kLoopOffMask;
+			}
+			if (tid == 0 && w) {
+				const int k = early ? kLoopPollEarly
+				            : (sp_hit && nw <= 64) ? kLoopPollStale : kLoopPollLate;
+				polls[k]++;
+				gcl::st_sys32(&L.polls[4 * blockIdx.x + k], polls[k]);
 			}
 			if (tid == 0) {
 				s_ctl[0] = w != 0;
@@ -3087,6 +3102,11 @@ static int page_node(const void *p)
 	return status;
 }
 
+/* the loop's control page: [0] stop, [1] exited, [8, 16) where, then 4
+ * poll counters per worker (gcl_rxloop_poll_stats) */
+constexpr uint32_t kLoopCtlPolls = 64;
+constexpr size_t kLoopCtlBytes = 4 * (kLoopCtlPolls + 4 * 64);
+
 struct gcl_rxloop {
 	gcl_ctx *c;
 	hipStream_t st;
@@ -3261,10 +3281,10 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 	if (hipHostMalloc((void **)&L->slots, lp.nslots * lp.slot_bytes, hf) != hipSuccess ||
 	    hipHostMalloc((void **)&L->img[0], 64 + c->image_cap, hf) != hipSuccess ||
 	    hipHostMalloc((void **)&L->img[1], 64 + c->image_cap, hf) != hipSuccess ||
-	    hipHostMalloc((void **)&L->ctl, 64, hf) != hipSuccess)
+	    hipHostMalloc((void **)&L->ctl, kLoopCtlBytes, hf) != hipSuccess)
 		goto fail;
 	memset(L->slots, 0, lp.nslots * lp.slot_bytes);
-	memset(L->ctl, 0, 64);
+	memset(L->ctl, 0, kLoopCtlBytes);
 	if (getenv("GCL_LOOP_DEBUG"))
 		fprintf(stderr, "gcl_rxloop_start: NUMA node of slots %d, image %d, ctl %d, region %d\n",
 		        page_node(L->slots), page_node(L->img[0]), page_node(L->ctl),
@@ -3288,6 +3308,7 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 	lp.stop = (const uint32_t *)d;
 	lp.where = (uint32_t *)d + 8;
 	lp.exited = (uint32_t *)d + 1;
+	lp.polls = (uint32_t *)d + kLoopCtlPolls;
 	if (hipStreamCreateWithFlags(&L->st, hipStreamNonBlocking) != hipSuccess)
 		goto fail;
 	{
@@ -3531,6 +3552,17 @@ extern "C" int gcl_rxloop_wait(struct gcl_rxloop *L, int64_t ticket, void *verdi
 	uint64_t &r = L->retired[(t - 1) % L->lp.nslots];
 	if (r < t)
 		r = t;
+	return 0;
+}
+
+extern "C" int gcl_rxloop_poll_stats(struct gcl_rxloop *L, uint64_t out[3])
+{
+	if (!L || !out)
+		return -EINVAL;
+	out[0] = out[1] = out[2] = 0;
+	for (uint32_t w = 0; w < L->lp.workers; w++)
+		for (int k = 0; k < 3; k++)
+			out[k] += __atomic_load_n(&L->ctl[kLoopCtlPolls + 4 * w + k], __ATOMIC_RELAXED);
 	return 0;
 }
 

@@ -224,6 +224,7 @@ def _load():
                                         vp, ctypes.c_uint8, vp, u64, ctypes.POINTER(GclHostOps), vp]),
         "gcl_rxloop_peek": (i32, [vp, ctypes.c_int64, u64, ctypes.POINTER(vp), ctypes.POINTER(u32)]),
         "gcl_rxloop_release": (i32, [vp, ctypes.c_int64]),
+        "gcl_rxloop_poll_stats": (i32, [vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -784,6 +785,12 @@ class RxLoop:
 
     def release(self, ticket):
         return _check(lib.gcl_rxloop_release(self._h, ticket), "gcl_rxloop_release")
+
+    def poll_stats(self):
+        """{early, stale, late}: how the bursts so far arrived (gcl_rxloop_poll_stats)."""
+        out = np.zeros(3, dtype=np.uint64)
+        _check(lib.gcl_rxloop_poll_stats(self._h, out.ctypes.data), "gcl_rxloop_poll_stats")
+        return dict(zip(("early", "stale", "late"), (int(x) for x in out)))
 
     def drive(self, offs, iters, depth=1):
         offs = np.ascontiguousarray(offs, dtype=np.uint64)

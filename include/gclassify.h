@@ -552,6 +552,13 @@ struct gcl_loop_rec {
 int gcl_rxloop_peek(struct gcl_rxloop *loop, int64_t ticket, uint64_t spin_ns,
                     const struct gcl_loop_rec **recs, uint32_t *n);
 int gcl_rxloop_release(struct gcl_rxloop *loop, int64_t ticket);
+/* gcl_rxloop_poll_stats - how the loop's bursts have arrived so far, summed
+ * over its workers: @out[0] with the poll that found the burst (offsets or
+ * header records already current: one PCIe round trip), @out[1] eligible
+ * for that (<= 64 packets, in the speculative window) but an entry still
+ * stale, so read after the word, @out[2] read after the word (the window
+ * over, a longer burst, or inline granules).  Before gcl_rxloop_stop. */
+int gcl_rxloop_poll_stats(struct gcl_rxloop *loop, uint64_t out[3]);
 int gcl_rxloop_stop(struct gcl_rxloop *loop);
 int gcl_rxloop_drive(struct gcl_rxloop *loop, uint32_t n, const uint64_t *offs, uint32_t iters,
                      uint32_t depth, uint64_t *lat_ns, uint64_t *elapsed_ns);

@@ -192,7 +192,7 @@ def test_rxloop_workers_pipelined_and_full_ring(g, orc):
 @pytest.mark.parametrize("max_burst,workers,lflag", [(64, 1, 0), (64, 3, 0), (256, 2, 0),
                                                      (64, 1, 2), (64, 3, 2), (256, 2, 2),
                                                      (1024, 2, 0), (1024, 2, 2)])
-def test_rxloop_stamped_offsets_ragged_bursts(g, orc, max_burst, workers, lflag):
+def test_rxloop_stamped_offsets_ragged_bursts(g, orc, max_burst, workers, lflag, monkeypatch):
     """Offsets ride in the slot stamped with the slot's use count, and a
     worker polling a burst of <= 64 takes them with the poll when every stamp
     is current (lflag 2: whole header records, GCL_LOOP_HDR_RECORDS, each
@@ -217,6 +217,10 @@ def test_rxloop_stamped_offsets_ragged_bursts(g, orc, max_burst, workers, lflag)
     clf = g.Classifier(0, max_rt, 1, 0, 0x09)
     apply_runtimes(clf, rts)
     g.host_register(frames)
+    # Python takes longer than the default 4-us speculative window between
+    # bursts: widen it (GCL_TUNE_LOOP_SPEC, 10-ns ticks) so that the bursts
+    # really arrive with the poll here, as they do from a C dataplane loop
+    monkeypatch.setenv("GCL_TUNE_LOOP_SPEC", "500000")
     loop = clf.rxloop(frames, slots=2, workers=workers, max_burst=max_burst, region_len=flen,
                       flags=LOOP_FLAGS[lflag](g))
     try:
@@ -231,6 +235,16 @@ def test_rxloop_stamped_offsets_ragged_bursts(g, orc, max_burst, workers, lflag)
             got = loop.wait(tk, int(m))
             bad = np.nonzero(got != ve[idx])[0]
             assert not len(bad), f"burst {k} (n {m}): packet {bad[0]} {got[bad[0]]} vs {ve[idx][bad[0]]}"
+        for _ in range(100):  # the counters are posted writes of their own
+            ps = loop.poll_stats()
+            if sum(ps.values()) == nb:
+                break
+            time.sleep(0.001)
+        assert sum(ps.values()) == nb, ps
+        if max_burst <= 64:  # the one-round-trip path really ran
+            assert ps["early"] > nb // 4, ps
+        else:
+            assert ps["early"] == 0 and ps["stale"] == 0, ps
     finally:
         loop.stop()
         g.host_unregister(frames)

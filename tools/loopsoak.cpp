@@ -154,13 +154,17 @@ int main(int argc, char **argv)
 		done++;
 	}
 	const double sec = (now_ns() - t0) * 1e-9;
+	uint64_t ps[3] = {0, 0, 0};
+	gcl_rxloop_poll_stats(loop, ps);
 	gcl_rxloop_stop(loop);
 	printf("{\"bursts\": %llu, \"workers\": %u, \"slots\": %u, \"depth\": %u, \"records\": %s, "
 	       "\"packets_checked\": %llu, "
-	       "\"mismatches\": %llu, \"first_mismatch_burst\": %lld, \"seconds\": %.1f, \"mpps\": %.1f}\n",
+	       "\"mismatches\": %llu, \"first_mismatch_burst\": %lld, \"seconds\": %.1f, \"mpps\": %.1f, "
+	       "\"bursts_early\": %llu, \"bursts_stale\": %llu, \"bursts_late\": %llu}\n",
 	       (unsigned long long)nbursts, workers, slots, depth, records ? "true" : "false",
 	       (unsigned long long)checked,
-	       (unsigned long long)bad, bad ? (long long)first_bad : -1LL, sec, checked / sec / 1e6);
+	       (unsigned long long)bad, bad ? (long long)first_bad : -1LL, sec, checked / sec / 1e6,
+	       (unsigned long long)ps[0], (unsigned long long)ps[1], (unsigned long long)ps[2]);
 	gcl_close(ctx);
 	CHECK(hipHostFree(vref));
 	CHECK(hipHostFree(region));

@@ -275,6 +275,8 @@ int main(int argc, char **argv)
 	pump(nbursts, true);
 	const uint64_t el = now_ns() - t0;
 	const double ns_tick = (double)el / (double)(ticks() - k0);
+	uint64_t ps[3] = {0, 0, 0};
+	gcl_rxloop_poll_stats(loop, ps);
 	gcl_rxloop_stop(loop);
 	std::sort(lat.begin(), lat.end());
 	const double pkts = (double)burst * nbursts;
@@ -283,7 +285,8 @@ int main(int argc, char **argv)
 	       "\"mpps_one_core\": %.2f, "
 	       "\"burst_latency_p50_us\": %.2f, \"burst_latency_p99_us\": %.2f, "
 	       "\"deliver_ns_per_pkt\": %.2f, \"submit_ns_per_pkt\": %.2f, \"wait_ns_per_pkt\": %.2f, "
-	       "\"delivered_check\": \"%s\", \"unicast_fail\": %llu, \"host_cpu\": %d}\n",
+	       "\"delivered_check\": \"%s\", \"unicast_fail\": %llu, \"host_cpu\": %d, "
+	       "\"bursts_early\": %llu, \"bursts_stale\": %llu, \"bursts_late\": %llu}\n",
 	       burst, workers, depth, nbursts,
 	       copy_out ? "copied out" : inline_hdrs ? "read in place, headers inlined in the slot"
 	       : hdr_records ? "read in place, stamped header records in the slot" : "read in place",
@@ -291,7 +294,8 @@ int main(int argc, char **argv)
 	       lat[lat.size() * 99 / 100] * ns_tick * 1e-3, t_deliver * ns_tick / tail_pkts,
 	       t_submit * ns_tick / sub_pkts, t_wait * ns_tick / tail_pkts,
 	       delivered == (uint64_t)burst * (nbursts + warm) ? "ok" : "MISMATCH",
-	       (unsigned long long)stats[GCL_RX_UNICAST_FAIL], cpu);
+	       (unsigned long long)stats[GCL_RX_UNICAST_FAIL], cpu, (unsigned long long)ps[0],
+	       (unsigned long long)ps[1], (unsigned long long)ps[2]);
 	gcl_close(ctx);
 	CHECK(hipHostFree(region));
 	return 0;
