@@ -526,7 +526,10 @@ struct gcl_rxloop_cfg {
  * packets reads the records with the slot word and, when every chunk carries
  * the current count, classifies at once: one PCIe round trip per burst
  * instead of two.  Ports past byte 43 (IHL >= 7) are read from the region.
- * Exclusive with GCL_LOOP_INLINE_HDRS (-EINVAL). */
+ * Exclusive with GCL_LOOP_INLINE_HDRS (-EINVAL).  A worker polls the records
+ * (or, without this flag, the stamped offsets) during the first 4 us of a
+ * wait (GCL_TUNE_LOOP_SPEC in the environment at gcl_rxloop_start: the
+ * window in 10-ns ticks); a burst found later is read after its word. */
 #define GCL_LOOP_HDR_RECORDS 0x2
 int gcl_rxloop_start(struct gcl_ctx *ctx, const struct gcl_rxloop_cfg *cfg,
                      struct gcl_rxloop **out);
