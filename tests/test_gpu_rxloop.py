@@ -49,7 +49,7 @@ LOOP_CASES = [(m, vb, 0, 0) for m in (0, 1, 2) for vb in (8, 4, 2)] + \
 
 
 @pytest.mark.parametrize("mode,vb,flags,inline", LOOP_CASES)
-def test_rxloop_fuzz_vs_oracle(g, orc, mode, vb, flags, inline):
+def test_rxloop_fuzz_vs_oracle(g, orc, mode, vb, flags, inline, monkeypatch):
     """vb: verdict bytes (8 gcl_verdict, 4 VERDICT4, 2 VERDICT2);
     flags: 0 plain, 1 Azure ARP mode (GCL_CFG_AZURE_ARP), 2 16-bit hash;
     inline: 1 header granules copied into the ring slot (GCL_LOOP_INLINE_HDRS),
@@ -71,6 +71,8 @@ def test_rxloop_fuzz_vs_oracle(g, orc, mode, vb, flags, inline):
     g.host_register(frames)
     cnt = torch.zeros(max_rt, dtype=torch.int64, device="cuda")
     st = torch.zeros(g.NR_STATS, dtype=torch.int64, device="cuda")
+    if inline == 2:  # header records taken with the poll (see the ragged-burst test)
+        monkeypatch.setenv("GCL_TUNE_LOOP_SPEC", "500000")
     loop = clf.rxloop(frames, slots=8, counts=cnt, stats=st, region_len=flen,
                       flags=LOOP_FLAGS[inline](g))
     try:
@@ -93,6 +95,8 @@ def test_rxloop_fuzz_vs_oracle(g, orc, mode, vb, flags, inline):
                 got.append(rec["verdict"].astype(np.uint16))
             loop.release(tk)
         got = np.concatenate(got)
+        if inline == 2:  # the side fields went through the one-round-trip path too
+            assert loop.poll_stats()["early"] > 0
     finally:
         loop.stop()
         g.host_unregister(frames)
