@@ -71,7 +71,10 @@ def test_rxloop_fuzz_vs_oracle(g, orc, mode, vb, flags, inline, monkeypatch):
     g.host_register(frames)
     cnt = torch.zeros(max_rt, dtype=torch.int64, device="cuda")
     st = torch.zeros(g.NR_STATS, dtype=torch.int64, device="cuda")
-    if inline == 2:  # header records taken with the poll (see the ragged-burst test)
+    # header records, and the offsets of the NIC-mode cases, taken with the
+    # poll (see the ragged-burst test); the other cases read after the word
+    early = inline == 2 or (inline == 0 and mode == 0)
+    if early:
         monkeypatch.setenv("GCL_TUNE_LOOP_SPEC", "500000")
     loop = clf.rxloop(frames, slots=8, counts=cnt, stats=st, region_len=flen,
                       flags=LOOP_FLAGS[inline](g))
@@ -95,8 +98,9 @@ def test_rxloop_fuzz_vs_oracle(g, orc, mode, vb, flags, inline, monkeypatch):
                 got.append(rec["verdict"].astype(np.uint16))
             loop.release(tk)
         got = np.concatenate(got)
-        if inline == 2:  # the side fields went through the one-round-trip path too
-            assert loop.poll_stats()["early"] > 0
+        ps = loop.poll_stats()
+        if early:  # the side fields went through the one-round-trip path too
+            assert ps["early"] > 0, ps
     finally:
         loop.stop()
         g.host_unregister(frames)
