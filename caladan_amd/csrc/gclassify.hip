@@ -1226,7 +1226,7 @@ __host__ __device__ constexpr uint64_t loop_stamp(uint64_t t, uint32_t nslots)
 }
 
 struct LoopImgHdr {        /* first 64 B of a table image buffer */
-	uint32_t bytes, ipt_mask, off_rt, off_flow, off_toep, ipt_seed, pad[10];
+	uint32_t bytes, ipt_mask, off_rt, off_flow, off_toep, ipt_seed, off_seed, off_crc, pad[8];
 };
 static_assert(sizeof(LoopImgHdr) == 64, "LoopImgHdr");
 
@@ -1256,6 +1256,7 @@ struct LoopParams {
 	uint32_t spec;             /* bursts <= 64: poll the stamped offsets (or records) too */
 	uint32_t hdr_rec;          /* off_hdr holds header records (GCL_LOOP_HDR_RECORDS) */
 	uint32_t spec_ticks;       /* how long a wait polls them (s_memrealtime ticks) */
+	uint32_t off_trans;        /* GCL_CFG_TRANS_HASH: 16-B {h5, h3, ticket} per packet; else 0 */
 };
 
 /* GCL_LOOP_HDR_RECORDS: the submitting core writes each packet as one 64-B
@@ -1290,9 +1291,10 @@ __device__ __forceinline__ void rec_to_row(const uint4 *q, uint4 *tile, int p, u
 	hint[p] = q[3].w;
 }
 
-/* header tile + 2 x side arrays (offs, rss, fdir, hint, olflags) + verdicts + ctl */
+/* header tile + 2 x side arrays (offs, rss, fdir, hint, olflags) + verdicts +
+ * transport hashes + ctl */
 constexpr uint32_t kLoopSide = 256 * 8 + 3 * 256 * 4 + 256;
-constexpr uint32_t kLoopFixedLds = 256 * 64 + 2 * kLoopSide + 256 * 8 + 64;
+constexpr uint32_t kLoopFixedLds = 256 * 64 + 2 * kLoopSide + 2 * 256 * 8 + 64;
 
 /* Side arrays of one 256-packet chunk, double-buffered in LDS so the next
  * chunk's arrive while the current one is classified. */
@@ -1334,7 +1336,8 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 	 * LoopSide indexed by chunk parity would live in scratch) */
 	auto side = [&](uint32_t b) { return LoopSide(side_mem + (b & 1) * kLoopSide); };
 	uint2 *s_verd = (uint2 *)(side_mem + 2 * kLoopSide);
-	uint32_t *s_ctl = (uint32_t *)(s_verd + 256);
+	uint2 *s_trans = s_verd + 256;
+	uint32_t *s_ctl = (uint32_t *)(s_trans + 256);
 	uint32_t *hist = s_ctl + 16;
 	uint8_t *lds_tab = (uint8_t *)(hist + ((L.max_rt + 3) & ~3u));
 	const int tid = threadIdx.x;
@@ -1350,6 +1353,7 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 	k.max_rt = L.max_rt;
 	k.cflags = L.cflags; /* with thread_bits in [31:24] */
 	k.default_flags = L.default_flags;
+	k.trans = L.off_trans ? s_trans : nullptr; /* classify_core's per-packet pair */
 	Tables tb = {};
 	uint32_t cur_seq = 0xFF; /* no image yet (versions are taken mod 64) */
 	uint32_t polls[3] = {0, 0, 0};
@@ -1458,6 +1462,8 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 			tb.rtab = (const RtEntry *)(lds_tab + gcl::ld_sys32(ib + 8));
 			tb.flow = lds_tab + gcl::ld_sys32(ib + 12);
 			tb.toep = (const uint32_t *)(lds_tab + gcl::ld_sys32(ib + 16));
+			tb.seed = (const uint32_t *)(lds_tab + gcl::ld_sys32(ib + 24));
+			tb.crc = (const uint32_t *)(lds_tab + gcl::ld_sys32(ib + 28));
 			cur_seq = img_seq;
 		}
 		for (uint32_t i = tid; i < L.max_rt; i += 256)
@@ -1546,6 +1552,11 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 				const uint32_t hsh = v4 || v2 ? 0u : s_verd[tid].x;
 				const uint32_t vlo = v2 ? ((const uint16_t *)s_verd)[tid]
 				                   : v4 ? ((const uint32_t *)s_verd)[tid] : s_verd[tid].y;
+				if (L.off_trans) { /* before the record: the host checks both tickets */
+					const gcl::u32x4 tr = {s_trans[tid].x, s_trans[tid].y, (uint32_t)t, (uint32_t)(t >> 32)};
+					__builtin_amdgcn_raw_buffer_store_b128(tr, srs, (int)(L.off_trans + 16 * (base + tid)),
+					                                       0, gcl::kSysAux);
+				}
 				const gcl::u32x4 rec = {hsh, vlo, (uint32_t)t, (uint32_t)(t >> 32)};
 				__builtin_amdgcn_raw_buffer_store_b128(
 				        rec, srs, (int)(L.off_verd + sizeof(LoopRec) * (base + tid)), 0, gcl::kSysAux);
@@ -3169,6 +3180,12 @@ static bool burst_complete(gcl_rxloop *L, uint64_t t)
 	for (uint32_t i = n; i-- > 0;)
 		if (__atomic_load_n(&r[i].ticket, __ATOMIC_ACQUIRE) != t)
 			return false;
+	if (L->lp.off_trans) { /* the transport hashes land by stores of their own */
+		const LoopRec *tr = (const LoopRec *)((const uint8_t *)h + L->lp.off_trans);
+		for (uint32_t i = n; i-- > 0;)
+			if (__atomic_load_n(&tr[i].ticket, __ATOMIC_ACQUIRE) != t)
+				return false;
+	}
 	return true;
 }
 
@@ -3197,6 +3214,8 @@ static int loop_write_image(gcl_rxloop *L, int i)
 	hdr.off_rt = c->off_rt;
 	hdr.off_flow = c->off_flow;
 	hdr.off_toep = c->off_toep;
+	hdr.off_seed = c->off_seed;
+	hdr.off_crc = c->off_crc;
 	memcpy(L->img[i] + 64, c->staging, bytes);
 	memcpy(L->img[i], &hdr, sizeof(hdr));
 	c->loop_dirty = false;
@@ -3225,8 +3244,6 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 	    cfg->max_burst > 4096 || !cfg->workers || cfg->workers > 64 || !cfg->lifetime_ms ||
 	    cfg->lifetime_ms > 600000)
 		return -EINVAL;
-	if (c->cfg.flags & GCL_CFG_TRANS_HASH)
-		return -ENOTSUP;
 	if ((cfg->flags & ~(uint32_t)(GCL_LOOP_INLINE_HDRS | GCL_LOOP_HDR_RECORDS)) ||
 	    (cfg->flags & GCL_LOOP_INLINE_HDRS && cfg->flags & GCL_LOOP_HDR_RECORDS))
 		return -EINVAL;
@@ -3263,8 +3280,11 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 	lp.spec_ticks = kLoopSpecTicks;
 	if (const char *e = getenv("GCL_TUNE_LOOP_SPEC")) /* experiments: ticks of 10 ns */
 		lp.spec_ticks = (uint32_t)atoi(e);
-	lp.slot_bytes = (lp.off_verd + sizeof(LoopRec) * mb + (lp.off_hdr ? GCL_HDR_GRANULE * mb : 0) +
-	                 255) & ~255ull;
+	{
+		const uint64_t end = lp.off_verd + sizeof(LoopRec) * mb + (lp.off_hdr ? GCL_HDR_GRANULE * mb : 0);
+		lp.off_trans = (c->cfg.flags & GCL_CFG_TRANS_HASH) ? (uint32_t)end : 0;
+		lp.slot_bytes = (end + (lp.off_trans ? 16 * mb : 0) + 255) & ~255ull;
+	}
 	lp.nslots = cfg->slots;
 	lp.workers = cfg->workers;
 	lp.lifetime_ticks = (uint64_t)cfg->lifetime_ms * 100000ull;
@@ -3552,6 +3572,25 @@ extern "C" int gcl_rxloop_wait(struct gcl_rxloop *L, int64_t ticket, void *verdi
 	uint64_t &r = L->retired[(t - 1) % L->lp.nslots];
 	if (r < t)
 		r = t;
+	return 0;
+}
+
+extern "C" int gcl_rxloop_trans(struct gcl_rxloop *L, int64_t ticket, struct gcl_trans *out)
+{
+	if (!L || !out || ticket < 1 || (uint64_t)ticket > L->next || !L->lp.off_trans)
+		return -EINVAL;
+	const uint64_t t = (uint64_t)ticket;
+	if (t + L->lp.nslots <= L->next)
+		return -ESTALE;
+	if (!burst_complete(L, t))
+		return -EAGAIN;
+	const LoopSlotHdr *h = loop_slot(L, t);
+	const uint32_t n = (uint32_t)(h->word >> 11) & 0x1FFF;
+	const LoopRec *tr = (const LoopRec *)((const uint8_t *)h + L->lp.off_trans);
+	for (uint32_t i = 0; i < n; i++) {
+		out[i].h5 = tr[i].hash;
+		out[i].h3 = tr[i].vlo;
+	}
 	return 0;
 }
 

@@ -225,6 +225,7 @@ def _load():
         "gcl_rxloop_peek": (i32, [vp, ctypes.c_int64, u64, ctypes.POINTER(vp), ctypes.POINTER(u32)]),
         "gcl_rxloop_release": (i32, [vp, ctypes.c_int64]),
         "gcl_rxloop_poll_stats": (i32, [vp, vp]),
+        "gcl_rxloop_trans": (i32, [vp, ctypes.c_int64, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -785,6 +786,12 @@ class RxLoop:
 
     def release(self, ticket):
         return _check(lib.gcl_rxloop_release(self._h, ticket), "gcl_rxloop_release")
+
+    def trans(self, ticket, n):
+        """The burst's transport demux hashes (TRANS_DTYPE[n]), GCL_CFG_TRANS_HASH contexts."""
+        out = np.zeros(n, dtype=TRANS_DTYPE)
+        _check(lib.gcl_rxloop_trans(self._h, ticket, out.ctypes.data), "gcl_rxloop_trans")
+        return out
 
     def poll_stats(self):
         """{early, stale, late}: how the bursts so far arrived (gcl_rxloop_poll_stats)."""

@@ -478,7 +478,8 @@ int gcl_dev_alloc_paired(int hip_device, size_t bytes, const void *partner, size
  *   registered with gcl_host_register; frames are addressed by byte offsets
  *   into it (mbuf data pointer - region base, like ptr_to_shmptr, shm.h:40-47).
  *   The kernel leaves by itself after @cfg->lifetime_ms.  Tables must fit in
- *   LDS (-E2BIG otherwise); GCL_CFG_TRANS_HASH is not supported (-ENOTSUP);
+ *   LDS (-E2BIG otherwise); with GCL_CFG_TRANS_HASH each burst's transport
+ *   demux hashes come back beside its verdicts (gcl_rxloop_trans);
  *   one loop per context (-EBUSY); the region must be shorter than 2^40 - 64
  *   bytes (-EINVAL: offsets share their slot entry with a stamp, so a burst
  *   of <= 64 packets has its offsets with the poll that finds it; offsets at
@@ -562,6 +563,13 @@ int gcl_rxloop_release(struct gcl_rxloop *loop, int64_t ticket);
  * stale, so read after the word, @out[2] read after the word (the window
  * over, a longer burst, or inline granules).  Before gcl_rxloop_stop. */
 int gcl_rxloop_poll_stats(struct gcl_rxloop *loop, uint64_t out[3]);
+/* gcl_rxloop_trans - a GCL_CFG_TRANS_HASH context's transport demux hashes
+ * of @ticket's burst (struct gcl_trans per packet, as gcl_classify_ex writes
+ * them), copied to @out once the burst is complete: after gcl_rxloop_wait
+ * and before the slot's next submit, or between gcl_rxloop_peek and
+ * _release.  -EINVAL (no transport hashes), -EAGAIN (not complete yet),
+ * -ESTALE (the slot was reused). */
+int gcl_rxloop_trans(struct gcl_rxloop *loop, int64_t ticket, struct gcl_trans *out);
 int gcl_rxloop_stop(struct gcl_rxloop *loop);
 int gcl_rxloop_drive(struct gcl_rxloop *loop, uint32_t n, const uint64_t *offs, uint32_t iters,
                      uint32_t depth, uint64_t *lat_ns, uint64_t *elapsed_ns);

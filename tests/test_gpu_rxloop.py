@@ -300,8 +300,65 @@ def test_rxloop_lifetime_and_errors(g):
             clf.rxloop(frames, flags=g.LOOP_INLINE_HDRS | g.LOOP_HDR_RECORDS)
         with pytest.raises(OSError):  # unknown flag
             clf.rxloop(frames, flags=0x4)
-        clf2 = g.Classifier(0, 16, 1, g.CFG_TRANS_HASH)
-        with pytest.raises(OSError):
-            clf2.rxloop(frames)
+        lp2 = clf.rxloop(frames, slots=4)
+        tk = lp2.submit(offs)
+        lp2.wait(tk, 4)
+        with pytest.raises(OSError):  # no transport hashes in this context
+            lp2.trans(tk, 4)
+        lp2.stop()
     finally:
         g.host_unregister(frames)
+
+
+@pytest.mark.parametrize("mode,vb,lflag", [(1, 8, 0), (0, 4, 0), (2, 8, 2), (1, 4, 2)])
+def test_rxloop_transport_hashes(g, orc, mode, vb, lflag, monkeypatch):
+    """GCL_CFG_TRANS_HASH through the loop: each delivered IPv4 TCP/UDP
+    packet's trans_hash_5tuple / _3tuple with its runtime's seed
+    (runtime/net/transport.c:29-42, as gcl_classify_ex computes them) come
+    back beside the verdicts (gcl_rxloop_trans), equal to the oracle's, with
+    the offsets or header records taken with the poll half the time."""
+    rng = np.random.default_rng(7500 + 10 * mode + vb + lflag)
+    max_rt = 64
+    rts = random_runtimes(rng, max_rt, 40)
+    n = 2500
+    frames, flen, offs, olf, rss, fdir, hint = fuzz_batch(rng, n, rts, max_rt)
+    key = bytes(rng.integers(0, 256, size=40, dtype=np.uint8))
+    cflags = g.CFG_TRANS_HASH | (g.CFG_VERDICT4 if vb == 4 else 0)
+    t = orc.Tables(max_rt, mode, cflags, 0x09, key)
+    apply_runtimes(t, rts)
+    clf = g.Classifier(0, max_rt, mode, cflags, 0x09, key)
+    apply_runtimes(clf, rts)
+    for r in rts:
+        seed = int(rng.integers(0, 2**32))
+        t.set_trans_seed(r["uniqid"], seed)
+        clf.set_trans_seed(r["uniqid"], seed)
+    ve, _, _, te = t.classify(frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir_hi=fdir,
+                              frames_len=flen, dst_hint=hint, trans=True)
+    assert (te["h5"] != 0).sum() > n // 10
+    g.host_register(frames)
+    if lflag == 2:
+        monkeypatch.setenv("GCL_TUNE_LOOP_SPEC", "500000")
+    loop = clf.rxloop(frames, slots=8, region_len=flen, flags=LOOP_FLAGS[lflag](g))
+    try:
+        got, gt = [], []
+        for k, (a, b) in enumerate(bursts(n)):
+            tk = loop.submit(offs[a:b], olf[a:b], rss[a:b], fdir[a:b], hint[a:b])
+            assert tk > 0
+            if k % 2:
+                rec = loop.peek(tk)
+                gt.append(loop.trans(tk, b - a))
+                v = rec["verdict"].copy()
+                got.append(((v.astype(np.uint64) << np.uint64(32)) | rec["hash"].astype(np.uint64))
+                           .view(g.VERDICT_DTYPE) if vb == 8 else v.view(g.VERDICT4_DTYPE))
+                loop.release(tk)
+            else:
+                got.append(loop.wait(tk, b - a))
+                gt.append(loop.trans(tk, b - a))
+        got, gt = np.concatenate(got), np.concatenate(gt)
+    finally:
+        loop.stop()
+        g.host_unregister(frames)
+    w = want(ve, tc_map(rts, max_rt), vb)
+    assert (got == w).all()
+    bad = np.nonzero(gt != te)[0]
+    assert not len(bad), f"{len(bad)} transport hashes differ, first {bad[0]}: {gt[bad[0]]} vs {te[bad[0]]}"
