@@ -56,12 +56,63 @@ static inline uint64_t ticks()
 	return __builtin_ia32_rdtsc();
 }
 
+/* Idle jiffies of every CPU from /proc/stat (index = CPU), empty on error. */
+static std::vector<uint64_t> cpu_idle()
+{
+	std::vector<uint64_t> idle;
+	FILE *f = fopen("/proc/stat", "r");
+	if (!f)
+		return idle;
+	char line[512];
+	while (fgets(line, sizeof(line), f)) {
+		int cpu;
+		unsigned long long v[8] = {0};
+		if (strncmp(line, "cpu", 3) || !isdigit((unsigned char)line[3]))
+			continue;
+		if (sscanf(line, "cpu%d %llu %llu %llu %llu %llu %llu %llu %llu", &cpu, &v[0], &v[1], &v[2],
+		           &v[3], &v[4], &v[5], &v[6], &v[7]) < 5 || cpu < 0 || cpu >= CPU_SETSIZE)
+			continue;
+		if ((size_t)cpu >= idle.size())
+			idle.resize(cpu + 1, 0);
+		idle[cpu] = v[3] + v[4]; /* idle + iowait */
+	}
+	fclose(f);
+	return idle;
+}
+
+/* The SMT siblings of @cpu (sysfs thread_siblings_list), @cpu included. */
+static std::vector<int> siblings(int cpu)
+{
+	std::vector<int> out;
+	char path[128];
+	snprintf(path, sizeof(path), "/sys/devices/system/cpu/cpu%d/topology/thread_siblings_list", cpu);
+	FILE *f = fopen(path, "r");
+	if (f) {
+		int lo, hi;
+		char sep;
+		while (fscanf(f, "%d", &lo) == 1) {
+			hi = lo;
+			if (fscanf(f, "%c", &sep) == 1 && sep == '-' && fscanf(f, "%d", &hi) == 1)
+				(void)fscanf(f, "%c", &sep);
+			for (int c = lo; c <= hi; c++)
+				out.push_back(c);
+		}
+		fclose(f);
+	}
+	if (out.empty())
+		out.push_back(cpu);
+	return out;
+}
+
 /* Pin this thread to one CPU, as the iokernel pins its dataplane lcore
- * (iokernel/dpdk.c:276-280): the LAST CPU of our affinity mask that is local
- * to GPU @dev's PCIe node (sysfs local_cpulist), else the last one of the
- * mask -- away from CPU 0, where housekeeping and interrupts tend to land.
- * RXPIPE_PIN=0 in the environment leaves the thread unpinned.  Returns the
- * CPU, or -1. */
+ * (iokernel/dpdk.c:276-280): among the CPUs of our affinity mask local to
+ * GPU @dev's PCIe node (sysfs local_cpulist; else the whole mask), the one
+ * whose physical core was idlest over 100 ms -- the CPU and its SMT
+ * siblings, from /proc/stat -- highest number first on a tie, away from
+ * CPU 0's housekeeping.  On a host shared with other jobs a fixed pick (the
+ * last local CPU, before) could land on a busy core and swing the rate 3x
+ * from run to run.  RXPIPE_PIN=0 in the environment leaves the thread
+ * unpinned.  Returns the CPU, or -1. */
 static int pin_near_gpu(int dev)
 {
 	const char *env = getenv("RXPIPE_PIN");
@@ -70,7 +121,7 @@ static int pin_near_gpu(int dev)
 	cpu_set_t allowed;
 	if (sched_getaffinity(0, sizeof(allowed), &allowed))
 		return -1;
-	int pick = -1;
+	std::vector<int> cand;
 	char bus[64] = {0}, path[160];
 	if (hipDeviceGetPCIBusId(bus, sizeof(bus), dev) == hipSuccess) {
 		for (char *c = bus; *c; c++)
@@ -86,16 +137,35 @@ static int pin_near_gpu(int dev)
 					(void)fscanf(f, "%c", &sep);
 				for (int cpu = lo; cpu <= hi; cpu++)
 					if (cpu < CPU_SETSIZE && CPU_ISSET(cpu, &allowed))
-						pick = cpu;
+						cand.push_back(cpu);
 			}
 			fclose(f);
 		}
 	}
-	for (int cpu = CPU_SETSIZE - 1; cpu >= 0 && pick < 0; cpu--)
-		if (CPU_ISSET(cpu, &allowed))
-			pick = cpu;
-	if (pick < 0)
+	if (cand.empty())
+		for (int cpu = 0; cpu < CPU_SETSIZE; cpu++)
+			if (CPU_ISSET(cpu, &allowed))
+				cand.push_back(cpu);
+	if (cand.empty())
 		return -1;
+	int pick = cand.back();
+	const std::vector<uint64_t> a = cpu_idle();
+	struct timespec ts = {0, 100 * 1000 * 1000};
+	nanosleep(&ts, nullptr);
+	const std::vector<uint64_t> b = cpu_idle();
+	if (!a.empty() && a.size() == b.size()) {
+		int64_t best = -1;
+		for (int cpu : cand) {
+			int64_t score = 0;
+			for (int sib : siblings(cpu))
+				if ((size_t)sib < a.size())
+					score += (int64_t)(b[sib] - a[sib]);
+			if (score >= best) {
+				best = score;
+				pick = cpu;
+			}
+		}
+	}
 	cpu_set_t one;
 	CPU_ZERO(&one);
 	CPU_SET(pick, &one);
