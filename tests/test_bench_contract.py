@@ -105,3 +105,24 @@ def test_frames_len_bounded_by_buffer():
         g._frames_len(buf, 4097)
     with pytest.raises(ValueError):
         g._frames_len(buf, -1)
+
+
+def test_rxpipe_rows_report_the_median_run(bench, monkeypatch):
+    """Each e2e.rx_burst_pipeline row runs tools/rxpipe in three fresh
+    processes and reports the median one, with all three rates."""
+    import subprocess
+    rates = iter([30.0, 10.0, 20.0] * 20)
+    calls = []
+
+    def fake_run(cmd, **kw):
+        calls.append(cmd)
+        line = json.dumps({"burst": int(cmd[1]), "workers": int(cmd[2]), "mpps_one_core": next(rates)})
+        return types.SimpleNamespace(returncode=0, stdout=line + "\n", stderr="")
+
+    monkeypatch.setattr(subprocess, "run", fake_run)
+    monkeypatch.setattr(os, "access", lambda p, m: True)
+    out = bench.rxpipe_bench()
+    rows = out["runs"]
+    assert out["reps_per_row"] == 3 and len(calls) == 3 * len(rows) and len(rows) >= 10
+    for r in rows:
+        assert r["mpps_one_core"] == 20.0 and r["mpps_samples"] == [10.0, 20.0, 30.0]
