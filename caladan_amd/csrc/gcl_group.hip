@@ -19,6 +19,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
+#include <unistd.h>
 
 #include <new>
 
@@ -92,7 +94,76 @@ struct gcl_group {
 	uint64_t *host_gath; /* pinned u64[kSlots][n * L]: GPU 0's gathered vectors */
 	uint64_t seq;        /* exchanges enqueued */
 	int last;            /* slot of the last exchange, -1 = none */
+	uint32_t timeout_ms; /* bound on RCCL init and on a non-blocking call's completion */
+	bool diverged;       /* a table change reached some replicas only: every
+	                        later call fails with -EIO (the GPUs would steer
+	                        with different tables) */
 };
+
+static uint64_t mono_ms()
+{
+	struct timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return (uint64_t)ts.tv_sec * 1000ull + (uint64_t)ts.tv_nsec / 1000000ull;
+}
+
+/* Non-blocking communicators: every RCCL call returns at once, possibly with
+ * ncclInProgress, and the state is polled here until each communicator is
+ * ready, has failed, or @deadline (CLOCK_MONOTONIC ms) passes.  0, -EIO
+ * (an RCCL error) or -ETIMEDOUT. */
+static int comms_wait(gcl_group *g, uint64_t deadline)
+{
+	for (;;) {
+		bool busy = false;
+		for (int i = 0; i < g->n; i++) {
+			ncclResult_t st = ncclSuccess;
+			if (ncclCommGetAsyncError(g->d[i].comm, &st) != ncclSuccess)
+				return -EIO;
+			if (st == ncclInProgress)
+				busy = true;
+			else if (st != ncclSuccess)
+				return -EIO;
+		}
+		if (!busy)
+			return 0;
+		if (mono_ms() >= deadline)
+			return -ETIMEDOUT;
+		usleep(100);
+	}
+}
+
+/* One communicator rank per GPU, initialised together from this thread as
+ * ncclCommInitAll does, but non-blocking so that a C caller gets -ETIMEDOUT
+ * after g->timeout_ms instead of blocking in RCCL's bootstrap; the partial
+ * communicators are aborted then. */
+static int comms_init(gcl_group *g, const int *devs)
+{
+	ncclUniqueId id;
+	if (ncclGetUniqueId(&id) != ncclSuccess)
+		return -EIO;
+	ncclConfig_t conf = NCCL_CONFIG_INITIALIZER;
+	conf.blocking = 0;
+	const uint64_t deadline = mono_ms() + g->timeout_ms;
+	bool ok = ncclGroupStart() == ncclSuccess;
+	for (int i = 0; i < g->n && ok; i++) {
+		ok = hipSetDevice(devs[i]) == hipSuccess;
+		const ncclResult_t r = ok ? ncclCommInitRankConfig(&g->d[i].comm, g->n, id, i, &conf)
+		                          : ncclInternalError;
+		ok = r == ncclSuccess || r == ncclInProgress;
+	}
+	const ncclResult_t e = ncclGroupEnd();
+	ok = ok && (e == ncclSuccess || e == ncclInProgress);
+	int ret = ok ? comms_wait(g, deadline) : -EIO;
+	if (ret) {
+		for (int i = 0; i < g->n; i++)
+			if (g->d[i].comm) {
+				(void)hipSetDevice(g->d[i].dev);
+				(void)ncclCommAbort(g->d[i].comm);
+				g->d[i].comm = nullptr;
+			}
+	}
+	return ret;
+}
 
 extern "C" uint64_t gcl_shard_count(uint64_t n, uint32_t world, uint32_t rank, uint64_t block)
 {
@@ -236,12 +307,9 @@ extern "C" int gcl_group_open(int ndev, const int *devs, const struct gcl_cfg *c
 			ret = -ENOMEM;
 	}
 	if (!ret && xchg == GCL_XCHG_RCCL) {
-		ncclComm_t comms[GCL_GROUP_MAX_DEV] = {};
-		if (ncclCommInitAll(comms, ndev, devs) != ncclSuccess)
-			ret = -EIO;
-		else
-			for (int i = 0; i < ndev; i++)
-				g->d[i].comm = comms[i];
+		g->timeout_ms = gcfg && gcfg->init_timeout_ms ? gcfg->init_timeout_ms
+		                                               : GCL_GROUP_INIT_TIMEOUT_MS;
+		ret = comms_init(g, devs);
 	}
 	if (ret) {
 		gcl_group_close(g);
@@ -263,45 +331,47 @@ extern "C" void *gcl_group_stream(struct gcl_group *g, int i)
 	return g && i >= 0 && i < g->n ? (void *)g->d[i].st[0] : nullptr;
 }
 
+/* A table change is checked by context 0 first: every context has the same
+ * cfg and the same tables, so a refusal there (-EINVAL, -EEXIST, -ENOENT)
+ * leaves all replicas untouched.  The replicas' setters only edit a host
+ * mirror and cannot fail differently; if one ever did, the group is marked
+ * diverged and refuses all further work rather than classify with tables
+ * that differ between GPUs. */
+template <typename F>
+static int fan_out(struct gcl_group *g, F f)
+{
+	if (!g)
+		return -EINVAL;
+	if (g->diverged)
+		return -EIO;
+	const int r0 = f(g->d[0].ctx);
+	if (r0)
+		return r0;
+	for (int i = 1; i < g->n; i++)
+		if (f(g->d[i].ctx)) {
+			g->diverged = true;
+			return -EIO;
+		}
+	return 0;
+}
+
 extern "C" int gcl_group_runtime_set(struct gcl_group *g, uint16_t uniqid, uint32_t ip_host,
                                      uint16_t thread_count, uint16_t active_count,
                                      const uint16_t *flow_tbl)
 {
-	if (!g)
-		return -EINVAL;
-	const int r0 = gcl_runtime_set(g->d[0].ctx, uniqid, ip_host, thread_count, active_count, flow_tbl);
-	if (r0)
-		return r0;
-	for (int i = 1; i < g->n; i++)
-		if (gcl_runtime_set(g->d[i].ctx, uniqid, ip_host, thread_count, active_count, flow_tbl))
-			return -EIO; /* replicas hold the same tables: cannot differ */
-	return 0;
+	return fan_out(g, [&](gcl_ctx *c) {
+		return gcl_runtime_set(c, uniqid, ip_host, thread_count, active_count, flow_tbl);
+	});
 }
 
 extern "C" int gcl_group_runtime_del(struct gcl_group *g, uint16_t uniqid)
 {
-	if (!g)
-		return -EINVAL;
-	const int r0 = gcl_runtime_del(g->d[0].ctx, uniqid);
-	if (r0)
-		return r0;
-	for (int i = 1; i < g->n; i++)
-		if (gcl_runtime_del(g->d[i].ctx, uniqid))
-			return -EIO;
-	return 0;
+	return fan_out(g, [&](gcl_ctx *c) { return gcl_runtime_del(c, uniqid); });
 }
 
 extern "C" int gcl_group_runtime_set_trans_seed(struct gcl_group *g, uint16_t uniqid, uint32_t seed)
 {
-	if (!g)
-		return -EINVAL;
-	const int r0 = gcl_runtime_set_trans_seed(g->d[0].ctx, uniqid, seed);
-	if (r0)
-		return r0;
-	for (int i = 1; i < g->n; i++)
-		if (gcl_runtime_set_trans_seed(g->d[i].ctx, uniqid, seed))
-			return -EIO;
-	return 0;
+	return fan_out(g, [&](gcl_ctx *c) { return gcl_runtime_set_trans_seed(c, uniqid, seed); });
 }
 
 extern "C" int gcl_group_classify(struct gcl_group *g, const struct gcl_batch *shards,
@@ -309,6 +379,8 @@ extern "C" int gcl_group_classify(struct gcl_group *g, const struct gcl_batch *s
 {
 	if (!g || !shards || !verdicts)
 		return -EINVAL;
+	if (g->diverged)
+		return -EIO;
 	for (int i = 0; i < g->n; i++) {
 		gcl_group::Dev &D = g->d[i];
 		const int r = gcl_classify(D.ctx, &shards[i], verdicts[i], D.acc, D.acc + g->R, D.st[0]);
@@ -396,6 +468,8 @@ extern "C" int gcl_group_classify_host(struct gcl_group *g, const struct gcl_bat
 	if (!g || !hb || !host_verdicts || !o || o->mode > GCL_E2E_ZEROCOPY ||
 	    o->nstreams > GCL_GROUP_MAX_STREAMS)
 		return -EINVAL;
+	if (g->diverged)
+		return -EIO;
 	if (hb->n == 0)
 		return 0;
 	if (!hb->frames || (!hb->offs && (hb->stride < 16 || (hb->stride & 15))))
@@ -522,12 +596,21 @@ extern "C" int gcl_group_exchange(struct gcl_group *g)
 		bool ok = ncclGroupStart() == ncclSuccess;
 		for (int i = 0; i < g->n && ok; i++) {
 			gcl_group::Dev &D = g->d[i];
-			ok = ncclAllGather(D.snap + b * L, D.gath + b * L * g->n, L, ncclUint64, D.comm,
-			                   D.xs) == ncclSuccess;
+			const ncclResult_t r = ncclAllGather(D.snap + b * L, D.gath + b * L * g->n, L,
+			                                     ncclUint64, D.comm, D.xs);
+			ok = r == ncclSuccess || r == ncclInProgress;
 		}
-		ok = ncclGroupEnd() == ncclSuccess && ok;
+		const ncclResult_t e = ncclGroupEnd();
+		ok = ok && (e == ncclSuccess || e == ncclInProgress);
 		if (!ok)
 			return -EIO;
+		/* non-blocking communicators: the enqueue itself may still be in
+		 * progress (the first all-gather connects the ring) */
+		if (e == ncclInProgress) {
+			const int w = comms_wait(g, mono_ms() + g->timeout_ms);
+			if (w)
+				return w;
+		}
 		for (int i = 0; i < g->n; i++) {
 			gcl_group::Dev &D = g->d[i];
 			he(hipSetDevice(D.dev));

@@ -200,17 +200,19 @@ uint64_t gcl_rx_make_cmd(uint16_t pkt_len, uint8_t olflags)
 	return 0 /* RX_NET_RECV */ | (uint64_t)pkt_len << 16 | csum << 48;
 }
 
-/* rx_send_to_runtime (rx.c:50-73).  @gpu_thread >= 0 is the GPU's thread
- * (DELIVER); otherwise the flow_tbl slot is @slot when >= 0 (a compact WAKE
- * verdict), else hash % thread_count. */
-static bool send_to_runtime(struct gcl_host_proc *p, uint32_t hash, int slot, int gpu_thread,
+/* rx_send_to_runtime (rx.c:50-73) for the flow_tbl slot @slot of runtime @p
+ * (hash % thread_count: every DELIVER or WAKE verdict carries it), or, when
+ * @slot < 0, the slot of @hash.  The flow_tbl and the active count are read
+ * here, at delivery time, like rx.c:55-72: a sched_add_core earlier in the
+ * same batch that re-steered @p (or took its last core) is seen. */
+static bool send_to_runtime(struct gcl_host_proc *p, uint32_t hash, int slot,
                             uint64_t cmd, unsigned long payload,
                             const struct gcl_host_ops *ops)
 {
 	int th;
 
-	/* verdicts come from device memory: a thread or flow_tbl slot outside
-	 * the runtime's thread_count (a stale or corrupted verdict) is refused
+	/* verdicts come from device memory: a flow_tbl slot outside the
+	 * runtime's thread_count (a stale or corrupted verdict) is refused
 	 * like a full ring, never used as an index */
 	if (p->thread_count == 0 || p->thread_count > GCL_NCPU)
 		return false;
@@ -218,9 +220,7 @@ static bool send_to_runtime(struct gcl_host_proc *p, uint32_t hash, int slot, in
 		slot = (int)(hash % p->thread_count);
 	else if (slot >= p->thread_count)
 		return false;
-	if (gpu_thread >= 0) {
-		th = gpu_thread;
-	} else if (p->active_thread_count > 0) {
+	if (p->active_thread_count > 0) {
 		th = p->flow_tbl[slot];
 	} else {
 		if (ops && ops->sched_add_core)
@@ -264,10 +264,7 @@ static uint64_t deliver(struct gcl_host_proc *const *clients_by_id, uint32_t max
 		if (act == GCL_ACT_DELIVER || act == GCL_ACT_WAKE) {
 			if (uniqid < max_runtimes)
 				p = clients_by_id[uniqid];
-			ok = p && send_to_runtime(p, hash,
-			                          act == GCL_ACT_WAKE && v4 ? (int)thread : -1,
-			                          act == GCL_ACT_DELIVER ? (int)thread : -1,
-			                          cmd, payload, ops);
+			ok = p && send_to_runtime(p, hash, (int)thread, cmd, payload, ops);
 			if (ok) {
 				delivered++;
 				if (ops && ops->owned)
@@ -278,7 +275,7 @@ static uint64_t deliver(struct gcl_host_proc *const *clients_by_id, uint32_t max
 		} else if (act == GCL_ACT_BROADCAST) {
 			int n_sent = 0;
 			for (int c = 0; c < nr_clients; c++) {
-				if (send_to_runtime(clients[c], hash, -1, -1, cmd, payload, ops)) {
+				if (send_to_runtime(clients[c], hash, -1, cmd, payload, ops)) {
 					n_sent++;
 					if (ops && ops->owned)
 						ops->owned(ops->arg, clients[c], base + i);
@@ -342,14 +339,14 @@ struct gcl_verdict4 gcl_verdict2_to4(uint16_t v, uint8_t thread_bits)
 }
 
 /* deliver() for compact verdicts, with the common case inlined: a DELIVER
- * verdict names the kthread, so the packet goes straight into that ring
- * (rx.c:56-58 with active threads, then :76-92) with the two per-delivery
- * callbacks of the reference, thread_enable_sched_poll and the ownership
- * record.  Everything else (WAKE, broadcast, drops, a full ring) takes
- * deliver() for that one packet, in order, so the outcome is the same packet
- * by packet.  2.1 ns/pkt against 3.1 for deliver() alone on the bench host
- * (EPYC 9575F, 16 x 8 rings, no callbacks, profiles/r01_deliver.txt); a
- * write prefetch of the ring slot 8-32 packets ahead made it slower.
+ * verdict for a runtime that still has an active kthread goes straight into
+ * the ring of flow_tbl[slot] as it stands now (rx.c:55-59, then :76-92),
+ * with the two per-delivery callbacks of the reference,
+ * thread_enable_sched_poll and the ownership record.  Everything else (WAKE,
+ * a runtime whose last core a scheduler side effect of this batch took,
+ * broadcast, drops, a full ring) takes deliver() for that one packet, in
+ * order, so the outcome is the same packet by packet.  A write prefetch of
+ * the ring slot 8-32 packets ahead made it slower (profiles/r01_deliver.txt).
  * Verdicts are @v2 (2-byte, of a context with @thread_bits) or @v4; always
  * inlined with a constant @v2 == NULL or not. */
 static inline __attribute__((always_inline)) uint64_t
@@ -370,7 +367,7 @@ deliver_compact(struct gcl_host_proc *const *clients_by_id, uint32_t max_runtime
 	for (uint64_t i = 0; i < n; i++) {
 		struct gcl_host_proc *p;
 		struct gcl_lrpc_chan_out *chan;
-		uint32_t uniqid, thread;
+		uint32_t uniqid, slot, th;
 		bool fast;
 
 		/* verdict i sits @vstride bytes after verdict i - 1: packed
@@ -381,16 +378,17 @@ deliver_compact(struct gcl_host_proc *const *clients_by_id, uint32_t max_runtime
 		if (v2) {
 			const uint16_t x = *v2i;
 			uniqid = (x & GCL_V2_Q_MASK) >> thread_bits;
-			thread = x & tmask;
+			slot = x & tmask;
 			fast = (x & GCL_V2_KIND) == GCL_V2_DELIVER;
 		} else {
 			const struct gcl_verdict4 x = *v4i;
 			uniqid = x.uniqid;
-			thread = x.thread;
+			slot = x.thread;
 			fast = (x.action & GCL_ACT_MASK) == GCL_ACT_DELIVER;
 		}
 		if (!fast || uniqid >= max_runtimes || !(p = clients_by_id[uniqid]) ||
-		    thread >= p->thread_count || !(chan = p->rxq[thread]) ||
+		    slot >= p->thread_count || p->active_thread_count == 0 ||
+		    (th = p->flow_tbl[slot]) >= p->thread_count || !(chan = p->rxq[th]) ||
 		    chan->send_head - chan->send_tail >= chan->size) {
 			const struct gcl_verdict4 w = v2 ? gcl_verdict2_to4(*v2i, thread_bits) : *v4i;
 			delivered += deliver(clients_by_id, max_runtimes, clients, nr_clients, NULL, &w,
@@ -400,7 +398,7 @@ deliver_compact(struct gcl_host_proc *const *clients_by_id, uint32_t max_runtime
 			continue;
 		}
 		if (enable_poll)
-			enable_poll(ops->arg, p, thread);
+			enable_poll(ops->arg, p, th);
 		const uint64_t csum = olflags ?
 			(olflags[i] & GCL_F_IP_CKSUM_MASK) == GCL_F_IP_CKSUM_GOOD : csum_def;
 		const uint32_t h = chan->send_head++;

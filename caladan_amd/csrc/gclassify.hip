@@ -150,11 +150,20 @@ __device__ __forceinline__ uint8_t fbyte(const KParams &k, uint64_t a)
 	return SYS ? gcl::byte_sys(k.frames, k.frames_len, a) : frame_byte(k, a);
 }
 
+/* A caller's frame offset, clamped to frames_len: every offset at or past it
+ * reads as a frame of zeros either way, and the clamp keeps a live packet
+ * clear of the kNoOff sentinel (~0) the kernels use for "no packet"
+ * (gcl_classify_ex refuses frames_len == ~0). */
+__device__ __forceinline__ uint64_t user_off(const KParams &k, uint64_t o)
+{
+	return o < k.frames_len ? o : k.frames_len;
+}
+
 template <bool GENERAL>
 __device__ __forceinline__ uint64_t frame_off(const KParams &k, uint64_t idx)
 {
 	if (GENERAL && k.offs)
-		return k.offs[idx];
+		return user_off(k, k.offs[idx]);
 	return idx * k.stride;
 }
 
@@ -548,7 +557,11 @@ __device__ __forceinline__ uint64_t classify_core(const KParams &k, const HdrWor
 	       : arp_respond ? GCL_ACT_ARP_RESPOND
 	       : unreg ? GCL_ACT_DROP_UNREG : action;
 
-	/* rx_send_to_runtime, rx.c:55-72: flow_tbl[hash % thread_count] */
+	/* rx_send_to_runtime, rx.c:55-72: the flow_tbl slot hash % thread_count.
+	 * The slot, not flow_tbl[slot], is the verdict: the host post-pass reads
+	 * the live flow_tbl and active count at delivery time, as rx.c does, so
+	 * a scheduler side effect earlier in the same batch (a wake that takes a
+	 * core from another runtime, sched.c:208-216) steers the later packets */
 	uint32_t uniq = GCL_NO_RUNTIME, thr = GCL_NO_THREAD;
 	if (p >= 0) {
 		const RtEntry re = tb.rtab[p];
@@ -557,14 +570,9 @@ __device__ __forceinline__ uint64_t classify_core(const KParams &k, const HdrWor
 			thr = hash & 7;
 		} else {
 			const uint64_t M = (uint64_t)re.m_hi << 32 | re.m_lo;
-			const uint32_t slot = gcl::fastmod(hash, M, re.tc);
-			if (re.active) {
-				thr = tb.flow[re.flow_off + slot];
-			} else {
+			thr = gcl::fastmod(hash, M, re.tc);
+			if (!re.active)
 				action |= GCL_ACT_WAKE;
-				if (k.cflags & (GCL_CFG_VERDICT4 | GCL_CFG_VERDICT2))
-					thr = slot; /* the host replays flow_tbl[slot] */
-			}
 		}
 		if (!(ablate & 4))
 			atomicAdd(&hist[p], 1u);
@@ -844,7 +852,7 @@ classify_kernel(KParams k)
 	const uint64_t *offs_src = k.offs ? k.offs : (const uint64_t *)k.tables;
 	auto my_ok = [&](uint64_t tt) { return tt < t_end && tt * NT + tid < k.n; };
 	auto my_off = [&](uint64_t tt) -> uint64_t {
-		return offs_src[k.offs && my_ok(tt) ? tt * NT + tid : 0];
+		return user_off(k, offs_src[k.offs && my_ok(tt) ? tt * NT + tid : 0]);
 	};
 	auto pref = [&](uint64_t tt, uint32_t pr[2]) {
 		if constexpr (goffs) {
@@ -1083,7 +1091,7 @@ classify_pair_kernel(KParams k)
 	const uint64_t *offs_src = k.offs ? k.offs : (const uint64_t *)k.tables;
 	auto ok = [&](uint64_t tt) { return tt < k.ntiles && tt * NT + tid < k.n; };
 	auto ld_off = [&](uint64_t tt) -> uint64_t {
-		return offs_src[k.offs && ok(tt) ? tt * NT + tid : 0];
+		return user_off(k, offs_src[k.offs && ok(tt) ? tt * NT + tid : 0]);
 	};
 	auto src_of = [&](uint64_t tt, uint64_t raw) -> uint64_t {
 		return pair_src(k, !ok(tt) ? kNoOff : k.offs ? raw : (tt * NT + tid) * k.stride);
@@ -1220,9 +1228,12 @@ constexpr uint64_t kLoopSpecTicks = 400;
  * read after it; or after the word, the speculative window over or the
  * burst too long for it */
 enum { kLoopPollEarly = 0, kLoopPollStale = 1, kLoopPollLate = 2 };
+/* never 0 (the use count runs 1 .. 2^24 - 1 and round again), so an entry
+ * that was never loaded, or never written since the loop started, cannot pass
+ * for a current one; host and device compute it the same way */
 __host__ __device__ constexpr uint64_t loop_stamp(uint64_t t, uint32_t nslots)
 {
-	return (((t - 1) / nslots + 1) & 0xFFFFFF) << kLoopStampShift;
+	return (((t - 1) / nslots) % 0xFFFFFFull + 1) << kLoopStampShift;
 }
 
 struct LoopImgHdr {        /* first 64 B of a table image buffer */
@@ -1257,6 +1268,8 @@ struct LoopParams {
 	uint32_t hdr_rec;          /* off_hdr holds header records (GCL_LOOP_HDR_RECORDS) */
 	uint32_t spec_ticks;       /* how long a wait polls them (s_memrealtime ticks) */
 	uint32_t off_trans;        /* GCL_CFG_TRANS_HASH: 16-B {h5, h3, ticket} per packet; else 0 */
+	uint64_t t0;               /* tickets start after t0 (0; GCL_TUNE_LOOP_T0 tests the
+	                              stamps' wrap), a multiple of nslots */
 };
 
 /* GCL_LOOP_HDR_RECORDS: the submitting core writes each packet as one 64-B
@@ -1273,7 +1286,7 @@ struct LoopParams {
  * frame at the record's offset. */
 __host__ __device__ constexpr uint32_t loop_rec_stamp(uint64_t t, uint32_t nslots)
 {
-	return (uint32_t)((t - 1) / nslots + 1);
+	return (uint32_t)(((t - 1) / nslots) % 0xFFFFFFFFull + 1); /* never 0, as loop_stamp */
 }
 
 /* a record's four chunks -> the packet's tile row and side-array entries */
@@ -1358,7 +1371,7 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 	uint32_t cur_seq = 0xFF; /* no image yet (versions are taken mod 64) */
 	uint32_t polls[3] = {0, 0, 0};
 
-	for (uint64_t t = blockIdx.x + 1;; t += L.workers) {
+	for (uint64_t t = L.t0 + blockIdx.x + 1;; t += L.workers) {
 		uint8_t *slot = L.slots + ((t - 1) % L.nslots) * L.slot_bytes;
 		LoopSlotHdr *h = (LoopSlotHdr *)slot;
 		const __amdgpu_buffer_rsrc_t srs = gcl::host_rsrc(slot, L.slot_bytes);
@@ -1417,7 +1430,10 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 				__builtin_amdgcn_s_sleep(1);
 			}
 			const uint32_t nw = (uint32_t)(w >> 11) & 0x1FFF;
-			const bool fresh = (uint32_t)tid >= nw || (rec ? rok : (e & ~kLoopOffMask) == stamp);
+			/* an entry counts only if it was loaded with the poll that found
+			 * the word (sp_hit): e is 0 otherwise */
+			const bool fresh = (uint32_t)tid >= nw ||
+			                   (rec ? rok : sp_hit && (e & ~kLoopOffMask) == stamp);
 			const bool early = spec && w && nw <= 64 && __all(fresh);
 			if (early && (uint32_t)tid < nw) {
 				const LoopSide s0 = side(0);
@@ -2105,8 +2121,7 @@ static uint32_t build_image(gcl_ctx *c)
 	if (!placed)
 		return 0; /* no seed placed every key: callers return -ENOSPC */
 	RtEntry *re = (RtEntry *)(img + c->off_rt);
-	uint8_t *flow = img + c->off_flow;
-	uint32_t fo = 0;
+	const uint32_t fo = 0;
 	for (uint32_t u = 0; u < max_rt; u++) {
 		const gcl_ctx::Rt &r = c->rt[u];
 		RtEntry e = {};
@@ -2116,9 +2131,9 @@ static uint32_t build_image(gcl_ctx *c)
 			e.m_hi = (uint32_t)(M >> 32);
 			e.tc = r.tc;
 			e.active = r.active;
-			e.flow_off = fo;
-			memcpy(flow + fo, r.flow, r.tc);
-			fo += r.tc;
+			/* no flow_tbl bytes: the device steers to a slot, the host
+			 * post-pass resolves it against the live flow_tbl */
+			e.flow_off = 0;
 		}
 		re[u] = e;
 	}
@@ -2461,6 +2476,9 @@ extern "C" int gcl_classify_ex(struct gcl_ctx *c, const struct gcl_batch *b,
 	if (b->n == 0)
 		return 0;
 	if (!b->frames || (!b->offs && (b->stride < 16 || (b->stride & 15) || b->stride > (1u << 20))))
+		return -EINVAL;
+	/* offsets are clamped to frames_len, which must stay clear of kNoOff */
+	if (b->frames_len == UINT64_MAX)
 		return -EINVAL;
 	/* at most 2^40 packets, so n * stride (and the fast-path range test on
 	 * it below) cannot wrap */
@@ -3132,7 +3150,8 @@ struct gcl_rxloop {
 	std::vector<uint64_t> retired; /* per slot: last ticket the host collected */
 	const uint8_t *region;         /* host view, for GCL_LOOP_INLINE_HDRS */
 	uint64_t region_len;
-	bool ended;
+	bool ended;              /* the kernel has finished (hipStreamQuery) */
+	bool left;               /* some worker has left: submit no more */
 };
 
 static uint64_t now_ns()
@@ -3154,15 +3173,17 @@ static bool loop_ended(gcl_rxloop *L)
 	return L->ended;
 }
 
-/* loop_ended without a HIP call: a worker that leaves raises ctl[1].  Per
- * burst on the submit path, where hipStreamQuery cost ~100 ns; a kernel that
- * died without raising it is still caught by loop_await's periodic
- * loop_ended. */
+/* The submit path's check, without a HIP call (hipStreamQuery cost ~100 ns
+ * per burst): a worker that leaves raises ctl[1], and no burst is published
+ * after that.  Bursts already published may still be classified by the
+ * other workers, so only loop_ended (the kernel finished) lets a wait give
+ * up with -ESHUTDOWN; a kernel that died without raising ctl[1] is caught by
+ * loop_await's periodic loop_ended. */
 static bool loop_left(gcl_rxloop *L)
 {
-	if (!L->ended && __atomic_load_n(&L->ctl[1], __ATOMIC_ACQUIRE))
-		L->ended = true;
-	return L->ended;
+	if (!L->left && (L->ended || __atomic_load_n(&L->ctl[1], __ATOMIC_ACQUIRE)))
+		L->left = true;
+	return L->left;
 }
 
 static const LoopRec *loop_recs(gcl_rxloop *L, LoopSlotHdr *h)
@@ -3262,7 +3283,14 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 	L->c = c;
 	L->region = (const uint8_t *)cfg->region;
 	L->region_len = cfg->region_len;
-	L->retired.assign(cfg->slots, 0);
+	{
+		uint64_t t0 = 0;
+		if (const char *e = getenv("GCL_TUNE_LOOP_T0")) /* tests: start near a stamp wrap */
+			t0 = strtoull(e, nullptr, 0) / cfg->slots * cfg->slots;
+		L->lp.t0 = t0;
+		L->next = t0;
+		L->retired.assign(cfg->slots, t0);
+	}
 	L->max_burst = cfg->max_burst;
 	L->vbytes = verdict_bytes(c);
 	const uint64_t mb = align16(cfg->max_burst);
@@ -3398,7 +3426,7 @@ static void loop_write_records(gcl_rxloop *L, uint64_t t, uint8_t *dst, uint32_t
 	}
 	/* records past n keep older stamps; rewrite them now and then so that
 	 * none is ever 2^32 uses stale (loop_stamp's rule for the offsets) */
-	if (S % kLoopRefresh == 0)
+	if (((t - 1) / L->lp.nslots) % kLoopRefresh == kLoopRefresh - 1)
 		for (uint32_t i = n; i < L->max_burst; i++, q += 4)
 			for (int j = 0; j < 4; j++)
 				q[j] = u32x4_h{S, 0, 0, 0};
@@ -3415,7 +3443,7 @@ static void loop_write_arrays(gcl_rxloop *L, uint64_t t, uint8_t *s, uint32_t n,
 		const uint64_t st = loop_stamp(t, L->lp.nslots);
 		for (uint32_t i = 0; i < n; i++) /* past the region either way: reads 0 */
 			so[i] = std::min<uint64_t>(offs[i], kLoopOffMask) | st;
-		if ((((t - 1) / L->lp.nslots + 1) % kLoopRefresh) == 0)
+		if ((((t - 1) / L->lp.nslots) % kLoopRefresh) == kLoopRefresh - 1)
 			for (uint32_t i = n; i < L->max_burst; i++)
 				so[i] = st;
 	}
@@ -3536,6 +3564,10 @@ extern "C" int gcl_rxloop_release(struct gcl_rxloop *L, int64_t ticket)
 	const uint64_t t = (uint64_t)ticket;
 	if (t + L->lp.nslots <= L->next)
 		return -ESTALE;
+	/* the GPU may still be writing an incomplete burst's slot: it is not
+	 * handed back for reuse until the burst is complete */
+	if (!burst_complete(L, t))
+		return -EAGAIN;
 	uint64_t &r = L->retired[(t - 1) % L->lp.nslots];
 	if (r < t)
 		r = t;

@@ -26,7 +26,7 @@ HASH_MODES = {"nic": HASH_NIC, "jenkins": HASH_JENKINS, "toeplitz": HASH_TOEPLIT
 
 CFG_AZURE_ARP, CFG_HASH16, CFG_PROFILE, CFG_TRANS_HASH, CFG_VERDICT4 = 0x1, 0x2, 0x4, 0x8, 0x10
 CFG_VERDICT2 = 0x20
-# GCL_CFG_VERDICT2: u16 q = uniqid << thread_bits | thread; kind in the top two bits
+# GCL_CFG_VERDICT2: u16 q = uniqid << thread_bits | flow_tbl slot; kind in the top two bits
 V2_Q_MASK, V2_KIND, V2_DELIVER, V2_WAKE, V2_OTHER, V2_QUEUES = 0x3FFF, 0xC000, 0, 0x4000, 0xC000, 0x4000
 PAIR_NEW_READS, PAIR_NEW_WRITES, PAIR_TRIES, PAIR_RUN = 0x1, 0x2, 24, 2
 
@@ -55,7 +55,8 @@ CALADAN_RSS_KEY = bytes([
     0x0D, 0x6D, 0x86, 0xBA, 0x61, 0x78, 0xEB])
 
 VERDICT_DTYPE = np.dtype([("hash", "<u4"), ("uniqid", "<u2"), ("thread", "u1"), ("action", "u1")])
-# GCL_CFG_VERDICT4: WAKE verdicts carry the flow_tbl slot (hash % thread_count) in `thread`
+# every DELIVER / WAKE verdict carries the flow_tbl slot (hash % thread_count) in `thread`:
+# the host post-pass reads flow_tbl[slot] at delivery time (rx.c:55-72)
 VERDICT4_DTYPE = np.dtype([("uniqid", "<u2"), ("thread", "u1"), ("action", "u1")])
 TRANS_DTYPE = np.dtype([("h5", "<u4"), ("h3", "<u4")])
 # struct gcl_loop_rec: one persistent-loop verdict record (gcl_rxloop_peek)
@@ -585,7 +586,8 @@ XCHG_RCCL, XCHG_HOST = 0, 1
 
 class GclGroupCfg(ctypes.Structure):
     _fields_ = [("block", ctypes.c_uint64), ("exchange", ctypes.c_uint32),
-                ("nstreams", ctypes.c_uint32)]
+                ("nstreams", ctypes.c_uint32), ("init_timeout_ms", ctypes.c_uint32),
+                ("pad", ctypes.c_uint32)]
 
 
 _glib = None
@@ -643,7 +645,8 @@ class Group:
 
     def __init__(self, devices, max_runtimes=16, hash_mode=HASH_JENKINS, flags=0,
                  default_olflags=F_RSS_HASH | F_IP_CKSUM_GOOD, rss_key=CALADAN_RSS_KEY,
-                 thread_bits=0, block=GROUP_BLOCK, exchange=XCHG_RCCL, nstreams=2):
+                 thread_bits=0, block=GROUP_BLOCK, exchange=XCHG_RCCL, nstreams=2,
+                 init_timeout_ms=0):
         gl = group_lib()
         if isinstance(hash_mode, str):
             hash_mode = HASH_MODES[hash_mode]
@@ -658,7 +661,8 @@ class Group:
         self.vbytes = verdict_bytes(flags)
         self.block = block
         devs = (ctypes.c_int * self.n)(*self.devices)
-        gc = GclGroupCfg(block=block, exchange=exchange, nstreams=nstreams)
+        gc = GclGroupCfg(block=block, exchange=exchange, nstreams=nstreams,
+                         init_timeout_ms=init_timeout_ms)
         self._g = ctypes.c_void_p()
         _check(gl.gcl_group_open(self.n, devs, ctypes.byref(cfg), ctypes.byref(gc), ctypes.byref(self._g)),
                "gcl_group_open")

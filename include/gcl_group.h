@@ -44,7 +44,11 @@ struct gcl_group_cfg {
 	uint64_t block;    /* packets per round-robin block, multiple of 256; 0 = GCL_GROUP_BLOCK */
 	uint32_t exchange; /* enum gcl_group_xchg */
 	uint32_t nstreams; /* work streams per GPU for gcl_group_classify_host, 1..4 (0 = 2) */
+	uint32_t init_timeout_ms; /* GCL_XCHG_RCCL: bound on communicator init, and on an
+	                             exchange's RCCL enqueue (0 = GCL_GROUP_INIT_TIMEOUT_MS) */
+	uint32_t pad;
 };
+#define GCL_GROUP_INIT_TIMEOUT_MS 60000
 
 struct gcl_group;
 
@@ -52,7 +56,11 @@ struct gcl_group;
  * gcl_group_open - one context per entry of @devs (HIP device ids, distinct
  * for GCL_XCHG_RCCL), all with @cfg, and the RCCL communicator over them.
  * @gcfg may be NULL (64 Ki blocks, RCCL, 2 streams).
- * Returns 0, -EINVAL, -ENODEV, -ENOMEM, or -EIO when RCCL init fails.
+ * The communicators are created non-blocking (ncclCommInitRankConfig with
+ * blocking = 0) and polled: a bootstrap that does not finish within
+ * init_timeout_ms is aborted and gives -ETIMEDOUT instead of blocking the
+ * caller.
+ * Returns 0, -EINVAL, -ENODEV, -ENOMEM, -ETIMEDOUT, or -EIO when RCCL init fails.
  */
 int gcl_group_open(int ndev, const int *devs, const struct gcl_cfg *cfg,
                    const struct gcl_group_cfg *gcfg, struct gcl_group **out);

@@ -106,7 +106,8 @@ struct gcl_cfg {
 /* One batch of received frames, resident in device memory. */
 struct gcl_batch {
 	const uint8_t  *frames;     /* frame bytes (mbuf data) */
-	uint64_t        frames_len; /* readable bytes at frames; reads past it see 0 */
+	uint64_t        frames_len; /* readable bytes at frames (< 2^64 - 1, else -EINVAL);
+	                               reads past it see 0, at any offset */
 	uint64_t        stride;     /* slot stride when offs == NULL (multiple of 16) */
 	const uint64_t *offs;       /* optional u64[n] frame start offsets, any alignment:
 	                               a 4-B-aligned frame (16-B aligned, or the

@@ -495,13 +495,13 @@ static void orc_rx_one_pkt(const struct orc_tables *t, const struct gcl_batch *b
 deliver:
 	v->uniqid = (uint16_t)p;
 	counts[p]++;
-	if (t->rt[p].active > 0) { /* rx.c:55-59 */
-		const struct orc_runtime *r = &t->rt[p];
-		v->thread = (uint8_t)r->flow_tbl[hash % r->thread_count];
+	/* rx_send_to_runtime's flow_tbl slot, hash % thread_count (rx.c:57, :68);
+	 * flow_tbl[slot] is read by the post-pass at delivery time */
+	v->thread = (uint8_t)(hash % t->rt[p].thread_count);
+	if (t->rt[p].active > 0) /* rx.c:55-59 */
 		v->action = (uint8_t)(GCL_ACT_DELIVER | fdir);
-	} else {
+	else
 		v->action = (uint8_t)(GCL_ACT_WAKE | fdir); /* rx.c:62-72 */
-	}
 	if (tr && (t->flags & GCL_CFG_TRANS_HASH) && orc_trans(t, &pv, p, tr))
 		v->action |= GCL_ACT_F_TRANS;
 }
@@ -618,22 +618,14 @@ static inline void rx_one_pkt_direct(const struct orc_tables *t, const struct gc
 	}
 	v->uniqid = (uint16_t)p;
 	counts[p]++;
-	if (t->rt[p].active > 0) { /* rx.c:55-59 */
-		v->thread = (uint8_t)t->rt[p].flow_tbl[hash % t->rt[p].thread_count];
-		v->action = GCL_ACT_DELIVER;
-	} else {
-		v->action = GCL_ACT_WAKE;
-	}
+	v->thread = (uint8_t)(hash % t->rt[p].thread_count); /* the flow_tbl slot */
+	v->action = t->rt[p].active > 0 ? GCL_ACT_DELIVER : GCL_ACT_WAKE; /* rx.c:55-72 */
 	return;
 deliver_fdir:
 	v->uniqid = (uint16_t)p;
 	counts[p]++;
-	if (t->rt[p].active > 0) {
-		v->thread = (uint8_t)t->rt[p].flow_tbl[hash % t->rt[p].thread_count];
-		v->action = GCL_ACT_DELIVER | GCL_ACT_F_FDIR;
-	} else {
-		v->action = GCL_ACT_WAKE | GCL_ACT_F_FDIR;
-	}
+	v->thread = (uint8_t)(hash % t->rt[p].thread_count);
+	v->action = (t->rt[p].active > 0 ? GCL_ACT_DELIVER : GCL_ACT_WAKE) | GCL_ACT_F_FDIR;
 }
 
 #define RX_PREFETCH_STRIDE 2 /* rx.c:22 */
@@ -765,7 +757,9 @@ static void classify_range_lrpc(const struct orc_tables *t, const struct gcl_bat
 				uint64_t csum = (fl & GCL_F_IP_CKSUM_MASK) == GCL_F_IP_CKSUM_GOOD;
 				uint64_t cmd = 0 | (len & 0xFFFF) << 16 | csum << 48;
 				uint64_t off = b->offs ? b->offs[k] : k * b->stride;
-				if (!lrpc_send(ring_of(rs, vk->uniqid, vk->thread), cmd, off)) {
+				/* rx_send_to_runtime: flow_tbl[slot] at send time (rx.c:57) */
+				const uint32_t th = t->rt[vk->uniqid].flow_tbl[vk->thread];
+				if (!lrpc_send(ring_of(rs, vk->uniqid, th), cmd, off)) {
 					stats[GCL_RX_UNICAST_FAIL]++;
 					stats[GCL_RX_UNHANDLED]++;
 				}

@@ -132,24 +132,33 @@ FLOW = {3: A_FLOW, 7: [0, 1, 2]}
 
 
 def steer(uniq, h):
-    """rx_send_to_runtime (rx.c:55-72): flow_tbl[hash % thread_count]."""
+    """rx_send_to_runtime (rx.c:55-72): the flow_tbl slot hash % thread_count
+    (the verdict's `thread`), and the kthread flow_tbl[slot] the post-pass
+    delivers to while the runtime has an active thread (None: wake path)."""
+    slot = h % TC[uniq]
     if uniq == 9:
-        return 0xFF, WAKE
-    return FLOW[uniq][h % TC[uniq]], DELIVER
+        return slot, None, WAKE
+    return slot, FLOW[uniq][slot], DELIVER
 
 
 def pkt(cite, frame, flags, rss, fdir, hash_, uniq, action, thread=None, hint=0, hint_hit=False,
         trans=None):
+    """`thread` given explicitly: a runtime with an identity flow_tbl, so the
+    slot is also the kthread."""
+    queue = None
     if uniq is None:
         uniq, thread = 0xFFFF, 0xFF
     elif thread is None:
-        thread, act = steer(uniq, hash_)
+        thread, queue, act = steer(uniq, hash_)
         action |= act
+    else:
+        queue = thread
     if trans is not None:
         action |= 0x40  # GCL_ACT_F_TRANS
     return {"cite": cite, "frame": frame.hex(), "olflags": flags, "rss": rss, "fdir_hi": fdir,
             "dst_hint": hint, "hint_hit": hint_hit, "expect_trans": list(trans or (0, 0)),
-            "expect": {"hash": hash_, "uniqid": uniq, "thread": thread, "action": action}}
+            "expect": {"hash": hash_, "uniqid": uniq, "thread": thread, "action": action},
+            "expect_kthread": queue}
 
 
 def nic_set():
@@ -457,7 +466,9 @@ def main():
         s["expect_stats"] = expected_stats(s)
         s["expect_counts"] = expected_counts(s)
     with open(os.path.join(HERE, "rx_scenarios.json"), "w") as f:
-        json.dump({"source": "hand-derived from iokernel/rx.c:116-233 (see make_golden.py)",
+        json.dump({"source": "hand-derived from iokernel/rx.c:116-233 (see make_golden.py); expect.thread is the "
+                           "flow_tbl slot hash % thread_count, expect_kthread the flow_tbl entry the "
+                           "host post-pass delivers to (rx.c:55-59), null on the wake path",
                    "slot": 128, "sets": sets}, f, indent=1)
     print("wrote", [s["name"] + f"({len(s['packets'])})" for s in sets])
 

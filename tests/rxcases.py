@@ -165,22 +165,21 @@ def fuzz_batch(rng, n, runtimes, max_runtimes, slot=128, tail_runts=True, misali
     return frames, frames_len, offs, olflags, rss, fdir, hint
 
 
-def to_verdict4(v, thread_count):
-    """8-B verdicts -> the GCL_CFG_VERDICT4 form: drop the hash; a WAKE
-    verdict carries its flow_tbl slot, hash % thread_count (rx.c:57, :68).
-    thread_count maps uniqid -> thread_count (dict or array)."""
+def to_verdict4(v, thread_count=None):
+    """8-B verdicts -> the GCL_CFG_VERDICT4 form: drop the hash.  Every
+    DELIVER and WAKE verdict, in either width, carries the flow_tbl slot
+    hash % thread_count (rx.c:57, :68); thread_count is not needed since
+    the 8-B verdicts already carry it (kept for callers)."""
     from caladan_amd.gclassify import VERDICT4_DTYPE
     out = np.zeros(len(v), dtype=VERDICT4_DTYPE)
     out["uniqid"], out["thread"], out["action"] = v["uniqid"], v["thread"], v["action"]
-    for i in np.nonzero((v["action"] & 0x3F) == 1)[0]:
-        out["thread"][i] = int(v["hash"][i]) % int(thread_count[int(v["uniqid"][i])])
     return out
 
 
 def to_verdict2(v, thread_count, thread_bits):
     """8-B verdicts -> the GCL_CFG_VERDICT2 form (include/gclassify.h): u16
-    q = uniqid << thread_bits | thread for DELIVER, 0x4000 | q (q holding
-    the flow_tbl slot) for WAKE, 0xC000 | action otherwise."""
+    q = uniqid << thread_bits | slot for DELIVER (slot = the flow_tbl slot),
+    0x4000 | q for WAKE, 0xC000 | action otherwise."""
     v4 = to_verdict4(v, thread_count)
     act = v4["action"].astype(np.uint32) & 0x3F
     q = v4["uniqid"].astype(np.uint32) << thread_bits | v4["thread"].astype(np.uint32)

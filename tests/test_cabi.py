@@ -212,8 +212,9 @@ def test_host_deliver_matches_reference_model(g, orc):
         act = v[i]["action"] & 0x3F
         if act in (0, 1):
             u = int(v[i]["uniqid"])
+            assert int(v[i]["thread"]) == int(v[i]["hash"]) % tc[u]  # the flow_tbl slot
             if act == 0:
-                th = int(v[i]["thread"])
+                th = flow[u][int(v[i]["thread"])]
             else:
                 if active[u] == 0:
                     active[u] = 1
@@ -384,6 +385,114 @@ def test_host_deliver4_matches_deliver(g, orc):
     assert full == compact2
     for vb in (4, 2, 8):
         assert full == run(f"recs{vb}"), vb
+
+
+def _live_batch(orc, seed, n=3000, R=64):
+    """A NIC-hash, Azure-ARP batch over 24 random runtimes (some with no
+    active thread) classified by the oracle: verdicts in all three widths."""
+    from tests.rxcases import fuzz_batch, random_runtimes, to_verdict2, to_verdict4
+    rng = np.random.default_rng(seed)
+    rts = random_runtimes(rng, R, 24, max_threads=6)
+    frames, flen, offs, olf, rss, fdir, _ = fuzz_batch(rng, n, rts, R, tail_runts=False)
+    t = orc.Tables(R, 0, 0x1, 0x09)
+    for r in rts:
+        assert t.runtime_set(r["uniqid"], r["ip"], r["thread_count"], r["active"], r["flow_tbl"]) == 0
+    v, _, _ = t.classify(frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir_hi=fdir, frames_len=flen)
+    tc = {r["uniqid"]: r["thread_count"] for r in rts}
+    pkt_len = rng.integers(60, 1515, size=n).astype(np.uint16)
+    return rts, v, to_verdict4(v), to_verdict2(v, tc, 3), pkt_len, olf, offs.astype(np.uint64), \
+        rss.astype(np.uint32)
+
+
+@pytest.mark.parametrize("form", [8, 4, 2, "recs8", "recs4", "recs2"])
+def test_host_deliver_live_flow_tbl(g, orc, form):
+    """The post-pass steers every DELIVER / WAKE verdict through the runtime's
+    flow_tbl and active count as they stand when the packet is delivered,
+    like rx.c:55-72, not as the device saw them: the sched_add_core of one
+    runtime's wake reaches __sched_run's pending branch (sched.c:208-216) and
+    disables a kthread of ANOTHER runtime (re-steering it, sched.c:174-192,
+    sometimes taking its last core), so that runtime's later packets in the
+    same batch follow the new table or take the wake path.  Ring contents,
+    counters and every callback equal the serial per-packet model."""
+    from tests.schedmodel import Sched, loop_records, make_cprocs, rx_model, run_post_pass
+    R, ring = 64, 32
+    rts, v, v4, v2, pkt_len, olf, shm, bh = _live_batch(orc, 21)
+    order = [r["uniqid"] for r in rts]
+    arp_ok = lambda i: i % 2 == 0  # noqa: E731
+
+    S_model = Sched(rts, 5, np.random.default_rng(5))
+    want = rx_model(S_model, v, order, ring, pkt_len, olf, shm, bh, arp_ok)
+    dis = [e for e in want[2] if e[0] == "disable"]
+    # the model really exercises the cross-runtime side effect, to zero too
+    assert len(dis) > 20 and any(e[3] == 0 for e in dis), dis[:5]
+    assert any(e[1] != w[1] for e, w in zip(want[2], want[2][1:]) if e[0] == "disable")
+
+    S = Sched(rts, 5, np.random.default_rng(5))
+    cprocs, rings = make_cprocs(g, S, ring, Ring)
+    if isinstance(form, str):
+        verd = loop_records(g, v, v4, v2, int(form[4:]))
+    else:
+        verd = {8: v, 4: v4, 2: v2}[form]
+    got = run_post_pass(g, S, cprocs, rings, form, verd, R, order, pkt_len, olf, shm, bh, arp_ok,
+                        thread_bits=3)
+    assert got[0] == want[0] and got[1] == want[1]
+    assert got[2] == want[2]
+    assert got[3] == want[3]
+
+
+def test_host_deliver_snapshot_thread_would_differ(g, orc):
+    """The batch of test_host_deliver_live_flow_tbl is one where steering
+    from the device's snapshot (flow_tbl as of classification) puts packets
+    in different rings: the live read above is observable."""
+    from tests.schedmodel import Sched, rx_model
+    R, ring = 64, 32
+    rts, v, v4, v2, pkt_len, olf, shm, bh = _live_batch(orc, 21)
+    order = [r["uniqid"] for r in rts]
+    S = Sched(rts, 5, np.random.default_rng(5))
+    snap = {u: list(p.flow) for u, p in S.procs.items()}
+    snap_active = {u: len(p.active) for u, p in S.procs.items()}
+    live = rx_model(S, v, order, ring, pkt_len, olf, shm, bh, lambda i: i % 2 == 0)[3]
+    moved = 0
+    for i in range(len(v)):
+        u = int(v["uniqid"][i])
+        if (v["action"][i] & 0x3F) == 0 and snap_active[u]:
+            th = snap[u][int(v["thread"][i])]
+            msg = (int(pkt_len[i]) << 16 | ((int(olf[i]) & 0x0C) == 0x08) << 48, int(shm[i]))
+            moved += msg not in live[(u, th)]
+    assert moved > 0
+
+
+def test_host_deliver_golden_kthreads(g):
+    """The hand-derived golden verdicts (tests/golden/rx_scenarios.json, each
+    from its rx.c line) through gcl_host_deliver: every DELIVER packet lands
+    in the ring of expect_kthread, flow_tbl[hash % thread_count] (rx.c:57),
+    and the wake verdicts (no sched_add_core here) in the idle thread's."""
+    from tests.rxcases import scenario_batch, scenario_sets
+    for s in scenario_sets():
+        rts = s["runtimes"]
+        R = s["cfg"]["max_runtimes"]
+        procs, rings, keep = _host_procs(g, rts, 64)
+        by_id = (ctypes.c_void_p * R)()
+        for u, p in procs.items():
+            by_id[u] = ctypes.addressof(p)
+        clients = (ctypes.c_void_p * len(procs))(*[ctypes.addressof(p) for p in procs.values()])
+        _, _, _, _, exp, _ = scenario_batch(s)
+        n = len(exp)
+        shm = np.arange(n, dtype=np.uint64) + 1000
+        stats = np.zeros(8, dtype=np.uint64)
+        g.lib.gcl_host_deliver(by_id, R, clients, len(procs), exp.ctypes.data, None, None, 0,
+                               shm.ctypes.data, n, None, stats.ctypes.data)
+        seen = {}
+        for (u, th), ring in rings.items():
+            for _, pay in ring.drain():
+                seen[int(pay) - 1000] = (u, th)
+        for i, pk in enumerate(s["packets"]):
+            a = pk["expect"]["action"] & 0x3F
+            if a == g.ACT_DELIVER:
+                assert seen[i] == (pk["expect"]["uniqid"], pk["expect_kthread"]), (s["name"], pk["cite"])
+            elif a == g.ACT_WAKE:
+                u = pk["expect"]["uniqid"]
+                assert seen[i] == (u, procs[u].idle_top), (s["name"], pk["cite"])
 
 
 @pytest.mark.parametrize("meta", ["all", "no_olflags", "none"])

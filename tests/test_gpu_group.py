@@ -325,3 +325,73 @@ def test_gpu_group_errors(g):
         assert not c.any() and not s.any()
     finally:
         grp.close()
+
+
+def test_gpu_group_eight_contexts(g, orc):
+    """The driver's 8-GPU shape rehearsed on the one GPU: a group of 8
+    contexts (host exchange), a ragged batch generated in place per rank
+    (gcl_group_classify) and one host batch split by the C splitter over the
+    8 (gcl_group_classify_host): every verdict equals the oracle's at its
+    global position, node counts and counters equal the oracle's, and each
+    rank's RX_PULLED is gcl_shard_count for that rank."""
+    from caladan_amd import shard
+    W, B, stride = 8, 4096, 64
+    n = 11 * B + 333  # blocks 0..10 plus a ragged block 11: ranks 0-3 take 2
+    grp = g.Group([0] * W, R, g.HASH_JENKINS, block=B, exchange=g.XCHG_HOST)
+    tables(grp)
+    t = orc.Tables(R, 1, 0, 0x09)
+    tables(t)
+    frames, _, _ = orc.generate(g.WL_UDP64, n, stride, R)
+    ve, ce, se = t.classify(frames, n, stride)
+    # device-resident shards
+    shards, vs = [], []
+    for r in range(W):
+        m = g.shard_count(n, W, r, B)
+        fr = torch.zeros(max(m, 1) * stride, dtype=torch.uint8, device="cuda")
+        g.generate(g.WL_UDP64, m, stride, R, fr, rank=r, world=W, shard_block=B)
+        shards.append({"frames": fr, "n": m, "stride": stride})
+        vs.append(torch.zeros(max(m, 1) * 8, dtype=torch.uint8, device="cuda"))
+    grp.classify(shards, vs)
+    grp.exchange()
+    c, s, per = grp.read()
+    for r in range(W):
+        idx = shard.shard_indices(n, r, W, B)
+        got = vs[r].cpu().numpy().view(g.VERDICT_DTYPE)[:len(idx)]
+        assert (got == ve[idx]).all(), r
+        assert int(per[r, R + g.RX_PULLED]) == g.shard_count(n, W, r, B), r
+    assert (c == ce).all() and (s == se).all()
+    # one host batch, split by the C splitter
+    grp.reset()
+    hv = pinned(np.zeros(n, dtype=g.VERDICT_DTYPE))
+    grp.classify_host(pinned(frames), n, stride, verdicts=hv, mode=g.E2E_ZEROCOPY)
+    grp.exchange()
+    c, s, per = grp.read()
+    assert (hv == ve).all(), np.nonzero(hv != ve)[0][:5]
+    assert (c == ce).all() and (s == se).all()
+    for r in range(W):
+        assert int(per[r, R + g.RX_PULLED]) == g.shard_count(n, W, r, B), r
+    assert sum(g.shard_count(n, W, r, B) for r in range(W)) == n
+    grp.close()
+
+
+def test_gpu_group_rccl_init_bounded(g):
+    """gcl_group_open's RCCL init is non-blocking and bounded: with a 1 ms
+    bound it either finishes or returns -ETIMEDOUT having aborted the
+    partial communicator; a group opened afterwards with the default bound
+    initialises and its all-gather runs."""
+    try:
+        grp = g.Group([0], R, g.HASH_JENKINS, init_timeout_ms=1)
+        grp.close()
+    except OSError as e:
+        assert e.errno == 110, e  # ETIMEDOUT
+    grp = g.Group([0], R, g.HASH_JENKINS)
+    tables(grp)
+    n = 4096
+    fr = torch.zeros(n * 64, dtype=torch.uint8, device="cuda")
+    g.generate(g.WL_UDP64, n, 64, R, fr)
+    v = torch.zeros(n * 8, dtype=torch.uint8, device="cuda")
+    grp.classify([{"frames": fr, "n": n, "stride": 64}], [v])
+    grp.exchange()
+    c, s, _ = grp.read()
+    assert int(c.sum()) + int(s[g.RX_UNHANDLED]) == n and int(s[g.RX_PULLED]) == n
+    grp.close()

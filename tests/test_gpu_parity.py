@@ -981,6 +981,45 @@ def test_gpu_reference_struct_frames(g, orc):
     assert int(c.sum()) == int(hit.sum())
 
 
+@pytest.mark.parametrize("vbytes", [8, 4, 2])
+def test_gpu_post_pass_live_flow_tbl(g, orc, vbytes):
+    """A GPU batch's verdicts through the host post-pass while sched_add_core
+    side effects re-steer OTHER runtimes mid-batch (tests/schedmodel.py,
+    sched.c:174-216): ring contents, counters and callbacks equal the serial
+    per-packet model of rx.c:50-92, for all three verdict widths."""
+    from tests.rxcases import fuzz_batch
+    from tests.schedmodel import Sched, make_cprocs, rx_model, run_post_pass
+    from tests.test_cabi import Ring
+    R, ring, tb = 64, 32, 3
+    rng = np.random.default_rng(21)
+    rts = random_runtimes(rng, R, 24, max_threads=6)
+    n = 3000
+    frames, flen, offs, olf, rss, fdir, _ = fuzz_batch(rng, n, rts, R, tail_runts=False)
+    t = orc.Tables(R, 0, 0x1, 0x09)
+    apply_runtimes(t, rts)
+    ve, ce, se = t.classify(frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir_hi=fdir, frames_len=flen)
+    flag = {8: 0, 4: g.CFG_VERDICT4, 2: g.CFG_VERDICT2}[vbytes]
+    clf = g.Classifier(0, R, 0, 0x1 | flag, 0x09, thread_bits=tb if vbytes == 2 else 0)
+    apply_runtimes(clf, rts)
+    v, c, st = gpu_run(g, clf, frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir=fdir, frames_len=flen)
+    tc = {r["uniqid"]: r["thread_count"] for r in rts}
+    exp = {8: ve, 4: to_verdict4(ve), 2: to_verdict2(ve, tc, tb)}[vbytes]
+    assert_same(v, exp, f"post-pass batch, {vbytes}-B verdicts")
+    assert (c == ce).all() and (st == se).all()
+    pkt_len = rng.integers(60, 1515, size=n).astype(np.uint16)
+    shm, bh = offs.astype(np.uint64), rss.astype(np.uint32)
+    order = [r["uniqid"] for r in rts]
+    arp_ok = lambda i: i % 2 == 0  # noqa: E731
+    want = rx_model(Sched(rts, 5, np.random.default_rng(5)), ve, order, ring, pkt_len, olf, shm, bh,
+                    arp_ok)
+    assert any(e[0] == "disable" and e[3] == 0 for e in want[2])
+    S = Sched(rts, 5, np.random.default_rng(5))
+    cprocs, rings = make_cprocs(g, S, ring, Ring)
+    got = run_post_pass(g, S, cprocs, rings, vbytes, np.ascontiguousarray(v), R, order, pkt_len, olf,
+                        shm, bh, arp_ok, thread_bits=tb)
+    assert got == want
+
+
 def test_gpu_rejects_oversized_batch(g):
     """n > 2^40 is refused before any launch (n * stride must not wrap)."""
     import ctypes

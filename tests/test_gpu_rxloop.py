@@ -362,3 +362,64 @@ def test_rxloop_transport_hashes(g, orc, mode, vb, lflag, monkeypatch):
     assert (got == w).all()
     bad = np.nonzero(gt != te)[0]
     assert not len(bad), f"{len(bad)} transport hashes differ, first {bad[0]}: {gt[bad[0]]} vs {te[bad[0]]}"
+
+
+@pytest.mark.parametrize("lflag,spec,use0", [(0, "0", (1 << 24) - 150), (0, "500000", (1 << 24) - 150),
+                                             (2, "500000", (1 << 32) - 150), (2, "0", (1 << 32) - 150)])
+def test_rxloop_stamp_wrap(g, orc, lflag, spec, use0, monkeypatch):
+    """The slots' use count crossing the stamps' wrap (2^24 for stamped
+    offsets, 2^32 for header records) with the loop started near it
+    (GCL_TUNE_LOOP_T0): stamps are never 0, so a zeroed or never-loaded
+    entry never passes for a current one, with the speculative window closed
+    (spec 0: every burst read after its word) or wide open (every burst with
+    the poll).  Every verdict equals the oracle's."""
+    rng = np.random.default_rng(7700 + lflag + len(spec))
+    max_rt = 16
+    rts = random_runtimes(rng, max_rt, 12)
+    n = 2048
+    frames, flen, offs, olf, rss, fdir, hint = fuzz_batch(rng, n, rts, max_rt)
+    t = orc.Tables(max_rt, 1, 0, 0x09)
+    apply_runtimes(t, rts)
+    ve, _, _ = t.classify(frames, n, 0, offs=offs, olflags=olf, rss=rss, frames_len=flen)
+    clf = g.Classifier(0, max_rt, 1, 0, 0x09)
+    apply_runtimes(clf, rts)
+    g.host_register(frames)
+    slots = 2
+    monkeypatch.setenv("GCL_TUNE_LOOP_SPEC", spec)
+    monkeypatch.setenv("GCL_TUNE_LOOP_T0", str(slots * use0))
+    loop = clf.rxloop(frames, slots=slots, workers=1, region_len=flen, flags=LOOP_FLAGS[lflag](g))
+    try:
+        nb = 600  # 300 uses of each slot: across the wrap
+        for k in range(nb):
+            m = int(rng.integers(1, 65))
+            idx = rng.integers(0, n, size=m)
+            tk = loop.submit(offs[idx], olf[idx], rss[idx])
+            assert tk == slots * use0 + k + 1
+            got = loop.wait(tk, m)
+            bad = np.nonzero(got != ve[idx])[0]
+            assert not len(bad), f"burst {k} (use {use0 + k // slots + 1}): {got[bad[0]]} vs {ve[idx][bad[0]]}"
+        ps = loop.poll_stats()
+        if spec == "0":
+            assert ps["early"] == 0, ps
+    finally:
+        loop.stop()
+        g.host_unregister(frames)
+
+
+def test_rxloop_release_incomplete(g):
+    """gcl_rxloop_release refuses (-EAGAIN) a burst the GPU has not completed,
+    so its slot is never handed to the next submit while still being written."""
+    frames = np.zeros(1 << 16, dtype=np.uint8)
+    clf = g.Classifier(0, 16, 1)
+    g.host_register(frames)
+    try:
+        loop = clf.rxloop(frames, slots=2, lifetime_ms=2000)
+        offs = np.arange(64, dtype=np.uint64) * 64
+        tk = loop.submit(offs)
+        r = g.lib.gcl_rxloop_release(loop._h, tk)
+        assert r in (0, -11)  # -EAGAIN unless the GPU was already done
+        loop.wait(tk, 64)
+        assert g.lib.gcl_rxloop_release(loop._h, tk) == 0
+        loop.stop()
+    finally:
+        g.host_unregister(frames)

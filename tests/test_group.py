@@ -31,7 +31,7 @@ def test_group_library_exports_every_declared_symbol(g):
 
 
 def test_group_cfg_layout(g):
-    assert ctypes.sizeof(g.GclGroupCfg) == 16
+    assert ctypes.sizeof(g.GclGroupCfg) == 24
 
 
 @pytest.mark.parametrize("block", [256, 4096, 64 << 10])

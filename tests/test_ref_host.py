@@ -168,15 +168,15 @@ def test_deliver_rings_read_by_reference_consumer(g, ref, orc):
     d = g.lib.gcl_host_deliver4(by_id, R, clients, len(procs), v4.ctypes.data, None,
                                 pkt_len.ctypes.data, olf.ctypes.data, 0x09, shm.ctypes.data, n,
                                 None, stats.ctypes.data)
-    # expected: DELIVER to its thread, WAKE (no sched_add_core here) to the
-    # idle thread, in packet order per ring
+    # expected: DELIVER to flow_tbl[slot], WAKE (no sched_add_core here) to
+    # the idle thread, in packet order per ring
     want = {k: [] for k in rings}
     for i in range(n):
         a = int(v4["action"][i]) & 0x3F
         if a not in (g.ACT_DELIVER, g.ACT_WAKE):
             continue
         u = int(v4["uniqid"][i])
-        th = int(v4["thread"][i]) if a == g.ACT_DELIVER else procs[u].idle_top
+        th = procs[u].flow_tbl[int(v4["thread"][i])] if a == g.ACT_DELIVER else procs[u].idle_top
         good = (int(olf[i]) & g.F_IP_CKSUM_MASK) == g.F_IP_CKSUM_GOOD
         want[(u, th)].append((ref.ref_rxq_cmd(int(pkt_len[i]), int(good)), int(shm[i])))
     assert d == sum(len(x) for x in want.values()) > n // 3
