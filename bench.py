@@ -846,6 +846,20 @@ def timed_launches(fn, reps):
     return (time.perf_counter() - t0) / reps, e0.elapsed_time(e1) / reps
 
 
+def ceiling(clf, frames, n, stride, out, kernel_ms, reps=10, **kw):
+    """The layout's own ceiling, measured in this process on the same buffers:
+    gcl_access_probe -- the classify launch's loads (frame bytes [0, 40) as
+    16-B chunks, the descriptor arrays) and its per-packet stores, no
+    classification -- timed like the kernel.  frac_of_ceiling = probe time /
+    kernel time: how close the kernel runs to what this frame layout allows
+    (e.g. one 128-B line per header of a 1536-B slot)."""
+    st = torch.cuda.current_stream().cuda_stream
+    _, pms = timed_launches(lambda: clf.access_probe(frames, n, stride, out=out, stream=st, **kw), reps)
+    return {"ceiling_ms": round(pms, 4), "frac_of_ceiling": round(pms / kernel_ms, 4),
+            "ceiling_what": ("gcl_access_probe on the same buffers: the launch's header loads, "
+                             "descriptor loads and per-packet stores without the classification")}
+
+
 # Algorithmic bytes of the integrated rx_burst shape (INTEGRATION.md §4), per
 # packet: the 64-B header granule + the descriptor's u64 offset into the mbuf
 # pool + u8 ol_flags + u32 hash.rss + the verdict.
@@ -918,7 +932,9 @@ def ingress_pool_bench(device, vbytes, cycles=64, reps=10, zerocopy=True,
             "device_resident_mpps": round(n / wall / 1e6, 1),
             "counts_check": "ok" if counts_ok() else "MISMATCH",
             "roofline": roofline_obj(n * bpp, gms, pmc_traffic("ingress_nic", vbytes),
-                                     {"bytes_per_pkt": bpp})}
+                                     {"bytes_per_pkt": bpp,
+                                      **ceiling(nic, region, n, 0, dv, gms, offs=offs, olflags=olf,
+                                                rss=rss)})}
     jen = None
     if "jenkins" in rows:
         cnt.zero_()
@@ -1031,32 +1047,30 @@ def trace_replay(device, n=64 << 10, reps=3):
 BOX_CPU_SHARE = 16
 
 
-def cpu_baseline(budget_s=12.0):
-    """rx.c's per-packet work on this host's cores, timed on the oracle's
-    restatement (TEST INFRASTRUCTURE, used here only as the baseline):
-    rx_one_pkt with rx.c's direct header-struct loads (rx.c:127-167), bursts
-    of 64 with prefetch stride 2 (rx.c:281-287), -O3 -march=native.
-      nic_mode     hash.rss from the NIC (rx.c:83) -- what rx.c computes per
-                   packet, the `value`;
+# bounded CPU samples of each timed stream (SURVEY §8d "CPU timing beside
+# it"; BASELINE.md: 64 B, 1500 B with 1024 runtimes and Zipf, mixed jumbo):
+# (packets, share of the budget).  The 1500-B and jumbo samples are far larger
+# than the host's caches, so every header is a DRAM miss as on the NIC's mbufs.
+CPU_STREAMS = {"udp64": (2 << 20, 0.5), "tcp1500": (512 << 10, 0.25), "mixed": (256 << 10, 0.25)}
+ZIPF_FLOWS = 1 << 20
+
+
+def cpu_stream(name, n, budget_s, native, threads):
+    """rx.c's per-packet work on this host's cores over a sample of stream
+    @name, timed on the oracle's restatement (TEST INFRASTRUCTURE, used here
+    only as the baseline): rx_one_pkt with rx.c's direct header-struct loads
+    (rx.c:127-167), bursts of 64 with prefetch stride 2 (rx.c:281-287),
+    -O3 -march=native; 1 core classify-only, 1 core classify + lrpc_send into
+    4096-deep rings (rx.c:76-92), and @threads cores on contiguous shards.
+      nic_mode     hash.rss from the NIC (rx.c:83) -- what rx.c computes;
       jenkins_mode the 13-B lookup3 flow hash computed on the CPU, the same
-                   work as the GPU headline.
-    Sample: the first 2 Mi packets of the udp64 stream (identical bytes to
-    the GPU's) with the generator's ol_flags and NIC hashes."""
+                   work as the GPU lines."""
     from oracle import orc
-    try:
-        orc.build(native=True)
-        native = True
-    except Exception as e:  # pragma: no cover - gcc missing on the box
-        log("native oracle build failed, using portable build:", e)
-        native = False
-    wl, _, stride, R, T, _ = WORKLOADS["udp64"]
-    n = 2 << 20
-    frames, olf, rss = orc.generate(wl, n, stride, R, seed=SEED, native=native)
-    try:
-        avail = len(os.sched_getaffinity(0))
-    except AttributeError:  # pragma: no cover
-        avail = os.cpu_count() or 1
-    threads = max(1, min(BOX_CPU_SHARE, avail))
+    wl, _, stride, R, T, _ = WORKLOADS[name]
+    cdf = orc.zipf_cdf(ZIPF_FLOWS) if wl == g.WL_TCP1500_ZIPF else None
+    pkt_len = np.zeros(n, dtype=np.uint16)
+    frames, olf, rss = orc.generate(wl, n, stride, R, seed=SEED, native=native, cdf=cdf,
+                                    pkt_len=pkt_len)
 
     def tables(mode):
         t = orc.Tables(R, mode, 0, g.F_RSS_HASH | g.F_IP_CKSUM_GOOD, native=native)
@@ -1068,12 +1082,13 @@ def cpu_baseline(budget_s=12.0):
         return t
 
     spent = 0.0
-    res = {}
-    for name, mode, share in (("nic_mode", g.HASH_NIC, 0.5), ("jenkins_mode", g.HASH_JENKINS, 0.5)):
+    res = {"sample": f"first {n} pkts of the {name} stream ({stride}-B slots, {R} runtimes x {T})",
+           "pkts": n}
+    for mname, mode in (("nic_mode", g.HASH_NIC), ("jenkins_mode", g.HASH_JENKINS)):
         t = tables(mode)
-        kw = dict(olflags=olf, rss=rss, direct=True)
+        kw = dict(olflags=olf, rss=rss, pkt_len=pkt_len, direct=True)
         probe = t.bench(frames, n, stride, threads=1, passes=1, **kw)
-        budget = budget_s * share
+        budget = budget_s * 0.5
         p1 = max(1, int(budget * 0.45 / max(probe, 1e-6)))
         s1 = t.bench(frames, n, stride, threads=1, passes=p1, **kw)
         pl = max(1, p1 // 2)
@@ -1081,10 +1096,36 @@ def cpu_baseline(budget_s=12.0):
         pm = max(1, int(budget * 0.3 / max(probe / threads, 1e-6)))
         sm = t.bench(frames, n, stride, threads=threads, passes=pm, **kw)
         spent += probe + s1 + sl + sm
-        res[name] = {"1core_mpps": round(n * p1 / s1 / 1e6, 2),
-                     "1core_lrpc_mpps": round(n * pl / sl / 1e6, 2),
-                     "all_cores_mpps": round(n * pm / sm / 1e6, 2), "all_cores": threads,
-                     "passes": [p1, pl, pm]}
+        res[mname] = {"1core_mpps": round(n * p1 / s1 / 1e6, 2),
+                      "1core_lrpc_mpps": round(n * pl / sl / 1e6, 2),
+                      "all_cores_mpps": round(n * pm / sm / 1e6, 2), "all_cores": threads,
+                      "passes": [p1, pl, pm]}
+    res["seconds"] = round(spent, 2)
+    del frames
+    return res
+
+
+def cpu_baseline(budget_s=24.0):
+    """The CPU baseline beside every timed stream: `value` is one core's
+    classify-only rate on the udp64 stream in NIC mode (the reference's own
+    per-packet work, one dataplane core, dpdk.c:276-280); `streams` holds the
+    same measurement on the tcp1500 and mixed samples, which bench.py also
+    attaches to the lines they stand beside."""
+    from oracle import orc
+    try:
+        orc.build(native=True)
+        native = True
+    except Exception as e:  # pragma: no cover - gcc missing on the box
+        log("native oracle build failed, using portable build:", e)
+        native = False
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        avail = os.cpu_count() or 1
+    threads = max(1, min(BOX_CPU_SHARE, avail))
+    streams = {name: cpu_stream(name, n, budget_s * share, native, threads)
+               for name, (n, share) in CPU_STREAMS.items()}
+    u = streams["udp64"]
     cpu_model = ""
     try:
         with open("/proc/cpuinfo") as f:
@@ -1095,15 +1136,17 @@ def cpu_baseline(budget_s=12.0):
     except OSError:
         pass
     return {
-        "value": res["nic_mode"]["1core_mpps"], "unit": "Mpkt/s", "cores": 1, "kind": "port",
-        "sample": (f"first {n} pkts of the udp64 stream, classify-only rx_one_pkt restatement with "
-                   f"rx.c's direct header loads and the NIC's hash.rss (rx.c:83), bursts of 64, "
+        "value": u["nic_mode"]["1core_mpps"], "unit": "Mpkt/s", "cores": 1, "kind": "port",
+        "sample": (f"first {u['pkts']} pkts of the udp64 stream, classify-only rx_one_pkt restatement "
+                   f"with rx.c's direct header loads and the NIC's hash.rss (rx.c:83), bursts of 64, "
                    f"prefetch stride 2, -O3 -march={'native' if native else 'x86-64-v2'}"),
-        "nic_mode": res["nic_mode"], "jenkins_mode": res["jenkins_mode"],
+        "nic_mode": u["nic_mode"], "jenkins_mode": u["jenkins_mode"],
+        "streams": {k: v for k, v in streams.items() if k != "udp64"},
         "all_cores_note": (f"{threads} threads: the GPU box's CPU share for one GPU "
                            f"(min({BOX_CPU_SHARE}, {avail} CPUs in this process's affinity mask)); "
                            f"the host reports nproc={os.cpu_count()}"),
-        "cpu_model": cpu_model, "nproc": os.cpu_count(), "seconds": round(spent, 2),
+        "cpu_model": cpu_model, "nproc": os.cpu_count(),
+        "seconds": round(sum(v["seconds"] for v in streams.values()), 2),
     }
 
 
@@ -1144,7 +1187,7 @@ def main():
     ap.add_argument("--group-node-force", action="store_true",
                     help="run the all-GPU group line even with one GPU visible")
     ap.add_argument("--group-child", type=int, default=0, help=argparse.SUPPRESS)
-    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--cpu-budget", type=float, default=24.0)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo only to rehearse N>1 on one GPU")
     ap.add_argument("--allow-shared-gpu", action="store_true",
@@ -1222,7 +1265,8 @@ def main():
                    "parallelism": (f"dp{world}: round-robin 64Ki-pkt shards, {args.dist_backend} "
                                    f"all_gather of per-runtime counts every {args.exchange_every} step(s), overlapped"
                                    if dist_on else "single GPU")},
-        "roofline": roofline(w, gms_k),
+        "roofline": {**roofline(w, gms_k),
+                     **ceiling(w.clf, w.frames, w.n, w.stride, w.verdicts, gms_k)},
         "kernel_only": {
             "value": round(w_n * world * args.steps / el_k / 1e6, 1), "unit": "Mpkt/s",
             "ms_per_step": round(el_k / args.steps * 1e3, 4), "gpu_ms_per_step": round(gms_k, 4),
@@ -1284,10 +1328,12 @@ def main():
         for vb2 in (SECONDARY_VERDICT_BYTES,) + tuple(b for b in (vb,) if b != SECONDARY_VERDICT_BYTES):
             w2 = Workload("tcp1500", rank, world, device, vbytes=vb2)
             el2, gms2 = run_timed(w2, steps2, 3, 1)
+            rf2 = roofline(w2, gms2)
+            rf2.update(ceiling(w2.clf, w2.frames, w2.n, w2.stride, w2.verdicts, gms2))
             sec[vb2] = {"verdict": VERDICT_NAMES[vb2],
                         "value": round(w2.n * steps2 / el2 / 1e6, 1), "unit": "Mpkt/s",
                         "ms_per_step": round(el2 / steps2 * 1e3, 4), "steps": steps2,
-                        "roofline": roofline(w2, gms2), "placement": placement(w2),
+                        "roofline": rf2, "placement": placement(w2),
                         "frame_bytes_rate_GBs": round(w2.n * 1500 / (gms2 * 1e-3) / 1e9, 1)}
             del w2
             torch.cuda.empty_cache()
@@ -1308,8 +1354,17 @@ def main():
         result["e2e"] = e2e_bench(device, vb)
 
     if world == 1 and not args.no_cpu:
-        result["cpu_baseline"] = cpu_baseline(args.cpu_budget)
-        result["cpu_baseline"]["gpu_over_1core_nic"] = round(value / result["cpu_baseline"]["value"], 1)
+        cpu = cpu_baseline(args.cpu_budget)
+        cpu["gpu_over_1core_nic"] = round(value / cpu["value"], 1)
+        result["cpu_baseline"] = cpu
+        # each stream's CPU rate beside the line it stands next to
+        if "secondary" in result:
+            c3 = cpu["streams"]["tcp1500"]
+            result["secondary"]["cpu_baseline"] = {
+                **c3, "gpu_over_1core_jenkins": round(result["secondary"]["value"] /
+                                                       c3["jenkins_mode"]["1core_mpps"], 1)}
+        if "e2e" in result:
+            result["e2e"]["mixed"]["cpu_baseline"] = cpu["streams"]["mixed"]
     if world > 1 and not args.no_e2e:
         result["e2e_multi"] = e2e_multi(device, rank, world, vb)
     if dist_on:

@@ -1755,6 +1755,67 @@ __global__ void __launch_bounds__(256) generate_kernel(GParams p)
 
 } // namespace
 
+/* --------------------------------------------------------------------------
+ * gcl_access_probe: one classify launch's memory traffic without the
+ * classification -- the layout's own ceiling.  Four lanes per packet load the
+ * 16-B-aligned chunks covering frame bytes [0, 40) (Ethernet, an IHL-5 IPv4
+ * header and the L4 ports: what the common case reads, in as few lines as any
+ * kernel can) with the tile kernel's streaming hint, lanes 1 and 2 the
+ * packet's ol_flags and hash.rss when the batch has them, every lane its
+ * offset when it has offsets, and lane 0 stores VB bytes per packet
+ * write-through like the verdict stores.  Four packets' loads per lane are in
+ * flight before any is used.
+ */
+template <int VB>
+__global__ void __launch_bounds__(256) access_probe_kernel(KParams k)
+{
+	const uint64_t lanes = k.n * 4;
+	const uint64_t G = (uint64_t)gridDim.x * 256;
+	const uint64_t base = (uint64_t)(uintptr_t)k.frames, end = base + k.frames_len;
+	uint32_t acc = 0;
+	for (uint64_t c0 = (uint64_t)blockIdx.x * 256 + threadIdx.x; c0 < lanes; c0 += 4 * G) {
+		uint4 v[4];
+		uint32_t side[4];
+#pragma unroll
+		for (int u = 0; u < 4; u++) {
+			const uint64_t c = c0 + u * G, p = c >> 2;
+			const uint32_t q = (uint32_t)c & 3;
+			v[u] = make_uint4(0, 0, 0, 0);
+			side[u] = 0;
+			if (c < lanes) {
+				const uint64_t off = k.offs ? user_off(k, k.offs[p]) : p * k.stride;
+				const uint64_t A = base + off;
+				const uint64_t a = (A & ~15ull) + 16 * q;
+				if (a < ((A + 40 + 15) & ~15ull) && a >= base && a + 16 <= end)
+					v[u] = gcl::load16_nt((const void *)a);
+				if (q == 1 && k.olflags)
+					side[u] = k.olflags[p];
+				if (q == 2 && k.rss)
+					side[u] = k.rss[p];
+			}
+		}
+#pragma unroll
+		for (int u = 0; u < 4; u++) {
+			const uint64_t c = c0 + u * G;
+			const uint32_t x = v[u].x ^ v[u].y ^ v[u].z ^ v[u].w ^ side[u];
+			acc ^= x;
+			if (c < lanes && (c & 3) == 0) {
+				if (VB == 2)
+					__hip_atomic_store((uint16_t *)k.verdicts + (c >> 2), (uint16_t)x, __ATOMIC_RELAXED,
+					                   __HIP_MEMORY_SCOPE_SYSTEM);
+				else if (VB == 4)
+					__hip_atomic_store((uint32_t *)k.verdicts + (c >> 2), x, __ATOMIC_RELAXED,
+					                   __HIP_MEMORY_SCOPE_SYSTEM);
+				else
+					__hip_atomic_store((uint64_t *)k.verdicts + (c >> 2), (uint64_t)x, __ATOMIC_RELAXED,
+					                   __HIP_MEMORY_SCOPE_SYSTEM);
+			}
+		}
+	}
+	if (acc == 0x9E3779B9u && k.stats) /* keeps every load live; practically never */
+		k.stats[GCL_NR_STATS - 1] = acc;
+}
+
 /* ==========================================================================
  * Host side of the C ABI.
  */
@@ -2461,6 +2522,39 @@ extern "C" int gcl_classify(struct gcl_ctx *c, const struct gcl_batch *b,
 {
 	struct gcl_out o = {verdicts, runtime_counts, stats, nullptr};
 	return gcl_classify_ex(c, b, &o, hip_stream);
+}
+
+extern "C" int gcl_access_probe(struct gcl_ctx *c, const struct gcl_batch *b, void *out,
+                                uint32_t vbytes, void *hip_stream)
+{
+	if (!c || !b || !out || (vbytes != 2 && vbytes != 4 && vbytes != 8))
+		return -EINVAL;
+	if (b->n == 0)
+		return 0;
+	if (!b->frames || b->frames_len == UINT64_MAX || b->n > (1ull << 40) ||
+	    (!b->offs && (b->stride < 16 || (b->stride & 15) || b->stride > (1u << 20))))
+		return -EINVAL;
+	if (hipSetDevice(c->device) != hipSuccess)
+		return -ENODEV;
+	KParams k = {};
+	k.frames = b->frames;
+	k.frames_len = b->frames_len;
+	k.stride = b->stride;
+	k.offs = b->offs;
+	k.olflags = b->olflags;
+	k.rss = b->rss;
+	k.n = b->n;
+	k.verdicts = (uint2 *)out;
+	const uint64_t need = (b->n * 4 + 255) / 256;
+	const unsigned grid = (unsigned)std::min<uint64_t>((uint64_t)c->num_cus * 8, need);
+	hipStream_t s = (hipStream_t)hip_stream;
+	if (vbytes == 2)
+		hipLaunchKernelGGL(access_probe_kernel<2>, dim3(grid), dim3(256), 0, s, k);
+	else if (vbytes == 4)
+		hipLaunchKernelGGL(access_probe_kernel<4>, dim3(grid), dim3(256), 0, s, k);
+	else
+		hipLaunchKernelGGL(access_probe_kernel<8>, dim3(grid), dim3(256), 0, s, k);
+	return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
 extern "C" int gcl_classify_ex(struct gcl_ctx *c, const struct gcl_batch *b,

@@ -182,6 +182,7 @@ def _load():
         "gcl_steer_flows": (i32, [u16, ctypes.POINTER(u16), u16, ctypes.POINTER(u16)]),
         "gcl_classify": (i32, [vp, ctypes.POINTER(GclBatch), vp, vp, vp, vp]),
         "gcl_classify_ex": (i32, [vp, ctypes.POINTER(GclBatch), ctypes.POINTER(GclOut), vp]),
+        "gcl_access_probe": (i32, [vp, ctypes.POINTER(GclBatch), vp, u32, vp]),
         "gcl_runtime_set_trans_seed": (i32, [vp, u16, u32]),
         "gcl_crc32c_u64": (u32, [u32, u64]),
         "gcl_trans_hash": (None, [u32, ctypes.c_uint8, u32, u16, u32, u16, ctypes.POINTER(GclTrans)]),
@@ -538,6 +539,19 @@ class Classifier:
                    trans=_ptr(trans))
         return _check(lib.gcl_classify_ex(self._ctx, ctypes.byref(b), ctypes.byref(o), stream),
                       "gcl_classify_ex")
+
+    def access_probe(self, frames, n, stride=0, out=None, vbytes=None, offs=None, olflags=None,
+                     rss=None, frames_len=None, stream=None):
+        """gcl_access_probe: a classify launch's loads and stores without the
+        classification (the layout's ceiling).  Asynchronous."""
+        vbytes = self.vbytes if vbytes is None else vbytes
+        if out is None or _nbytes(out) < vbytes * n:
+            raise ValueError("probe output buffer too small")
+        b = GclBatch(frames=_ptr(frames), frames_len=_frames_len(frames, frames_len),
+                     stride=stride, offs=_ptr(offs), olflags=_ptr(olflags), rss=_ptr(rss),
+                     fdir_hi=None, pkt_len=None, n=n, dst_hint=None)
+        return _check(lib.gcl_access_probe(self._ctx, ctypes.byref(b), _ptr(out), vbytes, stream),
+                      "gcl_access_probe")
 
     def classify_host(self, frames, n, stride=0, verdicts=None, counts=None, stats=None,
                       olflags=None, rss=None, fdir_hi=None, offs=None, frames_len=None,

@@ -331,6 +331,21 @@ struct gcl_out {
 int gcl_classify_ex(struct gcl_ctx *ctx, const struct gcl_batch *b, const struct gcl_out *out,
                     void *hip_stream);
 
+/*
+ * gcl_access_probe - the memory traffic of one gcl_classify launch over @b
+ * without the classification: the ceiling the frame layout itself sets
+ * (e.g. one 128-B line fetched per 64-B header of a 1536-B slot).  Every
+ * packet's frame bytes [0, 40) are loaded as the 16-B-aligned chunks that
+ * cover them, with the classify kernels' streaming hint, plus @b's offs,
+ * olflags and rss when given, and @vbytes (2, 4 or 8) bytes per packet are
+ * stored to device memory @out (not verdicts: a checksum of the loads).
+ * Asynchronous on @hip_stream; 0, -EINVAL or -EIO.  A measurement aid beside
+ * the classify kernel's roofline (bench.py roofline.ceiling), not part of
+ * the rx path.
+ */
+int gcl_access_probe(struct gcl_ctx *ctx, const struct gcl_batch *b, void *out, uint32_t vbytes,
+                     void *hip_stream);
+
 /* Host CRC32C step with the crc32q contract (no inversion, inc/asm/ops.h:77-80)
  * and the two transport hashes, for the runtime side. */
 uint32_t gcl_crc32c_u64(uint32_t crc, uint64_t val);

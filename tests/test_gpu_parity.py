@@ -1211,3 +1211,31 @@ def test_gpu_full_size_ingress_pool(g, orc, order):
     assert_same(q[sample], want, f"ingress pool {order} sample")
     del region, placed, dv
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("vbytes", [2, 4, 8])
+def test_gpu_access_probe(g, vbytes):
+    """gcl_access_probe (the layout-ceiling probe beside the roofline) reads
+    what it claims: packet p's stored word is the XOR of the four dwords of
+    the first 16-B chunk of its header window (fixed slots and offsets)."""
+    rng = np.random.default_rng(99)
+    n, stride = 5000, 1536
+    frames = rng.integers(0, 256, size=n * stride, dtype=np.uint8)
+    clf = g.Classifier(0, 16, 1)
+    f = dev(frames)
+    out = torch.zeros(n * vbytes, dtype=torch.uint8, device="cuda")
+    clf.access_probe(f, n, stride, out=out, vbytes=vbytes)
+    torch.cuda.synchronize()
+    w = frames.reshape(n, stride)[:, :16].copy().view(np.uint32)
+    x = (w[:, 0] ^ w[:, 1] ^ w[:, 2] ^ w[:, 3]).astype(np.uint64)
+    got = out.cpu().numpy().view({2: np.uint16, 4: np.uint32, 8: np.uint64}[vbytes]).astype(np.uint64)
+    assert (got == (x & {2: 0xFFFF, 4: 0xFFFFFFFF, 8: 0xFFFFFFFF}[vbytes])).all()
+    offs = (rng.permutation(n).astype(np.uint64) * np.uint64(stride) + np.uint64(344 % 16))
+    out.zero_()
+    clf.access_probe(f, n, 0, out=out, vbytes=vbytes, offs=dev(offs.astype(np.int64)))
+    torch.cuda.synchronize()
+    a = (offs & ~np.uint64(15)).astype(np.int64)
+    w = np.stack([frames[o:o + 16] for o in a]).view(np.uint32)
+    x = (w[:, 0] ^ w[:, 1] ^ w[:, 2] ^ w[:, 3]).astype(np.uint64)
+    got = out.cpu().numpy().view({2: np.uint16, 4: np.uint32, 8: np.uint64}[vbytes]).astype(np.uint64)
+    assert (got == (x & {2: 0xFFFF, 4: 0xFFFFFFFF, 8: 0xFFFFFFFF}[vbytes])).all()
