@@ -1270,6 +1270,7 @@ struct LoopParams {
 	uint32_t off_trans;        /* GCL_CFG_TRANS_HASH: 16-B {h5, h3, ticket} per packet; else 0 */
 	uint64_t t0;               /* tickets start after t0 (0; GCL_TUNE_LOOP_T0 tests the
 	                              stamps' wrap), a multiple of nslots */
+	uint32_t stamps;           /* GCL_LOOP_STAMPS: per-burst stage times into the slot header */
 };
 
 /* GCL_LOOP_HDR_RECORDS: the submitting core writes each packet as one 64-B
@@ -1370,6 +1371,7 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 	Tables tb = {};
 	uint32_t cur_seq = 0xFF; /* no image yet (versions are taken mod 64) */
 	uint32_t polls[3] = {0, 0, 0};
+	int poll_kind = 0; /* tid 0: how this burst arrived */
 
 	for (uint64_t t = L.t0 + blockIdx.x + 1;; t += L.workers) {
 		uint8_t *slot = L.slots + ((t - 1) % L.nslots) * L.slot_bytes;
@@ -1394,7 +1396,12 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 			uint64_t w = 0, e = 0;
 			bool rok = false, sp_hit = false;
 			uint4 q[4], qv[4] = {}; /* header records: the lane's packet's chunks */
+			uint64_t t_issue = 0;   /* GCL_LOOP_STAMPS: this poll's issue time */
+			uint32_t npoll = 0;
 			for (uint32_t k = 0;; k++) {
+				if (L.stamps)
+					t_issue = __builtin_amdgcn_s_memrealtime();
+				npoll = k + 1;
 				const bool sp = spec && __builtin_amdgcn_s_memrealtime() < spec_end;
 				const uint64_t ev = sp && !rec ? gcl::ld_sys64(slot + L.off_offs + 8 * tid) : 0;
 				if (sp && rec) {
@@ -1443,10 +1450,14 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 					s0.offs[tid] = e & kLoopOffMask;
 			}
 			if (tid == 0 && w) {
-				const int k = early ? kLoopPollEarly
-				            : (sp_hit && nw <= 64) ? kLoopPollStale : kLoopPollLate;
-				polls[k]++;
-				gcl::st_sys32(&L.polls[4 * blockIdx.x + k], polls[k]);
+				/* counted now, published after the burst's records: on gfx9
+				 * stores share vmcnt with loads, and any vmcnt(0) between
+				 * the hit and the records (the classify path has several)
+				 * would wait for this store's PCIe round trip, ~1.2 us
+				 * (GCL_LOOP_STAMPS, profiles/r04_stages.jsonl) */
+				poll_kind = early ? kLoopPollEarly
+				          : (sp_hit && nw <= 64) ? kLoopPollStale : kLoopPollLate;
+				polls[poll_kind]++;
 			}
 			if (tid == 0) {
 				s_ctl[0] = w != 0;
@@ -1455,9 +1466,19 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 				s_ctl[3] = (uint32_t)(w >> 6) & 1;
 				s_ctl[4] = (uint32_t)w & 63;
 				s_ctl[5] = early;
+				if (L.stamps) { /* hit time, the hitting poll's round trip, polls */
+					const uint64_t now = __builtin_amdgcn_s_memrealtime();
+					s_ctl[6] = (uint32_t)now;
+					s_ctl[7] = (uint32_t)(now >> 32);
+					s_ctl[8] = (uint32_t)(now - t_issue);
+					s_ctl[9] = npoll;
+				}
 			}
 		}
 		__syncthreads();
+		uint32_t st_b1 = 0, st_b2 = 0, st_b3 = 0; /* GCL_LOOP_STAMPS: past each barrier */
+		if (L.stamps && tid == 0)
+			st_b1 = (uint32_t)__builtin_amdgcn_s_memrealtime();
 		if (!s_ctl[0]) {
 			/* the host stops publishing on this (one word it can read
 			 * without asking the HIP runtime per burst) */
@@ -1486,6 +1507,8 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 			hist[i] = 0;
 		Counters cnt = {0, 0, 0, 0};
 		__syncthreads(); /* s_ctl consumed, tables and hist ready */
+		if (L.stamps && tid == 0)
+			st_b2 = (uint32_t)__builtin_amdgcn_s_memrealtime();
 		/* chunk pipeline: the side arrays of chunk c+1 and the frames of
 		 * chunk c are in flight together, and chunk c+1's frame loads are
 		 * issued before chunk c is classified */
@@ -1552,6 +1575,8 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 				}
 			}
 			__syncthreads(); /* tile of c and side arrays of c + 1 in LDS */
+			if (L.stamps && tid == 0)
+				st_b3 = (uint32_t)__builtin_amdgcn_s_memrealtime();
 			if (c + 1 < nch)
 				load_frames(side(c + 1), c + 1, chunk_m(c + 1));
 			k.n = m;
@@ -1573,9 +1598,25 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 					__builtin_amdgcn_raw_buffer_store_b128(tr, srs, (int)(L.off_trans + 16 * (base + tid)),
 					                                       0, gcl::kSysAux);
 				}
+				const uint64_t t_cls = L.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
 				const gcl::u32x4 rec = {hsh, vlo, (uint32_t)t, (uint32_t)(t >> 32)};
 				__builtin_amdgcn_raw_buffer_store_b128(
 				        rec, srs, (int)(L.off_verd + sizeof(LoopRec) * (base + tid)), 0, gcl::kSysAux);
+				if (L.stamps && tid == 0 && c + 1 == nch) {
+					/* stage times of this burst (10-ns ticks from the hit):
+					 * {ticket, hit's round trip, classified, record stored}
+					 * {ticket, polls, hit time lo, hi} */
+					const uint64_t hit = (uint64_t)s_ctl[7] << 32 | s_ctl[6];
+					const uint64_t t_st = __builtin_amdgcn_s_memrealtime();
+					const gcl::u32x4 a = {(uint32_t)t, s_ctl[8], (uint32_t)(t_cls - hit),
+					                      (uint32_t)(t_st - hit)};
+					const gcl::u32x4 b2 = {(uint32_t)t, s_ctl[9], s_ctl[6], s_ctl[7]};
+					const gcl::u32x4 c3 = {(uint32_t)t, st_b1 - (uint32_t)hit, st_b2 - (uint32_t)hit,
+					                       st_b3 - (uint32_t)hit};
+					__builtin_amdgcn_raw_buffer_store_b128(a, srs, 16, 0, gcl::kSysAux);
+					__builtin_amdgcn_raw_buffer_store_b128(b2, srs, 32, 0, gcl::kSysAux);
+					__builtin_amdgcn_raw_buffer_store_b128(c3, srs, 48, 0, gcl::kSysAux);
+				}
 			}
 			__syncthreads(); /* tile and side(c) free again */
 		}
@@ -1603,6 +1644,8 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 			if (tid == 0)
 				atomicAdd(&L.stats[GCL_RX_PULLED], (unsigned long long)n);
 		}
+		if (tid == 0)
+			gcl::st_sys32(&L.polls[4 * blockIdx.x + poll_kind], polls[poll_kind]);
 	}
 }
 
@@ -1756,58 +1799,54 @@ __global__ void __launch_bounds__(256) generate_kernel(GParams p)
 } // namespace
 
 /* --------------------------------------------------------------------------
- * gcl_access_probe: one classify launch's memory traffic without the
- * classification -- the layout's own ceiling.  Four lanes per packet load the
- * 16-B-aligned chunks covering frame bytes [0, 40) (Ethernet, an IHL-5 IPv4
- * header and the L4 ports: what the common case reads, in as few lines as any
- * kernel can) with the tile kernel's streaming hint, lanes 1 and 2 the
- * packet's ol_flags and hash.rss when the batch has them, every lane its
- * offset when it has offsets, and lane 0 stores VB bytes per packet
- * write-through like the verdict stores.  Four packets' loads per lane are in
- * flight before any is used.
+ * gcl_access_probe: the fewest memory requests one classify launch over the
+ * batch could make, without the classification -- the layout's own ceiling.
+ * One lane per packet issues one 16-B load of the 128-B line holding frame
+ * byte 0 and, only when frame bytes [0, 40) (Ethernet, an IHL-5 IPv4 header,
+ * the L4 ports: the common case's bytes) run into the next line, one of that
+ * line too; lines shared by neighbouring packets are fetched once by the L2.
+ * It also loads the packet's offset, ol_flags and hash.rss when the batch
+ * has them, and stores VB bytes per packet write-through like the verdict
+ * stores.  Four packets per lane are in flight before any load is used.
  */
 template <int VB>
 __global__ void __launch_bounds__(256) access_probe_kernel(KParams k)
 {
-	const uint64_t lanes = k.n * 4;
 	const uint64_t G = (uint64_t)gridDim.x * 256;
 	const uint64_t base = (uint64_t)(uintptr_t)k.frames, end = base + k.frames_len;
 	uint32_t acc = 0;
-	for (uint64_t c0 = (uint64_t)blockIdx.x * 256 + threadIdx.x; c0 < lanes; c0 += 4 * G) {
-		uint4 v[4];
+	for (uint64_t p0 = (uint64_t)blockIdx.x * 256 + threadIdx.x; p0 < k.n; p0 += 4 * G) {
+		uint4 v[4], w[4];
 		uint32_t side[4];
 #pragma unroll
 		for (int u = 0; u < 4; u++) {
-			const uint64_t c = c0 + u * G, p = c >> 2;
-			const uint32_t q = (uint32_t)c & 3;
-			v[u] = make_uint4(0, 0, 0, 0);
+			const uint64_t p = p0 + u * G;
+			v[u] = w[u] = make_uint4(0, 0, 0, 0);
 			side[u] = 0;
-			if (c < lanes) {
+			if (p < k.n) {
 				const uint64_t off = k.offs ? user_off(k, k.offs[p]) : p * k.stride;
-				const uint64_t A = base + off;
-				const uint64_t a = (A & ~15ull) + 16 * q;
-				if (a < ((A + 40 + 15) & ~15ull) && a >= base && a + 16 <= end)
-					v[u] = gcl::load16_nt((const void *)a);
-				if (q == 1 && k.olflags)
-					side[u] = k.olflags[p];
-				if (q == 2 && k.rss)
-					side[u] = k.rss[p];
+				const uint64_t A = base + off, a0 = A & ~15ull, a1 = (A + 39) & ~127ull;
+				if (a0 >= base && a0 + 16 <= end)
+					v[u] = gcl::load16_nt((const void *)a0);
+				if (a1 > a0 && a1 + 16 <= end) /* [0, 40) crosses into the next line */
+					w[u] = gcl::load16_nt((const void *)a1);
+				side[u] = (k.olflags ? k.olflags[p] : 0u) ^ (k.rss ? k.rss[p] : 0u);
 			}
 		}
 #pragma unroll
 		for (int u = 0; u < 4; u++) {
-			const uint64_t c = c0 + u * G;
-			const uint32_t x = v[u].x ^ v[u].y ^ v[u].z ^ v[u].w ^ side[u];
-			acc ^= x;
-			if (c < lanes && (c & 3) == 0) {
+			const uint64_t p = p0 + u * G;
+			const uint32_t x = v[u].x ^ v[u].y ^ v[u].z ^ v[u].w ^ w[u].x ^ side[u];
+			acc ^= x ^ w[u].y ^ w[u].z ^ w[u].w;
+			if (p < k.n) {
 				if (VB == 2)
-					__hip_atomic_store((uint16_t *)k.verdicts + (c >> 2), (uint16_t)x, __ATOMIC_RELAXED,
+					__hip_atomic_store((uint16_t *)k.verdicts + p, (uint16_t)x, __ATOMIC_RELAXED,
 					                   __HIP_MEMORY_SCOPE_SYSTEM);
 				else if (VB == 4)
-					__hip_atomic_store((uint32_t *)k.verdicts + (c >> 2), x, __ATOMIC_RELAXED,
+					__hip_atomic_store((uint32_t *)k.verdicts + p, x, __ATOMIC_RELAXED,
 					                   __HIP_MEMORY_SCOPE_SYSTEM);
 				else
-					__hip_atomic_store((uint64_t *)k.verdicts + (c >> 2), (uint64_t)x, __ATOMIC_RELAXED,
+					__hip_atomic_store((uint64_t *)k.verdicts + p, (uint64_t)x, __ATOMIC_RELAXED,
 					                   __HIP_MEMORY_SCOPE_SYSTEM);
 			}
 		}
@@ -2545,7 +2584,7 @@ extern "C" int gcl_access_probe(struct gcl_ctx *c, const struct gcl_batch *b, vo
 	k.rss = b->rss;
 	k.n = b->n;
 	k.verdicts = (uint2 *)out;
-	const uint64_t need = (b->n * 4 + 255) / 256;
+	const uint64_t need = (b->n + 255) / 256;
 	const unsigned grid = (unsigned)std::min<uint64_t>((uint64_t)c->num_cus * 8, need);
 	hipStream_t s = (hipStream_t)hip_stream;
 	if (vbytes == 2)
@@ -3359,7 +3398,7 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 	    cfg->max_burst > 4096 || !cfg->workers || cfg->workers > 64 || !cfg->lifetime_ms ||
 	    cfg->lifetime_ms > 600000)
 		return -EINVAL;
-	if ((cfg->flags & ~(uint32_t)(GCL_LOOP_INLINE_HDRS | GCL_LOOP_HDR_RECORDS)) ||
+	if ((cfg->flags & ~(uint32_t)(GCL_LOOP_INLINE_HDRS | GCL_LOOP_HDR_RECORDS | GCL_LOOP_STAMPS)) ||
 	    (cfg->flags & GCL_LOOP_INLINE_HDRS && cfg->flags & GCL_LOOP_HDR_RECORDS))
 		return -EINVAL;
 	if (cfg->region_len > kLoopOffMask - GCL_HDR_GRANULE)
@@ -3396,6 +3435,7 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 	lp.off_hint = lp.off_fdir + 4 * mb;
 	lp.off_verd = lp.off_hint + 4 * mb;
 	lp.hdr_rec = (cfg->flags & GCL_LOOP_HDR_RECORDS) != 0;
+	lp.stamps = (cfg->flags & GCL_LOOP_STAMPS) != 0;
 	lp.off_hdr = (cfg->flags & (GCL_LOOP_INLINE_HDRS | GCL_LOOP_HDR_RECORDS))
 	                     ? lp.off_verd + sizeof(LoopRec) * mb : 0;
 	lp.spec = (!lp.off_hdr || lp.hdr_rec) && cfg->max_burst <= 64;
@@ -3717,6 +3757,29 @@ extern "C" int gcl_rxloop_trans(struct gcl_rxloop *L, int64_t ticket, struct gcl
 		out[i].h5 = tr[i].hash;
 		out[i].h3 = tr[i].vlo;
 	}
+	return 0;
+}
+
+extern "C" int gcl_rxloop_stamps(struct gcl_rxloop *L, int64_t ticket, uint64_t out[8])
+{
+	if (!L || !out || !L->lp.stamps || ticket < 1 || (uint64_t)ticket > L->next)
+		return -EINVAL;
+	const uint64_t t = (uint64_t)ticket;
+	if (t + L->lp.nslots <= L->next)
+		return -ESTALE;
+	const uint32_t *h = (const uint32_t *)loop_slot(L, t);
+	const uint32_t a0 = __atomic_load_n(&h[4], __ATOMIC_ACQUIRE);
+	const uint32_t b0 = __atomic_load_n(&h[8], __ATOMIC_ACQUIRE);
+	const uint32_t c0 = __atomic_load_n(&h[12], __ATOMIC_ACQUIRE);
+	if (a0 != (uint32_t)t || b0 != (uint32_t)t || c0 != (uint32_t)t)
+		return -EAGAIN; /* posted after the records: not landed yet */
+	out[0] = 10ull * __atomic_load_n(&h[5], __ATOMIC_RELAXED); /* hitting poll's round trip */
+	out[1] = 10ull * __atomic_load_n(&h[6], __ATOMIC_RELAXED); /* hit -> classified */
+	out[2] = 10ull * __atomic_load_n(&h[7], __ATOMIC_RELAXED); /* hit -> last record issued */
+	out[3] = __atomic_load_n(&h[9], __ATOMIC_RELAXED);         /* polls of this wait */
+	for (int i = 0; i < 3; i++) /* hit -> past the loop's first three barriers */
+		out[4 + i] = 10ull * __atomic_load_n(&h[13 + i], __ATOMIC_RELAXED);
+	out[7] = 0;
 	return 0;
 }
 

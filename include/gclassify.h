@@ -332,16 +332,15 @@ int gcl_classify_ex(struct gcl_ctx *ctx, const struct gcl_batch *b, const struct
                     void *hip_stream);
 
 /*
- * gcl_access_probe - the memory traffic of one gcl_classify launch over @b
- * without the classification: the ceiling the frame layout itself sets
- * (e.g. one 128-B line fetched per 64-B header of a 1536-B slot).  Every
- * packet's frame bytes [0, 40) are loaded as the 16-B-aligned chunks that
- * cover them, with the classify kernels' streaming hint, plus @b's offs,
- * olflags and rss when given, and @vbytes (2, 4 or 8) bytes per packet are
- * stored to device memory @out (not verdicts: a checksum of the loads).
- * Asynchronous on @hip_stream; 0, -EINVAL or -EIO.  A measurement aid beside
- * the classify kernel's roofline (bench.py roofline.ceiling), not part of
- * the rx path.
+ * gcl_access_probe - the memory requests one gcl_classify launch over @b
+ * cannot do without, and nothing else: the ceiling the frame layout itself
+ * sets (e.g. one 128-B line fetched per 64-B header of a 1536-B slot).  One
+ * 16-B load per packet of the line holding frame byte 0 (plus one of the
+ * next line when frame bytes [0, 40) cross into it), @b's offs, olflags and
+ * rss when given, and @vbytes (2, 4 or 8) bytes stored per packet to device
+ * memory @out (not verdicts: a checksum of the loads).  Asynchronous on
+ * @hip_stream; 0, -EINVAL or -EIO.  A measurement aid beside the classify
+ * kernel's roofline (bench.py roofline.ceiling_ms), not part of the rx path.
  */
 int gcl_access_probe(struct gcl_ctx *ctx, const struct gcl_batch *b, void *out, uint32_t vbytes,
                      void *hip_stream);
@@ -548,6 +547,9 @@ struct gcl_rxloop_cfg {
  * wait (GCL_TUNE_LOOP_SPEC in the environment at gcl_rxloop_start: the
  * window in 10-ns ticks); a burst found later is read after its word. */
 #define GCL_LOOP_HDR_RECORDS 0x2
+/* Measurement: lane 0 of the worker stores each burst's stage times into
+ * the slot header after its records (gcl_rxloop_stamps). */
+#define GCL_LOOP_STAMPS 0x4
 int gcl_rxloop_start(struct gcl_ctx *ctx, const struct gcl_rxloop_cfg *cfg,
                      struct gcl_rxloop **out);
 int64_t gcl_rxloop_submit(struct gcl_rxloop *loop, uint32_t n, const uint64_t *offs,
@@ -586,6 +588,16 @@ int gcl_rxloop_poll_stats(struct gcl_rxloop *loop, uint64_t out[3]);
  * _release.  -EINVAL (no transport hashes), -EAGAIN (not complete yet),
  * -ESTALE (the slot was reused). */
 int gcl_rxloop_trans(struct gcl_rxloop *loop, int64_t ticket, struct gcl_trans *out);
+/* gcl_rxloop_stamps - with GCL_LOOP_STAMPS: @ticket's stage times in ns
+ * (s_memrealtime, 10-ns ticks): @out[0] the round trip of the poll that
+ * found the burst (its issue to its return), @out[1] from that return to
+ * the packets classified, @out[2] to the last verdict record's store issued,
+ * @out[3] the polls of that wait, @out[4..6] from the return to past the
+ * worker's first, second and third barriers (burst header shared, tables
+ * and histogram ready, tile ready), @out[7] 0.  -EAGAIN until they land
+ * (they are posted after the records), -ESTALE once the slot is reused,
+ * -EINVAL without the flag. */
+int gcl_rxloop_stamps(struct gcl_rxloop *loop, int64_t ticket, uint64_t out[8]);
 int gcl_rxloop_stop(struct gcl_rxloop *loop);
 int gcl_rxloop_drive(struct gcl_rxloop *loop, uint32_t n, const uint64_t *offs, uint32_t iters,
                      uint32_t depth, uint64_t *lat_ns, uint64_t *elapsed_ns);

@@ -342,8 +342,8 @@ struct pkt_view {
 /* byte k of the frame; bytes past frames_len read as 0 */
 static inline uint8_t fb(const struct pkt_view *pv, uint64_t k)
 {
-	uint64_t a = pv->off + k;
-	return a < pv->frames_len ? pv->frames[a] : 0;
+	/* no off + k: an offset near 2^64 must read 0, not wrap into the buffer */
+	return pv->off < pv->frames_len && k < pv->frames_len - pv->off ? pv->frames[pv->off + k] : 0;
 }
 
 static inline uint16_t fbe16(const struct pkt_view *pv, uint64_t k)

@@ -1217,25 +1217,68 @@ def test_gpu_full_size_ingress_pool(g, orc, order):
 def test_gpu_access_probe(g, vbytes):
     """gcl_access_probe (the layout-ceiling probe beside the roofline) reads
     what it claims: packet p's stored word is the XOR of the four dwords of
-    the first 16-B chunk of its header window (fixed slots and offsets)."""
+    the 16-B chunk holding its frame byte 0 and of the first dword of the next
+    line's chunk when frame bytes [0, 40) cross into it (fixed slots, and
+    offsets that straddle lines)."""
     rng = np.random.default_rng(99)
     n, stride = 5000, 1536
     frames = rng.integers(0, 256, size=n * stride, dtype=np.uint8)
     clf = g.Classifier(0, 16, 1)
     f = dev(frames)
     out = torch.zeros(n * vbytes, dtype=torch.uint8, device="cuda")
+    dt = {2: np.uint16, 4: np.uint32, 8: np.uint64}[vbytes]
+    mask = {2: 0xFFFF, 4: 0xFFFFFFFF, 8: 0xFFFFFFFF}[vbytes]
+
+    def want(offs):
+        x = np.zeros(n, dtype=np.uint64)
+        for i, o in enumerate(offs):
+            a0 = int(o) & ~15
+            w = frames[a0:a0 + 16].view(np.uint32)
+            v = int(w[0] ^ w[1] ^ w[2] ^ w[3])
+            a1 = (int(o) + 39) & ~127
+            if a1 > a0:
+                v ^= int(frames[a1:a1 + 4].view(np.uint32)[0])
+            x[i] = v
+        return x & np.uint64(mask)
+
     clf.access_probe(f, n, stride, out=out, vbytes=vbytes)
     torch.cuda.synchronize()
-    w = frames.reshape(n, stride)[:, :16].copy().view(np.uint32)
-    x = (w[:, 0] ^ w[:, 1] ^ w[:, 2] ^ w[:, 3]).astype(np.uint64)
-    got = out.cpu().numpy().view({2: np.uint16, 4: np.uint32, 8: np.uint64}[vbytes]).astype(np.uint64)
-    assert (got == (x & {2: 0xFFFF, 4: 0xFFFFFFFF, 8: 0xFFFFFFFF}[vbytes])).all()
-    offs = (rng.permutation(n).astype(np.uint64) * np.uint64(stride) + np.uint64(344 % 16))
+    got = out.cpu().numpy().view(dt).astype(np.uint64)
+    assert (got == want(np.arange(n, dtype=np.uint64) * np.uint64(stride))).all()
+    offs = rng.permutation(n).astype(np.uint64) * np.uint64(stride) + \
+        rng.choice([0, 8, 88, 96, 100, 120], size=n).astype(np.uint64)
     out.zero_()
     clf.access_probe(f, n, 0, out=out, vbytes=vbytes, offs=dev(offs.astype(np.int64)))
     torch.cuda.synchronize()
-    a = (offs & ~np.uint64(15)).astype(np.int64)
-    w = np.stack([frames[o:o + 16] for o in a]).view(np.uint32)
-    x = (w[:, 0] ^ w[:, 1] ^ w[:, 2] ^ w[:, 3]).astype(np.uint64)
-    got = out.cpu().numpy().view({2: np.uint16, 4: np.uint32, 8: np.uint64}[vbytes]).astype(np.uint64)
-    assert (got == (x & {2: 0xFFFF, 4: 0xFFFFFFFF, 8: 0xFFFFFFFF}[vbytes])).all()
+    got = out.cpu().numpy().view(dt).astype(np.uint64)
+    assert (got == want(offs)).all()
+
+
+@pytest.mark.parametrize("kernel", ["tile", "pair"])
+def test_gpu_offsets_at_the_top_of_u64(g, orc, monkeypatch, kernel):
+    """Offsets at and near 2^64 - 1 (the kernels' no-packet sentinel, ~0),
+    2^63 and frames_len read as frames of zeros like any offset past the
+    buffer, in both GENERAL kernels; gcl_classify refuses frames_len == ~0."""
+    monkeypatch.setenv("GCL_TUNE_PAIR", "0" if kernel == "tile" else "1")
+    rng = np.random.default_rng(9500 + (kernel == "pair"))
+    rts = random_runtimes(rng, 16, 12)
+    n = 3001
+    frames, flen, offs, olf, rss, fdir, hint = fuzz_batch(rng, n, rts, 16, tail_runts=False)
+    top = np.array([2**64 - 1, 2**64 - 2, 2**64 - 16, 2**63, flen, flen - 1, flen + 7], dtype=np.uint64)
+    idx = rng.choice(n, size=300, replace=False)
+    offs = offs.copy()
+    offs[idx] = top[np.arange(300) % len(top)]
+    t = orc.Tables(16, 1, 0, 0x09)
+    apply_runtimes(t, rts)
+    clf = g.Classifier(0, 16, 1, 0, 0x09)
+    apply_runtimes(clf, rts)
+    ve, ce, se = t.classify(frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir_hi=fdir, frames_len=flen)
+    v, c, st = gpu_run(g, clf, frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir=fdir, frames_len=flen)
+    assert_same(v, ve, f"top-of-u64 offsets, {kernel}")
+    assert (c == ce).all() and (st == se).all()
+    import ctypes
+    f, o = dev(frames), dev(offs.astype(np.int64))
+    vb = torch.zeros(n * 8, dtype=torch.uint8, device="cuda")
+    b = g.GclBatch(frames=f.data_ptr(), frames_len=2**64 - 1, stride=0, offs=o.data_ptr(), n=n)
+    out = g.GclOut(verdicts=vb.data_ptr())
+    assert g.lib.gcl_classify_ex(clf._ctx, ctypes.byref(b), ctypes.byref(out), None) == -22

@@ -26,6 +26,7 @@
 //         -Lcaladan_amd -lgclassify -Wl,-rpath,'$ORIGIN/../caladan_amd'
 #include <hip/hip_runtime.h>
 #include <ctype.h>
+#include <errno.h>
 #include <sched.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -251,6 +252,13 @@ int main(int argc, char **argv)
 	lc.region = region;
 	lc.region_len = nframes * stride;
 	lc.flags = inline_hdrs ? GCL_LOOP_INLINE_HDRS : hdr_records ? GCL_LOOP_HDR_RECORDS : 0;
+	/* RXPIPE_STAMPS=1: the lone-burst breakdown (depth 1): host submit and
+	 * submit -> records seen on the TSC, the worker's stage times
+	 * (GCL_LOOP_STAMPS) per burst */
+	const bool stamps = getenv("RXPIPE_STAMPS") && atoi(getenv("RXPIPE_STAMPS")) && depth == 1;
+	if (stamps)
+		lc.flags |= GCL_LOOP_STAMPS;
+	std::vector<uint64_t> st_sub, st_seen, st_rtt, st_cls, st_store, st_polls, st_b1, st_b2, st_b3;
 	struct gcl_rxloop *loop;
 	int ret = gcl_rxloop_start(ctx, &lc, &loop);
 	if (ret) {
@@ -286,6 +294,8 @@ int main(int argc, char **argv)
 					t_submit += ticks() - ts;
 					n_sub++;
 				}
+				if (stamps && timed)
+					st_sub.push_back(ticks() - ts);
 				if (r < 0) {
 					fprintf(stderr, "submit: %lld\n", (long long)r);
 					exit(1);
@@ -331,6 +341,20 @@ int main(int argc, char **argv)
 				t_wait += d0 - tw;
 				n_tail++;
 			}
+			if (stamps && timed) {
+				/* d0 is the peek's return when sampled; re-take it otherwise */
+				uint64_t g[8];
+				while (gcl_rxloop_stamps(loop, t, g) == -EAGAIN)
+					__builtin_ia32_pause();
+				st_seen.push_back(samp ? d0 - t_sub[tail % depth] : 0);
+				st_rtt.push_back(g[0]);
+				st_cls.push_back(g[1]);
+				st_store.push_back(g[2]);
+				st_polls.push_back(g[3]);
+				st_b1.push_back(g[4]);
+				st_b2.push_back(g[5]);
+				st_b3.push_back(g[6]);
+			}
 			if (timed)
 				lat.push_back(d1 - t_sub[tail % depth]);
 			tail++;
@@ -366,6 +390,27 @@ int main(int argc, char **argv)
 	       delivered == (uint64_t)burst * (nbursts + warm) ? "ok" : "MISMATCH",
 	       (unsigned long long)stats[GCL_RX_UNICAST_FAIL], cpu, (unsigned long long)ps[0],
 	       (unsigned long long)ps[1], (unsigned long long)ps[2]);
+	if (stamps) {
+		/* medians; the submit -> seen split only on the sampled bursts */
+		auto med = [](std::vector<uint64_t> v, bool drop0) {
+			if (drop0)
+				v.erase(std::remove(v.begin(), v.end(), 0ull), v.end());
+			if (v.empty())
+				return 0.0;
+			std::sort(v.begin(), v.end());
+			return (double)v[v.size() / 2];
+		};
+		const double sub = med(st_sub, false) * ns_tick, seen = med(st_seen, true) * ns_tick;
+		const double rtt = med(st_rtt, false), cls = med(st_cls, false), sto = med(st_store, false);
+		printf("{\"lone_burst_stages_ns\": {\"host_submit\": %.0f, \"submit_to_records_seen\": %.0f, "
+		       "\"gpu_hit_poll_round_trip\": %.0f, \"gpu_hit_to_classified\": %.0f, "
+		       "\"gpu_hit_to_last_record_issued\": %.0f, \"polls_per_wait\": %.0f, "
+		       "\"residual_word_to_hit_plus_writeback\": %.0f, \"gpu_hit_to_barrier1\": %.0f, "
+		       "\"gpu_hit_to_barrier2\": %.0f, \"gpu_hit_to_barrier3\": %.0f}, \"burst\": %u, \"flags\": \"%s\"}\n",
+		       sub, seen, rtt, cls, sto, med(st_polls, false), seen - sub - sto, med(st_b1, false),
+		       med(st_b2, false), med(st_b3, false), burst,
+		       hdr_records ? "records" : inline_hdrs ? "inline" : "offsets");
+	}
 	gcl_close(ctx);
 	CHECK(hipHostFree(region));
 	return 0;
