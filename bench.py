@@ -994,6 +994,17 @@ def ingress_pool_bench(device, vbytes, cycles=64, reps=10, zerocopy=True,
     for _ in range(3):
         nic.classify_host(hreg, n, 0, **kw)
     out["integrated_nic"]["zerocopy_mpps"] = round(n / ((time.perf_counter() - t0) / 3) / 1e6, 1)
+    # COPY over the same descriptors: the header gather kernel pulls each
+    # mbuf's first 80 B out of the pinned pool into HBM rows, chunk by chunk
+    # on 2 or 4 streams, and the batch kernel classifies the rows
+    for nst in (2, 4):
+        kwc = dict(kw, mode=g.E2E_COPY, nstreams=nst, chunk=1 << 20)
+        nic.classify_host(hreg, n, 0, **kwc)
+        t0 = time.perf_counter()
+        for _ in range(3):
+            nic.classify_host(hreg, n, 0, **kwc)
+        out["integrated_nic"][f"copy_gather_{nst}streams_mpps"] = round(
+            n / ((time.perf_counter() - t0) / 3) / 1e6, 1)
     del hreg, hoffs, holf, hrss, hv, offs, olf, rss, dv, nic, jen
     torch.cuda.empty_cache()
     return out

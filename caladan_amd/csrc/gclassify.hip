@@ -1855,6 +1855,72 @@ __global__ void __launch_bounds__(256) access_probe_kernel(KParams k)
 		k.stats[GCL_NR_STATS - 1] = acc;
 }
 
+/* --------------------------------------------------------------------------
+ * Header gather for gcl_classify_host's COPY transport over per-packet
+ * offsets (the reference's mbuf pool, frame data at element + 344): frame
+ * bytes [0, kGatherRow) of every packet, read out of mapped host memory into
+ * dense kGatherRow-byte rows of an HBM slab, which the batch kernel then
+ * classifies like fixed slots.  kGatherRow covers everything rx_one_pkt can
+ * read (ports at 14 + 4 * IHL + 4 <= 78 for IHL 15).  Eight lanes per
+ * packet: lanes 0-5 load the six 16-B-aligned chunks that cover the row at
+ * any alignment (coalesced into the fewest 64-B requests), lanes 0-4 funnel
+ * their chunk and the next lane's into one row chunk.  Bytes at or past
+ * frames_len, and every byte of a frame whose offset is, read 0.
+ */
+constexpr uint32_t kGatherRow = 80;
+
+__device__ __forceinline__ uint32_t funnel(uint32_t lo, uint32_t hi, uint32_t b)
+{
+	return b ? (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * b)) : lo;
+}
+
+__global__ void __launch_bounds__(256) header_gather_kernel(const uint8_t *frames, uint64_t frames_len,
+                                                            const uint64_t *offs, uint64_t n,
+                                                            uint8_t *slab)
+{
+	const uint64_t G = (uint64_t)gridDim.x * 32; /* packets per grid pass */
+	const uint32_t q = threadIdx.x & 7;
+	const uint64_t base = (uint64_t)(uintptr_t)frames, end = base + frames_len;
+	for (uint64_t p = (uint64_t)blockIdx.x * 32 + (threadIdx.x >> 3); p < n; p += G) {
+		const uint64_t o0 = offs[p];
+		const uint64_t off = o0 < frames_len ? o0 : frames_len;
+		const uint64_t A = base + off;
+		const uint64_t c = (A & ~15ull) + 16ull * q;
+		uint4 v = make_uint4(0, 0, 0, 0);
+		if (q < 6 && off < frames_len) {
+			if (c >= base && c + 16 <= end) {
+				v = *(const uint4 *)c;
+			} else { /* the region's first or last chunk: bytewise, 0 past it */
+				uint32_t w[4];
+				for (int i = 0; i < 4; i++) {
+					w[i] = 0;
+					for (int j = 0; j < 4; j++) {
+						const uint64_t a = c + 4 * i + j;
+						if (a >= base && a < end)
+							w[i] |= (uint32_t)*(const uint8_t *)a << (8 * j);
+					}
+				}
+				v = make_uint4(w[0], w[1], w[2], w[3]);
+			}
+		}
+		/* the next lane's chunk (a packet's lanes are 8 consecutive lanes) */
+		const uint32_t nx = __shfl_down(v.x, 1, 8), ny = __shfl_down(v.y, 1, 8);
+		const uint32_t nz = __shfl_down(v.z, 1, 8), nw = __shfl_down(v.w, 1, 8);
+		if (q < kGatherRow / 16) {
+			const uint32_t sh = (uint32_t)(A & 15), d = sh >> 2, b = sh & 3;
+			const uint32_t w[8] = {v.x, v.y, v.z, v.w, nx, ny, nz, nw};
+			uint32_t r[4];
+#pragma unroll
+			for (int i = 0; i < 4; i++) {
+				const uint32_t lo = d == 0 ? w[i] : d == 1 ? w[i + 1] : d == 2 ? w[i + 2] : w[i + 3];
+				const uint32_t hi = d == 0 ? w[i + 1] : d == 1 ? w[i + 2] : d == 2 ? w[i + 3] : w[i + 4];
+				r[i] = funnel(lo, hi, b);
+			}
+			*(uint4 *)(slab + p * kGatherRow + 16 * q) = make_uint4(r[0], r[1], r[2], r[3]);
+		}
+	}
+}
+
 /* ==========================================================================
  * Host side of the C ABI.
  */
@@ -3098,8 +3164,8 @@ static int e2e_setup(gcl_ctx *c, int nstreams, uint64_t chunk)
 	e.nstreams = 0;
 	for (int i = 0; i < nstreams; i++) {
 		if (hipStreamCreateWithFlags(&e.st[i], hipStreamNonBlocking) != hipSuccess ||
-		    hipMalloc(&e.slab[i], chunk * GCL_HDR_GRANULE) != hipSuccess ||
-		    hipMalloc(&e.side[i], chunk * 13) != hipSuccess ||
+		    hipMalloc(&e.slab[i], chunk * kGatherRow) != hipSuccess ||
+		    hipMalloc(&e.side[i], chunk * 21) != hipSuccess ||
 		    hipMalloc(&e.verd[i], chunk * sizeof(struct gcl_verdict)) != hipSuccess)
 			return -ENOMEM;
 		e.nstreams = i + 1;
@@ -3173,30 +3239,51 @@ extern "C" int gcl_classify_host(struct gcl_ctx *c, const struct gcl_batch *hb,
 		}
 		ret = gcl_classify(c, &db, dv, dcounts, dstats, s0);
 	} else {
-		if (hb->offs || (hb->stride & 15) || hb->stride < GCL_HDR_GRANULE) {
+		/* frames at per-packet offsets are gathered by a kernel reading the
+		 * mapped region; fixed slots by the DMA engine */
+		const uint8_t *dframes = hb->offs ? (const uint8_t *)mapped(hb->frames) : nullptr;
+		const uint64_t *doffs = hb->offs ? (const uint64_t *)mapped(hb->offs) : nullptr;
+		if (!hb->offs && ((hb->stride & 15) || hb->stride < GCL_HDR_GRANULE)) {
 			(void)hipEventDestroy(ready);
-			return -EINVAL; /* the copy path gathers fixed-stride header granules */
+			return -EINVAL;
 		}
+		if (hb->offs && (!dframes || hb->frames_len == UINT64_MAX)) {
+			(void)hipEventDestroy(ready);
+			return dframes ? -EINVAL : -EFAULT; /* the gather reads the registered region */
+		}
+		/* a row holds frame bytes [0, 80) (IHL 15's ports end at 78); a
+		 * 64-B slot stride is its own row (the next frame follows, as in
+		 * the host buffer) */
+		const uint64_t row = hb->offs || hb->stride >= kGatherRow ? kGatherRow : GCL_HDR_GRANULE;
 		for (uint64_t s = 0, ci = 0; s < hb->n && !ret; s += chunk, ci++) {
 			const int i = (int)(ci % nst);
 			const uint64_t m = hb->n - s < chunk ? hb->n - s : chunk;
 			hipStream_t st = e.st[i];
-			/* H2D of only the 64-B header granule of every slot (2D DMA) */
-			const uint8_t *src = hb->frames + s * hb->stride;
-			uint64_t avail = hb->frames_len > s * hb->stride ? hb->frames_len - s * hb->stride : 0;
-			if (avail < (m - 1) * hb->stride + GCL_HDR_GRANULE) {
-				ret = -EINVAL;
-				break;
+			if (hb->offs) {
+				const uint64_t *so = doffs ? doffs + s : (const uint64_t *)(e.side[i] + 13 * chunk);
+				if (!doffs)
+					he(hipMemcpyAsync((void *)so, hb->offs + s, m * 8, hipMemcpyHostToDevice, st));
+				const unsigned grid = (unsigned)std::min<uint64_t>((m + 31) / 32, (uint64_t)c->num_cus * 8);
+				hipLaunchKernelGGL(header_gather_kernel, dim3(grid), dim3(256), 0, st, dframes,
+				                   hb->frames_len, so, m, e.slab[i]);
+				he(hipGetLastError());
+			} else {
+				/* H2D of each slot's header row (2D DMA) */
+				const uint8_t *src = hb->frames + s * hb->stride;
+				uint64_t avail = hb->frames_len > s * hb->stride ? hb->frames_len - s * hb->stride : 0;
+				if (avail < (m - 1) * hb->stride + row) {
+					ret = -EINVAL;
+					break;
+				}
+				if (hb->stride == row)
+					he(hipMemcpyAsync(e.slab[i], src, m * row, hipMemcpyHostToDevice, st));
+				else
+					he(hipMemcpy2DAsync(e.slab[i], row, src, hb->stride, row, m, hipMemcpyHostToDevice, st));
 			}
-			if (hb->stride == GCL_HDR_GRANULE)
-				he(hipMemcpyAsync(e.slab[i], src, m * GCL_HDR_GRANULE, hipMemcpyHostToDevice, st));
-			else
-				he(hipMemcpy2DAsync(e.slab[i], GCL_HDR_GRANULE, src, hb->stride, GCL_HDR_GRANULE, m,
-				                    hipMemcpyHostToDevice, st));
 			struct gcl_batch db = {};
 			db.frames = e.slab[i];
-			db.frames_len = m * GCL_HDR_GRANULE;
-			db.stride = GCL_HDR_GRANULE;
+			db.frames_len = m * row;
+			db.stride = row;
 			db.n = m;
 			uint8_t *side = e.side[i];
 			if (hb->olflags) {

@@ -712,6 +712,14 @@ def test_gpu_ingress_pool_geometry(g, orc):
     clf.classify_host(hr, n, 0, verdicts=hv, counts=counts, stats=stats, offs=ho, mode=g.E2E_ZEROCOPY)
     assert_same(hv.numpy().view(g.VERDICT_DTYPE), ve, "ingress pool, zero-copy")
     assert (counts == ce).all() and (stats == se).all()
+    # COPY: the header gather kernel pulls each mbuf's first 80 B into HBM rows
+    hv.zero_()
+    counts[:] = 0
+    stats[:] = 0
+    clf.classify_host(hr, n, 0, verdicts=hv, counts=counts, stats=stats, offs=ho, mode=g.E2E_COPY,
+                      chunk=4096 + 3, nstreams=2)
+    assert_same(hv.numpy().view(g.VERDICT_DTYPE), ve, "ingress pool, header gather")
+    assert (counts == ce).all() and (stats == se).all()
 
 
 def test_gpu_ingress_integrated_nic_verdict2(g, orc):
@@ -1282,3 +1290,47 @@ def test_gpu_offsets_at_the_top_of_u64(g, orc, monkeypatch, kernel):
     b = g.GclBatch(frames=f.data_ptr(), frames_len=2**64 - 1, stride=0, offs=o.data_ptr(), n=n)
     out = g.GclOut(verdicts=vb.data_ptr())
     assert g.lib.gcl_classify_ex(clf._ctx, ctypes.byref(b), ctypes.byref(out), None) == -22
+
+
+@pytest.mark.parametrize("misalign", [None, "mixed", "lineend"])
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_gpu_copy_transport_fuzz(g, orc, misalign, mode):
+    """gcl_classify_host's COPY transport on the fuzz: per-packet offsets at
+    any alignment through the header gather kernel (frames straddling
+    frames_len, IHL up to 15 with ports up to byte 78, ARP target IPs), and
+    fixed 128-B slots through the 2D DMA of 80-B rows -- both bit-exact
+    against the oracle with ol_flags, hash.rss, FDIR marks and hints."""
+    rng = np.random.default_rng(9700 + 10 * mode + [None, "mixed", "lineend"].index(misalign))
+    rts = random_runtimes(rng, 64, 40)
+    n = 6001
+    slot = 256 if misalign == "lineend" else 128
+    frames, flen, offs, olf, rss, fdir, hint = fuzz_batch(rng, n, rts, 64, slot=slot, misalign=misalign)
+    key = bytes(rng.integers(0, 256, size=40, dtype=np.uint8))
+    t = orc.Tables(64, mode, 0, 0x09, key)
+    apply_runtimes(t, rts)
+    clf = g.Classifier(0, 64, mode, 0, 0x09, key)
+    apply_runtimes(clf, rts)
+    pin = lambda a: torch.from_numpy(np.ascontiguousarray(a)).pin_memory()  # noqa: E731
+    hr = pin(frames)
+    side = dict(olflags=pin(olf), rss=pin(rss.view(np.int32)), fdir_hi=pin(fdir.view(np.int32)),
+                dst_hint=pin(hint.view(np.int32)))
+    # offsets
+    ve, ce, se = t.classify(frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir_hi=fdir,
+                            frames_len=flen, dst_hint=hint)
+    hv = torch.zeros(n * 8, dtype=torch.uint8).pin_memory()
+    counts, stats = np.zeros(64, dtype=np.uint64), np.zeros(8, dtype=np.uint64)
+    clf.classify_host(hr, n, 0, verdicts=hv, counts=counts, stats=stats, offs=pin(offs.view(np.int64)),
+                      frames_len=flen, mode=g.E2E_COPY, chunk=2048 + 5, nstreams=3, **side)
+    assert_same(hv.numpy().view(g.VERDICT_DTYPE), ve, f"copy offsets {misalign} mode={mode}")
+    assert (counts == ce).all() and (stats == se).all()
+    if misalign is not None:
+        return
+    # fixed slots: the same buffer as n_slots x 128-B frames in slot order
+    ns = len(frames) // slot
+    ve, ce, se = t.classify(frames, ns, slot)
+    hv = torch.zeros(ns * 8, dtype=torch.uint8).pin_memory()
+    counts, stats = np.zeros(64, dtype=np.uint64), np.zeros(8, dtype=np.uint64)
+    clf.classify_host(hr, ns, slot, verdicts=hv, counts=counts, stats=stats, mode=g.E2E_COPY,
+                      chunk=1000, nstreams=2)
+    assert_same(hv.numpy().view(g.VERDICT_DTYPE), ve, f"copy slots mode={mode}")
+    assert (counts == ce).all() and (stats == se).all()
