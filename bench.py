@@ -62,7 +62,7 @@ HDR_BYTES = 64
 # slot, or a tagged drop/broadcast action -- everything rx_send_pkt_to_runtime
 # needs.  It halves the write requests of the 4-byte form: 331 vs 342 us for
 # udp64 and 174 vs 180 us for tcp1500 on the same buffers
-# (profiles/r02_defer_ab.jsonl).  The 4- and 8-byte forms stay as rows.
+# (profiles/archive/r02_defer_ab.jsonl).  The 4- and 8-byte forms stay as rows.
 VERDICT_BYTES = 2
 # the secondary (config 3, 1500-B TCP) line's verdict
 SECONDARY_VERDICT_BYTES = 2
@@ -147,7 +147,7 @@ def hip_copy(dst, src, nbytes):
 # chosen pair must run within this factor of the probe's time (per verdict
 # width), else the pool is placed again, at most PLACEMENT_TRIES times.  Fast
 # pairs measured kernel/probe 0.97-1.02 with 2-byte verdicts and 1.01-1.06
-# with 4-byte ones, slow pairs 1.12 and 1.19 (profiles/r02_pair_check.jsonl,
+# with 4-byte ones, slow pairs 1.12 and 1.19 (profiles/archive/r02_pair_check.jsonl,
 # r02_bench_spread_settle.jsonl, gpurun_out/r02c, r02g)
 PLACEMENT_SLACK = {2: 1.07, 4: 1.10, 8: 1.10}
 PLACEMENT_TRIES = 3
@@ -352,7 +352,7 @@ def run_timed(w, steps, warmup, world, ex=None):
     # settle: the kernel reaches its steady launch time only after ~40
     # back-to-back launches (~15 ms) following any pause -- 359 -> 343 -> 336
     # us per launch over the first 60 udp64 launches, then flat
-    # (profiles/r02_drift_v2.jsonl) -- so the timed steps start after at
+    # (profiles/archive/r02_drift_v2.jsonl) -- so the timed steps start after at
     # least SETTLE_MS of continuous steps, warmup included.  The step time is
     # estimated from the warmup (one settle step when there is none), and all
     # ranks run the same number of settle steps (the counts check needs it).
@@ -1335,7 +1335,7 @@ def main():
         sec = {}
         # config 3 leads with the 2-byte queue verdict (1024 runtimes x 4
         # kthreads fit thread_bits 2): 174 vs 180 us for the 4-byte one on
-        # the same buffers (profiles/r02_defer_ab.jsonl)
+        # the same buffers (profiles/archive/r02_defer_ab.jsonl)
         for vb2 in (SECONDARY_VERDICT_BYTES,) + tuple(b for b in (vb,) if b != SECONDARY_VERDICT_BYTES):
             w2 = Workload("tcp1500", rank, world, device, vbytes=vb2)
             el2, gms2 = run_timed(w2, steps2, 3, 1)

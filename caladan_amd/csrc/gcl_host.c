@@ -346,7 +346,7 @@ struct gcl_verdict4 gcl_verdict2_to4(uint16_t v, uint8_t thread_bits)
  * a runtime whose last core a scheduler side effect of this batch took,
  * broadcast, drops, a full ring) takes deliver() for that one packet, in
  * order, so the outcome is the same packet by packet.  A write prefetch of
- * the ring slot 8-32 packets ahead made it slower (profiles/r01_deliver.txt).
+ * the ring slot 8-32 packets ahead made it slower (profiles/archive/r01_deliver.txt).
  * Verdicts are @v2 (2-byte, of a context with @thread_bits) or @v4; always
  * inlined with a constant @v2 == NULL or not. */
 static inline __attribute__((always_inline)) uint64_t

@@ -66,11 +66,11 @@ constexpr int kDefaultXcdMap = 0; /* GCL_TUNE_XCD_MAP default: round-robin tiles
 /* GCL_TUNE_NT_STORE default: verdicts stored write-through (global_store
  * sc0 sc1).  Same buffers, one process: udp64 2.3-3.8 % faster for all three
  * verdict widths, tcp1500 2-2.4 %, the header-split layout unchanged
- * (profiles/r01_verdict_store_ab.jsonl) */
+ * (profiles/archive/r01_verdict_store_ab.jsonl) */
 constexpr int kDefaultVerdictStore = 2;
 /* Verdicts are stored at the end of their own tile.  Issuing them one tile
  * late (the former GCL_TUNE_DEFER=1) measured udp64 1-3 % slower and tcp1500
- * 0.4 % faster (profiles/r02_defer_ab.jsonl); the knob was removed for the
+ * 0.4 % faster (profiles/archive/r02_defer_ab.jsonl); the knob was removed for the
  * registers it held. */
 
 /* tuning knobs for experiments (GCL_TUNE_BLOCKS_PER_CU caps the grid) */
@@ -175,7 +175,7 @@ __device__ __forceinline__ uint64_t frame_off(const KParams &k, uint64_t idx)
  * 16-B loads instead of the eight or sixteen narrower ones an 8- or
  * 4-B-aligned granule needs (mbuf data at element + 344 in the reference's
  * ingress pool, defs.h:503-506, is 8-B aligned: 275 -> 216 us for 8 Mi random
- * mbufs, profiles/r01_ingress_ab.jsonl).  The window is cut at the end of its
+ * mbufs, profiles/archive/r01_ingress_ab.jsonl).  The window is cut at the end of its
  * first 128-B line (@cut < 64) when that line still holds frame bytes
  * [0, 40) -- Ethernet, an IHL-5 IPv4 header and the L4 ports, all the common
  * case reads -- so such a frame costs one line, not two; the rare packets
@@ -411,7 +411,7 @@ __device__ __forceinline__ uint32_t toeplitz_lut(const uint32_t *toep, uint32_t 
  * lookup drain alone 99.2-99.8 (8-B verdicts 85.9-87.3 against 92.7-93.9),
  * both drains 100.8-101.0 (92.5-92.8), a drain before both stages 86.7: the
  * HBM stream runs best with few requests outstanding per wave
- * (profiles/r02_dense_depth_ab.jsonl).
+ * (profiles/archive/r02_dense_depth_ab.jsonl).
  */
 __device__ __forceinline__ void dense_drain()
 {
@@ -819,7 +819,7 @@ classify_kernel(KParams k)
 	 * xcd_map (GCL_TUNE_XCD_MAP=1): block b walks XCD (b & 7)'s contiguous
 	 * eighth instead, eight separate streams; that measured 7% slower on
 	 * every buffer placement tried (tools/alloc_ab.cpp,
-	 * profiles/r01_alloc_placement.jsonl), so it stays an experiment. */
+	 * profiles/archive/r01_alloc_placement.jsonl), so it stays an experiment. */
 	uint64_t step = G, t_end = k.ntiles;
 	if (k.xcd_map && !k.sched) {
 		const uint64_t Gx = G / GCL_SCHED_XCD;
@@ -2519,9 +2519,9 @@ static Geometry choose_geometry(const gcl_ctx *c, uint32_t tab_lds, uint32_t his
 			g.bpc_cap = 1;
 	} else if (g.threads <= 512 && !c->tune_sched) {
 		/* a second tile in flight per block: 1.1-1.7 % faster on udp64 at
-		 * 4 x 256 lanes (profiles/r01_cbench_depth_*); at 2 x 512 lanes (the
+		 * 4 x 256 lanes (profiles/archive/r01_cbench_depth_*); at 2 x 512 lanes (the
 		 * 1024-runtime tables) 1 % on the 8 Mi header-split layout, 3.4 % at
-		 * 32 Mi, and no change on tcp1500 (profiles/r01_hsplit_geometry.jsonl) */
+		 * 32 Mi, and no change on tcp1500 (profiles/archive/r01_hsplit_geometry.jsonl) */
 		g.depth = 2;
 	}
 	if (g.pair && c->tune_pair == 2) { /* experiment: 2048 resident lanes per CU */
@@ -3002,7 +3002,7 @@ double pair_probe(const uint8_t *rd, size_t rd_bytes, uint8_t *wr, size_t wr_byt
 
 /* The class gap: same-class pairs measured 12-18% slower than cross-class
  * ones (406 vs 343 us classify; 375-382 vs 330-341 us in the probe's shape at
- * full size, profiles/r02_classmap.jsonl); run-to-run noise of one probe is
+ * full size, profiles/archive/r02_classmap.jsonl); run-to-run noise of one probe is
  * under 1.5%. */
 constexpr double kPairGap = 0.06;
 /* Of the free device memory at entry, at most this share is held by
@@ -3051,7 +3051,7 @@ extern "C" int gcl_dev_alloc_paired(int hip_device, size_t bytes, const void *pa
 		void *p = nullptr;
 		if (i && i % GCL_PAIR_RUN == 0) {
 			/* one class so far: step past the run.  Runs of one class span
-			 * 4-34 GiB of consecutive allocations (profiles/r02_classmap.jsonl),
+			 * 4-34 GiB of consecutive allocations (profiles/archive/r02_classmap.jsonl),
 			 * so the spacer grows: 2, 4, 8, then 16 x @bytes */
 			size_t sp_bytes = bytes * (2ull << std::min(nspacers, 3));
 			if (held + sp_bytes + bytes > hold_cap)

@@ -438,7 +438,7 @@ int gcl_dev_free(void *p);
  * iokernel's ingress region and rxq rings, shm.h:14-15, ioqueues.c:31-40).
  * On MI355X the header read stream and the verdict write stream run ~15%
  * slower when the two buffers fall in the same physical placement class
- * (measured: DESIGN.md §4 "Buffer placement", profiles/r01_pair_*.jsonl).
+ * (measured: DESIGN.md §4 "Buffer placement", profiles/archive/r01_pair_*.jsonl).
  * The class cannot be read from a virtual address, so this allocates a
  * candidate, times a read+write probe of the classify kernel's access shape
  * over the whole of both buffers (up to 4 GiB read, 256 MiB written) against
@@ -446,7 +446,7 @@ int gcl_dev_free(void *p);
  * earlier one by more than the class gap (the faster of the two), trying at
  * most GCL_PAIR_TRIES candidates; losers are freed.  Classes come in runs of
  * consecutive allocations (4-34 GiB of 2-GiB pools in a row were measured,
- * profiles/r02_classmap.jsonl), so after every GCL_PAIR_RUN candidates of one
+ * profiles/archive/r02_classmap.jsonl), so after every GCL_PAIR_RUN candidates of one
  * class a spacer of 2, 4, 8, then 16 x @bytes is allocated to step past the
  * run.  Candidates and spacers together hold at most 60% of the free device
  * memory; all but the kept buffer are freed before returning.  When no second

@@ -1,5 +1,5 @@
 #!/bin/bash
-# tools/alloc_ab experiments behind profiles/r01_alloc_placement.jsonl and
+# tools/alloc_ab experiments behind profiles/archive/r01_alloc_placement.jsonl and
 # r01_alloc_sweep_tlb.jsonl: $1 = default | cfirst | xcdmap | tlb
 export TMPDIR=/tmp
 O=gpurun_out/r01/alloc

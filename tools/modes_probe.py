@@ -1,5 +1,5 @@
 """Is the udp64 step's bimodal rate (~92 vs ~100 Gpkt/s in one process on
-the same buffers, profiles/r02_streams_ab.jsonl) a clock state?  Runs
+the same buffers, profiles/archive/r02_streams_ab.jsonl) a clock state?  Runs
 200-step samples for ~25 s and records, between samples, the current DPM
 levels the amdgpu driver exposes read-only in sysfs (pp_dpm_sclk / mclk /
 fclk / socclk, the '*' line) and the hwmon power reading.  Reads only.

@@ -69,7 +69,7 @@ def request_bytes(base, tag, wl):
     Bandwidth' formula prices reads as 128 x TCC_BUBBLE + 32 x RDREQ_32B + 64 x
     the rest, but on this ROCm 7.2 / gfx950 TCC_BUBBLE reads 0 even for a
     dense 2 GiB stream that is 16.8 M requests for 2.15 GB (tools/halfline.hip,
-    profiles/r01_halfline.jsonl): every read request carries a 128-B line, the
+    profiles/archive/r01_halfline.jsonl): every read request carries a 128-B line, the
     guide's x2.  So the request counts are reported, and the byte totals use
     128 B per read request and the write counters as documented."""
     d1 = os.path.join(base, f"{tag}_REQ", "run_counter_collection.csv")

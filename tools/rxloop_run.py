@@ -1,7 +1,7 @@
 """bench.py's rx loop latency leg alone (e2e.rxloop): burst latency of the
 persistent loop at 64..1024-packet bursts, one fresh process per call (the
 staggered-poller knobs it once compared are gone from the library,
-profiles/r02_loop_pollers_ab.jsonl).
+profiles/archive/r02_loop_pollers_ab.jsonl).
 
     python tools/rxloop_run.py [iters]
 """

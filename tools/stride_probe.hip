@@ -4,7 +4,7 @@
 // tcp1500 (config 3) reads the first 64 B of every 1536-B slot.  On ordinary
 // (coarse-grained, cached) device memory every such read fetches a whole
 // 128-B L2 line and the line rate, not the byte rate, bounds the kernel
-// (profiles/r01_halfline.jsonl, r01_membench.jsonl).  An uncached or
+// (profiles/archive/r01_halfline.jsonl, r01_membench.jsonl).  An uncached or
 // fine-grained allocation changes the memory type the L2 applies, and a
 // system-scope load changes how the L2 treats the request; if either lets the
 // fabric move 64 B instead of 128 B per slot, the layout's ceiling moves.
