@@ -8,8 +8,11 @@
  * the mbuf (rx.c:86-90), the sched_add_core wake path for runtimes with no
  * active kthread (rx.c:62-72), the Azure ARP broadcast/response, and the
  * ring-full counters RX_UNICAST_FAIL / RX_BROADCAST_FAIL.  Verdicts are
- * consumed in packet order, so a wake that activates a kthread is visible to
- * the later packets of the same batch exactly as in the reference.
+ * consumed in packet order and every DELIVER / WAKE verdict's flow_tbl slot
+ * is resolved against p->flow_tbl and p->active_thread_count as they stand
+ * when that packet is delivered (rx.c:55-72): a wake earlier in the batch
+ * whose sched_add_core activated a kthread, or disabled another runtime's
+ * (sched.c:208-216), steers the later packets exactly as in the reference.
  */
 #ifndef GCL_HOST_H
 #define GCL_HOST_H
@@ -95,8 +98,8 @@ uint64_t gcl_host_deliver(struct gcl_host_proc *const *clients_by_id, uint32_t m
                           const struct gcl_host_ops *ops, uint64_t *stats);
 
 /*
- * gcl_host_deliver4 - the same over compact verdicts (GCL_CFG_VERDICT4).  A
- * WAKE verdict's @thread is the flow_tbl slot (hash % thread_count).
+ * gcl_host_deliver4 - the same over compact verdicts (GCL_CFG_VERDICT4), whose
+ * @thread is the flow_tbl slot (hash % thread_count) like gcl_verdict's.
  * @bcast_hash     per-packet hash for GCL_ACT_BROADCAST fan-out: in
  *                 GCL_HASH_NIC mode the mbuf hash.rss array the batch was
  *                 classified with (masked to 16 bits under GCL_CFG_HASH16);
@@ -118,7 +121,7 @@ struct gcl_verdict4 gcl_verdict2_to4(uint16_t v, uint8_t thread_bits);
  * gcl_host_deliver2 - gcl_host_deliver4 over 2-byte verdicts: the same
  * replay of rx_send_pkt_to_runtime / rx_send_to_runtime (rx.c:50-92),
  * packet by packet, of @v widened by gcl_verdict2_to4.  The DELIVER
- * fast path reads the destination ring straight from the queue index.
+ * fast path reads flow_tbl[slot] of the runtime the queue index names.
  */
 uint64_t gcl_host_deliver2(struct gcl_host_proc *const *clients_by_id, uint32_t max_runtimes,
                            struct gcl_host_proc *const *clients, int nr_clients,

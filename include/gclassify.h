@@ -152,10 +152,19 @@ enum gcl_action {
 #define GCL_NO_RUNTIME  0xFFFF
 #define GCL_NO_THREAD   0xFF
 
+/*
+ * DELIVER and WAKE verdicts name the runtime and its flow-table SLOT,
+ * hash % thread_count (rx.c:57, :68), not the kthread: the host post-pass
+ * (gcl_host.h) reads p->flow_tbl[slot] and p->active_thread_count when it
+ * delivers the packet, as rx_send_to_runtime does (rx.c:55-72), so a
+ * scheduler change earlier in the same batch is seen by the later packets.
+ * DELIVER means the runtime had an active kthread in the classify snapshot,
+ * WAKE that it had none; the post-pass re-checks either way.
+ */
 struct gcl_verdict {
 	uint32_t hash;    /* steering hash (hash.rss, or the computed flow hash) */
 	uint16_t uniqid;  /* proc->uniqid of the destination, GCL_NO_RUNTIME if none */
-	uint8_t  thread;  /* flow_tbl[hash % thread_count], GCL_NO_THREAD if none */
+	uint8_t  thread;  /* the flow_tbl slot hash % thread_count, GCL_NO_THREAD if none */
 	uint8_t  action;  /* enum gcl_action | GCL_ACT_F_FDIR */
 };
 
@@ -163,26 +172,24 @@ struct gcl_verdict {
  * Compact verdict (GCL_CFG_VERDICT4): the last four bytes of gcl_verdict,
  * without the hash.  rx_send_to_runtime uses the hash only as
  * hash % thread_count (rx.c:57, :68), and thread_count is fixed per runtime,
- * so a WAKE verdict carries that flow_tbl slot in @thread instead: the host
- * replay indexes the flow_tbl as it stands after sched_add_core.  The only
- * other use of the hash is the Azure ARP broadcast fan-out, where it is
- * the mbuf's hash.rss in GCL_HASH_NIC mode and 0 in the computed modes (ARP
- * is not hashed): gcl_host_deliver4 takes it from the caller.
+ * so the slot in @thread is all the post-pass needs.  The only other use of
+ * the hash is the Azure ARP broadcast fan-out, where it is the mbuf's
+ * hash.rss in GCL_HASH_NIC mode and 0 in the computed modes (ARP is not
+ * hashed): gcl_host_deliver4 takes it from the caller.
  */
 struct gcl_verdict4 {
 	uint16_t uniqid;  /* as gcl_verdict */
-	uint8_t  thread;  /* DELIVER: flow_tbl[hash % thread_count];
-	                     WAKE: hash % thread_count; otherwise GCL_NO_THREAD */
+	uint8_t  thread;  /* DELIVER, WAKE: the flow_tbl slot hash % thread_count;
+	                     otherwise GCL_NO_THREAD */
 	uint8_t  action;  /* as gcl_verdict */
 };
 
 /*
- * 2-byte verdict (GCL_CFG_VERDICT2): a u16 per packet naming a kthread queue
- * q = uniqid << thread_bits | thread, one flat index over every runtime's
- * rxq (&p->threads[thread].rxq, defs.h:244).
- *   DELIVER (any flags)  q of flow_tbl[hash % thread_count]
- *   WAKE                 GCL_V2_WAKE | uniqid << thread_bits | hash % thread_count
- *                        (the flow_tbl slot, as gcl_verdict4's WAKE)
+ * 2-byte verdict (GCL_CFG_VERDICT2): a u16 per packet naming a runtime's
+ * flow-table slot q = uniqid << thread_bits | slot, one flat index over
+ * every runtime's flow_tbl (defs.h:244), slot = hash % thread_count.
+ *   DELIVER (any flags)  q
+ *   WAKE                 GCL_V2_WAKE | q
  *   every other action   GCL_V2_OTHER | action (DROP_*, BROADCAST, ARP_RESPOND)
  * It drops what gcl_verdict4 keeps beyond that: GCL_ACT_F_FDIR, which the
  * host never reads (RX_FLOW_TAG_MATCH is counted on the device).  Half the
