@@ -1223,6 +1223,8 @@ constexpr uint64_t kLoopRefresh = 256;
 /* s_memrealtime ticks (100 MHz) a wait polls the offsets with the word: a
  * burst that arrives later costs the offsets' round trip after the word */
 constexpr uint64_t kLoopSpecTicks = 400;
+/* GCL_TUNE_LOOP_CLOCK default: 0 polls on s_memrealtime, 1 on s_memtime */
+constexpr uint32_t kDefaultLoopClock = 0;
 /* how a worker's bursts arrived (gcl_rxloop_poll_stats): with the poll that
  * found the word; eligible for that, but an entry or record still stale so
  * read after it; or after the word, the speculative window over or the
@@ -1271,6 +1273,7 @@ struct LoopParams {
 	uint64_t t0;               /* tickets start after t0 (0; GCL_TUNE_LOOP_T0 tests the
 	                              stamps' wrap), a multiple of nslots */
 	uint32_t stamps;           /* GCL_LOOP_STAMPS: per-burst stage times into the slot header */
+	uint32_t fast_clock;       /* poll on the shader clock (GCL_TUNE_LOOP_CLOCK) */
 };
 
 /* GCL_LOOP_HDR_RECORDS: the submitting core writes each packet as one 64-B
@@ -1356,6 +1359,29 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 	uint8_t *lds_tab = (uint8_t *)(hist + ((L.max_rt + 3) & ~3u));
 	const int tid = threadIdx.x;
 	const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + L.lifetime_ticks;
+	/* the poll's clock: with L.fast_clock the speculative window runs on
+	 * the shader clock (s_memtime, read locally) and the lifetime bound on
+	 * the real-time counter only every 16th poll; s_memrealtime is a round
+	 * trip to the real-time counter (tools/clock_probe.hip) that a poll
+	 * otherwise waits for before issuing its loads.  The shader clock's
+	 * rate is calibrated against the real-time counter at start (10 us). */
+	uint64_t spec_cyc = L.spec_ticks, clk_r = 1, clk_c = 1;
+	if (L.fast_clock) {
+		const uint64_t r0 = __builtin_amdgcn_s_memrealtime(), c0 = __builtin_amdgcn_s_memtime();
+		uint64_t r1;
+		do {
+			r1 = __builtin_amdgcn_s_memrealtime();
+		} while (r1 - r0 < 1000);
+		const uint64_t c1 = __builtin_amdgcn_s_memtime();
+		clk_r = r1 - r0;
+		clk_c = c1 - c0;
+		spec_cyc = (uint64_t)L.spec_ticks * clk_c / clk_r;
+	}
+	/* GCL_LOOP_STAMPS: the poll's clock, and its ticks -> 10-ns ticks */
+	auto sclk = [&]() -> uint64_t {
+		return L.fast_clock ? __builtin_amdgcn_s_memtime() : __builtin_amdgcn_s_memrealtime();
+	};
+	auto to10 = [&](uint64_t d) -> uint32_t { return (uint32_t)(d * clk_r / clk_c); };
 	const __amdgpu_buffer_rsrc_t frs = gcl::host_rsrc(L.frames, L.frames_len);
 	if (tid == 0 && blockIdx.x < 8) /* which XCD this worker runs on */
 		gcl::st_sys32(&L.where[blockIdx.x], __builtin_amdgcn_s_getreg((3 << 11) | 20) + 1);
@@ -1392,7 +1418,8 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 			const bool spec = L.spec, rec = L.hdr_rec;
 			const uint64_t stamp = loop_stamp(t, L.nslots);
 			const uint32_t rstamp = loop_rec_stamp(t, L.nslots);
-			const uint64_t spec_end = __builtin_amdgcn_s_memrealtime() + L.spec_ticks;
+			const uint64_t spec_end = L.fast_clock ? __builtin_amdgcn_s_memtime() + spec_cyc
+			                                       : __builtin_amdgcn_s_memrealtime() + L.spec_ticks;
 			uint64_t w = 0, e = 0;
 			bool rok = false, sp_hit = false;
 			uint4 q[4], qv[4] = {}; /* header records: the lane's packet's chunks */
@@ -1400,9 +1427,10 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 			uint32_t npoll = 0;
 			for (uint32_t k = 0;; k++) {
 				if (L.stamps)
-					t_issue = __builtin_amdgcn_s_memrealtime();
+					t_issue = sclk();
 				npoll = k + 1;
-				const bool sp = spec && __builtin_amdgcn_s_memrealtime() < spec_end;
+				const bool sp = spec && (L.fast_clock ? __builtin_amdgcn_s_memtime()
+				                                      : __builtin_amdgcn_s_memrealtime()) < spec_end;
 				const uint64_t ev = sp && !rec ? gcl::ld_sys64(slot + L.off_offs + 8 * tid) : 0;
 				if (sp && rec) {
 #pragma unroll
@@ -1432,7 +1460,8 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 						q[j] = qv[j];
 					break;
 				}
-				if (sv || __builtin_amdgcn_s_memrealtime() > t_end)
+				if (sv || ((!L.fast_clock || (k & 15) == 15) &&
+				           __builtin_amdgcn_s_memrealtime() > t_end))
 					break;
 				__builtin_amdgcn_s_sleep(1);
 			}
@@ -1467,10 +1496,10 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 				s_ctl[4] = (uint32_t)w & 63;
 				s_ctl[5] = early;
 				if (L.stamps) { /* hit time, the hitting poll's round trip, polls */
-					const uint64_t now = __builtin_amdgcn_s_memrealtime();
+					const uint64_t now = sclk();
 					s_ctl[6] = (uint32_t)now;
 					s_ctl[7] = (uint32_t)(now >> 32);
-					s_ctl[8] = (uint32_t)(now - t_issue);
+					s_ctl[8] = to10(now - t_issue);
 					s_ctl[9] = npoll;
 				}
 			}
@@ -1478,7 +1507,7 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 		__syncthreads();
 		uint32_t st_b1 = 0, st_b2 = 0, st_b3 = 0; /* GCL_LOOP_STAMPS: past each barrier */
 		if (L.stamps && tid == 0)
-			st_b1 = (uint32_t)__builtin_amdgcn_s_memrealtime();
+			st_b1 = (uint32_t)sclk();
 		if (!s_ctl[0]) {
 			/* the host stops publishing on this (one word it can read
 			 * without asking the HIP runtime per burst) */
@@ -1508,7 +1537,7 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 		Counters cnt = {0, 0, 0, 0};
 		__syncthreads(); /* s_ctl consumed, tables and hist ready */
 		if (L.stamps && tid == 0)
-			st_b2 = (uint32_t)__builtin_amdgcn_s_memrealtime();
+			st_b2 = (uint32_t)sclk();
 		/* chunk pipeline: the side arrays of chunk c+1 and the frames of
 		 * chunk c are in flight together, and chunk c+1's frame loads are
 		 * issued before chunk c is classified */
@@ -1576,7 +1605,7 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 			}
 			__syncthreads(); /* tile of c and side arrays of c + 1 in LDS */
 			if (L.stamps && tid == 0)
-				st_b3 = (uint32_t)__builtin_amdgcn_s_memrealtime();
+				st_b3 = (uint32_t)sclk();
 			if (c + 1 < nch)
 				load_frames(side(c + 1), c + 1, chunk_m(c + 1));
 			k.n = m;
@@ -1598,7 +1627,7 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 					__builtin_amdgcn_raw_buffer_store_b128(tr, srs, (int)(L.off_trans + 16 * (base + tid)),
 					                                       0, gcl::kSysAux);
 				}
-				const uint64_t t_cls = L.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
+				const uint64_t t_cls = L.stamps ? sclk() : 0;
 				const gcl::u32x4 rec = {hsh, vlo, (uint32_t)t, (uint32_t)(t >> 32)};
 				__builtin_amdgcn_raw_buffer_store_b128(
 				        rec, srs, (int)(L.off_verd + sizeof(LoopRec) * (base + tid)), 0, gcl::kSysAux);
@@ -1607,12 +1636,11 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 					 * {ticket, hit's round trip, classified, record stored}
 					 * {ticket, polls, hit time lo, hi} */
 					const uint64_t hit = (uint64_t)s_ctl[7] << 32 | s_ctl[6];
-					const uint64_t t_st = __builtin_amdgcn_s_memrealtime();
-					const gcl::u32x4 a = {(uint32_t)t, s_ctl[8], (uint32_t)(t_cls - hit),
-					                      (uint32_t)(t_st - hit)};
+					const uint64_t t_st = sclk();
+					const gcl::u32x4 a = {(uint32_t)t, s_ctl[8], to10(t_cls - hit), to10(t_st - hit)};
 					const gcl::u32x4 b2 = {(uint32_t)t, s_ctl[9], s_ctl[6], s_ctl[7]};
-					const gcl::u32x4 c3 = {(uint32_t)t, st_b1 - (uint32_t)hit, st_b2 - (uint32_t)hit,
-					                       st_b3 - (uint32_t)hit};
+					const gcl::u32x4 c3 = {(uint32_t)t, to10(st_b1 - (uint32_t)hit),
+					                       to10(st_b2 - (uint32_t)hit), to10(st_b3 - (uint32_t)hit)};
 					__builtin_amdgcn_raw_buffer_store_b128(a, srs, 16, 0, gcl::kSysAux);
 					__builtin_amdgcn_raw_buffer_store_b128(b2, srs, 32, 0, gcl::kSysAux);
 					__builtin_amdgcn_raw_buffer_store_b128(c3, srs, 48, 0, gcl::kSysAux);
@@ -3523,6 +3551,9 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 	lp.off_verd = lp.off_hint + 4 * mb;
 	lp.hdr_rec = (cfg->flags & GCL_LOOP_HDR_RECORDS) != 0;
 	lp.stamps = (cfg->flags & GCL_LOOP_STAMPS) != 0;
+	lp.fast_clock = kDefaultLoopClock;
+	if (const char *e = getenv("GCL_TUNE_LOOP_CLOCK"))
+		lp.fast_clock = atoi(e) != 0;
 	lp.off_hdr = (cfg->flags & (GCL_LOOP_INLINE_HDRS | GCL_LOOP_HDR_RECORDS))
 	                     ? lp.off_verd + sizeof(LoopRec) * mb : 0;
 	lp.spec = (!lp.off_hdr || lp.hdr_rec) && cfg->max_burst <= 64;
