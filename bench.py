@@ -153,10 +153,14 @@ PLACEMENT_SLACK = {2: 1.07, 4: 1.10, 8: 1.10}
 PLACEMENT_TRIES = 3
 # the slack above was calibrated on 16-runtime udp64 pairs only; with 1024
 # runtimes the kernel's time is not predicted by the probe's read+write
-# shape (the header-split pool ran 96 us against an 81-83 us probe on every
-# placement, BENCH_r02.json), so those pools keep the probe's choice and the
-# kernel check is recorded as skipped instead of re-placing them
+# shape (the header-split pool ran 94-96 us against an 81-83 us probe on
+# every placement, BENCH_r02.json, r04), so those pools are checked with
+# gcl_access_probe instead: the kernel's memory requests without the
+# classification, whose time depends on the placement and not on the
+# runtime count.  ACCESS_SLACK[vbytes] bounds it against the pair probe's
+# chosen time the way PLACEMENT_SLACK bounds the kernel.
 PLACEMENT_CHECK_RUNTIMES = (16,)
+ACCESS_SLACK = {2: 1.10, 4: 1.10, 8: 1.10}
 PROBE_READ_CAP = 4 << 30  # gcl_dev_alloc_paired's probe reads at most this much
 
 
@@ -194,11 +198,7 @@ class Workload:
         self.tables = setup_tables(self.clf, R, T)
         torch.cuda.synchronize()
         if getattr(self, "paired", False) and stride == HDR_BYTES:
-            if R in PLACEMENT_CHECK_RUNTIMES:
-                self.check_placement()
-            else:
-                self.placement_checks.append({"skipped": f"kernel check calibrated for {PLACEMENT_CHECK_RUNTIMES} "
-                                                         f"runtimes only; {R} here: the probe's choice is kept"})
+            self.check_placement(access=R not in PLACEMENT_CHECK_RUNTIMES)
 
     def _new_pool(self):
         buf = g.DeviceBuffer(self.n * self.stride, self.device.index or 0,
@@ -229,7 +229,24 @@ class Workload:
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / reps * 1e3
 
-    def check_placement(self, tries=PLACEMENT_TRIES):
+    def access_us(self, reps=5):
+        """Mean gcl_access_probe time over this pair (the kernel's loads and
+        stores without the classification)."""
+        st = torch.cuda.current_stream()
+
+        def go():
+            self.clf.access_probe(self.frames, self.n, self.stride, out=self.verdicts,
+                                  stream=st.cuda_stream)
+        go()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(reps):
+            go()
+        e1.record(st)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps * 1e3
+
+    def check_placement(self, tries=PLACEMENT_TRIES, access=False):
         """Keep the frame pool only if the classify kernel itself runs in the
         fast class over it: its launch time within PLACEMENT_SLACK[vbytes] of the
         probe's chosen time (scaled to the probe's 4 GiB read cap).  A pool
@@ -244,10 +261,15 @@ class Workload:
             rd, wr = self.n * self.stride, self.n * self.vbytes
             probed = min(rd, PROBE_READ_CAP) + max(1, min(wr, info["probe_write_bytes"] or wr))
             scale = (rd + wr) / probed
-            us = self.kernel_us()
-            limit = info["probe_us_chosen"] * scale * PLACEMENT_SLACK[self.vbytes]
+            us = self.access_us() if access else self.kernel_us()
+            limit = info["probe_us_chosen"] * scale * (ACCESS_SLACK if access else PLACEMENT_SLACK)[self.vbytes]
             ok = us <= limit
-            self.placement_checks.append({"kernel_us": round(us, 2), "probe_us_chosen":
+            # the other time too (calibration data for ACCESS_SLACK)
+            other = self.kernel_us() if access else self.access_us()
+            self.placement_checks.append({("access_probe_us" if access else "kernel_us"): round(us, 2),
+                                          ("kernel_us" if access else "access_probe_us"): round(other, 2),
+                                          "checked_with": "gcl_access_probe" if access else "classify kernel",
+                                          "probe_us_chosen":
                                           info["probe_us_chosen"], "limit_us": round(limit, 2),
                                           "classes_seen": info["classes_seen"], "passed": ok,
                                           **({"kept": True} if ok else
