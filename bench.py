@@ -757,7 +757,8 @@ def rxpipe_bench(reps=3):
     for cfg in (("64", "1", "1", "20000"), ("64", "4", "8", "20000"), ("64", "4", "8", "20000", "copy"),
                 ("64", "8", "16", "40000"), ("64", "16", "32", "40000"), ("64", "32", "64", "60000"),
                 ("64", "8", "16", "40000", "inline"), ("64", "16", "32", "40000", "inline"),
-                ("64", "1", "1", "20000", "records"), ("64", "8", "16", "40000", "records"),
+                ("64", "1", "1", "20000", "records"), ("64", "4", "8", "20000", "records"),
+                ("64", "8", "16", "40000", "records"),
                 ("64", "16", "32", "40000", "records"),
                 ("256", "4", "8", "10000"),
                 ("1024", "8", "16", "4000"), ("4096", "16", "16", "1000")):
