@@ -428,8 +428,8 @@ static int ensure_staging(gcl_group *g, gcl_group::Dev &D, int nst)
 	for (int s = 0; s < nst; s++) {
 		if (D.slab[s])
 			continue;
-		if (hipMalloc(&D.slab[s], g->block * GCL_HDR_GRANULE) != hipSuccess ||
-		    hipMalloc(&D.side[s], g->block * 13) != hipSuccess ||
+		if (hipMalloc(&D.slab[s], g->block * GCL_GATHER_ROW) != hipSuccess ||
+		    hipMalloc(&D.side[s], g->block * 21) != hipSuccess ||
 		    hipMalloc(&D.verd[s], g->block * 8) != hipSuccess)
 			return -ENOMEM;
 	}
@@ -512,10 +512,25 @@ extern "C" int gcl_group_classify_host(struct gcl_group *g, const struct gcl_bat
 			                   D.st[(b / G) % nst]);
 		}
 	} else {
-		if (hb->offs || hb->stride < GCL_HDR_GRANULE)
-			return -EINVAL; /* the copy path gathers fixed-stride header granules */
-		if (hb->frames_len < (hb->n - 1) * hb->stride + GCL_HDR_GRANULE)
+		/* a row holds frame bytes [0, 80) (IHL 15's ports end at 78): 80-B
+		 * rows by 2D DMA from slots of >= 80 B, the 64-B slots themselves,
+		 * or gathered by gcl_header_gather from per-packet offsets */
+		const uint64_t row = hb->offs || hb->stride >= GCL_GATHER_ROW ? GCL_GATHER_ROW : GCL_HDR_GRANULE;
+		if (!hb->offs && (hb->stride < GCL_HDR_GRANULE ||
+		                  hb->frames_len < (hb->n - 1) * hb->stride + row))
 			return -EINVAL;
+		if (hb->offs && hb->frames_len == UINT64_MAX)
+			return -EINVAL;
+		const uint8_t *dfr[GCL_GROUP_MAX_DEV];
+		const uint64_t *dof[GCL_GROUP_MAX_DEV];
+		for (int i = 0; i < G && hb->offs; i++) {
+			if (hipSetDevice(g->d[i].dev) != hipSuccess)
+				return -ENODEV;
+			dfr[i] = (const uint8_t *)mapped(hb->frames);
+			dof[i] = (const uint64_t *)mapped(hb->offs);
+			if (!dfr[i])
+				return -EFAULT; /* the gather reads the registered region */
+		}
 		for (int i = 0; i < G; i++)
 			if ((ret = ensure_staging(g, g->d[i], nst)))
 				return ret;
@@ -528,16 +543,23 @@ extern "C" int gcl_group_classify_host(struct gcl_group *g, const struct gcl_bat
 			const uint64_t m = s.n, B = g->block;
 			if (hipSetDevice(D.dev) != hipSuccess)
 				return -ENODEV;
-			/* H2D of only the 64-B header granule of every slot (2D DMA) */
-			if (hb->stride == GCL_HDR_GRANULE)
-				he(hipMemcpyAsync(D.slab[si], s.frames, m * GCL_HDR_GRANULE, hipMemcpyHostToDevice, st));
-			else
-				he(hipMemcpy2DAsync(D.slab[si], GCL_HDR_GRANULE, s.frames, hb->stride,
-				                    GCL_HDR_GRANULE, m, hipMemcpyHostToDevice, st));
+			if (hb->offs) {
+				/* the block's offsets: mapped, or copied beside the side arrays */
+				const uint64_t *so = dof[i] ? dof[i] + b * B : (const uint64_t *)(D.side[si] + 13 * B);
+				if (!dof[i])
+					he(hipMemcpyAsync((void *)so, s.offs, m * 8, hipMemcpyHostToDevice, st));
+				if (gcl_header_gather(dfr[i], hb->frames_len, so, m, D.slab[si], st))
+					he(hipErrorLaunchFailure);
+			} else if (hb->stride == row) {
+				he(hipMemcpyAsync(D.slab[si], s.frames, m * row, hipMemcpyHostToDevice, st));
+			} else { /* H2D of each slot's header row (2D DMA) */
+				he(hipMemcpy2DAsync(D.slab[si], row, s.frames, hb->stride, row, m,
+				                    hipMemcpyHostToDevice, st));
+			}
 			gcl_batch db = {};
 			db.frames = D.slab[si];
-			db.frames_len = m * GCL_HDR_GRANULE;
-			db.stride = GCL_HDR_GRANULE;
+			db.frames_len = m * row;
+			db.stride = row;
 			db.n = m;
 			uint8_t *side = D.side[si];
 			if (s.olflags) {

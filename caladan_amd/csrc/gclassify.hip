@@ -1895,7 +1895,7 @@ __global__ void __launch_bounds__(256) access_probe_kernel(KParams k)
  * their chunk and the next lane's into one row chunk.  Bytes at or past
  * frames_len, and every byte of a frame whose offset is, read 0.
  */
-constexpr uint32_t kGatherRow = 80;
+constexpr uint32_t kGatherRow = GCL_GATHER_ROW;
 
 __device__ __forceinline__ uint32_t funnel(uint32_t lo, uint32_t hi, uint32_t b)
 {
@@ -2657,6 +2657,22 @@ extern "C" int gcl_classify(struct gcl_ctx *c, const struct gcl_batch *b,
 	return gcl_classify_ex(c, b, &o, hip_stream);
 }
 
+extern "C" int gcl_header_gather(const uint8_t *frames, uint64_t frames_len, const uint64_t *offs,
+                                 uint64_t n, uint8_t *rows, void *hip_stream)
+{
+	if (!n)
+		return 0;
+	if (!frames || !offs || !rows || frames_len == UINT64_MAX || n > (1ull << 40))
+		return -EINVAL;
+	int dev = 0, cus = 256;
+	if (hipGetDevice(&dev) == hipSuccess)
+		(void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+	const unsigned grid = (unsigned)std::min<uint64_t>((n + 31) / 32, (uint64_t)cus * 8);
+	hipLaunchKernelGGL(header_gather_kernel, dim3(grid), dim3(256), 0, (hipStream_t)hip_stream, frames,
+	                   frames_len, offs, n, rows);
+	return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
 extern "C" int gcl_access_probe(struct gcl_ctx *c, const struct gcl_batch *b, void *out,
                                 uint32_t vbytes, void *hip_stream)
 {
@@ -3291,10 +3307,8 @@ extern "C" int gcl_classify_host(struct gcl_ctx *c, const struct gcl_batch *hb,
 				const uint64_t *so = doffs ? doffs + s : (const uint64_t *)(e.side[i] + 13 * chunk);
 				if (!doffs)
 					he(hipMemcpyAsync((void *)so, hb->offs + s, m * 8, hipMemcpyHostToDevice, st));
-				const unsigned grid = (unsigned)std::min<uint64_t>((m + 31) / 32, (uint64_t)c->num_cus * 8);
-				hipLaunchKernelGGL(header_gather_kernel, dim3(grid), dim3(256), 0, st, dframes,
-				                   hb->frames_len, so, m, e.slab[i]);
-				he(hipGetLastError());
+				if (gcl_header_gather(dframes, hb->frames_len, so, m, e.slab[i], st))
+					he(hipErrorLaunchFailure);
 			} else {
 				/* H2D of each slot's header row (2D DMA) */
 				const uint8_t *src = hb->frames + s * hb->stride;

@@ -301,6 +301,22 @@ int gcl_classify_host(struct gcl_ctx *ctx, const struct gcl_batch *host_batch,
                       void *host_verdicts, uint64_t *host_counts,
                       uint64_t *host_stats, const struct gcl_e2e_opts *opts);
 
+/*
+ * gcl_header_gather - the COPY transport's gather step over per-packet
+ * offsets, as gcl_classify_host uses it (and gcl_group_classify_host, per
+ * GPU): on the current HIP device's @hip_stream, row i of @rows (device
+ * memory, @n x GCL_GATHER_ROW bytes) gets frame bytes [0, GCL_GATHER_ROW)
+ * of the frame at @frames + offs[i], bytes at or past @frames_len reading 0
+ * (offsets clamped as gcl_batch's).  @frames and @offs are device-visible
+ * pointers (a registered region's mapped address, or HBM).  The rows hold
+ * everything rx_one_pkt reads (ports end at byte 78 for IHL 15), so a
+ * classify over @rows with stride GCL_GATHER_ROW equals one over the
+ * frames.  Asynchronous; 0, -EINVAL or -EIO.
+ */
+#define GCL_GATHER_ROW 80
+int gcl_header_gather(const uint8_t *frames, uint64_t frames_len, const uint64_t *offs, uint64_t n,
+                      uint8_t *rows, void *hip_stream);
+
 /* Pin + map host memory for ZEROCOPY / async copies (hipHostRegister). */
 int gcl_host_register(void *p, size_t len);
 int gcl_host_unregister(void *p);

@@ -158,7 +158,8 @@ def test_gpu_group_classify_host_split(g, orc, mode, layout, nstreams):
     """One host batch split round-robin by the C splitter over two contexts:
     the verdicts land at their batch positions and equal the oracle's; the
     node-wide counts and counters equal the oracle's (NIC mode with ol_flags
-    and hash.rss, a ragged last block)."""
+    and hash.rss, a ragged last block).  COPY over per-packet offsets goes
+    through gcl_header_gather on each GPU, fixed slots through 2D DMA."""
     B = 4096
     n = 5 * B + 77
     rng = np.random.default_rng(3)
@@ -182,14 +183,6 @@ def test_gpu_group_classify_host_split(g, orc, mode, layout, nstreams):
     kw = dict(verdicts=hv, nstreams=nstreams, offs=None if offs is None else pinned(offs),
               olflags=pinned(olf), rss=pinned(rss),
               mode=g.E2E_ZEROCOPY if mode == "zerocopy" else g.E2E_COPY)
-    if mode == "copy" and layout == "offs":
-        # the header DMA-gather copies fixed-stride granules (one 2D DMA per
-        # block); descriptors at arbitrary offsets are refused, not gathered
-        with pytest.raises(OSError) as e:
-            grp.classify_host(pinned(frames), n, stride, **kw)
-        assert e.value.errno == 22
-        grp.close()
-        return
     grp.classify_host(pinned(frames), n, stride, **kw)
     grp.exchange()
     c, s, per = grp.read()
