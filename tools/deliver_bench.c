@@ -87,7 +87,7 @@ int main(int argc, char **argv)
 		x ^= x << 13, x ^= x >> 7, x ^= x << 17;
 		const uint32_t r = (uint32_t)(x % R);
 		v[i].uniqid = (uint16_t)r;
-		v[i].thread = (uint8_t)procs[r].flow_tbl[(x >> 32) % T];
+		v[i].thread = (uint8_t)((x >> 32) % T); /* the flow_tbl slot */
 		v[i].action = GCL_ACT_DELIVER;
 		len[i] = 60;
 		shm[i] = (uint64_t)i * 64;
