@@ -126,6 +126,7 @@ class GclRxloopCfg(ctypes.Structure):
 
 LOOP_INLINE_HDRS = 0x1
 LOOP_HDR_RECORDS = 0x2
+LOOP_STAMPS = 0x4
 
 
 class GclVerdict(ctypes.Structure):

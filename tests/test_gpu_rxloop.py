@@ -298,8 +298,8 @@ def test_rxloop_lifetime_and_errors(g):
         loop.stop()
         with pytest.raises(OSError):  # inline granules and header records exclude each other
             clf.rxloop(frames, flags=g.LOOP_INLINE_HDRS | g.LOOP_HDR_RECORDS)
-        with pytest.raises(OSError):  # unknown flag
-            clf.rxloop(frames, flags=0x4)
+        with pytest.raises(OSError):  # unknown flag (0x4 is GCL_LOOP_STAMPS)
+            clf.rxloop(frames, flags=0x8)
         lp2 = clf.rxloop(frames, slots=4)
         tk = lp2.submit(offs)
         lp2.wait(tk, 4)
