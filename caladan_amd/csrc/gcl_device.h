@@ -75,12 +75,17 @@ __device__ __forceinline__ uint4 load16_sys(const uint8_t *base, uint64_t len, u
 constexpr int kSysAux = 17;
 
 /* Buffer descriptor over host memory (< 4 GiB) the persistent loop reads or
- * writes; build it from wave-uniform values only. */
+ * writes; build it from wave-uniform values only.  The base and size go
+ * through readfirstlane, so the descriptor sits in scalar registers even where
+ * the compiler cannot prove them uniform (a loop variable, a value read from
+ * LDS): otherwise every buffer access gets a readfirstlane waterfall loop. */
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t host_rsrc(const void *p, uint64_t bytes)
 {
-	return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0,
-	                                         (int)(bytes < 0xFFFFFFFFull ? bytes : 0xFFFFFFFFull),
-	                                         0x00020000);
+	const uint64_t a = (uint64_t)(uintptr_t)p;
+	const uint64_t u = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32)) << 32 |
+	                   (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+	const int n = __builtin_amdgcn_readfirstlane((int)(bytes < 0xFFFFFFFFull ? bytes : 0xFFFFFFFFull));
+	return __builtin_amdgcn_make_buffer_rsrc((void *)(uintptr_t)u, 0, n, 0x00020000);
 }
 
 /* load16_sys as one 16-B (or two 8-B) system-scope buffer loads when the

@@ -438,8 +438,10 @@ struct HdrWords {
  * (classify_pair_kernel: headers in registers) reads from the frame instead.
  */
 /* VF: the verdict format when known at compile time (2: GCL_CFG_VERDICT2,
- * which excludes the transport pre-hash), 0: read from k.cflags */
-template <int MODE, bool GENERAL, bool SYS, bool REG, int VF = 0>
+ * which excludes the transport pre-hash), 0: read from k.cflags.  HIST false
+ * (rxloop64_kernel): no histogram add; @hist[tid] gets the packet's runtime
+ * (-1: none), which the loop's writer wave counts. */
+template <int MODE, bool GENERAL, bool SYS, bool REG, int VF = 0, bool HIST = true>
 __device__ __forceinline__ uint64_t classify_core(const KParams &k, const HdrWords &h,
                                                   const uint4 *tile, int tid, uint64_t idx,
                                                   const Tables &tb, uint32_t *hist, Counters &cnt,
@@ -574,9 +576,11 @@ __device__ __forceinline__ uint64_t classify_core(const KParams &k, const HdrWor
 			if (!re.active)
 				action |= GCL_ACT_WAKE;
 		}
-		if (!(ablate & 4))
+		if (HIST && !(ablate & 4))
 			atomicAdd(&hist[p], 1u);
 	}
+	if (!HIST)
+		hist[tid] = (uint32_t)p;
 	if (VF != 2 && k.trans) {
 		/* trans_lookup's hashes with runtime p's trans_seed
 		 * (transport.c:29-42, :366-375), for the packets net_rx_one passes
@@ -1209,14 +1213,14 @@ __host__ __device__ constexpr uint64_t loop_word(uint64_t t, uint32_t n, uint32_
 }
 static_assert(sizeof(LoopSlotHdr) == 64, "LoopSlotHdr");
 
-/* Offsets in a ring slot carry the slot's use count in their top 24 bits
+/* Offsets in a ring slot carry a stamp of the slot's use count in their top 24 bits
  * (offsets themselves are < 2^40: the ingress region is bounded at start).
  * An 8-B entry is written and read whole, so a lane that reads its entry
  * while polling knows by the stamp whether it holds this burst's offset or a
  * stale one: the offsets arrive with the poll that sees the burst, one PCIe
  * round trip sooner.  Entries past a burst's n keep older stamps; every
  * kLoopRefresh uses of a slot the host rewrites all of them, so no entry is
- * ever 2^24 uses stale and a stamp never aliases. */
+ * ever 2^23 uses stale (the stamp's period) and a stamp never aliases. */
 constexpr int kLoopStampShift = 40;
 constexpr uint64_t kLoopOffMask = (1ull << kLoopStampShift) - 1;
 constexpr uint64_t kLoopRefresh = 256;
@@ -1225,17 +1229,26 @@ constexpr uint64_t kLoopRefresh = 256;
 constexpr uint64_t kLoopSpecTicks = 400;
 /* GCL_TUNE_LOOP_CLOCK default: 0 polls on s_memrealtime, 1 on s_memtime */
 constexpr uint32_t kDefaultLoopClock = 0;
+/* GCL_TUNE_LOOP_WRITER default (rxloop64_kernel): 1 the writer wave stores
+ * the verdict records, 0 the poller does.  The handoff through the mailbox
+ * cost a lone 64-packet burst more (5.08 against 4.43 us p50 with stage
+ * stamps) than the poller's wait for its own stores' retirement costs a
+ * queued one (4 workers x 8: 78.5 against 79.7 Mpkt/s;
+ * profiles/r04_loop64_ab.jsonl) */
+constexpr uint32_t kDefaultLoopWriter = 0;
 /* how a worker's bursts arrived (gcl_rxloop_poll_stats): with the poll that
  * found the word; eligible for that, but an entry or record still stale so
  * read after it; or after the word, the speculative window over or the
  * burst too long for it */
 enum { kLoopPollEarly = 0, kLoopPollStale = 1, kLoopPollLate = 2 };
-/* never 0 (the use count runs 1 .. 2^24 - 1 and round again), so an entry
- * that was never loaded, or never written since the loop started, cannot pass
- * for a current one; host and device compute it the same way */
+/* never 0 (bit 23 of the stamp is always set, the slot's use count in bits
+ * 0-22), so an entry that was never loaded, or never written since the loop
+ * started, cannot pass for a current one; host and device compute it the same
+ * way.  Shifts and masks only (nslots is a power of two): the poller computes
+ * it per ticket. */
 __host__ __device__ constexpr uint64_t loop_stamp(uint64_t t, uint32_t nslots)
 {
-	return (((t - 1) / nslots) % 0xFFFFFFull + 1) << kLoopStampShift;
+	return ((((t - 1) >> __builtin_ctz(nslots)) & 0x7FFFFFull) | 0x800000ull) << kLoopStampShift;
 }
 
 struct LoopImgHdr {        /* first 64 B of a table image buffer */
@@ -1274,6 +1287,10 @@ struct LoopParams {
 	                              stamps' wrap), a multiple of nslots */
 	uint32_t stamps;           /* GCL_LOOP_STAMPS: per-burst stage times into the slot header */
 	uint32_t fast_clock;       /* poll on the shader clock (GCL_TUNE_LOOP_CLOCK) */
+	uint32_t rec_plane;        /* GCL_LOOP_HDR_RECORDS: bytes between the records' chunk
+	                              planes (chunk j of packet i at off_hdr + j * rec_plane + 16 i) */
+	uint32_t writer;           /* rxloop64_kernel: the writer wave stores the verdict
+	                              records (else the poller, GCL_TUNE_LOOP_WRITER=0) */
 };
 
 /* GCL_LOOP_HDR_RECORDS: the submitting core writes each packet as one 64-B
@@ -1287,10 +1304,25 @@ struct LoopParams {
  * (d4, total length and IP id, and the MAC addresses are never read.)  A burst
  * of <= 64 packets then arrives whole with the poll that finds its word: one
  * PCIe round trip per burst.  Ports past byte 43 (IHL >= 7) are read from the
- * frame at the record's offset. */
+ * frame at the record's offset.  The chunks lie in four planes (q_j of packet
+ * i at off_hdr + j * rec_plane + 16 i), so each of a poll's four loads reads
+ * 1 KiB contiguous across the wave: 64 PCIe read requests of 64 B for a
+ * 64-packet burst instead of 256 of 16 B with 64-B records. */
 __host__ __device__ constexpr uint32_t loop_rec_stamp(uint64_t t, uint32_t nslots)
 {
-	return (uint32_t)(((t - 1) / nslots) % 0xFFFFFFFFull + 1); /* never 0, as loop_stamp */
+	/* never 0, as loop_stamp: bit 31 set, the use count in bits 0-30 */
+	return (uint32_t)(((t - 1) >> __builtin_ctz(nslots)) & 0x7FFFFFFFull) | 0x80000000u;
+}
+
+/* the value lane 0 of the wave holds, in scalar registers: the poll's word
+ * and stop flag are loaded by lane 0 only, and a uniform broadcast keeps
+ * the loops they end uniform (a __shfl broadcast is an LDS round trip, and
+ * its VGPR result makes the compiler treat the slot address, and with it the
+ * buffer descriptors, as divergent: waterfall loops around every load) */
+__device__ __forceinline__ uint64_t lane0_u64(uint64_t v)
+{
+	return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32)) << 32 |
+	       (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
 }
 
 /* a record's four chunks -> the packet's tile row and side-array entries */
@@ -1436,7 +1468,7 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 #pragma unroll
 					for (int j = 0; j < 4; j++) {
 						const auto v = __builtin_amdgcn_raw_buffer_load_b128(
-						        srs, (int)(L.off_hdr + 64 * tid + 16 * j), 0, gcl::kSysAux);
+						        srs, (int)(L.off_hdr + L.rec_plane * j + 16 * tid), 0, gcl::kSysAux);
 						qv[j] = make_uint4(v[0], v[1], v[2], v[3]);
 					}
 				}
@@ -1447,8 +1479,8 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 					if ((k & 7) == 7) /* a stop waits for up to 8 polls */
 						sv = gcl::ld_sys32(L.stop);
 				}
-				wv = __shfl(wv, 0);
-				sv = __shfl(sv, 0);
+				wv = lane0_u64(wv);
+				sv = (uint32_t)__builtin_amdgcn_readfirstlane((int)sv);
 				if ((wv >> 24) == (t & ((1ull << 40) - 1))) {
 					w = wv;
 					e = ev;
@@ -1553,7 +1585,7 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 						r[j] = make_uint4(0, 0, 0, 0);
 					} else {
 						const auto v = __builtin_amdgcn_raw_buffer_load_b128(
-						        srs, (int)(L.off_hdr + 64 * (256 * c0 + tid) + 16 * j), 0, gcl::kSysAux);
+						        srs, (int)(L.off_hdr + L.rec_plane * j + 16 * (256 * c0 + tid)), 0, gcl::kSysAux);
 						r[j] = make_uint4(v[0], v[1], v[2], v[3]);
 					}
 				}
@@ -1674,6 +1706,370 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 		}
 		if (tid == 0)
 			gcl::st_sys32(&L.polls[4 * blockIdx.x + poll_kind], polls[poll_kind]);
+	}
+}
+
+/* ------------------------------------------------------------------------
+ * rxloop64_kernel: the loop at the reference's own burst size (<= 64 mbufs,
+ * IOKERNEL_RX_BURST_SIZE, defs.h:75), chosen by gcl_rxloop_start whenever
+ * max_burst <= 64.  A burst that size is one packet per lane of ONE wave, so
+ * the poller wave takes it from the poll to the verdicts alone, from
+ * registers, with no barrier: rxloop_kernel's three barriers and its LDS tile
+ * cost 0.7 us of a lone burst (GCL_LOOP_STAMPS, profiles/r04_stages_reentry.jsonl).
+ * A second wave (the writer) adds the counts and the counters (device
+ * atomics) and the poll counters, so their retirement never holds the
+ * poller's vmcnt.  It can also store the verdict records
+ * (GCL_TUNE_LOOP_WRITER=1): on gfx9 stores and loads share vmcnt, in order,
+ * and a store into host memory takes about a PCIe round trip to retire, so
+ * a poller that stores its own records consumes its next poll only after
+ * them; measured, the mailbox handoff costs a lone burst more than that wait
+ * costs a queued one, so the poller stores them (kDefaultLoopWriter).  The
+ * two waves hand bursts over through two LDS mailboxes, ordered by LDS-only
+ * fences (lgkmcnt, never vmcnt).
+ */
+struct Mbox64 {
+	uint4 rec[64];    /* verdict records {hash, verdict, ticket} (LoopRec) */
+	uint4 tr[64];     /* GCL_CFG_TRANS_HASH: {h5, h3, ticket} */
+	uint32_t p[64];   /* each packet's runtime (~0: none): the counts */
+	uint64_t t;       /* ticket */
+	uint32_t n, kind; /* packets; how the burst arrived (kLoopPollEarly ...) */
+	uint32_t cnt[4];  /* flowtag, hashmiss, unreg, unhandled */
+	uint32_t st[6];   /* GCL_LOOP_STAMPS: hit lo, hit hi, the hitting poll's round
+	                     trip, polls, hit -> packets in registers, hit -> posted */
+	uint32_t flag;    /* 1: posted by the poller, 0: free */
+	uint32_t pad;
+};
+static_assert(sizeof(Mbox64) % 16 == 0, "Mbox64");
+constexpr uint32_t kLoop64Lds = 2 * sizeof(Mbox64) + 64 * 8 + 2 * 64 * 4 + 64 * 8 + 16;
+
+/* rxloop64_kernel's writer wave: each posted burst's records (the transport
+ * hashes first: the host counts a burst complete only when both carry the
+ * ticket), its counts and counters, the poll counters, the stage stamps. */
+__device__ __forceinline__ void rxloop64_writer(const LoopParams &L, Mbox64 *mbox, const uint32_t *s_exit,
+                                             int lane)
+{
+	uint32_t pe = 0, ps = 0, pl = 0; /* bursts by how they arrived (no indexed array: scratch) */
+	for (uint32_t b = 0;; b ^= 1) {
+		Mbox64 &m = mbox[b];
+		for (;;) {
+			if (__hip_atomic_load(&m.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+				break;
+			if (__hip_atomic_load(s_exit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) &&
+			    !__hip_atomic_load(&m.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+				return;
+			__builtin_amdgcn_s_sleep(1);
+		}
+		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+		const uint64_t t_w = L.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
+		const uint64_t t = m.t;
+		const uint32_t n = m.n, kind = m.kind;
+		const __amdgpu_buffer_rsrc_t srs =
+		        gcl::host_rsrc(L.slots + ((t - 1) % L.nslots) * L.slot_bytes, L.slot_bytes);
+		if (L.writer && (uint32_t)lane < n) {
+			if (L.off_trans) {
+				const uint4 x = m.tr[lane];
+				const gcl::u32x4 v = {x.x, x.y, x.z, x.w};
+				__builtin_amdgcn_raw_buffer_store_b128(v, srs, (int)(L.off_trans + 16 * lane), 0,
+				                                       gcl::kSysAux);
+			}
+			const uint4 x = m.rec[lane];
+			const gcl::u32x4 v = {x.x, x.y, x.z, x.w};
+			__builtin_amdgcn_raw_buffer_store_b128(v, srs, (int)(L.off_verd + sizeof(LoopRec) * lane), 0,
+			                                       gcl::kSysAux);
+		}
+		const uint64_t t_s = L.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
+		const uint32_t p = m.p[lane];
+		if ((uint32_t)lane < n && p != ~0u && L.counts)
+			atomicAdd(&L.counts[p], 1ull);
+		uint32_t c[4] = {m.cnt[0], m.cnt[1], m.cnt[2], m.cnt[3]};
+		uint32_t st[6];
+		if (L.stamps)
+			for (int i = 0; i < 6; i++)
+				st[i] = m.st[i];
+		/* every LDS read of the mailbox is done: hand it back */
+		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+		if (lane == 0)
+			__hip_atomic_store(&m.flag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+		if (lane == 0) {
+			if (L.stats) {
+				if (c[0])
+					atomicAdd(&L.stats[GCL_RX_FLOW_TAG_MATCH], (unsigned long long)c[0]);
+				if (c[1])
+					atomicAdd(&L.stats[GCL_RX_HASH_MISSING], (unsigned long long)c[1]);
+				if (c[2])
+					atomicAdd(&L.stats[GCL_RX_UNREGISTERED_MAC], (unsigned long long)c[2]);
+				if (c[3])
+					atomicAdd(&L.stats[GCL_RX_UNHANDLED], (unsigned long long)c[3]);
+				atomicAdd(&L.stats[GCL_RX_PULLED], (unsigned long long)n);
+			}
+			pe += kind == kLoopPollEarly;
+			ps += kind == kLoopPollStale;
+			pl += kind == kLoopPollLate;
+			gcl::st_sys32(&L.polls[4 * blockIdx.x + kind],
+			              kind == kLoopPollEarly ? pe : kind == kLoopPollStale ? ps : pl);
+			if (L.stamps) {
+				/* {ticket, hit's round trip, hit -> posted, hit -> records issued}
+				 * {ticket, polls, hit lo, hi}
+				 * {ticket, hit -> packets in registers, hit -> posted, hit -> writer} */
+				const uint64_t hit = (uint64_t)st[1] << 32 | st[0];
+				const gcl::u32x4 a = {(uint32_t)t, st[2], st[5], (uint32_t)(t_s - hit)};
+				const gcl::u32x4 b2 = {(uint32_t)t, st[3], st[0], st[1]};
+				const gcl::u32x4 c3 = {(uint32_t)t, st[4], st[5], (uint32_t)(t_w - hit)};
+				__builtin_amdgcn_raw_buffer_store_b128(a, srs, 16, 0, gcl::kSysAux);
+				__builtin_amdgcn_raw_buffer_store_b128(b2, srs, 32, 0, gcl::kSysAux);
+				__builtin_amdgcn_raw_buffer_store_b128(c3, srs, 48, 0, gcl::kSysAux);
+			}
+		}
+	}
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
+{
+	extern __shared__ uint4 smem[];
+	Mbox64 *mbox = (Mbox64 *)smem;
+	uint64_t *s_offs = (uint64_t *)(mbox + 2);
+	uint32_t *s_fdir = (uint32_t *)(s_offs + 64), *s_hint = s_fdir + 64;
+	uint2 *s_trans = (uint2 *)(s_hint + 64);
+	uint32_t *s_exit = (uint32_t *)(s_trans + 64);
+	uint8_t *lds_tab = (uint8_t *)(s_exit + 4);
+	const int lane = threadIdx.x & 63;
+	if (threadIdx.x == 0) {
+		mbox[0].flag = 0;
+		mbox[1].flag = 0;
+		*s_exit = 0;
+	}
+	__syncthreads(); /* the only barrier */
+	if (threadIdx.x >= 64) {
+		rxloop64_writer(L, mbox, s_exit, lane);
+		return;
+	}
+	const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + L.lifetime_ticks;
+	const __amdgpu_buffer_rsrc_t frs = gcl::host_rsrc(L.frames, L.frames_len);
+	if (lane == 0 && blockIdx.x < 8) /* which XCD this worker runs on */
+		gcl::st_sys32(&L.where[blockIdx.x], __builtin_amdgcn_s_getreg((3 << 11) | 20) + 1);
+	KParams k = {};
+	k.frames = L.frames;
+	k.frames_len = L.frames_len;
+	k.max_rt = L.max_rt;
+	k.cflags = L.cflags; /* with thread_bits in [31:24] */
+	k.default_flags = L.default_flags;
+	k.offs = s_offs;
+	k.trans = L.off_trans ? s_trans : nullptr;
+	Tables tb = {};
+	uint32_t cur_seq = 0xFF; /* no image yet (versions are taken mod 64) */
+	uint32_t mb = 0;
+	const bool spec = L.spec, rec = L.hdr_rec;
+
+	for (uint64_t t = L.t0 + blockIdx.x + 1;; t += L.workers) {
+		uint8_t *slot = L.slots + ((t - 1) % L.nslots) * L.slot_bytes;
+		LoopSlotHdr *h = (LoopSlotHdr *)slot;
+		const __amdgpu_buffer_rsrc_t srs = gcl::host_rsrc(slot, L.slot_bytes);
+		/* the poll, as rxloop_kernel's: the slot word, and for the first
+		 * L.spec_ticks of a wait each lane's stamped offset or header record */
+		const uint64_t stamp = loop_stamp(t, L.nslots);
+		const uint32_t rstamp = loop_rec_stamp(t, L.nslots);
+		const uint64_t spec_end = __builtin_amdgcn_s_memrealtime() + L.spec_ticks;
+		uint64_t w = 0, e = 0;
+		bool sp_hit = false;
+		uint4 q[4] = {}, qv[4] = {};
+		uint64_t t_issue = 0, hit = 0;
+		uint32_t npoll = 0;
+		for (uint32_t kk = 0;; kk++) {
+			t_issue = __builtin_amdgcn_s_memrealtime();
+			npoll = kk + 1;
+			const bool sp = spec && t_issue < spec_end;
+			const uint64_t ev = sp && !rec ? gcl::ld_sys64(slot + L.off_offs + 8 * lane) : 0;
+			if (sp && rec) {
+#pragma unroll
+				for (int j = 0; j < 4; j++) {
+					const auto v = __builtin_amdgcn_raw_buffer_load_b128(
+					        srs, (int)(L.off_hdr + L.rec_plane * j + 16 * lane), 0, gcl::kSysAux);
+					qv[j] = make_uint4(v[0], v[1], v[2], v[3]);
+				}
+			}
+			uint64_t wv = 0;
+			uint32_t sv = 0;
+			if (lane == 0) {
+				wv = gcl::ld_sys64(&h->word);
+				if ((kk & 7) == 7) /* a stop waits for up to 8 polls */
+					sv = gcl::ld_sys32(L.stop);
+			}
+			wv = lane0_u64(wv);
+			sv = (uint32_t)__builtin_amdgcn_readfirstlane((int)sv);
+			if ((wv >> 24) == (t & ((1ull << 40) - 1))) {
+				w = wv;
+				e = ev;
+				sp_hit = sp;
+#pragma unroll
+				for (int j = 0; j < 4; j++)
+					q[j] = qv[j];
+				break;
+			}
+			if (sv || __builtin_amdgcn_s_memrealtime() > t_end)
+				break;
+			__builtin_amdgcn_s_sleep(1);
+		}
+		if (L.stamps)
+			hit = __builtin_amdgcn_s_memrealtime();
+		if (!w)
+			break; /* stopped, or the lifetime is over */
+		const uint32_t nw = (uint32_t)(w >> 11) & 0x1FFF, fl = (uint32_t)(w >> 7) & 0xF;
+		const uint32_t img = (uint32_t)(w >> 6) & 1, img_seq = (uint32_t)w & 63;
+		const bool live = (uint32_t)lane < nw;
+		const bool rok = sp_hit && q[0].x == rstamp && q[1].x == rstamp && q[2].x == rstamp &&
+		                 q[3].x == rstamp;
+		const bool fresh = !live || (rec ? rok : sp_hit && (e & ~kLoopOffMask) == stamp);
+		const bool early = spec && nw <= 64 && __all(fresh);
+		const uint32_t kind = early ? kLoopPollEarly : (sp_hit && nw <= 64) ? kLoopPollStale : kLoopPollLate;
+		if (img_seq != cur_seq) { /* a new table snapshot: this wave copies it into LDS */
+			const uint8_t *ib = L.img[img];
+			const uint32_t bytes = gcl::ld_sys32(ib);
+			const __amdgpu_buffer_rsrc_t irs = gcl::host_rsrc(ib, 64 + (uint64_t)bytes);
+			uint32_t *t32 = (uint32_t *)lds_tab;
+			for (uint32_t o = 16 * lane; o < bytes; o += 4 * 16 * 64) {
+				gcl::u32x4 x[4];
+#pragma unroll
+				for (int j = 0; j < 4; j++)
+					x[j] = __builtin_amdgcn_raw_buffer_load_b128(irs, (int)(64 + o + 1024 * j), 0,
+					                                            gcl::kSysAux);
+#pragma unroll
+				for (int j = 0; j < 4; j++)
+#pragma unroll
+					for (int d = 0; d < 4; d++)
+						if (o + 1024 * j + 4 * d < bytes)
+							t32[(o + 1024 * j) / 4 + d] = x[j][d];
+			}
+			k.ipt_mask = gcl::ld_sys32(ib + 4);
+			k.ipt_seed = gcl::ld_sys32(ib + 20);
+			tb.ipt = (const uint2 *)lds_tab;
+			tb.rtab = (const RtEntry *)(lds_tab + gcl::ld_sys32(ib + 8));
+			tb.flow = lds_tab + gcl::ld_sys32(ib + 12);
+			tb.toep = (const uint32_t *)(lds_tab + gcl::ld_sys32(ib + 16));
+			tb.seed = (const uint32_t *)(lds_tab + gcl::ld_sys32(ib + 24));
+			tb.crc = (const uint32_t *)(lds_tab + gcl::ld_sys32(ib + 28));
+			cur_seq = img_seq;
+		}
+		/* this lane's packet in registers: its header words and side fields */
+		HdrWords hw;
+		uint64_t off = 0;
+		uint32_t olf = 0, rss = 0, fdir = 0, hint = 0;
+		if (rec) {
+			if (!early && live) { /* the records after the word: a second round trip */
+#pragma unroll
+				for (int j = 0; j < 4; j++) {
+					const auto v = __builtin_amdgcn_raw_buffer_load_b128(
+					        srs, (int)(L.off_hdr + L.rec_plane * j + 16 * lane), 0, gcl::kSysAux);
+					q[j] = make_uint4(v[0], v[1], v[2], v[3]);
+				}
+			}
+			hw.d3 = q[0].y, hw.d5 = q[0].z, hw.d6 = q[0].w, hw.d7 = q[1].y;
+			hw.d8 = q[1].z, hw.d9 = q[1].w, hw.d10 = q[2].y;
+			off = (uint64_t)(q[3].z & 0xFF) << 32 | q[3].y;
+			olf = (q[3].z >> 8) & 0xFF;
+			rss = q[2].z;
+			fdir = q[2].w;
+			hint = q[3].w;
+		} else {
+			uint4 r[4] = {};
+			if (live) {
+				const uint64_t ent = early ? e : gcl::ld_sys64(slot + L.off_offs + 8 * lane);
+				if (fl & GCL_LOOP_F_OLF)
+					olf = (gcl::ld_sys32(slot + L.off_olf + (lane & ~3)) >> (8 * (lane & 3))) & 0xFF;
+				if (fl & GCL_LOOP_F_RSS)
+					rss = gcl::ld_sys32(slot + L.off_rss + 4 * lane);
+				if (fl & GCL_LOOP_F_FDIR)
+					fdir = gcl::ld_sys32(slot + L.off_fdir + 4 * lane);
+				if (fl & GCL_LOOP_F_HINT)
+					hint = gcl::ld_sys32(slot + L.off_hint + 4 * lane);
+				off = ent & kLoopOffMask;
+#pragma unroll
+				for (int j = 0; j < 4; j++) {
+					if (L.off_hdr) { /* granules inlined in the slot by the host */
+						const auto v = __builtin_amdgcn_raw_buffer_load_b128(
+						        srs, (int)(L.off_hdr + 64 * lane + 16 * j), 0, gcl::kSysAux);
+						r[j] = make_uint4(v[0], v[1], v[2], v[3]);
+					} else {
+						r[j] = gcl::load16_host(frs, L.frames, L.frames_len, off + 16 * (uint64_t)j);
+					}
+				}
+			}
+			hw.d3 = r[0].w, hw.d5 = r[1].y, hw.d6 = r[1].z, hw.d7 = r[1].w;
+			hw.d8 = r[2].x, hw.d9 = r[2].y, hw.d10 = r[2].z;
+		}
+		const uint64_t t_data = L.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
+		s_offs[lane] = off;
+		s_fdir[lane] = fdir;
+		s_hint[lane] = hint;
+		k.olflags = (fl & GCL_LOOP_F_OLF) ? (const uint8_t *)s_hint : nullptr; /* read via pre */
+		k.rss = (fl & GCL_LOOP_F_RSS) ? s_hint : nullptr;                      /* read via pre */
+		k.fdir = (fl & GCL_LOOP_F_FDIR) ? s_fdir : nullptr;
+		k.dst_hint = (fl & GCL_LOOP_F_HINT) ? s_hint : nullptr;
+		const uint32_t pre[2] = {olf, rss};
+		/* a free mailbox (the writer hands one back per burst) */
+		Mbox64 &m = mbox[mb];
+		while (__hip_atomic_load(&m.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+			__builtin_amdgcn_s_sleep(1);
+		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+		Counters cnt = {0, 0, 0, 0};
+		if (live) {
+			const uint64_t v = classify_core<MODE, true, true, true, 0, false>(
+			        k, hw, nullptr, lane, (uint64_t)lane, tb, m.p, cnt, 0, 64, pre);
+			const bool v4 = L.cflags & GCL_CFG_VERDICT4, v2 = L.cflags & GCL_CFG_VERDICT2;
+			const uint32_t hsh = v4 || v2 ? 0u : (uint32_t)v;
+			const uint32_t vlo = v2 ? (uint32_t)(uint16_t)v : v4 ? (uint32_t)v : (uint32_t)(v >> 32);
+			if (L.writer) {
+				m.rec[lane] = make_uint4(hsh, vlo, (uint32_t)t, (uint32_t)(t >> 32));
+				if (L.off_trans) {
+					const uint2 tr = s_trans[lane];
+					m.tr[lane] = make_uint4(tr.x, tr.y, (uint32_t)t, (uint32_t)(t >> 32));
+				}
+			} else { /* the records straight from the poller */
+				if (L.off_trans) {
+					const uint2 tr = s_trans[lane];
+					const gcl::u32x4 x = {tr.x, tr.y, (uint32_t)t, (uint32_t)(t >> 32)};
+					__builtin_amdgcn_raw_buffer_store_b128(x, srs, (int)(L.off_trans + 16 * lane), 0,
+					                                       gcl::kSysAux);
+				}
+				const gcl::u32x4 x = {hsh, vlo, (uint32_t)t, (uint32_t)(t >> 32)};
+				__builtin_amdgcn_raw_buffer_store_b128(x, srs, (int)(L.off_verd + sizeof(LoopRec) * lane),
+				                                       0, gcl::kSysAux);
+			}
+		}
+		/* one packet per lane: each counter is 0 or 1 per lane, a ballot
+		 * (no cross-lane shuffles, which are LDS round trips) */
+		const uint32_t c_ft = (uint32_t)__popcll(__ballot(cnt.flowtag != 0));
+		const uint32_t c_hm = (uint32_t)__popcll(__ballot(cnt.hashmiss != 0));
+		const uint32_t c_ur = (uint32_t)__popcll(__ballot(cnt.unreg != 0));
+		const uint32_t c_uh = (uint32_t)__popcll(__ballot(cnt.unhandled != 0));
+		if (lane == 0) {
+			m.t = t;
+			m.n = nw;
+			m.kind = kind;
+			m.cnt[0] = c_ft;
+			m.cnt[1] = c_hm;
+			m.cnt[2] = c_ur;
+			m.cnt[3] = c_uh;
+			if (L.stamps) {
+				m.st[0] = (uint32_t)hit;
+				m.st[1] = (uint32_t)(hit >> 32);
+				m.st[2] = (uint32_t)(hit - t_issue);
+				m.st[3] = npoll;
+				m.st[4] = (uint32_t)(t_data - hit);
+				m.st[5] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - hit);
+			}
+		}
+		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+		if (lane == 0)
+			__hip_atomic_store(&m.flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+		mb ^= 1;
+	}
+	/* the writer drains what was posted, then leaves; the host stops
+	 * publishing on this word (one it reads without a HIP call per burst) */
+	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+	if (lane == 0) {
+		__hip_atomic_store(s_exit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+		gcl::st_sys32(L.exited, 1);
 	}
 }
 
@@ -3505,17 +3901,24 @@ static int loop_write_image(gcl_rxloop *L, int i)
 	return 0;
 }
 
+/* bursts of <= 64 packets: rxloop64_kernel (2 waves, no barrier), unless
+ * GCL_TUNE_LOOP64=0 asks for the general loop (A/B) */
 template <int MODE>
-static hipError_t loop_launch(const LoopParams &lp, uint32_t lds, hipStream_t s)
+static hipError_t loop_launch(const LoopParams &lp, bool k64, hipStream_t s)
 {
+	const void *fn = k64 ? (const void *)rxloop64_kernel<MODE> : (const void *)rxloop_kernel<MODE>;
+	const uint32_t lds = k64 ? kLoop64Lds + kLdsTableBudget
+	                         : kLoopFixedLds + ((lp.max_rt + 3) & ~3u) * 4 + kLdsTableBudget;
 	if (lds > 64 * 1024) {
-		const hipError_t e = hipFuncSetAttribute((const void *)rxloop_kernel<MODE>,
-		                                         hipFuncAttributeMaxDynamicSharedMemorySize,
+		const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
 		                                         160 * 1024);
 		if (e != hipSuccess)
 			return e;
 	}
-	hipLaunchKernelGGL(rxloop_kernel<MODE>, dim3(lp.workers), dim3(256), lds, s, lp);
+	if (k64)
+		hipLaunchKernelGGL(rxloop64_kernel<MODE>, dim3(lp.workers), dim3(128), lds, s, lp);
+	else
+		hipLaunchKernelGGL(rxloop_kernel<MODE>, dim3(lp.workers), dim3(256), lds, s, lp);
 	return hipGetLastError();
 }
 
@@ -3566,10 +3969,14 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 	lp.hdr_rec = (cfg->flags & GCL_LOOP_HDR_RECORDS) != 0;
 	lp.stamps = (cfg->flags & GCL_LOOP_STAMPS) != 0;
 	lp.fast_clock = kDefaultLoopClock;
+	lp.writer = kDefaultLoopWriter;
+	if (const char *e = getenv("GCL_TUNE_LOOP_WRITER"))
+		lp.writer = atoi(e) != 0;
 	if (const char *e = getenv("GCL_TUNE_LOOP_CLOCK"))
 		lp.fast_clock = atoi(e) != 0;
 	lp.off_hdr = (cfg->flags & (GCL_LOOP_INLINE_HDRS | GCL_LOOP_HDR_RECORDS))
 	                     ? lp.off_verd + sizeof(LoopRec) * mb : 0;
+	lp.rec_plane = (uint32_t)(16 * mb);
 	lp.spec = (!lp.off_hdr || lp.hdr_rec) && cfg->max_burst <= 64;
 	lp.spec_ticks = kLoopSpecTicks;
 	if (const char *e = getenv("GCL_TUNE_LOOP_SPEC")) /* experiments: ticks of 10 ns */
@@ -3626,10 +4033,12 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 	if (hipStreamCreateWithFlags(&L->st, hipStreamNonBlocking) != hipSuccess)
 		goto fail;
 	{
-		const uint32_t lds = kLoopFixedLds + ((lp.max_rt + 3) & ~3u) * 4 + kLdsTableBudget;
-		hipError_t e = c->cfg.hash_mode == GCL_HASH_NIC ? loop_launch<GCL_HASH_NIC>(lp, lds, L->st)
-		             : c->cfg.hash_mode == GCL_HASH_JENKINS ? loop_launch<GCL_HASH_JENKINS>(lp, lds, L->st)
-		             : loop_launch<GCL_HASH_TOEPLITZ>(lp, lds, L->st);
+		bool k64 = cfg->max_burst <= 64;
+		if (const char *e = getenv("GCL_TUNE_LOOP64"))
+			k64 = k64 && atoi(e) != 0;
+		hipError_t e = c->cfg.hash_mode == GCL_HASH_NIC ? loop_launch<GCL_HASH_NIC>(lp, k64, L->st)
+		             : c->cfg.hash_mode == GCL_HASH_JENKINS ? loop_launch<GCL_HASH_JENKINS>(lp, k64, L->st)
+		             : loop_launch<GCL_HASH_TOEPLITZ>(lp, k64, L->st);
 		if (e != hipSuccess) {
 			(void)hipStreamDestroy(L->st);
 			L->st = nullptr;
@@ -3660,10 +4069,14 @@ static void loop_write_records(gcl_rxloop *L, uint64_t t, uint8_t *dst, uint32_t
                                const uint32_t *fdir_hi, const uint32_t *dst_hint)
 {
 	const uint32_t S = loop_rec_stamp(t, L->lp.nslots);
+	/* four planes of 16-B chunks, chunk j of packet i at j * plane + 16 i: a
+	 * poll's 64 lanes read each plane as one contiguous 1 KiB (16 64-B PCIe
+	 * reads a plane, not 64 16-B ones) */
+	const size_t P = L->lp.rec_plane / sizeof(u32x4_h);
 	volatile u32x4_h *q = (volatile u32x4_h *)dst;
 	/* (prefetching 6 ahead, or the record lines for ownership, measured
 	 * the same: profiles/r03_hdr_records_prefetch_ab.jsonl) */
-	for (uint32_t i = 0; i < n; i++, q += 4) {
+	for (uint32_t i = 0; i < n; i++, q++) {
 		if (i + 2 < n && offs[i + 2] < L->region_len)
 			__builtin_prefetch(L->region + offs[i + 2] + 12, 0, 3);
 		const uint64_t o = offs[i];
@@ -3684,18 +4097,18 @@ static void loop_write_records(gcl_rxloop *L, uint64_t t, uint8_t *dst, uint32_t
 		const uint32_t olf = olflags ? olflags[i] : 0;
 		const u32x4_h sv = {S, S, S, S};
 		const u32x4_h side = {S, 0, rss ? rss[i] : 0u, fdir_hi ? fdir_hi[i] : 0u};
-		q[0] = __builtin_shufflevector(v0, sv, 4, 0, 2, 3);   /* S d3 d5 d6 */
-		q[1] = __builtin_shufflevector(v1, sv, 4, 0, 1, 2);   /* S d7 d8 d9 */
-		q[2] = __builtin_shufflevector(side, v1, 0, 7, 2, 3); /* S d10 rss fdir */
-		q[3] = u32x4_h{S, (uint32_t)off, (uint32_t)(off >> 32) | olf << 8,
-		               dst_hint ? dst_hint[i] : 0u};
+		q[0] = __builtin_shufflevector(v0, sv, 4, 0, 2, 3);       /* S d3 d5 d6 */
+		q[P] = __builtin_shufflevector(v1, sv, 4, 0, 1, 2);       /* S d7 d8 d9 */
+		q[2 * P] = __builtin_shufflevector(side, v1, 0, 7, 2, 3); /* S d10 rss fdir */
+		q[3 * P] = u32x4_h{S, (uint32_t)off, (uint32_t)(off >> 32) | olf << 8,
+		                   dst_hint ? dst_hint[i] : 0u};
 	}
 	/* records past n keep older stamps; rewrite them now and then so that
-	 * none is ever 2^32 uses stale (loop_stamp's rule for the offsets) */
+	 * none is ever 2^31 uses stale (loop_stamp's rule for the offsets) */
 	if (((t - 1) / L->lp.nslots) % kLoopRefresh == kLoopRefresh - 1)
-		for (uint32_t i = n; i < L->max_burst; i++, q += 4)
+		for (uint32_t i = n; i < L->max_burst; i++, q++)
 			for (int j = 0; j < 4; j++)
-				q[j] = u32x4_h{S, 0, 0, 0};
+				q[j * P] = u32x4_h{S, 0, 0, 0};
 }
 
 /* Ticket @t's burst into slot @s as stamped offsets, the optional header

@@ -561,7 +561,8 @@ struct gcl_rxloop_cfg {
 /* gcl_rxloop_submit writes each packet as one 64-B header record in the
  * slot: the header words rx_one_pkt reads (frame bytes 12-15 and 20-43), its
  * offset and its side fields, every 16-B chunk led by the slot's use count
- * and written with one 16-B store.  A worker polling a burst of <= 64
+ * and written with one 16-B store (the four chunks of a record in four
+ * planes, so the GPU reads each plane contiguously).  A worker polling a burst of <= 64
  * packets reads the records with the slot word and, when every chunk carries
  * the current count, classifies at once: one PCIe round trip per burst
  * instead of two.  Ports past byte 43 (IHL >= 7) are read from the region.

@@ -48,9 +48,12 @@ LOOP_CASES = [(m, vb, 0, 0) for m in (0, 1, 2) for vb in (8, 4, 2)] + \
     [(m, vb, 0, 2) for m in (0, 1, 2) for vb in (8, 4, 2)] + [(0, 8, 1, 2), (2, 8, 2, 2)]
 
 
+@pytest.mark.parametrize("k64", [1, 0])
 @pytest.mark.parametrize("mode,vb,flags,inline", LOOP_CASES)
-def test_rxloop_fuzz_vs_oracle(g, orc, mode, vb, flags, inline, monkeypatch):
-    """vb: verdict bytes (8 gcl_verdict, 4 VERDICT4, 2 VERDICT2);
+def test_rxloop_fuzz_vs_oracle(g, orc, mode, vb, flags, inline, k64, monkeypatch):
+    """k64: bursts of <= 64 through rxloop64_kernel (the default for
+    max_burst <= 64), or through the general loop kernel (GCL_TUNE_LOOP64=0);
+    vb: verdict bytes (8 gcl_verdict, 4 VERDICT4, 2 VERDICT2);
     flags: 0 plain, 1 Azure ARP mode (GCL_CFG_AZURE_ARP), 2 16-bit hash;
     inline: 1 header granules copied into the ring slot (GCL_LOOP_INLINE_HDRS),
     2 stamped header records (GCL_LOOP_HDR_RECORDS), including the frames that
@@ -76,6 +79,7 @@ def test_rxloop_fuzz_vs_oracle(g, orc, mode, vb, flags, inline, monkeypatch):
     early = inline == 2 or (inline == 0 and mode == 0)
     if early:
         monkeypatch.setenv("GCL_TUNE_LOOP_SPEC", "500000")
+    monkeypatch.setenv("GCL_TUNE_LOOP64", str(k64))
     loop = clf.rxloop(frames, slots=8, counts=cnt, stats=st, region_len=flen,
                       flags=LOOP_FLAGS[inline](g))
     try:
@@ -364,11 +368,11 @@ def test_rxloop_transport_hashes(g, orc, mode, vb, lflag, monkeypatch):
     assert not len(bad), f"{len(bad)} transport hashes differ, first {bad[0]}: {gt[bad[0]]} vs {te[bad[0]]}"
 
 
-@pytest.mark.parametrize("lflag,spec,use0", [(0, "0", (1 << 24) - 150), (0, "500000", (1 << 24) - 150),
-                                             (2, "500000", (1 << 32) - 150), (2, "0", (1 << 32) - 150)])
+@pytest.mark.parametrize("lflag,spec,use0", [(0, "0", (1 << 23) - 150), (0, "500000", (1 << 23) - 150),
+                                             (2, "500000", (1 << 31) - 150), (2, "0", (1 << 31) - 150)])
 def test_rxloop_stamp_wrap(g, orc, lflag, spec, use0, monkeypatch):
-    """The slots' use count crossing the stamps' wrap (2^24 for stamped
-    offsets, 2^32 for header records) with the loop started near it
+    """The slots' use count crossing the stamps' wrap (2^23 for stamped
+    offsets, 2^31 for header records) with the loop started near it
     (GCL_TUNE_LOOP_T0): stamps are never 0, so a zeroed or never-loaded
     entry never passes for a current one, with the speculative window closed
     (spec 0: every burst read after its word) or wide open (every burst with
