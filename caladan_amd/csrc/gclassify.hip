@@ -1734,10 +1734,11 @@ struct Mbox64 {
 	uint64_t t;       /* ticket */
 	uint32_t n, kind; /* packets; how the burst arrived (kLoopPollEarly ...) */
 	uint32_t cnt[4];  /* flowtag, hashmiss, unreg, unhandled */
-	uint32_t st[6];   /* GCL_LOOP_STAMPS: hit lo, hit hi, the hitting poll's round
-	                     trip, polls, hit -> packets in registers, hit -> posted */
+	uint32_t st[8];   /* GCL_LOOP_STAMPS: hit lo, hit hi, the hitting poll's round
+	                     trip, polls, hit -> packets in registers, hit -> posted,
+	                     hit -> classified, hit -> records issued */
 	uint32_t flag;    /* 1: posted by the poller, 0: free */
-	uint32_t pad;
+	uint32_t pad[3];
 };
 static_assert(sizeof(Mbox64) % 16 == 0, "Mbox64");
 constexpr uint32_t kLoop64Lds = 2 * sizeof(Mbox64) + 64 * 8 + 2 * 64 * 4 + 64 * 8 + 16;
@@ -1782,9 +1783,9 @@ __device__ __forceinline__ void rxloop64_writer(const LoopParams &L, Mbox64 *mbo
 		if ((uint32_t)lane < n && p != ~0u && L.counts)
 			atomicAdd(&L.counts[p], 1ull);
 		uint32_t c[4] = {m.cnt[0], m.cnt[1], m.cnt[2], m.cnt[3]};
-		uint32_t st[6];
+		uint32_t st[8];
 		if (L.stamps)
-			for (int i = 0; i < 6; i++)
+			for (int i = 0; i < 8; i++)
 				st[i] = m.st[i];
 		/* every LDS read of the mailbox is done: hand it back */
 		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
@@ -1808,11 +1809,13 @@ __device__ __forceinline__ void rxloop64_writer(const LoopParams &L, Mbox64 *mbo
 			gcl::st_sys32(&L.polls[4 * blockIdx.x + kind],
 			              kind == kLoopPollEarly ? pe : kind == kLoopPollStale ? ps : pl);
 			if (L.stamps) {
-				/* {ticket, hit's round trip, hit -> posted, hit -> records issued}
+				/* {ticket, hit's round trip, hit -> classified, hit -> records
+				 *  issued (by the writer when L.writer)}
 				 * {ticket, polls, hit lo, hi}
 				 * {ticket, hit -> packets in registers, hit -> posted, hit -> writer} */
 				const uint64_t hit = (uint64_t)st[1] << 32 | st[0];
-				const gcl::u32x4 a = {(uint32_t)t, st[2], st[5], (uint32_t)(t_s - hit)};
+				const gcl::u32x4 a = {(uint32_t)t, st[2], st[6],
+				                      L.writer ? (uint32_t)(t_s - hit) : st[7]};
 				const gcl::u32x4 b2 = {(uint32_t)t, st[3], st[0], st[1]};
 				const gcl::u32x4 c3 = {(uint32_t)t, st[4], st[5], (uint32_t)(t_w - hit)};
 				__builtin_amdgcn_raw_buffer_store_b128(a, srs, 16, 0, gcl::kSysAux);
@@ -1865,8 +1868,18 @@ __global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
 		uint8_t *slot = L.slots + ((t - 1) % L.nslots) * L.slot_bytes;
 		LoopSlotHdr *h = (LoopSlotHdr *)slot;
 		const __amdgpu_buffer_rsrc_t srs = gcl::host_rsrc(slot, L.slot_bytes);
+		/* the mailbox this burst will be posted to, freed by the writer long
+		 * before (waited for here, not after the hit) */
+		Mbox64 &m = mbox[mb];
+		while (__hip_atomic_load(&m.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+			__builtin_amdgcn_s_sleep(1);
+		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 		/* the poll, as rxloop_kernel's: the slot word, and for the first
-		 * L.spec_ticks of a wait each lane's stamped offset or header record */
+		 * L.spec_ticks of a wait each lane's stamped offset or header record.
+		 * (Two polls in flight, so the slot is sampled twice per round trip,
+		 * measured slower: the lone burst 4.07 -> 4.35 us p50, 4 x 8 with
+		 * records 88 -> 72 Mpkt/s, offsets caught stale more often;
+		 * profiles/r04_loop64_ab.jsonl) */
 		const uint64_t stamp = loop_stamp(t, L.nslots);
 		const uint32_t rstamp = loop_rec_stamp(t, L.nslots);
 		const uint64_t spec_end = __builtin_amdgcn_s_memrealtime() + L.spec_ticks;
@@ -2006,15 +2019,13 @@ __global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
 		k.fdir = (fl & GCL_LOOP_F_FDIR) ? s_fdir : nullptr;
 		k.dst_hint = (fl & GCL_LOOP_F_HINT) ? s_hint : nullptr;
 		const uint32_t pre[2] = {olf, rss};
-		/* a free mailbox (the writer hands one back per burst) */
-		Mbox64 &m = mbox[mb];
-		while (__hip_atomic_load(&m.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
-			__builtin_amdgcn_s_sleep(1);
-		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 		Counters cnt = {0, 0, 0, 0};
+		uint64_t t_cls = 0, t_st = 0;
 		if (live) {
 			const uint64_t v = classify_core<MODE, true, true, true, 0, false>(
 			        k, hw, nullptr, lane, (uint64_t)lane, tb, m.p, cnt, 0, 64, pre);
+			if (L.stamps)
+				t_cls = __builtin_amdgcn_s_memrealtime();
 			const bool v4 = L.cflags & GCL_CFG_VERDICT4, v2 = L.cflags & GCL_CFG_VERDICT2;
 			const uint32_t hsh = v4 || v2 ? 0u : (uint32_t)v;
 			const uint32_t vlo = v2 ? (uint32_t)(uint16_t)v : v4 ? (uint32_t)v : (uint32_t)(v >> 32);
@@ -2034,6 +2045,8 @@ __global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
 				const gcl::u32x4 x = {hsh, vlo, (uint32_t)t, (uint32_t)(t >> 32)};
 				__builtin_amdgcn_raw_buffer_store_b128(x, srs, (int)(L.off_verd + sizeof(LoopRec) * lane),
 				                                       0, gcl::kSysAux);
+				if (L.stamps)
+					t_st = __builtin_amdgcn_s_memrealtime();
 			}
 		}
 		/* one packet per lane: each counter is 0 or 1 per lane, a ballot
@@ -2057,6 +2070,8 @@ __global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
 				m.st[3] = npoll;
 				m.st[4] = (uint32_t)(t_data - hit);
 				m.st[5] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - hit);
+				m.st[6] = (uint32_t)(t_cls - hit);
+				m.st[7] = (uint32_t)(t_st - hit);
 			}
 		}
 		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
@@ -3810,6 +3825,7 @@ struct gcl_rxloop {
 	uint64_t region_len;
 	bool ended;              /* the kernel has finished (hipStreamQuery) */
 	bool left;               /* some worker has left: submit no more */
+	bool k64;                /* rxloop64_kernel (bursts <= 64) */
 };
 
 static uint64_t now_ns()
@@ -4036,6 +4052,7 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 		bool k64 = cfg->max_burst <= 64;
 		if (const char *e = getenv("GCL_TUNE_LOOP64"))
 			k64 = k64 && atoi(e) != 0;
+		L->k64 = k64;
 		hipError_t e = c->cfg.hash_mode == GCL_HASH_NIC ? loop_launch<GCL_HASH_NIC>(lp, k64, L->st)
 		             : c->cfg.hash_mode == GCL_HASH_JENKINS ? loop_launch<GCL_HASH_JENKINS>(lp, k64, L->st)
 		             : loop_launch<GCL_HASH_TOEPLITZ>(lp, k64, L->st);
@@ -4322,9 +4339,9 @@ extern "C" int gcl_rxloop_stamps(struct gcl_rxloop *L, int64_t ticket, uint64_t 
 	out[1] = 10ull * __atomic_load_n(&h[6], __ATOMIC_RELAXED); /* hit -> classified */
 	out[2] = 10ull * __atomic_load_n(&h[7], __ATOMIC_RELAXED); /* hit -> last record issued */
 	out[3] = __atomic_load_n(&h[9], __ATOMIC_RELAXED);         /* polls of this wait */
-	for (int i = 0; i < 3; i++) /* hit -> past the loop's first three barriers */
+	for (int i = 0; i < 3; i++) /* hit -> past the first three barriers, or (loop64) stages */
 		out[4 + i] = 10ull * __atomic_load_n(&h[13 + i], __ATOMIC_RELAXED);
-	out[7] = 0;
+	out[7] = L->k64;
 	return 0;
 }
 

@@ -618,7 +618,10 @@ int gcl_rxloop_trans(struct gcl_rxloop *loop, int64_t ticket, struct gcl_trans *
  * the packets classified, @out[2] to the last verdict record's store issued,
  * @out[3] the polls of that wait, @out[4..6] from the return to past the
  * worker's first, second and third barriers (burst header shared, tables
- * and histogram ready, tile ready), @out[7] 0.  -EAGAIN until they land
+ * and histogram ready, tile ready), @out[7] 0; with the kernel for bursts of
+ * <= 64 (max_burst <= 64), @out[4..6] from the return to the packets in
+ * registers, the burst posted to the writer wave, the writer taking it,
+ * and @out[7] 1.  -EAGAIN until they land
  * (they are posted after the records), -ESTALE once the slot is reused,
  * -EINVAL without the flag. */
 int gcl_rxloop_stamps(struct gcl_rxloop *loop, int64_t ticket, uint64_t out[8]);

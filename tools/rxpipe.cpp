@@ -259,6 +259,7 @@ int main(int argc, char **argv)
 	if (stamps)
 		lc.flags |= GCL_LOOP_STAMPS;
 	std::vector<uint64_t> st_sub, st_seen, st_rtt, st_cls, st_store, st_polls, st_b1, st_b2, st_b3;
+	uint64_t st_kernel = 0; /* gcl_rxloop_stamps out[7]: 1 = the loop64 kernel */
 	struct gcl_rxloop *loop;
 	int ret = gcl_rxloop_start(ctx, &lc, &loop);
 	if (ret) {
@@ -354,6 +355,7 @@ int main(int argc, char **argv)
 				st_b1.push_back(g[4]);
 				st_b2.push_back(g[5]);
 				st_b3.push_back(g[6]);
+				st_kernel = g[7];
 			}
 			if (timed)
 				lat.push_back(d1 - t_sub[tail % depth]);
@@ -402,14 +404,19 @@ int main(int argc, char **argv)
 		};
 		const double sub = med(st_sub, false) * ns_tick, seen = med(st_seen, true) * ns_tick;
 		const double rtt = med(st_rtt, false), cls = med(st_cls, false), sto = med(st_store, false);
+		static const char *const b64[] = {"gpu_hit_to_data_in_registers", "gpu_hit_to_posted_to_writer",
+		                                  "gpu_hit_to_writer_start"};
+		static const char *const bar[] = {"gpu_hit_to_barrier1", "gpu_hit_to_barrier2", "gpu_hit_to_barrier3"};
+		const char *const *b = st_kernel ? b64 : bar;
 		printf("{\"lone_burst_stages_ns\": {\"host_submit\": %.0f, \"submit_to_records_seen\": %.0f, "
 		       "\"gpu_hit_poll_round_trip\": %.0f, \"gpu_hit_to_classified\": %.0f, "
 		       "\"gpu_hit_to_last_record_issued\": %.0f, \"polls_per_wait\": %.0f, "
-		       "\"residual_word_to_hit_plus_writeback\": %.0f, \"gpu_hit_to_barrier1\": %.0f, "
-		       "\"gpu_hit_to_barrier2\": %.0f, \"gpu_hit_to_barrier3\": %.0f}, \"burst\": %u, \"flags\": \"%s\"}\n",
-		       sub, seen, rtt, cls, sto, med(st_polls, false), seen - sub - sto, med(st_b1, false),
-		       med(st_b2, false), med(st_b3, false), burst,
-		       hdr_records ? "records" : inline_hdrs ? "inline" : "offsets");
+		       "\"residual_word_to_hit_plus_writeback\": %.0f, \"%s\": %.0f, "
+		       "\"%s\": %.0f, \"%s\": %.0f}, \"burst\": %u, \"flags\": \"%s\", \"kernel\": \"%s\"}\n",
+		       sub, seen, rtt, cls, sto, med(st_polls, false), seen - sub - sto, b[0], med(st_b1, false),
+		       b[1], med(st_b2, false), b[2], med(st_b3, false), burst,
+		       hdr_records ? "records" : inline_hdrs ? "inline" : "offsets",
+		       st_kernel ? "rxloop64" : "rxloop");
 	}
 	gcl_close(ctx);
 	CHECK(hipHostFree(region));
