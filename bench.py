@@ -52,30 +52,53 @@ WORKLOADS = {
               "1Mi mixed frames (70% IPv4 TCP/UDP 64..9014B, 20% IPv6, 10% ARP), 9216B slots, 16 runtimes"),
 }
 # algorithmic bytes per packet: one 64-B header granule read + one verdict
-# written, 8 B (gcl_verdict), 4 B (gcl_verdict4) or 2 B (the kthread-queue
-# verdict of GCL_CFG_VERDICT2) (DESIGN.md "Roofline"); tables and counters
-# amortise to ~0.
+# written, 8 B (gcl_verdict), 4 B (gcl_verdict4), 2 B or 1 B (the kthread-queue
+# verdicts of GCL_CFG_VERDICT2 / VERDICT1) (DESIGN.md "Roofline"); tables and
+# counters amortise to ~0.
 HDR_BYTES = 64
-# the bench default is the 2-byte queue verdict (GCL_CFG_VERDICT2): the flat
+# Through round 3 the bench default was the 2-byte queue verdict (GCL_CFG_VERDICT2): the flat
 # kthread-queue index q = uniqid << thread_bits | thread that the lrpc
 # post-pass (gcl_host_deliver2) indexes its rings with, a wake's flow_tbl
 # slot, or a tagged drop/broadcast action -- everything rx_send_pkt_to_runtime
 # needs.  It halves the write requests of the 4-byte form: 331 vs 342 us for
 # udp64 and 174 vs 180 us for tcp1500 on the same buffers
 # (profiles/archive/r02_defer_ab.jsonl).  The 4- and 8-byte forms stay as rows.
-VERDICT_BYTES = 2
-# the secondary (config 3, 1500-B TCP) line's verdict
+# Since round 4 the headline runs the 1-byte form (GCL_CFG_VERDICT1: the
+# same queue index in one byte, which 16 runtimes x 8 kthreads fit, WAKE left
+# to the post-pass's live active count): 330.7 vs 333.7-336.4 us, 101.3 vs
+# 99.6-100.4 Gpkt/s in alternating fresh processes (profiles/r04_verdict1_ab.jsonl).
+VERDICT_BYTES = 1
+# the secondary (config 3, 1500-B TCP) line's verdict: 1024 x 4 queues need 2 B
 SECONDARY_VERDICT_BYTES = 2
+# the integrated ingress rows (e2e.ingress_pool) keep the 2-byte form their
+# PMC passes were taken with (profiles/pmc_ingress_nic_v2.json)
+INGRESS_VERDICT_BYTES = 2
 VERDICT_NAMES = {8: "gcl_verdict, 8 B", 4: "gcl_verdict4, 4 B",
-                 2: "queue verdict (GCL_CFG_VERDICT2), 2 B"}
+                 2: "queue verdict (GCL_CFG_VERDICT2), 2 B",
+                 1: "queue verdict (GCL_CFG_VERDICT1), 1 B"}
 
 
 def verdict_cfg(vbytes, R, T):
     """(cfg flags, thread_bits) of a context writing @vbytes-byte verdicts
     for R runtimes of up to T kthreads."""
+    if vbytes == 1:
+        tb = g.thread_bits_for(R, T)
+        if tb is None or (R << tb) > g.V1_QUEUES:
+            raise ValueError(f"1-byte verdicts need R << thread_bits <= 128 ({R} x {T})")
+        return g.CFG_VERDICT1, tb
     if vbytes == 2:
         return g.CFG_VERDICT2, g.thread_bits_for(R, T)
     return (g.CFG_VERDICT4 if vbytes == 4 else 0), 0
+
+
+def fit_vbytes(vbytes, R, T):
+    """@vbytes, or the 2-byte queue verdict where the 1-byte one cannot name
+    every queue (1024 runtimes x 4 kthreads)."""
+    if vbytes == 1:
+        tb = g.thread_bits_for(R, T)
+        if tb is None or (R << tb) > g.V1_QUEUES:
+            return 2
+    return vbytes
 
 
 def classifier(device, R, T, vbytes, extra_flags=0, hash_mode=g.HASH_JENKINS):
@@ -149,7 +172,7 @@ def hip_copy(dst, src, nbytes):
 # pairs measured kernel/probe 0.97-1.02 with 2-byte verdicts and 1.01-1.06
 # with 4-byte ones, slow pairs 1.12 and 1.19 (profiles/archive/r02_pair_check.jsonl,
 # r02_bench_spread_settle.jsonl, gpurun_out/r02c, r02g)
-PLACEMENT_SLACK = {2: 1.07, 4: 1.10, 8: 1.10}
+PLACEMENT_SLACK = {1: 1.07, 2: 1.07, 4: 1.10, 8: 1.10}
 PLACEMENT_TRIES = 3
 # the slack above was calibrated on 16-runtime udp64 pairs only; with 1024
 # runtimes the kernel's time is not predicted by the probe's read+write
@@ -160,15 +183,20 @@ PLACEMENT_TRIES = 3
 # runtime count.  ACCESS_SLACK[vbytes] bounds it against the pair probe's
 # chosen time the way PLACEMENT_SLACK bounds the kernel.
 PLACEMENT_CHECK_RUNTIMES = (16,)
-ACCESS_SLACK = {2: 1.10, 4: 1.10, 8: 1.10}
+ACCESS_SLACK = {1: 1.10, 2: 1.10, 4: 1.10, 8: 1.10}
+# strided slots: the kernel within this of gcl_access_probe on the same pair
+# (tcp1500 measured 1.03: profiles/r04_bench.json, secondary.roofline)
+LAYOUT_SLACK = 1.10
 PROBE_READ_CAP = 4 << 30  # gcl_dev_alloc_paired's probe reads at most this much
 
 
 class Workload:
-    def __init__(self, name, rank, world, device, hash_mode=g.HASH_JENKINS, vbytes=VERDICT_BYTES,
+    def __init__(self, name, rank, world, device, hash_mode=g.HASH_JENKINS, vbytes=None,
                  n=None):
         wl, n_default, stride, R, T, desc = WORKLOADS[name]
         n = n_default if n is None else n
+        if vbytes is None:  # the bench default where it fits, else the 2-byte form
+            vbytes = fit_vbytes(VERDICT_BYTES, R, T)
         self.name, self.wl, self.n, self.stride, self.R, self.T, self.desc = name, wl, n, stride, R, T, desc
         self.vbytes = vbytes
         self.bytes_per_pkt = HDR_BYTES + vbytes
@@ -197,8 +225,11 @@ class Workload:
         self.clf = g.Classifier(device.index or 0, R, hash_mode, fl, thread_bits=tb)
         self.tables = setup_tables(self.clf, R, T)
         torch.cuda.synchronize()
-        if getattr(self, "paired", False) and stride == HDR_BYTES:
-            self.check_placement(access=R not in PLACEMENT_CHECK_RUNTIMES)
+        if getattr(self, "paired", False):
+            if stride == HDR_BYTES:
+                self.check_placement(access=R not in PLACEMENT_CHECK_RUNTIMES)
+            else:
+                self.check_layout()
 
     def _new_pool(self):
         buf = g.DeviceBuffer(self.n * self.stride, self.device.index or 0,
@@ -281,6 +312,21 @@ class Workload:
             old.free()
             self._fill(self.frames)
             torch.cuda.synchronize()
+
+    def check_layout(self):
+        """Strided slots (tcp1500's 1536 B): the pair probe that placed the
+        pool reads it densely, so its time does not predict a strided
+        launch's.  The check here is the kernel against gcl_access_probe --
+        the same strided header loads and verdict stores without the
+        classification -- on the same buffers: within LAYOUT_SLACK of it, the
+        launch runs at what its access pattern allows over this pair."""
+        ku, au = self.kernel_us(), self.access_us()
+        ok = ku <= au * LAYOUT_SLACK
+        self.placement_checks.append({"kernel_us": round(ku, 2), "access_probe_us": round(au, 2),
+                                      "checked_with": "classify kernel against gcl_access_probe "
+                                                      "(strided slots)",
+                                      "limit_us": round(au * LAYOUT_SLACK, 2), "passed": ok,
+                                      **({"kept": True} if ok else {"kept_failed": True})})
 
     def step(self, stream):
         self.clf.classify(self.frames, self.n, self.stride, verdicts=self.verdicts,
@@ -689,7 +735,7 @@ def e2e_bench(device, vbytes=VERDICT_BYTES, reps=3):
     out["rxloop"] = rxloop_bench(device, vbytes)
     out["rx_burst_pipeline"] = rxpipe_bench()
     out["mixed"]["trace_replay"] = trace_replay(device)
-    out["ingress_pool"] = ingress_pool_bench(device, vbytes)
+    out["ingress_pool"] = ingress_pool_bench(device, INGRESS_VERDICT_BYTES)
     return out
 
 
@@ -1228,9 +1274,10 @@ def main():
                     help="rehearsal only: let several ranks share a GPU")
     ap.add_argument("--exchange-every", type=int, default=EXCHANGE_EVERY,
                     help="steps per counts all_gather (multi-GPU exchange period)")
-    ap.add_argument("--verdict-bytes", type=int, default=VERDICT_BYTES, choices=[2, 4, 8],
+    ap.add_argument("--verdict-bytes", type=int, default=VERDICT_BYTES, choices=[1, 2, 4, 8],
                     help="8: struct gcl_verdict (with the hash); 4: struct gcl_verdict4; "
-                         "2: kthread-queue verdict (GCL_CFG_VERDICT2)")
+                         "2: kthread-queue verdict (GCL_CFG_VERDICT2); 1: the same in one "
+                         "byte (GCL_CFG_VERDICT1, <= 128 queues: config 2's 16 x 8)")
     ap.add_argument("--force-exchange", action="store_true",
                     help="run the multi-GPU step (RCCL all_gather on a side stream) even at N=1")
     args = ap.parse_args()
@@ -1333,7 +1380,7 @@ def main():
     if world == 1 and not args.no_secondary and args.workload == "udp64" and args.scaling == "weak":
         # the same udp64 step with the other verdict formats
         other = []
-        for ob in (b for b in (8, 4, 2) if b != vb):
+        for ob in (b for b in (8, 4, 2, 1) if b != vb):
             w4 = Workload(args.workload, rank, world, device, vbytes=ob)
             el4, gms4 = run_timed(w4, args.steps, 3, 1)
             other.append({"verdict": VERDICT_NAMES[ob],
@@ -1359,7 +1406,8 @@ def main():
         # config 3 leads with the 2-byte queue verdict (1024 runtimes x 4
         # kthreads fit thread_bits 2): 174 vs 180 us for the 4-byte one on
         # the same buffers (profiles/archive/r02_defer_ab.jsonl)
-        for vb2 in (SECONDARY_VERDICT_BYTES,) + tuple(b for b in (vb,) if b != SECONDARY_VERDICT_BYTES):
+        vbt = fit_vbytes(vb, *WORKLOADS["tcp1500"][3:5])
+        for vb2 in (SECONDARY_VERDICT_BYTES,) + tuple(b for b in (vbt,) if b != SECONDARY_VERDICT_BYTES):
             w2 = Workload("tcp1500", rank, world, device, vbytes=vb2)
             el2, gms2 = run_timed(w2, steps2, 3, 1)
             rf2 = roofline(w2, gms2)
@@ -1371,7 +1419,8 @@ def main():
                         "frame_bytes_rate_GBs": round(w2.n * 1500 / (gms2 * 1e-3) / 1e9, 1)}
             del w2
             torch.cuda.empty_cache()
-        w3 = Workload("tcp1500_hsplit", rank, world, device, vbytes=vb)
+        w3 = Workload("tcp1500_hsplit", rank, world, device,
+                      vbytes=fit_vbytes(vb, *WORKLOADS["tcp1500_hsplit"][3:5]))
         el3, gms3 = run_timed(w3, steps2, 2, 1)
         hsplit = {"workload": f"tcp1500_hsplit: {w3.desc}",
                   "value": round(w3.n * steps2 / el3 / 1e6, 1), "unit": "Mpkt/s",

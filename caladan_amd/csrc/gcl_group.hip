@@ -59,7 +59,7 @@ __global__ void __launch_bounds__(256) sum_rows_kernel(const unsigned long long 
 
 uint32_t verdict_size(uint32_t flags)
 {
-	return (flags & GCL_CFG_VERDICT2) ? 2 : (flags & GCL_CFG_VERDICT4) ? 4 : 8;
+	return (flags & GCL_CFG_VERDICT1) ? 1 : (flags & GCL_CFG_VERDICT2) ? 2 : (flags & GCL_CFG_VERDICT4) ? 4 : 8;
 }
 
 } // namespace

@@ -338,6 +338,22 @@ struct gcl_verdict4 gcl_verdict2_to4(uint16_t v, uint8_t thread_bits)
 	return o;
 }
 
+struct gcl_verdict4 gcl_verdict1_to4(uint8_t v, uint8_t thread_bits)
+{
+	struct gcl_verdict4 o;
+
+	if (!(v & GCL_V1_OTHER)) {
+		o.uniqid = (uint16_t)((v & GCL_V1_Q_MASK) >> thread_bits);
+		o.thread = (uint8_t)(v & ((1u << thread_bits) - 1));
+		o.action = GCL_ACT_DELIVER;
+	} else {
+		o.uniqid = GCL_NO_RUNTIME;
+		o.thread = GCL_NO_THREAD;
+		o.action = (uint8_t)(v & GCL_ACT_MASK);
+	}
+	return o;
+}
+
 /* deliver() for compact verdicts, with the common case inlined: a DELIVER
  * verdict for a runtime that still has an active kthread goes straight into
  * the ring of flow_tbl[slot] as it stands now (rx.c:55-59, then :76-92),
@@ -347,12 +363,13 @@ struct gcl_verdict4 gcl_verdict2_to4(uint16_t v, uint8_t thread_bits)
  * broadcast, drops, a full ring) takes deliver() for that one packet, in
  * order, so the outcome is the same packet by packet.  A write prefetch of
  * the ring slot 8-32 packets ahead made it slower (profiles/archive/r01_deliver.txt).
- * Verdicts are @v2 (2-byte, of a context with @thread_bits) or @v4; always
- * inlined with a constant @v2 == NULL or not. */
+ * Verdicts are @v2 (2-byte, of a context with @thread_bits), @v1 (1-byte) or
+ * @v4; always inlined with constant NULLs for the two absent forms. */
 static inline __attribute__((always_inline)) uint64_t
 deliver_compact(struct gcl_host_proc *const *clients_by_id, uint32_t max_runtimes,
                 struct gcl_host_proc *const *clients, int nr_clients,
-                const struct gcl_verdict4 *v4, const uint16_t *v2, uint8_t thread_bits,
+                const struct gcl_verdict4 *v4, const uint16_t *v2, const uint8_t *v1,
+                uint8_t thread_bits,
                 const uint32_t *bcast_hash, const uint16_t *pkt_len, const uint8_t *olflags,
                 uint8_t default_olflags, const uint64_t *shmptr, uint64_t n,
                 const struct gcl_host_ops *ops, uint64_t *stats, size_t vstride)
@@ -373,9 +390,15 @@ deliver_compact(struct gcl_host_proc *const *clients_by_id, uint32_t max_runtime
 		/* verdict i sits @vstride bytes after verdict i - 1: packed
 		 * arrays, or the rx loop's 16-B records read in place */
 		const uint16_t *v2i = v2 ? (const uint16_t *)((const char *)v2 + i * vstride) : NULL;
+		const uint8_t *v1i = v1 ? (const uint8_t *)v1 + i * vstride : NULL;
 		const struct gcl_verdict4 *v4i =
 			v4 ? (const struct gcl_verdict4 *)((const char *)v4 + i * vstride) : NULL;
-		if (v2) {
+		if (v1) { /* no WAKE mark: the active count below decides, as rx.c:59 */
+			const uint8_t x = *v1i;
+			uniqid = (x & GCL_V1_Q_MASK) >> thread_bits;
+			slot = x & tmask;
+			fast = !(x & GCL_V1_OTHER);
+		} else if (v2) {
 			const uint16_t x = *v2i;
 			uniqid = (x & GCL_V2_Q_MASK) >> thread_bits;
 			slot = x & tmask;
@@ -390,7 +413,8 @@ deliver_compact(struct gcl_host_proc *const *clients_by_id, uint32_t max_runtime
 		    slot >= p->thread_count || p->active_thread_count == 0 ||
 		    (th = p->flow_tbl[slot]) >= p->thread_count || !(chan = p->rxq[th]) ||
 		    chan->send_head - chan->send_tail >= chan->size) {
-			const struct gcl_verdict4 w = v2 ? gcl_verdict2_to4(*v2i, thread_bits) : *v4i;
+			const struct gcl_verdict4 w = v1 ? gcl_verdict1_to4(*v1i, thread_bits)
+			                            : v2 ? gcl_verdict2_to4(*v2i, thread_bits) : *v4i;
 			delivered += deliver(clients_by_id, max_runtimes, clients, nr_clients, NULL, &w,
 			                     bcast_hash ? bcast_hash + i : NULL, pkt_len ? pkt_len + i : NULL,
 			                     olflags ? olflags + i : NULL, default_olflags,
@@ -421,7 +445,7 @@ uint64_t gcl_host_deliver4(struct gcl_host_proc *const *clients_by_id, uint32_t 
                            uint8_t default_olflags, const uint64_t *shmptr, uint64_t n,
                            const struct gcl_host_ops *ops, uint64_t *stats)
 {
-	return deliver_compact(clients_by_id, max_runtimes, clients, nr_clients, v, NULL, 0,
+	return deliver_compact(clients_by_id, max_runtimes, clients, nr_clients, v, NULL, NULL, 0,
 	                       bcast_hash, pkt_len, olflags, default_olflags, shmptr, n, ops, stats,
 	                       sizeof(*v));
 }
@@ -435,7 +459,21 @@ uint64_t gcl_host_deliver2(struct gcl_host_proc *const *clients_by_id, uint32_t 
 {
 	if (thread_bits > 8 || !v)
 		return 0;
-	return deliver_compact(clients_by_id, max_runtimes, clients, nr_clients, NULL, v,
+	return deliver_compact(clients_by_id, max_runtimes, clients, nr_clients, NULL, v, NULL,
+	                       thread_bits, bcast_hash, pkt_len, olflags, default_olflags, shmptr,
+	                       n, ops, stats, sizeof(*v));
+}
+
+uint64_t gcl_host_deliver1(struct gcl_host_proc *const *clients_by_id, uint32_t max_runtimes,
+                           struct gcl_host_proc *const *clients, int nr_clients,
+                           const uint8_t *v, uint8_t thread_bits, const uint32_t *bcast_hash,
+                           const uint16_t *pkt_len, const uint8_t *olflags,
+                           uint8_t default_olflags, const uint64_t *shmptr, uint64_t n,
+                           const struct gcl_host_ops *ops, uint64_t *stats)
+{
+	if (thread_bits > 7 || !v)
+		return 0;
+	return deliver_compact(clients_by_id, max_runtimes, clients, nr_clients, NULL, NULL, v,
 	                       thread_bits, bcast_hash, pkt_len, olflags, default_olflags, shmptr,
 	                       n, ops, stats, sizeof(*v));
 }
@@ -454,14 +492,21 @@ uint64_t gcl_host_deliver_recs(struct gcl_host_proc *const *clients_by_id, uint3
 		return 0;
 	if (vbytes == 4)
 		return deliver_compact(clients_by_id, max_runtimes, clients, nr_clients,
-		                       (const struct gcl_verdict4 *)&recs[0].verdict, NULL, 0, bcast_hash,
-		                       pkt_len, olflags, default_olflags, shmptr, n, ops, stats,
+		                       (const struct gcl_verdict4 *)&recs[0].verdict, NULL, NULL, 0,
+		                       bcast_hash, pkt_len, olflags, default_olflags, shmptr, n, ops, stats,
 		                       sizeof(*recs));
 	if (vbytes == 2)
 		return deliver_compact(clients_by_id, max_runtimes, clients, nr_clients, NULL,
-		                       (const uint16_t *)&recs[0].verdict, thread_bits, bcast_hash,
+		                       (const uint16_t *)&recs[0].verdict, NULL, thread_bits, bcast_hash,
 		                       pkt_len, olflags, default_olflags, shmptr, n, ops, stats,
 		                       sizeof(*recs));
+	if (vbytes == 1)
+		return thread_bits > 7 ? 0
+		                       : deliver_compact(clients_by_id, max_runtimes, clients, nr_clients,
+		                                         NULL, NULL, (const uint8_t *)&recs[0].verdict,
+		                                         thread_bits, bcast_hash, pkt_len, olflags,
+		                                         default_olflags, shmptr, n, ops, stats,
+		                                         sizeof(*recs));
 	if (vbytes != 8)
 		return 0;
 	/* 8-byte contexts: a record's first 8 bytes are the struct gcl_verdict */

@@ -111,7 +111,8 @@ struct KParams {
 	 * classification (the membench tile body), 64 no counter flush, 128 no
 	 * rx_one_pkt in classify_pair_kernel (the register loop alone), 256
 	 * dummy loads on one shared address (side_dummy), 512 no verdict
-	 * stores (classify_pair_kernel) */
+	 * stores (classify_pair_kernel), 1024 1-byte stores of the 2-byte
+	 * verdict's low half (classify_kernel) */
 	uint32_t ablate;
 	uint2 *trans;    /* struct gcl_trans[n] or NULL */
 	uint32_t off_seed, off_crc;
@@ -600,6 +601,12 @@ __device__ __forceinline__ uint64_t classify_core(const KParams &k, const HdrWor
 		k.trans[idx] = tr;
 	}
 	const uint32_t vlo = uniq | thr << 16 | action << 24;
+	if (VF == 0 && (k.cflags & GCL_CFG_VERDICT1)) {
+		/* q = uniqid << thread_bits | slot; no WAKE mark (gclassify.h) */
+		const uint32_t a = action & GCL_ACT_MASK;
+		const uint32_t q = uniq << (k.cflags >> 24) | thr;
+		return a == GCL_ACT_DELIVER || a == GCL_ACT_WAKE ? q : GCL_V1_OTHER | a;
+	}
 	if (VF == 2 || (VF == 0 && (k.cflags & GCL_CFG_VERDICT2))) {
 		/* q = uniqid << thread_bits | thread (thread_bits in cflags[31:24]) */
 		const uint32_t a = action & GCL_ACT_MASK;
@@ -661,8 +668,17 @@ __device__ __forceinline__ void put_verdict_vf(const KParams &k, uint64_t idx, u
 
 __device__ __forceinline__ void put_verdict(const KParams &k, uint64_t idx, uint64_t w)
 {
-	if (k.cflags & GCL_CFG_VERDICT2) {
-		if (k.nt_store == 2)
+	if (k.cflags & GCL_CFG_VERDICT1) {
+		if (k.nt_store == 2) /* write-through (sc0 sc1), kDefaultVerdictStore */
+			__hip_atomic_store((uint8_t *)k.verdicts + idx, (uint8_t)w, __ATOMIC_RELAXED,
+			                   __HIP_MEMORY_SCOPE_SYSTEM);
+		else
+			((uint8_t *)k.verdicts)[idx] = (uint8_t)w;
+	} else if (k.cflags & GCL_CFG_VERDICT2) {
+		if (k.ablate & 1024) /* timing only: a 1-byte verdict store */
+			__hip_atomic_store((uint8_t *)k.verdicts + idx, (uint8_t)w, __ATOMIC_RELAXED,
+			                   __HIP_MEMORY_SCOPE_SYSTEM);
+		else if (k.nt_store == 2)
 			__hip_atomic_store((uint16_t *)k.verdicts + idx, (uint16_t)w, __ATOMIC_RELAXED,
 			                   __HIP_MEMORY_SCOPE_SYSTEM);
 		else
@@ -1651,8 +1667,10 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 				            classify_one<MODE, true, true>(k, tile, tid, (uint64_t)tid, tb, hist, cnt,
 				                                           rec ? kSpanRec : kSpanFull));
 				const bool v4 = L.cflags & GCL_CFG_VERDICT4, v2 = L.cflags & GCL_CFG_VERDICT2;
-				const uint32_t hsh = v4 || v2 ? 0u : s_verd[tid].x;
-				const uint32_t vlo = v2 ? ((const uint16_t *)s_verd)[tid]
+				const bool v1 = L.cflags & GCL_CFG_VERDICT1;
+				const uint32_t hsh = v4 || v2 || v1 ? 0u : s_verd[tid].x;
+				const uint32_t vlo = v1 ? ((const uint8_t *)s_verd)[tid]
+				                   : v2 ? ((const uint16_t *)s_verd)[tid]
 				                   : v4 ? ((const uint32_t *)s_verd)[tid] : s_verd[tid].y;
 				if (L.off_trans) { /* before the record: the host checks both tickets */
 					const gcl::u32x4 tr = {s_trans[tid].x, s_trans[tid].y, (uint32_t)t, (uint32_t)(t >> 32)};
@@ -2027,8 +2045,10 @@ __global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
 			if (L.stamps)
 				t_cls = __builtin_amdgcn_s_memrealtime();
 			const bool v4 = L.cflags & GCL_CFG_VERDICT4, v2 = L.cflags & GCL_CFG_VERDICT2;
-			const uint32_t hsh = v4 || v2 ? 0u : (uint32_t)v;
-			const uint32_t vlo = v2 ? (uint32_t)(uint16_t)v : v4 ? (uint32_t)v : (uint32_t)(v >> 32);
+			const bool v1 = L.cflags & GCL_CFG_VERDICT1;
+			const uint32_t hsh = v4 || v2 || v1 ? 0u : (uint32_t)v;
+			const uint32_t vlo = v1 ? (uint32_t)(uint8_t)v : v2 ? (uint32_t)(uint16_t)v
+			                   : v4 ? (uint32_t)v : (uint32_t)(v >> 32);
 			if (L.writer) {
 				m.rec[lane] = make_uint4(hsh, vlo, (uint32_t)t, (uint32_t)(t >> 32));
 				if (L.off_trans) {
@@ -2278,7 +2298,10 @@ __global__ void __launch_bounds__(256) access_probe_kernel(KParams k)
 			const uint32_t x = v[u].x ^ v[u].y ^ v[u].z ^ v[u].w ^ w[u].x ^ side[u];
 			acc ^= x ^ w[u].y ^ w[u].z ^ w[u].w;
 			if (p < k.n) {
-				if (VB == 2)
+				if (VB == 1)
+					__hip_atomic_store((uint8_t *)k.verdicts + p, (uint8_t)x, __ATOMIC_RELAXED,
+					                   __HIP_MEMORY_SCOPE_SYSTEM);
+				else if (VB == 2)
 					__hip_atomic_store((uint16_t *)k.verdicts + p, (uint16_t)x, __ATOMIC_RELAXED,
 					                   __HIP_MEMORY_SCOPE_SYSTEM);
 				else if (VB == 4)
@@ -2460,8 +2483,12 @@ extern "C" int gcl_open(int hip_device, const struct gcl_cfg *cfg, struct gcl_ct
 	    cfg->hash_mode > GCL_HASH_TOEPLITZ)
 		return -EINVAL;
 	if ((cfg->flags & GCL_CFG_VERDICT2) &&
-	    ((cfg->flags & (GCL_CFG_VERDICT4 | GCL_CFG_TRANS_HASH)) || cfg->thread_bits > 8 ||
-	     ((uint64_t)cfg->max_runtimes << cfg->thread_bits) > GCL_V2_QUEUES))
+	    ((cfg->flags & (GCL_CFG_VERDICT4 | GCL_CFG_TRANS_HASH | GCL_CFG_VERDICT1)) ||
+	     cfg->thread_bits > 8 || ((uint64_t)cfg->max_runtimes << cfg->thread_bits) > GCL_V2_QUEUES))
+		return -EINVAL;
+	if ((cfg->flags & GCL_CFG_VERDICT1) &&
+	    ((cfg->flags & (GCL_CFG_VERDICT4 | GCL_CFG_TRANS_HASH)) || cfg->thread_bits > 7 ||
+	     ((uint64_t)cfg->max_runtimes << cfg->thread_bits) > GCL_V1_QUEUES))
 		return -EINVAL;
 	if (hipGetDeviceCount(&ndev) != hipSuccess || hip_device < 0 || hip_device >= ndev)
 		return -ENODEV;
@@ -2612,7 +2639,7 @@ extern "C" int gcl_runtime_set(struct gcl_ctx *c, uint16_t uniqid, uint32_t ip_h
 	if (!c || uniqid >= c->cfg.max_runtimes || thread_count == 0 ||
 	    thread_count > GCL_NCPU || active_count > thread_count)
 		return -EINVAL;
-	if ((c->cfg.flags & GCL_CFG_VERDICT2) && thread_count > (1u << c->cfg.thread_bits))
+	if ((c->cfg.flags & (GCL_CFG_VERDICT2 | GCL_CFG_VERDICT1)) && thread_count > (1u << c->cfg.thread_bits))
 		return -EINVAL; /* its queues would not fit the 2-byte verdict */
 	if (active_count) {
 		if (!flow_tbl)
@@ -2999,7 +3026,8 @@ static int image_used(gcl_ctx *c, hipStream_t s)
 
 static uint32_t verdict_bytes(const gcl_ctx *c)
 {
-	return (c->cfg.flags & GCL_CFG_VERDICT2) ? 2 : (c->cfg.flags & GCL_CFG_VERDICT4) ? 4 : 8;
+	return (c->cfg.flags & GCL_CFG_VERDICT1) ? 1 : (c->cfg.flags & GCL_CFG_VERDICT2) ? 2
+	     : (c->cfg.flags & GCL_CFG_VERDICT4) ? 4 : 8;
 }
 
 /* the kernels' cflags: cfg.flags with thread_bits in [31:24] */
@@ -3087,7 +3115,7 @@ extern "C" int gcl_header_gather(const uint8_t *frames, uint64_t frames_len, con
 extern "C" int gcl_access_probe(struct gcl_ctx *c, const struct gcl_batch *b, void *out,
                                 uint32_t vbytes, void *hip_stream)
 {
-	if (!c || !b || !out || (vbytes != 2 && vbytes != 4 && vbytes != 8))
+	if (!c || !b || !out || (vbytes != 1 && vbytes != 2 && vbytes != 4 && vbytes != 8))
 		return -EINVAL;
 	if (b->n == 0)
 		return 0;
@@ -3108,7 +3136,9 @@ extern "C" int gcl_access_probe(struct gcl_ctx *c, const struct gcl_batch *b, vo
 	const uint64_t need = (b->n + 255) / 256;
 	const unsigned grid = (unsigned)std::min<uint64_t>((uint64_t)c->num_cus * 8, need);
 	hipStream_t s = (hipStream_t)hip_stream;
-	if (vbytes == 2)
+	if (vbytes == 1)
+		hipLaunchKernelGGL(access_probe_kernel<1>, dim3(grid), dim3(256), 0, s, k);
+	else if (vbytes == 2)
 		hipLaunchKernelGGL(access_probe_kernel<2>, dim3(grid), dim3(256), 0, s, k);
 	else if (vbytes == 4)
 		hipLaunchKernelGGL(access_probe_kernel<4>, dim3(grid), dim3(256), 0, s, k);
@@ -3377,7 +3407,12 @@ __global__ void __launch_bounds__(256) pair_probe_kernel(const uint8_t *rd, uint
 		const uint32_t v = a.x ^ a.w ^ b.y ^ b.z;
 		const uint64_t i = (t % wtiles) * 256 + p;
 		/* WT: the classify kernel's default verdict store (kDefaultVerdictStore) */
-		if (VB == 2) {
+		if (VB == 1) {
+			if (WT)
+				__hip_atomic_store(wr + i, (uint8_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+			else
+				wr[i] = (uint8_t)v;
+		} else if (VB == 2) {
 			if (WT)
 				__hip_atomic_store((uint16_t *)wr + i, (uint16_t)v, __ATOMIC_RELAXED,
 				                   __HIP_MEMORY_SCOPE_SYSTEM);
@@ -3423,7 +3458,11 @@ double pair_probe(const uint8_t *rd, size_t rd_bytes, uint8_t *wr, size_t wr_byt
 	auto launch = [&]() {
 		const dim3 g(cus * 4), b(256);
 #define GCL_PROBE(W, V) hipLaunchKernelGGL((pair_probe_kernel<W, V>), g, b, 0, s, rd, ntiles, wr, wtiles)
-		if (vb == 2 && wt)
+		if (vb == 1 && wt)
+			GCL_PROBE(true, 1);
+		else if (vb == 1)
+			GCL_PROBE(false, 1);
+		else if (vb == 2 && wt)
 			GCL_PROBE(true, 2);
 		else if (vb == 2)
 			GCL_PROBE(false, 2);
@@ -3474,7 +3513,7 @@ extern "C" int gcl_dev_alloc_paired(int hip_device, size_t bytes, const void *pa
 	const bool new_reads = dir == GCL_PAIR_NEW_READS;
 	if (!out || !bytes || !partner || !partner_bytes ||
 	    (dir != GCL_PAIR_NEW_READS && dir != GCL_PAIR_NEW_WRITES) ||
-	    (vb != 2 && vb != 4 && vb != 8) || (flags >> 16))
+	    (vb != 1 && vb != 2 && vb != 4 && vb != 8) || (flags >> 16))
 		return -EINVAL;
 	const size_t rd_bytes = new_reads ? bytes : partner_bytes;
 	const size_t wr_bytes = new_reads ? partner_bytes : bytes;
@@ -4286,7 +4325,10 @@ extern "C" int gcl_rxloop_wait(struct gcl_rxloop *L, int64_t ticket, void *verdi
 	if (verdicts_out) {
 		const uint32_t n = (uint32_t)(h->word >> 11) & 0x1FFF;
 		const LoopRec *r = loop_recs(L, h);
-		if (L->vbytes == 2) {
+		if (L->vbytes == 1) {
+			for (uint32_t i = 0; i < n; i++)
+				((uint8_t *)verdicts_out)[i] = (uint8_t)r[i].vlo;
+		} else if (L->vbytes == 2) {
 			for (uint32_t i = 0; i < n; i++)
 				((uint16_t *)verdicts_out)[i] = (uint16_t)r[i].vlo;
 		} else if (L->vbytes == 4) {

@@ -25,9 +25,11 @@ HASH_NIC, HASH_JENKINS, HASH_TOEPLITZ = 0, 1, 2
 HASH_MODES = {"nic": HASH_NIC, "jenkins": HASH_JENKINS, "toeplitz": HASH_TOEPLITZ}
 
 CFG_AZURE_ARP, CFG_HASH16, CFG_PROFILE, CFG_TRANS_HASH, CFG_VERDICT4 = 0x1, 0x2, 0x4, 0x8, 0x10
-CFG_VERDICT2 = 0x20
+CFG_VERDICT2, CFG_VERDICT1 = 0x20, 0x40
 # GCL_CFG_VERDICT2: u16 q = uniqid << thread_bits | flow_tbl slot; kind in the top two bits
 V2_Q_MASK, V2_KIND, V2_DELIVER, V2_WAKE, V2_OTHER, V2_QUEUES = 0x3FFF, 0xC000, 0, 0x4000, 0xC000, 0x4000
+# GCL_CFG_VERDICT1: u8 q (DELIVER or WAKE, unmarked) or V1_OTHER | action
+V1_Q_MASK, V1_OTHER, V1_QUEUES = 0x7F, 0x80, 0x80
 PAIR_NEW_READS, PAIR_NEW_WRITES, PAIR_TRIES, PAIR_RUN = 0x1, 0x2, 24, 2
 
 F_RSS_HASH, F_FDIR_ID = 0x01, 0x02
@@ -223,6 +225,9 @@ def _load():
         "gcl_host_deliver2": (u64, [vp, u32, vp, i32, vp, ctypes.c_uint8, vp, vp, vp,
                                     ctypes.c_uint8, vp, u64, ctypes.POINTER(GclHostOps), vp]),
         "gcl_verdict2_to4": (ctypes.c_uint32, [ctypes.c_uint16, ctypes.c_uint8]),
+        "gcl_host_deliver1": (u64, [vp, u32, vp, i32, vp, ctypes.c_uint8, vp, vp, vp,
+                                    ctypes.c_uint8, vp, u64, ctypes.POINTER(GclHostOps), vp]),
+        "gcl_verdict1_to4": (ctypes.c_uint32, [ctypes.c_uint8, ctypes.c_uint8]),
         "gcl_host_deliver_recs": (u64, [vp, u32, vp, i32, vp, ctypes.c_uint8, ctypes.c_uint8, vp, vp,
                                         vp, ctypes.c_uint8, vp, u64, ctypes.POINTER(GclHostOps), vp]),
         "gcl_rxloop_peek": (i32, [vp, ctypes.c_int64, u64, ctypes.POINTER(vp), ctypes.POINTER(u32)]),
@@ -318,7 +323,7 @@ class DeviceBuffer:
         by gcl_dev_alloc_paired so that reading the frame side while writing
         the verdict side does not hit the same-placement-class slowdown.
         new_reads: the new buffer is the frame (read) side.
-        vbytes: the verdict width the classifier will write (2, 4 or 8)."""
+        vbytes: the verdict width the classifier will write (1, 2, 4 or 8)."""
         p = ctypes.c_void_p()
         self.probe_us = None
         self.pair_info = None
@@ -455,11 +460,11 @@ def generate(workload, n, stride, nruntimes, frames, olflags=None, rss=None, see
 
 
 def verdict_bytes(flags):
-    return 2 if flags & CFG_VERDICT2 else 4 if flags & CFG_VERDICT4 else 8
+    return 1 if flags & CFG_VERDICT1 else 2 if flags & CFG_VERDICT2 else 4 if flags & CFG_VERDICT4 else 8
 
 
 def verdict_dtype(vbytes):
-    return {2: np.dtype("<u2"), 4: VERDICT4_DTYPE, 8: VERDICT_DTYPE}[vbytes]
+    return {1: np.dtype("u1"), 2: np.dtype("<u2"), 4: VERDICT4_DTYPE, 8: VERDICT_DTYPE}[vbytes]
 
 
 def thread_bits_for(max_runtimes, max_threads):

@@ -130,12 +130,29 @@ uint64_t gcl_host_deliver2(struct gcl_host_proc *const *clients_by_id, uint32_t 
                            uint8_t default_olflags, const uint64_t *shmptr, uint64_t n,
                            const struct gcl_host_ops *ops, uint64_t *stats);
 
+/* gcl_verdict1_to4 - widen a GCL_CFG_VERDICT1 verdict of a context opened
+ * with @thread_bits: a queue verdict becomes DELIVER of that flow_tbl slot
+ * (the post-pass takes rx.c's wake path itself when the runtime has no
+ * active kthread), any other its action. */
+struct gcl_verdict4 gcl_verdict1_to4(uint8_t v, uint8_t thread_bits);
+
+/*
+ * gcl_host_deliver1 - gcl_host_deliver2 over 1-byte verdicts (GCL_CFG_VERDICT1),
+ * with the same outcome packet by packet.
+ */
+uint64_t gcl_host_deliver1(struct gcl_host_proc *const *clients_by_id, uint32_t max_runtimes,
+                           struct gcl_host_proc *const *clients, int nr_clients,
+                           const uint8_t *v, uint8_t thread_bits, const uint32_t *bcast_hash,
+                           const uint16_t *pkt_len, const uint8_t *olflags,
+                           uint8_t default_olflags, const uint64_t *shmptr, uint64_t n,
+                           const struct gcl_host_ops *ops, uint64_t *stats);
+
 /*
  * gcl_host_deliver_recs - the same post-pass straight over a burst's verdict
  * records in the persistent loop's ring slot (gcl_rxloop_peek), without
- * copying them out: @vbytes is the context's verdict width (2, 4 or 8) and
- * @thread_bits its GclCfg.thread_bits (2-byte verdicts).  Returns 0 for a bad
- * @vbytes / @thread_bits.
+ * copying them out: @vbytes is the context's verdict width (1, 2, 4 or 8)
+ * and @thread_bits its GclCfg.thread_bits (1- and 2-byte verdicts).
+ * Returns 0 for a bad @vbytes / @thread_bits.
  */
 uint64_t gcl_host_deliver_recs(struct gcl_host_proc *const *clients_by_id, uint32_t max_runtimes,
                                struct gcl_host_proc *const *clients, int nr_clients,

@@ -90,6 +90,10 @@ enum gcl_hash_mode {
 #define GCL_CFG_VERDICT2   0x20 /* write 2-byte queue verdicts (gcl_verdict2 below);
                                    needs cfg.thread_bits, excludes VERDICT4 and
                                    TRANS_HASH */
+#define GCL_CFG_VERDICT1   0x40 /* write 1-byte queue verdicts (gcl_verdict1 below):
+                                   needs cfg.thread_bits with max_runtimes <<
+                                   thread_bits <= GCL_V1_QUEUES, excludes VERDICT2,
+                                   VERDICT4 and TRANS_HASH */
 
 struct gcl_cfg {
 	uint32_t max_runtimes;    /* uniqids must be < max_runtimes (<= GCL_MAX_PROC) */
@@ -97,9 +101,10 @@ struct gcl_cfg {
 	uint32_t flags;           /* GCL_CFG_* */
 	uint8_t  default_olflags; /* flags of every packet when gcl_batch.olflags == NULL */
 	uint8_t  rss_key[40];     /* Toeplitz key (NIC key, dpdk.c:219-228) */
-	uint8_t  thread_bits;     /* GCL_CFG_VERDICT2: kthread queues per runtime are
-	                             1 << thread_bits (thread_count may not exceed it),
-	                             and max_runtimes << thread_bits <= GCL_V2_QUEUES */
+	uint8_t  thread_bits;     /* GCL_CFG_VERDICT2 / VERDICT1: kthread queues per runtime
+	                             are 1 << thread_bits (thread_count may not exceed it),
+	                             and max_runtimes << thread_bits <= GCL_V2_QUEUES
+	                             (GCL_V1_QUEUES) */
 	uint8_t  pad[2];
 };
 
@@ -201,6 +206,20 @@ struct gcl_verdict4 {
 #define GCL_V2_DELIVER  0x0000
 #define GCL_V2_WAKE     0x4000
 #define GCL_V2_OTHER    0xC000
+
+/*
+ * 1-byte verdict (GCL_CFG_VERDICT1), for contexts whose queues fit 7 bits
+ * (max_runtimes << thread_bits <= 128: config 2's 16 runtimes x 8 kthreads):
+ *   DELIVER or WAKE      q = uniqid << thread_bits | slot
+ *   every other action   GCL_V1_OTHER | action (DROP_*, BROADCAST, ARP_RESPOND)
+ * A WAKE is not marked: the post-pass reads the runtime's live
+ * active_thread_count at delivery anyway and takes rx.c's wake path when it
+ * is 0 (rx.c:55-72), so the mark carried nothing the host uses.  Half the
+ * verdict bytes of the 2-byte form; gcl_verdict1_to4 (gcl_host.h) widens one.
+ */
+#define GCL_V1_QUEUES   0x80
+#define GCL_V1_Q_MASK   0x7F
+#define GCL_V1_OTHER    0x80
 
 /*
  * Counter slots; indices 0..5 keep the order of the reference enum
@@ -360,7 +379,7 @@ int gcl_classify_ex(struct gcl_ctx *ctx, const struct gcl_batch *b, const struct
  * sets (e.g. one 128-B line fetched per 64-B header of a 1536-B slot).  One
  * 16-B load per packet of the line holding frame byte 0 (plus one of the
  * next line when frame bytes [0, 40) cross into it), @b's offs, olflags and
- * rss when given, and @vbytes (2, 4 or 8) bytes stored per packet to device
+ * rss when given, and @vbytes (1, 2, 4 or 8) bytes stored per packet to device
  * memory @out (not verdicts: a checksum of the loads).  Asynchronous on
  * @hip_stream; 0, -EINVAL or -EIO.  A measurement aid beside the classify
  * kernel's roofline (bench.py roofline.ceiling_ms), not part of the rx path.
@@ -479,7 +498,7 @@ int gcl_dev_free(void *p);
  * GCL_PAIR_NEW_READS: the new buffer is the one stream-read (frames) and
  *                     @partner the one written (verdicts);
  * GCL_PAIR_NEW_WRITES: the reverse.
- * OR in GCL_PAIR_VBYTES(2|4|8), the verdict width the kernel will write
+ * OR in GCL_PAIR_VBYTES(1|2|4|8), the verdict width the kernel will write
  * (default 4): the probe stores the same width, so its time tracks the
  * kernel's for every format.
  * The probe WRITES to the written side's first min(bytes, 256 MiB), rounded

@@ -187,6 +187,17 @@ def to_verdict2(v, thread_count, thread_bits):
     return out.astype(np.uint16)
 
 
+def to_verdict1(v, thread_count, thread_bits):
+    """8-B verdicts -> the GCL_CFG_VERDICT1 form (include/gclassify.h): u8
+    q = uniqid << thread_bits | slot for DELIVER and WAKE alike (no wake
+    mark), 0x80 | action otherwise."""
+    v4 = to_verdict4(v, thread_count)
+    act = v4["action"].astype(np.uint32) & 0x3F
+    q = v4["uniqid"].astype(np.uint32) << thread_bits | v4["thread"].astype(np.uint32)
+    out = np.where((act == 0) | (act == 1), q, 0x80 | act)
+    return out.astype(np.uint8)
+
+
 def load_struct_frames():
     """tests/golden/struct_frames_ref.npz (make_struct_frames.py): (ips,
     frames[n, 64], uniqid, hash, hit), frames written by the reference's

@@ -188,7 +188,7 @@ def make_cprocs(g, S, ring_size, ring_cls):
 def run_post_pass(g, S, cprocs, rings, form, verdicts, max_runtimes, client_order, pkt_len,
                   olflags, shmptr, bcast_hash, arp_ok, thread_bits=0):
     """Run one gcl_host_deliver* form over `verdicts` with callbacks driving S.
-    form: 8, 4, 2 (packed arrays) or "recs8"/"recs4"/"recs2" (loop records,
+    form: 8, 4, 2, 1 (packed arrays) or "recs8"/.../"recs1" (loop records,
     `verdicts` then an array of LOOP_REC_DTYPE)."""
     events = S.events
     by_id = (ctypes.c_void_p * max_runtimes)()
@@ -240,6 +240,9 @@ def run_post_pass(g, S, cprocs, rings, form, verdicts, max_runtimes, client_orde
     elif form == 2:
         d = g.lib.gcl_host_deliver2(by_id, max_runtimes, clients, len(client_order),
                                     verdicts.ctypes.data, thread_bits, bh, *common)
+    elif form == 1:
+        d = g.lib.gcl_host_deliver1(by_id, max_runtimes, clients, len(client_order),
+                                    verdicts.ctypes.data, thread_bits, bh, *common)
     else:
         vb = int(form[4:])
         d = g.lib.gcl_host_deliver_recs(by_id, max_runtimes, clients, len(client_order),
@@ -248,7 +251,7 @@ def run_post_pass(g, S, cprocs, rings, form, verdicts, max_runtimes, client_orde
     return d, [int(x) for x in stats], events, {k: r.drain() for k, r in rings.items()}
 
 
-def loop_records(g, v8, v4, v2, vb):
+def loop_records(g, v8, v4, v2, vb, v1=None):
     """The rx loop's 16-B records (struct gcl_loop_rec) of these verdicts."""
     r = np.zeros(len(v8), dtype=g.LOOP_REC_DTYPE)
     r["ticket"] = 7
@@ -256,5 +259,6 @@ def loop_records(g, v8, v4, v2, vb):
         r["hash"], r["verdict"] = v8.view(np.uint64) & 0xFFFFFFFF, v8.view(np.uint64) >> 32
     else:
         r["hash"] = 0xDEADBEEF  # unused by the compact forms
-        r["verdict"] = v4.view(np.uint32) if vb == 4 else v2.astype(np.uint32)
+        r["verdict"] = v4.view(np.uint32) if vb == 4 else v2.astype(np.uint32) if vb == 2 \
+            else v1.astype(np.uint32)
     return r

@@ -24,7 +24,7 @@ def test_metric_matches_baseline(bench):
     assert bench.HBM_PEAK_GBS == 8000.0
 
 
-@pytest.mark.parametrize("vbytes", [8, 4, 2])
+@pytest.mark.parametrize("vbytes", [8, 4, 2, 1])
 def test_roofline_object(bench, vbytes):
     name, n = "udp64", 32 << 20
     w = types.SimpleNamespace(name=name, n=n, vbytes=vbytes, bytes_per_pkt=bench.HDR_BYTES + vbytes)
@@ -48,7 +48,12 @@ def test_verdict_configs(bench):
     assert bench.verdict_cfg(4, 1024, 4) == (g.CFG_VERDICT4, 0)
     assert bench.verdict_cfg(2, 16, 8) == (g.CFG_VERDICT2, 3)
     assert bench.verdict_cfg(2, 1024, 4) == (g.CFG_VERDICT2, 2)
-    assert set(bench.VERDICT_NAMES) == {8, 4, 2}
+    assert bench.verdict_cfg(1, 16, 8) == (g.CFG_VERDICT1, 3)
+    with pytest.raises(ValueError):
+        bench.verdict_cfg(1, 1024, 4)
+    assert bench.fit_vbytes(1, 16, 8) == 1 and bench.fit_vbytes(1, 1024, 4) == 2
+    assert bench.fit_vbytes(4, 1024, 4) == 4
+    assert set(bench.VERDICT_NAMES) == {8, 4, 2, 1}
 
 
 def test_workloads_match_baseline_configs(bench):

@@ -280,15 +280,18 @@ def test_host_deliver_broadcast_and_arp(g):
     assert stats[0] == 1 and stats[4] == 1
 
 
-def test_host_deliver4_matches_deliver(g, orc):
-    """Compact verdicts (4 and 2 bytes) replay exactly like 8-B ones: same rings, counters and
+@pytest.mark.parametrize("R,nrt,forms", [(64, 24, (4, 2, "recs4", "recs2", "recs8")),
+                                         (16, 12, (1, "recs1"))])
+def test_host_deliver4_matches_deliver(g, orc, R, nrt, forms):
+    """Compact verdicts (4, 2 and 1 bytes) replay exactly like 8-B ones: same rings, counters and
     callbacks in the same order with the same packet indices (polls, ownership
     records, frees, ARP responses), including wakes that change the flow_tbl
-    mid-batch and broadcasts fanned out with the caller's hashes."""
-    from tests.rxcases import fuzz_batch, random_runtimes, to_verdict2, to_verdict4
+    mid-batch and broadcasts fanned out with the caller's hashes.  The 1-byte
+    form (16 runtimes x 8 queues) carries no WAKE mark: the wakes come from
+    the live active count alone."""
+    from tests.rxcases import fuzz_batch, random_runtimes, to_verdict1, to_verdict2, to_verdict4
     rng = np.random.default_rng(12)
-    R = 64
-    rts = random_runtimes(rng, R, 24, max_threads=6)
+    rts = random_runtimes(rng, R, nrt, max_threads=6)
     n = 3000
     frames, flen, offs, olf, rss, fdir, _ = fuzz_batch(rng, n, rts, R, tail_runts=False)
     t = orc.Tables(R, 0, 0x1, 0x09)  # NIC hash, Azure ARP: broadcasts too
@@ -298,6 +301,7 @@ def test_host_deliver4_matches_deliver(g, orc):
     assert ((v["action"] & 0x3F) == g.ACT_WAKE).any() and ((v["action"] & 0x3F) == g.ACT_BROADCAST).any()
     v4 = to_verdict4(v, {r["uniqid"]: r["thread_count"] for r in rts})
     v2 = to_verdict2(v, {r["uniqid"]: r["thread_count"] for r in rts}, 3)
+    v1 = to_verdict1(v, {r["uniqid"]: r["thread_count"] for r in rts}, 3) if R << 3 <= 128 else None
     pkt_len = rng.integers(60, 1515, size=n).astype(np.uint16)
     shm = offs.astype(np.uint64)
     bhash = rss.astype(np.uint32)  # NIC mode: the hash is hash.rss whatever the flags
@@ -310,7 +314,8 @@ def test_host_deliver4_matches_deliver(g, orc):
             r["hash"], r["verdict"] = v.view(np.uint64) & 0xFFFFFFFF, v.view(np.uint64) >> 32
         else:
             r["hash"] = 0xDEADBEEF  # unused in the compact forms
-            r["verdict"] = v4.view(np.uint32) if vb == 4 else v2.astype(np.uint32)
+            r["verdict"] = v4.view(np.uint32) if vb == 4 else v2.astype(np.uint32) if vb == 2 \
+                else v1.astype(np.uint32)
         return r
 
     def run(compact):
@@ -367,7 +372,12 @@ def test_host_deliver4_matches_deliver(g, orc):
                                         bhash.ctypes.data, pkt_len.ctypes.data, olf.ctypes.data,
                                         0x09, shm.ctypes.data, n, ctypes.byref(ops),
                                         stats.ctypes.data)
-        elif compact:
+        elif compact == 1:
+            d = g.lib.gcl_host_deliver1(by_id, R, clients, len(procs), v1.ctypes.data, 3,
+                                        bhash.ctypes.data, pkt_len.ctypes.data, olf.ctypes.data,
+                                        0x09, shm.ctypes.data, n, ctypes.byref(ops),
+                                        stats.ctypes.data)
+        elif compact == 4:
             d = g.lib.gcl_host_deliver4(by_id, R, clients, len(procs), v4.ctypes.data,
                                         bhash.ctypes.data, pkt_len.ctypes.data, olf.ctypes.data,
                                         0x09, shm.ctypes.data, n, ctypes.byref(ops),
@@ -378,21 +388,19 @@ def test_host_deliver4_matches_deliver(g, orc):
                                        shm.ctypes.data, n, ctypes.byref(ops), stats.ctypes.data)
         return d, list(stats), events, {k: r.drain() for k, r in rings.items()}
 
-    full, compact, compact2 = run(False), run(True), run(2)
+    full = run(False)
     kinds = {e[0] for e in full[2]}
     assert full[0] > 0 and {"wake", "own", "poll", "free", "ref", "arp"} <= kinds, kinds
-    assert full == compact
-    assert full == compact2
-    for vb in (4, 2, 8):
-        assert full == run(f"recs{vb}"), vb
+    for f in forms:
+        assert full == run(f), f
 
 
-def _live_batch(orc, seed, n=3000, R=64):
-    """A NIC-hash, Azure-ARP batch over 24 random runtimes (some with no
+def _live_batch(orc, seed, n=3000, R=64, nrt=24):
+    """A NIC-hash, Azure-ARP batch over @nrt random runtimes (some with no
     active thread) classified by the oracle: verdicts in all three widths."""
     from tests.rxcases import fuzz_batch, random_runtimes, to_verdict2, to_verdict4
     rng = np.random.default_rng(seed)
-    rts = random_runtimes(rng, R, 24, max_threads=6)
+    rts = random_runtimes(rng, R, nrt, max_threads=6)
     frames, flen, offs, olf, rss, fdir, _ = fuzz_batch(rng, n, rts, R, tail_runts=False)
     t = orc.Tables(R, 0, 0x1, 0x09)
     for r in rts:
@@ -536,7 +544,7 @@ def test_host_deliver4_fast_path(g, orc, meta):
             d = g.lib.gcl_host_deliver_recs(by_id, R, clients, len(procs), rr.ctypes.data, 4, 0,
                                             bhash.ctypes.data, pl, of, 0x09, sp, n, None,
                                             stats.ctypes.data)
-        elif compact:
+        elif compact == 4:
             d = g.lib.gcl_host_deliver4(by_id, R, clients, len(procs), v4.ctypes.data,
                                         bhash.ctypes.data, pl, of, 0x09, sp, n, None,
                                         stats.ctypes.data)
@@ -598,6 +606,66 @@ def test_verdict2_widening(g, orc):
         assert (w & 0xFFFF == v4["uniqid"]).all()
         assert (w >> 16 & 0xFF == v4["thread"]).all()
         assert (w >> 24 == v4["action"] & 0x3F).all()
+
+
+@pytest.mark.parametrize("form", [1, "recs1"])
+def test_host_deliver1_live_flow_tbl(g, orc, form):
+    """test_host_deliver_live_flow_tbl for the 1-byte verdicts (16 runtimes
+    x 8 queues): no WAKE mark in the verdict, the wakes and the re-steered
+    runtimes come from the live flow_tbl and active count alone, and every
+    ring, counter and callback equals the serial per-packet model."""
+    from tests.rxcases import to_verdict1
+    from tests.schedmodel import Sched, loop_records, make_cprocs, rx_model, run_post_pass
+    R, ring = 16, 32
+    rts, v, v4, v2, pkt_len, olf, shm, bh = _live_batch(orc, 23, R=R, nrt=12)
+    v1 = to_verdict1(v, {r["uniqid"]: r["thread_count"] for r in rts}, 3)
+    order = [r["uniqid"] for r in rts]
+    arp_ok = lambda i: i % 2 == 0  # noqa: E731
+    want = rx_model(Sched(rts, 5, np.random.default_rng(5)), v, order, ring, pkt_len, olf, shm, bh, arp_ok)
+    assert any(e[0] == "disable" for e in want[2])
+    assert ((v["action"] & 0x3F) == g.ACT_WAKE).any()
+    S = Sched(rts, 5, np.random.default_rng(5))
+    cprocs, rings = make_cprocs(g, S, ring, Ring)
+    verd = loop_records(g, v, v4, v2, 1, v1) if isinstance(form, str) else v1
+    got = run_post_pass(g, S, cprocs, rings, form, verd, R, order, pkt_len, olf, shm, bh, arp_ok,
+                        thread_bits=3)
+    assert got == want
+
+
+def test_verdict1_roundtrip(g, orc):
+    """gcl_verdict1_to4 inverts the 1-byte encoding: every oracle verdict of a
+    fuzz batch, narrowed to u8 and widened again, is its gcl_verdict4 with
+    WAKE read as DELIVER (the post-pass decides the wake) and the FDIR /
+    TRANS flags dropped."""
+    from tests.rxcases import fuzz_batch, random_runtimes, to_verdict1, to_verdict4
+    rng = np.random.default_rng(15)
+    for R, tb in [(16, 3), (32, 2), (128, 0), (1, 7)]:
+        rts = random_runtimes(rng, R, min(R, 40), max_threads=1 << tb)
+        frames, flen, offs, olf, rss, fdir, hint = fuzz_batch(rng, 2000, rts, R)
+        t = orc.Tables(R, 0, 0x1, 0x09)
+        for r in rts:
+            assert t.runtime_set(r["uniqid"], r["ip"], r["thread_count"], r["active"], r["flow_tbl"]) == 0
+        v, _, _ = t.classify(frames, 2000, 0, offs=offs, olflags=olf, rss=rss, fdir_hi=fdir,
+                             frames_len=flen, dst_hint=hint)
+        tc = {r["uniqid"]: r["thread_count"] for r in rts}
+        v4, v1 = to_verdict4(v, tc), to_verdict1(v, tc, tb)
+        w = np.array([g.lib.gcl_verdict1_to4(int(x), tb) for x in v1], dtype=np.uint32)
+        act = v4["action"] & 0x3F
+        assert (w & 0xFFFF == v4["uniqid"]).all()
+        assert (w >> 16 & 0xFF == v4["thread"]).all()
+        assert (w >> 24 == np.where(act == g.ACT_WAKE, g.ACT_DELIVER, act)).all()
+
+
+def test_open_rejects_bad_verdict1_cfg(g):
+    """Checked before the device: past 128 queues, thread_bits > 7, or
+    combined with VERDICT2 / VERDICT4 / TRANS_HASH."""
+    ctx = ctypes.c_void_p()
+    for flags, R, tb in [(g.CFG_VERDICT1, 32, 3), (g.CFG_VERDICT1, 1, 8), (g.CFG_VERDICT1, 129, 0),
+                         (g.CFG_VERDICT1 | g.CFG_VERDICT2, 16, 3),
+                         (g.CFG_VERDICT1 | g.CFG_VERDICT4, 16, 3),
+                         (g.CFG_VERDICT1 | g.CFG_TRANS_HASH, 16, 3)]:
+        cfg = g.GclCfg(max_runtimes=R, hash_mode=1, flags=flags, thread_bits=tb)
+        assert g.lib.gcl_open(0, ctypes.byref(cfg), ctypes.byref(ctx)) == -22, (flags, R, tb)
 
 
 def test_open_rejects_bad_verdict2_cfg(g):

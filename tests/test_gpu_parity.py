@@ -4,7 +4,7 @@ import numpy as np
 import pytest
 
 from tests.rxcases import (apply_runtimes, apply_seeds, fuzz_batch, random_runtimes, scenario_batch,
-                           to_verdict2, to_verdict4,
+                           to_verdict1, to_verdict2, to_verdict4,
                            scenario_sets, scenario_trans)
 
 pytestmark = pytest.mark.gpu
@@ -243,6 +243,85 @@ def test_gpu_verdict2_limits(g):
         with pytest.raises(OSError):
             g.Classifier(0, R, 1, flags, thread_bits=tb)
     g.Classifier(0, 4096, 1, g.CFG_VERDICT2, thread_bits=2).close()
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("flags", [1, 2])
+@pytest.mark.parametrize("max_rt,max_th", [(16, 8), (32, 4), (128, 1)])
+def test_gpu_fuzz_verdict1(g, orc, mode, flags, max_rt, max_th):
+    """GCL_CFG_VERDICT1: one u8 kthread-queue index per packet, up to all 128
+    queues (16 x 8, 32 x 4, 128 x 1), WAKE unmarked; per-packet offsets and
+    side arrays (the GENERAL kernel)."""
+    rng = np.random.default_rng(7150 + 1000 * mode + 10 * flags + max_rt)
+    rts = random_runtimes(rng, max_rt, min(max_rt, 40), max_threads=max_th)
+    for r in rts[:2]:  # runtimes with no active kthread: WAKE in the 4-B form
+        r.update(active=0, active_idx=[], flow_tbl=None)
+    n = 5000
+    frames, flen, offs, olf, rss, fdir, hint = fuzz_batch(rng, n, rts, max_rt)
+    key = bytes(rng.integers(0, 256, size=40, dtype=np.uint8))
+    tb = max(0, (max_th - 1).bit_length())
+    assert max_rt << tb <= g.V1_QUEUES
+    t = orc.Tables(max_rt, mode, flags, 0x09, key)
+    apply_runtimes(t, rts)
+    clf = g.Classifier(0, max_rt, mode, flags | g.CFG_VERDICT1, 0x09, key, thread_bits=tb)
+    assert clf.vbytes == 1
+    apply_runtimes(clf, rts)
+    ve, ce, se = t.classify(frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir_hi=fdir,
+                            frames_len=flen, dst_hint=hint)
+    v, c, st = gpu_run(g, clf, frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir=fdir,
+                       frames_len=flen, hint=hint)
+    assert ((ve["action"] & 0x3F) == g.ACT_WAKE).any()
+    exp = to_verdict1(ve, {r["uniqid"]: r["thread_count"] for r in rts}, tb)
+    assert_same(v, exp, f"verdict1 mode={mode} flags={flags} R={max_rt}")
+    assert (c == ce).all() and (st == se).all()
+    # every queue verdict decodes (gcl_verdict1_to4) to the 4-B form's runtime
+    # and slot, WAKE read back as DELIVER
+    w4 = to_verdict4(ve, {r["uniqid"]: r["thread_count"] for r in rts})
+    dec = np.array([g.lib.gcl_verdict1_to4(int(x), tb) for x in v], dtype=np.uint32).view(g.VERDICT4_DTYPE)
+    act = w4["action"] & 0x3F
+    assert (dec["uniqid"] == w4["uniqid"]).all() and (dec["thread"] == w4["thread"]).all()
+    assert (dec["action"] == np.where(act == g.ACT_WAKE, g.ACT_DELIVER, act)).all()
+
+
+@pytest.mark.parametrize("wl,R,T", [(0, 16, 8), (2, 16, 8)])
+def test_gpu_dense_verdict1(g, orc, wl, R, T):
+    """GCL_CFG_VERDICT1 on the dense path (fixed slots, no side arrays: the
+    bench's udp64 format) and on the mixed stream's 9216-B slots."""
+    stride = {0: 64, 2: 9216}[wl]
+    n = 40000 if wl == 0 else 6000
+    df = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
+    g.generate(wl, n, stride, R, df, seed=11)
+    frames = df.cpu().numpy()
+    del df
+    tb = 3
+    clf = g.Classifier(0, R, g.HASH_JENKINS, g.CFG_VERDICT1, thread_bits=tb)
+    t = orc.Tables(R, g.HASH_JENKINS, 0, g.F_RSS_HASH | g.F_IP_CKSUM_GOOD)
+    for r in range(R):
+        act = r % T  # runtimes 0 and 8: no active kthread (WAKE in the 4-B form)
+        fl = g.steer_flows(T, list(range(act))) if act else None
+        clf.runtime_set(r, g.runtime_ip(r), T, act, fl)
+        t.runtime_set(r, orc.runtime_ip(r), T, act, fl)
+    v, c, st = gpu_run(g, clf, frames, n, stride)
+    ve, ce, se = t.classify(frames, n, stride)
+    assert_same(v, to_verdict1(ve, [T] * R, tb), f"dense verdict1 wl={wl}")
+    assert (c == ce).all() and (st == se).all()
+
+
+def test_gpu_verdict1_limits(g):
+    """More than 128 queues, thread_bits past 7, or VERDICT1 with VERDICT2,
+    VERDICT4 or TRANS_HASH does not open; kthreads past 1 << thread_bits are
+    refused."""
+    clf = g.Classifier(0, 16, 1, g.CFG_VERDICT1, thread_bits=3)
+    assert clf.runtime_set(5, 0x0A000001, 8, 8, list(range(8))) == 0
+    with pytest.raises(OSError):
+        clf.runtime_set(6, 0x0A000002, 9, 0, None)
+    for flags, R, tb in [(g.CFG_VERDICT1, 32, 3), (g.CFG_VERDICT1, 1, 8),
+                         (g.CFG_VERDICT1 | g.CFG_VERDICT2, 16, 3),
+                         (g.CFG_VERDICT1 | g.CFG_VERDICT4, 16, 3),
+                         (g.CFG_VERDICT1 | g.CFG_TRANS_HASH, 16, 3)]:
+        with pytest.raises(OSError):
+            g.Classifier(0, R, 1, flags, thread_bits=tb)
+    g.Classifier(0, 128, 1, g.CFG_VERDICT1, thread_bits=0).close()
 
 
 @pytest.mark.parametrize("wl,stride,R", [(0, 64, 16), (1, 1536, 1024), (2, 9216, 16)])
@@ -527,33 +606,36 @@ def test_gpu_full_size_tcp1500_properties(g, orc):
     assert_same(vv[sample], ve, "tcp1500 sample")
 
 
-@pytest.mark.parametrize("name", ["udp64", "tcp1500", "tcp1500_hsplit"])
-def test_gpu_full_size_bench_format(g, orc, name):
+@pytest.mark.parametrize("name,vb", [("udp64", 1), ("udp64", 2), ("tcp1500", 2), ("tcp1500_hsplit", 2)])
+def test_gpu_full_size_bench_format(g, orc, name, vb):
     """The bench lines' own instances at full size, in exactly the format and
     allocation they time: bench.Workload (frame pool placed against the
-    verdict ring by gcl_dev_alloc_paired, 2-byte queue verdicts with
+    verdict ring by gcl_dev_alloc_paired, 1- or 2-byte queue verdicts with
     thread_bits 3 for 16 x 8 and 2 for 1024 x 4, the bench's seeded tables)
     stepped once.  Every verdict is a DELIVER to a queue of a registered
     runtime, the queue histogram equals the device counts, and a
-    65536-packet random sample decodes (to_verdict2) to the oracle's
-    verdicts bit for bit."""
+    65536-packet random sample decodes (to_verdict1 / to_verdict2) to the
+    oracle's verdicts bit for bit."""
     import bench
     from tests.rxcases import to_verdict2
     dev = torch.device("cuda", 0)
-    w = bench.Workload(name, 0, 1, dev, vbytes=2)
-    assert w.vbytes == 2 and w.clf.vbytes == 2
+    w = bench.Workload(name, 0, 1, dev, vbytes=vb)
+    assert w.vbytes == vb and w.clf.vbytes == vb
     tb = w.clf.thread_bits
     assert tb == {16: 3, 1024: 2}[w.R]
     w.step(torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     n, R = w.n, w.R
-    hv = torch.empty(n * 2, dtype=torch.uint8).pin_memory()
-    bench.hip_copy(hv, w.verdicts, n * 2)
-    q = hv.numpy().view(np.uint16)
+    hv = torch.empty(n * vb, dtype=torch.uint8).pin_memory()
+    bench.hip_copy(hv, w.verdicts, n * vb)
+    q = hv.numpy().view(np.uint16 if vb == 2 else np.uint8)
     cc = w.counts[:R].cpu().numpy()
     ss = w.counts[R:].cpu().numpy()
     assert cc.sum() == n and ss[g.RX_PULLED] == n and ss[g.RX_UNHANDLED] == 0
-    assert ((q & g.V2_KIND) == g.V2_DELIVER).all()
+    if vb == 2:
+        assert ((q & g.V2_KIND) == g.V2_DELIVER).all()
+    else:
+        assert ((q & g.V1_OTHER) == 0).all()
     assert (np.bincount(q >> tb, minlength=R)[:R] == cc).all()
     # the sample: the same bytes from the CPU generator, classified by the oracle
     t = orc.Tables(R, 1, 0, 0x09)
@@ -566,8 +648,9 @@ def test_gpu_full_size_bench_format(g, orc, name):
     fr = fr_dev.view(n, w.stride)[torch.from_numpy(sample).cuda(), :64].cpu().numpy().reshape(-1)
     del fr_dev
     ve, _, _ = t.classify(fr, len(sample), 64)
-    want = to_verdict2(ve, {r: T for (r, _, T, _, _) in w.tables}, tb)
-    assert_same(q[sample], want, f"{name} 2-B sample")
+    tcs = {r: T for (r, _, T, _, _) in w.tables}
+    want = to_verdict2(ve, tcs, tb) if vb == 2 else to_verdict1(ve, tcs, tb)
+    assert_same(q[sample], want, f"{name} {vb}-B sample")
     del w
     torch.cuda.empty_cache()
 
@@ -642,6 +725,28 @@ def test_gpu_end_to_end_verdict2(g, orc, mode):
     clf.classify_host(hf, n, 64, verdicts=hv, counts=counts, stats=stats, mode=mode,
                       chunk=65536 + 17, nstreams=3)
     assert_same(hv.numpy().view(np.uint16), to_verdict2(ve, [T] * R, 3), f"e2e2 mode={mode}")
+    assert (counts == ce).all() and (stats == se).all()
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_gpu_end_to_end_verdict1(g, orc, mode):
+    """Both transports with 1-byte verdicts, chunks of odd length."""
+    n, R, T = 300000, 16, 8
+    frames, olf, rss = orc.generate(0, n, 64, R)
+    t = orc.Tables(R, 1, 0, 0x09)
+    clf = g.Classifier(0, R, 1, g.CFG_VERDICT1, thread_bits=3)
+    for r in range(R):
+        fl = orc.steer_flows(T, list(range(r % T)))
+        t.runtime_set(r, orc.runtime_ip(r), T, r % T, fl if r % T else None)
+        clf.runtime_set(r, g.runtime_ip(r), T, r % T, fl if r % T else None)
+    ve, ce, se = t.classify(frames, n, 64)
+    hf = torch.from_numpy(frames).pin_memory()
+    hv = torch.zeros(n, dtype=torch.uint8).pin_memory()
+    counts = np.zeros(R, dtype=np.uint64)
+    stats = np.zeros(8, dtype=np.uint64)
+    clf.classify_host(hf, n, 64, verdicts=hv, counts=counts, stats=stats, mode=mode,
+                      chunk=65536 + 17, nstreams=3)
+    assert_same(hv.numpy(), to_verdict1(ve, [T] * R, 3), f"e2e1 mode={mode}")
     assert (counts == ce).all() and (stats == se).all()
 
 
@@ -989,29 +1094,29 @@ def test_gpu_reference_struct_frames(g, orc):
     assert int(c.sum()) == int(hit.sum())
 
 
-@pytest.mark.parametrize("vbytes", [8, 4, 2])
+@pytest.mark.parametrize("vbytes", [8, 4, 2, 1])
 def test_gpu_post_pass_live_flow_tbl(g, orc, vbytes):
     """A GPU batch's verdicts through the host post-pass while sched_add_core
     side effects re-steer OTHER runtimes mid-batch (tests/schedmodel.py,
     sched.c:174-216): ring contents, counters and callbacks equal the serial
-    per-packet model of rx.c:50-92, for all three verdict widths."""
+    per-packet model of rx.c:50-92, for all four verdict widths."""
     from tests.rxcases import fuzz_batch
     from tests.schedmodel import Sched, make_cprocs, rx_model, run_post_pass
     from tests.test_cabi import Ring
-    R, ring, tb = 64, 32, 3
+    R, ring, tb = (16 if vbytes == 1 else 64), 32, 3
     rng = np.random.default_rng(21)
-    rts = random_runtimes(rng, R, 24, max_threads=6)
+    rts = random_runtimes(rng, R, 12 if vbytes == 1 else 24, max_threads=6)
     n = 3000
     frames, flen, offs, olf, rss, fdir, _ = fuzz_batch(rng, n, rts, R, tail_runts=False)
     t = orc.Tables(R, 0, 0x1, 0x09)
     apply_runtimes(t, rts)
     ve, ce, se = t.classify(frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir_hi=fdir, frames_len=flen)
-    flag = {8: 0, 4: g.CFG_VERDICT4, 2: g.CFG_VERDICT2}[vbytes]
-    clf = g.Classifier(0, R, 0, 0x1 | flag, 0x09, thread_bits=tb if vbytes == 2 else 0)
+    flag = {8: 0, 4: g.CFG_VERDICT4, 2: g.CFG_VERDICT2, 1: g.CFG_VERDICT1}[vbytes]
+    clf = g.Classifier(0, R, 0, 0x1 | flag, 0x09, thread_bits=tb if vbytes <= 2 else 0)
     apply_runtimes(clf, rts)
     v, c, st = gpu_run(g, clf, frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir=fdir, frames_len=flen)
     tc = {r["uniqid"]: r["thread_count"] for r in rts}
-    exp = {8: ve, 4: to_verdict4(ve), 2: to_verdict2(ve, tc, tb)}[vbytes]
+    exp = {8: ve, 4: to_verdict4(ve), 2: to_verdict2(ve, tc, tb), 1: to_verdict1(ve, tc, tb)}[vbytes]
     assert_same(v, exp, f"post-pass batch, {vbytes}-B verdicts")
     assert (c == ce).all() and (st == se).all()
     pkt_len = rng.integers(60, 1515, size=n).astype(np.uint16)

@@ -9,7 +9,8 @@ import time
 import numpy as np
 import pytest
 
-from tests.rxcases import apply_runtimes, fuzz_batch, random_runtimes, to_verdict2, to_verdict4
+from tests.rxcases import (apply_runtimes, fuzz_batch, random_runtimes, to_verdict1, to_verdict2,
+                           to_verdict4)
 
 pytestmark = pytest.mark.gpu
 
@@ -29,7 +30,8 @@ def bursts(n, size=64):
 
 
 def want(ve, tc, vb, tb=4):
-    return to_verdict2(ve, tc, tb) if vb == 2 else to_verdict4(ve, tc) if vb == 4 else ve
+    return to_verdict1(ve, tc, tb) if vb == 1 else to_verdict2(ve, tc, tb) if vb == 2 \
+        else to_verdict4(ve, tc) if vb == 4 else ve
 
 
 LOOP_FLAGS = (lambda g: 0, lambda g: g.LOOP_INLINE_HDRS, lambda g: g.LOOP_HDR_RECORDS)
@@ -45,7 +47,8 @@ def tc_map(rts, max_rt):
 LOOP_CASES = [(m, vb, 0, 0) for m in (0, 1, 2) for vb in (8, 4, 2)] + \
     [(m, 8, fl, 0) for m in (0, 1, 2) for fl in (1, 2)] + \
     [(0, 8, 1, 1), (1, 4, 0, 1), (2, 8, 2, 1), (1, 2, 1, 1)] + \
-    [(m, vb, 0, 2) for m in (0, 1, 2) for vb in (8, 4, 2)] + [(0, 8, 1, 2), (2, 8, 2, 2)]
+    [(m, vb, 0, 2) for m in (0, 1, 2) for vb in (8, 4, 2)] + [(0, 8, 1, 2), (2, 8, 2, 2)] + \
+    [(m, 1, 0, i) for m in (0, 2) for i in (0, 1, 2)] + [(0, 1, 1, 2), (2, 1, 2, 0)]
 
 
 @pytest.mark.parametrize("k64", [1, 0])
@@ -53,21 +56,23 @@ LOOP_CASES = [(m, vb, 0, 0) for m in (0, 1, 2) for vb in (8, 4, 2)] + \
 def test_rxloop_fuzz_vs_oracle(g, orc, mode, vb, flags, inline, k64, monkeypatch):
     """k64: bursts of <= 64 through rxloop64_kernel (the default for
     max_burst <= 64), or through the general loop kernel (GCL_TUNE_LOOP64=0);
-    vb: verdict bytes (8 gcl_verdict, 4 VERDICT4, 2 VERDICT2);
+    vb: verdict bytes (8 gcl_verdict, 4 VERDICT4, 2 VERDICT2, 1 VERDICT1 with
+    16 runtimes x up to 8 kthreads);
     flags: 0 plain, 1 Azure ARP mode (GCL_CFG_AZURE_ARP), 2 16-bit hash;
     inline: 1 header granules copied into the ring slot (GCL_LOOP_INLINE_HDRS),
     2 stamped header records (GCL_LOOP_HDR_RECORDS), including the frames that
     straddle the end of the region and IPv4 options past byte 43."""
     rng = np.random.default_rng(7000 + 10 * mode + vb + 100 * flags + 1000 * inline)
-    max_rt = 1024 if mode == 1 else 16
-    rts = random_runtimes(rng, max_rt, 300 if max_rt == 1024 else 12)
+    max_rt = 1024 if mode == 1 and vb != 1 else 16
+    rts = random_runtimes(rng, max_rt, 300 if max_rt == 1024 else 12, max_threads=8 if vb == 1 else 16)
+    tb = 3 if vb == 1 else 4
     n = 3000
     frames, flen, offs, olf, rss, fdir, hint = fuzz_batch(rng, n, rts, max_rt)
     key = bytes(rng.integers(0, 256, size=40, dtype=np.uint8))
-    cflags = {8: 0, 4: g.CFG_VERDICT4, 2: g.CFG_VERDICT2}[vb] | flags
+    cflags = {8: 0, 4: g.CFG_VERDICT4, 2: g.CFG_VERDICT2, 1: g.CFG_VERDICT1}[vb] | flags
     t = orc.Tables(max_rt, mode, flags, 0x09, key)
     apply_runtimes(t, rts)
-    clf = g.Classifier(0, max_rt, mode, cflags, 0x09, key, thread_bits=4)
+    clf = g.Classifier(0, max_rt, mode, cflags, 0x09, key, thread_bits=tb)
     apply_runtimes(clf, rts)
     ve, ce, se = t.classify(frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir_hi=fdir,
                             frames_len=flen, dst_hint=hint)
@@ -98,8 +103,10 @@ def test_rxloop_fuzz_vs_oracle(g, orc, mode, vb, flags, inline, k64, monkeypatch
                 got.append(x.view(g.VERDICT_DTYPE))
             elif vb == 4:
                 got.append(rec["verdict"].copy().view(g.VERDICT4_DTYPE))
-            else:
+            elif vb == 2:
                 got.append(rec["verdict"].astype(np.uint16))
+            else:
+                got.append(rec["verdict"].astype(np.uint8))
             loop.release(tk)
         got = np.concatenate(got)
         ps = loop.poll_stats()
@@ -108,7 +115,7 @@ def test_rxloop_fuzz_vs_oracle(g, orc, mode, vb, flags, inline, k64, monkeypatch
     finally:
         loop.stop()
         g.host_unregister(frames)
-    w = want(ve, tc_map(rts, max_rt), vb)
+    w = want(ve, tc_map(rts, max_rt), vb, tb)
     bad = np.nonzero(got != w)[0]
     assert not len(bad), f"{len(bad)} differ, first {bad[0]}: {got[bad[0]]} vs {w[bad[0]]}"
     torch.cuda.synchronize()

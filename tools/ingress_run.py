@@ -24,6 +24,6 @@ if __name__ == "__main__":
     torch.cuda.set_device(dev)
     rows = (("nic",) if "--nic-only" in sys.argv else ("working_set",) if "--ws-only" in sys.argv
             else ("nic", "jenkins", "working_set"))
-    vb = int(sys.argv[sys.argv.index("--vbytes") + 1]) if "--vbytes" in sys.argv else bench.VERDICT_BYTES
+    vb = int(sys.argv[sys.argv.index("--vbytes") + 1]) if "--vbytes" in sys.argv else bench.INGRESS_VERDICT_BYTES
     print(json.dumps(bench.ingress_pool_bench(dev, vb, reps=reps, zerocopy=False,
                                               rows=rows)))
