@@ -68,6 +68,8 @@ constexpr int kDefaultXcdMap = 0; /* GCL_TUNE_XCD_MAP default: round-robin tiles
  * verdict widths, tcp1500 2-2.4 %, the header-split layout unchanged
  * (profiles/archive/r01_verdict_store_ab.jsonl) */
 constexpr int kDefaultVerdictStore = 2;
+/* GCL_TUNE_VSTAGE default (dense classify_kernel, 1-/2-B verdicts) */
+constexpr int kDefaultVstage = 0;
 /* Verdicts are stored at the end of their own tile.  Issuing them one tile
  * late (the former GCL_TUNE_DEFER=1) measured udp64 1-3 % slower and tcp1500
  * 0.4 % faster (profiles/archive/r02_defer_ab.jsonl); the knob was removed for the
@@ -118,6 +120,9 @@ struct KParams {
 	uint32_t off_seed, off_crc;
 	uint32_t *sched; /* tile queue slot (SchedSlot) or NULL = static persistent grid */
 	uint32_t xcd_map; /* static grid: 1 = each XCD walks one contiguous eighth of the tiles */
+	uint32_t vstage;  /* classify_kernel, dense slots, 1-/2-B verdicts: a full tile's verdicts
+	                     staged in LDS and stored by NT/4 lanes, 4 packets each
+	                     (GCL_TUNE_VSTAGE) */
 };
 
 /* Dynamic tile queue of one launch: tiles are dealt per XCD (tile t belongs
@@ -701,6 +706,42 @@ __device__ __forceinline__ void put_verdict(const KParams &k, uint64_t idx, uint
 	}
 }
 
+/* GCL_TUNE_VSTAGE: packet @tid's verdict into the tile's LDS staging row */
+__device__ __forceinline__ void stage_verdict(const KParams &k, uint8_t *s_vst, int tid, uint64_t w)
+{
+	if (k.cflags & GCL_CFG_VERDICT1)
+		s_vst[tid] = (uint8_t)w;
+	else
+		((uint16_t *)s_vst)[tid] = (uint16_t)w;
+}
+
+/* ... and the staged tile @t stored by lanes < NT/4, four packets a lane: one
+ * wave writes 256 (1-B) or 512 (2-B) contiguous bytes, whole 128-B lines,
+ * where the tile's waves would each write 64 or 128 */
+template <int NT>
+__device__ __forceinline__ void flush_verdicts(const KParams &k, const uint8_t *s_vst, uint64_t t)
+{
+	const int tid = threadIdx.x;
+	if (tid >= NT / 4)
+		return;
+	const uint64_t i = t * NT + 4 * (uint64_t)tid;
+	if (k.cflags & GCL_CFG_VERDICT1) {
+		const uint32_t v = ((const uint32_t *)s_vst)[tid];
+		if (k.nt_store == 2)
+			__hip_atomic_store((uint32_t *)((uint8_t *)k.verdicts + i), v, __ATOMIC_RELAXED,
+			                   __HIP_MEMORY_SCOPE_SYSTEM);
+		else
+			*(uint32_t *)((uint8_t *)k.verdicts + i) = v;
+	} else {
+		const uint64_t v = ((const uint64_t *)s_vst)[tid];
+		if (k.nt_store == 2)
+			__hip_atomic_store((uint64_t *)((uint16_t *)k.verdicts + i), v, __ATOMIC_RELAXED,
+			                   __HIP_MEMORY_SCOPE_SYSTEM);
+		else
+			*(uint64_t *)((uint16_t *)k.verdicts + i) = v;
+	}
+}
+
 template <int NT>
 __device__ __forceinline__ void stage_tile(uint4 *tile, const uint4 r[4])
 {
@@ -865,6 +906,10 @@ classify_kernel(KParams k)
 	 * path (load_tile). */
 	constexpr bool goffs = GENERAL && DEPTH == 2;
 	uint4 *s_src = (uint4 *)(lds_tab + k.tables_lds_bytes);
+	/* GCL_TUNE_VSTAGE (dense slots only): full tiles' verdicts via LDS */
+	uint8_t *s_vst = lds_tab + k.tables_lds_bytes + (goffs ? NT * 16 : 0);
+	const bool vst = !GENERAL && k.vstage;
+	auto full_tile = [&](uint64_t tt) { return vst && (tt + 1) * NT <= k.n; };
 	/* offs[] of this lane's packet of tile tt, loaded unconditionally (the
 	 * table image stands in without offs[]); whether there is a packet is
 	 * my_ok(tt), applied by pub() when the offset is published, after the
@@ -947,8 +992,12 @@ classify_kernel(KParams k)
 			if (t * NT + tid < k.n) /* in the verdict format: never past the buffer */
 				put_verdict(k, t * NT + tid, (uint64_t)(a.w ^ b.y) << 32 | (b.z ^ a.x));
 		} else if (t * NT + tid < k.n) {
-			put_verdict(k, t * NT + tid, classify_one<MODE, GENERAL>(k, tile, tid, t * NT + tid, tb,
-			                                                         hist, cnt, sp, goffs ? pra : nullptr));
+			const uint64_t v = classify_one<MODE, GENERAL>(k, tile, tid, t * NT + tid, tb, hist, cnt, sp,
+			                                               goffs ? pra : nullptr);
+			if (full_tile(t))
+				stage_verdict(k, s_vst, tid, v);
+			else
+				put_verdict(k, t * NT + tid, v);
 		}
 		pref(nxt, pra);
 		if (dyn && tid == 0)
@@ -956,6 +1005,8 @@ classify_kernel(KParams k)
 			                                                 x0, xs, got)
 			                                 : k.ntiles;
 		__syncthreads();
+		if (!(k.ablate & 16) && full_tile(t))
+			flush_verdicts<NT>(k, s_vst, t);
 		if (dyn) {
 			t = nxt;
 			par ^= 1;
@@ -977,12 +1028,18 @@ classify_kernel(KParams k)
 			load_tile<GENERAL, NT, goffs>(k, t + 2 * step, t + 2 * step < t_end, rb, spb, s_src);
 			if (goffs)
 				offb = my_off(t + 4 * step);
-			if (t < t_end && t * NT + tid < k.n)
-				put_verdict(k, t * NT + tid, classify_one<MODE, GENERAL>(k, tile, tid, t * NT + tid,
-				                                                         tb, hist, cnt, sp2,
-				                                                         goffs ? prb : nullptr));
+			if (t < t_end && t * NT + tid < k.n) {
+				const uint64_t v = classify_one<MODE, GENERAL>(k, tile, tid, t * NT + tid, tb, hist, cnt,
+				                                               sp2, goffs ? prb : nullptr);
+				if (full_tile(t))
+					stage_verdict(k, s_vst, tid, v);
+				else
+					put_verdict(k, t * NT + tid, v);
+			}
 			pref(t + 2 * step, prb);
 			__syncthreads();
+			if (t < t_end && full_tile(t))
+				flush_verdicts<NT>(k, s_vst, t);
 			t += step;
 		}
 	}
@@ -2447,6 +2504,7 @@ struct gcl_ctx {
 	int tune_nt_store; /* GCL_TUNE_NT_STORE: verdict store policy, 0 plain, 1 non-temporal
 	                      (8-B verdicts), 2 write-through sc0 sc1 (default) */
 	int tune_ablate;   /* GCL_TUNE_ABLATE bitmask (timing experiments only) */
+	int tune_vstage;   /* GCL_TUNE_VSTAGE: 1 = dense tiles' 1-/2-B verdicts staged in LDS */
 	int tune_sched;    /* GCL_TUNE_SCHED: 0 static persistent grid, 1 dynamic tile queue */
 	int tune_xcd_map;  /* GCL_TUNE_XCD_MAP: 1 contiguous eighth per XCD, 0 round-robin tiles */
 	int tune_pair;     /* GCL_TUNE_PAIR: 1 GENERAL batches on classify_pair_kernel */
@@ -2532,6 +2590,8 @@ extern "C" int gcl_open(int hip_device, const struct gcl_cfg *cfg, struct gcl_ct
 		c->tune_nt_store = e ? atoi(e) : kDefaultVerdictStore;
 		e = getenv("GCL_TUNE_ABLATE");
 		c->tune_ablate = e ? atoi(e) : 0;
+		e = getenv("GCL_TUNE_VSTAGE");
+		c->tune_vstage = e ? atoi(e) : kDefaultVstage;
 		e = getenv("GCL_TUNE_GRID");
 		g_tune_grid = e ? atoi(e) : 0;
 		e = getenv("GCL_TUNE_BLOCKS_PER_CU");
@@ -2923,7 +2983,8 @@ static hipError_t launch_mode(const KParams &k, bool tlds, bool general, const G
 		return launch_pair<MODE, 256>(k, tlds, lds, num_cus, geo.bpc_cap, geo.ntl, s);
 	}
 	const uint32_t lds = (uint32_t)geo.threads * 64 + kLdsQueueBytes + hist_bytes + tab_lds +
-	                     offs_lds_bytes(general, (uint32_t)geo.threads);
+	                     offs_lds_bytes(general, (uint32_t)geo.threads) +
+	                     (k.vstage ? (uint32_t)geo.threads * 2 : 0);
 #define GCL_LAUNCH(D, T) \
 	return launch_nt<MODE, D, T>(k, tlds, general, lds, num_cus, geo.bpc_cap, s)
 	if (geo.depth == 2) {
@@ -2969,7 +3030,8 @@ static Geometry choose_geometry(const gcl_ctx *c, uint32_t tab_lds, uint32_t his
 	auto per_block = [&](uint32_t nt) -> uint32_t {
 		if (g.pair)
 			return hist_bytes + tab_lds;
-		return nt * 64 + kLdsQueueBytes + hist_bytes + tab_lds + offs_lds_bytes(general, nt);
+		return nt * 64 + kLdsQueueBytes + hist_bytes + tab_lds + offs_lds_bytes(general, nt) +
+		       (c->tune_vstage && !general ? nt * 2 : 0);
 	};
 	for (int nt = 256; nt <= 1024 && !g.threads; nt *= 2) {
 		const uint32_t pb = per_block((uint32_t)nt);
@@ -3218,6 +3280,8 @@ extern "C" int gcl_classify_ex(struct gcl_ctx *c, const struct gcl_batch *b,
 	else if (c->tune_tables == 2)
 		tlds = tab_bytes <= kLdsTableBudget;
 	k.tables_lds_bytes = tlds ? tab_bytes : 0;
+	k.vstage = c->tune_vstage && !general && ((uintptr_t)verdicts & 7) == 0 &&
+	           (k.cflags & (GCL_CFG_VERDICT1 | GCL_CFG_VERDICT2)) ? 1 : 0;
 	Geometry geo = choose_geometry(c, tlds ? tab_bytes : 0, hist_bytes, general);
 
 	HipErr he;
@@ -3865,6 +3929,7 @@ struct gcl_rxloop {
 	bool ended;              /* the kernel has finished (hipStreamQuery) */
 	bool left;               /* some worker has left: submit no more */
 	bool k64;                /* rxloop64_kernel (bursts <= 64) */
+	bool nt_submit;          /* header records by non-temporal stores (GCL_TUNE_LOOP_NT) */
 };
 
 static uint64_t now_ns()
@@ -4092,6 +4157,8 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 		if (const char *e = getenv("GCL_TUNE_LOOP64"))
 			k64 = k64 && atoi(e) != 0;
 		L->k64 = k64;
+		if (const char *e = getenv("GCL_TUNE_LOOP_NT"))
+			L->nt_submit = atoi(e) != 0;
 		hipError_t e = c->cfg.hash_mode == GCL_HASH_NIC ? loop_launch<GCL_HASH_NIC>(lp, k64, L->st)
 		             : c->cfg.hash_mode == GCL_HASH_JENKINS ? loop_launch<GCL_HASH_JENKINS>(lp, k64, L->st)
 		             : loop_launch<GCL_HASH_TOEPLITZ>(lp, k64, L->st);
@@ -4153,12 +4220,28 @@ static void loop_write_records(gcl_rxloop *L, uint64_t t, uint8_t *dst, uint32_t
 		const uint32_t olf = olflags ? olflags[i] : 0;
 		const u32x4_h sv = {S, S, S, S};
 		const u32x4_h side = {S, 0, rss ? rss[i] : 0u, fdir_hi ? fdir_hi[i] : 0u};
-		q[0] = __builtin_shufflevector(v0, sv, 4, 0, 2, 3);       /* S d3 d5 d6 */
-		q[P] = __builtin_shufflevector(v1, sv, 4, 0, 1, 2);       /* S d7 d8 d9 */
-		q[2 * P] = __builtin_shufflevector(side, v1, 0, 7, 2, 3); /* S d10 rss fdir */
-		q[3 * P] = u32x4_h{S, (uint32_t)off, (uint32_t)(off >> 32) | olf << 8,
-		                   dst_hint ? dst_hint[i] : 0u};
+		const u32x4_h c0 = __builtin_shufflevector(v0, sv, 4, 0, 2, 3);   /* S d3 d5 d6 */
+		const u32x4_h c1 = __builtin_shufflevector(v1, sv, 4, 0, 1, 2);   /* S d7 d8 d9 */
+		const u32x4_h c2 = __builtin_shufflevector(side, v1, 0, 7, 2, 3); /* S d10 rss fdir */
+		const u32x4_h c3 = u32x4_h{S, (uint32_t)off, (uint32_t)(off >> 32) | olf << 8,
+		                           dst_hint ? dst_hint[i] : 0u};
+		if (L->nt_submit) {
+			/* past the core's caches: the GPU's poll then reads the lines
+			 * from memory, not by a probe of a dirty line in this core */
+			u32x4_h *w = (u32x4_h *)q;
+			__builtin_nontemporal_store(c0, w);
+			__builtin_nontemporal_store(c1, w + P);
+			__builtin_nontemporal_store(c2, w + 2 * P);
+			__builtin_nontemporal_store(c3, w + 3 * P);
+		} else {
+			q[0] = c0;
+			q[P] = c1;
+			q[2 * P] = c2;
+			q[3 * P] = c3;
+		}
 	}
+	if (L->nt_submit)
+		__builtin_ia32_sfence(); /* the records before the slot word */
 	/* records past n keep older stamps; rewrite them now and then so that
 	 * none is ever 2^31 uses stale (loop_stamp's rule for the offsets) */
 	if (((t - 1) / L->lp.nslots) % kLoopRefresh == kLoopRefresh - 1)
