@@ -146,7 +146,7 @@ def main(rnd):
         cal = calib(base)
         with open(os.path.join(prof, f"{rnd}_calibration.json"), "w") as f:
             json.dump({"note": __doc__.strip().split("\n\n")[2], "patterns": cal}, f, indent=1)
-    for wl, vb in [(w, v) for w in PKTS for v in (2, 4, 8)]:
+    for wl, vb in [(w, v) for w in PKTS for v in (1, 2, 4, 8)]:
         tag = f"{wl}_v{vb}"
         tdir = os.path.join(base, f"{tag}_trace")
         if not os.path.isdir(tdir):
