@@ -68,7 +68,13 @@ constexpr int kDefaultXcdMap = 0; /* GCL_TUNE_XCD_MAP default: round-robin tiles
  * verdict widths, tcp1500 2-2.4 %, the header-split layout unchanged
  * (profiles/archive/r01_verdict_store_ab.jsonl) */
 constexpr int kDefaultVerdictStore = 2;
-/* GCL_TUNE_VSTAGE default (dense classify_kernel, 1-/2-B verdicts) */
+/* GCL_TUNE_VSTAGE default (dense classify_kernel, 1-/2-B verdicts): off.
+ * Staging a tile's verdicts in LDS so one wave stores them as whole lines
+ * measured within noise of the per-wave 64-B stores on the udp64 headline
+ * with write-through stores (kernel 0.3296-0.3298 against 0.3297-0.3319 ms,
+ * alternating fresh processes), 0.6 % faster with plain ones, which stay
+ * 2 % slower than write-through either way (profiles/r04_vstage_ab.jsonl):
+ * the fabric sees 64-B write requests in both forms (pmc_udp64_v1.json) */
 constexpr int kDefaultVstage = 0;
 /* Verdicts are stored at the end of their own tile.  Issuing them one tile
  * late (the former GCL_TUNE_DEFER=1) measured udp64 1-3 % slower and tcp1500
@@ -618,6 +624,65 @@ __device__ __forceinline__ uint64_t classify_core(const KParams &k, const HdrWor
 		const uint32_t q = uniq << (k.cflags >> 24) | thr;
 		return a == GCL_ACT_DELIVER ? q : a == GCL_ACT_WAKE ? GCL_V2_WAKE | q : GCL_V2_OTHER | a;
 	}
+	if (k.cflags & GCL_CFG_VERDICT4)
+		return vlo;
+	return (uint64_t)vlo << 32 | hash;
+}
+
+/*
+ * rxloop64_kernel's lean rx_one_pkt: classify_core restricted to what a burst
+ * of plain IPv4 traffic needs -- Ethertype IPv4, IHL 5, no FDIR mark, no
+ * dst_ip hint, no transport pre-hash -- which the caller checks for every
+ * packet of the burst (a uniform ballot) before taking it.  Same verdicts and
+ * counters as classify_core on those packets (rx.c:154-163, :197-207, :55-72);
+ * a burst with any other packet takes classify_core.  One wave classifies a
+ * lone burst on its own, so its latency is the instruction count: this path
+ * skips the FDIR, hint, options-port, ARP and action-ladder selects.
+ * @flags: ol_flags (or the context default), @rss: hash.rss (NIC mode).
+ */
+template <int MODE>
+__device__ __forceinline__ uint64_t classify_lean(const KParams &k, const HdrWords &h, const Tables &tb,
+                                                  uint32_t flags, uint32_t rss, uint32_t *hist, int tid,
+                                                  Counters &cnt)
+{
+	const uint32_t frag = gcl::bswap16(h.d5 & 0xFFFF);
+	const uint32_t proto = h.d5 >> 24;
+	const uint32_t saddr = gcl::bswap32(gcl::mid32(h.d6, h.d7));
+	const uint32_t daddr = gcl::bswap32(gcl::mid32(h.d7, h.d8));     /* rx.c:157-159 */
+	uint32_t hash = 0;
+	if (MODE == GCL_HASH_NIC) {
+		if (k.rss)
+			hash = rss;
+	} else {
+		const bool hashable = (frag & 0x3FFF) == 0 && (proto == 6 || proto == 17);
+		const uint32_t sport = gcl::bswap16(h.d8 >> 16), dport = gcl::bswap16(h.d9 & 0xFFFF);
+		const uint32_t x = MODE == GCL_HASH_JENKINS ? gcl::jhash_5tuple(saddr, daddr, sport, dport, proto)
+		                                            : toeplitz_lut(tb.toep, saddr, daddr, sport, dport);
+		hash = hashable ? x : 0;
+	}
+	if (k.cflags & GCL_CFG_HASH16)
+		hash &= 0xFFFF;
+	cnt.hashmiss += !(flags & GCL_F_RSS_HASH); /* rx.c:160-163 */
+	const int p = ipt_lookup(tb.ipt, k.ipt_mask, k.ipt_seed, daddr); /* rx.c:197 */
+	const bool miss = p < 0;
+	cnt.unreg += miss;     /* rx.c:205 */
+	cnt.unhandled += miss; /* rx.c:232 */
+	uint32_t action = miss ? GCL_ACT_DROP_UNREG : GCL_ACT_DELIVER;
+	uint32_t uniq = GCL_NO_RUNTIME, thr = GCL_NO_THREAD;
+	if (!miss) { /* rx_send_to_runtime's slot, rx.c:55-72 */
+		const RtEntry re = tb.rtab[p];
+		uniq = (uint32_t)p;
+		thr = gcl::fastmod(hash, (uint64_t)re.m_hi << 32 | re.m_lo, re.tc);
+		if (!re.active)
+			action |= GCL_ACT_WAKE;
+	}
+	hist[tid] = (uint32_t)p;
+	const uint32_t q = uniq << (k.cflags >> 24) | thr;
+	if (k.cflags & GCL_CFG_VERDICT1)
+		return miss ? GCL_V1_OTHER | GCL_ACT_DROP_UNREG : q;
+	if (k.cflags & GCL_CFG_VERDICT2)
+		return miss ? GCL_V2_OTHER | GCL_ACT_DROP_UNREG : action == GCL_ACT_WAKE ? GCL_V2_WAKE | q : q;
+	const uint32_t vlo = uniq | thr << 16 | action << 24;
 	if (k.cflags & GCL_CFG_VERDICT4)
 		return vlo;
 	return (uint64_t)vlo << 32 | hash;
@@ -1309,6 +1374,9 @@ constexpr uint32_t kDefaultLoopClock = 0;
  * queued one (4 workers x 8: 78.5 against 79.7 Mpkt/s;
  * profiles/r04_loop64_ab.jsonl) */
 constexpr uint32_t kDefaultLoopWriter = 0;
+/* GCL_TUNE_LOOP_LEAN default: bursts whose every packet is plain IPv4 (IHL 5,
+ * no FDIR mark, no hint) classified by classify_lean */
+constexpr uint32_t kDefaultLoopLean = 1;
 /* how a worker's bursts arrived (gcl_rxloop_poll_stats): with the poll that
  * found the word; eligible for that, but an entry or record still stale so
  * read after it; or after the word, the speculative window over or the
@@ -1364,6 +1432,8 @@ struct LoopParams {
 	                              planes (chunk j of packet i at off_hdr + j * rec_plane + 16 i) */
 	uint32_t writer;           /* rxloop64_kernel: the writer wave stores the verdict
 	                              records (else the poller, GCL_TUNE_LOOP_WRITER=0) */
+	uint32_t lean;             /* rxloop64_kernel: plain-IPv4 bursts on classify_lean
+	                              (GCL_TUNE_LOOP_LEAN=0: always classify_core) */
 };
 
 /* GCL_LOOP_HDR_RECORDS: the submitting core writes each packet as one 64-B
@@ -1813,7 +1883,8 @@ struct Mbox64 {
 	                     trip, polls, hit -> packets in registers, hit -> posted,
 	                     hit -> classified, hit -> records issued */
 	uint32_t flag;    /* 1: posted by the poller, 0: free */
-	uint32_t pad[3];
+	uint32_t lean;    /* classified by classify_lean */
+	uint32_t pad[2];
 };
 static_assert(sizeof(Mbox64) % 16 == 0, "Mbox64");
 constexpr uint32_t kLoop64Lds = 2 * sizeof(Mbox64) + 64 * 8 + 2 * 64 * 4 + 64 * 8 + 16;
@@ -1825,6 +1896,7 @@ __device__ __forceinline__ void rxloop64_writer(const LoopParams &L, Mbox64 *mbo
                                              int lane)
 {
 	uint32_t pe = 0, ps = 0, pl = 0; /* bursts by how they arrived (no indexed array: scratch) */
+	uint32_t pn = 0;                 /* bursts on classify_lean (gcl_rxloop_lean_bursts) */
 	for (uint32_t b = 0;; b ^= 1) {
 		Mbox64 &m = mbox[b];
 		for (;;) {
@@ -1838,7 +1910,7 @@ __device__ __forceinline__ void rxloop64_writer(const LoopParams &L, Mbox64 *mbo
 		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 		const uint64_t t_w = L.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
 		const uint64_t t = m.t;
-		const uint32_t n = m.n, kind = m.kind;
+		const uint32_t n = m.n, kind = m.kind, lean = m.lean;
 		const __amdgpu_buffer_rsrc_t srs =
 		        gcl::host_rsrc(L.slots + ((t - 1) % L.nslots) * L.slot_bytes, L.slot_bytes);
 		if (L.writer && (uint32_t)lane < n) {
@@ -1883,6 +1955,8 @@ __device__ __forceinline__ void rxloop64_writer(const LoopParams &L, Mbox64 *mbo
 			pl += kind == kLoopPollLate;
 			gcl::st_sys32(&L.polls[4 * blockIdx.x + kind],
 			              kind == kLoopPollEarly ? pe : kind == kLoopPollStale ? ps : pl);
+			if (lean)
+				gcl::st_sys32(&L.polls[4 * blockIdx.x + 3], ++pn);
 			if (L.stamps) {
 				/* {ticket, hit's round trip, hit -> classified, hit -> records
 				 *  issued (by the writer when L.writer)}
@@ -2096,9 +2170,14 @@ __global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
 		const uint32_t pre[2] = {olf, rss};
 		Counters cnt = {0, 0, 0, 0};
 		uint64_t t_cls = 0, t_st = 0;
+		/* plain IPv4 only (and nothing that needs the general path): lean */
+		const uint32_t lflags = (fl & GCL_LOOP_F_OLF) ? olf : k.default_flags;
+		const bool plain = !live || ((hw.d3 & 0x000FFFFF) == 0x00050008 && !(lflags & GCL_F_FDIR_ID));
+		const bool lean = L.lean && !(fl & GCL_LOOP_F_HINT) && !L.off_trans && __all(plain);
 		if (live) {
-			const uint64_t v = classify_core<MODE, true, true, true, 0, false>(
-			        k, hw, nullptr, lane, (uint64_t)lane, tb, m.p, cnt, 0, 64, pre);
+			const uint64_t v = lean ? classify_lean<MODE>(k, hw, tb, lflags, rss, m.p, lane, cnt)
+			                        : classify_core<MODE, true, true, true, 0, false>(
+			                                  k, hw, nullptr, lane, (uint64_t)lane, tb, m.p, cnt, 0, 64, pre);
 			if (L.stamps)
 				t_cls = __builtin_amdgcn_s_memrealtime();
 			const bool v4 = L.cflags & GCL_CFG_VERDICT4, v2 = L.cflags & GCL_CFG_VERDICT2;
@@ -2136,6 +2215,7 @@ __global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
 			m.t = t;
 			m.n = nw;
 			m.kind = kind;
+			m.lean = lean;
 			m.cnt[0] = c_ft;
 			m.cnt[1] = c_hm;
 			m.cnt[2] = c_ur;
@@ -3929,7 +4009,9 @@ struct gcl_rxloop {
 	bool ended;              /* the kernel has finished (hipStreamQuery) */
 	bool left;               /* some worker has left: submit no more */
 	bool k64;                /* rxloop64_kernel (bursts <= 64) */
-	bool nt_submit;          /* header records by non-temporal stores (GCL_TUNE_LOOP_NT) */
+	bool nt_submit;          /* header records by non-temporal stores (GCL_TUNE_LOOP_NT):
+	                            measured no different, lone burst 3.90-4.02 us p50 either
+	                            way (profiles/r04_loop_nt_ab.jsonl); off */
 };
 
 static uint64_t now_ns()
@@ -4092,6 +4174,9 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 	lp.writer = kDefaultLoopWriter;
 	if (const char *e = getenv("GCL_TUNE_LOOP_WRITER"))
 		lp.writer = atoi(e) != 0;
+	lp.lean = kDefaultLoopLean;
+	if (const char *e = getenv("GCL_TUNE_LOOP_LEAN"))
+		lp.lean = atoi(e) != 0;
 	if (const char *e = getenv("GCL_TUNE_LOOP_CLOCK"))
 		lp.fast_clock = atoi(e) != 0;
 	lp.off_hdr = (cfg->flags & (GCL_LOOP_INLINE_HDRS | GCL_LOOP_HDR_RECORDS))
@@ -4478,6 +4563,16 @@ extern "C" int gcl_rxloop_poll_stats(struct gcl_rxloop *L, uint64_t out[3])
 	for (uint32_t w = 0; w < L->lp.workers; w++)
 		for (int k = 0; k < 3; k++)
 			out[k] += __atomic_load_n(&L->ctl[kLoopCtlPolls + 4 * w + k], __ATOMIC_RELAXED);
+	return 0;
+}
+
+extern "C" int gcl_rxloop_lean_bursts(struct gcl_rxloop *L, uint64_t *out)
+{
+	if (!L || !out)
+		return -EINVAL;
+	*out = 0;
+	for (uint32_t w = 0; w < L->lp.workers; w++)
+		*out += __atomic_load_n(&L->ctl[kLoopCtlPolls + 4 * w + 3], __ATOMIC_RELAXED);
 	return 0;
 }
 

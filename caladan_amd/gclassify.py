@@ -233,6 +233,7 @@ def _load():
         "gcl_rxloop_peek": (i32, [vp, ctypes.c_int64, u64, ctypes.POINTER(vp), ctypes.POINTER(u32)]),
         "gcl_rxloop_release": (i32, [vp, ctypes.c_int64]),
         "gcl_rxloop_poll_stats": (i32, [vp, vp]),
+        "gcl_rxloop_lean_bursts": (i32, [vp, vp]),
         "gcl_rxloop_trans": (i32, [vp, ctypes.c_int64, vp]),
     }
     for name, (res, args) in sig.items():
@@ -822,6 +823,12 @@ class RxLoop:
         out = np.zeros(3, dtype=np.uint64)
         _check(lib.gcl_rxloop_poll_stats(self._h, out.ctypes.data), "gcl_rxloop_poll_stats")
         return dict(zip(("early", "stale", "late"), (int(x) for x in out)))
+
+    def lean_bursts(self):
+        """Bursts classified on rxloop64_kernel's lean path (gcl_rxloop_lean_bursts)."""
+        out = np.zeros(1, dtype=np.uint64)
+        _check(lib.gcl_rxloop_lean_bursts(self._h, out.ctypes.data), "gcl_rxloop_lean_bursts")
+        return int(out[0])
 
     def drive(self, offs, iters, depth=1):
         offs = np.ascontiguousarray(offs, dtype=np.uint64)

@@ -624,6 +624,12 @@ int gcl_rxloop_release(struct gcl_rxloop *loop, int64_t ticket);
  * stale, so read after the word, @out[2] read after the word (the window
  * over, a longer burst, or inline granules).  Before gcl_rxloop_stop. */
 int gcl_rxloop_poll_stats(struct gcl_rxloop *loop, uint64_t out[3]);
+/* gcl_rxloop_lean_bursts - how many of the loop's bursts so far were
+ * classified by the burst-of-64 kernel's lean path (every packet plain IPv4:
+ * IHL 5, no FDIR mark, no dst_ip hint, no transport pre-hash; the verdicts and
+ * counters are classify_core's), summed over its workers, into @out.  Before
+ * gcl_rxloop_stop. */
+int gcl_rxloop_lean_bursts(struct gcl_rxloop *loop, uint64_t *out);
 /* gcl_rxloop_trans - a GCL_CFG_TRANS_HASH context's transport demux hashes
  * of @ticket's burst (struct gcl_trans per packet, as gcl_classify_ex writes
  * them), copied to @out once the burst is complete: after gcl_rxloop_wait

@@ -165,6 +165,34 @@ def fuzz_batch(rng, n, runtimes, max_runtimes, slot=128, tail_runts=True, misali
     return frames, frames_len, offs, olflags, rss, fdir, hint
 
 
+def plain_batch(rng, n, runtimes, slot=128):
+    """Plain IPv4 frames (Ethertype IPv4, IHL 5: the burst-of-64 loop's lean
+    path) with every field that path still decides on varied: UDP/TCP/other
+    protocols, fragment fields, any version nibble, registered and unknown
+    destinations, ol_flags with and without RSS_HASH (never FDIR), hash.rss.
+    Shuffled 16-B aligned offsets; fdir all 0."""
+    ips = [r["ip"] for r in runtimes] or [0x0A000001]
+    order = rng.permutation(n + 8)[:n]
+    offs = order.astype(np.uint64) * np.uint64(slot)
+    frames = np.zeros((n + 8) * slot, dtype=np.uint8)
+    for i in range(n):
+        dst = int(rng.choice(ips)) if rng.random() < 0.8 else int(rng.integers(0, 2**32))
+        src = int(rng.integers(0, 2**32))
+        ver = 4 if rng.random() < 0.9 else int(rng.integers(0, 16))
+        proto = int(rng.choice([6, 17, 6, 17, 1, 47]))
+        frag = int(rng.choice([0, 0x4000, 0x4000, 0x2000, 0x0001, 0x8000]))
+        hdr = struct.pack("!BBHHHBBHII", ver << 4 | 5, int(rng.integers(0, 256)), 100, 7, frag, 64,
+                          proto, 0, src, dst)
+        hdr = hdr[:10] + struct.pack("!H", _csum(hdr)) + hdr[12:]
+        l4 = struct.pack("!HH", int(rng.integers(0, 65536)), int(rng.integers(0, 65536)))
+        fr = bytes(rng.integers(0, 256, size=12, dtype=np.uint8)) + b"\x08\x00" + hdr + l4 + bytes(8)
+        frames[int(offs[i]):int(offs[i]) + len(fr)] = np.frombuffer(fr, dtype=np.uint8)
+    olflags = (rng.integers(0, 16, size=n, dtype=np.uint8) & np.uint8(0xFD))
+    rss = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
+    fdir = np.zeros(n, dtype=np.uint32)
+    return frames, offs, olflags, rss, fdir
+
+
 def to_verdict4(v, thread_count=None):
     """8-B verdicts -> the GCL_CFG_VERDICT4 form: drop the hash.  Every
     DELIVER and WAKE verdict, in either width, carries the flow_tbl slot

@@ -9,8 +9,8 @@ import time
 import numpy as np
 import pytest
 
-from tests.rxcases import (apply_runtimes, fuzz_batch, random_runtimes, to_verdict1, to_verdict2,
-                           to_verdict4)
+from tests.rxcases import (apply_runtimes, fuzz_batch, plain_batch, random_runtimes, to_verdict1,
+                           to_verdict2, to_verdict4)
 
 pytestmark = pytest.mark.gpu
 
@@ -118,6 +118,71 @@ def test_rxloop_fuzz_vs_oracle(g, orc, mode, vb, flags, inline, k64, monkeypatch
     w = want(ve, tc_map(rts, max_rt), vb, tb)
     bad = np.nonzero(got != w)[0]
     assert not len(bad), f"{len(bad)} differ, first {bad[0]}: {got[bad[0]]} vs {w[bad[0]]}"
+    torch.cuda.synchronize()
+    assert (cnt.cpu().numpy().astype(np.uint64) == ce).all()
+    assert (st.cpu().numpy().astype(np.uint64) == se).all()
+
+
+LEAN_CASES = [(m, vb, fl, lf) for m in (0, 1, 2) for vb in (8, 4, 2, 1) for fl, lf in ((0, 2), (2, 0))]
+
+
+@pytest.mark.parametrize("mode,vb,flags,lflag", LEAN_CASES)
+def test_rxloop_lean_path(g, orc, mode, vb, flags, lflag, monkeypatch):
+    """rxloop64_kernel's lean path (classify_lean) against the oracle: bursts
+    of plain IPv4 (every packet Ethertype IPv4, IHL 5, no FDIR mark) take it,
+    bursts with one FDIR-marked packet, or with dst_ip hints, take
+    classify_core; both give the oracle's verdicts and counters, and
+    gcl_rxloop_lean_bursts counts exactly the plain bursts.  Modes NIC /
+    JENKINS / TOEPLITZ, every verdict width, the 16-bit hash, records or
+    offsets; misses, runtimes with no active kthread (WAKE), fragments and
+    non-TCP/UDP protocols (hash 0), ol_flags without RSS_HASH."""
+    rng = np.random.default_rng(9100 + 10 * mode + vb + 100 * flags + 1000 * lflag)
+    max_rt = 16
+    rts = random_runtimes(rng, max_rt, 12, max_threads=8 if vb == 1 else 16)
+    tb = 3 if vb == 1 else 4
+    n = 64 * 24 + 17
+    frames, offs, olf, rss, fdir = plain_batch(rng, n, rts)
+    hint = np.zeros(n, dtype=np.uint32)
+    spans = bursts(n)
+    # every 4th burst general: one FDIR-marked packet, or (every 8th) dst_ip hints
+    fdir_b = {k for k in range(len(spans)) if k % 8 == 3}
+    hint_b = {k for k in range(len(spans)) if k % 8 == 7}
+    for k in fdir_b:
+        a, _ = spans[k]
+        olf[a + 5] |= np.uint8(0x02)  # GCL_F_FDIR_ID
+        fdir[a + 5] = np.uint32(rts[0]["uniqid"])
+    for k in hint_b:
+        a, b = spans[k]
+        hint[a:b:3] = np.uint32(rts[1]["ip"])
+    key = bytes(rng.integers(0, 256, size=40, dtype=np.uint8))
+    cflags = {8: 0, 4: g.CFG_VERDICT4, 2: g.CFG_VERDICT2, 1: g.CFG_VERDICT1}[vb] | flags
+    t = orc.Tables(max_rt, mode, flags, 0x09, key)
+    apply_runtimes(t, rts)
+    clf = g.Classifier(0, max_rt, mode, cflags, 0x09, key, thread_bits=tb)
+    apply_runtimes(clf, rts)
+    ve, ce, se = t.classify(frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir_hi=fdir,
+                            frames_len=frames.nbytes, dst_hint=hint)
+    g.host_register(frames)
+    cnt = torch.zeros(max_rt, dtype=torch.int64, device="cuda")
+    st = torch.zeros(g.NR_STATS, dtype=torch.int64, device="cuda")
+    monkeypatch.setenv("GCL_TUNE_LOOP_SPEC", "500000")
+    loop = clf.rxloop(frames, slots=8, counts=cnt, stats=st, flags=LOOP_FLAGS[lflag](g))
+    try:
+        got = []
+        for k, (a, b) in enumerate(spans):
+            tk = loop.submit(offs[a:b], olf[a:b], rss[a:b], fdir[a:b],
+                             hint[a:b] if k in hint_b else None)
+            assert tk > 0
+            got.append(loop.wait(tk, b - a))
+        got = np.concatenate(got)
+        lean = loop.lean_bursts()
+    finally:
+        loop.stop()
+        g.host_unregister(frames)
+    w = want(ve, tc_map(rts, max_rt), vb, tb)
+    bad = np.nonzero(got != w)[0]
+    assert not len(bad), f"{len(bad)} differ, first {bad[0]}: {got[bad[0]]} vs {w[bad[0]]}"
+    assert lean == len(spans) - len(fdir_b) - len(hint_b), lean
     torch.cuda.synchronize()
     assert (cnt.cpu().numpy().astype(np.uint64) == ce).all()
     assert (st.cpu().numpy().astype(np.uint64) == se).all()
