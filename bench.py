@@ -799,21 +799,31 @@ def rxpipe_bench(reps=3):
     # burst 64 is the reference's own (IOKERNEL_RX_BURST_SIZE, defs.h:75):
     # throughput there is workers / round trip, so it is run at 1, 4, 8, 16
     # and 32 workers; verdicts are read in place in the slot
-    # (gcl_rxloop_peek), and once copied out (the round-2 form) for comparison
+    # (gcl_rxloop_peek), and once copied out (the round-2 form) for comparison.
+    # The flow hash is the JENKINS 5-tuple computed on the GPU, and in the
+    # "nic" rows the mbuf's hash.rss submitted with the packets -- what rx.c
+    # itself steers by (rx.c:83), and what cpu_baseline.nic_mode times
+    nic = "RXPIPE_HASH=nic"
     for cfg in (("64", "1", "1", "20000"), ("64", "4", "8", "20000"), ("64", "4", "8", "20000", "copy"),
                 ("64", "8", "16", "40000"), ("64", "16", "32", "40000"), ("64", "32", "64", "60000"),
                 ("64", "8", "16", "40000", "inline"), ("64", "16", "32", "40000", "inline"),
                 ("64", "1", "1", "20000", "records"), ("64", "4", "8", "20000", "records"),
                 ("64", "8", "16", "40000", "records"),
                 ("64", "16", "32", "40000", "records"),
+                (nic, "64", "1", "1", "20000", "records"), (nic, "64", "4", "8", "20000", "records"),
+                (nic, "64", "8", "16", "40000", "records"), (nic, "64", "16", "32", "40000", "records"),
                 ("256", "4", "8", "10000"),
                 ("1024", "8", "16", "4000"), ("4096", "16", "16", "1000")):
+        env = dict(os.environ)
+        if cfg[0] == nic:
+            env["RXPIPE_HASH"] = "nic"
+            cfg = cfg[1:]
         # the host core's rate swings run to run on a shared host: three
         # fresh processes per row, the median one reported with all three rates
         samples, err = [], None
         for _ in range(reps):
             try:
-                r = subprocess.run([exe, *cfg], capture_output=True, text=True, timeout=120)
+                r = subprocess.run([exe, *cfg], capture_output=True, text=True, timeout=120, env=env)
             except subprocess.TimeoutExpired:
                 err = {"burst": int(cfg[0]), "error": "timeout"}
                 break

@@ -307,6 +307,38 @@ def test_gpu_dense_verdict1(g, orc, wl, R, T):
     assert (c == ce).all() and (st == se).all()
 
 
+@pytest.mark.parametrize("wl,R,T,vb,store", [(0, 16, 8, 1, 2), (0, 16, 8, 1, 0), (0, 16, 8, 2, 2),
+                                              (1, 1024, 4, 2, 2), (1, 1024, 4, 2, 0)])
+def test_gpu_dense_vstage(g, orc, wl, R, T, vb, store, monkeypatch):
+    """GCL_TUNE_VSTAGE=1 (measured, off by default): full dense tiles' 1- and
+    2-B verdicts staged in LDS and stored by NT/4 lanes as whole lines, the
+    partial last tile stored per lane; write-through and plain stores; 256-
+    (udp64) and 512-lane (1024-runtime tcp1500) blocks."""
+    monkeypatch.setenv("GCL_TUNE_VSTAGE", "1")
+    monkeypatch.setenv("GCL_TUNE_NT_STORE", str(store))
+    stride = {0: 64, 1: 1536}[wl]
+    n = 40000 + 77
+    df = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
+    cdf = orc.zipf_cdf(1 << 16) if wl == 1 else None
+    g.generate(wl, n, stride, R, df, seed=13, zipf_cdf_dev=dev(cdf.view(np.int64)) if cdf is not None else None,
+               nflows=0 if cdf is None else len(cdf))
+    frames = df.cpu().numpy()
+    del df
+    tb = 3 if vb == 1 else 4
+    clf = g.Classifier(0, R, g.HASH_JENKINS, g.CFG_VERDICT1 if vb == 1 else g.CFG_VERDICT2, thread_bits=tb)
+    t = orc.Tables(R, g.HASH_JENKINS, 0, g.F_RSS_HASH | g.F_IP_CKSUM_GOOD)
+    for r in range(R):
+        act = r % T
+        fl = g.steer_flows(T, list(range(act))) if act else None
+        clf.runtime_set(r, g.runtime_ip(r), T, act, fl)
+        t.runtime_set(r, orc.runtime_ip(r), T, act, fl)
+    v, c, st = gpu_run(g, clf, frames, n, stride)
+    ve, ce, se = t.classify(frames, n, stride)
+    w = to_verdict1(ve, [T] * R, tb) if vb == 1 else to_verdict2(ve, [T] * R, tb)
+    assert_same(v, w, f"vstage wl={wl} vb={vb} store={store}")
+    assert (c == ce).all() and (st == se).all()
+
+
 def test_gpu_verdict1_limits(g):
     """More than 128 queues, thread_bits past 7, or VERDICT1 with VERDICT2,
     VERDICT4 or TRANS_HASH does not open; kthreads past 1 << thread_bits are

@@ -189,9 +189,15 @@ int main(int argc, char **argv)
 		return 1;
 	}
 
+	/* RXPIPE_HASH=nic: the flow hash is the mbuf's hash.rss, as rx.c:83 passes
+	 * it (GCL_HASH_NIC, rss[] submitted with the offsets); default: JENKINS, the
+	 * 5-tuple lookup3 computed on the GPU (no NIC in the loop) */
+	const bool nic = getenv("RXPIPE_HASH") && !strcmp(getenv("RXPIPE_HASH"), "nic");
 	/* ingress region: udp64 frames generated on the GPU, copied to pinned host memory */
 	uint8_t *dfr, *region;
+	uint32_t *drss;
 	CHECK(hipMalloc(&dfr, nframes * stride));
+	CHECK(hipMalloc(&drss, nframes * 4));
 	CHECK(hipMemset(dfr, 0, nframes * stride));
 	struct gcl_gen_params gp = {};
 	gp.workload = GCL_WL_UDP64;
@@ -200,15 +206,18 @@ int main(int argc, char **argv)
 	gp.n = nframes;
 	gp.stride = stride;
 	gp.world = 1;
-	if (gcl_generate(&gp, dfr, nullptr, nullptr, nullptr))
+	if (gcl_generate(&gp, dfr, nullptr, drss, nullptr))
 		return 1;
+	std::vector<uint32_t> rss(nframes);
+	CHECK(hipMemcpy(rss.data(), drss, nframes * 4, hipMemcpyDeviceToHost));
+	CHECK(hipFree(drss));
 	CHECK(hipHostMalloc((void **)&region, nframes * stride, hipHostMallocMapped));
 	CHECK(hipMemcpy(region, dfr, nframes * stride, hipMemcpyDeviceToHost));
 	CHECK(hipFree(dfr));
 
 	struct gcl_cfg cfg = {};
 	cfg.max_runtimes = R;
-	cfg.hash_mode = GCL_HASH_JENKINS;
+	cfg.hash_mode = nic ? GCL_HASH_NIC : GCL_HASH_JENKINS;
 	cfg.flags = GCL_CFG_VERDICT4;
 	cfg.default_olflags = GCL_F_RSS_HASH | GCL_F_IP_CKSUM_GOOD;
 	struct gcl_ctx *ctx;
@@ -290,7 +299,8 @@ int main(int argc, char **argv)
 				const uint64_t ts = ticks();
 				t_sub[head % depth] = ts;
 				const int64_t r = gcl_rxloop_submit(loop, burst, &offs[(size_t)b * burst], nullptr,
-				                                    nullptr, nullptr, nullptr);
+				                                    nic ? &rss[(size_t)b * burst] : nullptr, nullptr,
+				                                    nullptr);
 				if (timed && (head & 7) == 0) {
 					t_submit += ticks() - ts;
 					n_sub++;
@@ -377,13 +387,14 @@ int main(int argc, char **argv)
 	std::sort(lat.begin(), lat.end());
 	const double pkts = (double)burst * nbursts;
 	const double sub_pkts = (double)burst * (n_sub ? n_sub : 1), tail_pkts = (double)burst * (n_tail ? n_tail : 1);
-	printf("{\"burst\": %u, \"workers\": %u, \"depth\": %u, \"bursts\": %u, \"verdicts\": \"%s\", "
+	printf("{\"burst\": %u, \"workers\": %u, \"depth\": %u, \"bursts\": %u, \"hash\": \"%s\", "
+	       "\"verdicts\": \"%s\", "
 	       "\"mpps_one_core\": %.2f, "
 	       "\"burst_latency_p50_us\": %.2f, \"burst_latency_p99_us\": %.2f, "
 	       "\"deliver_ns_per_pkt\": %.2f, \"submit_ns_per_pkt\": %.2f, \"wait_ns_per_pkt\": %.2f, "
 	       "\"delivered_check\": \"%s\", \"unicast_fail\": %llu, \"host_cpu\": %d, "
 	       "\"bursts_early\": %llu, \"bursts_stale\": %llu, \"bursts_late\": %llu}\n",
-	       burst, workers, depth, nbursts,
+	       burst, workers, depth, nbursts, nic ? "nic (hash.rss, rx.c:83)" : "jenkins",
 	       copy_out ? "copied out" : inline_hdrs ? "read in place, headers inlined in the slot"
 	       : hdr_records ? "read in place, stamped header records in the slot" : "read in place",
 	       pkts / (el * 1e-3), lat[lat.size() / 2] * ns_tick * 1e-3,
