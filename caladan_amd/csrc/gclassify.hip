@@ -2134,17 +2134,26 @@ __global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
 			hint = q[3].w;
 		} else {
 			uint4 r[4] = {};
+			uint32_t olw = 0;
 			if (live) {
+				/* the offset first (a late burst's own round trip); then the
+				 * side arrays and the frames, all in flight together.  The
+				 * side loads issued between the offset's load and its use
+				 * made that use wait for them as well (vmcnt counts in
+				 * order, and the early path shares the use): two round trips */
 				const uint64_t ent = early ? e : gcl::ld_sys64(slot + L.off_offs + 8 * lane);
+				off = ent & kLoopOffMask;
+				/* keeps the side loads below the offset's use (the scheduler
+				 * would hoist them above it, and its wait with them) */
+				asm volatile("" : : "v"((uint32_t)off), "v"((uint32_t)(off >> 32)) : "memory");
 				if (fl & GCL_LOOP_F_OLF)
-					olf = (gcl::ld_sys32(slot + L.off_olf + (lane & ~3)) >> (8 * (lane & 3))) & 0xFF;
+					olw = gcl::ld_sys32(slot + L.off_olf + (lane & ~3));
 				if (fl & GCL_LOOP_F_RSS)
 					rss = gcl::ld_sys32(slot + L.off_rss + 4 * lane);
 				if (fl & GCL_LOOP_F_FDIR)
 					fdir = gcl::ld_sys32(slot + L.off_fdir + 4 * lane);
 				if (fl & GCL_LOOP_F_HINT)
 					hint = gcl::ld_sys32(slot + L.off_hint + 4 * lane);
-				off = ent & kLoopOffMask;
 #pragma unroll
 				for (int j = 0; j < 4; j++) {
 					if (L.off_hdr) { /* granules inlined in the slot by the host */
@@ -2156,6 +2165,7 @@ __global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
 					}
 				}
 			}
+			olf = (olw >> (8 * (lane & 3))) & 0xFF;
 			hw.d3 = r[0].w, hw.d5 = r[1].y, hw.d6 = r[1].z, hw.d7 = r[1].w;
 			hw.d8 = r[2].x, hw.d9 = r[2].y, hw.d10 = r[2].z;
 		}
