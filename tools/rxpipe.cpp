@@ -290,12 +290,42 @@ int main(int argc, char **argv)
 	/* the submit / wait / deliver split is sampled on every 8th burst; the
 	 * latency (submit -> delivered) is taken on every one */
 	uint64_t delivered = 0, t_deliver = 0, t_submit = 0, t_wait = 0, seq = 0, n_sub = 0, n_tail = 0;
+	/* RXPIPE_GAP_NS (depth 1): spin this long after a burst's delivery before
+	 * the next submit, or "rand": a uniform [0, 2000) ns per burst, so that
+	 * the submit lands at any phase of the worker's polls (which start when
+	 * it has stored the previous burst's records) as bursts from a NIC do */
+	const char *gap_env = getenv("RXPIPE_GAP_NS");
+	const bool gap_rand = gap_env && !strcmp(gap_env, "rand");
+	const uint64_t gap_fixed = gap_env && !gap_rand ? strtoull(gap_env, nullptr, 0) : 0;
+	double ticks_per_ns = 1.0;
+	{
+		const uint64_t n0 = now_ns(), k0 = ticks();
+		while (now_ns() - n0 < 20000000ull)
+			;
+		ticks_per_ns = (double)(ticks() - k0) / (double)(now_ns() - n0);
+	}
+	uint64_t gap_state = 0x9E3779B97F4A7C15ull;
+	auto gap_spin = [&]() {
+		if (depth != 1 || (!gap_rand && !gap_fixed))
+			return;
+		uint64_t g = gap_fixed;
+		if (gap_rand) {
+			gap_state ^= gap_state << 13;
+			gap_state ^= gap_state >> 7;
+			gap_state ^= gap_state << 17;
+			g = gap_state % 2000;
+		}
+		const uint64_t end = ticks() + (uint64_t)(g * ticks_per_ns);
+		while (ticks() < end)
+			__builtin_ia32_pause();
+	};
 	/* @count bursts with up to @depth in flight, in ticket order */
 	auto pump = [&](uint32_t count, bool timed) {
 		uint32_t head = 0, tail = 0;
 		while (tail < count) {
 			while (head < count && head - tail < depth) {
 				const uint32_t b = (uint32_t)((seq + head) % nb);
+				gap_spin();
 				const uint64_t ts = ticks();
 				t_sub[head % depth] = ts;
 				const int64_t r = gcl_rxloop_submit(loop, burst, &offs[(size_t)b * burst], nullptr,
@@ -388,13 +418,14 @@ int main(int argc, char **argv)
 	const double pkts = (double)burst * nbursts;
 	const double sub_pkts = (double)burst * (n_sub ? n_sub : 1), tail_pkts = (double)burst * (n_tail ? n_tail : 1);
 	printf("{\"burst\": %u, \"workers\": %u, \"depth\": %u, \"bursts\": %u, \"hash\": \"%s\", "
-	       "\"verdicts\": \"%s\", "
+	       "\"gap_ns\": \"%s\", \"verdicts\": \"%s\", "
 	       "\"mpps_one_core\": %.2f, "
 	       "\"burst_latency_p50_us\": %.2f, \"burst_latency_p99_us\": %.2f, "
 	       "\"deliver_ns_per_pkt\": %.2f, \"submit_ns_per_pkt\": %.2f, \"wait_ns_per_pkt\": %.2f, "
 	       "\"delivered_check\": \"%s\", \"unicast_fail\": %llu, \"host_cpu\": %d, "
 	       "\"bursts_early\": %llu, \"bursts_stale\": %llu, \"bursts_late\": %llu}\n",
 	       burst, workers, depth, nbursts, nic ? "nic (hash.rss, rx.c:83)" : "jenkins",
+	       gap_rand ? "rand [0, 2000)" : gap_env ? gap_env : "0",
 	       copy_out ? "copied out" : inline_hdrs ? "read in place, headers inlined in the slot"
 	       : hdr_records ? "read in place, stamped header records in the slot" : "read in place",
 	       pkts / (el * 1e-3), lat[lat.size() / 2] * ns_tick * 1e-3,
