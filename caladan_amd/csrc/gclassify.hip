@@ -1434,6 +1434,8 @@ struct LoopParams {
 	                              records (else the poller, GCL_TUNE_LOOP_WRITER=0) */
 	uint32_t lean;             /* rxloop64_kernel: plain-IPv4 bursts on classify_lean
 	                              (GCL_TUNE_LOOP_LEAN=0: always classify_core) */
+	uint32_t dual;             /* rxloop64_kernel: two polls in flight, the second this
+	                              many s_memrealtime ticks after the first (0: one) */
 };
 
 /* GCL_LOOP_HDR_RECORDS: the submitting core writes each packet as one 64-B
@@ -2037,40 +2039,105 @@ __global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
 		uint4 q[4] = {}, qv[4] = {};
 		uint64_t t_issue = 0, hit = 0;
 		uint32_t npoll = 0;
-		for (uint32_t kk = 0;; kk++) {
-			t_issue = __builtin_amdgcn_s_memrealtime();
-			npoll = kk + 1;
-			const bool sp = spec && t_issue < spec_end;
-			const uint64_t ev = sp && !rec ? gcl::ld_sys64(slot + L.off_offs + 8 * lane) : 0;
-			if (sp && rec) {
+		/* GCL_TUNE_LOOP_DUAL (experiment): two polls in flight, the second
+		 * issued half a round trip after the first, so the slot is sampled
+		 * twice per round trip: half the wait for a burst that lands just
+		 * after a sample */
+		struct PollSet {
+			uint64_t ev, wv, t_issue;
+			uint4 q[4];
+			uint32_t sv;
+			bool sp;
+		};
+		auto issue = [&](PollSet &P, uint32_t kk) {
+			P.t_issue = __builtin_amdgcn_s_memrealtime();
+			P.sp = spec && P.t_issue < spec_end;
+			P.ev = P.sp && !rec ? gcl::ld_sys64(slot + L.off_offs + 8 * lane) : 0;
 #pragma unroll
-				for (int j = 0; j < 4; j++) {
+			for (int j = 0; j < 4; j++) {
+				if (P.sp && rec) {
 					const auto v = __builtin_amdgcn_raw_buffer_load_b128(
 					        srs, (int)(L.off_hdr + L.rec_plane * j + 16 * lane), 0, gcl::kSysAux);
-					qv[j] = make_uint4(v[0], v[1], v[2], v[3]);
+					P.q[j] = make_uint4(v[0], v[1], v[2], v[3]);
+				} else {
+					P.q[j] = make_uint4(0, 0, 0, 0);
 				}
 			}
-			uint64_t wv = 0;
-			uint32_t sv = 0;
+			P.wv = 0;
+			P.sv = 0;
 			if (lane == 0) {
-				wv = gcl::ld_sys64(&h->word);
-				if ((kk & 7) == 7) /* a stop waits for up to 8 polls */
-					sv = gcl::ld_sys32(L.stop);
+				P.wv = gcl::ld_sys64(&h->word);
+				if ((kk & 7) >= 6) /* a stop waits for up to 8 polls */
+					P.sv = gcl::ld_sys32(L.stop);
 			}
-			wv = lane0_u64(wv);
-			sv = (uint32_t)__builtin_amdgcn_readfirstlane((int)sv);
+		};
+		/* true: leave the wait (the burst, a stop, or the lifetime's end) */
+		auto check = [&](PollSet &P, uint32_t kk) -> bool {
+			const uint64_t wv = lane0_u64(P.wv);
+			const uint32_t sv = (uint32_t)__builtin_amdgcn_readfirstlane((int)P.sv);
 			if ((wv >> 24) == (t & ((1ull << 40) - 1))) {
 				w = wv;
-				e = ev;
-				sp_hit = sp;
+				e = P.ev;
+				sp_hit = P.sp;
+				t_issue = P.t_issue;
+				npoll = kk + 1;
 #pragma unroll
 				for (int j = 0; j < 4; j++)
-					q[j] = qv[j];
-				break;
+					q[j] = P.q[j];
+				return true;
 			}
-			if (sv || __builtin_amdgcn_s_memrealtime() > t_end)
-				break;
-			__builtin_amdgcn_s_sleep(1);
+			return sv || __builtin_amdgcn_s_memrealtime() > t_end;
+		};
+		if (L.dual) {
+			PollSet A, B;
+			issue(A, 0);
+			while (__builtin_amdgcn_s_memrealtime() < A.t_issue + L.dual)
+				__builtin_amdgcn_s_sleep(1);
+			issue(B, 1);
+			for (uint32_t kk = 0;; kk += 2) {
+				if (check(A, kk))
+					break;
+				issue(A, kk + 2);
+				if (check(B, kk + 1))
+					break;
+				issue(B, kk + 3);
+			}
+		} else {
+			for (uint32_t kk = 0;; kk++) {
+				t_issue = __builtin_amdgcn_s_memrealtime();
+				npoll = kk + 1;
+				const bool sp = spec && t_issue < spec_end;
+				const uint64_t ev = sp && !rec ? gcl::ld_sys64(slot + L.off_offs + 8 * lane) : 0;
+				if (sp && rec) {
+	#pragma unroll
+					for (int j = 0; j < 4; j++) {
+						const auto v = __builtin_amdgcn_raw_buffer_load_b128(
+						        srs, (int)(L.off_hdr + L.rec_plane * j + 16 * lane), 0, gcl::kSysAux);
+						qv[j] = make_uint4(v[0], v[1], v[2], v[3]);
+					}
+				}
+				uint64_t wv = 0;
+				uint32_t sv = 0;
+				if (lane == 0) {
+					wv = gcl::ld_sys64(&h->word);
+					if ((kk & 7) == 7) /* a stop waits for up to 8 polls */
+						sv = gcl::ld_sys32(L.stop);
+				}
+				wv = lane0_u64(wv);
+				sv = (uint32_t)__builtin_amdgcn_readfirstlane((int)sv);
+				if ((wv >> 24) == (t & ((1ull << 40) - 1))) {
+					w = wv;
+					e = ev;
+					sp_hit = sp;
+	#pragma unroll
+					for (int j = 0; j < 4; j++)
+						q[j] = qv[j];
+					break;
+				}
+				if (sv || __builtin_amdgcn_s_memrealtime() > t_end)
+					break;
+				__builtin_amdgcn_s_sleep(1);
+			}
 		}
 		if (L.stamps)
 			hit = __builtin_amdgcn_s_memrealtime();
@@ -4187,6 +4254,8 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 	lp.lean = kDefaultLoopLean;
 	if (const char *e = getenv("GCL_TUNE_LOOP_LEAN"))
 		lp.lean = atoi(e) != 0;
+	if (const char *e = getenv("GCL_TUNE_LOOP_DUAL")) /* experiment: ticks of 10 ns */
+		lp.dual = (uint32_t)atoi(e);
 	if (const char *e = getenv("GCL_TUNE_LOOP_CLOCK"))
 		lp.fast_clock = atoi(e) != 0;
 	lp.off_hdr = (cfg->flags & (GCL_LOOP_INLINE_HDRS | GCL_LOOP_HDR_RECORDS))
