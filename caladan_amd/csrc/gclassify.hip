@@ -2071,11 +2071,23 @@ __global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
 					P.sv = gcl::ld_sys32(L.stop);
 			}
 		};
-		/* true: leave the wait (the burst, a stop, or the lifetime's end) */
-		auto check = [&](PollSet &P, uint32_t kk) -> bool {
+		/* true: leave the wait (the burst, a stop, or the lifetime's end).
+		 * @defer: a set that finds the word with a record or offset still
+		 * stale is passed over once, when the other set -- issued half a
+		 * round trip later -- will likely bring them current */
+		auto check = [&](PollSet &P, uint32_t kk, bool defer) -> bool {
 			const uint64_t wv = lane0_u64(P.wv);
 			const uint32_t sv = (uint32_t)__builtin_amdgcn_readfirstlane((int)P.sv);
 			if ((wv >> 24) == (t & ((1ull << 40) - 1))) {
+				if (defer && P.sp) {
+					const uint32_t n1 = (uint32_t)(wv >> 11) & 0x1FFF;
+					const bool cur = (uint32_t)lane >= n1 ||
+					                 (rec ? P.q[0].x == rstamp && P.q[1].x == rstamp &&
+					                                P.q[2].x == rstamp && P.q[3].x == rstamp
+					                      : (P.ev & ~kLoopOffMask) == stamp);
+					if (n1 <= 64 && !__all(cur))
+						return false;
+				}
 				w = wv;
 				e = P.ev;
 				sp_hit = P.sp;
@@ -2094,12 +2106,25 @@ __global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
 			while (__builtin_amdgcn_s_memrealtime() < A.t_issue + L.dual)
 				__builtin_amdgcn_s_sleep(1);
 			issue(B, 1);
+			/* a set passed over as stale is taken as it is on its next
+			 * check only if the other set did not bring the burst first */
+			bool stale_a = false, stale_b = false;
 			for (uint32_t kk = 0;; kk += 2) {
-				if (check(A, kk))
+				if (check(A, kk, !stale_a))
 					break;
+				stale_a = (lane0_u64(A.wv) >> 24) == (t & ((1ull << 40) - 1));
+				if (stale_a) { /* the word is there: B, half a round trip on, decides */
+					if (check(B, kk + 1, false))
+						break;
+				}
 				issue(A, kk + 2);
-				if (check(B, kk + 1))
+				if (check(B, kk + 1, !stale_b))
 					break;
+				stale_b = (lane0_u64(B.wv) >> 24) == (t & ((1ull << 40) - 1));
+				if (stale_b) {
+					if (check(A, kk + 2, false))
+						break;
+				}
 				issue(B, kk + 3);
 			}
 		} else {
