@@ -582,6 +582,9 @@ def test_rxloop_rejects_bad_args(g):
     assert g.lib.gcl_rxloop_wait(None, 1, None, 0) == -22
     assert g.lib.gcl_rxloop_stop(None) == -22
     assert g.lib.gcl_rxloop_drive(None, 1, 4096, 1, 1, None, None) == -22
+    cnt = np.zeros(3, dtype=np.uint64)
+    assert g.lib.gcl_rxloop_poll_stats(None, cnt.ctypes.data) == -22
+    assert g.lib.gcl_rxloop_lean_bursts(None, cnt.ctypes.data) == -22
     assert ctypes.sizeof(g.GclRxloopCfg) == 56
 
 
