@@ -1377,6 +1377,8 @@ constexpr uint32_t kDefaultLoopWriter = 0;
 /* GCL_TUNE_LOOP_LEAN default: bursts whose every packet is plain IPv4 (IHL 5,
  * no FDIR mark, no hint) classified by classify_lean */
 constexpr uint32_t kDefaultLoopLean = 1;
+/* GCL_TUNE_LOOP_HYBRID default (s_memrealtime ticks, 0 = off) */
+constexpr uint32_t kDefaultLoopHybrid = 0;
 /* how a worker's bursts arrived (gcl_rxloop_poll_stats): with the poll that
  * found the word; eligible for that, but an entry or record still stale so
  * read after it; or after the word, the speculative window over or the
@@ -1436,6 +1438,8 @@ struct LoopParams {
 	                              (GCL_TUNE_LOOP_LEAN=0: always classify_core) */
 	uint32_t dual;             /* rxloop64_kernel: two polls in flight, the second this
 	                              many s_memrealtime ticks after the first (0: one) */
+	uint32_t hybrid;           /* rxloop64_kernel: a caught-up worker's first poll this
+	                              many ticks after its last records (GCL_TUNE_LOOP_HYBRID) */
 };
 
 /* GCL_LOOP_HDR_RECORDS: the submitting core writes each packet as one 64-B
@@ -2013,6 +2017,11 @@ __global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
 	Tables tb = {};
 	uint32_t cur_seq = 0xFF; /* no image yet (versions are taken mod 64) */
 	uint32_t mb = 0;
+	/* hybrid polling (L.hybrid): the previous burst's wait took more than
+	 * one poll (the worker had caught up with the host), and when its
+	 * records were issued */
+	uint32_t prev_npoll = 1;
+	uint64_t t_done = 0;
 	const bool spec = L.spec, rec = L.hdr_rec;
 
 	for (uint64_t t = L.t0 + blockIdx.x + 1;; t += L.workers) {
@@ -2033,6 +2042,17 @@ __global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
 		 * profiles/r04_loop64_ab.jsonl) */
 		const uint64_t stamp = loop_stamp(t, L.nslots);
 		const uint32_t rstamp = loop_rec_stamp(t, L.nslots);
+		/* Hybrid polling: a worker that had to wait for its last burst has
+		 * caught up with the host, whose next submit cannot land before it
+		 * has seen that burst's records (a PCIe write, then its post-pass):
+		 * a poll issued at once samples the slot too early and puts the
+		 * next samples a whole round trip apart from then on.  Its first
+		 * poll waits L.hybrid ticks after the records went out instead (as
+		 * NVMe hybrid polling sleeps before it spins).  A worker with bursts
+		 * queued (found on its first poll) never waits. */
+		if (L.hybrid && prev_npoll > 1)
+			while (__builtin_amdgcn_s_memrealtime() < t_done + L.hybrid)
+				__builtin_amdgcn_s_sleep(1);
 		const uint64_t spec_end = __builtin_amdgcn_s_memrealtime() + L.spec_ticks;
 		uint64_t w = 0, e = 0;
 		bool sp_hit = false;
@@ -2337,6 +2357,9 @@ __global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
 		if (lane == 0)
 			__hip_atomic_store(&m.flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 		mb ^= 1;
+		prev_npoll = npoll;
+		if (L.hybrid)
+			t_done = __builtin_amdgcn_s_memrealtime();
 	}
 	/* the writer drains what was posted, then leaves; the host stops
 	 * publishing on this word (one it reads without a HIP call per burst) */
@@ -4281,6 +4304,9 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 		lp.lean = atoi(e) != 0;
 	if (const char *e = getenv("GCL_TUNE_LOOP_DUAL")) /* experiment: ticks of 10 ns */
 		lp.dual = (uint32_t)atoi(e);
+	lp.hybrid = kDefaultLoopHybrid;
+	if (const char *e = getenv("GCL_TUNE_LOOP_HYBRID")) /* ticks of 10 ns, 0: off */
+		lp.hybrid = (uint32_t)atoi(e);
 	if (const char *e = getenv("GCL_TUNE_LOOP_CLOCK"))
 		lp.fast_clock = atoi(e) != 0;
 	lp.off_hdr = (cfg->flags & (GCL_LOOP_INLINE_HDRS | GCL_LOOP_HDR_RECORDS))
