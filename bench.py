@@ -131,6 +131,137 @@ def emit_json(obj):
         os.write(_JSON_FD, line)
 
 
+# The driver keeps only the tail of stdout (~8.5 KB): round 4's 23-KB line
+# was cut and never parsed.  The stdout line is the summary below, held
+# under LINE_LIMIT bytes; the full result goes to DETAIL_PATH and stderr.
+LINE_LIMIT = 8192
+DETAIL_PATH = os.environ.get("GCL_BENCH_DETAIL", os.path.join("gpurun_out", "bench_detail.json"))
+CONTRACT_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                 "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config")
+
+
+def _pick(d, *keys):
+    """The keys of dict @d that exist (nested dicts are never walked)."""
+    if not isinstance(d, dict):
+        return None
+    return {k: d[k] for k in keys if k in d}
+
+
+def _roof(r, *extra):
+    return _pick(r, "bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_source",
+                 "kernel_ms", "bytes_per_pkt", "ceiling_ms", "frac_of_ceiling", *extra)
+
+
+def _cpu_mode(m):
+    return _pick(m, "1core_mpps", "1core_lrpc_mpps", "all_cores_mpps", "all_cores", "spread")
+
+
+def _pipe_row(rows, burst, workers, verdicts, hash_prefix):
+    for r in rows or ():
+        if (r.get("burst") == burst and r.get("workers") == workers and
+                r.get("verdicts") == verdicts and str(r.get("hash", "")).startswith(hash_prefix)):
+            return _pick(r, "mpps_one_core", "burst_latency_p50_us", "burst_latency_p99_us",
+                         "delivered_check", "mpps_samples")
+    return None
+
+
+def compact(result, detail_path=DETAIL_PATH):
+    """The stdout line: the contract keys plus one summary row per measured
+    section (the VERDICT r04 list), every other field in the detail file."""
+    out = {k: result[k] for k in CONTRACT_KEYS if k in result}
+    if "roofline" in result:
+        out["roofline"] = _roof(result["roofline"])
+    for k in ("kernel_only",):
+        if k in result:
+            out[k] = _pick(result[k], "value", "unit", "ms_per_step", "gpu_ms_per_step")
+    for k in ("counts_check", "exchange", "e2e_multi", "launch"):
+        if k in result:
+            out[k] = result[k]
+    if "placement" in result:
+        p = result["placement"]
+        out["placement"] = _pick(p, "probe_us_chosen", "classes_seen", "replaced")
+    cpu = result.get("cpu_baseline")
+    if cpu:
+        out["cpu_baseline"] = {**_pick(cpu, "value", "unit", "cores", "kind", "sample", "pinning",
+                                       "cpu_model", "nproc", "seconds", "gpu_over_1core_nic"),
+                               "nic_mode": _cpu_mode(cpu.get("nic_mode")),
+                               "jenkins_mode": _cpu_mode(cpu.get("jenkins_mode"))}
+    grp = result.get("group")
+    if grp:
+        out["group"] = _pick(grp, "n_gpus", "exchange", "value", "gpu_ms_per_step", "counts_check", "error")
+    node = result.get("group_node")
+    if node:
+        out["group_node"] = _pick(node, "n_gpus", "value", "ms_per_step", "counts_check", "error")
+    sec = result.get("secondary")
+    if sec:
+        s = {"workload": "tcp1500 (config 3)", **_pick(sec, "verdict", "value", "unit", "ms_per_step"),
+             "roofline": _roof(sec.get("roofline", {}))}
+        c3 = sec.get("cpu_baseline", {})
+        if c3:
+            s["cpu_1core_mpps"] = {"nic": c3.get("nic_mode", {}).get("1core_mpps"),
+                                   "jenkins": c3.get("jenkins_mode", {}).get("1core_mpps")}
+        out["secondary"] = s
+        hs = sec.get("header_split_layout")
+        if hs:
+            out["header_split"] = {"value": hs.get("value"), "frac": hs.get("roofline", {}).get("frac"),
+                                   "kernel_ms": hs.get("roofline", {}).get("kernel_ms")}
+        tp = sec.get("udp64_toeplitz")
+        if tp:
+            out["toeplitz"] = {"value": tp.get("value"), "frac": tp.get("roofline", {}).get("frac")}
+        ov = sec.get("udp64_other_verdicts")
+        if ov:
+            out["udp64_other_verdicts"] = {o.get("verdict", "?").split(",")[-1].strip(): o.get("value")
+                                           for o in ov}
+    e2e = result.get("e2e")
+    if e2e:
+        e = {}
+        for name in ("udp64", "mixed"):
+            if name in e2e:
+                e[name] = _pick(e2e[name], "zerocopy_mpps", "copy_hdr_2streams_mpps", "copy_full_frames_mpps")
+        tr = e2e.get("mixed", {}).get("trace_replay")
+        if tr:
+            e["mixed_trace_replay_mpps"] = tr.get("zerocopy_mpps")
+        ing = e2e.get("ingress_pool", {}).get("integrated_nic")
+        if ing:
+            e["ingress_integrated_nic"] = {
+                "device_resident_mpps": ing.get("device_resident_mpps"),
+                "frac": ing.get("roofline", {}).get("frac"),
+                "frac_of_ceiling": ing.get("roofline", {}).get("frac_of_ceiling"),
+                "zerocopy_mpps": ing.get("zerocopy_mpps"), "counts_check": ing.get("counts_check")}
+        rows = e2e.get("rx_burst_pipeline", {}).get("runs")
+        rec = "read in place, stamped header records in the slot"
+        e["pipeline"] = {"records_1x1_nic": _pipe_row(rows, 64, 1, rec, "nic"),
+                         "records_4x8_nic": _pipe_row(rows, 64, 4, rec, "nic"),
+                         "records_1x1_jenkins": _pipe_row(rows, 64, 1, rec, "jenkins"),
+                         "records_4x8_jenkins": _pipe_row(rows, 64, 4, rec, "jenkins")}
+        lp = e2e.get("rxloop", {})
+        for k in ("loop_burst64_w1_d1_hdr_records", "loop_burst64_w4_d8_hdr_records"):
+            if k in lp:
+                e.setdefault("rxloop", {})[k] = _pick(lp[k], "p50_us", "p99_us", "mpps")
+        out["e2e"] = e
+    out["detail"] = detail_path
+    # never past the limit: drop the least central summaries first
+    for k in ("udp64_other_verdicts", "placement", "toeplitz", "header_split", "group_node",
+              "e2e_multi", "exchange", "group", "e2e", "secondary"):
+        if len(json.dumps(out)) < LINE_LIMIT:
+            break
+        out.pop(k, None)
+    return out
+
+
+def emit_result(result):
+    """Full result to DETAIL_PATH and stderr, the compact line to stdout."""
+    full = json.dumps(result)
+    try:
+        os.makedirs(os.path.dirname(DETAIL_PATH) or ".", exist_ok=True)
+        with open(DETAIL_PATH, "w") as f:
+            f.write(full + "\n")
+    except OSError as e:
+        log(f"bench.py: could not write {DETAIL_PATH}: {e}")
+    log("bench detail:", full)
+    emit_json(compact(result))
+
+
 def setup_tables(clf, R, T, seed=SEED):
     """Runtime r owns 10.0.0.(r+1); active kthreads seeded in [1, T];
     flow tables from the sched_steer_flows rule (gcl_steer_flows)."""
@@ -640,24 +771,44 @@ def grouppipe_run(ndev, n=8 << 20, iters=5):
     return json.loads(r.stdout.strip().splitlines()[-1])
 
 
-def pmc_traffic(name, vbytes):
-    """HBM bytes per launch from the committed PMC passes (profiles/pmc_*.json,
-    tools/prof_summary.py: FETCH_SIZE + WRITE_SIZE, gfx950-corrected)."""
-    prof = os.path.join(ROOT, "profiles", f"pmc_{name}{'' if vbytes == 8 else f'_v{vbytes}'}.json")
-    if not os.path.exists(prof):
-        return None
+# a committed PMC pass stands for this run's launch only if its kernel time
+# is within this of the launch time measured here (a stale profile of a
+# different kernel build or placement is dropped, not passed off as current)
+PMC_TIME_SLACK = 0.15
+
+
+def pmc_traffic(name, vbytes, kernel_ms=None, scale=1.0):
+    """(HBM bytes per launch, source label) from the committed PMC passes
+    (profiles/pmc_*.json, tools/prof_summary.py: FETCH_SIZE + WRITE_SIZE,
+    gfx950-corrected), scaled by @scale packets; (None, label) when there is
+    no profile or its kernel time disagrees with @kernel_ms.  The counters are
+    NOT taken in this run: rocprofv3 --pmc cannot run under the bench's own
+    timing, so the label names the file and the kernel time it was taken at."""
+    rel = f"profiles/pmc_{name}{'' if vbytes == 8 else f'_v{vbytes}'}.json"
     try:
-        with open(prof) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
+        with open(os.path.join(ROOT, rel)) as f:
+            prof = json.load(f)
     except (OSError, ValueError):
-        return None
+        return None, None
+    traffic = prof.get("hbm_bytes_per_launch")
+    avg_ms = (prof.get("avg_kernel_ns") or 0) / 1e6 * scale
+    label = f"{rel}: committed PMC pass, not this run's counters; kernel avg {avg_ms:.4f} ms there"
+    if traffic is None:
+        return None, label
+    if kernel_ms and avg_ms and abs(avg_ms / kernel_ms - 1) > PMC_TIME_SLACK:
+        return None, label + f" vs {kernel_ms:.4f} ms here: dropped as stale"
+    return traffic * scale, label
 
 
 def roofline_obj(bytes_per_launch, kernel_ms, traffic, extra=None, bound="hbm", peak=HBM_PEAK_GBS):
+    """@traffic: None, or (bytes, source label) from pmc_traffic."""
+    traffic, source = traffic if isinstance(traffic, tuple) else (traffic, None)
     achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
     r = {"bound": bound, "achieved": round(achieved, 1), "peak": peak, "unit": "GB/s",
          "frac": round(achieved / peak, 4), "traffic": traffic,
          "kernel_ms": round(kernel_ms, 4)}
+    if source:
+        r["traffic_source"] = source
     if extra:
         r.update(extra)
     if traffic:
@@ -671,9 +822,7 @@ def roofline(w, kernel_ms):
     """The roofline object of one workload's classify launch.  The committed
     PMC passes were taken at the workload's default batch size, so their
     bytes are scaled per packet to this launch's (strong scaling)."""
-    traffic = pmc_traffic(w.name, w.vbytes)
-    if traffic is not None:
-        traffic = traffic / WORKLOADS[w.name][1] * w.n
+    traffic = pmc_traffic(w.name, w.vbytes, kernel_ms, w.n / WORKLOADS[w.name][1])
     return roofline_obj(w.n * w.bytes_per_pkt, kernel_ms, traffic,
                         {"bytes_per_pkt": w.bytes_per_pkt})
 
@@ -1010,7 +1159,7 @@ def ingress_pool_bench(device, vbytes, cycles=64, reps=10, zerocopy=True,
             "what": "offs[] + ol_flags[] + hash.rss[] per descriptor, GCL_HASH_NIC (INTEGRATION.md §4)",
             "device_resident_mpps": round(n / wall / 1e6, 1),
             "counts_check": "ok" if counts_ok() else "MISMATCH",
-            "roofline": roofline_obj(n * bpp, gms, pmc_traffic("ingress_nic", vbytes),
+            "roofline": roofline_obj(n * bpp, gms, pmc_traffic("ingress_nic", vbytes, gms),
                                      {"bytes_per_pkt": bpp,
                                       **ceiling(nic, region, n, 0, dv, gms, offs=offs, olflags=olf,
                                                 rss=rss)})}
@@ -1052,7 +1201,7 @@ def ingress_pool_bench(device, vbytes, cycles=64, reps=10, zerocopy=True,
             "counts_check": "ok" if counts_ok() else "MISMATCH",
             # the working set's frames (~1 MB of header lines) stay in L2:
             # the bound is the L2's, not HBM's (HBM moves 0.26 of its peak)
-            "roofline": roofline_obj(n * bpp, gms_w, pmc_traffic("ingress_ws", vbytes),
+            "roofline": roofline_obj(n * bpp, gms_w, pmc_traffic("ingress_ws", vbytes, gms_w),
                                      {"bytes_per_pkt": bpp}, bound="l2", peak=L2_PEAK_GBS)}
         del offs_w, olf_w, rss_w, order_ws
     if not zerocopy or "nic" not in rows:
@@ -1145,6 +1294,67 @@ CPU_STREAMS = {"udp64": (2 << 20, 0.5), "tcp1500": (512 << 10, 0.25), "mixed": (
 ZIPF_FLOWS = 1 << 20
 
 
+def _proc_stat_idle():
+    """Idle + iowait jiffies of every CPU (/proc/stat), {} on error."""
+    idle = {}
+    try:
+        with open("/proc/stat") as f:
+            for line in f:
+                if line.startswith("cpu") and line[3].isdigit():
+                    p = line.split()
+                    idle[int(p[0][3:])] = int(p[4]) + int(p[5])
+    except (OSError, ValueError, IndexError):
+        return {}
+    return idle
+
+
+def _siblings(cpu):
+    """The SMT siblings of @cpu (sysfs thread_siblings_list), @cpu included."""
+    try:
+        with open(f"/sys/devices/system/cpu/cpu{cpu}/topology/thread_siblings_list") as f:
+            out = set()
+            for part in f.read().strip().split(","):
+                lo, _, hi = part.partition("-")
+                out.update(range(int(lo), int(hi or lo) + 1))
+            return frozenset(out)
+    except (OSError, ValueError):
+        return frozenset((cpu,))
+
+
+def pick_cores(k, allowed=None, idle_a=None, idle_b=None, siblings=_siblings):
+    """@k CPUs on @k distinct physical cores of this process's affinity mask,
+    the idlest cores first (idle jiffies of the CPU and its SMT siblings over
+    100 ms; highest CPU number on a tie, away from CPU 0's housekeeping) --
+    the way tools/rxpipe.cpp pins its host core, and the iokernel its
+    dataplane lcore (dpdk.c:276-280)."""
+    if allowed is None:
+        try:
+            allowed = sorted(os.sched_getaffinity(0))
+        except AttributeError:  # pragma: no cover
+            allowed = list(range(os.cpu_count() or 1))
+    if idle_a is None:
+        idle_a = _proc_stat_idle()
+        time.sleep(0.1)
+        idle_b = _proc_stat_idle()
+    cores = {}
+    for c in allowed:
+        cores.setdefault(siblings(c), []).append(c)
+    ranked = []
+    for sib, cpus in cores.items():
+        idle = sum(idle_b.get(s, 0) - idle_a.get(s, 0) for s in sib)
+        ranked.append((idle, max(cpus), min(cpus)))
+    ranked.sort(reverse=True)
+    return [cpu for _, _, cpu in ranked[:k]]
+
+
+CPU_REPS = 3  # runs per baseline cell, the median reported
+
+
+def _median_rate(samples):
+    s = sorted(samples)
+    return s[len(s) // 2]
+
+
 def cpu_stream(name, n, budget_s, native, threads):
     """rx.c's per-packet work on this host's cores over a sample of stream
     @name, timed on the oracle's restatement (TEST INFRASTRUCTURE, used here
@@ -1174,21 +1384,34 @@ def cpu_stream(name, n, budget_s, native, threads):
     spent = 0.0
     res = {"sample": f"first {n} pkts of the {name} stream ({stride}-B slots, {R} runtimes x {T})",
            "pkts": n}
+    # pinned: one core (the idlest physical core) for the 1-core cells, that
+    # core and the next idlest ones for the all-cores cell
+    cpus = pick_cores(threads)
+    res["cpus"] = cpus
     for mname, mode in (("nic_mode", g.HASH_NIC), ("jenkins_mode", g.HASH_JENKINS)):
         t = tables(mode)
         kw = dict(olflags=olf, rss=rss, pkt_len=pkt_len, direct=True)
-        probe = t.bench(frames, n, stride, threads=1, passes=1, **kw)
-        budget = budget_s * 0.5
-        p1 = max(1, int(budget * 0.45 / max(probe, 1e-6)))
-        s1 = t.bench(frames, n, stride, threads=1, passes=p1, **kw)
-        pl = max(1, p1 // 2)
-        sl = t.bench(frames, n, stride, threads=1, passes=pl, lrpc=True, **kw)
-        pm = max(1, int(budget * 0.3 / max(probe / threads, 1e-6)))
-        sm = t.bench(frames, n, stride, threads=threads, passes=pm, **kw)
-        spent += probe + s1 + sl + sm
-        res[mname] = {"1core_mpps": round(n * p1 / s1 / 1e6, 2),
-                      "1core_lrpc_mpps": round(n * pl / sl / 1e6, 2),
-                      "all_cores_mpps": round(n * pm / sm / 1e6, 2), "all_cores": threads,
+        probe = t.bench(frames, n, stride, threads=1, passes=1, cpus=cpus[:1], **kw)
+        budget = budget_s * 0.5 / CPU_REPS
+        p1 = max(1, int(budget * 0.4 / max(probe, 1e-6)))
+        pl = max(1, int(budget * 0.35 / max(probe * 1.3, 1e-6)))
+        pm = max(1, int(budget * 0.25 / max(probe / len(cpus), 1e-6)))
+        r1, rl, rm = [], [], []
+        # the three cells interleaved, CPU_REPS rounds: a drift of the host
+        # hits every cell alike
+        for _ in range(CPU_REPS):
+            s1 = t.bench(frames, n, stride, threads=1, passes=p1, cpus=cpus[:1], **kw)
+            sl = t.bench(frames, n, stride, threads=1, passes=pl, lrpc=True, cpus=cpus[:1], **kw)
+            sm = t.bench(frames, n, stride, threads=len(cpus), passes=pm, cpus=cpus, **kw)
+            spent += s1 + sl + sm
+            r1.append(round(n * p1 / s1 / 1e6, 2))
+            rl.append(round(n * pl / sl / 1e6, 2))
+            rm.append(round(n * pm / sm / 1e6, 2))
+        spent += probe
+        res[mname] = {"1core_mpps": _median_rate(r1), "1core_lrpc_mpps": _median_rate(rl),
+                      "all_cores_mpps": _median_rate(rm), "all_cores": len(cpus),
+                      "samples": {"1core": r1, "1core_lrpc": rl, "all_cores": rm},
+                      "spread": round(max((max(x) - min(x)) / _median_rate(x) for x in (r1, rl, rm)), 4),
                       "passes": [p1, pl, pm]}
     res["seconds"] = round(spent, 2)
     del frames
@@ -1229,7 +1452,10 @@ def cpu_baseline(budget_s=24.0):
         "value": u["nic_mode"]["1core_mpps"], "unit": "Mpkt/s", "cores": 1, "kind": "port",
         "sample": (f"first {u['pkts']} pkts of the udp64 stream, classify-only rx_one_pkt restatement "
                    f"with rx.c's direct header loads and the NIC's hash.rss (rx.c:83), bursts of 64, "
-                   f"prefetch stride 2, -O3 -march={'native' if native else 'x86-64-v2'}"),
+                   f"prefetch stride 2, -O3 -march={'native' if native else 'x86-64-v2'}; "
+                   f"median of {CPU_REPS} pinned runs"),
+        "pinning": (f"1-core cells on CPU {u['cpus'][0]} (idlest physical core of the affinity mask), "
+                    f"all-cores cells on {len(u['cpus'])} distinct physical cores"),
         "nic_mode": u["nic_mode"], "jenkins_mode": u["jenkins_mode"],
         "streams": {k: v for k, v in streams.items() if k != "udp64"},
         "all_cores_note": (f"{threads} threads: the GPU box's CPU share for one GPU "
@@ -1257,6 +1483,69 @@ def pick_device(local, world, allow_shared):
                              f"refusing to put two ranks on one GPU (--allow-shared-gpu to rehearse)")
         return local % ndev
     return local
+
+
+def free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_envs(n, port, base=None):
+    """The environment torchrun would give each of @n local ranks."""
+    base = dict(os.environ if base is None else base)
+    return [{**base, "RANK": str(r), "WORLD_SIZE": str(n), "LOCAL_RANK": str(r),
+             "LOCAL_WORLD_SIZE": str(n), "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1",
+             "MASTER_PORT": str(port)} for r in range(n)]
+
+
+SPAWN_TIMEOUT_S = float(os.environ.get("GCL_BENCH_SPAWN_TIMEOUT", "1800"))
+
+
+def spawn_ranks(n, argv, timeout_s=SPAWN_TIMEOUT_S):
+    """`bench.py --gpus N` started without a launcher: one fresh rank process
+    per GPU (this process has made no GPU call and only waits), rank 0's
+    JSON line relayed to stdout.  A rank that fails ends the others; the exit
+    code is the worst rank's, and no line is printed unless every rank
+    succeeded -- never a 1-GPU line for --gpus N."""
+    import subprocess
+    port = free_port()
+    procs = []
+    for r, env in enumerate(rank_envs(n, port)):
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    out0 = []
+    import threading
+    rd = threading.Thread(target=lambda: out0.append(procs[0].stdout.read()), daemon=True)
+    rd.start()
+    t0 = time.monotonic()
+    rcs = [None] * n
+    while any(rc is None for rc in rcs):
+        for i, p in enumerate(procs):
+            if rcs[i] is None:
+                rcs[i] = p.poll()
+        failed = any(rc not in (None, 0) for rc in rcs)
+        if failed or time.monotonic() - t0 > timeout_s:
+            time.sleep(5 if failed else 0)  # a failing rank's peers get a moment to report
+            for i, p in enumerate(procs):
+                if p.poll() is None:
+                    p.kill()
+                rcs[i] = p.wait()
+            break
+        time.sleep(0.05)
+    rd.join(timeout=10)
+    bad = [rc for rc in rcs if rc != 0]
+    if bad:
+        log(f"bench.py: --gpus {n} ranks exited {rcs}; no line printed")
+        return max(abs(rc) for rc in bad) or 1
+    lines = [ln for ln in (out0[0] if out0 else b"").decode().splitlines() if ln.startswith("{")]
+    if not lines:
+        log("bench.py: rank 0 printed no JSON line")
+        return 1
+    sys.stdout.write(lines[-1] + "\n")
+    sys.stdout.flush()
+    return 0
 
 
 def main():
@@ -1291,6 +1580,11 @@ def main():
     ap.add_argument("--force-exchange", action="store_true",
                     help="run the multi-GPU step (RCCL all_gather on a side stream) even at N=1")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ and not args.group_child:
+        # no launcher: start the N ranks here, before anything touches a GPU
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     _claim_stdout()
     if args.group_child:  # group_node_line's child: one JSON line, nothing else
         emit_json(group_node_bench(args.group_child, args.steps, args.warmup, args.exchange_every))
@@ -1298,7 +1592,7 @@ def main():
 
     rank, world, local = shard.dist_env()
     if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world} (set by the launcher); using WORLD_SIZE")
     dev_index = pick_device(local, world, args.allow_shared_gpu)
     torch.cuda.set_device(dev_index)
     device = torch.device("cuda", dev_index)
@@ -1463,7 +1757,7 @@ def main():
     if dist_on:
         shard.finish()
     if rank == 0:
-        emit_json(result)
+        emit_result(result)
 
 
 if __name__ == "__main__":

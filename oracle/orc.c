@@ -809,6 +809,7 @@ struct bench_arg {
 	const struct gcl_batch *b;
 	uint64_t lo, hi;
 	int passes, with_lrpc, direct;
+	int cpu; /* pinned to this CPU before the clock starts (-1: not pinned) */
 	pthread_barrier_t *bar;
 };
 
@@ -821,6 +822,12 @@ static void *bench_thread(void *arg)
 	uint64_t stats[GCL_NR_STATS] = { 0 };
 	struct lrpc_set rs = { 0 };
 
+	if (a->cpu >= 0) { /* as the iokernel pins its dataplane lcore, dpdk.c:276-280 */
+		cpu_set_t one;
+		CPU_ZERO(&one);
+		CPU_SET(a->cpu, &one);
+		(void)pthread_setaffinity_np(pthread_self(), sizeof(one), &one);
+	}
 	if (a->with_lrpc)
 		lrpc_set_init(&rs, a->t);
 	/* touch the verdict buffer before the clock starts */
@@ -851,6 +858,12 @@ double orc_bench(const struct orc_tables *t, const struct gcl_batch *b,
 double orc_bench_ex(const struct orc_tables *t, const struct gcl_batch *b,
                     int threads, int passes, unsigned int flags)
 {
+	return orc_bench_pinned(t, b, threads, passes, flags, NULL);
+}
+
+double orc_bench_pinned(const struct orc_tables *t, const struct gcl_batch *b,
+                        int threads, int passes, unsigned int flags, const int *cpus)
+{
 	pthread_t tid[256];
 	struct bench_arg arg[256];
 	pthread_barrier_t bar;
@@ -869,6 +882,7 @@ double orc_bench_ex(const struct orc_tables *t, const struct gcl_batch *b,
 		arg[i].passes = passes;
 		arg[i].with_lrpc = !!(flags & ORC_BENCH_LRPC);
 		arg[i].direct = !!(flags & ORC_BENCH_DIRECT);
+		arg[i].cpu = cpus ? cpus[i] : -1;
 		arg[i].bar = &bar;
 		pthread_create(&tid[i], NULL, bench_thread, &arg[i]);
 	}

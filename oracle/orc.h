@@ -107,6 +107,10 @@ double orc_bench(const struct orc_tables *t, const struct gcl_batch *b,
 #define ORC_BENCH_DIRECT 0x2
 double orc_bench_ex(const struct orc_tables *t, const struct gcl_batch *b,
                     int threads, int passes, unsigned int flags);
+/* orc_bench_ex with thread i pinned to CPU @cpus[i] (a -1 entry, or a NULL
+ * @cpus, leaves a thread unpinned) */
+double orc_bench_pinned(const struct orc_tables *t, const struct gcl_batch *b,
+                        int threads, int passes, unsigned int flags, const int *cpus);
 
 /* orc_classify through the CPU-baseline form (direct header loads, same
  * preconditions as ORC_BENCH_DIRECT; dst_hint is ignored). */

@@ -70,6 +70,7 @@ def _bind(path):
         "orc_runtime_set_trans_seed": (i32, [vp, u16, u32]),
         "orc_bench": (ctypes.c_double, [vp, ctypes.POINTER(Batch), i32, i32, i32]),
         "orc_bench_ex": (ctypes.c_double, [vp, ctypes.POINTER(Batch), i32, i32, u32]),
+        "orc_bench_pinned": (ctypes.c_double, [vp, ctypes.POINTER(Batch), i32, i32, u32, vp]),
         "orc_classify_direct": (None, [vp, ctypes.POINTER(Batch), vp, vp, vp]),
         "orc_generate": (i32, [ctypes.POINTER(GenParams), vp, vp, vp, vp]),
         "orc_runtime_ip": (u32, [u32]),
@@ -296,14 +297,19 @@ class Tables:
         return v, counts, stats
 
     def bench(self, frames, n, stride, threads=1, passes=1, lrpc=False, offs=None, olflags=None,
-              rss=None, fdir_hi=None, pkt_len=None, direct=False):
+              rss=None, fdir_hi=None, pkt_len=None, direct=False, cpus=None):
         """Wall seconds of `passes` classifications on `threads` threads
-        (contiguous shards); direct=True times rx.c's direct-load form."""
+        (contiguous shards); direct=True times rx.c's direct-load form;
+        `cpus`: thread i pinned to CPU cpus[i]."""
         if direct and n and (n - 1) * stride + 54 > frames.nbytes and offs is None:
             raise ValueError("direct bench: a frame's header runs past the buffer")
         b = self._batch(frames, n, stride, offs, olflags, rss, fdir_hi, pkt_len, None)
         flags = (1 if lrpc else 0) | (2 if direct else 0)
-        return self._lib.orc_bench_ex(self.h, ctypes.byref(b), threads, passes, flags)
+        if cpus is None:
+            return self._lib.orc_bench_ex(self.h, ctypes.byref(b), threads, passes, flags)
+        c = np.full(max(threads, 1), -1, dtype=np.int32)
+        c[:min(len(cpus), len(c))] = cpus[:len(c)]
+        return self._lib.orc_bench_pinned(self.h, ctypes.byref(b), threads, passes, flags, c.ctypes.data)
 
 
 def generate(workload, n, stride, nruntimes, seed=0xCA1ADA4, rank=0, world=1, shard_block=0,

@@ -131,3 +131,133 @@ def test_rxpipe_rows_report_the_median_run(bench, monkeypatch):
     assert out["reps_per_row"] == 3 and len(calls) == 3 * len(rows) and len(rows) >= 10
     for r in rows:
         assert r["mpps_one_core"] == 20.0 and r["mpps_samples"] == [10.0, 20.0, 30.0]
+
+
+def _full_result():
+    """A fully populated bench result: round 4's final line (the 23-KB one the
+    driver could not parse, tests/golden/bench_full_r04.json), with the
+    fields added since filled in with fake numbers."""
+    with open(os.path.join(ROOT, "tests", "golden", "bench_full_r04.json")) as f:
+        r = json.load(f)
+    r["roofline"]["traffic_source"] = "profiles/pmc_udp64_v1.json: committed PMC pass, not this run"
+    cpu = r["cpu_baseline"]
+    cpu["pinning"] = "1-core cells on CPU 7, all-cores cells on 16 distinct physical cores"
+    for m in ("nic_mode", "jenkins_mode"):
+        cpu[m]["samples"] = {"1core": [60.0, 61.0, 62.0], "1core_lrpc": [50.0] * 3, "all_cores": [900.0] * 3}
+        cpu[m]["spread"] = 0.0328
+    r["group_node"] = {"n_gpus": 8, "value": 800000.0, "ms_per_step": 0.33, "counts_check": "ok",
+                       "what": "x" * 300, "host_ingress_c": {"rows": ["y" * 100] * 20}}
+    return r
+
+
+def test_compact_line_fits_the_driver(bench):
+    """The stdout line stays under 8 KB with every section populated, and
+    keeps the contract keys, the roofline and the CPU baseline."""
+    full = _full_result()
+    assert len(json.dumps(full)) > 16000  # the detail really is large
+    line = bench.compact(full)
+    n = len(json.dumps(line))
+    assert n < bench.LINE_LIMIT, n
+    for k in bench.CONTRACT_KEYS:
+        assert line[k] == full[k]
+    rf = line["roofline"]
+    assert rf["frac"] == full["roofline"]["frac"] and "frac_of_ceiling" in rf and "traffic_source" in rf
+    cb = line["cpu_baseline"]
+    assert cb["value"] == full["cpu_baseline"]["value"] and cb["cores"] == 1 and cb["kind"] == "port"
+    assert cb["nic_mode"]["1core_lrpc_mpps"] and cb["jenkins_mode"]["all_cores_mpps"]
+    assert line["secondary"]["roofline"]["frac"] == full["secondary"]["roofline"]["frac"]
+    assert line["header_split"]["value"] and line["toeplitz"]["value"] and line["group"]["counts_check"] == "ok"
+    assert line["group_node"]["n_gpus"] == 8
+    e = line["e2e"]
+    assert e["udp64"]["zerocopy_mpps"] and e["ingress_integrated_nic"]["frac"]
+    for k in ("records_1x1_nic", "records_4x8_nic"):
+        assert e["pipeline"][k]["mpps_one_core"] > 0
+    assert line["detail"]
+
+
+def test_compact_line_sheds_sections_past_the_limit(bench):
+    """Even an oversized summary is cut below the limit, contract keys kept."""
+    full = _full_result()
+    full["config"]["workload"] = "w" * 1000
+    full["secondary"]["verdict"] = "v" * 3000
+    full["cpu_baseline"]["sample"] = "s" * 2500
+    line = bench.compact(full)
+    assert len(json.dumps(line)) < bench.LINE_LIMIT
+    assert all(k in line for k in bench.CONTRACT_KEYS) and "roofline" in line and "cpu_baseline" in line
+
+
+def test_emit_result_writes_detail(bench, tmp_path, monkeypatch, capsys):
+    path = tmp_path / "d" / "detail.json"
+    monkeypatch.setattr(bench, "DETAIL_PATH", str(path))
+    monkeypatch.setattr(bench, "_JSON_FD", None)
+    full = _full_result()
+    bench.emit_result(full)
+    out = capsys.readouterr().out.strip().splitlines()
+    assert len(out) == 1 and len(out[0]) < bench.LINE_LIMIT
+    assert json.loads(out[0])["value"] == full["value"]
+    assert json.loads(path.read_text()) == full
+
+
+def test_pmc_traffic_is_labelled_and_stale_dropped(bench):
+    """roofline.traffic comes from a committed profile, and says so; a
+    profile whose kernel time disagrees with this run's is dropped."""
+    prof = os.path.join(ROOT, "profiles", "pmc_udp64_v1.json")
+    if not os.path.exists(prof):
+        pytest.skip("no committed udp64 PMC pass")
+    avg_ms = json.load(open(prof))["avg_kernel_ns"] / 1e6
+    t, src = bench.pmc_traffic("udp64", 1, avg_ms * 1.02)
+    assert t and "committed PMC pass" in src and "pmc_udp64_v1.json" in src
+    t2, src2 = bench.pmc_traffic("udp64", 1, avg_ms * 1.5)
+    assert t2 is None and "stale" in src2
+    assert bench.pmc_traffic("nonexistent", 1, 1.0) == (None, None)
+    r = bench.roofline_obj(1e9, avg_ms * 1.5, (t2, src2))
+    assert r["traffic"] is None and "stale" in r["traffic_source"]
+
+
+def test_rank_envs_match_torchrun(bench):
+    envs = bench.rank_envs(4, 29999, base={"PATH": "/bin"})
+    assert [e["RANK"] for e in envs] == ["0", "1", "2", "3"]
+    assert all(e["WORLD_SIZE"] == "4" and e["MASTER_ADDR"] == "127.0.0.1" and
+               e["MASTER_PORT"] == "29999" and e["PATH"] == "/bin" for e in envs)
+    assert [e["LOCAL_RANK"] for e in envs] == ["0", "1", "2", "3"]
+
+
+def test_gpus_n_without_launcher_never_prints_a_one_gpu_line():
+    """`bench.py --gpus 2` with no WORLD_SIZE spawns two rank processes; here
+    (no GPU) both refuse to start, so it exits non-zero with no line -- never
+    an n_gpus 1 line for --gpus 2."""
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1",
+                        "--warmup", "0"], capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode != 0
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert "ranks exited" in r.stderr
+
+
+def test_pick_cores_distinct_physical_idlest_first(bench):
+    """Two SMT siblings per core (c, c + 4); core {1, 5} idlest, then {3, 7}."""
+    sib = lambda c: frozenset((c % 4, c % 4 + 4))
+    a = {c: 0 for c in range(8)}
+    b = {0: 10, 4: 10, 1: 90, 5: 90, 2: 30, 6: 30, 3: 50, 7: 50}
+    assert bench.pick_cores(2, list(range(8)), a, b, sib) == [1, 3]
+    assert bench.pick_cores(8, list(range(8)), a, b, sib) == [1, 3, 2, 0]
+    assert bench.pick_cores(1, [2, 6], a, b, sib) == [2]
+
+
+def test_oracle_bench_pinned_runs():
+    """orc_bench_pinned: the CPU baseline's pinned timer (no GPU)."""
+    import numpy as np
+    from oracle import orc
+    from caladan_amd import gclassify as g
+    n, stride, R = 4096, 64, 16
+    frames, olf, rss = orc.generate(g.WL_UDP64, n, stride, R)
+    t = orc.Tables(R, g.HASH_JENKINS, 0, g.F_RSS_HASH)
+    for r in range(R):
+        t.runtime_set(r, orc.runtime_ip(r), 8, 8, orc.steer_flows(8, list(range(8))))
+    cpu = sorted(os.sched_getaffinity(0))[0]
+    s = t.bench(frames, n, stride, threads=1, passes=2, olflags=olf, rss=rss, direct=True, cpus=[cpu])
+    s2 = t.bench(frames, n, stride, threads=2, passes=2, olflags=olf, rss=rss, direct=True, cpus=[cpu, -1])
+    assert s > 0 and s2 > 0
