@@ -39,16 +39,14 @@ constexpr uint32_t kToepBytes = 12 * 256 * 4;
 constexpr uint32_t kCrcBytes = 8 * 256 * 4;
 constexpr uint32_t kLdsTableBudget = 96 * 1024;
 constexpr int kImgUsers = 8;             /* streams tracked per table image */
-/* GCL_TUNE_PAIR default: GENERAL batches on classify_pair_kernel.  Against
- * the LDS-tile classify_kernel, alternating in one process
- * (profiles/r03_general_ab.jsonl, r03_ws_ab.jsonl): the cache-resident
- * working-set row 107.4-109.5 -> 95.4-98.4 us, the random pool, the
- * JENKINS offsets-only row, PCIe zero-copy and the pcap replay within
- * +-1 %; 23 % fewer VALU instructions per wave (SQ counters,
- * profiles/r03_sq_ingress_ws_*.json).  GCL_TUNE_PAIR=0 restores the tile
- * kernel, =2 runs the pair kernel at 2048 lanes per CU. */
-constexpr int kDefaultPair = 1;
-constexpr uint32_t kLdsQueueBytes = 16; /* s_next[2] after the header tile */
+/* GENERAL batches (per-packet offsets or side arrays) run on
+ * classify_pair_kernel.  Against the LDS-tile kernel's GENERAL path,
+ * alternating in one process (profiles/r03_general_ab.jsonl,
+ * r03_ws_ab.jsonl): the cache-resident working-set row 107.4-109.5 ->
+ * 95.4-98.4 us, the random pool, the JENKINS offsets-only row, PCIe
+ * zero-copy and the pcap replay within +-1 %; 23 % fewer VALU instructions
+ * per wave (SQ counters, profiles/r03_sq_ingress_ws_*.json).  The tile
+ * kernel's GENERAL path was removed in round 5. */
 
 /* The first failure of a sequence of HIP calls whose outcome is checked
  * once, at the end (asynchronous copies, event records and waits). */
@@ -61,29 +59,17 @@ struct HipErr {
 	}
 	bool bad() const { return e != hipSuccess; }
 };
-constexpr int kDefaultSched = 0;  /* GCL_TUNE_SCHED default: static persistent grid */
-constexpr int kDefaultXcdMap = 0; /* GCL_TUNE_XCD_MAP default: round-robin tiles */
-/* GCL_TUNE_NT_STORE default: verdicts stored write-through (global_store
- * sc0 sc1).  Same buffers, one process: udp64 2.3-3.8 % faster for all three
- * verdict widths, tcp1500 2-2.4 %, the header-split layout unchanged
- * (profiles/archive/r01_verdict_store_ab.jsonl) */
-constexpr int kDefaultVerdictStore = 2;
-/* GCL_TUNE_VSTAGE default (dense classify_kernel, 1-/2-B verdicts): off.
- * Staging a tile's verdicts in LDS so one wave stores them as whole lines
- * measured within noise of the per-wave 64-B stores on the udp64 headline
- * with write-through stores (kernel 0.3296-0.3298 against 0.3297-0.3319 ms,
- * alternating fresh processes), 0.6 % faster with plain ones, which stay
- * 2 % slower than write-through either way (profiles/r04_vstage_ab.jsonl):
- * the fabric sees 64-B write requests in both forms (pmc_udp64_v1.json) */
-constexpr int kDefaultVstage = 0;
-/* Verdicts are stored at the end of their own tile.  Issuing them one tile
- * late (the former GCL_TUNE_DEFER=1) measured udp64 1-3 % slower and tcp1500
- * 0.4 % faster (profiles/archive/r02_defer_ab.jsonl); the knob was removed for the
- * registers it held. */
-
-/* tuning knobs for experiments (GCL_TUNE_BLOCKS_PER_CU caps the grid) */
-static int g_tune_bpc = 0;
-static int g_tune_grid = 0;
+/* Verdict stores are write-through (global_store sc0 sc1, a system-scope
+ * relaxed atomic store): against plain stores on the same buffers, one
+ * process, udp64 2.3-3.8 % faster for all verdict widths, tcp1500 2-2.4 %
+ * (profiles/archive/r01_verdict_store_ab.jsonl).  Measured and removed in
+ * round 5 (the A/B evidence stays in profiles/ and git history): verdicts
+ * staged in LDS and stored as whole lines (within noise,
+ * profiles/r04_vstage_ab.jsonl), stored one tile late (1-3 % slower,
+ * profiles/archive/r02_defer_ab.jsonl), a per-XCD contiguous tile walk (7 %
+ * slower, profiles/archive/r01_alloc_placement.jsonl), a dynamic per-XCD tile
+ * queue (83.8 against 101.1 Gpkt/s), non-temporal verdict stores and
+ * streaming-hint pair loads. */
 
 struct RtEntry {            /* 16 B per uniqid */
 	uint32_t m_lo, m_hi;     /* fastmod magic for thread_count */
@@ -113,32 +99,9 @@ struct KParams {
 	uint32_t off_rt, off_flow, off_toep, tables_lds_bytes;
 	uint32_t cflags;
 	uint32_t default_flags;
-	uint32_t nt_store;
-	/* GCL_TUNE_ABLATE, timing-only experiments with wrong results: 1 hash =
-	 * daddr, 2 no IP lookup, 4 no histogram add, 8 no flow_tbl read, 16 no
-	 * classification (the membench tile body), 64 no counter flush, 128 no
-	 * rx_one_pkt in classify_pair_kernel (the register loop alone), 256
-	 * dummy loads on one shared address (side_dummy), 512 no verdict
-	 * stores (classify_pair_kernel), 1024 1-byte stores of the 2-byte
-	 * verdict's low half (classify_kernel) */
-	uint32_t ablate;
 	uint2 *trans;    /* struct gcl_trans[n] or NULL */
 	uint32_t off_seed, off_crc;
-	uint32_t *sched; /* tile queue slot (SchedSlot) or NULL = static persistent grid */
-	uint32_t xcd_map; /* static grid: 1 = each XCD walks one contiguous eighth of the tiles */
-	uint32_t vstage;  /* classify_kernel, dense slots, 1-/2-B verdicts: a full tile's verdicts
-	                     staged in LDS and stored by NT/4 lanes, 4 packets each
-	                     (GCL_TUNE_VSTAGE) */
 };
-
-/* Dynamic tile queue of one launch: tiles are dealt per XCD (tile t belongs
- * to XCD t & 7, the one blockIdx.x & 7 is dispatched to), each XCD has its
- * own head on its own 128-B line, and a block whose XCD has run dry steals
- * from the next ones.  The last block to finish rewinds the slot. */
-#define GCL_SCHED_XCD 8
-#define GCL_SCHED_LINE 32 /* u32 per 128-B line */
-#define GCL_SCHED_WORDS ((GCL_SCHED_XCD + 1) * GCL_SCHED_LINE)
-#define GCL_SCHED_SLOTS 64
 
 /* ------------------------------------------------------------------------
  * Header tile: 256 packets x 64 B, 16-B chunks XOR-swizzled so that both the
@@ -179,67 +142,16 @@ __device__ __forceinline__ uint64_t frame_off(const KParams &k, uint64_t idx)
 	return idx * k.stride;
 }
 
-/*
- * Where a frame's header is staged from (frames at per-packet offsets; a
- * slot stride is always a multiple of 16, gcl_classify_ex refuses any
- * other).  A 4-B-aligned frame is read as the
- * 16-B-aligned 64-B window that starts @return (0-12) bytes before it: four
- * 16-B loads instead of the eight or sixteen narrower ones an 8- or
- * 4-B-aligned granule needs (mbuf data at element + 344 in the reference's
- * ingress pool, defs.h:503-506, is 8-B aligned: 275 -> 216 us for 8 Mi random
- * mbufs, profiles/archive/r01_ingress_ab.jsonl).  The window is cut at the end of its
- * first 128-B line (@cut < 64) when that line still holds frame bytes
- * [0, 40) -- Ethernet, an IHL-5 IPv4 header and the L4 ports, all the common
- * case reads -- so such a frame costs one line, not two; the rare packets
- * that need more (ARP's target IP at 38-41, IPv4 options) read it directly
- * (classify_one).  Frame bytes [0, @cut - @return) are staged.  Any other
- * frame (@return 0xFF) is read bytewise from its own start, all 64 bytes.
- */
-constexpr uint32_t kSpanFull = 64u << 8; /* no shift, 64 frame bytes staged */
-/* the rx loop's header records (GCL_LOOP_HDR_RECORDS) stage frame bytes 12-15
- * and 20-43 only: ports past byte 43 (IHL >= 7) are read from the frame */
+/* How much of a lane's header row classify_one may read: staged frame bytes
+ * << 8 (the low byte, a staging shift, is always 0 here).  The rx loop's
+ * header records (GCL_LOOP_HDR_RECORDS) stage frame bytes 12-15 and 20-43
+ * only: ports past byte 43 (IHL >= 7) are read from the frame. */
+constexpr uint32_t kSpanFull = 64u << 8;
 constexpr uint32_t kSpanRec = 44u << 8;
 
-__device__ __forceinline__ uint32_t hdr_window(const KParams &k, uint64_t off, uint32_t &cut)
-{
-	const uint64_t A = (uint64_t)(uintptr_t)k.frames + off;
-	const uint32_t s = (uint32_t)(A & 15);
-	cut = 64;
-	if ((A & 3) != 0 || off < s)
-		return 0xFF;
-	const uint32_t Ew = 128u - (uint32_t)((A - s) & 127);
-	if (Ew < 64 && Ew >= s + 40)
-		cut = Ew;
-	return s;
-}
-
-/*
- * Where the chunk loads of a packet at frame offset @off read from, as
- * published in LDS by the packet's own lane (classify_kernel, GENERAL
- * with DEPTH 2): {base lo, base hi, w, 0} with
- *   w = shift | cut << 8 (> 0xFF)  the hdr_window, base = off - shift, and
- *                                  the window's [0, cut) inside frames_len
- *   w = 0xFF                       bytewise from base = off (unaligned frame,
- *                                  or a window running past frames_len)
- *   w = 0                          no packet (@off == kNoOff, past the batch)
- * so a chunk load is one LDS read, a compare and a 64-bit add.
- */
+/* "no packet" offset (frames at or past frames_len are clamped to it, so a
+ * live packet never carries it) */
 constexpr uint64_t kNoOff = ~0ull;
-
-__device__ __forceinline__ uint4 hdr_src(const KParams &k, uint64_t off)
-{
-	if (off == kNoOff)
-		return make_uint4(0, 0, 0, 0);
-	uint32_t cut;
-	const uint32_t sh = hdr_window(k, off, cut);
-	uint64_t base = off;
-	uint32_t w = 0xFF;
-	if (sh != 0xFF && off - sh + cut <= k.frames_len) {
-		base = off - sh;
-		w = sh | cut << 8;
-	}
-	return make_uint4((uint32_t)base, (uint32_t)(base >> 32), w, 0);
-}
 
 /* 16 frame bytes from @a, bytewise (frame_byte: zero past frames_len) */
 __device__ __forceinline__ uint4 load16_bytes(const KParams &k, uint64_t a)
@@ -251,25 +163,6 @@ __device__ __forceinline__ uint4 load16_bytes(const KParams &k, uint64_t a)
 	return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-/*
- * Issue the four 16-B chunk loads of this lane for @tile (staged by
- * stage_tile after the loads land).  Every lane issues all four loads on
- * every path -- a chunk with nothing to read (past the batch, past the
- * first line, !@live, a bytewise frame) loads 16 B of the table image
- * instead and is never looked at -- and nothing here consumes a loaded
- * value.  Loads retire in order and the compiler's wait before staging a
- * tile counts the loads issued after that tile's on every path through
- * the loop, so with a fixed count it waits for this tile alone and the
- * next tile's loads stay in flight (DEPTH 2); one conditional load path
- * makes it wait for everything.
- *
- * @s_src (GENERAL, SRC: classify_kernel at DEPTH 2): the tile's
- * packets' hdr_src entries already in LDS, so a chunk load is one LDS read,
- * a compare and a 64-bit add.  !SRC: offsets read here (dependent loads).
- * @span: where this lane's own packet sits in its staged row (hdr_window):
- * shift | staged frame bytes << 8, for classify_one; bits 16-19 flag this
- * lane's chunks of bytewise frames, which patch_tile fills in after staging.
- */
 /* The tile kernel's 16-B frame loads carry the streaming hint: plain loads
  * measured 11 % slower on udp64 (88.7-89.6 vs 99.8-100.7 Gpkt/s) and 13 % on
  * tcp1500, alternating fresh processes on one box
@@ -280,71 +173,43 @@ __device__ __forceinline__ uint4 tile_load(const void *p)
 	return gcl::load16_nt(p);
 }
 
-template <bool GENERAL, int NT, bool SRC = false>
-__device__ __forceinline__ void load_tile(const KParams &k, uint64_t tile, bool live, uint4 r[4],
-                                          uint32_t &span, const uint4 *s_src = nullptr)
+/*
+ * Issue the four 16-B chunk loads of this lane for @tile of fixed-stride
+ * slots (staged by stage_tile after the loads land).  Every lane issues all
+ * four loads on every path -- a chunk past the batch or of a !@live tile
+ * loads 16 B of the table image instead and is never looked at -- and
+ * nothing here consumes a loaded value.  Loads retire in order and the
+ * compiler's wait before staging a tile counts the loads issued after that
+ * tile's on every path through the loop, so with a fixed count it waits for
+ * this tile alone and the next tile's loads stay in flight (DEPTH 2); one
+ * conditional load path makes it wait for everything.
+ */
+template <int NT>
+__device__ __forceinline__ void load_tile(const KParams &k, uint64_t tile, bool live, uint4 r[4])
 {
 	const uint8_t *dummy = k.tables; /* device table image: >= 16 B, always mapped */
-	span = kSpanFull;
-	if (!GENERAL) {
-		const uint64_t t0 = tile * NT;
-		const uint32_t lim = (!live || t0 >= k.n) ? 0u : k.n - t0 < NT ? (uint32_t)(k.n - t0) : NT;
-		const uint8_t *base = k.frames + t0 * k.stride;
-#pragma unroll
-		for (int j = 0; j < 4; j++) {
-			const uint32_t c = j * NT + threadIdx.x, p = c >> 2;
-			const uint8_t *a = p < lim ? base + (p * (uint32_t)k.stride + (c & 3) * 16) : dummy;
-			r[j] = tile_load(a);
-		}
-		return;
-	}
-	auto src = [&](uint32_t p) -> uint4 {
-		if (SRC)
-			return s_src[p];
-		const uint64_t idx = tile * NT + p;
-		return hdr_src(k, live && idx < k.n ? frame_off<GENERAL>(k, idx) : kNoOff);
-	};
-	const uint32_t me = src(threadIdx.x).z;
-	if (me > 0xFF)
-		span = (me & 0xFF) | ((me >> 8) - (me & 0xFF)) << 8;
+	const uint64_t t0 = tile * NT;
+	const uint32_t lim = (!live || t0 >= k.n) ? 0u : k.n - t0 < NT ? (uint32_t)(k.n - t0) : NT;
+	const uint8_t *base = k.frames + t0 * k.stride;
 #pragma unroll
 	for (int j = 0; j < 4; j++) {
-		const uint32_t c = j * NT + threadIdx.x, q16 = (c & 3) * 16;
-		const uint4 e = src(c >> 2);
-		/* past the first line (q16 >= cut): not staged, read on demand */
-		const bool use = e.z > 0xFF && q16 < (e.z >> 8);
-		const uint64_t a = ((uint64_t)e.y << 32 | e.x) + (use ? q16 : 0);
-		r[j] = tile_load(e.z > 0xFF && !(k.ablate & 256) ? k.frames + a : use ? k.frames + a : dummy);
-		span |= (uint32_t)(e.z == 0xFF) << (16 + j);
-	}
-}
-
-/* After stage_tile: this lane's chunks of @tile that load_tile flagged
- * bytewise (@mask, span bits 16-19: unaligned frames, the end of the
- * buffer), read byte by byte from the frame start into their tile slots.
- * Rare, and out of load_tile, so that its loads are not on the common path. */
-template <int NT>
-__device__ __forceinline__ void patch_tile(const KParams &k, uint4 *tile, uint64_t t, uint32_t mask)
-{
-	for (int j = 0; j < 4; j++) {
-		const uint32_t c = j * NT + threadIdx.x;
-		if (mask >> j & 1)
-			tile[tile_slot(c >> 2, c & 3)] =
-			        load16_bytes(k, frame_off<true>(k, t * NT + (c >> 2)) + (c & 3) * 16);
+		const uint32_t c = j * NT + threadIdx.x, p = c >> 2;
+		const uint8_t *a = p < lim ? base + (p * (uint32_t)k.stride + (c & 3) * 16) : dummy;
+		r[j] = tile_load(a);
 	}
 }
 
 /*
  * What a lane loads in place of an absent per-packet array (the loop keeps
  * one load count on every path): packet @i's own offs[] entry, a line the
- * kernel has already fetched, else the table image.  One address shared by
- * every lane of the chip (the table image) puts all these loads on one L2
- * channel; GCL_TUNE_ABLATE 256 restores that for the A/B.
+ * kernel has already fetched, else the table image.  (One address shared by
+ * every lane of the chip, the table image, would put all these loads on one
+ * L2 channel.)
  */
 template <typename T>
 __device__ __forceinline__ const T *side_dummy(const KParams &k, uint64_t i)
 {
-	return (const T *)(k.offs && !(k.ablate & 256) ? (const uint8_t *)(k.offs + i) : k.tables);
+	return (const T *)(k.offs ? (const uint8_t *)(k.offs + i) : k.tables);
 }
 
 /* dword at byte offset b (4-aligned, < 64) of this lane's staged header */
@@ -376,8 +241,6 @@ __device__ __forceinline__ uint32_t crc32c_u64(const uint32_t *T, uint32_t crc, 
 	       T[3 * 256 + (hi & 0xFF)] ^ T[2 * 256 + ((hi >> 8) & 0xFF)] ^
 	       T[1 * 256 + ((hi >> 16) & 0xFF)] ^ T[0 * 256 + (hi >> 24)];
 }
-
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 /*
  * ip_to_proc: a two-choice bucketised cuckoo table like DPDK's rte_hash (the
@@ -461,8 +324,6 @@ __device__ __forceinline__ uint64_t classify_core(const KParams &k, const HdrWor
                                                   uint64_t foff = kNoOff)
 {
 	const uint32_t d3 = h.d3, d5 = h.d5, d6 = h.d6, d7 = h.d7, d8 = h.d8, d9 = h.d9, d10 = h.d10;
-	/* timing-only ablations: never in a format-specialised (VF) kernel */
-	const uint32_t ablate = VF ? 0u : k.ablate;
 	const uint32_t et = gcl::bswap16(d3 & 0xFFFF);              /* rx.c:154 */
 	const uint32_t ihl = (d3 >> 16) & 0xF;
 	const uint32_t frag = gcl::bswap16(d5 & 0xFFFF);            /* ARP: opcode */
@@ -493,9 +354,7 @@ __device__ __forceinline__ uint64_t classify_core(const KParams &k, const HdrWor
 
 	/* steering hash (gclassify.h: NIC / JENKINS / TOEPLITZ) */
 	uint32_t hash = 0;
-	if (ablate & 1) {
-		hash = daddr;
-	} else if (MODE == GCL_HASH_NIC) {
+	if (MODE == GCL_HASH_NIC) {
 		if (k.rss)
 			hash = pre ? pre[1] : k.rss[idx];
 	} else {
@@ -551,15 +410,11 @@ __device__ __forceinline__ uint64_t classify_core(const KParams &k, const HdrWor
 	cnt.hashmiss += parse && is_ip && !(flags & GCL_F_RSS_HASH); /* rx.c:160-163 */
 	const uint32_t dst = is_ip ? daddr : arp_tip;
 
-	if constexpr (!GENERAL && !SYS)
+	if constexpr (!GENERAL)
 		dense_drain();
 	/* ip_to_proc: open addressing keyed by rte_jhash(&ip, 4, 0), rx.c:197 */
-	if (ablate & 2) {
-		if (lookup)
-			p = (int)(dst & 15);
-	} else if (lookup) {
+	if (lookup)
 		p = ipt_lookup(tb.ipt, k.ipt_mask, k.ipt_seed, dst);
-	}
 	const bool miss = lookup && p < 0;
 	const bool arp_respond = miss && azure && is_arp && frag == GCL_ARP_OP_REQUEST;
 	const bool unreg = miss && !arp_respond;                    /* rx.c:205 */
@@ -580,15 +435,11 @@ __device__ __forceinline__ uint64_t classify_core(const KParams &k, const HdrWor
 	if (p >= 0) {
 		const RtEntry re = tb.rtab[p];
 		uniq = (uint32_t)p;
-		if (ablate & 8) {
-			thr = hash & 7;
-		} else {
-			const uint64_t M = (uint64_t)re.m_hi << 32 | re.m_lo;
-			thr = gcl::fastmod(hash, M, re.tc);
-			if (!re.active)
-				action |= GCL_ACT_WAKE;
-		}
-		if (HIST && !(ablate & 4))
+		const uint64_t M = (uint64_t)re.m_hi << 32 | re.m_lo;
+		thr = gcl::fastmod(hash, M, re.tc);
+		if (!re.active)
+			action |= GCL_ACT_WAKE;
+		if (HIST)
 			atomicAdd(&hist[p], 1u);
 	}
 	if (!HIST)
@@ -688,123 +539,58 @@ __device__ __forceinline__ uint64_t classify_lean(const KParams &k, const HdrWor
 	return (uint64_t)vlo << 32 | hash;
 }
 
-/* rx_one_pkt for the packet staged in row `tid` of the LDS tile */
+/* rx_one_pkt for the packet staged in row `tid` of the LDS tile: dense
+ * slots (classify_kernel), or SYS (rxloop_kernel: frames at per-packet
+ * offsets in host memory, @span's staged bytes, 64 or 44 with header
+ * records, kSpanRec) */
 template <int MODE, bool GENERAL, bool SYS = false>
 __device__ __forceinline__ uint64_t classify_one(const KParams &k, const uint4 *tile, int tid,
                                                  uint64_t idx, const Tables &tb, uint32_t *hist,
-                                                 Counters &cnt, uint32_t span = kSpanFull,
-                                                 const uint32_t *pre = nullptr)
+                                                 Counters &cnt, uint32_t span = kSpanFull)
 {
-	/* frame byte b of this lane's header sits at tile byte b + sh, and frame
-	 * bytes [0, avail) are staged (hdr_window) */
-	const uint32_t sh = (GENERAL && !SYS) ? (span & 0xFF) : 0u;
-	/* SYS: 64, or 44 when the rx loop staged header records (kSpanRec) */
+	static_assert(!GENERAL || SYS, "GENERAL batches run on classify_pair_kernel");
 	const uint32_t avail = GENERAL ? (span >> 8 & 0xFF) : 64u;
+	const uint4 w0 = tile[tile_slot(tid, 0)];
+	const uint4 w1 = tile[tile_slot(tid, 1)];
+	const uint4 w2 = tile[tile_slot(tid, 2)];
 	HdrWords h;
-	if (GENERAL && !SYS && sh != 0) {
-		h.d3 = tile_dword(tile, tid, 12 + sh);
-		h.d5 = tile_dword(tile, tid, 20 + sh);
-		h.d6 = tile_dword(tile, tid, 24 + sh);
-		h.d7 = tile_dword(tile, tid, 28 + sh);
-		h.d8 = tile_dword(tile, tid, 32 + sh);
-		h.d9 = tile_dword(tile, tid, 36 + sh);
-		h.d10 = tile_dword(tile, tid, 40 + sh);
-	} else {
-		const uint4 w0 = tile[tile_slot(tid, 0)];
-		const uint4 w1 = tile[tile_slot(tid, 1)];
-		const uint4 w2 = tile[tile_slot(tid, 2)];
-		h.d3 = w0.w, h.d5 = w1.y, h.d6 = w1.z, h.d7 = w1.w;
-		h.d8 = w2.x, h.d9 = w2.y, h.d10 = w2.z;
-	}
-	return classify_core<MODE, GENERAL, SYS, false>(k, h, tile, tid, idx, tb, hist, cnt, sh, avail,
-	                                                 pre);
+	h.d3 = w0.w, h.d5 = w1.y, h.d6 = w1.z, h.d7 = w1.w;
+	h.d8 = w2.x, h.d9 = w2.y, h.d10 = w2.z;
+	return classify_core<MODE, GENERAL, SYS, false>(k, h, tile, tid, idx, tb, hist, cnt, 0, avail, nullptr);
 }
 
 /* Store verdict word @w (classify_one) of packet @idx in the context's
  * verdict format and store policy. */
 __device__ __forceinline__ void put_verdict(const KParams &k, uint64_t idx, uint64_t w);
 
-/* put_verdict with the format known at compile time: VF 2 is the 2-byte
- * verdict with the default write-through store (kDefaultVerdictStore) */
+/* a write-through (sc0 sc1) store of one verdict element */
+template <typename T>
+__device__ __forceinline__ void store_wt(T *p, T v)
+{
+	__hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+/* put_verdict with the format known at compile time (VF 2: the 2-byte
+ * queue verdict), else read from k.cflags */
 template <int VF>
 __device__ __forceinline__ void put_verdict_vf(const KParams &k, uint64_t idx, uint64_t w)
 {
 	if (VF == 2)
-		__hip_atomic_store((uint16_t *)k.verdicts + idx, (uint16_t)w, __ATOMIC_RELAXED,
-		                   __HIP_MEMORY_SCOPE_SYSTEM);
+		store_wt((uint16_t *)k.verdicts + idx, (uint16_t)w);
 	else
 		put_verdict(k, idx, w);
 }
 
 __device__ __forceinline__ void put_verdict(const KParams &k, uint64_t idx, uint64_t w)
 {
-	if (k.cflags & GCL_CFG_VERDICT1) {
-		if (k.nt_store == 2) /* write-through (sc0 sc1), kDefaultVerdictStore */
-			__hip_atomic_store((uint8_t *)k.verdicts + idx, (uint8_t)w, __ATOMIC_RELAXED,
-			                   __HIP_MEMORY_SCOPE_SYSTEM);
-		else
-			((uint8_t *)k.verdicts)[idx] = (uint8_t)w;
-	} else if (k.cflags & GCL_CFG_VERDICT2) {
-		if (k.ablate & 1024) /* timing only: a 1-byte verdict store */
-			__hip_atomic_store((uint8_t *)k.verdicts + idx, (uint8_t)w, __ATOMIC_RELAXED,
-			                   __HIP_MEMORY_SCOPE_SYSTEM);
-		else if (k.nt_store == 2)
-			__hip_atomic_store((uint16_t *)k.verdicts + idx, (uint16_t)w, __ATOMIC_RELAXED,
-			                   __HIP_MEMORY_SCOPE_SYSTEM);
-		else
-			((uint16_t *)k.verdicts)[idx] = (uint16_t)w;
-	} else if (k.cflags & GCL_CFG_VERDICT4) {
-		if (k.nt_store == 2) /* write-through (sc0 sc1), kDefaultVerdictStore */
-			__hip_atomic_store((uint32_t *)k.verdicts + idx, (uint32_t)w, __ATOMIC_RELAXED,
-			                   __HIP_MEMORY_SCOPE_SYSTEM);
-		else
-			((uint32_t *)k.verdicts)[idx] = (uint32_t)w;
-	} else {
-		const u32x2 vd = {(uint32_t)w, (uint32_t)(w >> 32)};
-		if (k.nt_store == 2)
-			__hip_atomic_store((uint64_t *)k.verdicts + idx, w, __ATOMIC_RELAXED,
-			                   __HIP_MEMORY_SCOPE_SYSTEM);
-		else if (k.nt_store)
-			__builtin_nontemporal_store(vd, (u32x2 *)&k.verdicts[idx]);
-		else
-			*(u32x2 *)&k.verdicts[idx] = vd;
-	}
-}
-
-/* GCL_TUNE_VSTAGE: packet @tid's verdict into the tile's LDS staging row */
-__device__ __forceinline__ void stage_verdict(const KParams &k, uint8_t *s_vst, int tid, uint64_t w)
-{
 	if (k.cflags & GCL_CFG_VERDICT1)
-		s_vst[tid] = (uint8_t)w;
+		store_wt((uint8_t *)k.verdicts + idx, (uint8_t)w);
+	else if (k.cflags & GCL_CFG_VERDICT2)
+		store_wt((uint16_t *)k.verdicts + idx, (uint16_t)w);
+	else if (k.cflags & GCL_CFG_VERDICT4)
+		store_wt((uint32_t *)k.verdicts + idx, (uint32_t)w);
 	else
-		((uint16_t *)s_vst)[tid] = (uint16_t)w;
-}
-
-/* ... and the staged tile @t stored by lanes < NT/4, four packets a lane: one
- * wave writes 256 (1-B) or 512 (2-B) contiguous bytes, whole 128-B lines,
- * where the tile's waves would each write 64 or 128 */
-template <int NT>
-__device__ __forceinline__ void flush_verdicts(const KParams &k, const uint8_t *s_vst, uint64_t t)
-{
-	const int tid = threadIdx.x;
-	if (tid >= NT / 4)
-		return;
-	const uint64_t i = t * NT + 4 * (uint64_t)tid;
-	if (k.cflags & GCL_CFG_VERDICT1) {
-		const uint32_t v = ((const uint32_t *)s_vst)[tid];
-		if (k.nt_store == 2)
-			__hip_atomic_store((uint32_t *)((uint8_t *)k.verdicts + i), v, __ATOMIC_RELAXED,
-			                   __HIP_MEMORY_SCOPE_SYSTEM);
-		else
-			*(uint32_t *)((uint8_t *)k.verdicts + i) = v;
-	} else {
-		const uint64_t v = ((const uint64_t *)s_vst)[tid];
-		if (k.nt_store == 2)
-			__hip_atomic_store((uint64_t *)((uint16_t *)k.verdicts + i), v, __ATOMIC_RELAXED,
-			                   __HIP_MEMORY_SCOPE_SYSTEM);
-		else
-			*(uint64_t *)((uint16_t *)k.verdicts + i) = v;
-	}
+		store_wt((uint64_t *)k.verdicts + idx, w);
 }
 
 template <int NT>
@@ -823,8 +609,6 @@ template <int NT>
 __device__ __forceinline__ void flush_counters(const KParams &k, const uint32_t *hist,
                                                const Counters &cnt)
 {
-	if (k.ablate & 64)
-		return;
 	const int tid = threadIdx.x;
 	for (uint32_t i = tid; i < k.max_rt; i += NT) {
 		uint32_t v = hist[i];
@@ -855,42 +639,15 @@ __device__ __forceinline__ void flush_counters(const KParams &k, const uint32_t 
 	}
 }
 
-__device__ __forceinline__ uint64_t sched_xcd_tiles(uint64_t ntiles, uint32_t x)
-{
-	return ntiles > x ? (ntiles - x + GCL_SCHED_XCD - 1) / GCL_SCHED_XCD : 0;
-}
-
-__device__ __forceinline__ uint32_t sched_xcd_blocks(uint32_t G, uint32_t x)
-{
-	return G > x ? (G - x + GCL_SCHED_XCD - 1) / GCL_SCHED_XCD : 0;
-}
-
-/* Resolve a dequeue from head @xs that returned @got; on an exhausted head,
- * move on to the next XCD's head (at most 7 more atomics per block, at the
- * very end of the launch).  Returns the tile or ntiles when all are gone. */
-__device__ __forceinline__ uint64_t sched_resolve(uint32_t *sched, uint64_t ntiles, uint32_t G,
-                                               uint32_t x0, uint32_t &xs, uint32_t got)
-{
-	for (;;) {
-		const uint64_t k = (uint64_t)sched_xcd_blocks(G, xs) + got;
-		if (k < sched_xcd_tiles(ntiles, xs))
-			return xs + GCL_SCHED_XCD * k;
-		xs = (xs + 1) & (GCL_SCHED_XCD - 1);
-		if (xs == x0)
-			return ntiles;
-		got = atomicAdd(&sched[xs * GCL_SCHED_LINE], 1u);
-	}
-}
-
 /*
- * Persistent grid.  Static schedule (k.sched == NULL): block b handles tiles
- * b, b + G, b + 2G, ...  Dynamic (k.sched): block b starts on tile
- * (b & 7) + 8 * (b >> 3) and then dequeues from its XCD's head, one tile
- * ahead, so the atomic's latency hides behind the current tile.  Either way
- * the frames of the next DEPTH tiles are in flight in registers while a tile
- * is parsed.
+ * The batch kernel for fixed-stride slots (classify_kernel; frames at
+ * per-packet offsets or with per-packet side arrays run on
+ * classify_pair_kernel).  Persistent grid: block b handles tiles b, b + G,
+ * b + 2G, ... (tiles dealt round-robin, so the whole chip sweeps one window
+ * of the batch), with the frames of the next DEPTH tiles in flight in
+ * registers while a tile is parsed.
  */
-template <int MODE, bool TLDS, bool GENERAL, int DEPTH, int NT>
+template <int MODE, bool TLDS, int DEPTH, int NT>
 /* 4 waves per SIMD (<= 128 VGPRs): the 1024 resident lanes per CU the
  * geometry policy plans for, at every tile size */
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4)))
@@ -898,8 +655,7 @@ classify_kernel(KParams k)
 {
 	extern __shared__ uint4 smem[];
 	uint4 *tile = smem;
-	uint64_t *s_next = (uint64_t *)(smem + NT * 4); /* tile queue hand-off, 16 B */
-	uint32_t *hist = (uint32_t *)(smem + NT * 4 + 1);
+	uint32_t *hist = (uint32_t *)(smem + NT * 4);
 	uint8_t *lds_tab = (uint8_t *)(hist + ((k.max_rt + 3) & ~3u));
 	const int tid = threadIdx.x;
 
@@ -927,156 +683,29 @@ classify_kernel(KParams k)
 	__syncthreads();
 
 	Counters cnt = {0, 0, 0, 0};
-	const uint64_t G = gridDim.x;
-	const bool dyn = DEPTH == 1 && k.sched != nullptr;
-	const uint32_t x0 = blockIdx.x & (GCL_SCHED_XCD - 1);
-	uint32_t xs = x0; /* head this block dequeues from (thread 0 only) */
 	uint4 ra[4], rb[4];
-	uint32_t spa = kSpanFull, spb = kSpanFull;
-	/* GENERAL, DEPTH 2: the descriptors' ol_flags and hash.rss, loaded a
-	 * tile ahead -- right after the previous use of the same registers, so
-	 * that no copy of an in-flight value (which waits for it) is needed --
-	 * and not looked at until the tile is parsed (loaded in classify_one,
-	 * they would wait for the next tile's loads issued before them) */
-	uint32_t pra[2] = {0, 0}, prb[2] = {0, 0};
 	uint64_t t = blockIdx.x;
-	/* static walk: tiles t, t + step, ... below t_end.  Default: tiles dealt
-	 * round-robin, so the whole chip sweeps one 16 MiB window of the batch.
-	 * xcd_map (GCL_TUNE_XCD_MAP=1): block b walks XCD (b & 7)'s contiguous
-	 * eighth instead, eight separate streams; that measured 7% slower on
-	 * every buffer placement tried (tools/alloc_ab.cpp,
-	 * profiles/archive/r01_alloc_placement.jsonl), so it stays an experiment. */
-	uint64_t step = G, t_end = k.ntiles;
-	if (k.xcd_map && !k.sched) {
-		const uint64_t Gx = G / GCL_SCHED_XCD;
-		const uint64_t chunk = (k.ntiles + GCL_SCHED_XCD - 1) / GCL_SCHED_XCD;
-		const uint64_t lo = (blockIdx.x & (GCL_SCHED_XCD - 1)) * chunk;
-		t = lo + blockIdx.x / GCL_SCHED_XCD;
-		t_end = lo + chunk < k.ntiles ? lo + chunk : k.ntiles;
-		step = Gx;
-	}
-	uint32_t got = 0;
-	if (dyn) {
-		const uint64_t j = blockIdx.x / GCL_SCHED_XCD;
-		t = j < sched_xcd_tiles(k.ntiles, x0) ? x0 + GCL_SCHED_XCD * j : k.ntiles;
-		if (tid == 0 && t < k.ntiles)
-			got = atomicAdd(&k.sched[x0 * GCL_SCHED_LINE], 1u);
-	}
-	/* GENERAL, DEPTH 2 (a static walk): frame offsets go through LDS.  Each
-	 * lane loads only its own packet's offset, DEPTH tiles ahead of the tile
-	 * whose frames it is for (offa/offb, coalesced), publishes its hdr_src in
-	 * s_src before the stage barrier, and the chunk loads after the barrier
-	 * read their packets' sources from LDS -- no dependent global offs[]
-	 * loads on the way to the frame loads, and the same load count on every
-	 * path (load_tile). */
-	constexpr bool goffs = GENERAL && DEPTH == 2;
-	uint4 *s_src = (uint4 *)(lds_tab + k.tables_lds_bytes);
-	/* GCL_TUNE_VSTAGE (dense slots only): full tiles' verdicts via LDS */
-	uint8_t *s_vst = lds_tab + k.tables_lds_bytes + (goffs ? NT * 16 : 0);
-	const bool vst = !GENERAL && k.vstage;
-	auto full_tile = [&](uint64_t tt) { return vst && (tt + 1) * NT <= k.n; };
-	/* offs[] of this lane's packet of tile tt, loaded unconditionally (the
-	 * table image stands in without offs[]); whether there is a packet is
-	 * my_ok(tt), applied by pub() when the offset is published, after the
-	 * load has landed */
-	const uint64_t *offs_src = k.offs ? k.offs : (const uint64_t *)k.tables;
-	auto my_ok = [&](uint64_t tt) { return tt < t_end && tt * NT + tid < k.n; };
-	auto my_off = [&](uint64_t tt) -> uint64_t {
-		return user_off(k, offs_src[k.offs && my_ok(tt) ? tt * NT + tid : 0]);
-	};
-	auto pref = [&](uint64_t tt, uint32_t pr[2]) {
-		if constexpr (goffs) {
-			const uint64_t i = my_ok(tt) ? tt * NT + tid : 0;
-			pr[0] = *(k.olflags ? k.olflags + i : side_dummy<uint8_t>(k, i));
-			if (MODE == GCL_HASH_NIC)
-				pr[1] = *(k.rss ? k.rss + i : side_dummy<uint32_t>(k, i));
-		}
-	};
-	auto pub = [&](uint64_t tt, uint64_t raw) {
-		const uint64_t i = tt * NT + tid;
-		s_src[tid] = hdr_src(k, !my_ok(tt) ? kNoOff : k.offs ? raw : i * k.stride);
-	};
-	uint64_t offa = 0, offb = 0;
-	if (goffs) {
-		/* the loop's waits count the loads issued after each one on
-		 * every path, this prologue included: offa and offb go out
-		 * before rb's loads, so waiting for them leaves rb in flight */
-		pub(t, my_off(t));
-		const uint64_t o1 = my_off(t + step);
-		__syncthreads();
-		load_tile<GENERAL, NT, goffs>(k, t, t < t_end, ra, spa, s_src);
-		pref(t, pra);
-		__syncthreads();
-		pub(t + step, o1);
-		offa = my_off(t + 2 * step);
-		offb = my_off(t + 3 * step);
-		__syncthreads();
-		load_tile<GENERAL, NT, goffs>(k, t + step, t + step < t_end, rb, spb, s_src);
-		pref(t + step, prb);
-		__syncthreads();
-	} else {
-		if (t < t_end)
-			load_tile<GENERAL, NT>(k, t, true, ra, spa);
-		if (DEPTH == 2)
-			load_tile<GENERAL, NT>(k, t + step, t + step < t_end, rb, spb);
-	}
-	if (dyn && tid == 0)
-		s_next[0] = t < k.ntiles ? sched_resolve(k.sched, k.ntiles, (uint32_t)G, x0, xs, got)
-		                         : k.ntiles;
-	int par = 0;
+	const uint64_t step = gridDim.x, t_end = k.ntiles;
+	if (t < t_end)
+		load_tile<NT>(k, t, true, ra);
+	if (DEPTH == 2)
+		load_tile<NT>(k, t + step, t + step < t_end, rb);
 
 	while (t < t_end) {
 		/* t opaque to the loop optimiser: without it every per-packet
-		 * address (offs, olflags, rss, fdir, verdicts, ...) becomes its
-		 * own 64-bit induction variable, held in VGPRs and spilled */
-		if constexpr (DEPTH == 2) /* (DEPTH 1 may take t from LDS: a VGPR) */
+		 * address (verdicts, ...) becomes its own 64-bit induction
+		 * variable, held in VGPRs and spilled */
+		if constexpr (DEPTH == 2)
 			asm volatile("" : "+s"(t));
-		if constexpr (!GENERAL) /* dense_drain: once per loop iteration too */
-			dense_drain();
+		dense_drain(); /* once per loop iteration too */
 		stage_tile<NT>(tile, ra);
-		const uint32_t sp = spa;
-		if (GENERAL && (sp >> 16))
-			patch_tile<NT>(k, tile, t, sp >> 16);
-		if (goffs)
-			pub(t + DEPTH * step, offa);
 		__syncthreads();
-		uint64_t nxt = t + DEPTH * step;
-		if (dyn) {
-			nxt = s_next[par];
-			/* issued before the tile loads, so waiting for it later does
-			 * not wait for them (vmcnt retires in order) */
-			if (tid == 0 && nxt < k.ntiles)
-				got = atomicAdd(&k.sched[xs * GCL_SCHED_LINE], 1u);
-		}
+		const uint64_t nxt = t + DEPTH * step;
 		/* in flight while parsing */
-		load_tile<GENERAL, NT, goffs>(k, nxt, nxt < t_end, ra, spa, s_src);
-		if (goffs)
-			offa = my_off(nxt + DEPTH * step);
-		if (k.ablate & 16) { /* timing only: the membench tile_v0 body */
-			const uint4 a = tile[tile_slot(tid, 0)], b = tile[tile_slot(tid, 1)];
-			if (t * NT + tid < k.n) /* in the verdict format: never past the buffer */
-				put_verdict(k, t * NT + tid, (uint64_t)(a.w ^ b.y) << 32 | (b.z ^ a.x));
-		} else if (t * NT + tid < k.n) {
-			const uint64_t v = classify_one<MODE, GENERAL>(k, tile, tid, t * NT + tid, tb, hist, cnt, sp,
-			                                               goffs ? pra : nullptr);
-			if (full_tile(t))
-				stage_verdict(k, s_vst, tid, v);
-			else
-				put_verdict(k, t * NT + tid, v);
-		}
-		pref(nxt, pra);
-		if (dyn && tid == 0)
-			s_next[par ^ 1] = nxt < k.ntiles ? sched_resolve(k.sched, k.ntiles, (uint32_t)G,
-			                                                 x0, xs, got)
-			                                 : k.ntiles;
+		load_tile<NT>(k, nxt, nxt < t_end, ra);
+		if (t * NT + tid < k.n)
+			put_verdict(k, t * NT + tid, classify_one<MODE, false>(k, tile, tid, t * NT + tid, tb, hist, cnt));
 		__syncthreads();
-		if (!(k.ablate & 16) && full_tile(t))
-			flush_verdicts<NT>(k, s_vst, t);
-		if (dyn) {
-			t = nxt;
-			par ^= 1;
-			continue;
-		}
 		t += step;
 		if (DEPTH == 2) {
 			/* runs past t_end too (an empty tile: dummy loads, nothing
@@ -1084,41 +713,15 @@ classify_kernel(KParams k)
 			 * the middle of the body, without the rb loads below, would
 			 * make the wait before staging ra wait for everything */
 			stage_tile<NT>(tile, rb);
-			const uint32_t sp2 = spb;
-			if (GENERAL && (sp2 >> 16))
-				patch_tile<NT>(k, tile, t, sp2 >> 16);
-			if (goffs)
-				pub(t + 2 * step, offb);
 			__syncthreads();
-			load_tile<GENERAL, NT, goffs>(k, t + 2 * step, t + 2 * step < t_end, rb, spb, s_src);
-			if (goffs)
-				offb = my_off(t + 4 * step);
-			if (t < t_end && t * NT + tid < k.n) {
-				const uint64_t v = classify_one<MODE, GENERAL>(k, tile, tid, t * NT + tid, tb, hist, cnt,
-				                                               sp2, goffs ? prb : nullptr);
-				if (full_tile(t))
-					stage_verdict(k, s_vst, tid, v);
-				else
-					put_verdict(k, t * NT + tid, v);
-			}
-			pref(t + 2 * step, prb);
+			load_tile<NT>(k, t + 2 * step, t + 2 * step < t_end, rb);
+			if (t < t_end && t * NT + tid < k.n)
+				put_verdict(k, t * NT + tid,
+				            classify_one<MODE, false>(k, tile, tid, t * NT + tid, tb, hist, cnt));
 			__syncthreads();
-			if (t < t_end && full_tile(t))
-				flush_verdicts<NT>(k, s_vst, t);
 			t += step;
 		}
 	}
-	/* every dequeue of this block has returned; the last block out rewinds */
-	if (dyn && tid == 0) {
-		uint32_t *done = &k.sched[GCL_SCHED_XCD * GCL_SCHED_LINE];
-		if (atomicAdd(done, 1u) == (uint32_t)G - 1) {
-			for (int x = 0; x < GCL_SCHED_XCD; x++)
-				__hip_atomic_store(&k.sched[x * GCL_SCHED_LINE], 0u, __ATOMIC_RELAXED,
-				                   __HIP_MEMORY_SCOPE_AGENT);
-			__hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-		}
-	}
-
 	flush_counters<NT>(k, hist, cnt);
 }
 
@@ -1177,16 +780,15 @@ typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 
 /* load J of this lane: half (lane & 1) of the pair's packet J, whose
  * pair_src lane J of the pair holds in @my (quad_perm broadcast) */
-template <int J, bool NTL>
+template <int J>
 __device__ __forceinline__ uint4 pair_load(const KParams &k, uint64_t my)
 {
 	constexpr int B = J ? 0xF5 : 0xA0; /* quad_perm [1,1,3,3] : [0,0,2,2] */
 	const uint32_t lo = mdpp<B>((uint32_t)my), hi = mdpp<B>((uint32_t)(my >> 32));
 	const uint64_t s = (uint64_t)hi << 32 | lo;
 	const uint8_t *a = (hi >> 31) ? k.tables : k.frames + s + 16 * (threadIdx.x & 1);
-	/* plain loads: the frames stay in L2 for the next use of the same mbuf;
-	 * NTL (GCL_TUNE_PAIR_LOADS=1, experiment) adds the streaming hint */
-	const u32x4a4 v = NTL ? __builtin_nontemporal_load((const u32x4a4 *)a) : *(const u32x4a4 *)a;
+	/* plain loads: the frames stay in L2 for the next use of the same mbuf */
+	const u32x4a4 v = *(const u32x4a4 *)a;
 	return make_uint4(v.x, v.y, v.z, v.w);
 }
 
@@ -1202,7 +804,7 @@ __device__ __forceinline__ void pair_exchange(uint4 r[2])
 	r[1] = sel4(odd, r[1], y);
 }
 
-template <int MODE, bool TLDS, int NT, int VF, bool NTL = false>
+template <int MODE, bool TLDS, int NT, int VF>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4)))
 classify_pair_kernel(KParams k)
 {
@@ -1245,8 +847,8 @@ classify_pair_kernel(KParams k)
 			pr[1] = *(k.rss ? k.rss + i : side_dummy<uint32_t>(k, i));
 	};
 	auto issue = [&](uint64_t my, uint4 r[2]) {
-		r[0] = pair_load<0, NTL>(k, my);
-		r[1] = pair_load<1, NTL>(k, my);
+		r[0] = pair_load<0>(k, my);
+		r[1] = pair_load<1>(k, my);
 	};
 	/* the landed halves -> this lane's header dwords (frame bytes 12-39;
 	 * d10, bytes 40-43, is not fetched: avail 40 sends ARP to the frame) */
@@ -1265,16 +867,8 @@ classify_pair_kernel(KParams k)
 			const uint64_t i = tt * NT + tid;
 			/* this packet's frame offset, for the ARP target's extra read */
 			const uint64_t foff = (my >> 63) ? (my & ~kPairBytewise) : my - 8;
-			if (!VF && (k.ablate & 128)) { /* timing only: the loop without rx_one_pkt */
-				put_verdict_vf<VF>(k, i, h.d3 ^ h.d7 ^ h.d9 ^ pr[0] ^ pr[1]);
-			} else {
-				const uint64_t w = classify_core<MODE, true, false, true, VF>(
-				        k, h, nullptr, tid, i, tb, hist, cnt, 0, 40, pr, foff);
-				if (VF || !(k.ablate & 512)) /* 512: timing only, no verdict stores */
-					put_verdict_vf<VF>(k, i, w);
-				else
-					cnt.flowtag += (uint32_t)w == 0xFFFFFFFFu; /* keep w live */
-			}
+			put_verdict_vf<VF>(k, i, classify_core<MODE, true, false, true, VF>(
+			                                 k, h, nullptr, tid, i, tb, hist, cnt, 0, 40, pr, foff));
 		}
 	};
 
@@ -1365,20 +959,11 @@ constexpr uint64_t kLoopRefresh = 256;
 /* s_memrealtime ticks (100 MHz) a wait polls the offsets with the word: a
  * burst that arrives later costs the offsets' round trip after the word */
 constexpr uint64_t kLoopSpecTicks = 400;
-/* GCL_TUNE_LOOP_CLOCK default: 0 polls on s_memrealtime, 1 on s_memtime */
-constexpr uint32_t kDefaultLoopClock = 0;
-/* GCL_TUNE_LOOP_WRITER default (rxloop64_kernel): 1 the writer wave stores
- * the verdict records, 0 the poller does.  The handoff through the mailbox
- * cost a lone 64-packet burst more (5.08 against 4.43 us p50 with stage
- * stamps) than the poller's wait for its own stores' retirement costs a
- * queued one (4 workers x 8: 78.5 against 79.7 Mpkt/s;
- * profiles/r04_loop64_ab.jsonl) */
-constexpr uint32_t kDefaultLoopWriter = 0;
 /* GCL_TUNE_LOOP_LEAN default: bursts whose every packet is plain IPv4 (IHL 5,
  * no FDIR mark, no hint) classified by classify_lean */
 constexpr uint32_t kDefaultLoopLean = 1;
-/* GCL_TUNE_LOOP_HYBRID default (s_memrealtime ticks, 0 = off) */
-constexpr uint32_t kDefaultLoopHybrid = 0;
+/* GCL_TUNE_LOOP_POLLERS default: rxloop64_kernel's poll-and-classify waves */
+constexpr int kDefaultLoopPollers = 1;
 /* how a worker's bursts arrived (gcl_rxloop_poll_stats): with the poll that
  * found the word; eligible for that, but an entry or record still stale so
  * read after it; or after the word, the speculative window over or the
@@ -1429,17 +1014,11 @@ struct LoopParams {
 	uint64_t t0;               /* tickets start after t0 (0; GCL_TUNE_LOOP_T0 tests the
 	                              stamps' wrap), a multiple of nslots */
 	uint32_t stamps;           /* GCL_LOOP_STAMPS: per-burst stage times into the slot header */
-	uint32_t fast_clock;       /* poll on the shader clock (GCL_TUNE_LOOP_CLOCK) */
 	uint32_t rec_plane;        /* GCL_LOOP_HDR_RECORDS: bytes between the records' chunk
 	                              planes (chunk j of packet i at off_hdr + j * rec_plane + 16 i) */
-	uint32_t writer;           /* rxloop64_kernel: the writer wave stores the verdict
-	                              records (else the poller, GCL_TUNE_LOOP_WRITER=0) */
 	uint32_t lean;             /* rxloop64_kernel: plain-IPv4 bursts on classify_lean
 	                              (GCL_TUNE_LOOP_LEAN=0: always classify_core) */
-	uint32_t dual;             /* rxloop64_kernel: two polls in flight, the second this
-	                              many s_memrealtime ticks after the first (0: one) */
-	uint32_t hybrid;           /* rxloop64_kernel: a caught-up worker's first poll this
-	                              many ticks after its last records (GCL_TUNE_LOOP_HYBRID) */
+	uint32_t lds_copy;         /* rxloop64_kernel: LDS bytes per table copy (header + image) */
 };
 
 /* GCL_LOOP_HDR_RECORDS: the submitting core writes each packet as one 64-B
@@ -1540,29 +1119,9 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 	uint8_t *lds_tab = (uint8_t *)(hist + ((L.max_rt + 3) & ~3u));
 	const int tid = threadIdx.x;
 	const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + L.lifetime_ticks;
-	/* the poll's clock: with L.fast_clock the speculative window runs on
-	 * the shader clock (s_memtime, read locally) and the lifetime bound on
-	 * the real-time counter only every 16th poll; s_memrealtime is a round
-	 * trip to the real-time counter (tools/clock_probe.hip) that a poll
-	 * otherwise waits for before issuing its loads.  The shader clock's
-	 * rate is calibrated against the real-time counter at start (10 us). */
-	uint64_t spec_cyc = L.spec_ticks, clk_r = 1, clk_c = 1;
-	if (L.fast_clock) {
-		const uint64_t r0 = __builtin_amdgcn_s_memrealtime(), c0 = __builtin_amdgcn_s_memtime();
-		uint64_t r1;
-		do {
-			r1 = __builtin_amdgcn_s_memrealtime();
-		} while (r1 - r0 < 1000);
-		const uint64_t c1 = __builtin_amdgcn_s_memtime();
-		clk_r = r1 - r0;
-		clk_c = c1 - c0;
-		spec_cyc = (uint64_t)L.spec_ticks * clk_c / clk_r;
-	}
-	/* GCL_LOOP_STAMPS: the poll's clock, and its ticks -> 10-ns ticks */
-	auto sclk = [&]() -> uint64_t {
-		return L.fast_clock ? __builtin_amdgcn_s_memtime() : __builtin_amdgcn_s_memrealtime();
-	};
-	auto to10 = [&](uint64_t d) -> uint32_t { return (uint32_t)(d * clk_r / clk_c); };
+	/* the poll's clock (s_memrealtime, 100 MHz: the stamps' 10-ns ticks) */
+	auto sclk = []() -> uint64_t { return __builtin_amdgcn_s_memrealtime(); };
+	auto to10 = [](uint64_t d) -> uint32_t { return (uint32_t)d; };
 	const __amdgpu_buffer_rsrc_t frs = gcl::host_rsrc(L.frames, L.frames_len);
 	if (tid == 0 && blockIdx.x < 8) /* which XCD this worker runs on */
 		gcl::st_sys32(&L.where[blockIdx.x], __builtin_amdgcn_s_getreg((3 << 11) | 20) + 1);
@@ -1599,8 +1158,7 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 			const bool spec = L.spec, rec = L.hdr_rec;
 			const uint64_t stamp = loop_stamp(t, L.nslots);
 			const uint32_t rstamp = loop_rec_stamp(t, L.nslots);
-			const uint64_t spec_end = L.fast_clock ? __builtin_amdgcn_s_memtime() + spec_cyc
-			                                       : __builtin_amdgcn_s_memrealtime() + L.spec_ticks;
+			const uint64_t spec_end = __builtin_amdgcn_s_memrealtime() + L.spec_ticks;
 			uint64_t w = 0, e = 0;
 			bool rok = false, sp_hit = false;
 			uint4 q[4], qv[4] = {}; /* header records: the lane's packet's chunks */
@@ -1610,8 +1168,7 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 				if (L.stamps)
 					t_issue = sclk();
 				npoll = k + 1;
-				const bool sp = spec && (L.fast_clock ? __builtin_amdgcn_s_memtime()
-				                                      : __builtin_amdgcn_s_memrealtime()) < spec_end;
+				const bool sp = spec && __builtin_amdgcn_s_memrealtime() < spec_end;
 				const uint64_t ev = sp && !rec ? gcl::ld_sys64(slot + L.off_offs + 8 * tid) : 0;
 				if (sp && rec) {
 #pragma unroll
@@ -1641,8 +1198,7 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 						q[j] = qv[j];
 					break;
 				}
-				if (sv || ((!L.fast_clock || (k & 15) == 15) &&
-				           __builtin_amdgcn_s_memrealtime() > t_end))
+				if (sv || __builtin_amdgcn_s_memrealtime() > t_end)
 					break;
 				__builtin_amdgcn_s_sleep(1);
 			}
@@ -1861,26 +1417,30 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 }
 
 /* ------------------------------------------------------------------------
- * rxloop64_kernel: the loop at the reference's own burst size (<= 64 mbufs,
- * IOKERNEL_RX_BURST_SIZE, defs.h:75), chosen by gcl_rxloop_start whenever
- * max_burst <= 64.  A burst that size is one packet per lane of ONE wave, so
- * the poller wave takes it from the poll to the verdicts alone, from
+ * rxloop64_kernel<MODE, NP>: the loop at the reference's own burst size (<= 64
+ * mbufs, IOKERNEL_RX_BURST_SIZE, defs.h:75), chosen by gcl_rxloop_start
+ * whenever max_burst <= 64.  A burst that size is one packet per lane of ONE
+ * wave, so a wave takes it from the poll to the verdicts alone, from
  * registers, with no barrier: rxloop_kernel's three barriers and its LDS tile
  * cost 0.7 us of a lone burst (GCL_LOOP_STAMPS, profiles/r04_stages_reentry.jsonl).
- * A second wave (the writer) adds the counts and the counters (device
- * atomics) and the poll counters, so their retirement never holds the
- * poller's vmcnt.  It can also store the verdict records
- * (GCL_TUNE_LOOP_WRITER=1): on gfx9 stores and loads share vmcnt, in order,
- * and a store into host memory takes about a PCIe round trip to retire, so
- * a poller that stores its own records consumes its next poll only after
- * them; measured, the mailbox handoff costs a lone burst more than that wait
- * costs a queued one, so the poller stores them (kDefaultLoopWriter).  The
- * two waves hand bursts over through two LDS mailboxes, ordered by LDS-only
- * fences (lgkmcnt, never vmcnt).
+ *
+ * NP poll-and-classify waves per worker.  With NP = 1 one wave polls the
+ * worker's next ticket, classifies the burst and stores its verdict records.
+ * With NP = 2 two such waves share the worker's ticket sequence through LDS:
+ * a wave polls the lowest unclaimed ticket, half a poll round trip after the
+ * other wave's poll of the same ticket (so the slot is sampled twice per round
+ * trip, each wave with its own vmcnt), or -- when bursts are queued -- the
+ * ticket after it; the wave whose poll brings a burst with current records
+ * claims it with an LDS compare-and-swap and classifies it, while the other
+ * keeps polling.  A poll that finds the word with stale records is not
+ * claimed: the next sample (the other wave's, half a round trip on) brings
+ * them.  One more wave (the writer) adds the counts and the counters (device
+ * atomics) and the poll counters, so their retirement never holds a poller's
+ * vmcnt (on gfx9 stores and loads share vmcnt and retire in order); bursts
+ * reach it through two LDS mailboxes per classifying wave, ordered by
+ * LDS-only fences (lgkmcnt, never vmcnt).
  */
 struct Mbox64 {
-	uint4 rec[64];    /* verdict records {hash, verdict, ticket} (LoopRec) */
-	uint4 tr[64];     /* GCL_CFG_TRANS_HASH: {h5, h3, ticket} */
 	uint32_t p[64];   /* each packet's runtime (~0: none): the counts */
 	uint64_t t;       /* ticket */
 	uint32_t n, kind; /* packets; how the burst arrived (kLoopPollEarly ...) */
@@ -1893,45 +1453,82 @@ struct Mbox64 {
 	uint32_t pad[2];
 };
 static_assert(sizeof(Mbox64) % 16 == 0, "Mbox64");
-constexpr uint32_t kLoop64Lds = 2 * sizeof(Mbox64) + 64 * 8 + 2 * 64 * 4 + 64 * 8 + 16;
 
-/* rxloop64_kernel's writer wave: each posted burst's records (the transport
- * hashes first: the host counts a burst complete only when both carry the
- * ticket), its counts and counters, the poll counters, the stage stamps. */
-__device__ __forceinline__ void rxloop64_writer(const LoopParams &L, Mbox64 *mbox, const uint32_t *s_exit,
-                                             int lane)
+/* one classifying wave's LDS: its mailboxes and the side arrays classify_core
+ * reads through KParams */
+struct Wave64 {
+	Mbox64 mbox[2];
+	uint64_t offs[64];
+	uint32_t fdir[64], hint[64];
+	uint2 trans[64];
+};
+static_assert(sizeof(Wave64) % 16 == 0, "Wave64");
+
+/* the worker's shared words (NP > 1: the ticket claims and the poll phases) */
+struct Ctl64 {
+	uint64_t state;     /* lowest unclaimed ticket index << 1 | (index + 1 claimed) */
+	uint64_t issue[2];  /* each wave's last poll issue (s_memrealtime) */
+	uint64_t target[2]; /* the ticket index each wave's poll is for */
+	uint64_t since;     /* when the lowest unclaimed index last moved (spec window) */
+	uint32_t exited;    /* classifying waves that have left */
+	uint32_t queued;    /* the last claim came with its ticket's first poll */
+	uint32_t seq[2];    /* image sequence held by LDS table copy i (0xFF: none) */
+};
+static_assert(sizeof(Ctl64) % 16 == 0, "Ctl64");
+
+/* LDS of rxloop64_kernel<NP> with @copy bytes per table copy (a 64-B image
+ * header + the image): NP = 2 keeps a copy per host image buffer, so one wave
+ * can take a new snapshot while the other still classifies with the last */
+__host__ __device__ constexpr uint32_t loop64_lds(int np, uint32_t copy)
+{
+	return (uint32_t)sizeof(Ctl64) + np * (uint32_t)sizeof(Wave64) + (np > 1 ? 2 : 1) * copy;
+}
+
+/* rxloop64_kernel's writer wave: each posted burst's counts and counters,
+ * the poll counters, the stage stamps; leaves once every classifying wave has
+ * left and its mailboxes are drained. */
+template <int NP>
+__device__ __forceinline__ void rxloop64_writer(const LoopParams &L, Wave64 *wv, Ctl64 *ctl, int lane)
 {
 	uint32_t pe = 0, ps = 0, pl = 0; /* bursts by how they arrived (no indexed array: scratch) */
 	uint32_t pn = 0;                 /* bursts on classify_lean (gcl_rxloop_lean_bursts) */
-	for (uint32_t b = 0;; b ^= 1) {
-		Mbox64 &m = mbox[b];
-		for (;;) {
-			if (__hip_atomic_load(&m.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
-				break;
-			if (__hip_atomic_load(s_exit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) &&
-			    !__hip_atomic_load(&m.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
-				return;
-			__builtin_amdgcn_s_sleep(1);
+	for (uint32_t b = 0;; b = (b + 1) % (2 * NP)) {
+		Mbox64 &m = wv[b >> 1].mbox[b & 1];
+		if (!__hip_atomic_load(&m.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+			if (NP == 1) {
+				/* one producer, in order: wait on this mailbox */
+				for (;;) {
+					if (__hip_atomic_load(&m.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+						break;
+					if (__hip_atomic_load(&ctl->exited, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) &&
+					    !__hip_atomic_load(&m.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+						return;
+					__builtin_amdgcn_s_sleep(1);
+				}
+			} else {
+				if (b + 1 == 2 * NP) { /* a whole round found nothing posted */
+					bool any = false;
+					for (int i = 0; i < 2 * NP; i++)
+						any |= __hip_atomic_load(&wv[i >> 1].mbox[i & 1].flag, __ATOMIC_RELAXED,
+						                         __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
+					if (!any && __hip_atomic_load(&ctl->exited, __ATOMIC_RELAXED,
+					                              __HIP_MEMORY_SCOPE_WORKGROUP) == NP) {
+						bool late = false; /* posted between the two reads */
+						for (int i = 0; i < 2 * NP; i++)
+							late |= __hip_atomic_load(&wv[i >> 1].mbox[i & 1].flag, __ATOMIC_RELAXED,
+							                          __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
+						if (!late)
+							return;
+					}
+					__builtin_amdgcn_s_sleep(1);
+				}
+				continue;
+			}
 		}
 		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 		const uint64_t t_w = L.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
 		const uint64_t t = m.t;
 		const uint32_t n = m.n, kind = m.kind, lean = m.lean;
-		const __amdgpu_buffer_rsrc_t srs =
-		        gcl::host_rsrc(L.slots + ((t - 1) % L.nslots) * L.slot_bytes, L.slot_bytes);
-		if (L.writer && (uint32_t)lane < n) {
-			if (L.off_trans) {
-				const uint4 x = m.tr[lane];
-				const gcl::u32x4 v = {x.x, x.y, x.z, x.w};
-				__builtin_amdgcn_raw_buffer_store_b128(v, srs, (int)(L.off_trans + 16 * lane), 0,
-				                                       gcl::kSysAux);
-			}
-			const uint4 x = m.rec[lane];
-			const gcl::u32x4 v = {x.x, x.y, x.z, x.w};
-			__builtin_amdgcn_raw_buffer_store_b128(v, srs, (int)(L.off_verd + sizeof(LoopRec) * lane), 0,
-			                                       gcl::kSysAux);
-		}
-		const uint64_t t_s = L.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
 		const uint32_t p = m.p[lane];
 		if ((uint32_t)lane < n && p != ~0u && L.counts)
 			atomicAdd(&L.counts[p], 1ull);
@@ -1964,13 +1561,13 @@ __device__ __forceinline__ void rxloop64_writer(const LoopParams &L, Mbox64 *mbo
 			if (lean)
 				gcl::st_sys32(&L.polls[4 * blockIdx.x + 3], ++pn);
 			if (L.stamps) {
-				/* {ticket, hit's round trip, hit -> classified, hit -> records
-				 *  issued (by the writer when L.writer)}
+				/* {ticket, hit's round trip, hit -> classified, hit -> records issued}
 				 * {ticket, polls, hit lo, hi}
 				 * {ticket, hit -> packets in registers, hit -> posted, hit -> writer} */
+				const __amdgpu_buffer_rsrc_t srs =
+				        gcl::host_rsrc(L.slots + ((t - 1) % L.nslots) * L.slot_bytes, L.slot_bytes);
 				const uint64_t hit = (uint64_t)st[1] << 32 | st[0];
-				const gcl::u32x4 a = {(uint32_t)t, st[2], st[6],
-				                      L.writer ? (uint32_t)(t_s - hit) : st[7]};
+				const gcl::u32x4 a = {(uint32_t)t, st[2], st[6], st[7]};
 				const gcl::u32x4 b2 = {(uint32_t)t, st[3], st[0], st[1]};
 				const gcl::u32x4 c3 = {(uint32_t)t, st[4], st[5], (uint32_t)(t_w - hit)};
 				__builtin_amdgcn_raw_buffer_store_b128(a, srs, 16, 0, gcl::kSysAux);
@@ -1981,30 +1578,81 @@ __device__ __forceinline__ void rxloop64_writer(const LoopParams &L, Mbox64 *mbo
 	}
 }
 
-template <int MODE>
-__global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
+/* a value of lane 0, uniform (scalar) */
+__device__ __forceinline__ uint32_t lane0_u32(uint32_t v)
+{
+	return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+
+/* a shared control word another wave may write: an atomic LDS load (never
+ * hoisted or merged), uniform */
+__device__ __forceinline__ uint64_t ctl_ld64(const uint64_t *p)
+{
+	return lane0_u64(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+
+__device__ __forceinline__ uint32_t ctl_ld32(const uint32_t *p)
+{
+	return lane0_u32(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+
+/* NP > 1: claim ticket index @k for this wave (lane 0's LDS compare-and-swap
+ * on Ctl64::state); false if another wave has it */
+__device__ __forceinline__ bool loop64_claim(Ctl64 *ctl, uint64_t k, int lane)
+{
+	uint32_t ok = 0;
+	if (lane == 0) {
+		uint64_t s = __hip_atomic_load(&ctl->state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+		for (;;) {
+			const uint64_t kc = s >> 1, ah = s & 1;
+			uint64_t nx;
+			if (k == kc)
+				nx = (kc + 1 + ah) << 1;
+			else if (k == kc + 1 && !ah)
+				nx = s | 1;
+			else
+				break; /* claimed already */
+			if (__hip_atomic_compare_exchange_strong(&ctl->state, &s, nx, __ATOMIC_RELAXED,
+			                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+				if (k == kc) /* the lowest unclaimed index moved: a new spec window */
+					__hip_atomic_store(&ctl->since, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+					                   __HIP_MEMORY_SCOPE_WORKGROUP);
+				ok = 1;
+				break;
+			}
+		}
+	}
+	return lane0_u32(ok) != 0;
+}
+
+template <int MODE, int NP>
+__global__ void __launch_bounds__(64 * (NP + 1)) rxloop64_kernel(LoopParams L)
 {
 	extern __shared__ uint4 smem[];
-	Mbox64 *mbox = (Mbox64 *)smem;
-	uint64_t *s_offs = (uint64_t *)(mbox + 2);
-	uint32_t *s_fdir = (uint32_t *)(s_offs + 64), *s_hint = s_fdir + 64;
-	uint2 *s_trans = (uint2 *)(s_hint + 64);
-	uint32_t *s_exit = (uint32_t *)(s_trans + 64);
-	uint8_t *lds_tab = (uint8_t *)(s_exit + 4);
-	const int lane = threadIdx.x & 63;
+	Ctl64 *ctl = (Ctl64 *)smem;
+	Wave64 *wv = (Wave64 *)(ctl + 1);
+	uint8_t *copies = (uint8_t *)(wv + NP); /* NP > 1: two; each a LoopImgHdr + image */
+	const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 	if (threadIdx.x == 0) {
-		mbox[0].flag = 0;
-		mbox[1].flag = 0;
-		*s_exit = 0;
+		for (int i = 0; i < NP; i++)
+			wv[i].mbox[0].flag = wv[i].mbox[1].flag = 0;
+		ctl->state = 0;
+		ctl->issue[0] = ctl->issue[1] = 0;
+		ctl->target[0] = ctl->target[1] = ~0ull;
+		ctl->since = __builtin_amdgcn_s_memrealtime();
+		ctl->exited = 0;
+		ctl->queued = 0;
+		ctl->seq[0] = ctl->seq[1] = 0xFF;
 	}
 	__syncthreads(); /* the only barrier */
-	if (threadIdx.x >= 64) {
-		rxloop64_writer(L, mbox, s_exit, lane);
+	if (w == NP) {
+		rxloop64_writer<NP>(L, wv, ctl, lane);
 		return;
 	}
+	Wave64 &me = wv[w];
 	const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + L.lifetime_ticks;
 	const __amdgpu_buffer_rsrc_t frs = gcl::host_rsrc(L.frames, L.frames_len);
-	if (lane == 0 && blockIdx.x < 8) /* which XCD this worker runs on */
+	if (lane == 0 && w == 0 && blockIdx.x < 8) /* which XCD this worker runs on */
 		gcl::st_sys32(&L.where[blockIdx.x], __builtin_amdgcn_s_getreg((3 << 11) | 20) + 1);
 	KParams k = {};
 	k.frames = L.frames;
@@ -2012,217 +1660,160 @@ __global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
 	k.max_rt = L.max_rt;
 	k.cflags = L.cflags; /* with thread_bits in [31:24] */
 	k.default_flags = L.default_flags;
-	k.offs = s_offs;
-	k.trans = L.off_trans ? s_trans : nullptr;
+	k.offs = me.offs;
+	k.trans = L.off_trans ? me.trans : nullptr;
 	Tables tb = {};
-	uint32_t cur_seq = 0xFF; /* no image yet (versions are taken mod 64) */
+	uint32_t cur_seq = 0xFF, cur_copy = 0; /* the image this wave's tb points at */
 	uint32_t mb = 0;
-	/* hybrid polling (L.hybrid): the previous burst's wait took more than
-	 * one poll (the worker had caught up with the host), and when its
-	 * records were issued */
-	uint32_t prev_npoll = 1;
-	uint64_t t_done = 0;
 	const bool spec = L.spec, rec = L.hdr_rec;
+	/* NP > 1: this wave's estimate of a poll's round trip (s_memrealtime
+	 * ticks), which sets the other wave's phase */
+	uint32_t rt_est = 136;
+	uint64_t kmine = 0;    /* NP == 1: this worker's next ticket index */
+	uint64_t spec_end = __builtin_amdgcn_s_memrealtime() + L.spec_ticks;
+	uint32_t npoll = 0;    /* polls since the ticket polled became the lowest unclaimed */
+	uint64_t kprev = ~0ull;
 
-	for (uint64_t t = L.t0 + blockIdx.x + 1;; t += L.workers) {
+	for (uint32_t kk = 0;; kk++) {
+		/* the ticket this poll is for */
+		uint64_t kt = kmine;
+		if (NP > 1) {
+			const uint64_t s = ctl_ld64(&ctl->state);
+			const uint64_t kc = s >> 1;
+			const bool ah = s & 1;
+			kt = kc;
+			const int o = w ^ 1;
+			const uint64_t o_target = ctl_ld64(&ctl->target[o]);
+			if (o_target == kc) {
+				const uint64_t o_issue = ctl_ld64(&ctl->issue[o]);
+				const bool queued = ctl_ld32(&ctl->queued) != 0;
+				if (queued && !ah) {
+					kt = kc + 1; /* bursts are queued: poll the next one too */
+				} else {
+					/* the slot sampled half a round trip after the other wave */
+					const uint64_t at = o_issue + rt_est / 2;
+					while (__builtin_amdgcn_s_memrealtime() < at)
+						__builtin_amdgcn_s_sleep(1);
+				}
+			}
+			if (kt != kprev) { /* a new ticket for this wave: its own spec window */
+				npoll = 0;
+				kprev = kt;
+			}
+			const uint64_t since = ctl_ld64(&ctl->since);
+			spec_end = since + L.spec_ticks + (kt != kc ? L.spec_ticks : 0);
+		}
+		const uint64_t t = L.t0 + blockIdx.x + 1 + kt * L.workers;
 		uint8_t *slot = L.slots + ((t - 1) % L.nslots) * L.slot_bytes;
 		LoopSlotHdr *h = (LoopSlotHdr *)slot;
 		const __amdgpu_buffer_rsrc_t srs = gcl::host_rsrc(slot, L.slot_bytes);
-		/* the mailbox this burst will be posted to, freed by the writer long
-		 * before (waited for here, not after the hit) */
-		Mbox64 &m = mbox[mb];
-		while (__hip_atomic_load(&m.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
-			__builtin_amdgcn_s_sleep(1);
-		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-		/* the poll, as rxloop_kernel's: the slot word, and for the first
-		 * L.spec_ticks of a wait each lane's stamped offset or header record.
-		 * (Two polls in flight, so the slot is sampled twice per round trip,
-		 * measured slower: the lone burst 4.07 -> 4.35 us p50, 4 x 8 with
-		 * records 88 -> 72 Mpkt/s, offsets caught stale more often;
-		 * profiles/r04_loop64_ab.jsonl) */
 		const uint64_t stamp = loop_stamp(t, L.nslots);
 		const uint32_t rstamp = loop_rec_stamp(t, L.nslots);
-		/* Hybrid polling: a worker that had to wait for its last burst has
-		 * caught up with the host, whose next submit cannot land before it
-		 * has seen that burst's records (a PCIe write, then its post-pass):
-		 * a poll issued at once samples the slot too early and puts the
-		 * next samples a whole round trip apart from then on.  Its first
-		 * poll waits L.hybrid ticks after the records went out instead (as
-		 * NVMe hybrid polling sleeps before it spins).  A worker with bursts
-		 * queued (found on its first poll) never waits. */
-		if (L.hybrid && prev_npoll > 1)
-			while (__builtin_amdgcn_s_memrealtime() < t_done + L.hybrid)
-				__builtin_amdgcn_s_sleep(1);
-		const uint64_t spec_end = __builtin_amdgcn_s_memrealtime() + L.spec_ticks;
-		uint64_t w = 0, e = 0;
-		bool sp_hit = false;
-		uint4 q[4] = {}, qv[4] = {};
-		uint64_t t_issue = 0, hit = 0;
-		uint32_t npoll = 0;
-		/* GCL_TUNE_LOOP_DUAL (experiment): two polls in flight, the second
-		 * issued half a round trip after the first, so the slot is sampled
-		 * twice per round trip: half the wait for a burst that lands just
-		 * after a sample */
-		struct PollSet {
-			uint64_t ev, wv, t_issue;
-			uint4 q[4];
-			uint32_t sv;
-			bool sp;
-		};
-		auto issue = [&](PollSet &P, uint32_t kk) {
-			P.t_issue = __builtin_amdgcn_s_memrealtime();
-			P.sp = spec && P.t_issue < spec_end;
-			P.ev = P.sp && !rec ? gcl::ld_sys64(slot + L.off_offs + 8 * lane) : 0;
+		/* the poll: the slot word, and for the first L.spec_ticks of a wait
+		 * each lane's stamped offset or header record */
+		const uint64_t t_issue = __builtin_amdgcn_s_memrealtime();
+		if (NP > 1 && lane == 0) {
+			__hip_atomic_store(&ctl->issue[w], t_issue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+			__hip_atomic_store(&ctl->target[w], kt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+		}
+		npoll++;
+		const bool sp = spec && t_issue < spec_end;
+		const uint64_t ev = sp && !rec ? gcl::ld_sys64(slot + L.off_offs + 8 * lane) : 0;
+		uint4 q[4] = {};
+		if (sp && rec) {
 #pragma unroll
 			for (int j = 0; j < 4; j++) {
-				if (P.sp && rec) {
-					const auto v = __builtin_amdgcn_raw_buffer_load_b128(
-					        srs, (int)(L.off_hdr + L.rec_plane * j + 16 * lane), 0, gcl::kSysAux);
-					P.q[j] = make_uint4(v[0], v[1], v[2], v[3]);
-				} else {
-					P.q[j] = make_uint4(0, 0, 0, 0);
-				}
-			}
-			P.wv = 0;
-			P.sv = 0;
-			if (lane == 0) {
-				P.wv = gcl::ld_sys64(&h->word);
-				if ((kk & 7) >= 6) /* a stop waits for up to 8 polls */
-					P.sv = gcl::ld_sys32(L.stop);
-			}
-		};
-		/* true: leave the wait (the burst, a stop, or the lifetime's end).
-		 * @defer: a set that finds the word with a record or offset still
-		 * stale is passed over once, when the other set -- issued half a
-		 * round trip later -- will likely bring them current */
-		auto check = [&](PollSet &P, uint32_t kk, bool defer) -> bool {
-			const uint64_t wv = lane0_u64(P.wv);
-			const uint32_t sv = (uint32_t)__builtin_amdgcn_readfirstlane((int)P.sv);
-			if ((wv >> 24) == (t & ((1ull << 40) - 1))) {
-				if (defer && P.sp) {
-					const uint32_t n1 = (uint32_t)(wv >> 11) & 0x1FFF;
-					const bool cur = (uint32_t)lane >= n1 ||
-					                 (rec ? P.q[0].x == rstamp && P.q[1].x == rstamp &&
-					                                P.q[2].x == rstamp && P.q[3].x == rstamp
-					                      : (P.ev & ~kLoopOffMask) == stamp);
-					if (n1 <= 64 && !__all(cur))
-						return false;
-				}
-				w = wv;
-				e = P.ev;
-				sp_hit = P.sp;
-				t_issue = P.t_issue;
-				npoll = kk + 1;
-#pragma unroll
-				for (int j = 0; j < 4; j++)
-					q[j] = P.q[j];
-				return true;
-			}
-			return sv || __builtin_amdgcn_s_memrealtime() > t_end;
-		};
-		if (L.dual) {
-			PollSet A, B;
-			issue(A, 0);
-			while (__builtin_amdgcn_s_memrealtime() < A.t_issue + L.dual)
-				__builtin_amdgcn_s_sleep(1);
-			issue(B, 1);
-			/* a set passed over as stale is taken as it is on its next
-			 * check only if the other set did not bring the burst first */
-			bool stale_a = false, stale_b = false;
-			for (uint32_t kk = 0;; kk += 2) {
-				if (check(A, kk, !stale_a))
-					break;
-				stale_a = (lane0_u64(A.wv) >> 24) == (t & ((1ull << 40) - 1));
-				if (stale_a) { /* the word is there: B, half a round trip on, decides */
-					if (check(B, kk + 1, false))
-						break;
-				}
-				issue(A, kk + 2);
-				if (check(B, kk + 1, !stale_b))
-					break;
-				stale_b = (lane0_u64(B.wv) >> 24) == (t & ((1ull << 40) - 1));
-				if (stale_b) {
-					if (check(A, kk + 2, false))
-						break;
-				}
-				issue(B, kk + 3);
-			}
-		} else {
-			for (uint32_t kk = 0;; kk++) {
-				t_issue = __builtin_amdgcn_s_memrealtime();
-				npoll = kk + 1;
-				const bool sp = spec && t_issue < spec_end;
-				const uint64_t ev = sp && !rec ? gcl::ld_sys64(slot + L.off_offs + 8 * lane) : 0;
-				if (sp && rec) {
-	#pragma unroll
-					for (int j = 0; j < 4; j++) {
-						const auto v = __builtin_amdgcn_raw_buffer_load_b128(
-						        srs, (int)(L.off_hdr + L.rec_plane * j + 16 * lane), 0, gcl::kSysAux);
-						qv[j] = make_uint4(v[0], v[1], v[2], v[3]);
-					}
-				}
-				uint64_t wv = 0;
-				uint32_t sv = 0;
-				if (lane == 0) {
-					wv = gcl::ld_sys64(&h->word);
-					if ((kk & 7) == 7) /* a stop waits for up to 8 polls */
-						sv = gcl::ld_sys32(L.stop);
-				}
-				wv = lane0_u64(wv);
-				sv = (uint32_t)__builtin_amdgcn_readfirstlane((int)sv);
-				if ((wv >> 24) == (t & ((1ull << 40) - 1))) {
-					w = wv;
-					e = ev;
-					sp_hit = sp;
-	#pragma unroll
-					for (int j = 0; j < 4; j++)
-						q[j] = qv[j];
-					break;
-				}
-				if (sv || __builtin_amdgcn_s_memrealtime() > t_end)
-					break;
-				__builtin_amdgcn_s_sleep(1);
+				const auto v = __builtin_amdgcn_raw_buffer_load_b128(
+				        srs, (int)(L.off_hdr + L.rec_plane * j + 16 * lane), 0, gcl::kSysAux);
+				q[j] = make_uint4(v[0], v[1], v[2], v[3]);
 			}
 		}
-		if (L.stamps)
-			hit = __builtin_amdgcn_s_memrealtime();
-		if (!w)
-			break; /* stopped, or the lifetime is over */
-		const uint32_t nw = (uint32_t)(w >> 11) & 0x1FFF, fl = (uint32_t)(w >> 7) & 0xF;
-		const uint32_t img = (uint32_t)(w >> 6) & 1, img_seq = (uint32_t)w & 63;
+		uint64_t wv0 = 0;
+		uint32_t sv = 0;
+		if (lane == 0) {
+			wv0 = gcl::ld_sys64(&h->word);
+			if ((kk & 7) == 7) /* a stop waits for up to 8 polls */
+				sv = gcl::ld_sys32(L.stop);
+		}
+		const uint64_t w_word = lane0_u64(wv0);
+		sv = lane0_u32(sv);
+		const bool found = (w_word >> 24) == (t & ((1ull << 40) - 1));
+		if (NP > 1) {
+			const uint32_t d = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_issue);
+			rt_est = std::min(400u, std::max(50u, rt_est - rt_est / 8 + d / 8));
+		}
+		if (!found) {
+			if (NP > 1 && lane == 0)
+				__hip_atomic_store(&ctl->queued, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+			if (sv || __builtin_amdgcn_s_memrealtime() > t_end)
+				break; /* stopped, or the lifetime is over */
+			__builtin_amdgcn_s_sleep(1);
+			continue;
+		}
+		const uint32_t nw = (uint32_t)(w_word >> 11) & 0x1FFF, fl = (uint32_t)(w_word >> 7) & 0xF;
+		const uint32_t img = (uint32_t)(w_word >> 6) & 1, img_seq = (uint32_t)w_word & 63;
 		const bool live = (uint32_t)lane < nw;
-		const bool rok = sp_hit && q[0].x == rstamp && q[1].x == rstamp && q[2].x == rstamp &&
-		                 q[3].x == rstamp;
-		const bool fresh = !live || (rec ? rok : sp_hit && (e & ~kLoopOffMask) == stamp);
+		const bool rok = sp && q[0].x == rstamp && q[1].x == rstamp && q[2].x == rstamp && q[3].x == rstamp;
+		const bool fresh = !live || (rec ? rok : sp && (ev & ~kLoopOffMask) == stamp);
 		const bool early = spec && nw <= 64 && __all(fresh);
-		const uint32_t kind = early ? kLoopPollEarly : (sp_hit && nw <= 64) ? kLoopPollStale : kLoopPollLate;
-		if (img_seq != cur_seq) { /* a new table snapshot: this wave copies it into LDS */
-			const uint8_t *ib = L.img[img];
-			const uint32_t bytes = gcl::ld_sys32(ib);
-			const __amdgpu_buffer_rsrc_t irs = gcl::host_rsrc(ib, 64 + (uint64_t)bytes);
-			uint32_t *t32 = (uint32_t *)lds_tab;
-			for (uint32_t o = 16 * lane; o < bytes; o += 4 * 16 * 64) {
-				gcl::u32x4 x[4];
-#pragma unroll
-				for (int j = 0; j < 4; j++)
-					x[j] = __builtin_amdgcn_raw_buffer_load_b128(irs, (int)(64 + o + 1024 * j), 0,
-					                                            gcl::kSysAux);
-#pragma unroll
-				for (int j = 0; j < 4; j++)
-#pragma unroll
-					for (int d = 0; d < 4; d++)
-						if (o + 1024 * j + 4 * d < bytes)
-							t32[(o + 1024 * j) / 4 + d] = x[j][d];
+		if (NP > 1) {
+			/* stale records while the window lasts: the next sample brings them */
+			if (!early && sp && nw <= 64) {
+				__builtin_amdgcn_s_sleep(1);
+				continue;
 			}
-			k.ipt_mask = gcl::ld_sys32(ib + 4);
-			k.ipt_seed = gcl::ld_sys32(ib + 20);
-			tb.ipt = (const uint2 *)lds_tab;
-			tb.rtab = (const RtEntry *)(lds_tab + gcl::ld_sys32(ib + 8));
-			tb.flow = lds_tab + gcl::ld_sys32(ib + 12);
-			tb.toep = (const uint32_t *)(lds_tab + gcl::ld_sys32(ib + 16));
-			tb.seed = (const uint32_t *)(lds_tab + gcl::ld_sys32(ib + 24));
-			tb.crc = (const uint32_t *)(lds_tab + gcl::ld_sys32(ib + 28));
-			cur_seq = img_seq;
+			if (!loop64_claim(ctl, kt, lane))
+				continue; /* the other wave has it */
+			if (lane == 0)
+				__hip_atomic_store(&ctl->queued, npoll == 1 ? 1u : 0u, __ATOMIC_RELAXED,
+				                   __HIP_MEMORY_SCOPE_WORKGROUP);
+		}
+		const uint64_t hit = L.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
+		const uint32_t kind = early ? kLoopPollEarly : (sp && nw <= 64) ? kLoopPollStale : kLoopPollLate;
+		const uint32_t polls_used = npoll;
+		Mbox64 &m = me.mbox[mb]; /* free: waited for after the last post */
+		{ /* this burst's table snapshot */
+			const uint32_t cp = NP > 1 ? img : 0;
+			uint8_t *cb = copies + cp * L.lds_copy;
+			if (img_seq != cur_seq || cp != cur_copy) {
+				if (ctl_ld32(&ctl->seq[cp]) != img_seq) { /* copy it into LDS */
+					const uint8_t *ib = L.img[img];
+					const uint32_t bytes = gcl::ld_sys32(ib);
+					const __amdgpu_buffer_rsrc_t irs = gcl::host_rsrc(ib, 64 + (uint64_t)bytes);
+					uint32_t *t32 = (uint32_t *)cb;
+					for (uint32_t o = 16 * lane; o < 64 + bytes; o += 4 * 16 * 64) {
+						gcl::u32x4 x[4];
+#pragma unroll
+						for (int j = 0; j < 4; j++)
+							x[j] = __builtin_amdgcn_raw_buffer_load_b128(irs, (int)(o + 1024 * j), 0,
+							                                            gcl::kSysAux);
+#pragma unroll
+						for (int j = 0; j < 4; j++)
+#pragma unroll
+							for (int d = 0; d < 4; d++)
+								if (o + 1024 * j + 4 * d < 64 + bytes)
+									t32[(o + 1024 * j) / 4 + d] = x[j][d];
+					}
+					__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+					if (lane == 0)
+						__hip_atomic_store(&ctl->seq[cp], img_seq, __ATOMIC_RELAXED,
+						                   __HIP_MEMORY_SCOPE_WORKGROUP);
+				}
+				/* the copy (this wave's or the other's) before its reads */
+				__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+				const LoopImgHdr *ih = (const LoopImgHdr *)cb;
+				const uint8_t *tab = cb + 64;
+				k.ipt_mask = lane0_u32(ih->ipt_mask);
+				k.ipt_seed = lane0_u32(ih->ipt_seed);
+				tb.ipt = (const uint2 *)tab;
+				tb.rtab = (const RtEntry *)(tab + lane0_u32(ih->off_rt));
+				tb.flow = tab + lane0_u32(ih->off_flow);
+				tb.toep = (const uint32_t *)(tab + lane0_u32(ih->off_toep));
+				tb.seed = (const uint32_t *)(tab + lane0_u32(ih->off_seed));
+				tb.crc = (const uint32_t *)(tab + lane0_u32(ih->off_crc));
+				cur_seq = img_seq;
+				cur_copy = cp;
+			}
 		}
 		/* this lane's packet in registers: its header words and side fields */
 		HdrWords hw;
@@ -2253,7 +1844,7 @@ __global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
 				 * side loads issued between the offset's load and its use
 				 * made that use wait for them as well (vmcnt counts in
 				 * order, and the early path shares the use): two round trips */
-				const uint64_t ent = early ? e : gcl::ld_sys64(slot + L.off_offs + 8 * lane);
+				const uint64_t ent = early ? ev : gcl::ld_sys64(slot + L.off_offs + 8 * lane);
 				off = ent & kLoopOffMask;
 				/* keeps the side loads below the offset's use (the scheduler
 				 * would hoist them above it, and its wait with them) */
@@ -2282,13 +1873,13 @@ __global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
 			hw.d8 = r[2].x, hw.d9 = r[2].y, hw.d10 = r[2].z;
 		}
 		const uint64_t t_data = L.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
-		s_offs[lane] = off;
-		s_fdir[lane] = fdir;
-		s_hint[lane] = hint;
-		k.olflags = (fl & GCL_LOOP_F_OLF) ? (const uint8_t *)s_hint : nullptr; /* read via pre */
-		k.rss = (fl & GCL_LOOP_F_RSS) ? s_hint : nullptr;                      /* read via pre */
-		k.fdir = (fl & GCL_LOOP_F_FDIR) ? s_fdir : nullptr;
-		k.dst_hint = (fl & GCL_LOOP_F_HINT) ? s_hint : nullptr;
+		me.offs[lane] = off;
+		me.fdir[lane] = fdir;
+		me.hint[lane] = hint;
+		k.olflags = (fl & GCL_LOOP_F_OLF) ? (const uint8_t *)me.hint : nullptr; /* read via pre */
+		k.rss = (fl & GCL_LOOP_F_RSS) ? me.hint : nullptr;                      /* read via pre */
+		k.fdir = (fl & GCL_LOOP_F_FDIR) ? me.fdir : nullptr;
+		k.dst_hint = (fl & GCL_LOOP_F_HINT) ? me.hint : nullptr;
 		const uint32_t pre[2] = {olf, rss};
 		Counters cnt = {0, 0, 0, 0};
 		uint64_t t_cls = 0, t_st = 0;
@@ -2307,25 +1898,17 @@ __global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
 			const uint32_t hsh = v4 || v2 || v1 ? 0u : (uint32_t)v;
 			const uint32_t vlo = v1 ? (uint32_t)(uint8_t)v : v2 ? (uint32_t)(uint16_t)v
 			                   : v4 ? (uint32_t)v : (uint32_t)(v >> 32);
-			if (L.writer) {
-				m.rec[lane] = make_uint4(hsh, vlo, (uint32_t)t, (uint32_t)(t >> 32));
-				if (L.off_trans) {
-					const uint2 tr = s_trans[lane];
-					m.tr[lane] = make_uint4(tr.x, tr.y, (uint32_t)t, (uint32_t)(t >> 32));
-				}
-			} else { /* the records straight from the poller */
-				if (L.off_trans) {
-					const uint2 tr = s_trans[lane];
-					const gcl::u32x4 x = {tr.x, tr.y, (uint32_t)t, (uint32_t)(t >> 32)};
-					__builtin_amdgcn_raw_buffer_store_b128(x, srs, (int)(L.off_trans + 16 * lane), 0,
-					                                       gcl::kSysAux);
-				}
-				const gcl::u32x4 x = {hsh, vlo, (uint32_t)t, (uint32_t)(t >> 32)};
-				__builtin_amdgcn_raw_buffer_store_b128(x, srs, (int)(L.off_verd + sizeof(LoopRec) * lane),
-				                                       0, gcl::kSysAux);
-				if (L.stamps)
-					t_st = __builtin_amdgcn_s_memrealtime();
+			if (L.off_trans) { /* before the record: the host checks both tickets */
+				const uint2 tr = me.trans[lane];
+				const gcl::u32x4 x = {tr.x, tr.y, (uint32_t)t, (uint32_t)(t >> 32)};
+				__builtin_amdgcn_raw_buffer_store_b128(x, srs, (int)(L.off_trans + 16 * lane), 0,
+				                                       gcl::kSysAux);
 			}
+			const gcl::u32x4 x = {hsh, vlo, (uint32_t)t, (uint32_t)(t >> 32)};
+			__builtin_amdgcn_raw_buffer_store_b128(x, srs, (int)(L.off_verd + sizeof(LoopRec) * lane), 0,
+			                                       gcl::kSysAux);
+			if (L.stamps)
+				t_st = __builtin_amdgcn_s_memrealtime();
 		}
 		/* one packet per lane: each counter is 0 or 1 per lane, a ballot
 		 * (no cross-lane shuffles, which are LDS round trips) */
@@ -2346,7 +1929,7 @@ __global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
 				m.st[0] = (uint32_t)hit;
 				m.st[1] = (uint32_t)(hit >> 32);
 				m.st[2] = (uint32_t)(hit - t_issue);
-				m.st[3] = npoll;
+				m.st[3] = polls_used;
 				m.st[4] = (uint32_t)(t_data - hit);
 				m.st[5] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - hit);
 				m.st[6] = (uint32_t)(t_cls - hit);
@@ -2357,15 +1940,22 @@ __global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
 		if (lane == 0)
 			__hip_atomic_store(&m.flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 		mb ^= 1;
-		prev_npoll = npoll;
-		if (L.hybrid)
-			t_done = __builtin_amdgcn_s_memrealtime();
+		/* the mailbox the next burst will be posted to, freed by the writer
+		 * long before: waited for here, not after the next hit */
+		while (__hip_atomic_load(&me.mbox[mb].flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+			__builtin_amdgcn_s_sleep(1);
+		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+		if (NP == 1) { /* the next ticket, its own spec window */
+			kmine++;
+			npoll = 0;
+			spec_end = __builtin_amdgcn_s_memrealtime() + L.spec_ticks;
+		}
 	}
 	/* the writer drains what was posted, then leaves; the host stops
 	 * publishing on this word (one it reads without a HIP call per burst) */
 	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
 	if (lane == 0) {
-		__hip_atomic_store(s_exit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+		__hip_atomic_fetch_add(&ctl->exited, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 		gcl::st_sys32(L.exited, 1);
 	}
 }
@@ -2703,25 +2293,12 @@ struct gcl_ctx {
 	uint64_t prof_launches;
 	uint32_t prof_every;  /* time one launch in prof_every (gcl_profile_sample) */
 	uint64_t prof_seq;
+	/* geometry overrides, for the tests that cover every launch shape */
 	int tune_tables; /* GCL_TUNE_TABLES: 0 auto, 1 global, 2 lds-if-fits */
 	int tune_depth;  /* GCL_TUNE_DEPTH: tiles in flight per block (1 or 2) */
 	int tune_threads; /* GCL_TUNE_THREADS: 256, 512 or 1024 lanes per block */
-	int tune_nt_store; /* GCL_TUNE_NT_STORE: verdict store policy, 0 plain, 1 non-temporal
-	                      (8-B verdicts), 2 write-through sc0 sc1 (default) */
-	int tune_ablate;   /* GCL_TUNE_ABLATE bitmask (timing experiments only) */
-	int tune_vstage;   /* GCL_TUNE_VSTAGE: 1 = dense tiles' 1-/2-B verdicts staged in LDS */
-	int tune_sched;    /* GCL_TUNE_SCHED: 0 static persistent grid, 1 dynamic tile queue */
-	int tune_xcd_map;  /* GCL_TUNE_XCD_MAP: 1 contiguous eighth per XCD, 0 round-robin tiles */
-	int tune_pair;     /* GCL_TUNE_PAIR: 1 GENERAL batches on classify_pair_kernel */
-	int tune_pair_loads; /* GCL_TUNE_PAIR_LOADS: 1 = the pair kernel's frame loads non-temporal (experiment) */
-	int tune_general;  /* GCL_TUNE_GENERAL: 1 = fixed-slot batches on the GENERAL path too
-	                      (experiment: the pair kernel over host memory) */
-	/* dynamic tile queue: one slot per launch in flight, reused in turn; a
-	 * launch waits for the previous user of its slot (same or other stream) */
-	uint32_t *sched;
-	hipEvent_t sched_ev[GCL_SCHED_SLOTS];
-	bool sched_used[GCL_SCHED_SLOTS];
-	uint32_t sched_seq;
+	int tune_grid;    /* GCL_TUNE_GRID: blocks per launch (0: the persistent grid) */
+	int tune_bpc;     /* GCL_TUNE_BLOCKS_PER_CU: cap on blocks per CU (0: none) */
 };
 
 extern "C" {
@@ -2791,37 +2368,12 @@ extern "C" int gcl_open(int hip_device, const struct gcl_cfg *cfg, struct gcl_ct
 		c->tune_threads = e ? atoi(e) : 0;
 		if (c->tune_threads != 256 && c->tune_threads != 512 && c->tune_threads != 1024)
 			c->tune_threads = 0;
-		e = getenv("GCL_TUNE_NT_STORE");
-		c->tune_nt_store = e ? atoi(e) : kDefaultVerdictStore;
-		e = getenv("GCL_TUNE_ABLATE");
-		c->tune_ablate = e ? atoi(e) : 0;
-		e = getenv("GCL_TUNE_VSTAGE");
-		c->tune_vstage = e ? atoi(e) : kDefaultVstage;
 		e = getenv("GCL_TUNE_GRID");
-		g_tune_grid = e ? atoi(e) : 0;
+		c->tune_grid = e ? atoi(e) : 0;
 		e = getenv("GCL_TUNE_BLOCKS_PER_CU");
-		g_tune_bpc = e ? atoi(e) : 0;
-		e = getenv("GCL_TUNE_SCHED");
-		c->tune_sched = e ? atoi(e) : kDefaultSched;
-		e = getenv("GCL_TUNE_XCD_MAP");
-		c->tune_xcd_map = e ? atoi(e) : kDefaultXcdMap;
-		e = getenv("GCL_TUNE_PAIR");
-		c->tune_pair = e ? atoi(e) : kDefaultPair;
-		e = getenv("GCL_TUNE_PAIR_LOADS");
-		c->tune_pair_loads = e ? atoi(e) : 0;
-		e = getenv("GCL_TUNE_GENERAL");
-		c->tune_general = e ? atoi(e) : 0;
+		c->tune_bpc = e ? atoi(e) : 0;
 	}
 	c->dimg[0] = c->dimg[1] = nullptr;
-	c->sched = nullptr;
-	c->sched_seq = 0;
-	if (hipMalloc(&c->sched, GCL_SCHED_SLOTS * GCL_SCHED_WORDS * 4) != hipSuccess ||
-	    hipMemset(c->sched, 0, GCL_SCHED_SLOTS * GCL_SCHED_WORDS * 4) != hipSuccess)
-		goto fail;
-	for (int i = 0; i < GCL_SCHED_SLOTS; i++) {
-		he(hipEventCreateWithFlags(&c->sched_ev[i], hipEventDisableTiming));
-		c->sched_used[i] = false;
-	}
 	for (int i = 0; i < 2; i++) {
 		if (hipMalloc(&c->dimg[i], c->image_cap) != hipSuccess)
 			goto fail;
@@ -2848,8 +2400,6 @@ fail:
 	for (int i = 0; i < 2; i++)
 		if (c->dimg[i])
 			(void)hipFree(c->dimg[i]);
-	if (c->sched)
-		(void)hipFree(c->sched);
 	delete c;
 	return -ENOMEM;
 }
@@ -2870,9 +2420,6 @@ extern "C" void gcl_close(struct gcl_ctx *c)
 	(void)hipHostFree(c->staging);
 	(void)hipEventDestroy(c->staging_free);
 	(void)hipEventDestroy(c->tables_ready);
-	(void)hipFree(c->sched);
-	for (int i = 0; i < GCL_SCHED_SLOTS; i++)
-		(void)hipEventDestroy(c->sched_ev[i]);
 	for (int i = 0; i < c->e2e.nstreams; i++) {
 		(void)hipStreamDestroy(c->e2e.st[i]);
 		(void)hipFree(c->e2e.slab[i]);
@@ -3085,9 +2632,10 @@ static hipEvent_t prof_event(gcl_ctx *c)
 typedef void (*ClassifyFn)(KParams);
 
 /* Persistent grid of @fn (@nt-lane blocks, @lds bytes of LDS each): as many
- * blocks per CU as fit, capped at @bpc_cap, never more than tiles. */
+ * blocks per CU as fit, capped at @bpc_cap (or @grid blocks when > 0),
+ * never more than tiles. */
 static hipError_t launch_fn(ClassifyFn fn, int nt, KParams k, uint32_t lds, int num_cus,
-                            int bpc_cap, hipStream_t s)
+                            int bpc_cap, int grid_set, hipStream_t s)
 {
 	static std::mutex mu;
 	static std::map<std::pair<const void *, uint32_t>, int> occ_cache;
@@ -3114,84 +2662,67 @@ static hipError_t launch_fn(ClassifyFn fn, int nt, KParams k, uint32_t lds, int 
 	}
 	if (bpc_cap > 0 && bpc_cap < occ)
 		occ = bpc_cap;
-	if (g_tune_bpc > 0 && g_tune_bpc < occ)
-		occ = g_tune_bpc;
 	k.ntiles = (k.n + nt - 1) / nt;
 	uint64_t grid = (uint64_t)num_cus * (uint64_t)occ;
-	if (g_tune_grid > 0)
-		grid = (uint64_t)g_tune_grid;
+	if (grid_set > 0)
+		grid = (uint64_t)grid_set;
 	if (grid > k.ntiles)
 		grid = k.ntiles;
 	if (grid < 1)
 		grid = 1;
-	if (grid % GCL_SCHED_XCD) /* the per-XCD walk needs whole rows of 8 blocks */
-		k.xcd_map = 0;
 	hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(nt), lds, s, k);
 	return hipGetLastError();
 }
 
-template <int MODE, int DEPTH, int NT>
-static hipError_t launch_nt(const KParams &k, bool tlds, bool general, uint32_t lds,
-                            int num_cus, int bpc_cap, hipStream_t s)
-{
-	const ClassifyFn fn = tlds ? (general ? classify_kernel<MODE, true, true, DEPTH, NT>
-	                                      : classify_kernel<MODE, true, false, DEPTH, NT>)
-	                           : (general ? classify_kernel<MODE, false, true, DEPTH, NT>
-	                                      : classify_kernel<MODE, false, false, DEPTH, NT>);
-	return launch_fn(fn, NT, k, lds, num_cus, bpc_cap, s);
-}
-
-template <int MODE, int NT>
-static hipError_t launch_pair(const KParams &k, bool tlds, uint32_t lds, int num_cus, int bpc_cap,
-                              bool ntl, hipStream_t s)
-{
-	/* the bench's and the iokernel's format, 2-byte verdicts stored
-	 * write-through, compiled in; every other format (and the timing-only
-	 * ablations) reads k.cflags.  25 % fewer static VALU instructions and
-	 * SGPR spills 27 -> 8, but the working-set row is unchanged (96.5-97.3
-	 * us, profiles/r03_ws_ab_vf2.jsonl): the loop is not bound by them */
-	const bool v2 = (k.cflags & GCL_CFG_VERDICT2) && k.nt_store == 2 && !k.ablate;
-	ClassifyFn fn = v2 ? (tlds ? classify_pair_kernel<MODE, true, NT, 2>
-	                           : classify_pair_kernel<MODE, false, NT, 2>)
-	                   : (tlds ? classify_pair_kernel<MODE, true, NT, 0>
-	                           : classify_pair_kernel<MODE, false, NT, 0>);
-	if (ntl && v2 && tlds && NT == 256) /* the streaming-hint experiment */
-		fn = classify_pair_kernel<MODE, true, NT, 2, true>;
-	return launch_fn(fn, NT, k, lds, num_cus, bpc_cap, s);
-}
-
-/* Launch geometry (measured on MI355X, tools/cbench.cpp): */
+/* Launch geometry (measured on MI355X, choose_geometry) */
 struct Geometry {
 	int threads;  /* packets per tile = lanes per block */
 	int depth;    /* tiles in flight per block */
 	int bpc_cap;  /* blocks per CU */
+	int grid;     /* blocks per launch when > 0 (GCL_TUNE_GRID) */
 	bool pair;    /* classify_pair_kernel (GENERAL batches): [8, 40) per packet by lane pairs */
-	bool ntl;     /* its frame loads with the streaming hint (GCL_TUNE_PAIR_LOADS=1) */
 };
 
-/* LDS for the tile's header sources (s_src, classify_kernel): GENERAL */
-static uint32_t offs_lds_bytes(bool general, uint32_t nt)
+template <int MODE, int DEPTH, int NT>
+static hipError_t launch_nt(const KParams &k, bool tlds, uint32_t lds, int num_cus, const Geometry &geo,
+                            hipStream_t s)
 {
-	return general ? nt * 16 : 0; /* one hdr_src uint4 per packet */
+	const ClassifyFn fn = tlds ? classify_kernel<MODE, true, DEPTH, NT> : classify_kernel<MODE, false, DEPTH, NT>;
+	return launch_fn(fn, NT, k, lds, num_cus, geo.bpc_cap, geo.grid, s);
+}
+
+template <int MODE, int NT>
+static hipError_t launch_pair(const KParams &k, bool tlds, uint32_t lds, int num_cus, const Geometry &geo,
+                              hipStream_t s)
+{
+	/* the iokernel's ingress format, 2-byte queue verdicts, compiled in;
+	 * every other format reads k.cflags.  25 % fewer static VALU
+	 * instructions and SGPR spills 27 -> 8, but the working-set row is
+	 * unchanged (96.5-97.3 us, profiles/r03_ws_ab_vf2.jsonl): the loop is
+	 * not bound by them */
+	const bool v2 = (k.cflags & GCL_CFG_VERDICT2) != 0;
+	ClassifyFn fn = v2 ? (tlds ? classify_pair_kernel<MODE, true, NT, 2>
+	                           : classify_pair_kernel<MODE, false, NT, 2>)
+	                   : (tlds ? classify_pair_kernel<MODE, true, NT, 0>
+	                           : classify_pair_kernel<MODE, false, NT, 0>);
+	return launch_fn(fn, NT, k, lds, num_cus, geo.bpc_cap, geo.grid, s);
 }
 
 template <int MODE>
-static hipError_t launch_mode(const KParams &k, bool tlds, bool general, const Geometry &geo,
+static hipError_t launch_mode(const KParams &k, bool tlds, const Geometry &geo,
                               uint32_t tab_lds, uint32_t hist_bytes, int num_cus, hipStream_t s)
 {
 	if (geo.pair) {
 		const uint32_t lds = hist_bytes + tab_lds;
 		if (geo.threads == 1024)
-			return launch_pair<MODE, 1024>(k, tlds, lds, num_cus, geo.bpc_cap, geo.ntl, s);
+			return launch_pair<MODE, 1024>(k, tlds, lds, num_cus, geo, s);
 		if (geo.threads == 512)
-			return launch_pair<MODE, 512>(k, tlds, lds, num_cus, geo.bpc_cap, geo.ntl, s);
-		return launch_pair<MODE, 256>(k, tlds, lds, num_cus, geo.bpc_cap, geo.ntl, s);
+			return launch_pair<MODE, 512>(k, tlds, lds, num_cus, geo, s);
+		return launch_pair<MODE, 256>(k, tlds, lds, num_cus, geo, s);
 	}
-	const uint32_t lds = (uint32_t)geo.threads * 64 + kLdsQueueBytes + hist_bytes + tab_lds +
-	                     offs_lds_bytes(general, (uint32_t)geo.threads) +
-	                     (k.vstage ? (uint32_t)geo.threads * 2 : 0);
+	const uint32_t lds = (uint32_t)geo.threads * 64 + hist_bytes + tab_lds;
 #define GCL_LAUNCH(D, T) \
-	return launch_nt<MODE, D, T>(k, tlds, general, lds, num_cus, geo.bpc_cap, s)
+	return launch_nt<MODE, D, T>(k, tlds, lds, num_cus, geo, s)
 	if (geo.depth == 2) {
 		if (geo.threads == 1024) GCL_LAUNCH(2, 1024);
 		if (geo.threads == 512) GCL_LAUNCH(2, 512);
@@ -3204,7 +2735,7 @@ static hipError_t launch_mode(const KParams &k, bool tlds, bool general, const G
 }
 
 /*
- * Launch geometry.  Measured on MI355X with tools/cbench.cpp (interleaved, in
+ * Launch geometry.  Measured on MI355X with tools/cbench.cpp (removed in round 5; interleaved, in
  * one process, against a compute-free kernel of the same traffic): the
  * classifier is fastest with about 1024 resident lanes per CU -- 256-lane
  * blocks x 4 when the tables are small, and for the 1024-runtime tables
@@ -3219,24 +2750,16 @@ static Geometry choose_geometry(const gcl_ctx *c, uint32_t tab_lds, uint32_t his
 	Geometry g;
 	g.depth = 1;
 	g.threads = 0;
-	/* GENERAL batches run on the lane-pair classify_pair_kernel by default
-	 * (kDefaultPair 1), and on the LDS-tile classify_kernel with
-	 * GCL_TUNE_PAIR=0 -- or whenever the dynamic tile queue
-	 * (GCL_TUNE_SCHED), depth 1 (GCL_TUNE_DEPTH=1) or the membench body
-	 * (GCL_TUNE_ABLATE bit 16) is asked for, which only it implements.
-	 * (Round 2's register-header classify_quad_kernel, 64-B windows
-	 * transposed across lane quads, was removed in round 3: the pair kernel
-	 * does the same without the window, and beat it on every row --
-	 * working set 96 vs 109-111 us, random pool 181 vs 189,
-	 * profiles/r03_ws_ab.jsonl.) */
-	g.pair = general && c->tune_pair && !c->tune_sched && c->tune_depth != 1 &&
-	         !(c->tune_ablate & 16);
-	g.ntl = c->tune_pair_loads & 1;
+	/* GENERAL batches run on the lane-pair classify_pair_kernel.  (Round 2's
+	 * register-header classify_quad_kernel was removed in round 3, and the
+	 * LDS-tile kernel's GENERAL path -- 64-B windows staged per packet --
+	 * in round 5: the pair kernel beat both on every row, working set 96
+	 * vs 109-111 us, random pool 181 vs 189, profiles/r03_ws_ab.jsonl.) */
+	g.pair = general;
 	auto per_block = [&](uint32_t nt) -> uint32_t {
 		if (g.pair)
 			return hist_bytes + tab_lds;
-		return nt * 64 + kLdsQueueBytes + hist_bytes + tab_lds + offs_lds_bytes(general, nt) +
-		       (c->tune_vstage && !general ? nt * 2 : 0);
+		return nt * 64 + hist_bytes + tab_lds;
 	};
 	for (int nt = 256; nt <= 1024 && !g.threads; nt *= 2) {
 		const uint32_t pb = per_block((uint32_t)nt);
@@ -3250,24 +2773,20 @@ static Geometry choose_geometry(const gcl_ctx *c, uint32_t tab_lds, uint32_t his
 		g.bpc_cap = (int)(lds_cu / per_block(256));
 		if (g.bpc_cap < 1)
 			g.bpc_cap = 1;
-	} else if (g.threads <= 512 && !c->tune_sched) {
+	} else if (g.threads <= 512) {
 		/* a second tile in flight per block: 1.1-1.7 % faster on udp64 at
 		 * 4 x 256 lanes (profiles/archive/r01_cbench_depth_*); at 2 x 512 lanes (the
 		 * 1024-runtime tables) 1 % on the 8 Mi header-split layout, 3.4 % at
 		 * 32 Mi, and no change on tcp1500 (profiles/archive/r01_hsplit_geometry.jsonl) */
 		g.depth = 2;
 	}
-	if (g.pair && c->tune_pair == 2) { /* experiment: 2048 resident lanes per CU */
-		const uint32_t pb = per_block((uint32_t)g.threads);
-		if ((uint32_t)(2 * g.bpc_cap) * pb <= lds_cu)
-			g.bpc_cap *= 2;
-	}
 	if (c->tune_threads)
 		g.threads = c->tune_threads;
 	if (c->tune_depth)
 		g.depth = c->tune_depth;
-	if (g_tune_bpc)
-		g.bpc_cap = g_tune_bpc;
+	if (c->tune_bpc)
+		g.bpc_cap = c->tune_bpc;
+	g.grid = c->tune_grid;
 	return g;
 }
 
@@ -3469,14 +2988,11 @@ extern "C" int gcl_classify_ex(struct gcl_ctx *c, const struct gcl_batch *b,
 	k.trans = (uint2 *)out->trans;
 	k.cflags = kernel_cflags(c);
 	k.default_flags = c->cfg.default_olflags;
-	k.nt_store = c->tune_nt_store;
-	k.ablate = c->tune_ablate;
-	k.xcd_map = c->tune_xcd_map;
 
 	/* the specialised fast path needs every header granule in range */
 	bool general = b->offs || b->olflags || b->fdir_hi || b->dst_hint ||
 	               (c->cfg.default_olflags & GCL_F_FDIR_ID) ||
-	               b->frames_len < (b->n - 1) * b->stride + GCL_HDR_GRANULE || c->tune_general;
+	               b->frames_len < (b->n - 1) * b->stride + GCL_HDR_GRANULE;
 	uint32_t tab_bytes = c->image_bytes;
 	uint32_t hist_bytes = ((c->cfg.max_runtimes + 3) & ~3u) * 4;
 	bool tlds = tab_bytes <= kLdsTableBudget;
@@ -3485,18 +3001,9 @@ extern "C" int gcl_classify_ex(struct gcl_ctx *c, const struct gcl_batch *b,
 	else if (c->tune_tables == 2)
 		tlds = tab_bytes <= kLdsTableBudget;
 	k.tables_lds_bytes = tlds ? tab_bytes : 0;
-	k.vstage = c->tune_vstage && !general && ((uintptr_t)verdicts & 7) == 0 &&
-	           (k.cflags & (GCL_CFG_VERDICT1 | GCL_CFG_VERDICT2)) ? 1 : 0;
 	Geometry geo = choose_geometry(c, tlds ? tab_bytes : 0, hist_bytes, general);
 
 	HipErr he;
-	int slot = -1;
-	if (c->tune_sched && geo.depth == 1) {
-		slot = (int)(c->sched_seq++ % GCL_SCHED_SLOTS);
-		if (c->sched_used[slot])
-			he(hipStreamWaitEvent(s, c->sched_ev[slot], 0));
-		k.sched = c->sched + (size_t)slot * GCL_SCHED_WORDS;
-	}
 
 	hipEvent_t e0 = nullptr, e1 = nullptr;
 	if ((c->cfg.flags & GCL_CFG_PROFILE) && c->prof_seq++ % c->prof_every == 0) {
@@ -3515,16 +3022,13 @@ extern "C" int gcl_classify_ex(struct gcl_ctx *c, const struct gcl_batch *b,
 	hipError_t err;
 	switch (c->cfg.hash_mode) {
 	case GCL_HASH_NIC:
-		err = launch_mode<GCL_HASH_NIC>(k, tlds, general, geo, tlds ? tab_bytes : 0, hist_bytes,
-		                                c->num_cus, s);
+		err = launch_mode<GCL_HASH_NIC>(k, tlds, geo, tlds ? tab_bytes : 0, hist_bytes, c->num_cus, s);
 		break;
 	case GCL_HASH_JENKINS:
-		err = launch_mode<GCL_HASH_JENKINS>(k, tlds, general, geo, tlds ? tab_bytes : 0,
-		                                    hist_bytes, c->num_cus, s);
+		err = launch_mode<GCL_HASH_JENKINS>(k, tlds, geo, tlds ? tab_bytes : 0, hist_bytes, c->num_cus, s);
 		break;
 	default:
-		err = launch_mode<GCL_HASH_TOEPLITZ>(k, tlds, general, geo, tlds ? tab_bytes : 0,
-		                                     hist_bytes, c->num_cus, s);
+		err = launch_mode<GCL_HASH_TOEPLITZ>(k, tlds, geo, tlds ? tab_bytes : 0, hist_bytes, c->num_cus, s);
 		break;
 	}
 	if (e0) {
@@ -3537,10 +3041,6 @@ extern "C" int gcl_classify_ex(struct gcl_ctx *c, const struct gcl_batch *b,
 		}
 	}
 	const int iu = image_used(c, s);
-	if (slot >= 0) {
-		he(hipEventRecord(c->sched_ev[slot], s));
-		c->sched_used[slot] = true;
-	}
 	c->last_stream = s;
 	return err == hipSuccess && !he.bad() && !iu ? 0 : -EIO;
 }
@@ -3643,9 +3143,10 @@ extern "C" int gcl_dev_free(void *p)
 namespace {
 
 /* The classify kernel's memory shape without its compute: 256-packet tiles of
- * 64-B granules read with four nt 16-B loads per lane, one VB-byte store per
- * packet (tile t writes slot t % wtiles of the write side). */
-template <bool WT, int VB>
+ * 64-B granules read with four nt 16-B loads per lane, one VB-byte
+ * write-through store per packet, like the verdict stores (tile t writes slot
+ * t % wtiles of the write side). */
+template <int VB>
 __global__ void __launch_bounds__(256) pair_probe_kernel(const uint8_t *rd, uint64_t ntiles,
                                                          uint8_t *wr, uint64_t wtiles)
 {
@@ -3675,31 +3176,14 @@ __global__ void __launch_bounds__(256) pair_probe_kernel(const uint8_t *rd, uint
 		const uint4 a = tile[tile_slot(p, 0)], b = tile[tile_slot(p, 1)];
 		const uint32_t v = a.x ^ a.w ^ b.y ^ b.z;
 		const uint64_t i = (t % wtiles) * 256 + p;
-		/* WT: the classify kernel's default verdict store (kDefaultVerdictStore) */
-		if (VB == 1) {
-			if (WT)
-				__hip_atomic_store(wr + i, (uint8_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-			else
-				wr[i] = (uint8_t)v;
-		} else if (VB == 2) {
-			if (WT)
-				__hip_atomic_store((uint16_t *)wr + i, (uint16_t)v, __ATOMIC_RELAXED,
-				                   __HIP_MEMORY_SCOPE_SYSTEM);
-			else
-				((uint16_t *)wr)[i] = (uint16_t)v;
-		} else if (VB == 8) {
-			if (WT)
-				__hip_atomic_store((uint64_t *)wr + i, (uint64_t)v * 0x100000001ull,
-				                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-			else
-				((uint64_t *)wr)[i] = (uint64_t)v * 0x100000001ull;
-		} else {
-			if (WT)
-				__hip_atomic_store((uint32_t *)wr + i, v, __ATOMIC_RELAXED,
-				                   __HIP_MEMORY_SCOPE_SYSTEM);
-			else
-				((uint32_t *)wr)[i] = v;
-		}
+		if (VB == 1)
+			store_wt(wr + i, (uint8_t)v);
+		else if (VB == 2)
+			store_wt((uint16_t *)wr + i, (uint16_t)v);
+		else if (VB == 8)
+			store_wt((uint64_t *)wr + i, (uint64_t)((uint64_t)v * 0x100000001ull));
+		else
+			store_wt((uint32_t *)wr + i, v);
 		__syncthreads();
 		t = nx;
 	}
@@ -3720,29 +3204,19 @@ double pair_probe(const uint8_t *rd, size_t rd_bytes, uint8_t *wr, size_t wr_byt
 	const uint64_t wtiles = std::min<size_t>(wr_bytes, kPairProbeWriteMax) / (256 * (size_t)vb);
 	if (!ntiles || !wtiles)
 		return -1;
-	/* the store policy decides which pairs collide: probe with the one the
-	 * classify kernel will use (GCL_TUNE_NT_STORE, as gcl_open) */
-	const char *e = getenv("GCL_TUNE_NT_STORE");
-	const bool wt = (e ? atoi(e) : kDefaultVerdictStore) == 2;
+	/* the store policy decides which pairs collide: the probe stores the
+	 * way the classify kernel does (write-through) */
 	auto launch = [&]() {
 		const dim3 g(cus * 4), b(256);
-#define GCL_PROBE(W, V) hipLaunchKernelGGL((pair_probe_kernel<W, V>), g, b, 0, s, rd, ntiles, wr, wtiles)
-		if (vb == 1 && wt)
-			GCL_PROBE(true, 1);
-		else if (vb == 1)
-			GCL_PROBE(false, 1);
-		else if (vb == 2 && wt)
-			GCL_PROBE(true, 2);
+#define GCL_PROBE(V) hipLaunchKernelGGL((pair_probe_kernel<V>), g, b, 0, s, rd, ntiles, wr, wtiles)
+		if (vb == 1)
+			GCL_PROBE(1);
 		else if (vb == 2)
-			GCL_PROBE(false, 2);
-		else if (vb == 8 && wt)
-			GCL_PROBE(true, 8);
+			GCL_PROBE(2);
 		else if (vb == 8)
-			GCL_PROBE(false, 8);
-		else if (wt)
-			GCL_PROBE(true, 4);
+			GCL_PROBE(8);
 		else
-			GCL_PROBE(false, 4);
+			GCL_PROBE(4);
 #undef GCL_PROBE
 	};
 	double best = 1e30;
@@ -4134,9 +3608,7 @@ struct gcl_rxloop {
 	bool ended;              /* the kernel has finished (hipStreamQuery) */
 	bool left;               /* some worker has left: submit no more */
 	bool k64;                /* rxloop64_kernel (bursts <= 64) */
-	bool nt_submit;          /* header records by non-temporal stores (GCL_TUNE_LOOP_NT):
-	                            measured no different, lone burst 3.90-4.02 us p50 either
-	                            way (profiles/r04_loop_nt_ab.jsonl); off */
+	int np;                  /* its poll-and-classify waves (1 or 2) */
 };
 
 static uint64_t now_ns()
@@ -4211,7 +3683,7 @@ static int loop_write_image(gcl_rxloop *L, int i)
 	const uint32_t bytes = build_image(c);
 	if (!bytes)
 		return -ENOSPC;
-	if (bytes > kLdsTableBudget)
+	if (bytes > kLdsTableBudget || (L->k64 && 64 + bytes > L->lp.lds_copy))
 		return -E2BIG;
 	LoopImgHdr hdr = {};
 	hdr.bytes = bytes;
@@ -4228,22 +3700,26 @@ static int loop_write_image(gcl_rxloop *L, int i)
 	return 0;
 }
 
-/* bursts of <= 64 packets: rxloop64_kernel (2 waves, no barrier), unless
- * GCL_TUNE_LOOP64=0 asks for the general loop (A/B) */
+/* bursts of <= 64 packets: rxloop64_kernel with @np poll-and-classify waves
+ * (+ the writer, no barrier), or with np 0 the general loop (bursts past 64,
+ * or GCL_TUNE_LOOP64=0 for A/Bs) */
 template <int MODE>
-static hipError_t loop_launch(const LoopParams &lp, bool k64, hipStream_t s)
+static hipError_t loop_launch(const LoopParams &lp, int np, hipStream_t s)
 {
-	const void *fn = k64 ? (const void *)rxloop64_kernel<MODE> : (const void *)rxloop_kernel<MODE>;
-	const uint32_t lds = k64 ? kLoop64Lds + kLdsTableBudget
-	                         : kLoopFixedLds + ((lp.max_rt + 3) & ~3u) * 4 + kLdsTableBudget;
+	const void *fn = np == 2 ? (const void *)rxloop64_kernel<MODE, 2>
+	               : np == 1 ? (const void *)rxloop64_kernel<MODE, 1> : (const void *)rxloop_kernel<MODE>;
+	const uint32_t lds = np ? loop64_lds(np, lp.lds_copy)
+	                        : kLoopFixedLds + ((lp.max_rt + 3) & ~3u) * 4 + kLdsTableBudget;
 	if (lds > 64 * 1024) {
 		const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
 		                                         160 * 1024);
 		if (e != hipSuccess)
 			return e;
 	}
-	if (k64)
-		hipLaunchKernelGGL(rxloop64_kernel<MODE>, dim3(lp.workers), dim3(128), lds, s, lp);
+	if (np == 2)
+		hipLaunchKernelGGL((rxloop64_kernel<MODE, 2>), dim3(lp.workers), dim3(192), lds, s, lp);
+	else if (np == 1)
+		hipLaunchKernelGGL((rxloop64_kernel<MODE, 1>), dim3(lp.workers), dim3(128), lds, s, lp);
 	else
 		hipLaunchKernelGGL(rxloop_kernel<MODE>, dim3(lp.workers), dim3(256), lds, s, lp);
 	return hipGetLastError();
@@ -4295,25 +3771,30 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 	lp.off_verd = lp.off_hint + 4 * mb;
 	lp.hdr_rec = (cfg->flags & GCL_LOOP_HDR_RECORDS) != 0;
 	lp.stamps = (cfg->flags & GCL_LOOP_STAMPS) != 0;
-	lp.fast_clock = kDefaultLoopClock;
-	lp.writer = kDefaultLoopWriter;
-	if (const char *e = getenv("GCL_TUNE_LOOP_WRITER"))
-		lp.writer = atoi(e) != 0;
 	lp.lean = kDefaultLoopLean;
 	if (const char *e = getenv("GCL_TUNE_LOOP_LEAN"))
 		lp.lean = atoi(e) != 0;
-	if (const char *e = getenv("GCL_TUNE_LOOP_DUAL")) /* experiment: ticks of 10 ns */
-		lp.dual = (uint32_t)atoi(e);
-	lp.hybrid = kDefaultLoopHybrid;
-	if (const char *e = getenv("GCL_TUNE_LOOP_HYBRID")) /* ticks of 10 ns, 0: off */
-		lp.hybrid = (uint32_t)atoi(e);
-	if (const char *e = getenv("GCL_TUNE_LOOP_CLOCK"))
-		lp.fast_clock = atoi(e) != 0;
 	lp.off_hdr = (cfg->flags & (GCL_LOOP_INLINE_HDRS | GCL_LOOP_HDR_RECORDS))
 	                     ? lp.off_verd + sizeof(LoopRec) * mb : 0;
 	lp.rec_plane = (uint32_t)(16 * mb);
 	lp.spec = (!lp.off_hdr || lp.hdr_rec) && cfg->max_burst <= 64;
 	lp.spec_ticks = kLoopSpecTicks;
+	/* rxloop64_kernel: NP poll-and-classify waves; NP 2 holds two table
+	 * copies in LDS, so only where two fit */
+	L->k64 = cfg->max_burst <= 64;
+	if (const char *e = getenv("GCL_TUNE_LOOP64")) /* 0: the general loop, for A/Bs */
+		L->k64 = L->k64 && atoi(e) != 0;
+	L->np = kDefaultLoopPollers;
+	if (const char *e = getenv("GCL_TUNE_LOOP_POLLERS"))
+		L->np = atoi(e) == 2 ? 2 : 1;
+	lp.lds_copy = 64 + kLdsTableBudget;
+	if (L->np == 2) {
+		lp.lds_copy = align16(64 + std::min(c->image_cap, kLdsTableBudget));
+		if (loop64_lds(2, lp.lds_copy) > 160 * 1024) {
+			L->np = 1;
+			lp.lds_copy = 64 + kLdsTableBudget;
+		}
+	}
 	if (const char *e = getenv("GCL_TUNE_LOOP_SPEC")) /* experiments: ticks of 10 ns */
 		lp.spec_ticks = (uint32_t)atoi(e);
 	{
@@ -4368,15 +3849,10 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 	if (hipStreamCreateWithFlags(&L->st, hipStreamNonBlocking) != hipSuccess)
 		goto fail;
 	{
-		bool k64 = cfg->max_burst <= 64;
-		if (const char *e = getenv("GCL_TUNE_LOOP64"))
-			k64 = k64 && atoi(e) != 0;
-		L->k64 = k64;
-		if (const char *e = getenv("GCL_TUNE_LOOP_NT"))
-			L->nt_submit = atoi(e) != 0;
-		hipError_t e = c->cfg.hash_mode == GCL_HASH_NIC ? loop_launch<GCL_HASH_NIC>(lp, k64, L->st)
-		             : c->cfg.hash_mode == GCL_HASH_JENKINS ? loop_launch<GCL_HASH_JENKINS>(lp, k64, L->st)
-		             : loop_launch<GCL_HASH_TOEPLITZ>(lp, k64, L->st);
+		const int np = L->k64 ? L->np : 0;
+		hipError_t e = c->cfg.hash_mode == GCL_HASH_NIC ? loop_launch<GCL_HASH_NIC>(lp, np, L->st)
+		             : c->cfg.hash_mode == GCL_HASH_JENKINS ? loop_launch<GCL_HASH_JENKINS>(lp, np, L->st)
+		             : loop_launch<GCL_HASH_TOEPLITZ>(lp, np, L->st);
 		if (e != hipSuccess) {
 			(void)hipStreamDestroy(L->st);
 			L->st = nullptr;
@@ -4440,23 +3916,13 @@ static void loop_write_records(gcl_rxloop *L, uint64_t t, uint8_t *dst, uint32_t
 		const u32x4_h c2 = __builtin_shufflevector(side, v1, 0, 7, 2, 3); /* S d10 rss fdir */
 		const u32x4_h c3 = u32x4_h{S, (uint32_t)off, (uint32_t)(off >> 32) | olf << 8,
 		                           dst_hint ? dst_hint[i] : 0u};
-		if (L->nt_submit) {
-			/* past the core's caches: the GPU's poll then reads the lines
-			 * from memory, not by a probe of a dirty line in this core */
-			u32x4_h *w = (u32x4_h *)q;
-			__builtin_nontemporal_store(c0, w);
-			__builtin_nontemporal_store(c1, w + P);
-			__builtin_nontemporal_store(c2, w + 2 * P);
-			__builtin_nontemporal_store(c3, w + 3 * P);
-		} else {
-			q[0] = c0;
-			q[P] = c1;
-			q[2 * P] = c2;
-			q[3 * P] = c3;
-		}
+		/* (non-temporal stores, past the core's caches, measured no
+		 * different: profiles/r04_loop_nt_ab.jsonl) */
+		q[0] = c0;
+		q[P] = c1;
+		q[2 * P] = c2;
+		q[3 * P] = c3;
 	}
-	if (L->nt_submit)
-		__builtin_ia32_sfence(); /* the records before the slot word */
 	/* records past n keep older stamps; rewrite them now and then so that
 	 * none is ever 2^31 uses stale (loop_stamp's rule for the offsets) */
 	if (((t - 1) / L->lp.nslots) % kLoopRefresh == kLoopRefresh - 1)

@@ -135,21 +135,20 @@ def test_gpu_fuzz_misaligned_offsets(g, orc, misalign, mode):
     assert (tr == tre).all() and (c == ce).all() and (st == se).all()
 
 
-@pytest.mark.parametrize("kernel", ["tile", "pair"])
 @pytest.mark.parametrize("tables", ["lds", "global"])
 @pytest.mark.parametrize("misalign", ["mbuf", "mixed", "lineend"])
 @pytest.mark.parametrize("mode", [0, 1, 2])
-def test_gpu_general_kernels_fuzz(g, orc, monkeypatch, misalign, mode, tables, kernel):
-    """Every GENERAL kernel on the misaligned-offset fuzz, each forced by its
-    knob: the lane-pair kernel (classify_pair_kernel, the default) and the
-    LDS-tile kernel (classify_kernel, GCL_TUNE_PAIR=0).  Window shifts of 0-12
-    bytes, frames that are not 4-B aligned (bytewise), headers cut at the
-    first line end, frames straddling frames_len, IHL > 5 ports and ARP
-    target IPs read from the frame, loopback hints, FDIR marks and the
-    transport pre-hash, in all three hash modes, an odd packet count, with
-    the tables in LDS and forced to global memory (GCL_TUNE_TABLES=1)."""
+def test_gpu_general_kernels_fuzz(g, orc, monkeypatch, misalign, mode, tables):
+    """The GENERAL kernel (classify_pair_kernel) on the misaligned-offset
+    fuzz: frames at every 16-B phase, frames that are not 4-B aligned
+    (bytewise), headers cut at a line end, frames straddling frames_len,
+    IHL > 5 ports and ARP target IPs read from the frame, loopback hints,
+    FDIR marks and the transport pre-hash, in all three hash modes, an odd
+    packet count, with the tables in LDS and forced to global memory
+    (GCL_TUNE_TABLES=1)."""
+    kernel = "pair"
     rng = np.random.default_rng(9300 + 10 * mode + {"mbuf": 0, "mixed": 1, "lineend": 2}[misalign]
-                                + 100 * (tables == "global") + 1000 * ["quad", "tile", "pair"].index(kernel))
+                                + 100 * (tables == "global") + 1000 * 2)
     rts = random_runtimes(rng, 1024, 300)
     n = 7001
     frames, flen, offs, olf, rss, fdir, hint = fuzz_batch(
@@ -157,8 +156,7 @@ def test_gpu_general_kernels_fuzz(g, orc, monkeypatch, misalign, mode, tables, k
     key = bytes(rng.integers(0, 256, size=40, dtype=np.uint8))
     t = orc.Tables(1024, mode, g.CFG_TRANS_HASH, 0x09, key)
     apply_runtimes(t, rts)
-    env = {"GCL_TUNE_PAIR": "0" if kernel == "tile" else "1",
-           **({"GCL_TUNE_TABLES": "1"} if tables == "global" else {})}
+    env = {"GCL_TUNE_TABLES": "1"} if tables == "global" else {}
     for kk, vv in env.items():
         monkeypatch.setenv(kk, vv)
     try:
@@ -307,15 +305,11 @@ def test_gpu_dense_verdict1(g, orc, wl, R, T):
     assert (c == ce).all() and (st == se).all()
 
 
-@pytest.mark.parametrize("wl,R,T,vb,store", [(0, 16, 8, 1, 2), (0, 16, 8, 1, 0), (0, 16, 8, 2, 2),
-                                              (1, 1024, 4, 2, 2), (1, 1024, 4, 2, 0)])
-def test_gpu_dense_vstage(g, orc, wl, R, T, vb, store, monkeypatch):
-    """GCL_TUNE_VSTAGE=1 (measured, off by default): full dense tiles' 1- and
-    2-B verdicts staged in LDS and stored by NT/4 lanes as whole lines, the
-    partial last tile stored per lane; write-through and plain stores; 256-
-    (udp64) and 512-lane (1024-runtime tcp1500) blocks."""
-    monkeypatch.setenv("GCL_TUNE_VSTAGE", "1")
-    monkeypatch.setenv("GCL_TUNE_NT_STORE", str(store))
+@pytest.mark.parametrize("wl,R,T,vb", [(0, 16, 8, 1), (0, 16, 8, 2), (1, 1024, 4, 2)])
+def test_gpu_dense_narrow_verdicts(g, orc, wl, R, T, vb):
+    """Dense tiles' 1- and 2-B verdicts (write-through byte and short
+    stores), the partial last tile included; 256- (udp64) and 512-lane
+    (1024-runtime tcp1500) blocks."""
     stride = {0: 64, 1: 1536}[wl]
     n = 40000 + 77
     df = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
@@ -335,7 +329,7 @@ def test_gpu_dense_vstage(g, orc, wl, R, T, vb, store, monkeypatch):
     v, c, st = gpu_run(g, clf, frames, n, stride)
     ve, ce, se = t.classify(frames, n, stride)
     w = to_verdict1(ve, [T] * R, tb) if vb == 1 else to_verdict2(ve, [T] * R, tb)
-    assert_same(v, w, f"vstage wl={wl} vb={vb} store={store}")
+    assert_same(v, w, f"narrow verdicts wl={wl} vb={vb}")
     assert (c == ce).all() and (st == se).all()
 
 
@@ -1039,28 +1033,24 @@ def test_gpu_tables_in_hbm_forced(g, orc, monkeypatch):
 LOOP_GEOMETRIES = [
     {},
     {"GCL_TUNE_GRID": "3"},
-    {"GCL_TUNE_GRID": "16", "GCL_TUNE_XCD_MAP": "1"},
-    {"GCL_TUNE_GRID": "24", "GCL_TUNE_XCD_MAP": "1", "GCL_TUNE_THREADS": "512"},
+    {"GCL_TUNE_GRID": "16"},
+    {"GCL_TUNE_GRID": "24", "GCL_TUNE_THREADS": "512"},
     {"GCL_TUNE_DEPTH": "1", "GCL_TUNE_GRID": "5"},
-    {"GCL_TUNE_SCHED": "1"},
+    {"GCL_TUNE_DEPTH": "1", "GCL_TUNE_THREADS": "512"},
     {"GCL_TUNE_THREADS": "1024", "GCL_TUNE_GRID": "7"},
-    {"GCL_TUNE_PAIR": "0"},
-    {"GCL_TUNE_PAIR": "0", "GCL_TUNE_GRID": "3"},
-    {"GCL_TUNE_PAIR": "0", "GCL_TUNE_THREADS": "512", "GCL_TUNE_GRID": "5"},
-    {"GCL_TUNE_PAIR": "2", "GCL_TUNE_GRID": "7"},
+    {"GCL_TUNE_THREADS": "512", "GCL_TUNE_GRID": "5"},
+    {"GCL_TUNE_BLOCKS_PER_CU": "1"},
 ]
 
 
 @pytest.mark.parametrize("geo", range(len(LOOP_GEOMETRIES)))
 @pytest.mark.parametrize("general", [False, True, "stride"])
 def test_gpu_loop_geometries(g, orc, monkeypatch, geo, general):
-    """The tile loop's edges under every launch shape the knobs allow: few
-    blocks walking many tiles (odd counts per block, so the second half of the
-    DEPTH-2 loop runs past the end as an empty tile), the per-XCD contiguous
-    walk (a block's walk ends inside the batch), DEPTH 1, the dynamic tile
-    queue, 512/1024-lane tiles, the lane-pair GENERAL kernel (the default)
-    and the LDS-tile one (GCL_TUNE_PAIR=0; dense slots keep the dense tile
-    kernel either way); dense slots, per-frame offsets with
+    """The loops' edges under every launch shape the geometry knobs allow:
+    few blocks walking many tiles (odd counts per block, so the second half
+    of the DEPTH-2 loop runs past the end as an empty tile), DEPTH 1,
+    512/1024-lane tiles, one block per CU, for the dense tile kernel and the
+    lane-pair GENERAL kernel; dense slots, per-frame offsets with
     ol_flags / hash.rss (NIC mode), and fixed slots with ol_flags / hash.rss
     and a buffer ending inside the last frame ("stride": the GENERAL path
     without offs[]), ragged n.  Same verdicts, counts, stats."""
@@ -1244,20 +1234,18 @@ def test_gpu_ip_hdr_supported_reference(g):
 
 
 @pytest.mark.parametrize("pattern", ["arp", "ipv4"])
-@pytest.mark.parametrize("kernel", ["pair", "tile"])
 @pytest.mark.parametrize("mode", [0, 1])
-def test_gpu_general_frames_at_the_end(g, orc, monkeypatch, kernel, mode, pattern):
+def test_gpu_general_frames_at_the_end(g, orc, mode, pattern):
     """Frames at every byte offset from 80 bytes before frames_len to 8
     past it, over a tail whose bytes repeat 08 06 (ARP) or 08 00 (IPv4), so
     every other offset parses as that Ethertype and its destination (the ARP
     target at bytes 38-41, daddr at 30-33) is a registered runtime -- until
     the bytes it needs run past frames_len and read 0 (the build's rule; the
     bytes behind frames_len hold 0xEE).  This walks the pair kernel from its
-    16-B loads of [8, 40) to bytewise reads, the ARP target from one dword
-    load to bytewise, and the other GENERAL kernels' windows and line cuts,
-    each against the oracle."""
-    rng = np.random.default_rng(4400 + mode + 10 * ["pair", "tile", "quad"].index(kernel)
-                                + 100 * (pattern == "ipv4"))
+    16-B loads of [8, 40) to bytewise reads and the ARP target from one
+    dword load to bytewise, each against the oracle."""
+    kernel = "pair"
+    rng = np.random.default_rng(4400 + mode + 100 * (pattern == "ipv4"))
     R = 16
     unit = b"\x08\x06" if pattern == "arp" else b"\x08\x00"
     word = int.from_bytes(unit * 2, "big")  # the IP the pattern reads as, host order
@@ -1274,14 +1262,7 @@ def test_gpu_general_frames_at_the_end(g, orc, monkeypatch, kernel, mode, patter
     t = orc.Tables(R, mode, 0, 0x09)
     for r, ip in enumerate(ips):
         assert t.runtime_set(r, ip, 4, 4, [0, 1, 2, 3]) == 0
-    env = {"pair": {"GCL_TUNE_PAIR": "1"}, "tile": {"GCL_TUNE_PAIR": "0"}}[kernel]
-    for kk, vv in env.items():
-        monkeypatch.setenv(kk, vv)
-    try:
-        clf = g.Classifier(0, R, mode, 0, 0x09)
-    finally:
-        for kk in env:
-            monkeypatch.delenv(kk)
+    clf = g.Classifier(0, R, mode, 0, 0x09)
     for r, ip in enumerate(ips):
         clf.runtime_set(r, ip, 4, 4, [0, 1, 2, 3])
     ve, ce, se = t.classify(frames, n, 0, offs=offs, olflags=olf, rss=rss, frames_len=flen)
@@ -1399,13 +1380,12 @@ def test_gpu_access_probe(g, vbytes):
     assert (got == want(offs)).all()
 
 
-@pytest.mark.parametrize("kernel", ["tile", "pair"])
-def test_gpu_offsets_at_the_top_of_u64(g, orc, monkeypatch, kernel):
+def test_gpu_offsets_at_the_top_of_u64(g, orc):
     """Offsets at and near 2^64 - 1 (the kernels' no-packet sentinel, ~0),
     2^63 and frames_len read as frames of zeros like any offset past the
-    buffer, in both GENERAL kernels; gcl_classify refuses frames_len == ~0."""
-    monkeypatch.setenv("GCL_TUNE_PAIR", "0" if kernel == "tile" else "1")
-    rng = np.random.default_rng(9500 + (kernel == "pair"))
+    buffer in the GENERAL kernel; gcl_classify refuses frames_len == ~0."""
+    kernel = "pair"
+    rng = np.random.default_rng(9501)
     rts = random_runtimes(rng, 16, 12)
     n = 3001
     frames, flen, offs, olf, rss, fdir, hint = fuzz_batch(rng, n, rts, 16, tail_runts=False)
