@@ -98,7 +98,30 @@ struct gcl_group {
 	bool diverged;       /* a table change reached some replicas only: every
 	                        later call fails with -EIO (the GPUs would steer
 	                        with different tables) */
+	bool failed;         /* an exchange's RCCL enqueue failed or timed out: the
+	                        communicators were aborted, and every later call
+	                        fails with -EIO (a collective may still hold the
+	                        snapshot slots; the communicators' state is unknown) */
 };
+
+/* a group that must refuse all work */
+static bool broken(const gcl_group *g)
+{
+	return g->diverged || g->failed;
+}
+
+/* Abort every communicator (RCCL's bounded teardown, for communicators in
+ * an unknown state) and mark the group failed. */
+static void fail_group(gcl_group *g)
+{
+	for (int i = 0; i < g->n; i++)
+		if (g->d[i].comm) {
+			(void)hipSetDevice(g->d[i].dev);
+			(void)ncclCommAbort(g->d[i].comm);
+			g->d[i].comm = nullptr;
+		}
+	g->failed = true;
+}
 
 static uint64_t mono_ms()
 {
@@ -234,11 +257,13 @@ extern "C" void gcl_group_close(struct gcl_group *g)
 	delete g;
 }
 
-extern "C" int gcl_group_open(int ndev, const int *devs, const struct gcl_cfg *cfg,
-                              const struct gcl_group_cfg *gcfg, struct gcl_group **out)
+extern "C" int gcl_group_open_v2(int ndev, const int *devs, const struct gcl_cfg *cfg,
+                                 const struct gcl_group_cfg *gcfg, struct gcl_group **out)
 {
 	if (!out || !devs || !cfg || ndev < 1 || ndev > GCL_GROUP_MAX_DEV)
 		return -EINVAL;
+	if (gcfg && gcfg->size != sizeof(struct gcl_group_cfg))
+		return -EINVAL; /* a struct of another layout */
 	*out = nullptr;
 	const uint64_t block = gcfg && gcfg->block ? gcfg->block : GCL_GROUP_BLOCK;
 	const uint32_t xchg = gcfg ? gcfg->exchange : GCL_XCHG_RCCL;
@@ -319,6 +344,30 @@ extern "C" int gcl_group_open(int ndev, const int *devs, const struct gcl_cfg *c
 	return 0;
 }
 
+/* The ABI-1 entry point (the 16-B struct gcl_group_cfg of rounds 1-3:
+ * block, exchange, nstreams): binaries built against that header keep it,
+ * with the default RCCL init bound; the current header maps gcl_group_open
+ * to gcl_group_open_v2. */
+struct gcl_group_cfg_v1 {
+	uint64_t block;
+	uint32_t exchange;
+	uint32_t nstreams;
+};
+
+#undef gcl_group_open
+extern "C" int gcl_group_open(int ndev, const int *devs, const struct gcl_cfg *cfg,
+                              const struct gcl_group_cfg_v1 *gcfg, struct gcl_group **out)
+{
+	struct gcl_group_cfg c = {};
+	c.size = sizeof(c);
+	if (gcfg) {
+		c.block = gcfg->block;
+		c.exchange = gcfg->exchange;
+		c.nstreams = gcfg->nstreams;
+	}
+	return gcl_group_open_v2(ndev, devs, cfg, &c, out);
+}
+
 extern "C" int gcl_group_size(const struct gcl_group *g) { return g ? g->n : -EINVAL; }
 
 extern "C" struct gcl_ctx *gcl_group_ctx(struct gcl_group *g, int i)
@@ -342,7 +391,7 @@ static int fan_out(struct gcl_group *g, F f)
 {
 	if (!g)
 		return -EINVAL;
-	if (g->diverged)
+	if (broken(g))
 		return -EIO;
 	const int r0 = f(g->d[0].ctx);
 	if (r0)
@@ -379,7 +428,7 @@ extern "C" int gcl_group_classify(struct gcl_group *g, const struct gcl_batch *s
 {
 	if (!g || !shards || !verdicts)
 		return -EINVAL;
-	if (g->diverged)
+	if (broken(g))
 		return -EIO;
 	for (int i = 0; i < g->n; i++) {
 		gcl_group::Dev &D = g->d[i];
@@ -468,7 +517,7 @@ extern "C" int gcl_group_classify_host(struct gcl_group *g, const struct gcl_bat
 	if (!g || !hb || !host_verdicts || !o || o->mode > GCL_E2E_ZEROCOPY ||
 	    o->nstreams > GCL_GROUP_MAX_STREAMS)
 		return -EINVAL;
-	if (g->diverged)
+	if (broken(g))
 		return -EIO;
 	if (hb->n == 0)
 		return 0;
@@ -589,10 +638,20 @@ extern "C" int gcl_group_classify_host(struct gcl_group *g, const struct gcl_bat
 	return he.bad() ? -EIO : sr;
 }
 
+/* test hook: GCL_GROUP_FAULT=exchange makes every RCCL exchange's enqueue
+ * fail as a timed-out one would (-ETIMEDOUT), to exercise fail_group */
+static bool fault_exchange()
+{
+	const char *e = getenv("GCL_GROUP_FAULT");
+	return e && !strcmp(e, "exchange");
+}
+
 extern "C" int gcl_group_exchange(struct gcl_group *g)
 {
 	if (!g)
 		return -EINVAL;
+	if (broken(g))
+		return -EIO;
 	const int b = (int)(g->seq % kSlots);
 	const size_t L = g->L, L8 = L * 8;
 	HipErr he;
@@ -624,14 +683,17 @@ extern "C" int gcl_group_exchange(struct gcl_group *g)
 		}
 		const ncclResult_t e = ncclGroupEnd();
 		ok = ok && (e == ncclSuccess || e == ncclInProgress);
-		if (!ok)
-			return -EIO;
 		/* non-blocking communicators: the enqueue itself may still be in
 		 * progress (the first all-gather connects the ring) */
-		if (e == ncclInProgress) {
-			const int w = comms_wait(g, mono_ms() + g->timeout_ms);
-			if (w)
-				return w;
+		int w = !ok ? -EIO : e == ncclInProgress ? comms_wait(g, mono_ms() + g->timeout_ms) : 0;
+		if (!w && fault_exchange())
+			w = -ETIMEDOUT;
+		if (w) {
+			/* the all-gather may still be enqueued on D.xs, reading and
+			 * writing slot b: abort the communicators and refuse all
+			 * further work rather than reuse the slot or the communicators */
+			fail_group(g);
+			return w;
 		}
 		for (int i = 0; i < g->n; i++) {
 			gcl_group::Dev &D = g->d[i];
@@ -670,6 +732,8 @@ extern "C" int gcl_group_read(struct gcl_group *g, uint64_t *node_counts, uint64
 {
 	if (!g)
 		return -EINVAL;
+	if (broken(g))
+		return -EIO;
 	if (g->last < 0)
 		return -ENODATA;
 	const int b = g->last;

@@ -1565,7 +1565,7 @@ __device__ __forceinline__ void rxloop64_writer(const LoopParams &L, Wave64 *wv,
 				 * {ticket, polls, hit lo, hi}
 				 * {ticket, hit -> packets in registers, hit -> posted, hit -> writer} */
 				const __amdgpu_buffer_rsrc_t srs =
-				        gcl::host_rsrc(L.slots + ((t - 1) % L.nslots) * L.slot_bytes, L.slot_bytes);
+				        gcl::host_rsrc(L.slots + ((t - 1) & (L.nslots - 1)) * (uint64_t)L.slot_bytes, L.slot_bytes);
 				const uint64_t hit = (uint64_t)st[1] << 32 | st[0];
 				const gcl::u32x4 a = {(uint32_t)t, st[2], st[6], st[7]};
 				const gcl::u32x4 b2 = {(uint32_t)t, st[3], st[0], st[1]};
@@ -1703,8 +1703,12 @@ __global__ void __launch_bounds__(64 * (NP + 1)) rxloop64_kernel(LoopParams L)
 			const uint64_t since = ctl_ld64(&ctl->since);
 			spec_end = since + L.spec_ticks + (kt != kc ? L.spec_ticks : 0);
 		}
-		const uint64_t t = L.t0 + blockIdx.x + 1 + kt * L.workers;
-		uint8_t *slot = L.slots + ((t - 1) % L.nslots) * L.slot_bytes;
+		/* the ticket and its slot, uniform: a slot address the compiler
+		 * thinks divergent puts every buffer load in a waterfall loop
+		 * (nslots is a power of two: a mask, not a 64-bit modulo) */
+		kt = lane0_u64(kt);
+		const uint64_t t = lane0_u64(L.t0 + blockIdx.x + 1 + kt * L.workers);
+		uint8_t *slot = L.slots + ((t - 1) & (L.nslots - 1)) * (uint64_t)L.slot_bytes;
 		LoopSlotHdr *h = (LoopSlotHdr *)slot;
 		const __amdgpu_buffer_rsrc_t srs = gcl::host_rsrc(slot, L.slot_bytes);
 		const uint64_t stamp = loop_stamp(t, L.nslots);
@@ -3124,6 +3128,8 @@ extern "C" int gcl_generate(const struct gcl_gen_params *p, uint8_t *frames, uin
 
 extern "C" const char *gcl_version(void) { return GCL_VERSION; }
 
+extern "C" int gcl_abi_version(void) { return GCL_ABI_VERSION; }
+
 /* Device memory for frame slabs and verdict arrays: plain hipMalloc on the
  * context's device, so large batches get the allocator's large-page path. */
 extern "C" int gcl_dev_alloc(int hip_device, size_t bytes, void **out)
@@ -3385,6 +3391,15 @@ extern "C" int gcl_host_unregister(void *p)
 	return hipHostUnregister(p) == hipSuccess ? 0 : -EINVAL;
 }
 
+/* Per-packet sub-arrays of a COPY chunk's side buffer, at multiples of this
+ * many bytes: ol_flags [0, C), hash.rss [C, 5C), hash.fdir.hi [5C, 9C),
+ * dst_hint [9C, 13C), offsets [13C, 21C).  A multiple of 16, so every
+ * sub-array is 16-B aligned whatever chunk the caller asks for. */
+static uint64_t side_stride(uint64_t chunk)
+{
+	return (chunk + 15) & ~15ull;
+}
+
 static int e2e_setup(gcl_ctx *c, int nstreams, uint64_t chunk)
 {
 	gcl_ctx::E2E &e = c->e2e;
@@ -3402,7 +3417,7 @@ static int e2e_setup(gcl_ctx *c, int nstreams, uint64_t chunk)
 	for (int i = 0; i < nstreams; i++) {
 		if (hipStreamCreateWithFlags(&e.st[i], hipStreamNonBlocking) != hipSuccess ||
 		    hipMalloc(&e.slab[i], chunk * kGatherRow) != hipSuccess ||
-		    hipMalloc(&e.side[i], chunk * 21) != hipSuccess ||
+		    hipMalloc(&e.side[i], side_stride(chunk) * 21) != hipSuccess ||
 		    hipMalloc(&e.verd[i], chunk * sizeof(struct gcl_verdict)) != hipSuccess)
 			return -ENOMEM;
 		e.nstreams = i + 1;
@@ -3492,12 +3507,13 @@ extern "C" int gcl_classify_host(struct gcl_ctx *c, const struct gcl_batch *hb,
 		 * 64-B slot stride is its own row (the next frame follows, as in
 		 * the host buffer) */
 		const uint64_t row = hb->offs || hb->stride >= kGatherRow ? kGatherRow : GCL_HDR_GRANULE;
+		const uint64_t C = side_stride(chunk);
 		for (uint64_t s = 0, ci = 0; s < hb->n && !ret; s += chunk, ci++) {
 			const int i = (int)(ci % nst);
 			const uint64_t m = hb->n - s < chunk ? hb->n - s : chunk;
 			hipStream_t st = e.st[i];
 			if (hb->offs) {
-				const uint64_t *so = doffs ? doffs + s : (const uint64_t *)(e.side[i] + 13 * chunk);
+				const uint64_t *so = doffs ? doffs + s : (const uint64_t *)(e.side[i] + 13 * C);
 				if (!doffs)
 					he(hipMemcpyAsync((void *)so, hb->offs + s, m * 8, hipMemcpyHostToDevice, st));
 				if (gcl_header_gather(dframes, hb->frames_len, so, m, e.slab[i], st))
@@ -3526,16 +3542,16 @@ extern "C" int gcl_classify_host(struct gcl_ctx *c, const struct gcl_batch *hb,
 				db.olflags = side;
 			}
 			if (hb->rss) {
-				he(hipMemcpyAsync(side + chunk, hb->rss + s, m * 4, hipMemcpyHostToDevice, st));
-				db.rss = (const uint32_t *)(side + chunk);
+				he(hipMemcpyAsync(side + C, hb->rss + s, m * 4, hipMemcpyHostToDevice, st));
+				db.rss = (const uint32_t *)(side + C);
 			}
 			if (hb->fdir_hi) {
-				he(hipMemcpyAsync(side + 5 * chunk, hb->fdir_hi + s, m * 4, hipMemcpyHostToDevice, st));
-				db.fdir_hi = (const uint32_t *)(side + 5 * chunk);
+				he(hipMemcpyAsync(side + 5 * C, hb->fdir_hi + s, m * 4, hipMemcpyHostToDevice, st));
+				db.fdir_hi = (const uint32_t *)(side + 5 * C);
 			}
 			if (hb->dst_hint) {
-				he(hipMemcpyAsync(side + 9 * chunk, hb->dst_hint + s, m * 4, hipMemcpyHostToDevice, st));
-				db.dst_hint = (const uint32_t *)(side + 9 * chunk);
+				he(hipMemcpyAsync(side + 9 * C, hb->dst_hint + s, m * 4, hipMemcpyHostToDevice, st));
+				db.dst_hint = (const uint32_t *)(side + 9 * C);
 			}
 			ret = gcl_classify(c, &db, e.verd[i], dcounts, dstats, st);
 			he(hipMemcpyAsync((uint8_t *)host_verdicts + s * vsize, e.verd[i], m * vsize,

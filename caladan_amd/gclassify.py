@@ -606,9 +606,14 @@ XCHG_RCCL, XCHG_HOST = 0, 1
 
 
 class GclGroupCfg(ctypes.Structure):
+    """struct gcl_group_cfg (GCL_GROUP_ABI 2): `size` is filled in here."""
     _fields_ = [("block", ctypes.c_uint64), ("exchange", ctypes.c_uint32),
                 ("nstreams", ctypes.c_uint32), ("init_timeout_ms", ctypes.c_uint32),
-                ("pad", ctypes.c_uint32)]
+                ("size", ctypes.c_uint32)]
+
+    def __init__(self, **kw):
+        kw.setdefault("size", ctypes.sizeof(GclGroupCfg))
+        super().__init__(**kw)
 
 
 _glib = None
@@ -625,8 +630,11 @@ def group_lib():
     gl = ctypes.CDLL(GROUP_LIB_PATH)
     vp, u16, u32, u64, i32 = ctypes.c_void_p, ctypes.c_uint16, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
     sig = {
+        "gcl_group_open_v2": (i32, [i32, ctypes.POINTER(i32), ctypes.POINTER(GclCfg),
+                                    ctypes.POINTER(GclGroupCfg), ctypes.POINTER(vp)]),
+        # the ABI-1 symbol (16-B struct gcl_group_cfg_v1), kept for old binaries
         "gcl_group_open": (i32, [i32, ctypes.POINTER(i32), ctypes.POINTER(GclCfg),
-                                 ctypes.POINTER(GclGroupCfg), ctypes.POINTER(vp)]),
+                                 vp, ctypes.POINTER(vp)]),
         "gcl_group_close": (None, [vp]),
         "gcl_group_size": (i32, [vp]),
         "gcl_group_ctx": (vp, [vp, i32]),
@@ -685,8 +693,8 @@ class Group:
         gc = GclGroupCfg(block=block, exchange=exchange, nstreams=nstreams,
                          init_timeout_ms=init_timeout_ms)
         self._g = ctypes.c_void_p()
-        _check(gl.gcl_group_open(self.n, devs, ctypes.byref(cfg), ctypes.byref(gc), ctypes.byref(self._g)),
-               "gcl_group_open")
+        _check(gl.gcl_group_open_v2(self.n, devs, ctypes.byref(cfg), ctypes.byref(gc), ctypes.byref(self._g)),
+               "gcl_group_open_v2")
 
     def close(self):
         if self._g:

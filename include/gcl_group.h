@@ -46,8 +46,15 @@ struct gcl_group_cfg {
 	uint32_t nstreams; /* work streams per GPU for gcl_group_classify_host, 1..4 (0 = 2) */
 	uint32_t init_timeout_ms; /* GCL_XCHG_RCCL: bound on communicator init, and on an
 	                             exchange's RCCL enqueue (0 = GCL_GROUP_INIT_TIMEOUT_MS) */
-	uint32_t pad;
+	uint32_t size;     /* sizeof(struct gcl_group_cfg): GCL_GROUP_CFG_INIT sets it;
+	                      gcl_group_open refuses another value (-EINVAL) */
 };
+/* ABI 2 (round 4) added init_timeout_ms and size.  Binaries built against
+ * the ABI-1 header (a 16-B struct) keep calling the exported symbol
+ * gcl_group_open, which reads only the ABI-1 fields; this header maps the
+ * name to gcl_group_open_v2, which reads the whole struct. */
+#define GCL_GROUP_ABI 2
+#define GCL_GROUP_CFG_INIT { 0, GCL_XCHG_RCCL, 0, 0, sizeof(struct gcl_group_cfg) }
 #define GCL_GROUP_INIT_TIMEOUT_MS 60000
 
 struct gcl_group;
@@ -60,10 +67,12 @@ struct gcl_group;
  * blocking = 0) and polled: a bootstrap that does not finish within
  * init_timeout_ms is aborted and gives -ETIMEDOUT instead of blocking the
  * caller.
+ * @gcfg->size must be sizeof(struct gcl_group_cfg) (GCL_GROUP_CFG_INIT).
  * Returns 0, -EINVAL, -ENODEV, -ENOMEM, -ETIMEDOUT, or -EIO when RCCL init fails.
  */
-int gcl_group_open(int ndev, const int *devs, const struct gcl_cfg *cfg,
-                   const struct gcl_group_cfg *gcfg, struct gcl_group **out);
+int gcl_group_open_v2(int ndev, const int *devs, const struct gcl_cfg *cfg,
+                      const struct gcl_group_cfg *gcfg, struct gcl_group **out);
+#define gcl_group_open gcl_group_open_v2
 void gcl_group_close(struct gcl_group *g);
 
 /* Number of GPUs (contexts), and context @i (NULL if out of range): the
@@ -126,6 +135,12 @@ int gcl_group_classify_host(struct gcl_group *g, const struct gcl_batch *hb,
  * totals since open or the last reset, and optionally the gathered
  * per-GPU vectors (u64[n][max_runtimes + GCL_NR_STATS]).  Any output may be
  * NULL.  -ENODATA before the first exchange.
+ * An exchange whose RCCL enqueue fails (-EIO) or does not complete within
+ * init_timeout_ms (-ETIMEDOUT) aborts every communicator (ncclCommAbort) and
+ * leaves the group failed: every later call except close returns -EIO (the
+ * all-gather may still hold the exchange's buffers, and the communicators
+ * are in an unknown state).  GCL_GROUP_FAULT=exchange in the environment
+ * makes every RCCL exchange fail that way (tests).
  */
 int gcl_group_exchange(struct gcl_group *g);
 int gcl_group_read(struct gcl_group *g, uint64_t *node_counts, uint64_t *node_stats,

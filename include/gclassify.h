@@ -165,7 +165,16 @@ enum gcl_action {
  * scheduler change earlier in the same batch is seen by the later packets.
  * DELIVER means the runtime had an active kthread in the classify snapshot,
  * WAKE that it had none; the post-pass re-checks either way.
+ *
+ * BREAKING in ABI 4 (round 4): before it, .thread held the kthread
+ * (flow_tbl[slot]) in the same layout.  A direct consumer of the verdicts
+ * that indexes kthread rings with .thread must check gcl_abi_version() >= 4
+ * and read flow_tbl[.thread] itself (or use the gcl_host_deliver* post-pass).
  */
+#define GCL_ABI_VERSION 5
+/* GCL_ABI_VERSION of the library actually loaded: 4 = verdict .thread is
+ * the flow-table slot; 5 = gcl_group_open_v2 and struct gcl_group_cfg.size */
+int gcl_abi_version(void);
 struct gcl_verdict {
 	uint32_t hash;    /* steering hash (hash.rss, or the computed flow hash) */
 	uint16_t uniqid;  /* proc->uniqid of the destination, GCL_NO_RUNTIME if none */
@@ -622,7 +631,10 @@ int gcl_rxloop_release(struct gcl_rxloop *loop, int64_t ticket);
  * header records already current: one PCIe round trip), @out[1] eligible
  * for that (<= 64 packets, in the speculative window) but an entry still
  * stale, so read after the word, @out[2] read after the word (the window
- * over, a longer burst, or inline granules).  Before gcl_rxloop_stop. */
+ * over, a longer burst, or inline granules).  Before gcl_rxloop_stop.
+ * The burst-of-64 kernel's writer wave posts these counters (and the lean
+ * count below) after the burst's verdict records, so both can lag the bursts
+ * a gcl_rxloop_wait has seen complete by up to a few microseconds: poll. */
 int gcl_rxloop_poll_stats(struct gcl_rxloop *loop, uint64_t out[3]);
 /* gcl_rxloop_lean_bursts - how many of the loop's bursts so far were
  * classified by the burst-of-64 kernel's lean path (every packet plain IPv4:

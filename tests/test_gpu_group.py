@@ -388,3 +388,38 @@ def test_gpu_group_rccl_init_bounded(g):
     c, s, _ = grp.read()
     assert int(c.sum()) + int(s[g.RX_UNHANDLED]) == n and int(s[g.RX_PULLED]) == n
     grp.close()
+
+
+def test_gpu_group_failed_exchange_is_sticky(g, monkeypatch):
+    """An exchange whose RCCL enqueue fails or times out (injected with
+    GCL_GROUP_FAULT=exchange) aborts the communicators and leaves the group
+    failed: the exchange returns -ETIMEDOUT, and every later classify,
+    exchange, read and table change returns -EIO instead of reusing the
+    exchange's buffers or the aborted communicators; close still works,
+    and a new group runs normally."""
+    grp = g.Group([0], R, g.HASH_JENKINS, init_timeout_ms=5000)
+    tables(grp)
+    n = 4096
+    fr = torch.zeros(n * 64, dtype=torch.uint8, device="cuda")
+    g.generate(g.WL_UDP64, n, 64, R, fr)
+    v = torch.zeros(n * 8, dtype=torch.uint8, device="cuda")
+    grp.classify([{"frames": fr, "n": n, "stride": 64}], [v])
+    monkeypatch.setenv("GCL_GROUP_FAULT", "exchange")
+    with pytest.raises(OSError) as e:
+        grp.exchange()
+    assert e.value.errno == 110  # ETIMEDOUT
+    monkeypatch.delenv("GCL_GROUP_FAULT")
+    for call in (lambda: grp.classify([{"frames": fr, "n": n, "stride": 64}], [v]),
+                 grp.exchange, grp.read,
+                 lambda: grp.runtime_set(0, g.runtime_ip(0), 8, 8, g.steer_flows(8, list(range(8))))):
+        with pytest.raises(OSError) as e:
+            call()
+        assert e.value.errno == 5, call  # EIO
+    grp.close()
+    grp = g.Group([0], R, g.HASH_JENKINS)
+    tables(grp)
+    grp.classify([{"frames": fr, "n": n, "stride": 64}], [v])
+    grp.exchange()
+    c, s, _ = grp.read()
+    assert int(s[g.RX_PULLED]) == n
+    grp.close()

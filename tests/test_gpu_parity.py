@@ -1440,6 +1440,15 @@ def test_gpu_copy_transport_fuzz(g, orc, misalign, mode):
                       frames_len=flen, mode=g.E2E_COPY, chunk=2048 + 5, nstreams=3, **side)
     assert_same(hv.numpy().view(g.VERDICT_DTYPE), ve, f"copy offsets {misalign} mode={mode}")
     assert (counts == ce).all() and (stats == se).all()
+    # offsets in pageable memory: copied into the chunk's side buffer beside
+    # the other arrays, whose sub-arrays stay 16-B aligned at an odd chunk
+    hv.zero_()
+    counts, stats = np.zeros(64, dtype=np.uint64), np.zeros(8, dtype=np.uint64)
+    clf.classify_host(hr, n, 0, verdicts=hv, counts=counts, stats=stats,
+                      offs=np.ascontiguousarray(offs.view(np.int64)), frames_len=flen, mode=g.E2E_COPY,
+                      chunk=1000 + 3, nstreams=2, **side)
+    assert_same(hv.numpy().view(g.VERDICT_DTYPE), ve, f"copy pageable offsets {misalign} mode={mode}")
+    assert (counts == ce).all() and (stats == se).all()
     if misalign is not None:
         return
     # fixed slots: the same buffer as n_slots x 128-B frames in slot order

@@ -32,6 +32,7 @@ def test_group_library_exports_every_declared_symbol(g):
 
 def test_group_cfg_layout(g):
     assert ctypes.sizeof(g.GclGroupCfg) == 24
+    assert g.GclGroupCfg().size == 24  # GCL_GROUP_CFG_INIT's size, filled in by the binding
 
 
 @pytest.mark.parametrize("block", [256, 4096, 64 << 10])
@@ -75,19 +76,41 @@ def test_group_open_refuses_bad_args(g):
     cfg = g.GclCfg(max_runtimes=16, hash_mode=1)
     out = ctypes.c_void_p()
     devs = (ctypes.c_int * 2)(0, 0)
-    assert gl.gcl_group_open(0, devs, ctypes.byref(cfg), None, ctypes.byref(out)) == -22
-    assert gl.gcl_group_open(17, devs, ctypes.byref(cfg), None, ctypes.byref(out)) == -22
+    for op in (gl.gcl_group_open_v2, gl.gcl_group_open):
+        assert op(0, devs, ctypes.byref(cfg), None, ctypes.byref(out)) == -22
+        assert op(17, devs, ctypes.byref(cfg), None, ctypes.byref(out)) == -22
     bad_block = g.GclGroupCfg(block=1000, exchange=0, nstreams=2)
-    assert gl.gcl_group_open(1, devs, ctypes.byref(cfg), ctypes.byref(bad_block), ctypes.byref(out)) == -22
+    assert gl.gcl_group_open_v2(1, devs, ctypes.byref(cfg), ctypes.byref(bad_block), ctypes.byref(out)) == -22
     bad_x = g.GclGroupCfg(block=0, exchange=2, nstreams=2)
-    assert gl.gcl_group_open(1, devs, ctypes.byref(cfg), ctypes.byref(bad_x), ctypes.byref(out)) == -22
+    assert gl.gcl_group_open_v2(1, devs, ctypes.byref(cfg), ctypes.byref(bad_x), ctypes.byref(out)) == -22
     bad_s = g.GclGroupCfg(block=0, exchange=0, nstreams=5)
-    assert gl.gcl_group_open(1, devs, ctypes.byref(cfg), ctypes.byref(bad_s), ctypes.byref(out)) == -22
+    assert gl.gcl_group_open_v2(1, devs, ctypes.byref(cfg), ctypes.byref(bad_s), ctypes.byref(out)) == -22
+    # a struct of another layout (no size, or an ABI-1 caller's) is refused
+    # by the v2 entry point before anything else is read
+    bad_size = g.GclGroupCfg(block=0, exchange=0, nstreams=2, size=16)
+    assert gl.gcl_group_open_v2(1, devs, ctypes.byref(cfg), ctypes.byref(bad_size), ctypes.byref(out)) == -22
     for f in ("gcl_group_exchange", "gcl_group_sync", "gcl_group_reset"):
         assert getattr(gl, f)(None) == -22
     assert gl.gcl_group_read(None, None, None, None) == -22
     assert gl.gcl_group_size(None) == -22
     assert gl.gcl_group_ctx(None, 0) is None
+
+
+def test_group_abi1_entry_point_reads_16_bytes(g):
+    """The exported ABI-1 symbol gcl_group_open takes the 16-B struct of
+    rounds 1-3 (block, exchange, nstreams) and validates it like the v2
+    entry point: a bad block or exchange in it is refused."""
+    gl = g.group_lib()
+    cfg = g.GclCfg(max_runtimes=16, hash_mode=1)
+    out = ctypes.c_void_p()
+    devs = (ctypes.c_int * 1)(0)
+
+    class V1(ctypes.Structure):
+        _fields_ = [("block", ctypes.c_uint64), ("exchange", ctypes.c_uint32),
+                    ("nstreams", ctypes.c_uint32)]
+    assert ctypes.sizeof(V1) == 16
+    assert gl.gcl_group_open(1, devs, ctypes.byref(cfg), ctypes.byref(V1(1000, 0, 2)), ctypes.byref(out)) == -22
+    assert gl.gcl_group_open(1, devs, ctypes.byref(cfg), ctypes.byref(V1(0, 2, 2)), ctypes.byref(out)) == -22
 
 
 def test_group_open_without_gpu_is_enodev(g):

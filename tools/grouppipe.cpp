@@ -76,7 +76,7 @@ int main(int argc, char **argv)
 	std::vector<int> devs(ndev);
 	for (int i = 0; i < ndev; i++)
 		devs[i] = i;
-	struct gcl_group_cfg gc = {};
+	struct gcl_group_cfg gc = GCL_GROUP_CFG_INIT;
 	gc.block = GCL_GROUP_BLOCK;
 	gc.exchange = GCL_XCHG_RCCL;
 	gc.nstreams = 2;
