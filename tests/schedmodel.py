@@ -6,15 +6,20 @@ its scheduler that delivery can reach, for checking the host post-pass
   rx_send_pkt_to_runtime  iokernel/rx.c:76-92
   rx_one_pkt's exits      iokernel/rx.c:171-232 (broadcast, ARP, fail_free)
   sched_steer_flows       iokernel/sched.c:122-147
-  sched_enable_kthread    iokernel/sched.c:149-172
+  sched_enable_kthread    iokernel/sched.c:149-172 (appended to active_threads,
+                          last_core = NCPU)
   sched_disable_kthread   iokernel/sched.c:174-192 (steers BEFORE the thread
-                          leaves active_threads, as written)
+                          leaves active_threads, as written; then the last
+                          active thread is swapped into its index, :185-186)
+  sched_pick_kthread      iokernel/sched.c:194-206 (a thread last parked on
+                          this core or its hyperthread sibling first, else
+                          list_tail of idle_threads)
   __sched_run             iokernel/sched.c:208-236: a core still waiting on its
                           last request disables the kthread pending on it --
                           a thread of ANY runtime -- so one runtime's wake can
                           re-steer another runtime, or take its last core,
                           in the middle of a burst
-  sched_run_on_core       iokernel/sched.c:247-268 (list_tail of idle_threads)
+  sched_run_on_core       iokernel/sched.c:247-268
 
 `Sched` is the scheduler state; the model reads it directly, and the C
 post-pass sees it through the struct gcl_host_proc mirrors that `sync`
@@ -43,12 +48,26 @@ def steer(tc, active):
     return flow
 
 
+NCPU = 256             # inc/base/limits.h: last_core of a running thread
+UINT16_MAX = 0xFFFF    # last_core of a thread never parked (sched.c:898) or
+                       # disabled by __sched_run's pending branch (:220)
+
+
+def sibling(core):
+    """sched_siblings[] of the model's host: hyperthread pairs (2k, 2k + 1)."""
+    return core ^ 1
+
+
 class Proc:
-    def __init__(self, uniqid, tc, active):
+    def __init__(self, uniqid, tc, active, parked=None):
         self.uniqid, self.tc = uniqid, tc
         self.active = list(active)                        # p->active_threads order
         self.idle = [t for t in range(tc) if t not in self.active]  # head = list_top
         self.flow = steer(tc, self.active) or [0] * tc
+        # p->last_core: NCPU while running; where an idle thread was parked
+        # (@parked: thread -> core), else UINT16_MAX
+        self.last_core = [NCPU if t in self.active else (parked or {}).get(t, UINT16_MAX)
+                          for t in range(tc)]
 
 
 class Sched:
@@ -58,8 +77,14 @@ class Sched:
     whatever runtime, is disabled."""
 
     def __init__(self, runtimes, ncores, rng):
-        self.procs = {r["uniqid"]: Proc(r["uniqid"], r["thread_count"], r["active_idx"])
-                      for r in runtimes}
+        # idle kthreads parked earlier on cores of this host (sched_yield /
+        # detach paths, sched_disable_kthread(th, core)), so that
+        # sched_pick_kthread's last_core preference is exercised
+        self.procs = {}
+        for r in runtimes:
+            idle = [t for t in range(r["thread_count"]) if t not in r["active_idx"]]
+            parked = {t: int(rng.integers(0, ncores)) for t in idle if rng.random() < 0.5}
+            self.procs[r["uniqid"]] = Proc(r["uniqid"], r["thread_count"], r["active_idx"], parked)
         running = [(u, th) for u, p in self.procs.items() for th in p.active]
         rng.shuffle(running)
         self.pending = [running[i] if i < len(running) else None for i in range(ncores)]
@@ -67,14 +92,26 @@ class Sched:
         self.events = []
 
     def enable(self, p, th):
+        p.last_core[th] = NCPU                     # sched.c:157
         p.idle.remove(th)
-        p.active.append(th)
+        p.active.append(th)                        # at_idx = active_thread_count++
         p.flow = steer(p.tc, p.active) or p.flow
 
-    def disable(self, p, th):
-        p.flow = steer(p.tc, p.active) or p.flow  # before the removal, sched.c:182-186
-        p.active.remove(th)
-        p.idle.insert(0, th)                      # list_add: new head
+    def disable(self, p, th, last_core=UINT16_MAX):
+        p.last_core[th] = last_core                # sched.c:180
+        p.idle.insert(0, th)                       # list_add: new head
+        p.flow = steer(p.tc, p.active) or p.flow   # before the removal, sched.c:182-183
+        i = p.active.index(th)                     # at_idx
+        p.active[i] = p.active[-1]                 # sched.c:185-186: the last active
+        p.active.pop()                             # thread moves into the hole
+
+    @staticmethod
+    def pick(p, core):
+        """sched_pick_kthread (sched.c:194-206)."""
+        for i in range(p.tc):
+            if p.last_core[i] == core or p.last_core[i] == sibling(core):
+                return i
+        return p.idle[-1]                          # list_tail(&p->idle_threads)
 
     def add_core(self, u):
         """sched_add_core -> notify_core_needed -> sched_run_on_core(p, core)"""
@@ -84,13 +121,13 @@ class Sched:
             return  # sched_run_on_core: list_empty(&p->idle_threads) -> -EINVAL
         core = self.rr % len(self.pending)
         self.rr += 1
-        th = p.idle[-1]                           # list_tail(&p->idle_threads)
+        th = self.pick(p, core)
         self.enable(p, th)
         prev = self.pending[core]
         if prev is not None and prev != (u, th):
             q = self.procs[prev[0]]
             if prev[1] in q.active:
-                self.disable(q, prev[1])
+                self.disable(q, prev[1], UINT16_MAX)  # __sched_run, sched.c:218-221
                 self.events.append(("disable", prev[0], prev[1], len(q.active)))
         self.pending[core] = (u, th)
 
