@@ -105,6 +105,9 @@ double orc_bench(const struct orc_tables *t, const struct gcl_batch *b,
  * loads (no bounds test: every frame's first 54 bytes must be in range). */
 #define ORC_BENCH_LRPC   0x1
 #define ORC_BENCH_DIRECT 0x2
+/* the ORC_BENCH_LRPC loop (command, flow_tbl[slot]) without the ring write:
+ * isolates lrpc_send's own cost from the loop's shape */
+#define ORC_BENCH_NOSEND 0x4
 double orc_bench_ex(const struct orc_tables *t, const struct gcl_batch *b,
                     int threads, int passes, unsigned int flags);
 /* orc_bench_ex with thread i pinned to CPU @cpus[i] (a -1 entry, or a NULL

@@ -297,14 +297,14 @@ class Tables:
         return v, counts, stats
 
     def bench(self, frames, n, stride, threads=1, passes=1, lrpc=False, offs=None, olflags=None,
-              rss=None, fdir_hi=None, pkt_len=None, direct=False, cpus=None):
+              rss=None, fdir_hi=None, pkt_len=None, direct=False, cpus=None, nosend=False):
         """Wall seconds of `passes` classifications on `threads` threads
         (contiguous shards); direct=True times rx.c's direct-load form;
         `cpus`: thread i pinned to CPU cpus[i]."""
         if direct and n and (n - 1) * stride + 54 > frames.nbytes and offs is None:
             raise ValueError("direct bench: a frame's header runs past the buffer")
         b = self._batch(frames, n, stride, offs, olflags, rss, fdir_hi, pkt_len, None)
-        flags = (1 if lrpc else 0) | (2 if direct else 0)
+        flags = (1 if lrpc else 0) | (2 if direct else 0) | (4 if nosend else 0)
         if cpus is None:
             return self._lib.orc_bench_ex(self.h, ctypes.byref(b), threads, passes, flags)
         c = np.full(max(threads, 1), -1, dtype=np.int32)

@@ -32,3 +32,7 @@ for r in rows:
 PY
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread --deselect tests/test_gpu_rxloop.py --deselect tests/test_gpu_group.py > gpurun_out/r05c_gputests.log 2>&1 || { tail -30 gpurun_out/r05c_gputests.log; exit 1; }
 tail -2 gpurun_out/r05c_gputests.log
+timeout -k 10 300 tools/wdefer > gpurun_out/r05c_wdefer.jsonl 2> gpurun_out/r05c_wdefer.err || { cat gpurun_out/r05c_wdefer.err; exit 1; }
+cat gpurun_out/r05c_wdefer.jsonl
+timeout -k 10 600 python tools/cpu_forms.py 5 > gpurun_out/r05c_cpu_forms.jsonl 2> gpurun_out/r05c_cpu_forms.err || { tail -5 gpurun_out/r05c_cpu_forms.err; exit 1; }
+cat gpurun_out/r05c_cpu_forms.jsonl
