@@ -1469,7 +1469,7 @@ struct Ctl64 {
 	uint64_t state;     /* lowest unclaimed ticket index << 1 | (index + 1 claimed) */
 	uint64_t issue[2];  /* each wave's last poll issue (s_memrealtime) */
 	uint64_t target[2]; /* the ticket index each wave's poll is for */
-	uint64_t since;     /* when the lowest unclaimed index last moved (spec window) */
+	uint64_t since;     /* when the last burst was posted (the spec window's start) */
 	uint32_t exited;    /* classifying waves that have left */
 	uint32_t queued;    /* the last claim came with its ticket's first poll */
 	uint32_t seq[2];    /* image sequence held by LDS table copy i (0xFF: none) */
@@ -1614,9 +1614,6 @@ __device__ __forceinline__ bool loop64_claim(Ctl64 *ctl, uint64_t k, int lane)
 				break; /* claimed already */
 			if (__hip_atomic_compare_exchange_strong(&ctl->state, &s, nx, __ATOMIC_RELAXED,
 			                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
-				if (k == kc) /* the lowest unclaimed index moved: a new spec window */
-					__hip_atomic_store(&ctl->since, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
-					                   __HIP_MEMORY_SCOPE_WORKGROUP);
 				ok = 1;
 				break;
 			}
@@ -1714,7 +1711,13 @@ __global__ void __launch_bounds__(64 * (NP + 1)) rxloop64_kernel(LoopParams L)
 		const uint64_t stamp = loop_stamp(t, L.nslots);
 		const uint32_t rstamp = loop_rec_stamp(t, L.nslots);
 		/* the poll: the slot word, and for the first L.spec_ticks of a wait
-		 * each lane's stamped offset or header record */
+		 * each lane's stamped offset or header record.  The word goes out
+		 * first: the host writes the records before the word, so records
+		 * read after a word that shows the burst are current unless the
+		 * fabric reorders the two (the other order made nearly every lone
+		 * burst's records stale).  Every lane loads the word and the stop
+		 * flag (one address: one request), so no divergent branch lets the
+		 * compiler consume the records before the word is even issued. */
 		const uint64_t t_issue = __builtin_amdgcn_s_memrealtime();
 		if (NP > 1 && lane == 0) {
 			__hip_atomic_store(&ctl->issue[w], t_issue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1722,6 +1725,8 @@ __global__ void __launch_bounds__(64 * (NP + 1)) rxloop64_kernel(LoopParams L)
 		}
 		npoll++;
 		const bool sp = spec && t_issue < spec_end;
+		const uint64_t wv0 = gcl::ld_sys64(&h->word);
+		const uint32_t sv0 = (kk & 7) == 7 ? gcl::ld_sys32(L.stop) : 0u; /* a stop waits <= 8 polls */
 		const uint64_t ev = sp && !rec ? gcl::ld_sys64(slot + L.off_offs + 8 * lane) : 0;
 		uint4 q[4] = {};
 		if (sp && rec) {
@@ -1732,15 +1737,8 @@ __global__ void __launch_bounds__(64 * (NP + 1)) rxloop64_kernel(LoopParams L)
 				q[j] = make_uint4(v[0], v[1], v[2], v[3]);
 			}
 		}
-		uint64_t wv0 = 0;
-		uint32_t sv = 0;
-		if (lane == 0) {
-			wv0 = gcl::ld_sys64(&h->word);
-			if ((kk & 7) == 7) /* a stop waits for up to 8 polls */
-				sv = gcl::ld_sys32(L.stop);
-		}
 		const uint64_t w_word = lane0_u64(wv0);
-		sv = lane0_u32(sv);
+		const uint32_t sv = lane0_u32(sv0);
 		const bool found = (w_word >> 24) == (t & ((1ull << 40) - 1));
 		if (NP > 1) {
 			const uint32_t d = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_issue);
@@ -1944,6 +1942,9 @@ __global__ void __launch_bounds__(64 * (NP + 1)) rxloop64_kernel(LoopParams L)
 		if (lane == 0)
 			__hip_atomic_store(&m.flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 		mb ^= 1;
+		if (NP > 1 && lane == 0) /* the spec window runs from the last burst's end */
+			__hip_atomic_store(&ctl->since, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+			                   __HIP_MEMORY_SCOPE_WORKGROUP);
 		/* the mailbox the next burst will be posted to, freed by the writer
 		 * long before: waited for here, not after the next hit */
 		while (__hip_atomic_load(&me.mbox[mb].flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
