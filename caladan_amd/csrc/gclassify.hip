@@ -101,6 +101,8 @@ struct KParams {
 	uint32_t default_flags;
 	uint2 *trans;    /* struct gcl_trans[n] or NULL */
 	uint32_t off_seed, off_crc;
+	uint32_t vcap;   /* classify_pair_kernel DENSE: tiles of verdicts its LDS buffer holds
+	                    (0: every verdict stored at once) */
 };
 
 /* ------------------------------------------------------------------------
@@ -444,7 +446,7 @@ __device__ __forceinline__ uint64_t classify_core(const KParams &k, const HdrWor
 	}
 	if (!HIST)
 		hist[tid] = (uint32_t)p;
-	if (VF != 2 && k.trans) {
+	if (VF == 0 && k.trans) { /* VERDICT1/2 contexts never have the pre-hash */
 		/* trans_lookup's hashes with runtime p's trans_seed
 		 * (transport.c:29-42, :366-375), for the packets net_rx_one passes
 		 * to net_rx_trans (core.c:203-209, :281-300) */
@@ -463,7 +465,7 @@ __device__ __forceinline__ uint64_t classify_core(const KParams &k, const HdrWor
 		k.trans[idx] = tr;
 	}
 	const uint32_t vlo = uniq | thr << 16 | action << 24;
-	if (VF == 0 && (k.cflags & GCL_CFG_VERDICT1)) {
+	if (VF == 1 || (VF == 0 && (k.cflags & GCL_CFG_VERDICT1))) {
 		/* q = uniqid << thread_bits | slot; no WAKE mark (gclassify.h) */
 		const uint32_t a = action & GCL_ACT_MASK;
 		const uint32_t q = uniq << (k.cflags >> 24) | thr;
@@ -570,13 +572,15 @@ __device__ __forceinline__ void store_wt(T *p, T v)
 	__hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-/* put_verdict with the format known at compile time (VF 2: the 2-byte
- * queue verdict), else read from k.cflags */
+/* put_verdict with the format known at compile time (VF 1 / 2: the 1- or
+ * 2-byte queue verdict), else read from k.cflags */
 template <int VF>
 __device__ __forceinline__ void put_verdict_vf(const KParams &k, uint64_t idx, uint64_t w)
 {
 	if (VF == 2)
 		store_wt((uint16_t *)k.verdicts + idx, (uint16_t)w);
+	else if (VF == 1)
+		store_wt((uint8_t *)k.verdicts + idx, (uint8_t)w);
 	else
 		put_verdict(k, idx, w);
 }
@@ -780,15 +784,16 @@ typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 
 /* load J of this lane: half (lane & 1) of the pair's packet J, whose
  * pair_src lane J of the pair holds in @my (quad_perm broadcast) */
-template <int J>
+template <int J, bool NTL = false>
 __device__ __forceinline__ uint4 pair_load(const KParams &k, uint64_t my)
 {
 	constexpr int B = J ? 0xF5 : 0xA0; /* quad_perm [1,1,3,3] : [0,0,2,2] */
 	const uint32_t lo = mdpp<B>((uint32_t)my), hi = mdpp<B>((uint32_t)(my >> 32));
 	const uint64_t s = (uint64_t)hi << 32 | lo;
 	const uint8_t *a = (hi >> 31) ? k.tables : k.frames + s + 16 * (threadIdx.x & 1);
-	/* plain loads: the frames stay in L2 for the next use of the same mbuf */
-	const u32x4a4 v = *(const u32x4a4 *)a;
+	/* plain loads: the frames stay in L2 for the next use of the same mbuf;
+	 * NTL (dense slots, every frame read once): the streaming hint */
+	const u32x4a4 v = NTL ? __builtin_nontemporal_load((const u32x4a4 *)a) : *(const u32x4a4 *)a;
 	return make_uint4(v.x, v.y, v.z, v.w);
 }
 
@@ -804,10 +809,20 @@ __device__ __forceinline__ void pair_exchange(uint4 r[2])
 	r[1] = sel4(odd, r[1], y);
 }
 
-template <int MODE, bool TLDS, int NT, int VF>
+/*
+ * DENSE (fixed-stride slots, no per-packet arrays, every granule inside
+ * frames_len; VF 1 or 2): no offset or side-array loads, and -- with
+ * k.vcap -- the verdicts of the block's tiles kept in LDS and written
+ * after its last tile (or whenever the buffer holds k.vcap tiles), 16 B per
+ * lane.  Interleaved with the header reads, the 1-B verdict stream cost the
+ * udp64 read stream 28 us of 331; written after the reads it costs ~14
+ * (tools/wdefer.hip, profiles/r05_wdefer.jsonl).  NTL: streaming loads.
+ */
+template <int MODE, bool TLDS, int NT, int VF, bool DENSE = false, bool NTL = false>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4)))
 classify_pair_kernel(KParams k)
 {
+	static_assert(!DENSE || VF == 1 || VF == 2, "DENSE keeps 1- or 2-B verdicts in LDS");
 	extern __shared__ uint4 smem[];
 	uint32_t *hist = (uint32_t *)smem;
 	uint8_t *lds_tab = (uint8_t *)(hist + ((k.max_rt + 3) & ~3u));
@@ -835,20 +850,52 @@ classify_pair_kernel(KParams k)
 	const uint64_t *offs_src = k.offs ? k.offs : (const uint64_t *)k.tables;
 	auto ok = [&](uint64_t tt) { return tt < k.ntiles && tt * NT + tid < k.n; };
 	auto ld_off = [&](uint64_t tt) -> uint64_t {
+		if (DENSE)
+			return 0;
 		return user_off(k, offs_src[k.offs && ok(tt) ? tt * NT + tid : 0]);
 	};
 	auto src_of = [&](uint64_t tt, uint64_t raw) -> uint64_t {
+		if (DENSE)
+			return !ok(tt) ? kNoOff : (tt * NT + tid) * k.stride + 8;
 		return pair_src(k, !ok(tt) ? kNoOff : k.offs ? raw : (tt * NT + tid) * k.stride);
 	};
 	auto pref = [&](uint64_t tt, uint32_t pr[2]) {
+		if (DENSE)
+			return;
 		const uint64_t i = ok(tt) ? tt * NT + tid : 0;
 		pr[0] = *(k.olflags ? k.olflags + i : side_dummy<uint8_t>(k, i));
 		if (MODE == GCL_HASH_NIC)
 			pr[1] = *(k.rss ? k.rss + i : side_dummy<uint32_t>(k, i));
 	};
 	auto issue = [&](uint64_t my, uint4 r[2]) {
-		r[0] = pair_load<0>(k, my);
-		r[1] = pair_load<1>(k, my);
+		r[0] = pair_load<0, NTL>(k, my);
+		r[1] = pair_load<1, NTL>(k, my);
+	};
+	/* DENSE: the LDS verdict buffer, k.vcap tiles of NT * VB bytes */
+	constexpr uint32_t VB = VF == 1 ? 1 : 2;
+	uint8_t *vbuf = lds_tab + k.tables_lds_bytes;
+	const bool defer = DENSE && k.vcap != 0;
+	uint32_t kl = 0; /* this block's tiles classified so far (uniform) */
+	/* the block's local tiles [k0, k1) from the buffer to their places,
+	 * 16 B per lane, write-through like the per-packet stores; the batch's
+	 * last tile up to n only */
+	auto flush = [&](uint32_t k0, uint32_t k1) {
+		constexpr uint32_t C = NT * VB / 16; /* chunks per tile */
+		const uint64_t nb = k.n * VB;
+		for (uint32_t i = tid; i < (k1 - k0) * C; i += NT) {
+			const uint32_t kk = k0 + i / C, c = i % C;
+			const uint64_t o = ((uint64_t)blockIdx.x + (uint64_t)kk * step) * NT * VB + 16 * c;
+			const uint8_t *src = vbuf + (kk % k.vcap) * NT * VB + 16 * c;
+			uint8_t *dst = (uint8_t *)k.verdicts + o;
+			if (o + 16 <= nb) {
+				const uint4 v = *(const uint4 *)src;
+				store_wt((uint64_t *)dst, (uint64_t)v.x | (uint64_t)v.y << 32);
+				store_wt((uint64_t *)(dst + 8), (uint64_t)v.z | (uint64_t)v.w << 32);
+			} else {
+				for (uint32_t b = 0; o + b < nb && b < 16; b++)
+					store_wt(dst + b, src[b]);
+			}
+		}
 	};
 	/* the landed halves -> this lane's header dwords (frame bytes 12-39;
 	 * d10, bytes 40-43, is not fetched: avail 40 sends ARP to the frame) */
@@ -867,8 +914,27 @@ classify_pair_kernel(KParams k)
 			const uint64_t i = tt * NT + tid;
 			/* this packet's frame offset, for the ARP target's extra read */
 			const uint64_t foff = (my >> 63) ? (my & ~kPairBytewise) : my - 8;
-			put_verdict_vf<VF>(k, i, classify_core<MODE, true, false, true, VF>(
-			                                 k, h, nullptr, tid, i, tb, hist, cnt, 0, 40, pr, foff));
+			const uint64_t w = classify_core<MODE, true, false, true, VF>(k, h, nullptr, tid, i, tb, hist,
+			                                                               cnt, 0, 40, pr, foff);
+			if (defer) {
+				uint8_t *d = vbuf + ((kl % k.vcap) * NT + tid) * VB;
+				if (VB == 1)
+					*d = (uint8_t)w;
+				else
+					*(uint16_t *)d = (uint16_t)w;
+			} else {
+				put_verdict_vf<VF>(k, i, w);
+			}
+		}
+	};
+	/* after tile tt: count it, and flush a full buffer */
+	auto tile_done = [&](uint64_t tt) {
+		if (!defer || tt >= k.ntiles)
+			return;
+		if (++kl % k.vcap == 0) {
+			__syncthreads();
+			flush(kl - k.vcap, kl);
+			__syncthreads(); /* the buffer is free again */
 		}
 	};
 
@@ -893,6 +959,7 @@ classify_pair_kernel(KParams k)
 		sa = src_of(t + 2 * step, oa);
 		issue(sa, ra);
 		classify(t, h, pra, my);
+		tile_done(t);
 		pref(t + 2 * step, pra);
 		oa = ld_off(t + 4 * step);
 		t += step;
@@ -903,11 +970,14 @@ classify_pair_kernel(KParams k)
 		sb = src_of(t + 2 * step, ob);
 		issue(sb, rb);
 		classify(t, h, prb, my);
+		tile_done(t);
 		pref(t + 2 * step, prb);
 		ob = ld_off(t + 4 * step);
 		t += step;
 	}
-	__syncthreads(); /* every wave's histogram adds are in */
+	__syncthreads(); /* every wave's histogram adds (and buffered verdicts) are in */
+	if (defer && kl % k.vcap)
+		flush(kl - kl % k.vcap, kl);
 	flush_counters<NT>(k, hist, cnt);
 }
 
@@ -959,6 +1029,8 @@ constexpr uint64_t kLoopRefresh = 256;
 /* s_memrealtime ticks (100 MHz) a wait polls the offsets with the word: a
  * burst that arrives later costs the offsets' round trip after the word */
 constexpr uint64_t kLoopSpecTicks = 400;
+/* GCL_TUNE_DENSE default (Geometry::dense) */
+constexpr int kDefaultDense = 0;
 /* GCL_TUNE_LOOP_LEAN default: bursts whose every packet is plain IPv4 (IHL 5,
  * no FDIR mark, no hint) classified by classify_lean */
 constexpr uint32_t kDefaultLoopLean = 1;
@@ -2304,6 +2376,7 @@ struct gcl_ctx {
 	int tune_threads; /* GCL_TUNE_THREADS: 256, 512 or 1024 lanes per block */
 	int tune_grid;    /* GCL_TUNE_GRID: blocks per launch (0: the persistent grid) */
 	int tune_bpc;     /* GCL_TUNE_BLOCKS_PER_CU: cap on blocks per CU (0: none) */
+	int tune_dense;   /* GCL_TUNE_DENSE: Geometry::dense for eligible batches (A/B) */
 };
 
 extern "C" {
@@ -2377,6 +2450,10 @@ extern "C" int gcl_open(int hip_device, const struct gcl_cfg *cfg, struct gcl_ct
 		c->tune_grid = e ? atoi(e) : 0;
 		e = getenv("GCL_TUNE_BLOCKS_PER_CU");
 		c->tune_bpc = e ? atoi(e) : 0;
+		e = getenv("GCL_TUNE_DENSE");
+		c->tune_dense = e ? atoi(e) : kDefaultDense;
+		if (c->tune_dense < 0 || c->tune_dense > 3)
+			c->tune_dense = 0;
 	}
 	c->dimg[0] = c->dimg[1] = nullptr;
 	for (int i = 0; i < 2; i++) {
@@ -2686,6 +2763,9 @@ struct Geometry {
 	int bpc_cap;  /* blocks per CU */
 	int grid;     /* blocks per launch when > 0 (GCL_TUNE_GRID) */
 	bool pair;    /* classify_pair_kernel (GENERAL batches): [8, 40) per packet by lane pairs */
+	int dense;    /* dense slots with 1-/2-B verdicts on classify_pair_kernel<DENSE>:
+	                 0 no (classify_kernel), 1 verdicts deferred in LDS + streaming loads,
+	                 2 deferred + plain loads, 3 not deferred + streaming loads */
 };
 
 template <int MODE, int DEPTH, int NT>
@@ -2713,10 +2793,48 @@ static hipError_t launch_pair(const KParams &k, bool tlds, uint32_t lds, int num
 	return launch_fn(fn, NT, k, lds, num_cus, geo.bpc_cap, geo.grid, s);
 }
 
+/* Dense slots with 1-/2-B verdicts on classify_pair_kernel<DENSE>: the
+ * block's LDS is all it can have at geo.bpc_cap blocks per CU, and what the
+ * tables and histogram leave of it holds k.vcap tiles of verdicts. */
+template <int MODE, int NT>
+static hipError_t launch_dense(KParams k, bool tlds, uint32_t base_lds, int num_cus, const Geometry &geo,
+                               hipStream_t s)
+{
+	const uint32_t vb = (k.cflags & GCL_CFG_VERDICT1) ? 1 : 2;
+	const bool defer = geo.dense != 3, ntl = geo.dense != 2;
+	uint32_t lds = base_lds;
+	k.vcap = 0;
+	if (defer) {
+		const uint32_t per_cu = 160 * 1024 / (uint32_t)std::max(geo.bpc_cap, 1);
+		const uint64_t ntiles = (k.n + NT - 1) / NT;
+		const uint32_t want = (uint32_t)std::min<uint64_t>(
+		        (ntiles + (uint64_t)num_cus * geo.bpc_cap - 1) / ((uint64_t)num_cus * geo.bpc_cap), 1u << 20);
+		const uint32_t room = per_cu > base_lds ? (per_cu - base_lds) / (NT * vb) : 0;
+		k.vcap = std::max(1u, std::min(want, room));
+		lds = base_lds + k.vcap * NT * vb;
+	}
+	ClassifyFn fn;
+	if (vb == 1)
+		fn = tlds ? (ntl ? classify_pair_kernel<MODE, true, NT, 1, true, true> : classify_pair_kernel<MODE, true, NT, 1, true, false>)
+		          : (ntl ? classify_pair_kernel<MODE, false, NT, 1, true, true> : classify_pair_kernel<MODE, false, NT, 1, true, false>);
+	else
+		fn = tlds ? (ntl ? classify_pair_kernel<MODE, true, NT, 2, true, true> : classify_pair_kernel<MODE, true, NT, 2, true, false>)
+		          : (ntl ? classify_pair_kernel<MODE, false, NT, 2, true, true> : classify_pair_kernel<MODE, false, NT, 2, true, false>);
+	return launch_fn(fn, NT, k, lds, num_cus, geo.bpc_cap, geo.grid, s);
+}
+
 template <int MODE>
 static hipError_t launch_mode(const KParams &k, bool tlds, const Geometry &geo,
                               uint32_t tab_lds, uint32_t hist_bytes, int num_cus, hipStream_t s)
 {
+	if (geo.dense) {
+		const uint32_t lds = hist_bytes + tab_lds;
+		if (geo.threads == 1024)
+			return launch_dense<MODE, 1024>(k, tlds, lds, num_cus, geo, s);
+		if (geo.threads == 512)
+			return launch_dense<MODE, 512>(k, tlds, lds, num_cus, geo, s);
+		return launch_dense<MODE, 256>(k, tlds, lds, num_cus, geo, s);
+	}
 	if (geo.pair) {
 		const uint32_t lds = hist_bytes + tab_lds;
 		if (geo.threads == 1024)
@@ -2749,7 +2867,7 @@ static hipError_t launch_mode(const KParams &k, bool tlds, const Geometry &geo,
  * waves than that only add contention (udp64: 446 us at 8 x 256).
  */
 static Geometry choose_geometry(const gcl_ctx *c, uint32_t tab_lds, uint32_t hist_bytes,
-                                bool general)
+                                bool general, bool dense_ok)
 {
 	const uint32_t lds_cu = 160 * 1024, lanes_cu = 1024;
 	Geometry g;
@@ -2761,8 +2879,9 @@ static Geometry choose_geometry(const gcl_ctx *c, uint32_t tab_lds, uint32_t his
 	 * in round 5: the pair kernel beat both on every row, working set 96
 	 * vs 109-111 us, random pool 181 vs 189, profiles/r03_ws_ab.jsonl.) */
 	g.pair = general;
+	g.dense = dense_ok ? c->tune_dense : 0;
 	auto per_block = [&](uint32_t nt) -> uint32_t {
-		if (g.pair)
+		if (g.pair || g.dense)
 			return hist_bytes + tab_lds;
 		return nt * 64 + hist_bytes + tab_lds;
 	};
@@ -3006,7 +3125,11 @@ extern "C" int gcl_classify_ex(struct gcl_ctx *c, const struct gcl_batch *b,
 	else if (c->tune_tables == 2)
 		tlds = tab_bytes <= kLdsTableBudget;
 	k.tables_lds_bytes = tlds ? tab_bytes : 0;
-	Geometry geo = choose_geometry(c, tlds ? tab_bytes : 0, hist_bytes, general);
+	/* dense slots with 1-/2-B verdicts, 4-B-aligned frames and 16-B-aligned
+	 * verdicts (the deferred verdicts go out 16 B at a time) */
+	const bool dense_ok = !general && (k.cflags & (GCL_CFG_VERDICT1 | GCL_CFG_VERDICT2)) &&
+	                      ((uintptr_t)b->frames & 3) == 0 && ((uintptr_t)verdicts & 15) == 0;
+	Geometry geo = choose_geometry(c, tlds ? tab_bytes : 0, hist_bytes, general, dense_ok);
 
 	HipErr he;
 

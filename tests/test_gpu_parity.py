@@ -305,11 +305,20 @@ def test_gpu_dense_verdict1(g, orc, wl, R, T):
     assert (c == ce).all() and (st == se).all()
 
 
+DENSE_FORMS = {0: "tile kernel", 1: "pair DENSE deferred nt", 2: "pair DENSE deferred plain",
+               3: "pair DENSE per-packet"}
+
+
+@pytest.mark.parametrize("dense", sorted(DENSE_FORMS))
 @pytest.mark.parametrize("wl,R,T,vb", [(0, 16, 8, 1), (0, 16, 8, 2), (1, 1024, 4, 2)])
-def test_gpu_dense_narrow_verdicts(g, orc, wl, R, T, vb):
-    """Dense tiles' 1- and 2-B verdicts (write-through byte and short
-    stores), the partial last tile included; 256- (udp64) and 512-lane
-    (1024-runtime tcp1500) blocks."""
+def test_gpu_dense_narrow_verdicts(g, orc, wl, R, T, vb, dense, monkeypatch):
+    """Dense slots' 1- and 2-B verdicts on every dense form (GCL_TUNE_DENSE):
+    the LDS-tile kernel's write-through byte and short stores, and
+    classify_pair_kernel<DENSE> with the verdicts kept in LDS and written
+    after the block's tiles (streaming or plain loads) or per packet; the
+    partial last tile included; 256- (udp64) and 512-lane (1024-runtime
+    tcp1500) blocks."""
+    monkeypatch.setenv("GCL_TUNE_DENSE", str(dense))
     stride = {0: 64, 1: 1536}[wl]
     n = 40000 + 77
     df = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
@@ -329,8 +338,47 @@ def test_gpu_dense_narrow_verdicts(g, orc, wl, R, T, vb):
     v, c, st = gpu_run(g, clf, frames, n, stride)
     ve, ce, se = t.classify(frames, n, stride)
     w = to_verdict1(ve, [T] * R, tb) if vb == 1 else to_verdict2(ve, [T] * R, tb)
-    assert_same(v, w, f"narrow verdicts wl={wl} vb={vb}")
+    assert_same(v, w, f"narrow verdicts wl={wl} vb={vb} {DENSE_FORMS[dense]}")
     assert (c == ce).all() and (st == se).all()
+
+
+@pytest.mark.parametrize("dense,env", [(1, {}), (1, {"GCL_TUNE_GRID": "3"}), (2, {"GCL_TUNE_GRID": "5"}),
+                                       (1, {"GCL_TUNE_BLOCKS_PER_CU": "1", "GCL_TUNE_GRID": "301"})])
+@pytest.mark.parametrize("vb", [1, 2])
+def test_gpu_dense_deferred_flushes(g, orc, vb, dense, env, monkeypatch):
+    """classify_pair_kernel<DENSE>'s LDS verdict buffer when a block walks
+    more tiles than it holds (few blocks: GCL_TUNE_GRID): full buffers
+    flushed inside the loop, a partial one at the end, the batch's ragged
+    last tile cut at n -- against the oracle on a 1 Mi + 77-packet udp64
+    batch, with its counts and counters."""
+    for kk, vv in {"GCL_TUNE_DENSE": str(dense), **env}.items():
+        monkeypatch.setenv(kk, vv)
+    R, T, stride = 16, 8, 64
+    n = (1 << 20) + 77
+    df = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
+    g.generate(0, n, stride, R, df, seed=29)
+    frames = df.cpu().numpy()
+    tb = 3 if vb == 1 else 4
+    clf = g.Classifier(0, R, g.HASH_JENKINS, g.CFG_VERDICT1 if vb == 1 else g.CFG_VERDICT2, thread_bits=tb)
+    t = orc.Tables(R, g.HASH_JENKINS, 0, g.F_RSS_HASH | g.F_IP_CKSUM_GOOD)
+    for r in range(R):
+        act = (r * 3) % (T + 1)
+        fl = g.steer_flows(T, list(range(act))) if act else None
+        clf.runtime_set(r, g.runtime_ip(r), T, act, fl)
+        t.runtime_set(r, orc.runtime_ip(r), T, act, fl)
+    v = torch.full((n * vb + 64,), 0xEE, dtype=torch.uint8, device="cuda")
+    c = torch.zeros(R, dtype=torch.int64, device="cuda")
+    st = torch.zeros(g.NR_STATS, dtype=torch.int64, device="cuda")
+    clf.classify(df, n, stride, verdicts=v, counts=c, stats=st)
+    torch.cuda.synchronize()
+    got = v.cpu().numpy()
+    assert (got[n * vb:] == 0xEE).all(), "a verdict store past n"
+    got = got[:n * vb].view(np.uint8 if vb == 1 else np.uint16)
+    ve, ce, se = t.classify(frames, n, stride)
+    w = to_verdict1(ve, [T] * R, tb) if vb == 1 else to_verdict2(ve, [T] * R, tb)
+    assert_same(got, w, f"deferred flushes vb={vb} dense={dense} {env}")
+    assert (c.cpu().numpy().astype(np.uint64) == ce).all()
+    assert (st.cpu().numpy().astype(np.uint64) == se).all()
 
 
 def test_gpu_verdict1_limits(g):
