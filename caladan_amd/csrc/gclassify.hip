@@ -101,8 +101,8 @@ struct KParams {
 	uint32_t default_flags;
 	uint2 *trans;    /* struct gcl_trans[n] or NULL */
 	uint32_t off_seed, off_crc;
-	uint32_t vcap;   /* classify_pair_kernel DENSE: tiles of verdicts its LDS buffer holds
-	                    (0: every verdict stored at once) */
+	uint32_t vcap;   /* classify_kernel, 1-/2-B verdicts: tiles of verdicts its LDS buffer
+	                    holds (0: every verdict stored as it is made) */
 };
 
 /* ------------------------------------------------------------------------
@@ -690,6 +690,49 @@ classify_kernel(KParams k)
 	uint4 ra[4], rb[4];
 	uint64_t t = blockIdx.x;
 	const uint64_t step = gridDim.x, t_end = k.ntiles;
+	/* k.vcap (1-/2-B verdicts): each tile's verdicts kept in LDS after the
+	 * tables, and written out 16 B per lane once vcap tiles are in and after
+	 * the last tile, so the verdict stream does not interleave with the frame
+	 * reads (tools/wdefer.hip) */
+	const uint32_t vb = (k.cflags & GCL_CFG_VERDICT1) ? 1 : 2;
+	uint8_t *vbuf = lds_tab + ((k.tables_lds_bytes + 15) & ~15u);
+	uint32_t kl = 0, kf = 0; /* tiles in the buffer; tiles written before them (uniform) */
+	auto verdict = [&](uint64_t i, uint64_t w) {
+		if (!k.vcap) {
+			put_verdict(k, i, w);
+		} else {
+			uint8_t *d = vbuf + (kl * NT + tid) * vb;
+			if (vb == 1)
+				*d = (uint8_t)w;
+			else
+				*(uint16_t *)d = (uint16_t)w;
+		}
+	};
+	/* after a classified tile (and its barrier): count it, write a full buffer */
+	auto flush = [&]() {
+		const uint32_t cs = vb == 1 ? __builtin_ctz(NT / 16) : __builtin_ctz(NT / 8); /* log2 chunks per tile */
+		const uint64_t nb = k.n * vb;
+		const __amdgpu_buffer_rsrc_t vrs = gcl::host_rsrc(k.verdicts, nb);
+		for (uint32_t i = tid; i < kl << cs; i += NT) {
+			const uint32_t j = i >> cs, c = i & ((1u << cs) - 1);
+			const uint64_t o = ((uint64_t)blockIdx.x + (uint64_t)(kf + j) * step) * NT * vb + 16 * c;
+			const uint8_t *src = vbuf + j * NT * vb + 16 * c;
+			if (o + 16 <= nb) {
+				const uint4 v = *(const uint4 *)src;
+				const gcl::u32x4 x = {v.x, v.y, v.z, v.w};
+				__builtin_amdgcn_raw_buffer_store_b128(x, vrs, (int)o, 0, gcl::kSysAux);
+			} else {
+				for (uint32_t b = 0; o + b < nb && b < 16; b++)
+					store_wt((uint8_t *)k.verdicts + o + b, src[b]);
+			}
+		}
+		kf += kl;
+		kl = 0;
+	};
+	auto tile_done = [&](uint64_t tt) {
+		if (k.vcap && tt < t_end && ++kl == k.vcap)
+			flush(); /* the next writes to vbuf follow the next stage's barrier */
+	};
 	if (t < t_end)
 		load_tile<NT>(k, t, true, ra);
 	if (DEPTH == 2)
@@ -708,8 +751,9 @@ classify_kernel(KParams k)
 		/* in flight while parsing */
 		load_tile<NT>(k, nxt, nxt < t_end, ra);
 		if (t * NT + tid < k.n)
-			put_verdict(k, t * NT + tid, classify_one<MODE, false>(k, tile, tid, t * NT + tid, tb, hist, cnt));
+			verdict(t * NT + tid, classify_one<MODE, false>(k, tile, tid, t * NT + tid, tb, hist, cnt));
 		__syncthreads();
+		tile_done(t);
 		t += step;
 		if (DEPTH == 2) {
 			/* runs past t_end too (an empty tile: dummy loads, nothing
@@ -720,12 +764,14 @@ classify_kernel(KParams k)
 			__syncthreads();
 			load_tile<NT>(k, t + 2 * step, t + 2 * step < t_end, rb);
 			if (t < t_end && t * NT + tid < k.n)
-				put_verdict(k, t * NT + tid,
-				            classify_one<MODE, false>(k, tile, tid, t * NT + tid, tb, hist, cnt));
+				verdict(t * NT + tid, classify_one<MODE, false>(k, tile, tid, t * NT + tid, tb, hist, cnt));
 			__syncthreads();
+			tile_done(t);
 			t += step;
 		}
 	}
+	if (kl)
+		flush();
 	flush_counters<NT>(k, hist, cnt);
 }
 
@@ -784,16 +830,15 @@ typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 
 /* load J of this lane: half (lane & 1) of the pair's packet J, whose
  * pair_src lane J of the pair holds in @my (quad_perm broadcast) */
-template <int J, bool NTL = false>
+template <int J>
 __device__ __forceinline__ uint4 pair_load(const KParams &k, uint64_t my)
 {
 	constexpr int B = J ? 0xF5 : 0xA0; /* quad_perm [1,1,3,3] : [0,0,2,2] */
 	const uint32_t lo = mdpp<B>((uint32_t)my), hi = mdpp<B>((uint32_t)(my >> 32));
 	const uint64_t s = (uint64_t)hi << 32 | lo;
 	const uint8_t *a = (hi >> 31) ? k.tables : k.frames + s + 16 * (threadIdx.x & 1);
-	/* plain loads: the frames stay in L2 for the next use of the same mbuf;
-	 * NTL (dense slots, every frame read once): the streaming hint */
-	const u32x4a4 v = NTL ? __builtin_nontemporal_load((const u32x4a4 *)a) : *(const u32x4a4 *)a;
+	/* plain loads: the frames stay in L2 for the next use of the same mbuf */
+	const u32x4a4 v = *(const u32x4a4 *)a;
 	return make_uint4(v.x, v.y, v.z, v.w);
 }
 
@@ -809,20 +854,10 @@ __device__ __forceinline__ void pair_exchange(uint4 r[2])
 	r[1] = sel4(odd, r[1], y);
 }
 
-/*
- * DENSE (fixed-stride slots, no per-packet arrays, every granule inside
- * frames_len; VF 1 or 2): no offset or side-array loads, and -- with
- * k.vcap -- the verdicts of the block's tiles kept in LDS and written
- * after its last tile (or whenever the buffer holds k.vcap tiles), 16 B per
- * lane.  Interleaved with the header reads, the 1-B verdict stream cost the
- * udp64 read stream 28 us of 331; written after the reads it costs ~14
- * (tools/wdefer.hip, profiles/r05_wdefer.jsonl).  NTL: streaming loads.
- */
-template <int MODE, bool TLDS, int NT, int VF, bool DENSE = false, bool NTL = false>
+template <int MODE, bool TLDS, int NT, int VF>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4)))
 classify_pair_kernel(KParams k)
 {
-	static_assert(!DENSE || VF == 1 || VF == 2, "DENSE keeps 1- or 2-B verdicts in LDS");
 	extern __shared__ uint4 smem[];
 	uint32_t *hist = (uint32_t *)smem;
 	uint8_t *lds_tab = (uint8_t *)(hist + ((k.max_rt + 3) & ~3u));
@@ -850,52 +885,20 @@ classify_pair_kernel(KParams k)
 	const uint64_t *offs_src = k.offs ? k.offs : (const uint64_t *)k.tables;
 	auto ok = [&](uint64_t tt) { return tt < k.ntiles && tt * NT + tid < k.n; };
 	auto ld_off = [&](uint64_t tt) -> uint64_t {
-		if (DENSE)
-			return 0;
 		return user_off(k, offs_src[k.offs && ok(tt) ? tt * NT + tid : 0]);
 	};
 	auto src_of = [&](uint64_t tt, uint64_t raw) -> uint64_t {
-		if (DENSE)
-			return !ok(tt) ? kNoOff : (tt * NT + tid) * k.stride + 8;
 		return pair_src(k, !ok(tt) ? kNoOff : k.offs ? raw : (tt * NT + tid) * k.stride);
 	};
 	auto pref = [&](uint64_t tt, uint32_t pr[2]) {
-		if (DENSE)
-			return;
 		const uint64_t i = ok(tt) ? tt * NT + tid : 0;
 		pr[0] = *(k.olflags ? k.olflags + i : side_dummy<uint8_t>(k, i));
 		if (MODE == GCL_HASH_NIC)
 			pr[1] = *(k.rss ? k.rss + i : side_dummy<uint32_t>(k, i));
 	};
 	auto issue = [&](uint64_t my, uint4 r[2]) {
-		r[0] = pair_load<0, NTL>(k, my);
-		r[1] = pair_load<1, NTL>(k, my);
-	};
-	/* DENSE: the LDS verdict buffer, k.vcap tiles of NT * VB bytes */
-	constexpr uint32_t VB = VF == 1 ? 1 : 2;
-	uint8_t *vbuf = lds_tab + k.tables_lds_bytes;
-	const bool defer = DENSE && k.vcap != 0;
-	uint32_t kl = 0; /* this block's tiles classified so far (uniform) */
-	/* the block's local tiles [k0, k1) from the buffer to their places,
-	 * 16 B per lane, write-through like the per-packet stores; the batch's
-	 * last tile up to n only */
-	auto flush = [&](uint32_t k0, uint32_t k1) {
-		constexpr uint32_t C = NT * VB / 16; /* chunks per tile */
-		const uint64_t nb = k.n * VB;
-		for (uint32_t i = tid; i < (k1 - k0) * C; i += NT) {
-			const uint32_t kk = k0 + i / C, c = i % C;
-			const uint64_t o = ((uint64_t)blockIdx.x + (uint64_t)kk * step) * NT * VB + 16 * c;
-			const uint8_t *src = vbuf + (kk % k.vcap) * NT * VB + 16 * c;
-			uint8_t *dst = (uint8_t *)k.verdicts + o;
-			if (o + 16 <= nb) {
-				const uint4 v = *(const uint4 *)src;
-				store_wt((uint64_t *)dst, (uint64_t)v.x | (uint64_t)v.y << 32);
-				store_wt((uint64_t *)(dst + 8), (uint64_t)v.z | (uint64_t)v.w << 32);
-			} else {
-				for (uint32_t b = 0; o + b < nb && b < 16; b++)
-					store_wt(dst + b, src[b]);
-			}
-		}
+		r[0] = pair_load<0>(k, my);
+		r[1] = pair_load<1>(k, my);
 	};
 	/* the landed halves -> this lane's header dwords (frame bytes 12-39;
 	 * d10, bytes 40-43, is not fetched: avail 40 sends ARP to the frame) */
@@ -914,27 +917,8 @@ classify_pair_kernel(KParams k)
 			const uint64_t i = tt * NT + tid;
 			/* this packet's frame offset, for the ARP target's extra read */
 			const uint64_t foff = (my >> 63) ? (my & ~kPairBytewise) : my - 8;
-			const uint64_t w = classify_core<MODE, true, false, true, VF>(k, h, nullptr, tid, i, tb, hist,
-			                                                               cnt, 0, 40, pr, foff);
-			if (defer) {
-				uint8_t *d = vbuf + ((kl % k.vcap) * NT + tid) * VB;
-				if (VB == 1)
-					*d = (uint8_t)w;
-				else
-					*(uint16_t *)d = (uint16_t)w;
-			} else {
-				put_verdict_vf<VF>(k, i, w);
-			}
-		}
-	};
-	/* after tile tt: count it, and flush a full buffer */
-	auto tile_done = [&](uint64_t tt) {
-		if (!defer || tt >= k.ntiles)
-			return;
-		if (++kl % k.vcap == 0) {
-			__syncthreads();
-			flush(kl - k.vcap, kl);
-			__syncthreads(); /* the buffer is free again */
+			put_verdict_vf<VF>(k, i, classify_core<MODE, true, false, true, VF>(
+			                                 k, h, nullptr, tid, i, tb, hist, cnt, 0, 40, pr, foff));
 		}
 	};
 
@@ -959,7 +943,6 @@ classify_pair_kernel(KParams k)
 		sa = src_of(t + 2 * step, oa);
 		issue(sa, ra);
 		classify(t, h, pra, my);
-		tile_done(t);
 		pref(t + 2 * step, pra);
 		oa = ld_off(t + 4 * step);
 		t += step;
@@ -970,14 +953,11 @@ classify_pair_kernel(KParams k)
 		sb = src_of(t + 2 * step, ob);
 		issue(sb, rb);
 		classify(t, h, prb, my);
-		tile_done(t);
 		pref(t + 2 * step, prb);
 		ob = ld_off(t + 4 * step);
 		t += step;
 	}
-	__syncthreads(); /* every wave's histogram adds (and buffered verdicts) are in */
-	if (defer && kl % k.vcap)
-		flush(kl - kl % k.vcap, kl);
+	__syncthreads(); /* every wave's histogram adds are in */
 	flush_counters<NT>(k, hist, cnt);
 }
 
@@ -1029,13 +1009,11 @@ constexpr uint64_t kLoopRefresh = 256;
 /* s_memrealtime ticks (100 MHz) a wait polls the offsets with the word: a
  * burst that arrives later costs the offsets' round trip after the word */
 constexpr uint64_t kLoopSpecTicks = 400;
-/* GCL_TUNE_DENSE default (Geometry::dense) */
-constexpr int kDefaultDense = 0;
+/* GCL_TUNE_DEFER default (Geometry::defer) */
+constexpr int kDefaultDefer = 0;
 /* GCL_TUNE_LOOP_LEAN default: bursts whose every packet is plain IPv4 (IHL 5,
  * no FDIR mark, no hint) classified by classify_lean */
 constexpr uint32_t kDefaultLoopLean = 1;
-/* GCL_TUNE_LOOP_POLLERS default: rxloop64_kernel's poll-and-classify waves */
-constexpr int kDefaultLoopPollers = 1;
 /* how a worker's bursts arrived (gcl_rxloop_poll_stats): with the poll that
  * found the word; eligible for that, but an entry or record still stale so
  * read after it; or after the word, the speculative window over or the
@@ -1090,7 +1068,6 @@ struct LoopParams {
 	                              planes (chunk j of packet i at off_hdr + j * rec_plane + 16 i) */
 	uint32_t lean;             /* rxloop64_kernel: plain-IPv4 bursts on classify_lean
 	                              (GCL_TUNE_LOOP_LEAN=0: always classify_core) */
-	uint32_t lds_copy;         /* rxloop64_kernel: LDS bytes per table copy (header + image) */
 };
 
 /* GCL_LOOP_HDR_RECORDS: the submitting core writes each packet as one 64-B
@@ -1489,28 +1466,25 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
 }
 
 /* ------------------------------------------------------------------------
- * rxloop64_kernel<MODE, NP>: the loop at the reference's own burst size (<= 64
+ * rxloop64_kernel<MODE>: the loop at the reference's own burst size (<= 64
  * mbufs, IOKERNEL_RX_BURST_SIZE, defs.h:75), chosen by gcl_rxloop_start
  * whenever max_burst <= 64.  A burst that size is one packet per lane of ONE
  * wave, so a wave takes it from the poll to the verdicts alone, from
  * registers, with no barrier: rxloop_kernel's three barriers and its LDS tile
  * cost 0.7 us of a lone burst (GCL_LOOP_STAMPS, profiles/r04_stages_reentry.jsonl).
  *
- * NP poll-and-classify waves per worker.  With NP = 1 one wave polls the
- * worker's next ticket, classifies the burst and stores its verdict records.
- * With NP = 2 two such waves share the worker's ticket sequence through LDS:
- * a wave polls the lowest unclaimed ticket, half a poll round trip after the
- * other wave's poll of the same ticket (so the slot is sampled twice per round
- * trip, each wave with its own vmcnt), or -- when bursts are queued -- the
- * ticket after it; the wave whose poll brings a burst with current records
- * claims it with an LDS compare-and-swap and classifies it, while the other
- * keeps polling.  A poll that finds the word with stale records is not
- * claimed: the next sample (the other wave's, half a round trip on) brings
- * them.  One more wave (the writer) adds the counts and the counters (device
- * atomics) and the poll counters, so their retirement never holds a poller's
- * vmcnt (on gfx9 stores and loads share vmcnt and retire in order); bursts
- * reach it through two LDS mailboxes per classifying wave, ordered by
- * LDS-only fences (lgkmcnt, never vmcnt).
+ * Two waves per worker.  The poller polls the worker's next ticket,
+ * classifies the burst and stores its verdict records.  The writer adds the
+ * counts and the counters (device atomics) and the poll counters, so their
+ * retirement never holds the poller's vmcnt (on gfx9 stores and loads share
+ * vmcnt and retire in order); bursts reach it through two LDS mailboxes,
+ * ordered by LDS-only fences (lgkmcnt, never vmcnt).
+ *
+ * A second poller sharing the ticket sequence through LDS (each slot sampled
+ * twice per poll round trip, the burst claimed by an LDS compare-and-swap)
+ * lost the round-5 A/B on header records: lone bursts 3.84 -> 3.9-4.06 us p50,
+ * 4 workers x 8 deep 103 -> 92 Mpkt/s (profiles/r05_pollers_ab.jsonl); it
+ * won only on stamped offsets, the slower form, and was removed.
  */
 struct Mbox64 {
 	uint32_t p[64];   /* each packet's runtime (~0: none): the counts */
@@ -1536,66 +1510,37 @@ struct Wave64 {
 };
 static_assert(sizeof(Wave64) % 16 == 0, "Wave64");
 
-/* the worker's shared words (NP > 1: the ticket claims and the poll phases) */
+/* the worker's shared words */
 struct Ctl64 {
-	uint64_t state;     /* lowest unclaimed ticket index << 1 | (index + 1 claimed) */
-	uint64_t issue[2];  /* each wave's last poll issue (s_memrealtime) */
-	uint64_t target[2]; /* the ticket index each wave's poll is for */
-	uint64_t since;     /* when the last burst was posted (the spec window's start) */
-	uint32_t exited;    /* classifying waves that have left */
-	uint32_t queued;    /* the last claim came with its ticket's first poll */
-	uint32_t seq[2];    /* image sequence held by LDS table copy i (0xFF: none) */
+	uint32_t exited; /* the poller has left */
+	uint32_t pad[3];
 };
 static_assert(sizeof(Ctl64) % 16 == 0, "Ctl64");
 
-/* LDS of rxloop64_kernel<NP> with @copy bytes per table copy (a 64-B image
- * header + the image): NP = 2 keeps a copy per host image buffer, so one wave
- * can take a new snapshot while the other still classifies with the last */
-__host__ __device__ constexpr uint32_t loop64_lds(int np, uint32_t copy)
+/* LDS of rxloop64_kernel with @copy bytes for the table copy (a 64-B image
+ * header + the image) */
+__host__ __device__ constexpr uint32_t loop64_lds(uint32_t copy)
 {
-	return (uint32_t)sizeof(Ctl64) + np * (uint32_t)sizeof(Wave64) + (np > 1 ? 2 : 1) * copy;
+	return (uint32_t)sizeof(Ctl64) + (uint32_t)sizeof(Wave64) + copy;
 }
 
 /* rxloop64_kernel's writer wave: each posted burst's counts and counters,
- * the poll counters, the stage stamps; leaves once every classifying wave has
- * left and its mailboxes are drained. */
-template <int NP>
+ * the poll counters, the stage stamps; leaves once the poller has left and
+ * its mailboxes are drained. */
 __device__ __forceinline__ void rxloop64_writer(const LoopParams &L, Wave64 *wv, Ctl64 *ctl, int lane)
 {
 	uint32_t pe = 0, ps = 0, pl = 0; /* bursts by how they arrived (no indexed array: scratch) */
 	uint32_t pn = 0;                 /* bursts on classify_lean (gcl_rxloop_lean_bursts) */
-	for (uint32_t b = 0;; b = (b + 1) % (2 * NP)) {
-		Mbox64 &m = wv[b >> 1].mbox[b & 1];
-		if (!__hip_atomic_load(&m.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
-			if (NP == 1) {
-				/* one producer, in order: wait on this mailbox */
-				for (;;) {
-					if (__hip_atomic_load(&m.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
-						break;
-					if (__hip_atomic_load(&ctl->exited, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) &&
-					    !__hip_atomic_load(&m.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
-						return;
-					__builtin_amdgcn_s_sleep(1);
-				}
-			} else {
-				if (b + 1 == 2 * NP) { /* a whole round found nothing posted */
-					bool any = false;
-					for (int i = 0; i < 2 * NP; i++)
-						any |= __hip_atomic_load(&wv[i >> 1].mbox[i & 1].flag, __ATOMIC_RELAXED,
-						                         __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
-					if (!any && __hip_atomic_load(&ctl->exited, __ATOMIC_RELAXED,
-					                              __HIP_MEMORY_SCOPE_WORKGROUP) == NP) {
-						bool late = false; /* posted between the two reads */
-						for (int i = 0; i < 2 * NP; i++)
-							late |= __hip_atomic_load(&wv[i >> 1].mbox[i & 1].flag, __ATOMIC_RELAXED,
-							                          __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
-						if (!late)
-							return;
-					}
-					__builtin_amdgcn_s_sleep(1);
-				}
-				continue;
-			}
+	for (uint32_t b = 0;; b ^= 1) {
+		Mbox64 &m = wv->mbox[b];
+		/* one producer, in order: wait on this mailbox */
+		for (;;) {
+			if (__hip_atomic_load(&m.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+				break;
+			if (__hip_atomic_load(&ctl->exited, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) &&
+			    !__hip_atomic_load(&m.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+				return;
+			__builtin_amdgcn_s_sleep(1);
 		}
 		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 		const uint64_t t_w = L.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -1656,69 +1601,24 @@ __device__ __forceinline__ uint32_t lane0_u32(uint32_t v)
 	return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
 }
 
-/* a shared control word another wave may write: an atomic LDS load (never
- * hoisted or merged), uniform */
-__device__ __forceinline__ uint64_t ctl_ld64(const uint64_t *p)
-{
-	return lane0_u64(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-}
-
-__device__ __forceinline__ uint32_t ctl_ld32(const uint32_t *p)
-{
-	return lane0_u32(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-}
-
-/* NP > 1: claim ticket index @k for this wave (lane 0's LDS compare-and-swap
- * on Ctl64::state); false if another wave has it */
-__device__ __forceinline__ bool loop64_claim(Ctl64 *ctl, uint64_t k, int lane)
-{
-	uint32_t ok = 0;
-	if (lane == 0) {
-		uint64_t s = __hip_atomic_load(&ctl->state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-		for (;;) {
-			const uint64_t kc = s >> 1, ah = s & 1;
-			uint64_t nx;
-			if (k == kc)
-				nx = (kc + 1 + ah) << 1;
-			else if (k == kc + 1 && !ah)
-				nx = s | 1;
-			else
-				break; /* claimed already */
-			if (__hip_atomic_compare_exchange_strong(&ctl->state, &s, nx, __ATOMIC_RELAXED,
-			                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
-				ok = 1;
-				break;
-			}
-		}
-	}
-	return lane0_u32(ok) != 0;
-}
-
-template <int MODE, int NP>
-__global__ void __launch_bounds__(64 * (NP + 1)) rxloop64_kernel(LoopParams L)
+template <int MODE>
+__global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
 {
 	extern __shared__ uint4 smem[];
 	Ctl64 *ctl = (Ctl64 *)smem;
 	Wave64 *wv = (Wave64 *)(ctl + 1);
-	uint8_t *copies = (uint8_t *)(wv + NP); /* NP > 1: two; each a LoopImgHdr + image */
+	uint8_t *cb = (uint8_t *)(wv + 1); /* the table copy: a LoopImgHdr + the image */
 	const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 	if (threadIdx.x == 0) {
-		for (int i = 0; i < NP; i++)
-			wv[i].mbox[0].flag = wv[i].mbox[1].flag = 0;
-		ctl->state = 0;
-		ctl->issue[0] = ctl->issue[1] = 0;
-		ctl->target[0] = ctl->target[1] = ~0ull;
-		ctl->since = __builtin_amdgcn_s_memrealtime();
+		wv->mbox[0].flag = wv->mbox[1].flag = 0;
 		ctl->exited = 0;
-		ctl->queued = 0;
-		ctl->seq[0] = ctl->seq[1] = 0xFF;
 	}
 	__syncthreads(); /* the only barrier */
-	if (w == NP) {
-		rxloop64_writer<NP>(L, wv, ctl, lane);
+	if (w == 1) {
+		rxloop64_writer(L, wv, ctl, lane);
 		return;
 	}
-	Wave64 &me = wv[w];
+	Wave64 &me = *wv;
 	const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + L.lifetime_ticks;
 	const __amdgpu_buffer_rsrc_t frs = gcl::host_rsrc(L.frames, L.frames_len);
 	if (lane == 0 && w == 0 && blockIdx.x < 8) /* which XCD this worker runs on */
@@ -1732,46 +1632,14 @@ __global__ void __launch_bounds__(64 * (NP + 1)) rxloop64_kernel(LoopParams L)
 	k.offs = me.offs;
 	k.trans = L.off_trans ? me.trans : nullptr;
 	Tables tb = {};
-	uint32_t cur_seq = 0xFF, cur_copy = 0; /* the image this wave's tb points at */
+	uint32_t cur_seq = 0xFF; /* the image tb points at (0xFF: none) */
 	uint32_t mb = 0;
 	const bool spec = L.spec, rec = L.hdr_rec;
-	/* NP > 1: this wave's estimate of a poll's round trip (s_memrealtime
-	 * ticks), which sets the other wave's phase */
-	uint32_t rt_est = 136;
-	uint64_t kmine = 0;    /* NP == 1: this worker's next ticket index */
+	uint64_t kt = 0; /* this worker's next ticket index */
 	uint64_t spec_end = __builtin_amdgcn_s_memrealtime() + L.spec_ticks;
-	uint32_t npoll = 0;    /* polls since the ticket polled became the lowest unclaimed */
-	uint64_t kprev = ~0ull;
+	uint32_t npoll = 0; /* polls of this ticket */
 
 	for (uint32_t kk = 0;; kk++) {
-		/* the ticket this poll is for */
-		uint64_t kt = kmine;
-		if (NP > 1) {
-			const uint64_t s = ctl_ld64(&ctl->state);
-			const uint64_t kc = s >> 1;
-			const bool ah = s & 1;
-			kt = kc;
-			const int o = w ^ 1;
-			const uint64_t o_target = ctl_ld64(&ctl->target[o]);
-			if (o_target == kc) {
-				const uint64_t o_issue = ctl_ld64(&ctl->issue[o]);
-				const bool queued = ctl_ld32(&ctl->queued) != 0;
-				if (queued && !ah) {
-					kt = kc + 1; /* bursts are queued: poll the next one too */
-				} else {
-					/* the slot sampled half a round trip after the other wave */
-					const uint64_t at = o_issue + rt_est / 2;
-					while (__builtin_amdgcn_s_memrealtime() < at)
-						__builtin_amdgcn_s_sleep(1);
-				}
-			}
-			if (kt != kprev) { /* a new ticket for this wave: its own spec window */
-				npoll = 0;
-				kprev = kt;
-			}
-			const uint64_t since = ctl_ld64(&ctl->since);
-			spec_end = since + L.spec_ticks + (kt != kc ? L.spec_ticks : 0);
-		}
 		/* the ticket and its slot, uniform: a slot address the compiler
 		 * thinks divergent puts every buffer load in a waterfall loop
 		 * (nslots is a power of two: a mask, not a 64-bit modulo) */
@@ -1791,10 +1659,6 @@ __global__ void __launch_bounds__(64 * (NP + 1)) rxloop64_kernel(LoopParams L)
 		 * flag (one address: one request), so no divergent branch lets the
 		 * compiler consume the records before the word is even issued. */
 		const uint64_t t_issue = __builtin_amdgcn_s_memrealtime();
-		if (NP > 1 && lane == 0) {
-			__hip_atomic_store(&ctl->issue[w], t_issue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-			__hip_atomic_store(&ctl->target[w], kt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-		}
 		npoll++;
 		const bool sp = spec && t_issue < spec_end;
 		const uint64_t wv0 = gcl::ld_sys64(&h->word);
@@ -1812,13 +1676,7 @@ __global__ void __launch_bounds__(64 * (NP + 1)) rxloop64_kernel(LoopParams L)
 		const uint64_t w_word = lane0_u64(wv0);
 		const uint32_t sv = lane0_u32(sv0);
 		const bool found = (w_word >> 24) == (t & ((1ull << 40) - 1));
-		if (NP > 1) {
-			const uint32_t d = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_issue);
-			rt_est = std::min(400u, std::max(50u, rt_est - rt_est / 8 + d / 8));
-		}
 		if (!found) {
-			if (NP > 1 && lane == 0)
-				__hip_atomic_store(&ctl->queued, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 			if (sv || __builtin_amdgcn_s_memrealtime() > t_end)
 				break; /* stopped, or the lifetime is over */
 			__builtin_amdgcn_s_sleep(1);
@@ -1830,64 +1688,40 @@ __global__ void __launch_bounds__(64 * (NP + 1)) rxloop64_kernel(LoopParams L)
 		const bool rok = sp && q[0].x == rstamp && q[1].x == rstamp && q[2].x == rstamp && q[3].x == rstamp;
 		const bool fresh = !live || (rec ? rok : sp && (ev & ~kLoopOffMask) == stamp);
 		const bool early = spec && nw <= 64 && __all(fresh);
-		if (NP > 1) {
-			/* stale records while the window lasts: the next sample brings them */
-			if (!early && sp && nw <= 64) {
-				__builtin_amdgcn_s_sleep(1);
-				continue;
-			}
-			if (!loop64_claim(ctl, kt, lane))
-				continue; /* the other wave has it */
-			if (lane == 0)
-				__hip_atomic_store(&ctl->queued, npoll == 1 ? 1u : 0u, __ATOMIC_RELAXED,
-				                   __HIP_MEMORY_SCOPE_WORKGROUP);
-		}
 		const uint64_t hit = L.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
 		const uint32_t kind = early ? kLoopPollEarly : (sp && nw <= 64) ? kLoopPollStale : kLoopPollLate;
 		const uint32_t polls_used = npoll;
 		Mbox64 &m = me.mbox[mb]; /* free: waited for after the last post */
-		{ /* this burst's table snapshot */
-			const uint32_t cp = NP > 1 ? img : 0;
-			uint8_t *cb = copies + cp * L.lds_copy;
-			if (img_seq != cur_seq || cp != cur_copy) {
-				if (ctl_ld32(&ctl->seq[cp]) != img_seq) { /* copy it into LDS */
-					const uint8_t *ib = L.img[img];
-					const uint32_t bytes = gcl::ld_sys32(ib);
-					const __amdgpu_buffer_rsrc_t irs = gcl::host_rsrc(ib, 64 + (uint64_t)bytes);
-					uint32_t *t32 = (uint32_t *)cb;
-					for (uint32_t o = 16 * lane; o < 64 + bytes; o += 4 * 16 * 64) {
-						gcl::u32x4 x[4];
+		if (img_seq != cur_seq) { /* this burst's table snapshot: copied into LDS */
+			const uint8_t *ib = L.img[img];
+			const uint32_t bytes = gcl::ld_sys32(ib);
+			const __amdgpu_buffer_rsrc_t irs = gcl::host_rsrc(ib, 64 + (uint64_t)bytes);
+			uint32_t *t32 = (uint32_t *)cb;
+			for (uint32_t o = 16 * lane; o < 64 + bytes; o += 4 * 16 * 64) {
+				gcl::u32x4 x[4];
 #pragma unroll
-						for (int j = 0; j < 4; j++)
-							x[j] = __builtin_amdgcn_raw_buffer_load_b128(irs, (int)(o + 1024 * j), 0,
-							                                            gcl::kSysAux);
+				for (int j = 0; j < 4; j++)
+					x[j] = __builtin_amdgcn_raw_buffer_load_b128(irs, (int)(o + 1024 * j), 0, gcl::kSysAux);
 #pragma unroll
-						for (int j = 0; j < 4; j++)
+				for (int j = 0; j < 4; j++)
 #pragma unroll
-							for (int d = 0; d < 4; d++)
-								if (o + 1024 * j + 4 * d < 64 + bytes)
-									t32[(o + 1024 * j) / 4 + d] = x[j][d];
-					}
-					__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-					if (lane == 0)
-						__hip_atomic_store(&ctl->seq[cp], img_seq, __ATOMIC_RELAXED,
-						                   __HIP_MEMORY_SCOPE_WORKGROUP);
-				}
-				/* the copy (this wave's or the other's) before its reads */
-				__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-				const LoopImgHdr *ih = (const LoopImgHdr *)cb;
-				const uint8_t *tab = cb + 64;
-				k.ipt_mask = lane0_u32(ih->ipt_mask);
-				k.ipt_seed = lane0_u32(ih->ipt_seed);
-				tb.ipt = (const uint2 *)tab;
-				tb.rtab = (const RtEntry *)(tab + lane0_u32(ih->off_rt));
-				tb.flow = tab + lane0_u32(ih->off_flow);
-				tb.toep = (const uint32_t *)(tab + lane0_u32(ih->off_toep));
-				tb.seed = (const uint32_t *)(tab + lane0_u32(ih->off_seed));
-				tb.crc = (const uint32_t *)(tab + lane0_u32(ih->off_crc));
-				cur_seq = img_seq;
-				cur_copy = cp;
+					for (int d = 0; d < 4; d++)
+						if (o + 1024 * j + 4 * d < 64 + bytes)
+							t32[(o + 1024 * j) / 4 + d] = x[j][d];
 			}
+			/* the copy before its reads */
+			__builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup", "local");
+			const LoopImgHdr *ih = (const LoopImgHdr *)cb;
+			const uint8_t *tab = cb + 64;
+			k.ipt_mask = lane0_u32(ih->ipt_mask);
+			k.ipt_seed = lane0_u32(ih->ipt_seed);
+			tb.ipt = (const uint2 *)tab;
+			tb.rtab = (const RtEntry *)(tab + lane0_u32(ih->off_rt));
+			tb.flow = tab + lane0_u32(ih->off_flow);
+			tb.toep = (const uint32_t *)(tab + lane0_u32(ih->off_toep));
+			tb.seed = (const uint32_t *)(tab + lane0_u32(ih->off_seed));
+			tb.crc = (const uint32_t *)(tab + lane0_u32(ih->off_crc));
+			cur_seq = img_seq;
 		}
 		/* this lane's packet in registers: its header words and side fields */
 		HdrWords hw;
@@ -2014,19 +1848,15 @@ __global__ void __launch_bounds__(64 * (NP + 1)) rxloop64_kernel(LoopParams L)
 		if (lane == 0)
 			__hip_atomic_store(&m.flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 		mb ^= 1;
-		if (NP > 1 && lane == 0) /* the spec window runs from the last burst's end */
-			__hip_atomic_store(&ctl->since, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
-			                   __HIP_MEMORY_SCOPE_WORKGROUP);
 		/* the mailbox the next burst will be posted to, freed by the writer
 		 * long before: waited for here, not after the next hit */
 		while (__hip_atomic_load(&me.mbox[mb].flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
 			__builtin_amdgcn_s_sleep(1);
 		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-		if (NP == 1) { /* the next ticket, its own spec window */
-			kmine++;
-			npoll = 0;
-			spec_end = __builtin_amdgcn_s_memrealtime() + L.spec_ticks;
-		}
+		/* the next ticket, its own spec window */
+		kt++;
+		npoll = 0;
+		spec_end = __builtin_amdgcn_s_memrealtime() + L.spec_ticks;
 	}
 	/* the writer drains what was posted, then leaves; the host stops
 	 * publishing on this word (one it reads without a HIP call per burst) */
@@ -2376,7 +2206,7 @@ struct gcl_ctx {
 	int tune_threads; /* GCL_TUNE_THREADS: 256, 512 or 1024 lanes per block */
 	int tune_grid;    /* GCL_TUNE_GRID: blocks per launch (0: the persistent grid) */
 	int tune_bpc;     /* GCL_TUNE_BLOCKS_PER_CU: cap on blocks per CU (0: none) */
-	int tune_dense;   /* GCL_TUNE_DENSE: Geometry::dense for eligible batches (A/B) */
+	int tune_defer;   /* GCL_TUNE_DEFER: Geometry::defer for eligible batches (0-2) */
 };
 
 extern "C" {
@@ -2450,10 +2280,8 @@ extern "C" int gcl_open(int hip_device, const struct gcl_cfg *cfg, struct gcl_ct
 		c->tune_grid = e ? atoi(e) : 0;
 		e = getenv("GCL_TUNE_BLOCKS_PER_CU");
 		c->tune_bpc = e ? atoi(e) : 0;
-		e = getenv("GCL_TUNE_DENSE");
-		c->tune_dense = e ? atoi(e) : kDefaultDense;
-		if (c->tune_dense < 0 || c->tune_dense > 3)
-			c->tune_dense = 0;
+		e = getenv("GCL_TUNE_DEFER");
+		c->tune_defer = e ? std::min(std::max(atoi(e), 0), 2) : kDefaultDefer;
 	}
 	c->dimg[0] = c->dimg[1] = nullptr;
 	for (int i = 0; i < 2; i++) {
@@ -2763,15 +2591,30 @@ struct Geometry {
 	int bpc_cap;  /* blocks per CU */
 	int grid;     /* blocks per launch when > 0 (GCL_TUNE_GRID) */
 	bool pair;    /* classify_pair_kernel (GENERAL batches): [8, 40) per packet by lane pairs */
-	int dense;    /* dense slots with 1-/2-B verdicts on classify_pair_kernel<DENSE>:
-	                 0 no (classify_kernel), 1 verdicts deferred in LDS + streaming loads,
-	                 2 deferred + plain loads, 3 not deferred + streaming loads */
+	int defer;    /* classify_kernel with 1-/2-B verdicts kept in LDS and written in
+	                 batches: 1 where that takes <= 2 writes per block, 2 always (tests) */
 };
 
+/* geo.defer: what the CU's LDS leaves the block at geo.bpc_cap blocks per
+ * CU holds k.vcap tiles of verdicts -- at most the block's share of the
+ * batch, and only where that takes at most two writes per block */
 template <int MODE, int DEPTH, int NT>
-static hipError_t launch_nt(const KParams &k, bool tlds, uint32_t lds, int num_cus, const Geometry &geo,
+static hipError_t launch_nt(KParams k, bool tlds, uint32_t lds, int num_cus, const Geometry &geo,
                             hipStream_t s)
 {
+	k.vcap = 0;
+	if (geo.defer) {
+		const uint32_t vb = (k.cflags & GCL_CFG_VERDICT1) ? 1 : 2;
+		const uint32_t base = align16(lds);
+		const uint32_t per_cu = 160 * 1024 / (uint32_t)std::max(geo.bpc_cap, 1);
+		const uint64_t blocks = geo.grid > 0 ? (uint64_t)geo.grid : (uint64_t)num_cus * std::max(geo.bpc_cap, 1);
+		const uint64_t want = ((k.n + NT - 1) / NT + blocks - 1) / blocks;
+		const uint64_t room = per_cu > base ? (per_cu - base) / (NT * vb) : 0;
+		if (room && (2 * room >= want || geo.defer == 2)) {
+			k.vcap = (uint32_t)std::min(want, room);
+			lds = base + k.vcap * NT * vb;
+		}
+	}
 	const ClassifyFn fn = tlds ? classify_kernel<MODE, true, DEPTH, NT> : classify_kernel<MODE, false, DEPTH, NT>;
 	return launch_fn(fn, NT, k, lds, num_cus, geo.bpc_cap, geo.grid, s);
 }
@@ -2793,48 +2636,10 @@ static hipError_t launch_pair(const KParams &k, bool tlds, uint32_t lds, int num
 	return launch_fn(fn, NT, k, lds, num_cus, geo.bpc_cap, geo.grid, s);
 }
 
-/* Dense slots with 1-/2-B verdicts on classify_pair_kernel<DENSE>: the
- * block's LDS is all it can have at geo.bpc_cap blocks per CU, and what the
- * tables and histogram leave of it holds k.vcap tiles of verdicts. */
-template <int MODE, int NT>
-static hipError_t launch_dense(KParams k, bool tlds, uint32_t base_lds, int num_cus, const Geometry &geo,
-                               hipStream_t s)
-{
-	const uint32_t vb = (k.cflags & GCL_CFG_VERDICT1) ? 1 : 2;
-	const bool defer = geo.dense != 3, ntl = geo.dense != 2;
-	uint32_t lds = base_lds;
-	k.vcap = 0;
-	if (defer) {
-		const uint32_t per_cu = 160 * 1024 / (uint32_t)std::max(geo.bpc_cap, 1);
-		const uint64_t ntiles = (k.n + NT - 1) / NT;
-		const uint32_t want = (uint32_t)std::min<uint64_t>(
-		        (ntiles + (uint64_t)num_cus * geo.bpc_cap - 1) / ((uint64_t)num_cus * geo.bpc_cap), 1u << 20);
-		const uint32_t room = per_cu > base_lds ? (per_cu - base_lds) / (NT * vb) : 0;
-		k.vcap = std::max(1u, std::min(want, room));
-		lds = base_lds + k.vcap * NT * vb;
-	}
-	ClassifyFn fn;
-	if (vb == 1)
-		fn = tlds ? (ntl ? classify_pair_kernel<MODE, true, NT, 1, true, true> : classify_pair_kernel<MODE, true, NT, 1, true, false>)
-		          : (ntl ? classify_pair_kernel<MODE, false, NT, 1, true, true> : classify_pair_kernel<MODE, false, NT, 1, true, false>);
-	else
-		fn = tlds ? (ntl ? classify_pair_kernel<MODE, true, NT, 2, true, true> : classify_pair_kernel<MODE, true, NT, 2, true, false>)
-		          : (ntl ? classify_pair_kernel<MODE, false, NT, 2, true, true> : classify_pair_kernel<MODE, false, NT, 2, true, false>);
-	return launch_fn(fn, NT, k, lds, num_cus, geo.bpc_cap, geo.grid, s);
-}
-
 template <int MODE>
 static hipError_t launch_mode(const KParams &k, bool tlds, const Geometry &geo,
                               uint32_t tab_lds, uint32_t hist_bytes, int num_cus, hipStream_t s)
 {
-	if (geo.dense) {
-		const uint32_t lds = hist_bytes + tab_lds;
-		if (geo.threads == 1024)
-			return launch_dense<MODE, 1024>(k, tlds, lds, num_cus, geo, s);
-		if (geo.threads == 512)
-			return launch_dense<MODE, 512>(k, tlds, lds, num_cus, geo, s);
-		return launch_dense<MODE, 256>(k, tlds, lds, num_cus, geo, s);
-	}
 	if (geo.pair) {
 		const uint32_t lds = hist_bytes + tab_lds;
 		if (geo.threads == 1024)
@@ -2867,7 +2672,7 @@ static hipError_t launch_mode(const KParams &k, bool tlds, const Geometry &geo,
  * waves than that only add contention (udp64: 446 us at 8 x 256).
  */
 static Geometry choose_geometry(const gcl_ctx *c, uint32_t tab_lds, uint32_t hist_bytes,
-                                bool general, bool dense_ok)
+                                bool general, bool defer_ok)
 {
 	const uint32_t lds_cu = 160 * 1024, lanes_cu = 1024;
 	Geometry g;
@@ -2879,9 +2684,9 @@ static Geometry choose_geometry(const gcl_ctx *c, uint32_t tab_lds, uint32_t his
 	 * in round 5: the pair kernel beat both on every row, working set 96
 	 * vs 109-111 us, random pool 181 vs 189, profiles/r03_ws_ab.jsonl.) */
 	g.pair = general;
-	g.dense = dense_ok ? c->tune_dense : 0;
+	g.defer = defer_ok ? c->tune_defer : 0;
 	auto per_block = [&](uint32_t nt) -> uint32_t {
-		if (g.pair || g.dense)
+		if (g.pair)
 			return hist_bytes + tab_lds;
 		return nt * 64 + hist_bytes + tab_lds;
 	};
@@ -3125,11 +2930,11 @@ extern "C" int gcl_classify_ex(struct gcl_ctx *c, const struct gcl_batch *b,
 	else if (c->tune_tables == 2)
 		tlds = tab_bytes <= kLdsTableBudget;
 	k.tables_lds_bytes = tlds ? tab_bytes : 0;
-	/* dense slots with 1-/2-B verdicts, 4-B-aligned frames and 16-B-aligned
-	 * verdicts (the deferred verdicts go out 16 B at a time) */
-	const bool dense_ok = !general && (k.cflags & (GCL_CFG_VERDICT1 | GCL_CFG_VERDICT2)) &&
-	                      ((uintptr_t)b->frames & 3) == 0 && ((uintptr_t)verdicts & 15) == 0;
-	Geometry geo = choose_geometry(c, tlds ? tab_bytes : 0, hist_bytes, general, dense_ok);
+	/* dense slots with 1-/2-B verdicts, 16-B-aligned (the deferred verdicts
+	 * go out 16 B at a time, through a buffer descriptor: below 4 GiB) */
+	const bool defer_ok = !general && (k.cflags & (GCL_CFG_VERDICT1 | GCL_CFG_VERDICT2)) &&
+	                      ((uintptr_t)verdicts & 15) == 0 && b->n * 2 < (1ull << 32);
+	Geometry geo = choose_geometry(c, tlds ? tab_bytes : 0, hist_bytes, general, defer_ok);
 
 	HipErr he;
 
@@ -3748,7 +3553,6 @@ struct gcl_rxloop {
 	bool ended;              /* the kernel has finished (hipStreamQuery) */
 	bool left;               /* some worker has left: submit no more */
 	bool k64;                /* rxloop64_kernel (bursts <= 64) */
-	int np;                  /* its poll-and-classify waves (1 or 2) */
 };
 
 static uint64_t now_ns()
@@ -3823,7 +3627,7 @@ static int loop_write_image(gcl_rxloop *L, int i)
 	const uint32_t bytes = build_image(c);
 	if (!bytes)
 		return -ENOSPC;
-	if (bytes > kLdsTableBudget || (L->k64 && 64 + bytes > L->lp.lds_copy))
+	if (bytes > kLdsTableBudget)
 		return -E2BIG;
 	LoopImgHdr hdr = {};
 	hdr.bytes = bytes;
@@ -3840,26 +3644,23 @@ static int loop_write_image(gcl_rxloop *L, int i)
 	return 0;
 }
 
-/* bursts of <= 64 packets: rxloop64_kernel with @np poll-and-classify waves
- * (+ the writer, no barrier), or with np 0 the general loop (bursts past 64,
- * or GCL_TUNE_LOOP64=0 for A/Bs) */
+/* bursts of <= 64 packets (@k64): rxloop64_kernel, a poller wave and the
+ * writer, no barrier; else the general loop (bursts past 64, or
+ * GCL_TUNE_LOOP64=0: the tests' way to run short bursts through it) */
 template <int MODE>
-static hipError_t loop_launch(const LoopParams &lp, int np, hipStream_t s)
+static hipError_t loop_launch(const LoopParams &lp, bool k64, hipStream_t s)
 {
-	const void *fn = np == 2 ? (const void *)rxloop64_kernel<MODE, 2>
-	               : np == 1 ? (const void *)rxloop64_kernel<MODE, 1> : (const void *)rxloop_kernel<MODE>;
-	const uint32_t lds = np ? loop64_lds(np, lp.lds_copy)
-	                        : kLoopFixedLds + ((lp.max_rt + 3) & ~3u) * 4 + kLdsTableBudget;
+	const void *fn = k64 ? (const void *)rxloop64_kernel<MODE> : (const void *)rxloop_kernel<MODE>;
+	const uint32_t lds = k64 ? loop64_lds(64 + kLdsTableBudget)
+	                         : kLoopFixedLds + ((lp.max_rt + 3) & ~3u) * 4 + kLdsTableBudget;
 	if (lds > 64 * 1024) {
 		const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
 		                                         160 * 1024);
 		if (e != hipSuccess)
 			return e;
 	}
-	if (np == 2)
-		hipLaunchKernelGGL((rxloop64_kernel<MODE, 2>), dim3(lp.workers), dim3(192), lds, s, lp);
-	else if (np == 1)
-		hipLaunchKernelGGL((rxloop64_kernel<MODE, 1>), dim3(lp.workers), dim3(128), lds, s, lp);
+	if (k64)
+		hipLaunchKernelGGL(rxloop64_kernel<MODE>, dim3(lp.workers), dim3(128), lds, s, lp);
 	else
 		hipLaunchKernelGGL(rxloop_kernel<MODE>, dim3(lp.workers), dim3(256), lds, s, lp);
 	return hipGetLastError();
@@ -3919,22 +3720,9 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 	lp.rec_plane = (uint32_t)(16 * mb);
 	lp.spec = (!lp.off_hdr || lp.hdr_rec) && cfg->max_burst <= 64;
 	lp.spec_ticks = kLoopSpecTicks;
-	/* rxloop64_kernel: NP poll-and-classify waves; NP 2 holds two table
-	 * copies in LDS, so only where two fit */
 	L->k64 = cfg->max_burst <= 64;
-	if (const char *e = getenv("GCL_TUNE_LOOP64")) /* 0: the general loop, for A/Bs */
+	if (const char *e = getenv("GCL_TUNE_LOOP64")) /* 0: tests, the general loop */
 		L->k64 = L->k64 && atoi(e) != 0;
-	L->np = kDefaultLoopPollers;
-	if (const char *e = getenv("GCL_TUNE_LOOP_POLLERS"))
-		L->np = atoi(e) == 2 ? 2 : 1;
-	lp.lds_copy = 64 + kLdsTableBudget;
-	if (L->np == 2) {
-		lp.lds_copy = align16(64 + std::min(c->image_cap, kLdsTableBudget));
-		if (loop64_lds(2, lp.lds_copy) > 160 * 1024) {
-			L->np = 1;
-			lp.lds_copy = 64 + kLdsTableBudget;
-		}
-	}
 	if (const char *e = getenv("GCL_TUNE_LOOP_SPEC")) /* experiments: ticks of 10 ns */
 		lp.spec_ticks = (uint32_t)atoi(e);
 	{
@@ -3989,10 +3777,9 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 	if (hipStreamCreateWithFlags(&L->st, hipStreamNonBlocking) != hipSuccess)
 		goto fail;
 	{
-		const int np = L->k64 ? L->np : 0;
-		hipError_t e = c->cfg.hash_mode == GCL_HASH_NIC ? loop_launch<GCL_HASH_NIC>(lp, np, L->st)
-		             : c->cfg.hash_mode == GCL_HASH_JENKINS ? loop_launch<GCL_HASH_JENKINS>(lp, np, L->st)
-		             : loop_launch<GCL_HASH_TOEPLITZ>(lp, np, L->st);
+		hipError_t e = c->cfg.hash_mode == GCL_HASH_NIC ? loop_launch<GCL_HASH_NIC>(lp, L->k64, L->st)
+		             : c->cfg.hash_mode == GCL_HASH_JENKINS ? loop_launch<GCL_HASH_JENKINS>(lp, L->k64, L->st)
+		             : loop_launch<GCL_HASH_TOEPLITZ>(lp, L->k64, L->st);
 		if (e != hipSuccess) {
 			(void)hipStreamDestroy(L->st);
 			L->st = nullptr;

@@ -305,20 +305,17 @@ def test_gpu_dense_verdict1(g, orc, wl, R, T):
     assert (c == ce).all() and (st == se).all()
 
 
-DENSE_FORMS = {0: "tile kernel", 1: "pair DENSE deferred nt", 2: "pair DENSE deferred plain",
-               3: "pair DENSE per-packet"}
+DEFER_FORMS = {0: "per-packet stores", 1: "deferred (<= 2 writes per block)", 2: "deferred always"}
 
 
-@pytest.mark.parametrize("dense", sorted(DENSE_FORMS))
+@pytest.mark.parametrize("defer", sorted(DEFER_FORMS))
 @pytest.mark.parametrize("wl,R,T,vb", [(0, 16, 8, 1), (0, 16, 8, 2), (1, 1024, 4, 2)])
-def test_gpu_dense_narrow_verdicts(g, orc, wl, R, T, vb, dense, monkeypatch):
-    """Dense slots' 1- and 2-B verdicts on every dense form (GCL_TUNE_DENSE):
-    the LDS-tile kernel's write-through byte and short stores, and
-    classify_pair_kernel<DENSE> with the verdicts kept in LDS and written
-    after the block's tiles (streaming or plain loads) or per packet; the
-    partial last tile included; 256- (udp64) and 512-lane (1024-runtime
-    tcp1500) blocks."""
-    monkeypatch.setenv("GCL_TUNE_DENSE", str(dense))
+def test_gpu_dense_narrow_verdicts(g, orc, wl, R, T, vb, defer, monkeypatch):
+    """Dense slots' 1- and 2-B verdicts in every form (GCL_TUNE_DEFER): the
+    tile kernel's write-through byte and short stores per packet, or kept in
+    LDS and written 16 B per lane in batches; the partial last tile
+    included; 256- (udp64) and 512-lane (1024-runtime tcp1500) blocks."""
+    monkeypatch.setenv("GCL_TUNE_DEFER", str(defer))
     stride = {0: 64, 1: 1536}[wl]
     n = 40000 + 77
     df = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
@@ -338,20 +335,23 @@ def test_gpu_dense_narrow_verdicts(g, orc, wl, R, T, vb, dense, monkeypatch):
     v, c, st = gpu_run(g, clf, frames, n, stride)
     ve, ce, se = t.classify(frames, n, stride)
     w = to_verdict1(ve, [T] * R, tb) if vb == 1 else to_verdict2(ve, [T] * R, tb)
-    assert_same(v, w, f"narrow verdicts wl={wl} vb={vb} {DENSE_FORMS[dense]}")
+    assert_same(v, w, f"narrow verdicts wl={wl} vb={vb} {DEFER_FORMS[defer]}")
     assert (c == ce).all() and (st == se).all()
 
 
-@pytest.mark.parametrize("dense,env", [(1, {}), (1, {"GCL_TUNE_GRID": "3"}), (2, {"GCL_TUNE_GRID": "5"}),
-                                       (1, {"GCL_TUNE_BLOCKS_PER_CU": "1", "GCL_TUNE_GRID": "301"})])
+@pytest.mark.parametrize("defer,env", [
+    (1, {}), (2, {"GCL_TUNE_GRID": "3"}), (2, {"GCL_TUNE_GRID": "5", "GCL_TUNE_DEPTH": "1"}),
+    (1, {"GCL_TUNE_BLOCKS_PER_CU": "1", "GCL_TUNE_GRID": "301"}),
+    (2, {"GCL_TUNE_THREADS": "512", "GCL_TUNE_GRID": "7"}), (2, {"GCL_TUNE_THREADS": "1024", "GCL_TUNE_GRID": "7"})])
 @pytest.mark.parametrize("vb", [1, 2])
-def test_gpu_dense_deferred_flushes(g, orc, vb, dense, env, monkeypatch):
-    """classify_pair_kernel<DENSE>'s LDS verdict buffer when a block walks
-    more tiles than it holds (few blocks: GCL_TUNE_GRID): full buffers
-    flushed inside the loop, a partial one at the end, the batch's ragged
-    last tile cut at n -- against the oracle on a 1 Mi + 77-packet udp64
-    batch, with its counts and counters."""
-    for kk, vv in {"GCL_TUNE_DENSE": str(dense), **env}.items():
+def test_gpu_dense_deferred_flushes(g, orc, vb, defer, env, monkeypatch):
+    """The tile kernel's LDS verdict buffer when a block walks more tiles
+    than it holds (few blocks: GCL_TUNE_GRID, GCL_TUNE_DEFER=2): full
+    buffers written inside the loop, a partial one at the end, the batch's
+    ragged last tile cut at n; DEPTH 1 and 2; 256-, 512- and 1024-lane
+    tiles -- against the oracle on a 1 Mi + 77-packet udp64 batch, with its
+    counts and counters."""
+    for kk, vv in {"GCL_TUNE_DEFER": str(defer), **env}.items():
         monkeypatch.setenv(kk, vv)
     R, T, stride = 16, 8, 64
     n = (1 << 20) + 77
@@ -376,7 +376,7 @@ def test_gpu_dense_deferred_flushes(g, orc, vb, dense, env, monkeypatch):
     got = got[:n * vb].view(np.uint8 if vb == 1 else np.uint16)
     ve, ce, se = t.classify(frames, n, stride)
     w = to_verdict1(ve, [T] * R, tb) if vb == 1 else to_verdict2(ve, [T] * R, tb)
-    assert_same(got, w, f"deferred flushes vb={vb} dense={dense} {env}")
+    assert_same(got, w, f"deferred flushes vb={vb} defer={defer} {env}")
     assert (c.cpu().numpy().astype(np.uint64) == ce).all()
     assert (st.cpu().numpy().astype(np.uint64) == se).all()
 

@@ -51,13 +51,11 @@ LOOP_CASES = [(m, vb, 0, 0) for m in (0, 1, 2) for vb in (8, 4, 2)] + \
     [(m, 1, 0, i) for m in (0, 2) for i in (0, 1, 2)] + [(0, 1, 1, 2), (2, 1, 2, 0)]
 
 
-@pytest.mark.parametrize("k64", [1, 2, 0])
+@pytest.mark.parametrize("k64", [1, 0])
 @pytest.mark.parametrize("mode,vb,flags,inline", LOOP_CASES)
 def test_rxloop_fuzz_vs_oracle(g, orc, mode, vb, flags, inline, k64, monkeypatch):
     """k64: bursts of <= 64 through rxloop64_kernel (the default for
-    max_burst <= 64) with one poll-and-classify wave (1) or two (2,
-    GCL_TUNE_LOOP_POLLERS=2), or through the general loop kernel
-    (GCL_TUNE_LOOP64=0);
+    max_burst <= 64), or through the general loop kernel (GCL_TUNE_LOOP64=0);
     vb: verdict bytes (8 gcl_verdict, 4 VERDICT4, 2 VERDICT2, 1 VERDICT1 with
     16 runtimes x up to 8 kthreads);
     flags: 0 plain, 1 Azure ARP mode (GCL_CFG_AZURE_ARP), 2 16-bit hash;
@@ -87,7 +85,6 @@ def test_rxloop_fuzz_vs_oracle(g, orc, mode, vb, flags, inline, k64, monkeypatch
     if early:
         monkeypatch.setenv("GCL_TUNE_LOOP_SPEC", "500000")
     monkeypatch.setenv("GCL_TUNE_LOOP64", "1" if k64 else "0")
-    monkeypatch.setenv("GCL_TUNE_LOOP_POLLERS", "2" if k64 == 2 else "1")
     loop = clf.rxloop(frames, slots=8, counts=cnt, stats=st, region_len=flen,
                       flags=LOOP_FLAGS[inline](g))
     try:
@@ -129,9 +126,8 @@ def test_rxloop_fuzz_vs_oracle(g, orc, mode, vb, flags, inline, k64, monkeypatch
 LEAN_CASES = [(m, vb, fl, lf) for m in (0, 1, 2) for vb in (8, 4, 2, 1) for fl, lf in ((0, 2), (2, 0))]
 
 
-@pytest.mark.parametrize("pollers", [1, 2])
 @pytest.mark.parametrize("mode,vb,flags,lflag", LEAN_CASES)
-def test_rxloop_lean_path(g, orc, mode, vb, flags, lflag, pollers, monkeypatch):
+def test_rxloop_lean_path(g, orc, mode, vb, flags, lflag, monkeypatch):
     """rxloop64_kernel's lean path (classify_lean) against the oracle: bursts
     of plain IPv4 (every packet Ethertype IPv4, IHL 5, no FDIR mark) take it,
     bursts with one FDIR-marked packet, or with dst_ip hints, take
@@ -170,7 +166,6 @@ def test_rxloop_lean_path(g, orc, mode, vb, flags, lflag, pollers, monkeypatch):
     cnt = torch.zeros(max_rt, dtype=torch.int64, device="cuda")
     st = torch.zeros(g.NR_STATS, dtype=torch.int64, device="cuda")
     monkeypatch.setenv("GCL_TUNE_LOOP_SPEC", "500000")
-    monkeypatch.setenv("GCL_TUNE_LOOP_POLLERS", str(pollers))
     loop = clf.rxloop(frames, slots=8, counts=cnt, stats=st, flags=LOOP_FLAGS[lflag](g))
     try:
         got = []
@@ -285,11 +280,10 @@ def test_rxloop_workers_pipelined_and_full_ring(g, orc):
         g.host_unregister(frames)
 
 
-@pytest.mark.parametrize("pollers", [1, 2])
 @pytest.mark.parametrize("max_burst,workers,lflag", [(64, 1, 0), (64, 3, 0), (256, 2, 0),
                                                      (64, 1, 2), (64, 3, 2), (256, 2, 2),
                                                      (1024, 2, 0), (1024, 2, 2)])
-def test_rxloop_stamped_offsets_ragged_bursts(g, orc, max_burst, workers, lflag, pollers, monkeypatch):
+def test_rxloop_stamped_offsets_ragged_bursts(g, orc, max_burst, workers, lflag, monkeypatch):
     """Offsets ride in the slot stamped with the slot's use count, and a
     worker polling a burst of <= 64 takes them with the poll when every stamp
     is current (lflag 2: whole header records, GCL_LOOP_HDR_RECORDS, each
@@ -298,8 +292,6 @@ def test_rxloop_stamped_offsets_ragged_bursts(g, orc, max_burst, workers, lflag,
     1..max_burst so stale entries of longer bursts sit behind shorter ones,
     and offsets at and past 2^40 (the stamp's bit) that read as frames past
     the region."""
-    if max_burst > 64 and pollers == 2:  # before anything is registered
-        pytest.skip("the poll-and-classify waves are rxloop64_kernel's")
     rng = np.random.default_rng(7300 + max_burst + workers + 17 * lflag)
     max_rt = 16
     rts = random_runtimes(rng, max_rt, 12)
@@ -320,7 +312,6 @@ def test_rxloop_stamped_offsets_ragged_bursts(g, orc, max_burst, workers, lflag,
     # bursts: widen it (GCL_TUNE_LOOP_SPEC, 10-ns ticks) so that the bursts
     # really arrive with the poll here, as they do from a C dataplane loop
     monkeypatch.setenv("GCL_TUNE_LOOP_SPEC", "500000")
-    monkeypatch.setenv("GCL_TUNE_LOOP_POLLERS", str(pollers))
     loop = clf.rxloop(frames, slots=2, workers=workers, max_burst=max_burst, region_len=flen,
                       flags=LOOP_FLAGS[lflag](g))
     try:
@@ -350,14 +341,10 @@ def test_rxloop_stamped_offsets_ragged_bursts(g, orc, max_burst, workers, lflag,
         g.host_unregister(frames)
 
 
-@pytest.mark.parametrize("cfg,pollers", [(("200000", "1", "2", "1"), 1), (("400000", "4", "4", "4"), 1),
-                                         (("400000", "32", "64", "64"), 1),
-                                         (("200000", "1", "2", "1", "records"), 1),
-                                         (("400000", "4", "4", "4", "records"), 1),
-                                         (("400000", "32", "64", "64", "records"), 1),
-                                         (("200000", "1", "2", "1"), 2),
-                                         (("400000", "4", "4", "4", "records"), 2)])
-def test_rxloop_soak_stamped_offsets(g, cfg, pollers):
+@pytest.mark.parametrize("cfg", [("200000", "1", "2", "1"), ("400000", "4", "4", "4"), ("400000", "32", "64", "64"),
+                                 ("200000", "1", "2", "1", "records"), ("400000", "4", "4", "4", "records"),
+                                 ("400000", "32", "64", "64", "records")])
+def test_rxloop_soak_stamped_offsets(g, cfg):
     """tools/loopsoak: random 1..64-packet bursts at random offsets into a
     mixed-traffic region, few slots, a tight host loop with random pauses
     racing the workers' polls; every verdict equal to the batch kernel's for
@@ -368,8 +355,7 @@ def test_rxloop_soak_stamped_offsets(g, cfg, pollers):
     exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "loopsoak")
     if not os.access(exe, os.X_OK):
         pytest.fail("tools/loopsoak not built (python -c 'import __graft_entry__ as g; g.build()')")
-    env = dict(os.environ, GCL_TUNE_LOOP_POLLERS=str(pollers))
-    r = subprocess.run([exe, *cfg], capture_output=True, text=True, timeout=100, env=env)
+    r = subprocess.run([exe, *cfg], capture_output=True, text=True, timeout=100)
     assert r.returncode == 0, (r.stdout[-300:], r.stderr[-300:])
     out = json.loads(r.stdout.strip().splitlines()[-1])
     assert out["mismatches"] == 0 and out["packets_checked"] > int(cfg[0]) * 30
@@ -460,10 +446,9 @@ def test_rxloop_transport_hashes(g, orc, mode, vb, lflag, monkeypatch):
     assert not len(bad), f"{len(bad)} transport hashes differ, first {bad[0]}: {gt[bad[0]]} vs {te[bad[0]]}"
 
 
-@pytest.mark.parametrize("pollers", [1, 2])
 @pytest.mark.parametrize("lflag,spec,use0", [(0, "0", (1 << 23) - 150), (0, "500000", (1 << 23) - 150),
                                              (2, "500000", (1 << 31) - 150), (2, "0", (1 << 31) - 150)])
-def test_rxloop_stamp_wrap(g, orc, lflag, spec, use0, pollers, monkeypatch):
+def test_rxloop_stamp_wrap(g, orc, lflag, spec, use0, monkeypatch):
     """The slots' use count crossing the stamps' wrap (2^23 for stamped
     offsets, 2^31 for header records) with the loop started near it
     (GCL_TUNE_LOOP_T0): stamps are never 0, so a zeroed or never-loaded
@@ -484,7 +469,6 @@ def test_rxloop_stamp_wrap(g, orc, lflag, spec, use0, pollers, monkeypatch):
     slots = 2
     monkeypatch.setenv("GCL_TUNE_LOOP_SPEC", spec)
     monkeypatch.setenv("GCL_TUNE_LOOP_T0", str(slots * use0))
-    monkeypatch.setenv("GCL_TUNE_LOOP_POLLERS", str(pollers))
     loop = clf.rxloop(frames, slots=slots, workers=1, region_len=flen, flags=LOOP_FLAGS[lflag](g))
     try:
         nb = 600  # 300 uses of each slot: across the wrap

@@ -1,12 +1,11 @@
-"""A/B of the dense-slot kernels on the bench's own placed buffers, in one
-process: the LDS-tile classify_kernel (GCL_TUNE_DENSE=0) against
-classify_pair_kernel<DENSE> with the verdicts kept in LDS and written after
-the block's tiles (1: streaming loads, 2: plain loads) or stored per packet
-(3).  One context per form over the same frames and verdict ring, launches
-interleaved round by round; every form's verdicts and counts are checked
-against form 0's.
+"""A/B of the dense tile kernel's verdict writes on the bench's own placed
+buffers, in one process: stored per packet (GCL_TUNE_DEFER=0) against kept
+in LDS and written 16 B per lane in at most two batches per block (1), or
+in as many batches as the LDS left over takes (2).  One context per form
+over the same frames and verdict ring, launches interleaved round by round;
+every form's verdicts and counts are checked against form 0's.
 
-    python tools/dense_ab.py [workload ...]     (default: udp64 tcp1500)
+    python tools/defer_ab.py [workload ...]     (default: udp64 tcp1500)
 One JSON line per (workload, round, form).
 """
 import json
@@ -20,8 +19,7 @@ import torch  # noqa: E402
 
 import bench  # noqa: E402
 
-FORMS = {0: "tile kernel", 1: "pair DENSE, deferred verdicts, nt loads",
-         2: "pair DENSE, deferred verdicts, plain loads", 3: "pair DENSE, per-packet stores, nt loads"}
+FORMS = {0: "per-packet stores", 1: "deferred, <= 2 writes per block", 2: "deferred always"}
 
 
 def main():
@@ -31,10 +29,10 @@ def main():
         w = bench.Workload(name, 0, 1, dev)
         clfs = {}
         for f in FORMS:
-            os.environ["GCL_TUNE_DENSE"] = str(f)
+            os.environ["GCL_TUNE_DEFER"] = str(f)
             clfs[f] = bench.classifier(dev, w.R, w.T, w.vbytes)
             bench.setup_tables(clfs[f], w.R, w.T)
-        os.environ.pop("GCL_TUNE_DENSE", None)
+        os.environ.pop("GCL_TUNE_DEFER", None)
         st = torch.cuda.current_stream().cuda_stream
         ref = None
         for f, clf in clfs.items():  # correctness: same verdicts and counts as form 0
