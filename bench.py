@@ -1393,17 +1393,21 @@ def cpu_stream(name, n, budget_s, native, threads):
         kw = dict(olflags=olf, rss=rss, pkt_len=pkt_len, direct=True)
         probe = t.bench(frames, n, stride, threads=1, passes=1, cpus=cpus[:1], **kw)
         budget = budget_s * 0.5 / CPU_REPS
-        p1 = max(1, int(budget * 0.4 / max(probe, 1e-6)))
-        pl = max(1, int(budget * 0.35 / max(probe * 1.3, 1e-6)))
-        pm = max(1, int(budget * 0.25 / max(probe / len(cpus), 1e-6)))
+        p1 = max(1, int(budget * 0.35 / max(probe, 1e-6)))
+        pl = max(1, int(budget * 0.3 / max(probe * 1.3, 1e-6)))
+        pm = max(1, int(budget * 0.35 / max(probe / len(cpus), 1e-6)))
         r1, rl, rm = [], [], []
         # the three cells interleaved, CPU_REPS rounds: a drift of the host
-        # hits every cell alike
+        # hits every cell alike.  Every thread runs one untimed pass on its own
+        # core first (orc.c bench_thread), so no cell starts with the
+        # sample's lines in another CCD's L3 or its rings untouched: the
+        # cold first pass made 1-core classify read slower than classify +
+        # lrpc_send on the mixed stream (gpurun_out/r05a_bench_detail.json)
         for _ in range(CPU_REPS):
             s1 = t.bench(frames, n, stride, threads=1, passes=p1, cpus=cpus[:1], **kw)
             sl = t.bench(frames, n, stride, threads=1, passes=pl, lrpc=True, cpus=cpus[:1], **kw)
             sm = t.bench(frames, n, stride, threads=len(cpus), passes=pm, cpus=cpus, **kw)
-            spent += s1 + sl + sm
+            spent += (s1 * (p1 + 1) / p1 + sl * (pl + 1) / pl + sm * (pm + 1) / pm)
             r1.append(round(n * p1 / s1 / 1e6, 2))
             rl.append(round(n * pl / sl / 1e6, 2))
             rm.append(round(n * pm / sm / 1e6, 2))
@@ -1418,7 +1422,7 @@ def cpu_stream(name, n, budget_s, native, threads):
     return res
 
 
-def cpu_baseline(budget_s=24.0):
+def cpu_baseline(budget_s=30.0):
     """The CPU baseline beside every timed stream: `value` is one core's
     classify-only rate on the udp64 stream in NIC mode (the reference's own
     per-packet work, one dataplane core, dpdk.c:276-280); `streams` holds the
@@ -1566,7 +1570,7 @@ def main():
     ap.add_argument("--group-node-force", action="store_true",
                     help="run the all-GPU group line even with one GPU visible")
     ap.add_argument("--group-child", type=int, default=0, help=argparse.SUPPRESS)
-    ap.add_argument("--cpu-budget", type=float, default=24.0)
+    ap.add_argument("--cpu-budget", type=float, default=30.0)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo only to rehearse N>1 on one GPU")
     ap.add_argument("--allow-shared-gpu", action="store_true",
