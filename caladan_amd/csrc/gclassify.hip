@@ -103,7 +103,12 @@ struct KParams {
 	uint32_t off_seed, off_crc;
 	uint32_t vcap;   /* classify_kernel, 1-/2-B verdicts: tiles of verdicts its LDS buffer
 	                    holds (0: every verdict stored as it is made) */
+	uint32_t vregs;  /* with vcap: tiles past a full LDS buffer held in registers */
 };
+
+/* classify_kernel's verdict registers: kVregs dwords per lane, so 4 * kVregs
+ * tiles of 1-B verdicts (2 * kVregs of 2-B ones) past a full LDS buffer */
+constexpr int kVregs = 10;
 
 /* ------------------------------------------------------------------------
  * Header tile: 256 packets x 64 B, 16-B chunks XOR-swizzled so that both the
@@ -691,31 +696,52 @@ classify_kernel(KParams k)
 	uint64_t t = blockIdx.x;
 	const uint64_t step = gridDim.x, t_end = k.ntiles;
 	/* k.vcap (1-/2-B verdicts): each tile's verdicts kept in LDS after the
-	 * tables, and written out 16 B per lane once vcap tiles are in and after
-	 * the last tile, so the verdict stream does not interleave with the frame
-	 * reads (tools/wdefer.hip) */
+	 * tables -- and with k.vregs, once vcap tiles are in, the next ones in a
+	 * shift register of kVregs dwords per lane -- and written out when both
+	 * are full and after the last tile, so the verdict stream does not
+	 * interleave with the frame reads (tools/wdefer.hip) */
 	const uint32_t vb = (k.cflags & GCL_CFG_VERDICT1) ? 1 : 2;
+	const uint32_t rcap = k.vregs ? kVregs * 4 / vb : 0; /* tiles the registers hold */
 	uint8_t *vbuf = lds_tab + ((k.tables_lds_bytes + 15) & ~15u);
-	uint32_t kl = 0, kf = 0; /* tiles in the buffer; tiles written before them (uniform) */
-	auto verdict = [&](uint64_t i, uint64_t w) {
+	/* uniform: kl tiles in the buffer, local tiles [kf, kf + kl); nreg in
+	 * the registers, local tiles [kf + vcap, kf + vcap + nreg) */
+	uint32_t kl = 0, kf = 0, nreg = 0;
+	uint32_t vr[kVregs];
+#pragma unroll
+	for (int i = 0; i < kVregs; i++)
+		vr[i] = 0;
+	/* every lane, live or not, so each lane's register chain stays aligned */
+	auto verdict = [&](uint64_t i, bool live, uint64_t w) {
 		if (!k.vcap) {
-			put_verdict(k, i, w);
-		} else {
+			if (live)
+				put_verdict(k, i, w);
+		} else if (kl < k.vcap) {
 			uint8_t *d = vbuf + (kl * NT + tid) * vb;
 			if (vb == 1)
 				*d = (uint8_t)w;
 			else
 				*(uint16_t *)d = (uint16_t)w;
+		} else {
+			const uint32_t sh = 8 * vb;
+#pragma unroll
+			for (int r = kVregs - 1; r > 0; r--)
+				vr[r] = (vr[r] << sh) | (vr[r - 1] >> (32 - sh));
+			vr[0] = (vr[0] << sh) | ((uint32_t)w & ((1u << sh) - 1));
 		}
 	};
-	/* after a classified tile (and its barrier): count it, write a full buffer */
-	auto flush = [&]() {
+	const uint64_t nb = k.n * vb;
+	/* the global byte offset of local tile @j's first verdict */
+	auto tile_off = [&](uint32_t j) -> uint64_t {
+		return ((uint64_t)blockIdx.x + (uint64_t)j * step) * NT * vb;
+	};
+	/* the buffer to its places, 16 B per lane, write-through like the
+	 * per-packet stores; the batch's last tile up to n only */
+	auto flush_lds = [&]() {
 		const uint32_t cs = vb == 1 ? __builtin_ctz(NT / 16) : __builtin_ctz(NT / 8); /* log2 chunks per tile */
-		const uint64_t nb = k.n * vb;
 		const __amdgpu_buffer_rsrc_t vrs = gcl::host_rsrc(k.verdicts, nb);
 		for (uint32_t i = tid; i < kl << cs; i += NT) {
 			const uint32_t j = i >> cs, c = i & ((1u << cs) - 1);
-			const uint64_t o = ((uint64_t)blockIdx.x + (uint64_t)(kf + j) * step) * NT * vb + 16 * c;
+			const uint64_t o = tile_off(kf + j) + 16 * c;
 			const uint8_t *src = vbuf + j * NT * vb + 16 * c;
 			if (o + 16 <= nb) {
 				const uint4 v = *(const uint4 *)src;
@@ -726,12 +752,40 @@ classify_kernel(KParams k)
 					store_wt((uint8_t *)k.verdicts + o + b, src[b]);
 			}
 		}
-		kf += kl;
-		kl = 0;
 	};
+	/* the registers, newest tile first: each lane its own packet's verdict */
+	auto flush_regs = [&]() {
+		const uint32_t sh = 8 * vb;
+		for (uint32_t q = 0; q < nreg; q++) {
+			const uint64_t o = tile_off(kf + k.vcap + nreg - 1 - q) + (uint64_t)tid * vb;
+			if (o < nb) {
+				if (vb == 1)
+					store_wt((uint8_t *)k.verdicts + o, (uint8_t)vr[0]);
+				else
+					store_wt((uint16_t *)((uint8_t *)k.verdicts + o), (uint16_t)vr[0]);
+			}
+#pragma unroll
+			for (int r = 0; r < kVregs - 1; r++)
+				vr[r] = (vr[r] >> sh) | (vr[r + 1] << (32 - sh));
+			vr[kVregs - 1] >>= sh;
+		}
+	};
+	/* after a classified tile and its barrier (the buffer complete): count
+	 * it; both full -> write them out (the next writes to vbuf follow the
+	 * next stage's barrier) */
 	auto tile_done = [&](uint64_t tt) {
-		if (k.vcap && tt < t_end && ++kl == k.vcap)
-			flush(); /* the next writes to vbuf follow the next stage's barrier */
+		if (!k.vcap || tt >= t_end)
+			return;
+		if (kl < k.vcap)
+			kl++;
+		else
+			nreg++;
+		if (kl == k.vcap && nreg == rcap) {
+			flush_lds();
+			flush_regs();
+			kf += kl + nreg;
+			kl = nreg = 0;
+		}
 	};
 	if (t < t_end)
 		load_tile<NT>(k, t, true, ra);
@@ -750,8 +804,11 @@ classify_kernel(KParams k)
 		const uint64_t nxt = t + DEPTH * step;
 		/* in flight while parsing */
 		load_tile<NT>(k, nxt, nxt < t_end, ra);
-		if (t * NT + tid < k.n)
-			verdict(t * NT + tid, classify_one<MODE, false>(k, tile, tid, t * NT + tid, tb, hist, cnt));
+		{
+			const bool live = t * NT + tid < k.n;
+			const uint64_t w = live ? classify_one<MODE, false>(k, tile, tid, t * NT + tid, tb, hist, cnt) : 0;
+			verdict(t * NT + tid, live, w);
+		}
 		__syncthreads();
 		tile_done(t);
 		t += step;
@@ -763,15 +820,21 @@ classify_kernel(KParams k)
 			stage_tile<NT>(tile, rb);
 			__syncthreads();
 			load_tile<NT>(k, t + 2 * step, t + 2 * step < t_end, rb);
-			if (t < t_end && t * NT + tid < k.n)
-				verdict(t * NT + tid, classify_one<MODE, false>(k, tile, tid, t * NT + tid, tb, hist, cnt));
+			{
+				const bool live = t < t_end && t * NT + tid < k.n;
+				const uint64_t w =
+				        live ? classify_one<MODE, false>(k, tile, tid, t * NT + tid, tb, hist, cnt) : 0;
+				verdict(t * NT + tid, live, w);
+			}
 			__syncthreads();
 			tile_done(t);
 			t += step;
 		}
 	}
 	if (kl)
-		flush();
+		flush_lds();
+	if (nreg)
+		flush_regs();
 	flush_counters<NT>(k, hist, cnt);
 }
 
@@ -2281,7 +2344,7 @@ extern "C" int gcl_open(int hip_device, const struct gcl_cfg *cfg, struct gcl_ct
 		e = getenv("GCL_TUNE_BLOCKS_PER_CU");
 		c->tune_bpc = e ? atoi(e) : 0;
 		e = getenv("GCL_TUNE_DEFER");
-		c->tune_defer = e ? std::min(std::max(atoi(e), 0), 2) : kDefaultDefer;
+		c->tune_defer = e ? std::min(std::max(atoi(e), 0), 3) : kDefaultDefer;
 	}
 	c->dimg[0] = c->dimg[1] = nullptr;
 	for (int i = 0; i < 2; i++) {
@@ -2592,7 +2655,8 @@ struct Geometry {
 	int grid;     /* blocks per launch when > 0 (GCL_TUNE_GRID) */
 	bool pair;    /* classify_pair_kernel (GENERAL batches): [8, 40) per packet by lane pairs */
 	int defer;    /* classify_kernel with 1-/2-B verdicts kept in LDS and written in
-	                 batches: 1 where that takes <= 2 writes per block, 2 always (tests) */
+	                 batches: 1 where that takes <= 2 writes per block, 2 always (tests),
+	                 3 as 1 with kVregs registers per lane past a full buffer */
 };
 
 /* geo.defer: what the CU's LDS leaves the block at geo.bpc_cap blocks per
@@ -2603,6 +2667,7 @@ static hipError_t launch_nt(KParams k, bool tlds, uint32_t lds, int num_cus, con
                             hipStream_t s)
 {
 	k.vcap = 0;
+	k.vregs = 0;
 	if (geo.defer) {
 		const uint32_t vb = (k.cflags & GCL_CFG_VERDICT1) ? 1 : 2;
 		const uint32_t base = align16(lds);
@@ -2610,8 +2675,11 @@ static hipError_t launch_nt(KParams k, bool tlds, uint32_t lds, int num_cus, con
 		const uint64_t blocks = geo.grid > 0 ? (uint64_t)geo.grid : (uint64_t)num_cus * std::max(geo.bpc_cap, 1);
 		const uint64_t want = ((k.n + NT - 1) / NT + blocks - 1) / blocks;
 		const uint64_t room = per_cu > base ? (per_cu - base) / (NT * vb) : 0;
-		if (room && (2 * room >= want || geo.defer == 2)) {
+		/* 3: past a full buffer, kVregs registers per lane as well */
+		const uint64_t rcap = geo.defer == 3 ? kVregs * 4 / vb : 0;
+		if (room && (2 * (room + rcap) >= want || geo.defer == 2)) {
 			k.vcap = (uint32_t)std::min(want, room);
+			k.vregs = rcap && want > room;
 			lds = base + k.vcap * NT * vb;
 		}
 	}

@@ -1,7 +1,8 @@
 """A/B of the dense tile kernel's verdict writes on the bench's own placed
 buffers, in one process: stored per packet (GCL_TUNE_DEFER=0) against kept
 in LDS and written 16 B per lane in at most two batches per block (1), or
-in as many batches as the LDS left over takes (2).  One context per form
+in as many batches as the LDS left over takes (2), or with kVregs
+registers per lane holding the tiles past a full LDS buffer (3).  One context per form
 over the same frames and verdict ring, launches interleaved round by round;
 every form's verdicts and counts are checked against form 0's.
 
@@ -19,7 +20,8 @@ import torch  # noqa: E402
 
 import bench  # noqa: E402
 
-FORMS = {0: "per-packet stores", 1: "deferred, <= 2 writes per block", 2: "deferred always"}
+FORMS = {0: "per-packet stores", 1: "deferred, <= 2 writes per block", 2: "deferred always",
+         3: "deferred, LDS + registers"}
 
 
 def main():
@@ -48,7 +50,7 @@ def main():
                 ref = got
             ok = bool(torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1]))
             print(json.dumps({"workload": name, "form": f, "check": "ok" if ok else "MISMATCH"}), flush=True)
-        for rnd in range(3):
+        for rnd in range(int(os.environ.get("AB_ROUNDS", "3"))):
             for f, clf in clfs.items():
                 scratch = torch.zeros(w.R + bench.g.NR_STATS, dtype=torch.int64, device=dev)
 
