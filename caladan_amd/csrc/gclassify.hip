@@ -710,8 +710,10 @@ classify_kernel(KParams k)
 #pragma unroll
 	for (int i = 0; i < kVregs; i++)
 		vr[i] = 0;
-	/* every lane, live or not, so each lane's register chain stays aligned */
-	auto verdict = [&](uint64_t i, bool live, uint64_t w) {
+	/* every lane of every tile before t_end, live or not, so each lane's
+	 * register chain stays aligned with tile_done's count (the DEPTH-2
+	 * loop's empty tile past t_end is neither) */
+	auto verdict = [&](uint64_t i, bool real, bool live, uint64_t w) {
 		if (!k.vcap) {
 			if (live)
 				put_verdict(k, i, w);
@@ -721,7 +723,7 @@ classify_kernel(KParams k)
 				*d = (uint8_t)w;
 			else
 				*(uint16_t *)d = (uint16_t)w;
-		} else {
+		} else if (real) {
 			const uint32_t sh = 8 * vb;
 #pragma unroll
 			for (int r = kVregs - 1; r > 0; r--)
@@ -807,7 +809,7 @@ classify_kernel(KParams k)
 		{
 			const bool live = t * NT + tid < k.n;
 			const uint64_t w = live ? classify_one<MODE, false>(k, tile, tid, t * NT + tid, tb, hist, cnt) : 0;
-			verdict(t * NT + tid, live, w);
+			verdict(t * NT + tid, true, live, w);
 		}
 		__syncthreads();
 		tile_done(t);
@@ -824,7 +826,7 @@ classify_kernel(KParams k)
 				const bool live = t < t_end && t * NT + tid < k.n;
 				const uint64_t w =
 				        live ? classify_one<MODE, false>(k, tile, tid, t * NT + tid, tb, hist, cnt) : 0;
-				verdict(t * NT + tid, live, w);
+				verdict(t * NT + tid, t < t_end, live, w);
 			}
 			__syncthreads();
 			tile_done(t);
@@ -1072,8 +1074,9 @@ constexpr uint64_t kLoopRefresh = 256;
 /* s_memrealtime ticks (100 MHz) a wait polls the offsets with the word: a
  * burst that arrives later costs the offsets' round trip after the word */
 constexpr uint64_t kLoopSpecTicks = 400;
-/* GCL_TUNE_DEFER default (Geometry::defer) */
-constexpr int kDefaultDefer = 0;
+/* GCL_TUNE_DEFER default (Geometry::defer): udp64 328.2-329.1 -> 323.4-324.2
+ * us, three fresh processes (profiles/r05_defer_ab.jsonl) */
+constexpr int kDefaultDefer = 1;
 /* GCL_TUNE_LOOP_LEAN default: bursts whose every packet is plain IPv4 (IHL 5,
  * no FDIR mark, no hint) classified by classify_lean */
 constexpr uint32_t kDefaultLoopLean = 1;
@@ -2344,7 +2347,7 @@ extern "C" int gcl_open(int hip_device, const struct gcl_cfg *cfg, struct gcl_ct
 		e = getenv("GCL_TUNE_BLOCKS_PER_CU");
 		c->tune_bpc = e ? atoi(e) : 0;
 		e = getenv("GCL_TUNE_DEFER");
-		c->tune_defer = e ? std::min(std::max(atoi(e), 0), 3) : kDefaultDefer;
+		c->tune_defer = e ? std::min(std::max(atoi(e), 0), 2) : kDefaultDefer;
 	}
 	c->dimg[0] = c->dimg[1] = nullptr;
 	for (int i = 0; i < 2; i++) {
@@ -2654,9 +2657,9 @@ struct Geometry {
 	int bpc_cap;  /* blocks per CU */
 	int grid;     /* blocks per launch when > 0 (GCL_TUNE_GRID) */
 	bool pair;    /* classify_pair_kernel (GENERAL batches): [8, 40) per packet by lane pairs */
-	int defer;    /* classify_kernel with 1-/2-B verdicts kept in LDS and written in
-	                 batches: 1 where that takes <= 2 writes per block, 2 always (tests),
-	                 3 as 1 with kVregs registers per lane past a full buffer */
+	int defer;    /* classify_kernel with 1-/2-B verdicts kept in LDS (and past a full
+	                 buffer in kVregs registers per lane) and written in batches: 1 where
+	                 that takes <= 2 writes per block, 2 always (tests) */
 };
 
 /* geo.defer: what the CU's LDS leaves the block at geo.bpc_cap blocks per
@@ -2675,8 +2678,7 @@ static hipError_t launch_nt(KParams k, bool tlds, uint32_t lds, int num_cus, con
 		const uint64_t blocks = geo.grid > 0 ? (uint64_t)geo.grid : (uint64_t)num_cus * std::max(geo.bpc_cap, 1);
 		const uint64_t want = ((k.n + NT - 1) / NT + blocks - 1) / blocks;
 		const uint64_t room = per_cu > base ? (per_cu - base) / (NT * vb) : 0;
-		/* 3: past a full buffer, kVregs registers per lane as well */
-		const uint64_t rcap = geo.defer == 3 ? kVregs * 4 / vb : 0;
+		const uint64_t rcap = kVregs * 4 / vb; /* tiles the registers hold past a full buffer */
 		if (room && (2 * (room + rcap) >= want || geo.defer == 2)) {
 			k.vcap = (uint32_t)std::min(want, room);
 			k.vregs = rcap && want > room;

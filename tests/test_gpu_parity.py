@@ -305,8 +305,7 @@ def test_gpu_dense_verdict1(g, orc, wl, R, T):
     assert (c == ce).all() and (st == se).all()
 
 
-DEFER_FORMS = {0: "per-packet stores", 1: "deferred (<= 2 writes per block)", 2: "deferred always",
-               3: "deferred, LDS + registers"}
+DEFER_FORMS = {0: "per-packet stores", 1: "deferred (<= 2 writes per block, the default)", 2: "deferred always"}
 
 
 @pytest.mark.parametrize("defer", sorted(DEFER_FORMS))
@@ -344,16 +343,16 @@ def test_gpu_dense_narrow_verdicts(g, orc, wl, R, T, vb, defer, monkeypatch):
     (1, {}), (2, {"GCL_TUNE_GRID": "3"}), (2, {"GCL_TUNE_GRID": "5", "GCL_TUNE_DEPTH": "1"}),
     (1, {"GCL_TUNE_BLOCKS_PER_CU": "1", "GCL_TUNE_GRID": "301"}),
     (2, {"GCL_TUNE_THREADS": "512", "GCL_TUNE_GRID": "7"}), (2, {"GCL_TUNE_THREADS": "1024", "GCL_TUNE_GRID": "7"}),
-    (3, {}), (3, {"GCL_TUNE_GRID": "20"}), (3, {"GCL_TUNE_GRID": "40"}), (3, {"GCL_TUNE_GRID": "70"}),
-    (3, {"GCL_TUNE_GRID": "20", "GCL_TUNE_DEPTH": "1"}), (3, {"GCL_TUNE_THREADS": "512", "GCL_TUNE_GRID": "12"})])
+    (1, {"GCL_TUNE_GRID": "20"}), (1, {"GCL_TUNE_GRID": "40"}), (1, {"GCL_TUNE_GRID": "70"}),
+    (1, {"GCL_TUNE_GRID": "20", "GCL_TUNE_DEPTH": "1"}), (1, {"GCL_TUNE_THREADS": "512", "GCL_TUNE_GRID": "12"})])
 @pytest.mark.parametrize("vb", [1, 2])
 def test_gpu_dense_deferred_flushes(g, orc, vb, defer, env, monkeypatch):
     """The tile kernel's LDS verdict buffer when a block walks more tiles
     than it holds (few blocks: GCL_TUNE_GRID, GCL_TUNE_DEFER=2): full
     buffers written inside the loop, a partial one at the end, the batch's
-    ragged last tile cut at n; with GCL_TUNE_DEFER=3 the registers past a
-    full buffer, partly filled, full and written out inside the loop (grid
-    20 / 12), or unused (grid 70 at 1-B verdicts); DEPTH 1 and 2; 256-, 512-
+    ragged last tile cut at n; the registers past a full buffer partly
+    filled (grid 40), full and written out inside the loop (grid 20 / 12),
+    or unused (grid 70 at 1-B verdicts); DEPTH 1 and 2; 256-, 512-
     and 1024-lane tiles -- against the oracle on a 1 Mi + 77-packet udp64
     batch, with its counts and counters."""
     for kk, vv in {"GCL_TUNE_DEFER": str(defer), **env}.items():

@@ -1,8 +1,9 @@
 """A/B of the dense tile kernel's verdict writes on the bench's own placed
 buffers, in one process: stored per packet (GCL_TUNE_DEFER=0) against kept
-in LDS and written 16 B per lane in at most two batches per block (1), or
-in as many batches as the LDS left over takes (2), or with kVregs
-registers per lane holding the tiles past a full LDS buffer (3).  One context per form
+in LDS (and past a full buffer in registers) and written in at most two
+batches per block (1, the default), or in as many as it takes (2).  Round
+5's A/B also had an LDS-only form, since folded into 1
+(profiles/r05_defer_ab.jsonl).  One context per form
 over the same frames and verdict ring, launches interleaved round by round;
 every form's verdicts and counts are checked against form 0's.
 
@@ -20,8 +21,7 @@ import torch  # noqa: E402
 
 import bench  # noqa: E402
 
-FORMS = {0: "per-packet stores", 1: "deferred, <= 2 writes per block", 2: "deferred always",
-         3: "deferred, LDS + registers"}
+FORMS = {0: "per-packet stores", 1: "deferred, <= 2 writes per block", 2: "deferred always"}
 
 
 def main():
@@ -30,7 +30,8 @@ def main():
     for name in wls:
         w = bench.Workload(name, 0, 1, dev)
         clfs = {}
-        for f in FORMS:
+        forms = [int(x) for x in os.environ.get("AB_FORMS", ",".join(map(str, FORMS))).split(",")]
+        for f in forms:
             os.environ["GCL_TUNE_DEFER"] = str(f)
             clfs[f] = bench.classifier(dev, w.R, w.T, w.vbytes)
             bench.setup_tables(clfs[f], w.R, w.T)
