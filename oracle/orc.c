@@ -729,10 +729,17 @@ static struct orc_lrpc *ring_of(struct lrpc_set *s, uint32_t p, uint32_t th)
 	return r;
 }
 
-static void classify_range_lrpc(const struct orc_tables *t, const struct gcl_batch *b,
-                                uint64_t lo, uint64_t hi, struct gcl_verdict *v,
-                                uint64_t *counts, uint64_t *stats,
-                                struct lrpc_set *rs, int direct, int send)
+/* rx_burst's loop with the post-pass of every delivered packet: @post 2
+ * rx_make_cmd + flow_tbl[slot] + lrpc_send (rx.c:76-92), 1 all but the ring
+ * write (ORC_BENCH_NOSEND), 0 none (the direct CPU baseline's classify-only
+ * cell).  Not inlined, so the classify-only and lrpc cells time one loop
+ * that differs only by @post: inlined separately, the two loops' code
+ * differed enough that on the mixed stream the one with the ring writes ran
+ * 3 % faster (gpurun_out/r05i_bench_detail.json) */
+__attribute__((noinline)) static void classify_range_lrpc(const struct orc_tables *t, const struct gcl_batch *b,
+                                                          uint64_t lo, uint64_t hi, struct gcl_verdict *v,
+                                                          uint64_t *counts, uint64_t *stats,
+                                                          struct lrpc_set *rs, int direct, int post)
 {
 	uint64_t sink = 0;
 	for (uint64_t s = lo; s < hi; s += GCL_RX_BURST_SIZE) {
@@ -751,7 +758,7 @@ static void classify_range_lrpc(const struct orc_tables *t, const struct gcl_bat
 				rx_one_pkt_direct(t, b, k, vk, counts, stats);
 			else
 				orc_rx_one_pkt(t, b, k, vk, counts, stats, NULL);
-			if ((vk->action & GCL_ACT_MASK) == GCL_ACT_DELIVER) {
+			if (post && (vk->action & GCL_ACT_MASK) == GCL_ACT_DELIVER) {
 				/* rx_make_cmd, rx.c:24-38 */
 				uint8_t fl = b->olflags ? b->olflags[k] : t->default_olflags;
 				uint64_t len = b->pkt_len ? b->pkt_len[k] : b->stride;
@@ -760,7 +767,7 @@ static void classify_range_lrpc(const struct orc_tables *t, const struct gcl_bat
 				uint64_t off = b->offs ? b->offs[k] : k * b->stride;
 				/* rx_send_to_runtime: flow_tbl[slot] at send time (rx.c:57) */
 				const uint32_t th = t->rt[vk->uniqid].flow_tbl[vk->thread];
-				if (!send) { /* ORC_BENCH_NOSEND: everything but the ring write */
+				if (post == 1) { /* ORC_BENCH_NOSEND: everything but the ring write */
 					sink += cmd ^ off ^ th;
 				} else if (!lrpc_send(ring_of(rs, vk->uniqid, th), cmd, off)) {
 					stats[GCL_RX_UNICAST_FAIL]++;
@@ -803,7 +810,7 @@ void orc_classify_lrpc(const struct orc_tables *t, const struct gcl_batch *b,
 {
 	struct lrpc_set rs;
 	lrpc_set_init(&rs, t);
-	classify_range_lrpc(t, b, 0, b->n, v, counts, stats, &rs, 0, 1);
+	classify_range_lrpc(t, b, 0, b->n, v, counts, stats, &rs, 0, 2);
 	lrpc_set_free(&rs, t);
 }
 
@@ -843,10 +850,9 @@ static void *bench_thread(void *arg)
 	for (int p = -1; p < a->passes; p++) {
 		if (p == 0)
 			pthread_barrier_wait(a->bar);
-		if (a->with_lrpc)
-			classify_range_lrpc(a->t, a->b, a->lo, a->hi, v, counts, stats, &rs, a->direct, a->send);
-		else if (a->direct)
-			classify_range_direct(a->t, a->b, a->lo, a->hi, v, counts, stats);
+		if (a->with_lrpc || a->direct)
+			classify_range_lrpc(a->t, a->b, a->lo, a->hi, v, counts, stats, &rs, a->direct,
+			                    a->with_lrpc ? (a->send ? 2 : 1) : 0);
 		else
 			classify_range(a->t, a->b, a->lo, a->hi, v, counts, stats, NULL);
 	}

@@ -144,7 +144,8 @@ def _full_result():
     cpu["pinning"] = "1-core cells on CPU 7, all-cores cells on 16 distinct physical cores"
     for m in ("nic_mode", "jenkins_mode"):
         cpu[m]["samples"] = {"1core": [60.0, 61.0, 62.0], "1core_lrpc": [50.0] * 3, "all_cores": [900.0] * 3}
-        cpu[m]["spread"] = 0.0328
+        cpu[m]["spread_1core"] = 0.0328
+        cpu[m]["spread_all_cores"] = 0.2406
     r["group_node"] = {"n_gpus": 8, "value": 800000.0, "ms_per_step": 0.33, "counts_check": "ok",
                        "what": "x" * 300, "host_ingress_c": {"rows": ["y" * 100] * 20}}
     return r
