@@ -1389,30 +1389,41 @@ def cpu_stream(name, n, budget_s, native, threads):
     # core and the next idlest ones for the all-cores cell
     cpus = pick_cores(threads)
     res["cpus"] = cpus
-    for mname, mode in (("nic_mode", g.HASH_NIC), ("jenkins_mode", g.HASH_JENKINS)):
+    modes = (("nic_mode", g.HASH_NIC), ("jenkins_mode", g.HASH_JENKINS))
+    kw = dict(olflags=olf, rss=rss, pkt_len=pkt_len, direct=True)
+    cells = {}
+    for mname, mode in modes:
         t = tables(mode)
-        kw = dict(olflags=olf, rss=rss, pkt_len=pkt_len, direct=True)
         probe = t.bench(frames, n, stride, threads=1, passes=1, cpus=cpus[:1], **kw)
-        budget = budget_s * 0.5 / CPU_REPS
-        p1 = max(1, int(budget * 0.35 / max(probe, 1e-6)))
-        pl = max(1, int(budget * 0.3 / max(probe * 1.3, 1e-6)))
-        pm = max(1, int(budget * 0.35 / max(probe / len(cpus), 1e-6)))
-        r1, rl, rm = [], [], []
-        # the three cells interleaved, CPU_REPS rounds: a drift of the host
-        # hits every cell alike.  Every thread runs one untimed pass on its own
-        # core first (orc.c bench_thread), so no cell starts with the
-        # sample's lines in another CCD's L3 or its rings untouched: the
-        # cold first pass made 1-core classify read slower than classify +
-        # lrpc_send on the mixed stream (gpurun_out/r05a_bench_detail.json)
-        for _ in range(CPU_REPS):
-            s1 = t.bench(frames, n, stride, threads=1, passes=p1, cpus=cpus[:1], **kw)
-            sl = t.bench(frames, n, stride, threads=1, passes=pl, lrpc=True, cpus=cpus[:1], **kw)
-            sm = t.bench(frames, n, stride, threads=len(cpus), passes=pm, cpus=cpus, **kw)
-            spent += (s1 * (p1 + 1) / p1 + sl * (pl + 1) / pl + sm * (pm + 1) / pm)
-            r1.append(round(n * p1 / s1 / 1e6, 2))
-            rl.append(round(n * pl / sl / 1e6, 2))
-            rm.append(round(n * pm / sm / 1e6, 2))
         spent += probe
+        budget = budget_s * 0.5 / CPU_REPS
+        cells[mname] = dict(t=t, p1=max(1, int(budget * 0.35 / max(probe, 1e-6))),
+                            pl=max(1, int(budget * 0.3 / max(probe * 1.3, 1e-6))),
+                            pm=max(1, int(budget * 0.35 / max(probe / len(cpus), 1e-6))),
+                            r1=[], rl=[], rm=[])
+    # The 1-core cells of both modes interleaved over CPU_REPS rounds (a
+    # drift of the host hits them alike), then the all-cores cells: a 1-core
+    # cell timed right after an all-cores one ran 3-22 % slow (classify-only
+    # below classify + lrpc_send on the mixed stream, gpurun_out/r05j) even
+    # with the untimed first pass every thread makes (orc.c bench_thread).
+    time.sleep(0.5)
+    for _ in range(CPU_REPS):
+        for mname, _m in modes:
+            c = cells[mname]
+            s1 = c["t"].bench(frames, n, stride, threads=1, passes=c["p1"], cpus=cpus[:1], **kw)
+            sl = c["t"].bench(frames, n, stride, threads=1, passes=c["pl"], lrpc=True, cpus=cpus[:1], **kw)
+            spent += s1 * (c["p1"] + 1) / c["p1"] + sl * (c["pl"] + 1) / c["pl"]
+            c["r1"].append(round(n * c["p1"] / s1 / 1e6, 2))
+            c["rl"].append(round(n * c["pl"] / sl / 1e6, 2))
+    for _ in range(CPU_REPS):
+        for mname, _m in modes:
+            c = cells[mname]
+            sm = c["t"].bench(frames, n, stride, threads=len(cpus), passes=c["pm"], cpus=cpus, **kw)
+            spent += sm * (c["pm"] + 1) / c["pm"]
+            c["rm"].append(round(n * c["pm"] / sm / 1e6, 2))
+    for mname, _m in modes:
+        c = cells[mname]
+        r1, rl, rm = c["r1"], c["rl"], c["rm"]
         res[mname] = {"1core_mpps": _median_rate(r1), "1core_lrpc_mpps": _median_rate(rl),
                       "all_cores_mpps": _median_rate(rm), "all_cores": len(cpus),
                       "samples": {"1core": r1, "1core_lrpc": rl, "all_cores": rm},
@@ -1421,7 +1432,7 @@ def cpu_stream(name, n, budget_s, native, threads):
                       # other tenants share memory bandwidth with
                       "spread_1core": round(max((max(x) - min(x)) / _median_rate(x) for x in (r1, rl)), 4),
                       "spread_all_cores": round((max(rm) - min(rm)) / _median_rate(rm), 4),
-                      "passes": [p1, pl, pm]}
+                      "passes": [c["p1"], c["pl"], c["pm"]]}
     res["seconds"] = round(spent, 2)
     del frames
     return res
