@@ -2,8 +2,9 @@
 buffers, in one process: stored per packet (GCL_TUNE_DEFER=0) against kept
 in LDS (and past a full buffer in registers) and written in at most two
 batches per block (1, the default), or in as many as it takes (2).  Round
-5's A/B also had an LDS-only form, since folded into 1
-(profiles/r05_defer_ab.jsonl).  One context per form
+5's A/Bs also had an LDS-only form, since folded into 1
+(profiles/r05_defer_ab.jsonl), and the batch writes through LDS, non-temporal
+or plain (GCL_TUNE_VFLUSH, removed: no difference, r05_vflush_ab.jsonl).  One context per form
 over the same frames and verdict ring, launches interleaved round by round;
 every form's verdicts and counts are checked against form 0's.
 
@@ -21,12 +22,7 @@ import torch  # noqa: E402
 
 import bench  # noqa: E402
 
-FORMS = {0: "per-packet stores", 1: "deferred, <= 2 writes per block", 2: "deferred always",
-         # GCL_TUNE_VFLUSH variants of form 1 (A/B of the batch writes)
-         11: "deferred, registers through LDS", 12: "deferred, nt batch stores",
-         13: "deferred, registers through LDS + nt", 14: "deferred, plain batch stores",
-         15: "deferred, registers through LDS + plain"}
-VFLUSH = {11: 1, 12: 2, 13: 3, 14: 4, 15: 5}
+FORMS = {0: "per-packet stores", 1: "deferred, <= 2 writes per block", 2: "deferred always"}
 
 
 def main():
@@ -37,12 +33,10 @@ def main():
         clfs = {}
         forms = [int(x) for x in os.environ.get("AB_FORMS", ",".join(map(str, FORMS))).split(",")]
         for f in forms:
-            os.environ["GCL_TUNE_DEFER"] = str(f if f < 10 else 1)
-            os.environ["GCL_TUNE_VFLUSH"] = str(VFLUSH.get(f, 0))
+            os.environ["GCL_TUNE_DEFER"] = str(f)
             clfs[f] = bench.classifier(dev, w.R, w.T, w.vbytes)
             bench.setup_tables(clfs[f], w.R, w.T)
         os.environ.pop("GCL_TUNE_DEFER", None)
-        os.environ.pop("GCL_TUNE_VFLUSH", None)
         st = torch.cuda.current_stream().cuda_stream
         ref = None
         for f, clf in clfs.items():  # correctness: same verdicts and counts as form 0
