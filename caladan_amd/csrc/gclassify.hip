@@ -104,6 +104,7 @@ struct KParams {
 	uint32_t vcap;   /* classify_kernel, 1-/2-B verdicts: tiles of verdicts its LDS buffer
 	                    holds (0: every verdict stored as it is made) */
 	uint32_t vregs;  /* with vcap: tiles past a full LDS buffer held in registers */
+	uint32_t plean;  /* classify_pair_kernel: plain-IPv4 waves on classify_lean */
 };
 
 /* classify_kernel's verdict registers: kVregs dwords per lane, so 4 * kVregs
@@ -498,7 +499,9 @@ __device__ __forceinline__ uint64_t classify_core(const KParams &k, const HdrWor
  * skips the FDIR, hint, options-port, ARP and action-ladder selects.
  * @flags: ol_flags (or the context default), @rss: hash.rss (NIC mode).
  */
-template <int MODE>
+/* HIST: add the packet to the LDS histogram (classify_pair_kernel) rather
+ * than hand its runtime to the loop's writer wave in @hist[tid] */
+template <int MODE, bool HIST = false>
 __device__ __forceinline__ uint64_t classify_lean(const KParams &k, const HdrWords &h, const Tables &tb,
                                                   uint32_t flags, uint32_t rss, uint32_t *hist, int tid,
                                                   Counters &cnt)
@@ -533,8 +536,11 @@ __device__ __forceinline__ uint64_t classify_lean(const KParams &k, const HdrWor
 		thr = gcl::fastmod(hash, (uint64_t)re.m_hi << 32 | re.m_lo, re.tc);
 		if (!re.active)
 			action |= GCL_ACT_WAKE;
+		if (HIST)
+			atomicAdd(&hist[p], 1u);
 	}
-	hist[tid] = (uint32_t)p;
+	if (!HIST)
+		hist[tid] = (uint32_t)p;
 	const uint32_t q = uniq << (k.cflags >> 24) | thr;
 	if (k.cflags & GCL_CFG_VERDICT1)
 		return miss ? GCL_V1_OTHER | GCL_ACT_DROP_UNREG : q;
@@ -977,8 +983,17 @@ classify_pair_kernel(KParams k)
 		h.d3 = r[0].y, h.d5 = r[0].w, h.d6 = r[1].x, h.d7 = r[1].y;
 		h.d8 = r[1].z, h.d9 = r[1].w, h.d10 = 0;
 	};
+	/* a wave whose packets are all plain IPv4 (IHL 5, no FDIR mark) in a
+	 * batch without dst_ip hints or the transport pre-hash takes
+	 * classify_lean (one ballot), the others classify_core (k.plean) */
+	const bool lean_ok = k.plean && !k.dst_hint && !k.trans;
 	auto classify = [&](uint64_t tt, const HdrWords &h, const uint32_t pr[2], uint64_t my) {
-		if (ok(tt)) {
+		const uint32_t fl = k.olflags ? pr[0] & 0xFF : k.default_flags;
+		const bool plain = !ok(tt) || ((h.d3 & 0x000FFFFF) == 0x00050008 && !(fl & GCL_F_FDIR_ID));
+		if (lean_ok && __all(plain)) {
+			if (ok(tt))
+				put_verdict_vf<VF>(k, tt * NT + tid, classify_lean<MODE, true>(k, h, tb, fl, pr[1], hist, tid, cnt));
+		} else if (ok(tt)) {
 			const uint64_t i = tt * NT + tid;
 			/* this packet's frame offset, for the ARP target's extra read */
 			const uint64_t foff = (my >> 63) ? (my & ~kPairBytewise) : my - 8;
@@ -1074,6 +1089,10 @@ constexpr uint64_t kLoopRefresh = 256;
 /* s_memrealtime ticks (100 MHz) a wait polls the offsets with the word: a
  * burst that arrives later costs the offsets' round trip after the word */
 constexpr uint64_t kLoopSpecTicks = 400;
+/* GCL_TUNE_PAIR_LEAN default: classify_pair_kernel's plain-IPv4 waves on
+ * classify_lean -- the ingress working set 64.6-65.3 -> 62.7-63.3 us, the
+ * random pool unchanged (memory-bound), profiles/r05_pair_lean_ab.jsonl */
+constexpr int kDefaultPairLean = 1;
 /* GCL_TUNE_DEFER default (Geometry::defer): udp64 328.2-329.1 -> 323.4-324.2
  * us, three fresh processes (profiles/r05_defer_ab.jsonl) */
 constexpr int kDefaultDefer = 1;
@@ -2273,6 +2292,7 @@ struct gcl_ctx {
 	int tune_grid;    /* GCL_TUNE_GRID: blocks per launch (0: the persistent grid) */
 	int tune_bpc;     /* GCL_TUNE_BLOCKS_PER_CU: cap on blocks per CU (0: none) */
 	int tune_defer;   /* GCL_TUNE_DEFER: Geometry::defer for eligible batches (0-2) */
+	int tune_plean;   /* GCL_TUNE_PAIR_LEAN: KParams::plean (0: off, tests and A/Bs) */
 };
 
 extern "C" {
@@ -2346,6 +2366,8 @@ extern "C" int gcl_open(int hip_device, const struct gcl_cfg *cfg, struct gcl_ct
 		c->tune_grid = e ? atoi(e) : 0;
 		e = getenv("GCL_TUNE_BLOCKS_PER_CU");
 		c->tune_bpc = e ? atoi(e) : 0;
+		e = getenv("GCL_TUNE_PAIR_LEAN");
+		c->tune_plean = e ? atoi(e) != 0 : kDefaultPairLean;
 		e = getenv("GCL_TUNE_DEFER");
 		c->tune_defer = e ? std::min(std::max(atoi(e), 0), 2) : kDefaultDefer;
 	}
@@ -2986,6 +3008,7 @@ extern "C" int gcl_classify_ex(struct gcl_ctx *c, const struct gcl_batch *b,
 	k.off_crc = c->off_crc;
 	k.trans = (uint2 *)out->trans;
 	k.cflags = kernel_cflags(c);
+	k.plean = (uint32_t)c->tune_plean;
 	k.default_flags = c->cfg.default_olflags;
 
 	/* the specialised fast path needs every header granule in range */

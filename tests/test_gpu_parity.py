@@ -905,6 +905,46 @@ def test_gpu_ingress_pool_geometry(g, orc):
     assert (counts == ce).all() and (stats == se).all()
 
 
+@pytest.mark.parametrize("pair_lean", [1, 0])
+@pytest.mark.parametrize("mode,vb", [(0, 2), (0, 1), (1, 8), (1, 2), (2, 4), (2, 1)])
+def test_gpu_pair_lean_waves(g, orc, mode, vb, pair_lean, monkeypatch):
+    """classify_pair_kernel's lean path (GCL_TUNE_PAIR_LEAN, on by default):
+    a wave whose packets are all plain IPv4 takes classify_lean, a wave with
+    one FDIR-marked packet (every 997th, no fdir array: mark 0) or without the
+    NIC's hash flag on some frames takes the same counters through either
+    path -- mbuf-pool offsets with ol_flags and hash.rss, every hash mode and
+    verdict width, both settings, bit-exact against the oracle."""
+    monkeypatch.setenv("GCL_TUNE_PAIR_LEAN", str(pair_lean))
+    n, R, T, P = 40000, 16, 8, 8192
+    hdr, olf_p, rss_p = orc.generate(0, P, 64, R)
+    rng = np.random.default_rng(23 + mode + 10 * vb)
+    pool = g.mbuf_data_offsets(P)
+    order = np.concatenate([rng.permutation(P) for _ in range(-(-n // P))])[:n]
+    offs = pool[order]
+    olf = np.ascontiguousarray(olf_p[order])
+    rss = np.ascontiguousarray(rss_p[order])
+    olf[::13] &= ~np.uint8(g.F_RSS_HASH)
+    olf[::997] |= np.uint8(g.F_FDIR_ID)
+    region = np.zeros(g.mbuf_region_bytes(P), dtype=np.uint8)
+    region[pool[:, None].astype(np.int64) + np.arange(64)] = hdr.reshape(P, 64)
+    tb = g.thread_bits_for(R, T) if vb <= 2 else 0
+    cflags = {8: 0, 4: g.CFG_VERDICT4, 2: g.CFG_VERDICT2, 1: g.CFG_VERDICT1}[vb]
+    t = orc.Tables(R, mode, 0, 0x09, g.CALADAN_RSS_KEY)
+    clf = g.Classifier(0, R, mode, cflags, 0x09, g.CALADAN_RSS_KEY, thread_bits=tb)
+    for r in range(R):
+        act = (r * 5) % (T + 1)
+        fl = orc.steer_flows(T, list(range(act))) if act else None
+        t.runtime_set(r, orc.runtime_ip(r), T, act, fl)
+        clf.runtime_set(r, g.runtime_ip(r), T, act, fl)
+    ve, ce, se = t.classify(region, n, 0, offs=offs, olflags=olf, rss=rss)
+    v, c, st = gpu_run(g, clf, region, n, 0, offs=offs, olflags=olf, rss=rss)
+    assert se[g.RX_FLOW_TAG_MATCH] > 0 and se[g.RX_HASH_MISSING] > 0
+    want = {8: lambda: ve, 4: lambda: to_verdict4(ve), 2: lambda: to_verdict2(ve, [T] * R, tb),
+            1: lambda: to_verdict1(ve, [T] * R, tb)}[vb]()
+    assert_same(v, want, f"pair lean={pair_lean} mode={mode} vb={vb}")
+    assert (c == ce).all() and (st == se).all()
+
+
 def test_gpu_ingress_integrated_nic_verdict2(g, orc):
     """The bench's integrated ingress shape (e2e.ingress_pool.integrated_nic,
     INTEGRATION.md §4): descriptors into the reference's mbuf pool geometry
