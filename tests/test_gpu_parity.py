@@ -344,7 +344,8 @@ def test_gpu_dense_narrow_verdicts(g, orc, wl, R, T, vb, defer, monkeypatch):
     (1, {"GCL_TUNE_BLOCKS_PER_CU": "1", "GCL_TUNE_GRID": "301"}),
     (2, {"GCL_TUNE_THREADS": "512", "GCL_TUNE_GRID": "7"}), (2, {"GCL_TUNE_THREADS": "1024", "GCL_TUNE_GRID": "7"}),
     (1, {"GCL_TUNE_GRID": "20"}), (1, {"GCL_TUNE_GRID": "40"}), (1, {"GCL_TUNE_GRID": "70"}),
-    (1, {"GCL_TUNE_GRID": "20", "GCL_TUNE_DEPTH": "1"}), (1, {"GCL_TUNE_THREADS": "512", "GCL_TUNE_GRID": "12"})])
+    (1, {"GCL_TUNE_GRID": "20", "GCL_TUNE_DEPTH": "1"}), (1, {"GCL_TUNE_THREADS": "512", "GCL_TUNE_GRID": "12"}),
+    (1, {"GCL_TUNE_TABLES": "1", "GCL_TUNE_GRID": "40"}), (2, {"GCL_TUNE_TABLES": "1", "GCL_TUNE_GRID": "9"})])
 @pytest.mark.parametrize("vb", [1, 2])
 def test_gpu_dense_deferred_flushes(g, orc, vb, defer, env, monkeypatch):
     """The tile kernel's LDS verdict buffer when a block walks more tiles
@@ -352,9 +353,9 @@ def test_gpu_dense_deferred_flushes(g, orc, vb, defer, env, monkeypatch):
     buffers written inside the loop, a partial one at the end, the batch's
     ragged last tile cut at n; the registers past a full buffer partly
     filled (grid 40), full and written out inside the loop (grid 20 / 12),
-    or unused (grid 70 at 1-B verdicts); DEPTH 1 and 2; 256-, 512-
-    and 1024-lane tiles -- against the oracle on a 1 Mi + 77-packet udp64
-    batch, with its counts and counters."""
+    or unused (grid 70 at 1-B verdicts); DEPTH 1 and 2; 256-, 512- and
+    1024-lane tiles; tables in LDS and in HBM -- against the oracle on a
+    1 Mi + 77-packet udp64 batch, with its counts and counters."""
     for kk, vv in {"GCL_TUNE_DEFER": str(defer), **env}.items():
         monkeypatch.setenv(kk, vv)
     R, T, stride = 16, 8, 64
