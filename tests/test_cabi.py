@@ -34,6 +34,23 @@ def test_library_exports_every_declared_symbol(g):
     assert not missing, missing
 
 
+def test_integration_guide_calls_declared_functions():
+    """Every gcl_* function INTEGRATION.md's C calls, and every GCL_* name it
+    uses, is declared in include/ (gcl_group.h too), so the guide a
+    maintainer copies from cannot drift from the ABI."""
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    code = "\n".join(re.findall(r"```c\n(.*?)```", doc, flags=re.S))
+    assert code, "no C blocks in INTEGRATION.md"
+    hdr = "".join(open(os.path.join(ROOT, "include", h)).read()
+                  for h in ("gclassify.h", "gcl_host.h", "gcl_pcap.h", "gcl_group.h"))
+    own = set(re.findall(r"#define\s+(GCL_\w+)", code))  # the guide's own macros
+    calls = set(re.findall(r"\b(gcl_\w+)\s*\(", code))
+    names = set(re.findall(r"\b(GCL_[A-Z0-9_]+)\b", code)) - own
+    assert len(calls) >= 10, calls
+    missing = sorted(n for n in calls | names if not re.search(r"\b" + n + r"\b", hdr))
+    assert not missing, missing
+
+
 def test_struct_layouts(g):
     assert ctypes.sizeof(g.GclCfg) == 56
     assert ctypes.sizeof(g.GclBatch) == 80
