@@ -1086,9 +1086,17 @@ static_assert(sizeof(LoopSlotHdr) == 64, "LoopSlotHdr");
 constexpr int kLoopStampShift = 40;
 constexpr uint64_t kLoopOffMask = (1ull << kLoopStampShift) - 1;
 constexpr uint64_t kLoopRefresh = 256;
-/* s_memrealtime ticks (100 MHz) a wait polls the offsets with the word: a
- * burst that arrives later costs the offsets' round trip after the word */
+/* s_memrealtime ticks (100 MHz) a wait polls the offsets or header records
+ * with the word: a burst that arrives later costs their round trip after the
+ * word.  Loops of 1 or 2 workers keep polling them for kLoopSpecIdle (1 ms):
+ * sparse lone bursts (random gaps of [0, 20) us) 4.50-4.73 -> 3.76-3.81 us
+ * p50 for ~3 GB/s of idle PCIe reads per worker; with more workers that
+ * traffic costs the pipeline more than the late bursts do (8 x 16 records
+ * 139-142 -> 122-132 Mpkt/s), so they keep 4 us
+ * (profiles/r05_spec_ab.jsonl) */
 constexpr uint64_t kLoopSpecTicks = 400;
+constexpr uint64_t kLoopSpecIdle = 100000;
+constexpr uint32_t kLoopSpecIdleWorkers = 2;
 /* GCL_TUNE_PAIR_LEAN default: classify_pair_kernel's plain-IPv4 waves on
  * classify_lean -- the ingress working set 64.6-65.3 -> 62.7-63.3 us, the
  * random pool unchanged (memory-bound), profiles/r05_pair_lean_ab.jsonl */
@@ -3812,7 +3820,7 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 	                     ? lp.off_verd + sizeof(LoopRec) * mb : 0;
 	lp.rec_plane = (uint32_t)(16 * mb);
 	lp.spec = (!lp.off_hdr || lp.hdr_rec) && cfg->max_burst <= 64;
-	lp.spec_ticks = kLoopSpecTicks;
+	lp.spec_ticks = cfg->workers <= kLoopSpecIdleWorkers ? kLoopSpecIdle : kLoopSpecTicks;
 	L->k64 = cfg->max_burst <= 64;
 	if (const char *e = getenv("GCL_TUNE_LOOP64")) /* 0: tests, the general loop */
 		L->k64 = L->k64 && atoi(e) != 0;

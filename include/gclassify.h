@@ -596,8 +596,9 @@ struct gcl_rxloop_cfg {
  * instead of two.  Ports past byte 43 (IHL >= 7) are read from the region.
  * Exclusive with GCL_LOOP_INLINE_HDRS (-EINVAL).  A worker polls the records
  * (or, without this flag, the stamped offsets) during the first 4 us of a
- * wait (GCL_TUNE_LOOP_SPEC in the environment at gcl_rxloop_start: the
- * window in 10-ns ticks); a burst found later is read after its word. */
+ * wait, or the first 1 ms in a loop of 1 or 2 workers (GCL_TUNE_LOOP_SPEC
+ * in the environment at gcl_rxloop_start: the window in 10-ns ticks); a
+ * burst found later is read after its word. */
 #define GCL_LOOP_HDR_RECORDS 0x2
 /* Measurement: lane 0 of the worker stores each burst's stage times into
  * the slot header after its records (gcl_rxloop_stamps). */

@@ -293,9 +293,11 @@ int main(int argc, char **argv)
 	/* RXPIPE_GAP_NS (depth 1): spin this long after a burst's delivery before
 	 * the next submit, or "rand": a uniform [0, 2000) ns per burst, so that
 	 * the submit lands at any phase of the worker's polls (which start when
-	 * it has stored the previous burst's records) as bursts from a NIC do */
+	 * it has stored the previous burst's records) as bursts from a NIC do;
+	 * "rand:N": uniform [0, N) ns (sparser traffic) */
 	const char *gap_env = getenv("RXPIPE_GAP_NS");
-	const bool gap_rand = gap_env && !strcmp(gap_env, "rand");
+	const bool gap_rand = gap_env && !strncmp(gap_env, "rand", 4);
+	const uint64_t gap_span = gap_rand && gap_env[4] == ':' ? strtoull(gap_env + 5, nullptr, 0) : 2000;
 	const uint64_t gap_fixed = gap_env && !gap_rand ? strtoull(gap_env, nullptr, 0) : 0;
 	double ticks_per_ns = 1.0;
 	{
@@ -313,7 +315,7 @@ int main(int argc, char **argv)
 			gap_state ^= gap_state << 13;
 			gap_state ^= gap_state >> 7;
 			gap_state ^= gap_state << 17;
-			g = gap_state % 2000;
+			g = gap_state % (gap_span ? gap_span : 1);
 		}
 		const uint64_t end = ticks() + (uint64_t)(g * ticks_per_ns);
 		while (ticks() < end)
@@ -425,7 +427,7 @@ int main(int argc, char **argv)
 	       "\"delivered_check\": \"%s\", \"unicast_fail\": %llu, \"host_cpu\": %d, "
 	       "\"bursts_early\": %llu, \"bursts_stale\": %llu, \"bursts_late\": %llu}\n",
 	       burst, workers, depth, nbursts, nic ? "nic (hash.rss, rx.c:83)" : "jenkins",
-	       gap_rand ? "rand [0, 2000)" : gap_env ? gap_env : "0",
+	       gap_rand ? (gap_span == 2000 ? "rand [0, 2000)" : gap_env) : gap_env ? gap_env : "0",
 	       copy_out ? "copied out" : inline_hdrs ? "read in place, headers inlined in the slot"
 	       : hdr_records ? "read in place, stamped header records in the slot" : "read in place",
 	       pkts / (el * 1e-3), lat[lat.size() / 2] * ns_tick * 1e-3,
