@@ -1407,6 +1407,10 @@ def cpu_stream(name, n, budget_s, native, threads):
     # below classify + lrpc_send on the mixed stream, gpurun_out/r05j) even
     # with the untimed first pass every thread makes (orc.c bench_thread).
     time.sleep(0.5)
+    # one throwaway 1-core cell first: the first cell after the pause ran up
+    # to 6 % fast (tcp1500, profiles/r05_bench_detail.json)
+    c0 = cells[modes[0][0]]
+    spent += c0["t"].bench(frames, n, stride, threads=1, passes=c0["p1"], cpus=cpus[:1], **kw)
     for _ in range(CPU_REPS):
         for mname, _m in modes:
             c = cells[mname]
