@@ -209,6 +209,15 @@ extern "C" uint64_t gcl_shard_global(uint64_t j, uint32_t world, uint32_t rank, 
 	return ((j / block) * world + rank) * block + j % block;
 }
 
+/* zero a GPU's accumulators, complete before returning: the group's streams
+ * are non-blocking, so a null-stream hipMemset (which may return before it
+ * lands) is not ordered before the next exchange's snapshot on st[0] */
+static hipError_t zero_acc(gcl_group::Dev &D, size_t bytes)
+{
+	hipError_t e = hipMemsetAsync(D.acc, 0, bytes, D.st[0]);
+	return e != hipSuccess ? e : hipStreamSynchronize(D.st[0]);
+}
+
 static void free_dev(gcl_group::Dev &D, bool rccl)
 {
 	if (D.dev < 0)
@@ -320,7 +329,7 @@ extern "C" int gcl_group_open_v2(int ndev, const int *devs, const struct gcl_cfg
 		he(hipMalloc(&D.gath, L8 * kSlots * ndev));
 		he(hipMalloc(&D.node, L8 * kSlots));
 		if (!he.bad())
-			he(hipMemset(D.acc, 0, L8));
+			he(zero_acc(D, L8));
 		if (he.bad())
 			ret = he.e == hipErrorOutOfMemory ? -ENOMEM : -EIO;
 	}
@@ -790,7 +799,7 @@ extern "C" int gcl_group_reset(struct gcl_group *g)
 	int ret = gcl_group_sync(g);
 	for (int i = 0; i < g->n && !ret; i++) {
 		gcl_group::Dev &D = g->d[i];
-		if (hipSetDevice(D.dev) != hipSuccess || hipMemset(D.acc, 0, (size_t)g->L * 8) != hipSuccess)
+		if (hipSetDevice(D.dev) != hipSuccess || zero_acc(D, (size_t)g->L * 8) != hipSuccess)
 			ret = -EIO;
 	}
 	return ret;
