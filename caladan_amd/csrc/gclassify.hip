@@ -1107,6 +1107,15 @@ constexpr int kDefaultDefer = 1;
 /* GCL_TUNE_LOOP_LEAN default: bursts whose every packet is plain IPv4 (IHL 5,
  * no FDIR mark, no hint) classified by classify_lean */
 constexpr uint32_t kDefaultLoopLean = 1;
+/* GCL_TUNE_LOOP_PHASE default ("max,up,down" in ticks; loops of up to
+ * kLoopSpecIdleWorkers workers): the poll-phase delay's ceiling and steps.
+ * 1 x 1 header records, NIC hash, three fresh processes per form
+ * (profiles/r05_phase_ab.jsonl, r05_phase_sweep.jsonl): back to back
+ * 3.94-3.98 -> 3.11-3.19 us p50, random phase 3.61-3.90 -> 3.49-3.57, sparse
+ * lone bursts unchanged (3.64-4.02 / 3.76-3.79), 2 workers x 2 in flight
+ * 3.99-4.01 -> 3.14-3.45; a 200-tick ceiling let the delay outgrow the host's
+ * turnaround at a random phase (3.86-4.05) */
+constexpr uint32_t kDefaultLoopPhaseMax = 120, kDefaultLoopPhaseUp = 16, kDefaultLoopPhaseDown = 1;
 /* how a worker's bursts arrived (gcl_rxloop_poll_stats): with the poll that
  * found the word; eligible for that, but an entry or record still stale so
  * read after it; or after the word, the speculative window over or the
@@ -1161,6 +1170,9 @@ struct LoopParams {
 	                              planes (chunk j of packet i at off_hdr + j * rec_plane + 16 i) */
 	uint32_t lean;             /* rxloop64_kernel: plain-IPv4 bursts on classify_lean
 	                              (GCL_TUNE_LOOP_LEAN=0: always classify_core) */
+	uint32_t phase_max;        /* rxloop64_kernel: the poll-phase delay's ceiling in ticks
+	                              (0: off; GCL_TUNE_LOOP_PHASE), and its steps */
+	uint32_t phase_up, phase_down;
 };
 
 /* GCL_LOOP_HDR_RECORDS: the submitting core writes each packet as one 64-B
@@ -1578,6 +1590,15 @@ __global__ void __launch_bounds__(256) rxloop_kernel(LoopParams L)
  * lost the round-5 A/B on header records: lone bursts 3.84 -> 3.9-4.06 us p50,
  * 4 workers x 8 deep 103 -> 92 Mpkt/s (profiles/r05_pollers_ab.jsonl); it
  * won only on stamped offsets, the slower form, and was removed.
+ *
+ * The poll-phase delay (round 5, L.phase_max, loops of 1-2 workers): a host
+ * that submits once it has seen the last burst's verdicts cannot land before
+ * its own turnaround, so a ticket's first poll waits dly ticks after the last
+ * records, dly stepping down after a burst found whole by the first poll and
+ * up after one found by the second.  Round 4's form (GCL_TUNE_LOOP_HYBRID)
+ * delayed only after a burst that needed more than one poll, so a
+ * back-to-back stream alternated delayed and undelayed polls and never
+ * locked on.
  */
 struct Mbox64 {
 	uint32_t p[64];   /* each packet's runtime (~0: none): the counts */
@@ -1731,6 +1752,10 @@ __global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
 	uint64_t kt = 0; /* this worker's next ticket index */
 	uint64_t spec_end = __builtin_amdgcn_s_memrealtime() + L.spec_ticks;
 	uint32_t npoll = 0; /* polls of this ticket */
+	/* the poll-phase delay (L.phase_max): a ticket's first poll waits dly
+	 * ticks after the last burst's records went out */
+	uint32_t dly = 0;
+	uint64_t t_done = 0;
 
 	for (uint32_t kk = 0;; kk++) {
 		/* the ticket and its slot, uniform: a slot address the compiler
@@ -1751,6 +1776,17 @@ __global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
 		 * burst's records stale).  Every lane loads the word and the stop
 		 * flag (one address: one request), so no divergent branch lets the
 		 * compiler consume the records before the word is even issued. */
+		if (npoll == 0 && dly) {
+			/* A host that submits once it has seen the last records (a
+			 * closed loop) cannot land before its turnaround: a poll
+			 * issued at once samples the slot too early, and every later
+			 * sample is a round trip apart from it.  The first poll waits
+			 * instead; dly tracks that turnaround (below). */
+			const uint64_t until = t_done + dly;
+			while (__builtin_amdgcn_s_memrealtime() < until)
+				__builtin_amdgcn_s_sleep(1);
+			spec_end = __builtin_amdgcn_s_memrealtime() + L.spec_ticks;
+		}
 		const uint64_t t_issue = __builtin_amdgcn_s_memrealtime();
 		npoll++;
 		const bool sp = spec && t_issue < spec_end;
@@ -1784,6 +1820,19 @@ __global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
 		const uint64_t hit = L.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
 		const uint32_t kind = early ? kLoopPollEarly : (sp && nw <= 64) ? kLoopPollStale : kLoopPollLate;
 		const uint32_t polls_used = npoll;
+		if (L.phase_max) {
+			/* found whole by the first poll: it may have waited longer than
+			 * needed, so wait a step less next time; found by the second,
+			 * or with its records still being written: the first poll was
+			 * early, a step more.  Later finds are sparse traffic, whose
+			 * phase is its own: no change.  The steps are asymmetric, so
+			 * about phase_down / (phase_up + phase_down) of closed-loop
+			 * bursts pay the round trip a miss costs. */
+			if (polls_used == 1 && early)
+				dly = dly > L.phase_down ? dly - L.phase_down : 0;
+			else if (polls_used <= 2)
+				dly = dly + L.phase_up < L.phase_max ? dly + L.phase_up : L.phase_max;
+		}
 		Mbox64 &m = me.mbox[mb]; /* free: waited for after the last post */
 		if (img_seq != cur_seq) { /* this burst's table snapshot: copied into LDS */
 			const uint8_t *ib = L.img[img];
@@ -1950,6 +1999,7 @@ __global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
 		kt++;
 		npoll = 0;
 		spec_end = __builtin_amdgcn_s_memrealtime() + L.spec_ticks;
+		t_done = spec_end - L.spec_ticks;
 	}
 	/* the writer drains what was posted, then leaves; the host stops
 	 * publishing on this word (one it reads without a HIP call per burst) */
@@ -3826,6 +3876,19 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 		L->k64 = L->k64 && atoi(e) != 0;
 	if (const char *e = getenv("GCL_TUNE_LOOP_SPEC")) /* experiments: ticks of 10 ns */
 		lp.spec_ticks = (uint32_t)atoi(e);
+	/* the poll-phase delay: closed-loop submitters are the few-worker case;
+	 * a deep pipeline finds its bursts queued */
+	lp.phase_max = cfg->workers <= kLoopSpecIdleWorkers ? kDefaultLoopPhaseMax : 0;
+	lp.phase_up = kDefaultLoopPhaseUp;
+	lp.phase_down = kDefaultLoopPhaseDown;
+	if (const char *e = getenv("GCL_TUNE_LOOP_PHASE")) { /* "max[,up[,down]]", ticks */
+		unsigned m = 0, u = lp.phase_up, d = lp.phase_down;
+		if (sscanf(e, "%u,%u,%u", &m, &u, &d) >= 1 && m <= 1000 && u && d <= u) {
+			lp.phase_max = m;
+			lp.phase_up = u;
+			lp.phase_down = d;
+		}
+	}
 	{
 		const uint64_t end = lp.off_verd + sizeof(LoopRec) * mb + (lp.off_hdr ? GCL_HDR_GRANULE * mb : 0);
 		lp.off_trans = (c->cfg.flags & GCL_CFG_TRANS_HASH) ? (uint32_t)end : 0;

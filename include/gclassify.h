@@ -598,7 +598,12 @@ struct gcl_rxloop_cfg {
  * (or, without this flag, the stamped offsets) during the first 4 us of a
  * wait, or the first 1 ms in a loop of 1 or 2 workers (GCL_TUNE_LOOP_SPEC
  * in the environment at gcl_rxloop_start: the window in 10-ns ticks); a
- * burst found later is read after its word. */
+ * burst found later is read after its word.  In a loop of 1 or 2 workers
+ * with bursts of <= 64 a worker issues the first poll of each ticket a
+ * little after its last verdict records, the delay following the host's
+ * turnaround (up to 1.2 us; GCL_TUNE_LOOP_PHASE "max,up,down" in 10-ns
+ * ticks, "0" off): a dataplane core that submits once it has seen the last
+ * verdicts is sampled just after its submit rather than a round trip later. */
 #define GCL_LOOP_HDR_RECORDS 0x2
 /* Measurement: lane 0 of the worker stores each burst's stage times into
  * the slot header after its records (gcl_rxloop_stamps). */

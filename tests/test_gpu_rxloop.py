@@ -488,6 +488,44 @@ def test_rxloop_stamp_wrap(g, orc, lflag, spec, use0, monkeypatch):
         g.host_unregister(frames)
 
 
+@pytest.mark.parametrize("phase", [None, "0", "1000,1000,0", "1,1,1"])
+@pytest.mark.parametrize("workers,lflag", [(1, 2), (2, 2), (1, 0)])
+def test_rxloop_phase_delay(g, orc, phase, workers, lflag, monkeypatch):
+    """The poll-phase delay (GCL_TUNE_LOOP_PHASE "max,up,down"; None: the
+    default, on for loops of 1-2 workers) only moves when a ticket's first
+    poll is issued: bursts submitted in a closed loop (each after the last
+    one's verdicts), with host-side gaps now and then, come back equal to the
+    oracle's whatever the delay does -- off, pinned at 10 us after the first
+    late find ("1000,1000,0"), or one tick."""
+    rng = np.random.default_rng(7900 + workers + 10 * lflag + (len(phase) if phase else 0))
+    max_rt = 16
+    rts = random_runtimes(rng, max_rt, 12)
+    n = 2048
+    frames, flen, offs, olf, rss, fdir, hint = fuzz_batch(rng, n, rts, max_rt)
+    t = orc.Tables(max_rt, 1, 0, 0x09)
+    apply_runtimes(t, rts)
+    ve, _, _ = t.classify(frames, n, 0, offs=offs, olflags=olf, rss=rss, frames_len=flen)
+    clf = g.Classifier(0, max_rt, 1, 0, 0x09)
+    apply_runtimes(clf, rts)
+    g.host_register(frames)
+    if phase is not None:
+        monkeypatch.setenv("GCL_TUNE_LOOP_PHASE", phase)
+    loop = clf.rxloop(frames, slots=8, workers=workers, region_len=flen, flags=LOOP_FLAGS[lflag](g))
+    try:
+        for k in range(300):
+            m = int(rng.integers(1, 65))
+            idx = rng.integers(0, n, size=m)
+            tk = loop.submit(offs[idx], olf[idx], rss[idx])
+            got = loop.wait(tk, m)
+            bad = np.nonzero(got != ve[idx])[0]
+            assert not len(bad), f"burst {k}: {got[bad[0]]} vs {ve[idx][bad[0]]}"
+            if k % 50 == 49:
+                time.sleep(0.001)  # sparse now and then: the delay must not stall
+    finally:
+        loop.stop()
+        g.host_unregister(frames)
+
+
 def test_rxloop_release_incomplete(g):
     """gcl_rxloop_release refuses (-EAGAIN) a burst the GPU has not completed,
     so its slot is never handed to the next submit while still being written."""
