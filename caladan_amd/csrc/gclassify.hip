@@ -1116,6 +1116,14 @@ constexpr uint32_t kDefaultLoopLean = 1;
  * 3.99-4.01 -> 3.14-3.45; a 200-tick ceiling let the delay outgrow the host's
  * turnaround at a random phase (3.86-4.05) */
 constexpr uint32_t kDefaultLoopPhaseMax = 120, kDefaultLoopPhaseUp = 16, kDefaultLoopPhaseDown = 1;
+/* GCL_TUNE_LOOP_PREFETCH default (loops of more than kLoopSpecIdleWorkers
+ * workers over stamped offsets, whose bursts take a second round trip for
+ * the headers that the next poll overlaps): 4 x 8 offsets 58.2-59.8 ->
+ * 72.1-76.3 Mpkt/s in fresh processes (profiles/r05_prefetch_ab.jsonl,
+ * r05_prefetch_gated_ab.jsonl); with header records only the ~0.6-us
+ * classification is left to overlap and the gated form measured no gain
+ * (4 x 8 JENKINS 90.8-93.7 -> 82.2-95.1) */
+constexpr uint32_t kDefaultLoopPrefetch = 1;
 /* how a worker's bursts arrived (gcl_rxloop_poll_stats): with the poll that
  * found the word; eligible for that, but an entry or record still stale so
  * read after it; or after the word, the speculative window over or the
@@ -1173,6 +1181,8 @@ struct LoopParams {
 	uint32_t phase_max;        /* rxloop64_kernel: the poll-phase delay's ceiling in ticks
 	                              (0: off; GCL_TUNE_LOOP_PHASE), and its steps */
 	uint32_t phase_up, phase_down;
+	uint32_t prefetch;         /* rxloop64_kernel: the next ticket's poll issued before a
+	                              burst is classified (GCL_TUNE_LOOP_PREFETCH) */
 };
 
 /* GCL_LOOP_HDR_RECORDS: the submitting core writes each packet as one 64-B
@@ -1756,6 +1766,11 @@ __global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
 	 * ticks after the last burst's records went out */
 	uint32_t dly = 0;
 	uint64_t t_done = 0;
+	/* the next ticket's poll, issued while this burst is classified
+	 * (L.prefetch): its word, offsets or records, issue time and window */
+	bool pf = false, psp = false;
+	uint64_t pw = 0, pev = 0, pis = 0;
+	uint4 pq[4] = {};
 
 	for (uint32_t kk = 0;; kk++) {
 		/* the ticket and its slot, uniform: a slot address the compiler
@@ -1776,32 +1791,50 @@ __global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
 		 * burst's records stale).  Every lane loads the word and the stop
 		 * flag (one address: one request), so no divergent branch lets the
 		 * compiler consume the records before the word is even issued. */
-		if (npoll == 0 && dly) {
-			/* A host that submits once it has seen the last records (a
-			 * closed loop) cannot land before its turnaround: a poll
-			 * issued at once samples the slot too early, and every later
-			 * sample is a round trip apart from it.  The first poll waits
-			 * instead; dly tracks that turnaround (below). */
-			const uint64_t until = t_done + dly;
-			while (__builtin_amdgcn_s_memrealtime() < until)
-				__builtin_amdgcn_s_sleep(1);
-			spec_end = __builtin_amdgcn_s_memrealtime() + L.spec_ticks;
-		}
-		const uint64_t t_issue = __builtin_amdgcn_s_memrealtime();
-		npoll++;
-		const bool sp = spec && t_issue < spec_end;
-		const uint64_t wv0 = gcl::ld_sys64(&h->word);
-		const uint32_t sv0 = (kk & 7) == 7 ? gcl::ld_sys32(L.stop) : 0u; /* a stop waits <= 8 polls */
-		const uint64_t ev = sp && !rec ? gcl::ld_sys64(slot + L.off_offs + 8 * lane) : 0;
-		uint4 q[4] = {};
-		if (sp && rec) {
+		uint64_t t_issue, wv0, ev;
+		uint32_t sv0;
+		bool sp;
+		uint4 q[4];
+		if (pf) { /* issued while the last burst was classified */
+			pf = false;
+			t_issue = pis;
+			sp = psp;
+			wv0 = pw;
+			ev = pev;
+			sv0 = 0;
 #pragma unroll
-			for (int j = 0; j < 4; j++) {
-				const auto v = __builtin_amdgcn_raw_buffer_load_b128(
-				        srs, (int)(L.off_hdr + L.rec_plane * j + 16 * lane), 0, gcl::kSysAux);
-				q[j] = make_uint4(v[0], v[1], v[2], v[3]);
+			for (int j = 0; j < 4; j++)
+				q[j] = pq[j];
+		} else {
+			if (npoll == 0 && dly) {
+				/* A host that submits once it has seen the last records (a
+				 * closed loop) cannot land before its turnaround: a poll
+				 * issued at once samples the slot too early, and every
+				 * later sample is a round trip apart from it.  The first
+				 * poll waits instead; dly tracks that turnaround (below). */
+				const uint64_t until = t_done + dly;
+				while (__builtin_amdgcn_s_memrealtime() < until)
+					__builtin_amdgcn_s_sleep(1);
+				spec_end = __builtin_amdgcn_s_memrealtime() + L.spec_ticks;
+			}
+			t_issue = __builtin_amdgcn_s_memrealtime();
+			sp = spec && t_issue < spec_end;
+			wv0 = gcl::ld_sys64(&h->word);
+			sv0 = (kk & 7) == 7 ? gcl::ld_sys32(L.stop) : 0u; /* a stop waits <= 8 polls */
+			ev = sp && !rec ? gcl::ld_sys64(slot + L.off_offs + 8 * lane) : 0;
+#pragma unroll
+			for (int j = 0; j < 4; j++)
+				q[j] = make_uint4(0, 0, 0, 0);
+			if (sp && rec) {
+#pragma unroll
+				for (int j = 0; j < 4; j++) {
+					const auto v = __builtin_amdgcn_raw_buffer_load_b128(
+					        srs, (int)(L.off_hdr + L.rec_plane * j + 16 * lane), 0, gcl::kSysAux);
+					q[j] = make_uint4(v[0], v[1], v[2], v[3]);
+				}
 			}
 		}
+		npoll++;
 		const uint64_t w_word = lane0_u64(wv0);
 		const uint32_t sv = lane0_u32(sv0);
 		const bool found = (w_word >> 24) == (t & ((1ull << 40) - 1));
@@ -1922,6 +1955,38 @@ __global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
 			hw.d3 = r[0].w, hw.d5 = r[1].y, hw.d6 = r[1].z, hw.d7 = r[1].w;
 			hw.d8 = r[2].x, hw.d9 = r[2].y, hw.d10 = r[2].z;
 		}
+		if (L.prefetch && polls_used == 1) {
+			/* The next ticket's poll now, with this burst's fields in
+			 * registers: its round trip runs while this burst is
+			 * classified and its records stored, rather than after.
+			 * Nothing below waits on memory loads (the lean path reads
+			 * LDS), so the poll's loads hold no wait here; it is used,
+			 * whatever it finds, as the next ticket's first poll.  Only
+			 * while the host is ahead (this burst was there at the first
+			 * poll): a worker that has caught up would sample the next
+			 * slot too early and set every later sample a round trip
+			 * off (8 x 16 records 139-155 -> 93-112 Mpkt/s without this
+			 * condition, profiles/r05_prefetch_ab.jsonl). */
+			const uint64_t t2 = lane0_u64(L.t0 + blockIdx.x + 1 + (kt + 1) * L.workers);
+			uint8_t *slot2 = L.slots + ((t2 - 1) & (L.nslots - 1)) * (uint64_t)L.slot_bytes;
+			const __amdgpu_buffer_rsrc_t srs2 = gcl::host_rsrc(slot2, L.slot_bytes);
+			pis = __builtin_amdgcn_s_memrealtime();
+			psp = spec;
+			pw = gcl::ld_sys64(&((LoopSlotHdr *)slot2)->word);
+			pev = psp && !rec ? gcl::ld_sys64(slot2 + L.off_offs + 8 * lane) : 0;
+#pragma unroll
+			for (int j = 0; j < 4; j++)
+				pq[j] = make_uint4(0, 0, 0, 0);
+			if (psp && rec) {
+#pragma unroll
+				for (int j = 0; j < 4; j++) {
+					const auto v = __builtin_amdgcn_raw_buffer_load_b128(
+					        srs2, (int)(L.off_hdr + L.rec_plane * j + 16 * lane), 0, gcl::kSysAux);
+					pq[j] = make_uint4(v[0], v[1], v[2], v[3]);
+				}
+			}
+			pf = true;
+		}
 		const uint64_t t_data = L.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
 		me.offs[lane] = off;
 		me.fdir[lane] = fdir;
@@ -1998,8 +2063,8 @@ __global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
 		/* the next ticket, its own spec window */
 		kt++;
 		npoll = 0;
-		spec_end = __builtin_amdgcn_s_memrealtime() + L.spec_ticks;
-		t_done = spec_end - L.spec_ticks;
+		t_done = __builtin_amdgcn_s_memrealtime();
+		spec_end = (pf ? pis : t_done) + L.spec_ticks;
 	}
 	/* the writer drains what was posted, then leaves; the host stops
 	 * publishing on this word (one it reads without a HIP call per burst) */
@@ -3889,6 +3954,11 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 			lp.phase_down = d;
 		}
 	}
+	/* the next ticket's poll during classification: for workers that find
+	 * their bursts queued (more than the closed-loop few) */
+	lp.prefetch = cfg->workers > kLoopSpecIdleWorkers && !lp.hdr_rec ? kDefaultLoopPrefetch : 0;
+	if (const char *e = getenv("GCL_TUNE_LOOP_PREFETCH"))
+		lp.prefetch = atoi(e) != 0;
 	{
 		const uint64_t end = lp.off_verd + sizeof(LoopRec) * mb + (lp.off_hdr ? GCL_HDR_GRANULE * mb : 0);
 		lp.off_trans = (c->cfg.flags & GCL_CFG_TRANS_HASH) ? (uint32_t)end : 0;

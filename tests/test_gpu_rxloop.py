@@ -526,6 +526,50 @@ def test_rxloop_phase_delay(g, orc, phase, workers, lflag, monkeypatch):
         g.host_unregister(frames)
 
 
+@pytest.mark.parametrize("prefetch", [None, "0", "1"])
+@pytest.mark.parametrize("lflag", [0, 2])
+def test_rxloop_prefetch(g, orc, prefetch, lflag, monkeypatch):
+    """The next ticket's poll issued before a burst is classified
+    (GCL_TUNE_LOOP_PREFETCH; None: the default, on for stamped offsets with
+    more than two workers): bursts kept 12 deep across 4 workers, so that
+    polls find them queued, and drained now and then, so that they catch up;
+    every verdict equal to the oracle's."""
+    rng = np.random.default_rng(7950 + lflag + (len(prefetch) if prefetch else 0))
+    max_rt = 16
+    rts = random_runtimes(rng, max_rt, 12)
+    n = 2048
+    frames, flen, offs, olf, rss, fdir, hint = fuzz_batch(rng, n, rts, max_rt)
+    t = orc.Tables(max_rt, 1, 0, 0x09)
+    apply_runtimes(t, rts)
+    ve, _, _ = t.classify(frames, n, 0, offs=offs, olflags=olf, rss=rss, frames_len=flen)
+    clf = g.Classifier(0, max_rt, 1, 0, 0x09)
+    apply_runtimes(clf, rts)
+    g.host_register(frames)
+    if prefetch is not None:
+        monkeypatch.setenv("GCL_TUNE_LOOP_PREFETCH", prefetch)
+    loop = clf.rxloop(frames, slots=16, workers=4, region_len=flen, flags=LOOP_FLAGS[lflag](g))
+    try:
+        inflight = []
+        for k in range(600):
+            m = int(rng.integers(1, 65))
+            idx = rng.integers(0, n, size=m)
+            inflight.append((loop.submit(offs[idx], olf[idx], rss[idx]), m, idx))
+            if len(inflight) >= 12 or k % 97 == 96:
+                while inflight:  # every 97th burst: drain, so the workers catch up
+                    tk, mm, ii = inflight.pop(0)
+                    got = loop.wait(tk, mm)
+                    bad = np.nonzero(got != ve[ii])[0]
+                    assert not len(bad), f"ticket {tk}: {got[bad[0]]} vs {ve[ii][bad[0]]}"
+                    if len(inflight) < 8 and k % 97 != 96:
+                        break
+        for tk, mm, ii in inflight:
+            got = loop.wait(tk, mm)
+            assert (got == ve[ii]).all(), tk
+    finally:
+        loop.stop()
+        g.host_unregister(frames)
+
+
 def test_rxloop_release_incomplete(g):
     """gcl_rxloop_release refuses (-EAGAIN) a burst the GPU has not completed,
     so its slot is never handed to the next submit while still being written."""
