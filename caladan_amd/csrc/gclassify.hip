@@ -1860,8 +1860,10 @@ __global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
 			 * early, a step more.  Later finds are sparse traffic, whose
 			 * phase is its own: no change.  The steps are asymmetric, so
 			 * about phase_down / (phase_up + phase_down) of closed-loop
-			 * bursts pay the round trip a miss costs. */
-			if (polls_used == 1 && early)
+			 * bursts pay the round trip a miss costs.  (A loop without the
+			 * speculative window -- inline headers, GCL_TUNE_LOOP_SPEC=0
+			 * -- finds every burst "late": on time when at the first poll.) */
+			if (polls_used == 1 && kind != kLoopPollStale)
 				dly = dly > L.phase_down ? dly - L.phase_down : 0;
 			else if (polls_used <= 2)
 				dly = dly + L.phase_up < L.phase_max ? dly + L.phase_up : L.phase_max;

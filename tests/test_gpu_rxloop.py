@@ -489,7 +489,7 @@ def test_rxloop_stamp_wrap(g, orc, lflag, spec, use0, monkeypatch):
 
 
 @pytest.mark.parametrize("phase", [None, "0", "1000,1000,0", "1,1,1"])
-@pytest.mark.parametrize("workers,lflag", [(1, 2), (2, 2), (1, 0)])
+@pytest.mark.parametrize("workers,lflag", [(1, 2), (2, 2), (1, 0), (1, 1)])
 def test_rxloop_phase_delay(g, orc, phase, workers, lflag, monkeypatch):
     """The poll-phase delay (GCL_TUNE_LOOP_PHASE "max,up,down"; None: the
     default, on for loops of 1-2 workers) only moves when a ticket's first
