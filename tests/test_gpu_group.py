@@ -108,6 +108,38 @@ def test_gpu_group_rccl_one_device(g):
     grp.close()
 
 
+@pytest.mark.parametrize("xchg", ["rccl", "host"])
+def test_gpu_group_reset_orders_before_exchange(g, xchg):
+    """gcl_group_reset's zeroing completes before it returns, ahead of any
+    later work on the group's non-blocking streams: 25 rounds of classify,
+    exchange, reset, exchange, classify, exchange each read zero after the
+    reset and exactly one batch after it (round 5 caught a null-stream
+    hipMemset racing the next exchange's snapshot)."""
+    n, stride = (1 << 18) + 77, 64
+    fr = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
+    g.generate(g.WL_UDP64, n, stride, R, fr)
+    _, ce, se = single_run(g, fr, n, stride)
+    grp = g.Group([0], R, g.HASH_JENKINS, exchange=g.XCHG_RCCL if xchg == "rccl" else g.XCHG_HOST)
+    tables(grp)
+    v = torch.zeros(n * 8, dtype=torch.uint8, device="cuda")
+    shard = {"frames": fr, "n": n, "stride": stride}
+    try:
+        for k in range(25):
+            grp.classify([shard], [v])
+            grp.exchange()
+            grp.reset()
+            grp.exchange()
+            c, s, _ = grp.read()
+            assert not c.any() and not s.any(), (k, c, s)
+            grp.classify([shard], [v])
+            grp.exchange()
+            c, s, _ = grp.read()
+            assert (c == ce).all() and (s == se).all(), (k, c, ce)
+            grp.reset()
+    finally:
+        grp.close()
+
+
 @pytest.mark.parametrize("vbytes", [8, 2])
 def test_gpu_group_shards_two_contexts(g, orc, vbytes):
     """Two contexts on the one GPU, each classifying its round-robin shard
