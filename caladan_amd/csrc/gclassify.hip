@@ -1777,6 +1777,10 @@ __global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
 		 * thinks divergent puts every buffer load in a waterfall loop
 		 * (nslots is a power of two: a mask, not a 64-bit modulo) */
 		kt = lane0_u64(kt);
+		/* the context flags opaque here, so that the compiler keeps them in
+		 * registers rather than re-reading the kernel arguments (a scalar
+		 * load and its wait) between a hit and the classification */
+		asm volatile("" : "+s"(k.cflags), "+s"(k.default_flags));
 		const uint64_t t = lane0_u64(L.t0 + blockIdx.x + 1 + kt * L.workers);
 		uint8_t *slot = L.slots + ((t - 1) & (L.nslots - 1)) * (uint64_t)L.slot_bytes;
 		LoopSlotHdr *h = (LoopSlotHdr *)slot;
@@ -1853,21 +1857,6 @@ __global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
 		const uint64_t hit = L.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
 		const uint32_t kind = early ? kLoopPollEarly : (sp && nw <= 64) ? kLoopPollStale : kLoopPollLate;
 		const uint32_t polls_used = npoll;
-		if (L.phase_max) {
-			/* found whole by the first poll: it may have waited longer than
-			 * needed, so wait a step less next time; found by the second,
-			 * or with its records still being written: the first poll was
-			 * early, a step more.  Later finds are sparse traffic, whose
-			 * phase is its own: no change.  The steps are asymmetric, so
-			 * about phase_down / (phase_up + phase_down) of closed-loop
-			 * bursts pay the round trip a miss costs.  (A loop without the
-			 * speculative window -- inline headers, GCL_TUNE_LOOP_SPEC=0
-			 * -- finds every burst "late": on time when at the first poll.) */
-			if (polls_used == 1 && kind != kLoopPollStale)
-				dly = dly > L.phase_down ? dly - L.phase_down : 0;
-			else if (polls_used <= 2)
-				dly = dly + L.phase_up < L.phase_max ? dly + L.phase_up : L.phase_max;
-		}
 		Mbox64 &m = me.mbox[mb]; /* free: waited for after the last post */
 		if (img_seq != cur_seq) { /* this burst's table snapshot: copied into LDS */
 			const uint8_t *ib = L.img[img];
@@ -2010,8 +1999,8 @@ __global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
 			                                  k, hw, nullptr, lane, (uint64_t)lane, tb, m.p, cnt, 0, 64, pre);
 			if (L.stamps)
 				t_cls = __builtin_amdgcn_s_memrealtime();
-			const bool v4 = L.cflags & GCL_CFG_VERDICT4, v2 = L.cflags & GCL_CFG_VERDICT2;
-			const bool v1 = L.cflags & GCL_CFG_VERDICT1;
+			const bool v4 = k.cflags & GCL_CFG_VERDICT4, v2 = k.cflags & GCL_CFG_VERDICT2;
+			const bool v1 = k.cflags & GCL_CFG_VERDICT1;
 			const uint32_t hsh = v4 || v2 || v1 ? 0u : (uint32_t)v;
 			const uint32_t vlo = v1 ? (uint32_t)(uint8_t)v : v2 ? (uint32_t)(uint16_t)v
 			                   : v4 ? (uint32_t)v : (uint32_t)(v >> 32);
@@ -2062,6 +2051,26 @@ __global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
 		while (__hip_atomic_load(&me.mbox[mb].flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
 			__builtin_amdgcn_s_sleep(1);
 		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+		if (L.phase_max) {
+			/* The poll-phase delay, updated here, after the records went
+			 * out: its LoopParams reads are scalar loads the compiler
+			 * re-issues from the kernel arguments, which right after the
+			 * hit cost the burst ~0.1 us (profiles/r05_stages_phase.jsonl).
+			 * Found whole by the first poll: it may have waited longer
+			 * than needed, so wait a step less next time; found by the
+			 * second, or with its records still being written: the first
+			 * poll was early, a step more.  Later finds are sparse
+			 * traffic, whose phase is its own: no change.  The steps are
+			 * asymmetric, so about phase_down / (phase_up + phase_down)
+			 * of closed-loop bursts pay the round trip a miss costs.  (A
+			 * loop without the speculative window -- inline headers,
+			 * GCL_TUNE_LOOP_SPEC=0 -- finds every burst "late": on time
+			 * when at the first poll.) */
+			if (polls_used == 1 && kind != kLoopPollStale)
+				dly = dly > L.phase_down ? dly - L.phase_down : 0;
+			else if (polls_used <= 2)
+				dly = dly + L.phase_up < L.phase_max ? dly + L.phase_up : L.phase_max;
+		}
 		/* the next ticket, its own spec window */
 		kt++;
 		npoll = 0;
