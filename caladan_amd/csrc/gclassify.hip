@@ -1766,6 +1766,7 @@ __global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
 	 * ticks after the last burst's records went out */
 	uint32_t dly = 0;
 	uint64_t t_done = 0;
+	uint32_t ph_max = L.phase_max, ph_up = L.phase_up, ph_dn = L.phase_down;
 	/* the next ticket's poll, issued while this burst is classified
 	 * (L.prefetch): its word, offsets or records, issue time and window */
 	bool pf = false, psp = false;
@@ -1777,10 +1778,11 @@ __global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
 		 * thinks divergent puts every buffer load in a waterfall loop
 		 * (nslots is a power of two: a mask, not a 64-bit modulo) */
 		kt = lane0_u64(kt);
-		/* the context flags opaque here, so that the compiler keeps them in
-		 * registers rather than re-reading the kernel arguments (a scalar
-		 * load and its wait) between a hit and the classification */
-		asm volatile("" : "+s"(k.cflags), "+s"(k.default_flags));
+		/* the context flags and the delay's parameters opaque here, so that
+		 * the compiler keeps them in registers rather than re-reading the
+		 * kernel arguments (a scalar load and its wait) between a hit and
+		 * the classification, or between the store and the next poll */
+		asm volatile("" : "+s"(k.cflags), "+s"(k.default_flags), "+s"(ph_max), "+s"(ph_up), "+s"(ph_dn));
 		const uint64_t t = lane0_u64(L.t0 + blockIdx.x + 1 + kt * L.workers);
 		uint8_t *slot = L.slots + ((t - 1) & (L.nslots - 1)) * (uint64_t)L.slot_bytes;
 		LoopSlotHdr *h = (LoopSlotHdr *)slot;
@@ -2051,7 +2053,7 @@ __global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
 		while (__hip_atomic_load(&me.mbox[mb].flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
 			__builtin_amdgcn_s_sleep(1);
 		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-		if (L.phase_max) {
+		if (ph_max) {
 			/* The poll-phase delay, updated here, after the records went
 			 * out: its LoopParams reads are scalar loads the compiler
 			 * re-issues from the kernel arguments, which right after the
@@ -2067,9 +2069,9 @@ __global__ void __launch_bounds__(128) rxloop64_kernel(LoopParams L)
 			 * GCL_TUNE_LOOP_SPEC=0 -- finds every burst "late": on time
 			 * when at the first poll.) */
 			if (polls_used == 1 && kind != kLoopPollStale)
-				dly = dly > L.phase_down ? dly - L.phase_down : 0;
+				dly = dly > ph_dn ? dly - ph_dn : 0;
 			else if (polls_used <= 2)
-				dly = dly + L.phase_up < L.phase_max ? dly + L.phase_up : L.phase_max;
+				dly = dly + ph_up < ph_max ? dly + ph_up : ph_max;
 		}
 		/* the next ticket, its own spec window */
 		kt++;

@@ -1,0 +1,11 @@
+# round 5, the final tree (the delay's parameters and the context flags in registers; next-ticket poll during
+# classification for stamped-offset loops of > 2 workers): the whole GPU
+# suite, smoke and the driver's bench command
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests/ -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r05zk_gputests.log 2>&1 || { tail -30 gpurun_out/r05zk_gputests.log; exit 1; }
+tail -1 gpurun_out/r05zk_gputests.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r05zk_smoke.log 2>&1 || { tail -5 gpurun_out/r05zk_smoke.log; exit 1; }
+tail -1 gpurun_out/r05zk_smoke.log
+GCL_BENCH_DETAIL=gpurun_out/r05zk_bench_detail.json timeout -k 10 600 python bench.py > gpurun_out/r05zk_bench.json 2> gpurun_out/r05zk_bench.err || { tail -5 gpurun_out/r05zk_bench.err; exit 1; }
+wc -c gpurun_out/r05zk_bench.json
