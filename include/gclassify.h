@@ -603,7 +603,11 @@ struct gcl_rxloop_cfg {
  * little after its last verdict records, the delay following the host's
  * turnaround (up to 1.2 us; GCL_TUNE_LOOP_PHASE "max,up,down" in 10-ns
  * ticks, "0" off): a dataplane core that submits once it has seen the last
- * verdicts is sampled just after its submit rather than a round trip later. */
+ * verdicts is sampled just after its submit rather than a round trip later.
+ * In a loop of more than 2 workers without this flag (stamped offsets), a
+ * worker whose burst was already there at its first poll issues the next
+ * ticket's poll while it classifies that burst (GCL_TUNE_LOOP_PREFETCH=0/1
+ * overrides). */
 #define GCL_LOOP_HDR_RECORDS 0x2
 /* Measurement: lane 0 of the worker stores each burst's stage times into
  * the slot header after its records (gcl_rxloop_stamps). */
