@@ -1,8 +1,9 @@
 """Build the product shared libraries in-tree for gfx950.
 
-hipcc compiles the HIP kernels + C ABI (csrc/gclassify.hip); gcc compiles the
-host-side C (csrc/gcl_host.c, csrc/gcl_pcap.c); hipcc links them into
-caladan_amd/libgclassify.so.  The multi-GPU group (csrc/gcl_group.hip,
+hipcc compiles the HIP kernels + C ABI (csrc/gcl_*.hip: the context, the
+batch kernels, the persistent rx loop, the transports and allocation, the
+generator); gcc compiles the host-side C (csrc/gcl_host.c, csrc/gcl_pcap.c);
+hipcc links them into caladan_amd/libgclassify.so.  The multi-GPU group (csrc/gcl_group.hip,
 include/gcl_group.h) is its own library, caladan_amd/libgclgroup.so, linked
 against libgclassify.so and RCCL, so that a single-GPU dataplane does not
 load RCCL.  The .so files are git-ignored but travel to the GPU box with the
@@ -22,9 +23,9 @@ OBJ = os.path.join(HERE, "_obj")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("GCL_OFFLOAD_ARCH", "gfx950")
 
-SOURCES_HIP = ["gclassify.hip"]
+SOURCES_HIP = ["gcl_ctx.hip", "gcl_batch.hip", "gcl_loop.hip", "gcl_xfer.hip", "gcl_gen.hip"]
 SOURCES_C = ["gcl_host.c", "gcl_pcap.c"]
-DEPS = ["gcl_device.h", "../../include/gclassify.h", "../../include/gcl_host.h",
+DEPS = ["gcl_device.h", "gcl_kern.h", "gcl_ctx.h", "../../include/gclassify.h", "../../include/gcl_host.h",
         "../../include/gcl_pcap.h"]
 SOURCE_GROUP = "gcl_group.hip"
 DEPS_GROUP = ["../../include/gclassify.h", "../../include/gcl_group.h"]
@@ -45,7 +46,7 @@ def _stale(target, inputs):
 def build(force=False, verbose_resources=False):
     os.makedirs(OBJ, exist_ok=True)
     deps = [os.path.join(CSRC, d) for d in DEPS] + [os.path.abspath(__file__)]
-    objs = []
+    objs, cmds = [], []
     for src in SOURCES_HIP:
         s = os.path.join(CSRC, src)
         o = os.path.join(OBJ, src + ".o")
@@ -54,8 +55,12 @@ def build(force=False, verbose_resources=False):
                    "-Wall", "-Wno-unused-function", "-c", s, "-o", o]
             if verbose_resources:
                 cmd.insert(1, "-Rpass-analysis=kernel-resource-usage")
-            _run(cmd)
+            cmds.append(cmd)
         objs.append(o)
+    # the translation units are independent: compile them side by side
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=min(len(cmds), 4) or 1) as ex:
+        list(ex.map(_run, cmds))
     for src in SOURCES_C:
         s = os.path.join(CSRC, src)
         o = os.path.join(OBJ, src + ".o")
@@ -64,7 +69,13 @@ def build(force=False, verbose_resources=False):
                   "-Wno-unused-parameter", "-c", s, "-o", o])
         objs.append(o)
     if force or _stale(OUT, objs):
-        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT] + objs + ["-lm"])
+        # only the C ABI (gcl_*) is exported; the translation units' shared
+        # helpers (namespace gclk) stay internal to the library
+        vs = os.path.join(OBJ, "exports.map")
+        with open(vs, "w") as f:
+            f.write("{ global: gcl_*; local: *; };\n")
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT] + objs +
+             ["-lm", "-Wl,--version-script=" + vs])
     build_group(force)
     return OUT
 

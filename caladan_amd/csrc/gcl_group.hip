@@ -102,6 +102,7 @@ struct gcl_group {
 	                        communicators were aborted, and every later call
 	                        fails with -EIO (a collective may still hold the
 	                        snapshot slots; the communicators' state is unknown) */
+	uint32_t fault;      /* gcl_group_test_fault: GCL_GROUP_FAULT_* injected (tests) */
 };
 
 /* a group that must refuse all work */
@@ -353,10 +354,13 @@ extern "C" int gcl_group_open_v2(int ndev, const int *devs, const struct gcl_cfg
 	return 0;
 }
 
-/* The ABI-1 entry point (the 16-B struct gcl_group_cfg of rounds 1-3:
- * block, exchange, nstreams): binaries built against that header keep it,
- * with the default RCCL init bound; the current header maps gcl_group_open
- * to gcl_group_open_v2. */
+/* The exported gcl_group_open symbol reads the 16-B struct gcl_group_cfg of
+ * rounds 1-3 (block, exchange, nstreams), with the default RCCL init bound;
+ * the current header maps gcl_group_open to gcl_group_open_v2.  A binary
+ * built against the round-4 header (a 24-B struct with init_timeout_ms and a
+ * pad word, passed to this same symbol) loses its init_timeout_ms here until
+ * it is rebuilt against the current header: the two layouts cannot be told
+ * apart at run time. */
 struct gcl_group_cfg_v1 {
 	uint64_t block;
 	uint32_t exchange;
@@ -647,12 +651,12 @@ extern "C" int gcl_group_classify_host(struct gcl_group *g, const struct gcl_bat
 	return he.bad() ? -EIO : sr;
 }
 
-/* test hook: GCL_GROUP_FAULT=exchange makes every RCCL exchange's enqueue
- * fail as a timed-out one would (-ETIMEDOUT), to exercise fail_group */
-static bool fault_exchange()
+extern "C" int gcl_group_test_fault(struct gcl_group *g, uint32_t what)
 {
-	const char *e = getenv("GCL_GROUP_FAULT");
-	return e && !strcmp(e, "exchange");
+	if (!g || (what & ~(uint32_t)GCL_GROUP_FAULT_EXCHANGE))
+		return -EINVAL;
+	g->fault = what;
+	return 0;
 }
 
 extern "C" int gcl_group_exchange(struct gcl_group *g)
@@ -695,8 +699,8 @@ extern "C" int gcl_group_exchange(struct gcl_group *g)
 		/* non-blocking communicators: the enqueue itself may still be in
 		 * progress (the first all-gather connects the ring) */
 		int w = !ok ? -EIO : e == ncclInProgress ? comms_wait(g, mono_ms() + g->timeout_ms) : 0;
-		if (!w && fault_exchange())
-			w = -ETIMEDOUT;
+		if (!w && (g->fault & GCL_GROUP_FAULT_EXCHANGE))
+			w = -ETIMEDOUT; /* injected: as a timed-out enqueue */
 		if (w) {
 			/* the all-gather may still be enqueued on D.xs, reading and
 			 * writing slot b: abort the communicators and refuse all
@@ -778,7 +782,9 @@ extern "C" int gcl_group_sync(struct gcl_group *g)
 {
 	if (!g)
 		return -EINVAL;
-	int ret = 0;
+	/* a failed group's streams are still drained (close relies on it), but
+	 * the call reports the failure like every other one */
+	int ret = broken(g) ? -EIO : 0;
 	for (int i = 0; i < g->n; i++) {
 		gcl_group::Dev &D = g->d[i];
 		if (D.dev < 0 || hipSetDevice(D.dev) != hipSuccess)
@@ -796,6 +802,8 @@ extern "C" int gcl_group_reset(struct gcl_group *g)
 {
 	if (!g)
 		return -EINVAL;
+	if (broken(g))
+		return -EIO; /* the accumulators may still feed an aborted all-gather */
 	int ret = gcl_group_sync(g);
 	for (int i = 0; i < g->n && !ret; i++) {
 		gcl_group::Dev &D = g->d[i];

@@ -31,6 +31,7 @@ V2_Q_MASK, V2_KIND, V2_DELIVER, V2_WAKE, V2_OTHER, V2_QUEUES = 0x3FFF, 0xC000, 0
 # GCL_CFG_VERDICT1: u8 q (DELIVER or WAKE, unmarked) or V1_OTHER | action
 V1_Q_MASK, V1_OTHER, V1_QUEUES = 0x7F, 0x80, 0x80
 PAIR_NEW_READS, PAIR_NEW_WRITES, PAIR_TRIES, PAIR_RUN = 0x1, 0x2, 24, 2
+PAIR_QUIET, PAIR_VERBOSE = 0x10000, 0x20000
 
 F_RSS_HASH, F_FDIR_ID = 0x01, 0x02
 F_IP_CKSUM_MASK, F_IP_CKSUM_UNKNOWN, F_IP_CKSUM_BAD = 0x0C, 0x00, 0x04
@@ -129,6 +130,21 @@ class GclRxloopCfg(ctypes.Structure):
 LOOP_INLINE_HDRS = 0x1
 LOOP_HDR_RECORDS = 0x2
 LOOP_STAMPS = 0x4
+
+
+class GclTune(ctypes.Structure):
+    """struct gcl_tune: test / A-B overrides of the library's defaults
+    (GCL_TUNE_AUTO = -1 everywhere: the library's own choice)."""
+    _fields_ = [("size", ctypes.c_uint32), ("tables", ctypes.c_int32), ("depth", ctypes.c_int32),
+                ("threads", ctypes.c_int32), ("grid", ctypes.c_int32), ("blocks_per_cu", ctypes.c_int32),
+                ("defer", ctypes.c_int32), ("pair_lean", ctypes.c_int32), ("loop64", ctypes.c_int32),
+                ("loop_lean", ctypes.c_int32), ("loop_spec", ctypes.c_int32),
+                ("loop_phase_max", ctypes.c_int32), ("loop_phase_up", ctypes.c_int32),
+                ("loop_phase_down", ctypes.c_int32), ("loop_prefetch", ctypes.c_int32),
+                ("debug", ctypes.c_uint32), ("loop_t0", ctypes.c_uint64)]
+
+
+TUNE_AUTO = -1
 
 
 class GclVerdict(ctypes.Structure):
@@ -235,6 +251,9 @@ def _load():
         "gcl_rxloop_poll_stats": (i32, [vp, vp]),
         "gcl_rxloop_lean_bursts": (i32, [vp, vp]),
         "gcl_rxloop_trans": (i32, [vp, ctypes.c_int64, vp]),
+        "gcl_tune_init": (None, [ctypes.POINTER(GclTune)]),
+        "gcl_ctx_tune": (i32, [vp, ctypes.POINTER(GclTune)]),
+        "gcl_abi_version": (i32, []),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -281,6 +300,25 @@ def _frames_len(frames, frames_len):
     if frames_len < 0 or frames_len > size:
         raise ValueError(f"frames_len {frames_len} exceeds the {size}-byte frame buffer")
     return frames_len
+
+
+def make_tune(**kw):
+    """A struct gcl_tune with the library's defaults (gcl_tune_init) and the
+    fields in @kw set; loop_phase=(max, up, down) sets the three phase fields
+    together (0 as max: off)."""
+    t = GclTune()
+    lib.gcl_tune_init(ctypes.byref(t))
+    ph = kw.pop("loop_phase", None)
+    if ph is not None:
+        ph = tuple(ph) if not isinstance(ph, int) else (ph,)
+        t.loop_phase_max = ph[0]
+        t.loop_phase_up = ph[1] if len(ph) > 1 else 16
+        t.loop_phase_down = ph[2] if len(ph) > 2 else 1
+    for k, v in kw.items():
+        if not hasattr(t, k) or k == "size":
+            raise AttributeError(f"struct gcl_tune has no field {k}")
+        setattr(t, k, int(v))
+    return t
 
 
 def jenkins_hash(key: bytes) -> int:
@@ -480,7 +518,7 @@ class Classifier:
 
     def __init__(self, device=0, max_runtimes=16, hash_mode=HASH_JENKINS, flags=0,
                  default_olflags=F_RSS_HASH | F_IP_CKSUM_GOOD, rss_key=CALADAN_RSS_KEY,
-                 thread_bits=0):
+                 thread_bits=0, tune=None):
         if isinstance(hash_mode, str):
             hash_mode = HASH_MODES[hash_mode]
         cfg = GclCfg(max_runtimes=max_runtimes, hash_mode=hash_mode, flags=flags,
@@ -494,6 +532,15 @@ class Classifier:
         self.thread_bits = thread_bits
         self._ctx = ctypes.c_void_p()
         _check(lib.gcl_open(device, ctypes.byref(cfg), ctypes.byref(self._ctx)), "gcl_open")
+        if tune:
+            self.tune(**tune)
+
+    def tune(self, **kw):
+        """gcl_ctx_tune: the library's defaults with the fields in @kw
+        overridden (make_tune); no arguments: back to the defaults.  Batch
+        fields apply from the next classify, loop fields from the next rxloop."""
+        t = make_tune(**kw)
+        return _check(lib.gcl_ctx_tune(self._ctx, ctypes.byref(t)), "gcl_ctx_tune")
 
     def close(self):
         loop = getattr(self, "_loop", None)
@@ -603,6 +650,7 @@ def version():
 GROUP_LIB_PATH = os.path.join(HERE, "libgclgroup.so")
 GROUP_BLOCK = 64 << 10
 XCHG_RCCL, XCHG_HOST = 0, 1
+GROUP_FAULT_EXCHANGE = 0x1
 
 
 class GclGroupCfg(ctypes.Structure):
@@ -650,6 +698,7 @@ def group_lib():
         "gcl_group_read": (i32, [vp, vp, vp, vp]),
         "gcl_group_reset": (i32, [vp]),
         "gcl_group_sync": (i32, [vp]),
+        "gcl_group_test_fault": (i32, [vp, u32]),
     }
     for name, (res, args) in sig.items():
         f = getattr(gl, name)
@@ -769,6 +818,11 @@ class Group:
 
     def sync(self):
         return _check(group_lib().gcl_group_sync(self._g), "gcl_group_sync")
+
+    def test_fault(self, what=GROUP_FAULT_EXCHANGE):
+        """gcl_group_test_fault (tests): every later RCCL exchange fails as a
+        timed-out enqueue would; 0 clears it."""
+        return _check(group_lib().gcl_group_test_fault(self._g, what), "gcl_group_test_fault")
 
 
 __all__ = [n for n in dir() if not n.startswith("_")]

@@ -49,10 +49,13 @@ struct gcl_group_cfg {
 	uint32_t size;     /* sizeof(struct gcl_group_cfg): GCL_GROUP_CFG_INIT sets it;
 	                      gcl_group_open refuses another value (-EINVAL) */
 };
-/* ABI 2 (round 4) added init_timeout_ms and size.  Binaries built against
- * the ABI-1 header (a 16-B struct) keep calling the exported symbol
- * gcl_group_open, which reads only the ABI-1 fields; this header maps the
- * name to gcl_group_open_v2, which reads the whole struct. */
+/* The struct's history: rounds 1-3, 16 B (block, exchange, nstreams) through
+ * the symbol gcl_group_open; round 4, 24 B (+ init_timeout_ms and a pad word)
+ * through the same symbol; round 5 (GCL_GROUP_ABI 2, library ABI 5), the pad
+ * word became `size` and the entry point gcl_group_open_v2, to which this
+ * header maps the name.  The exported gcl_group_open reads only the 16-B
+ * fields: a binary built against the round-4 header loses init_timeout_ms
+ * (the default bound applies) until it is rebuilt against this header. */
 #define GCL_GROUP_ABI 2
 #define GCL_GROUP_CFG_INIT { 0, GCL_XCHG_RCCL, 0, 0, sizeof(struct gcl_group_cfg) }
 #define GCL_GROUP_INIT_TIMEOUT_MS 60000
@@ -139,16 +142,23 @@ int gcl_group_classify_host(struct gcl_group *g, const struct gcl_batch *hb,
  * init_timeout_ms (-ETIMEDOUT) aborts every communicator (ncclCommAbort) and
  * leaves the group failed: every later call except close returns -EIO (the
  * all-gather may still hold the exchange's buffers, and the communicators
- * are in an unknown state).  GCL_GROUP_FAULT=exchange in the environment
- * makes every RCCL exchange fail that way (tests).
+ * are in an unknown state).  gcl_group_test_fault makes every RCCL
+ * exchange fail that way (tests).
  */
 int gcl_group_exchange(struct gcl_group *g);
 int gcl_group_read(struct gcl_group *g, uint64_t *node_counts, uint64_t *node_stats,
                    uint64_t *per_gpu);
-/* Zero every GPU's accumulated counters (synchronises). */
+/* Zero every GPU's accumulated counters (synchronises); -EIO on a failed group. */
 int gcl_group_reset(struct gcl_group *g);
-/* Wait for everything enqueued on every GPU. */
+/* Wait for everything enqueued on every GPU; a failed group's streams are
+ * still drained, and the call returns -EIO. */
 int gcl_group_sync(struct gcl_group *g);
+
+/* Test hook: make every later RCCL exchange of @g fail as a timed-out
+ * enqueue would (GCL_GROUP_FAULT_EXCHANGE), to exercise the sticky failure
+ * above; 0 clears it.  0 or -EINVAL.  Not for production use. */
+#define GCL_GROUP_FAULT_EXCHANGE 0x1
+int gcl_group_test_fault(struct gcl_group *g, uint32_t what);
 
 #ifdef __cplusplus
 }

@@ -171,9 +171,10 @@ enum gcl_action {
  * that indexes kthread rings with .thread must check gcl_abi_version() >= 4
  * and read flow_tbl[.thread] itself (or use the gcl_host_deliver* post-pass).
  */
-#define GCL_ABI_VERSION 5
+#define GCL_ABI_VERSION 6
 /* GCL_ABI_VERSION of the library actually loaded: 4 = verdict .thread is
- * the flow-table slot; 5 = gcl_group_open_v2 and struct gcl_group_cfg.size */
+ * the flow-table slot; 5 = gcl_group_open_v2 and struct gcl_group_cfg.size;
+ * 6 = struct gcl_tune / gcl_ctx_tune (the library reads no environment) */
 int gcl_abi_version(void);
 struct gcl_verdict {
 	uint32_t hash;    /* steering hash (hash.rss, or the computed flow hash) */
@@ -396,6 +397,47 @@ int gcl_classify_ex(struct gcl_ctx *ctx, const struct gcl_batch *b, const struct
 int gcl_access_probe(struct gcl_ctx *ctx, const struct gcl_batch *b, void *out, uint32_t vbytes,
                      void *hip_stream);
 
+/*
+ * Test and A/B overrides of the library's measured defaults.  A dataplane
+ * never needs them: with every field GCL_TUNE_AUTO (gcl_tune_init) the
+ * library makes its own choice, and no environment variable changes it.  The
+ * parity tests use them to drive every launch shape and loop form through
+ * the same code, tools/ for its A/Bs.
+ *
+ * gcl_tune_init  - every field GCL_TUNE_AUTO, loop_t0 and debug 0, size set.
+ * gcl_ctx_tune   - copy @t into @ctx (NULL: back to the defaults); 0, or
+ *                  -EINVAL for a wrong size or a field out of its range.  The
+ *                  batch fields apply from the next gcl_classify*, the loop
+ *                  fields from the next gcl_rxloop_start.
+ */
+#define GCL_TUNE_AUTO (-1)
+struct gcl_tune {
+	uint32_t size;           /* sizeof(struct gcl_tune) */
+	/* batch kernels */
+	int32_t tables;          /* 0: tables in LDS when they fit, 1: in HBM */
+	int32_t depth;           /* tiles in flight per block: 1 or 2 */
+	int32_t threads;         /* lanes (packets) per block: 256, 512 or 1024 */
+	int32_t grid;            /* blocks per launch (default: the persistent grid) */
+	int32_t blocks_per_cu;   /* cap on blocks per CU */
+	int32_t defer;           /* dense 1-/2-B verdicts: 0 stored per packet, 1 kept in LDS +
+	                            registers and written after the reads where that takes
+	                            <= 2 writes per block (default), 2 always */
+	int32_t pair_lean;       /* classify_pair_kernel: plain-IPv4 waves on the lean path (1) */
+	/* the persistent loop */
+	int32_t loop64;          /* 0: bursts <= 64 through the general loop kernel */
+	int32_t loop_lean;       /* plain-IPv4 bursts on the lean path (1) */
+	int32_t loop_spec;       /* speculative window in 10-ns ticks (400; 1 ms with <= 2 workers) */
+	int32_t loop_phase_max;  /* poll-phase delay: ceiling in ticks (0 off), set with the two below */
+	int32_t loop_phase_up;   /* its step up (> 0) */
+	int32_t loop_phase_down; /* its step down (<= up) */
+	int32_t loop_prefetch;   /* the next ticket's poll during classification (0 / 1) */
+	uint32_t debug;          /* 1: loop diagnostics to stderr */
+	uint64_t loop_t0;        /* tickets start after loop_t0 (rounded down to a multiple of the
+	                            ring's slots): tests of the stamps' wrap */
+};
+void gcl_tune_init(struct gcl_tune *t);
+int gcl_ctx_tune(struct gcl_ctx *ctx, const struct gcl_tune *t);
+
 /* Host CRC32C step with the crc32q contract (no inversion, inc/asm/ops.h:77-80)
  * and the two transport hashes, for the runtime side. */
 uint32_t gcl_crc32c_u64(uint32_t crc, uint64_t val);
@@ -502,7 +544,8 @@ int gcl_dev_free(void *p);
  * run.  Candidates and spacers together hold at most 60% of the free device
  * memory; all but the kept buffer are freed before returning.  When no second
  * class shows up the fastest candidate is kept, @info->classes is 1 and a
- * warning goes to stderr (GCL_PAIR_QUIET silences it).
+ * warning goes to stderr (the GCL_PAIR_QUIET flag silences it;
+ * GCL_PAIR_VERBOSE prints every candidate's probe).
  *
  * GCL_PAIR_NEW_READS: the new buffer is the one stream-read (frames) and
  *                     @partner the one written (verdicts);
@@ -519,6 +562,8 @@ int gcl_dev_free(void *p);
 #define GCL_PAIR_NEW_WRITES 0x2
 #define GCL_PAIR_VBYTES(b)  ((uint32_t)(b) << 8)
 #define GCL_PAIR_VBYTES_OF(f) (((f) >> 8) & 0xFF)
+#define GCL_PAIR_QUIET      0x10000
+#define GCL_PAIR_VERBOSE    0x20000
 #define GCL_PAIR_TRIES      24
 #define GCL_PAIR_RUN        2
 struct gcl_pair_info {
@@ -596,18 +641,16 @@ struct gcl_rxloop_cfg {
  * instead of two.  Ports past byte 43 (IHL >= 7) are read from the region.
  * Exclusive with GCL_LOOP_INLINE_HDRS (-EINVAL).  A worker polls the records
  * (or, without this flag, the stamped offsets) during the first 4 us of a
- * wait, or the first 1 ms in a loop of 1 or 2 workers (GCL_TUNE_LOOP_SPEC
- * in the environment at gcl_rxloop_start: the window in 10-ns ticks); a
- * burst found later is read after its word.  In a loop of 1 or 2 workers
+ * wait, or the first 1 ms in a loop of 1 or 2 workers (gcl_tune.loop_spec);
+ * a burst found later is read after its word.  In a loop of 1 or 2 workers
  * with bursts of <= 64 a worker issues the first poll of each ticket a
  * little after its last verdict records, the delay following the host's
- * turnaround (up to 1.2 us; GCL_TUNE_LOOP_PHASE "max,up,down" in 10-ns
- * ticks, "0" off): a dataplane core that submits once it has seen the last
- * verdicts is sampled just after its submit rather than a round trip later.
- * In a loop of more than 2 workers without this flag (stamped offsets), a
- * worker whose burst was already there at its first poll issues the next
- * ticket's poll while it classifies that burst (GCL_TUNE_LOOP_PREFETCH=0/1
- * overrides). */
+ * turnaround (up to 1.2 us; gcl_tune.loop_phase_*): a dataplane core that
+ * submits once it has seen the last verdicts is sampled just after its
+ * submit rather than a round trip later.  In a loop of more than 2 workers
+ * without this flag (stamped offsets), a worker whose burst was already
+ * there at its first poll issues the next ticket's poll while it classifies
+ * that burst (gcl_tune.loop_prefetch). */
 #define GCL_LOOP_HDR_RECORDS 0x2
 /* Measurement: lane 0 of the worker stores each burst's stage times into
  * the slot header after its records (gcl_rxloop_stamps). */

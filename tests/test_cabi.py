@@ -717,3 +717,38 @@ def test_python_constants_match_header_defines(g):
     assert len(mirrored) >= 25 and "LOOP_HDR_RECORDS" in mirrored, sorted(mirrored)
     bad = {k: (v, getattr(g, k)) for k, v in mirrored.items() if getattr(g, k) != v}
     assert not bad, bad
+
+
+def test_tune_struct_and_defaults(g):
+    """struct gcl_tune (the tests' and tools' overrides since the library
+    stopped reading GCL_TUNE_* from the environment): the layout the header
+    declares, every field GCL_TUNE_AUTO after gcl_tune_init, and
+    gcl_ctx_tune refusing a NULL context."""
+    assert ctypes.sizeof(g.GclTune) == 72
+    t = g.make_tune()
+    assert t.size == 72 and t.loop_t0 == 0 and t.debug == 0
+    for name, _ in g.GclTune._fields_:
+        if name not in ("size", "loop_t0", "debug"):
+            assert getattr(t, name) == g.TUNE_AUTO, name
+    t = g.make_tune(defer=2, threads=512, loop_phase=(120, 8, 1))
+    assert (t.defer, t.threads, t.loop_phase_max, t.loop_phase_up, t.loop_phase_down) == (2, 512, 120, 8, 1)
+    with pytest.raises(AttributeError):
+        g.make_tune(no_such_knob=1)
+    assert g.lib.gcl_ctx_tune(None, ctypes.byref(t)) == -22
+    assert g.lib.gcl_abi_version() == 6
+
+
+def test_library_reads_no_environment(g):
+    """No getenv anywhere in the product's sources, and neither library
+    imports one: production behaviour cannot be changed from the
+    environment; overrides go through gcl_ctx_tune."""
+    import subprocess
+    csrc = os.path.join(ROOT, "caladan_amd", "csrc")
+    for f in sorted(os.listdir(csrc)):
+        src = re.sub(r"/\*.*?\*/", "", open(os.path.join(csrc, f)).read(), flags=re.S)
+        assert "getenv" not in src, f
+    for so in (g.LIB_PATH, g.GROUP_LIB_PATH):
+        if not os.path.exists(so):
+            continue
+        und = subprocess.run(["nm", "-D", "--undefined-only", so], capture_output=True, text=True).stdout
+        assert not re.search(r"\b(secure_)?getenv\b", und), so

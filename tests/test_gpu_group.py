@@ -422,13 +422,13 @@ def test_gpu_group_rccl_init_bounded(g):
     grp.close()
 
 
-def test_gpu_group_failed_exchange_is_sticky(g, monkeypatch):
+def test_gpu_group_failed_exchange_is_sticky(g):
     """An exchange whose RCCL enqueue fails or times out (injected with
-    GCL_GROUP_FAULT=exchange) aborts the communicators and leaves the group
+    gcl_group_test_fault) aborts the communicators and leaves the group
     failed: the exchange returns -ETIMEDOUT, and every later classify,
-    exchange, read and table change returns -EIO instead of reusing the
-    exchange's buffers or the aborted communicators; close still works,
-    and a new group runs normally."""
+    exchange, read, table change, reset and sync returns -EIO instead of
+    reusing the exchange's buffers or the aborted communicators (sync still
+    drains the streams); close still works, and a new group runs normally."""
     grp = g.Group([0], R, g.HASH_JENKINS, init_timeout_ms=5000)
     tables(grp)
     n = 4096
@@ -436,14 +436,15 @@ def test_gpu_group_failed_exchange_is_sticky(g, monkeypatch):
     g.generate(g.WL_UDP64, n, 64, R, fr)
     v = torch.zeros(n * 8, dtype=torch.uint8, device="cuda")
     grp.classify([{"frames": fr, "n": n, "stride": 64}], [v])
-    monkeypatch.setenv("GCL_GROUP_FAULT", "exchange")
+    grp.test_fault(g.GROUP_FAULT_EXCHANGE)
     with pytest.raises(OSError) as e:
         grp.exchange()
     assert e.value.errno == 110  # ETIMEDOUT
-    monkeypatch.delenv("GCL_GROUP_FAULT")
+    grp.test_fault(0)
     for call in (lambda: grp.classify([{"frames": fr, "n": n, "stride": 64}], [v]),
                  grp.exchange, grp.read,
-                 lambda: grp.runtime_set(0, g.runtime_ip(0), 8, 8, g.steer_flows(8, list(range(8))))):
+                 lambda: grp.runtime_set(0, g.runtime_ip(0), 8, 8, g.steer_flows(8, list(range(8)))),
+                 grp.reset, grp.sync):
         with pytest.raises(OSError) as e:
             call()
         assert e.value.errno == 5, call  # EIO

@@ -1,5 +1,7 @@
 """GPU parity: the HIP classifier through the C ABI vs the CPU oracle and the
 golden fixtures.  Bit-exact on every verdict, count and counter."""
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -138,14 +140,14 @@ def test_gpu_fuzz_misaligned_offsets(g, orc, misalign, mode):
 @pytest.mark.parametrize("tables", ["lds", "global"])
 @pytest.mark.parametrize("misalign", ["mbuf", "mixed", "lineend"])
 @pytest.mark.parametrize("mode", [0, 1, 2])
-def test_gpu_general_kernels_fuzz(g, orc, monkeypatch, misalign, mode, tables):
+def test_gpu_general_kernels_fuzz(g, orc, misalign, mode, tables):
     """The GENERAL kernel (classify_pair_kernel) on the misaligned-offset
     fuzz: frames at every 16-B phase, frames that are not 4-B aligned
     (bytewise), headers cut at a line end, frames straddling frames_len,
     IHL > 5 ports and ARP target IPs read from the frame, loopback hints,
     FDIR marks and the transport pre-hash, in all three hash modes, an odd
     packet count, with the tables in LDS and forced to global memory
-    (GCL_TUNE_TABLES=1)."""
+    (gcl_tune.tables = 1)."""
     kernel = "pair"
     rng = np.random.default_rng(9300 + 10 * mode + {"mbuf": 0, "mixed": 1, "lineend": 2}[misalign]
                                 + 100 * (tables == "global") + 1000 * 2)
@@ -156,14 +158,8 @@ def test_gpu_general_kernels_fuzz(g, orc, monkeypatch, misalign, mode, tables):
     key = bytes(rng.integers(0, 256, size=40, dtype=np.uint8))
     t = orc.Tables(1024, mode, g.CFG_TRANS_HASH, 0x09, key)
     apply_runtimes(t, rts)
-    env = {"GCL_TUNE_TABLES": "1"} if tables == "global" else {}
-    for kk, vv in env.items():
-        monkeypatch.setenv(kk, vv)
-    try:
-        clf = g.Classifier(0, 1024, mode, g.CFG_TRANS_HASH, 0x09, key)
-    finally:
-        for kk in env:
-            monkeypatch.delenv(kk)
+    clf = g.Classifier(0, 1024, mode, g.CFG_TRANS_HASH, 0x09, key,
+                       tune={"tables": 1} if tables == "global" else None)
     apply_runtimes(clf, rts)
     ve, ce, se, tre = t.classify(frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir_hi=fdir,
                                  frames_len=flen, dst_hint=hint, trans=True)
@@ -310,12 +306,11 @@ DEFER_FORMS = {0: "per-packet stores", 1: "deferred (<= 2 writes per block, the 
 
 @pytest.mark.parametrize("defer", sorted(DEFER_FORMS))
 @pytest.mark.parametrize("wl,R,T,vb", [(0, 16, 8, 1), (0, 16, 8, 2), (1, 1024, 4, 2)])
-def test_gpu_dense_narrow_verdicts(g, orc, wl, R, T, vb, defer, monkeypatch):
-    """Dense slots' 1- and 2-B verdicts in every form (GCL_TUNE_DEFER): the
+def test_gpu_dense_narrow_verdicts(g, orc, wl, R, T, vb, defer):
+    """Dense slots' 1- and 2-B verdicts in every form (gcl_tune.defer): the
     tile kernel's write-through byte and short stores per packet, or kept in
     LDS and written 16 B per lane in batches; the partial last tile
     included; 256- (udp64) and 512-lane (1024-runtime tcp1500) blocks."""
-    monkeypatch.setenv("GCL_TUNE_DEFER", str(defer))
     stride = {0: 64, 1: 1536}[wl]
     n = 40000 + 77
     df = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
@@ -325,7 +320,8 @@ def test_gpu_dense_narrow_verdicts(g, orc, wl, R, T, vb, defer, monkeypatch):
     frames = df.cpu().numpy()
     del df
     tb = 3 if vb == 1 else 4
-    clf = g.Classifier(0, R, g.HASH_JENKINS, g.CFG_VERDICT1 if vb == 1 else g.CFG_VERDICT2, thread_bits=tb)
+    clf = g.Classifier(0, R, g.HASH_JENKINS, g.CFG_VERDICT1 if vb == 1 else g.CFG_VERDICT2, thread_bits=tb,
+                       tune={"defer": defer})
     t = orc.Tables(R, g.HASH_JENKINS, 0, g.F_RSS_HASH | g.F_IP_CKSUM_GOOD)
     for r in range(R):
         act = r % T
@@ -340,31 +336,30 @@ def test_gpu_dense_narrow_verdicts(g, orc, wl, R, T, vb, defer, monkeypatch):
 
 
 @pytest.mark.parametrize("defer,env", [
-    (1, {}), (2, {"GCL_TUNE_GRID": "3"}), (2, {"GCL_TUNE_GRID": "5", "GCL_TUNE_DEPTH": "1"}),
-    (1, {"GCL_TUNE_BLOCKS_PER_CU": "1", "GCL_TUNE_GRID": "301"}),
-    (2, {"GCL_TUNE_THREADS": "512", "GCL_TUNE_GRID": "7"}), (2, {"GCL_TUNE_THREADS": "1024", "GCL_TUNE_GRID": "7"}),
-    (1, {"GCL_TUNE_GRID": "20"}), (1, {"GCL_TUNE_GRID": "40"}), (1, {"GCL_TUNE_GRID": "70"}),
-    (1, {"GCL_TUNE_GRID": "20", "GCL_TUNE_DEPTH": "1"}), (1, {"GCL_TUNE_THREADS": "512", "GCL_TUNE_GRID": "12"}),
-    (1, {"GCL_TUNE_TABLES": "1", "GCL_TUNE_GRID": "40"}), (2, {"GCL_TUNE_TABLES": "1", "GCL_TUNE_GRID": "9"})])
+    (1, {}), (2, {"grid": 3}), (2, {"grid": 5, "depth": 1}),
+    (1, {"blocks_per_cu": 1, "grid": 301}),
+    (2, {"threads": 512, "grid": 7}), (2, {"threads": 1024, "grid": 7}),
+    (1, {"grid": 20}), (1, {"grid": 40}), (1, {"grid": 70}),
+    (1, {"grid": 20, "depth": 1}), (1, {"threads": 512, "grid": 12}),
+    (1, {"tables": 1, "grid": 40}), (2, {"tables": 1, "grid": 9})])
 @pytest.mark.parametrize("vb", [1, 2])
-def test_gpu_dense_deferred_flushes(g, orc, vb, defer, env, monkeypatch):
+def test_gpu_dense_deferred_flushes(g, orc, vb, defer, env):
     """The tile kernel's LDS verdict buffer when a block walks more tiles
-    than it holds (few blocks: GCL_TUNE_GRID, GCL_TUNE_DEFER=2): full
+    than it holds (few blocks: gcl_tune.grid, gcl_tune.defer = 2): full
     buffers written inside the loop, a partial one at the end, the batch's
     ragged last tile cut at n; the registers past a full buffer partly
     filled (grid 40), full and written out inside the loop (grid 20 / 12),
     or unused (grid 70 at 1-B verdicts); DEPTH 1 and 2; 256-, 512- and
     1024-lane tiles; tables in LDS and in HBM -- against the oracle on a
     1 Mi + 77-packet udp64 batch, with its counts and counters."""
-    for kk, vv in {"GCL_TUNE_DEFER": str(defer), **env}.items():
-        monkeypatch.setenv(kk, vv)
     R, T, stride = 16, 8, 64
     n = (1 << 20) + 77
     df = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
     g.generate(0, n, stride, R, df, seed=29)
     frames = df.cpu().numpy()
     tb = 3 if vb == 1 else 4
-    clf = g.Classifier(0, R, g.HASH_JENKINS, g.CFG_VERDICT1 if vb == 1 else g.CFG_VERDICT2, thread_bits=tb)
+    clf = g.Classifier(0, R, g.HASH_JENKINS, g.CFG_VERDICT1 if vb == 1 else g.CFG_VERDICT2, thread_bits=tb,
+                       tune={"defer": defer, **env})
     t = orc.Tables(R, g.HASH_JENKINS, 0, g.F_RSS_HASH | g.F_IP_CKSUM_GOOD)
     for r in range(R):
         act = (r * 3) % (T + 1)
@@ -908,14 +903,13 @@ def test_gpu_ingress_pool_geometry(g, orc):
 
 @pytest.mark.parametrize("pair_lean", [1, 0])
 @pytest.mark.parametrize("mode,vb", [(0, 2), (0, 1), (1, 8), (1, 2), (2, 4), (2, 1)])
-def test_gpu_pair_lean_waves(g, orc, mode, vb, pair_lean, monkeypatch):
-    """classify_pair_kernel's lean path (GCL_TUNE_PAIR_LEAN, on by default):
+def test_gpu_pair_lean_waves(g, orc, mode, vb, pair_lean):
+    """classify_pair_kernel's lean path (gcl_tune.pair_lean, on by default):
     a wave whose packets are all plain IPv4 takes classify_lean, a wave with
     one FDIR-marked packet (every 997th, no fdir array: mark 0) or without the
     NIC's hash flag on some frames takes the same counters through either
     path -- mbuf-pool offsets with ol_flags and hash.rss, every hash mode and
     verdict width, both settings, bit-exact against the oracle."""
-    monkeypatch.setenv("GCL_TUNE_PAIR_LEAN", str(pair_lean))
     n, R, T, P = 40000, 16, 8, 8192
     hdr, olf_p, rss_p = orc.generate(0, P, 64, R)
     rng = np.random.default_rng(23 + mode + 10 * vb)
@@ -931,7 +925,8 @@ def test_gpu_pair_lean_waves(g, orc, mode, vb, pair_lean, monkeypatch):
     tb = g.thread_bits_for(R, T) if vb <= 2 else 0
     cflags = {8: 0, 4: g.CFG_VERDICT4, 2: g.CFG_VERDICT2, 1: g.CFG_VERDICT1}[vb]
     t = orc.Tables(R, mode, 0, 0x09, g.CALADAN_RSS_KEY)
-    clf = g.Classifier(0, R, mode, cflags, 0x09, g.CALADAN_RSS_KEY, thread_bits=tb)
+    clf = g.Classifier(0, R, mode, cflags, 0x09, g.CALADAN_RSS_KEY, thread_bits=tb,
+                       tune={"pair_lean": pair_lean})
     for r in range(R):
         act = (r * 5) % (T + 1)
         fl = orc.steer_flows(T, list(range(act))) if act else None
@@ -1102,8 +1097,8 @@ def test_gpu_tables_past_lds(g, orc, mode):
         g.host_unregister(frames)
 
 
-def test_gpu_tables_in_hbm_forced(g, orc, monkeypatch):
-    """GCL_TUNE_TABLES=1 keeps small tables in HBM too: same verdicts."""
+def test_gpu_tables_in_hbm_forced(g, orc):
+    """gcl_tune.tables = 1 keeps small tables in HBM too: same verdicts."""
     rng = np.random.default_rng(8200)
     R = 64
     rts = random_runtimes(rng, R, 40)
@@ -1111,9 +1106,7 @@ def test_gpu_tables_in_hbm_forced(g, orc, monkeypatch):
     frames, flen, offs, olf, rss, fdir, hint = fuzz_batch(rng, n, rts, R)
     t = orc.Tables(R, 1, 0, 0x09)
     apply_runtimes(t, rts)
-    monkeypatch.setenv("GCL_TUNE_TABLES", "1")
-    clf = g.Classifier(0, R, 1, 0, 0x09)
-    monkeypatch.delenv("GCL_TUNE_TABLES")
+    clf = g.Classifier(0, R, 1, 0, 0x09, tune={"tables": 1})
     apply_runtimes(clf, rts)
     ve, ce, se = t.classify(frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir_hi=fdir,
                             frames_len=flen, dst_hint=hint)
@@ -1123,22 +1116,43 @@ def test_gpu_tables_in_hbm_forced(g, orc, monkeypatch):
     assert (c == ce).all() and (st == se).all()
 
 
+def test_gpu_ctx_tune_validation(g):
+    """gcl_ctx_tune refuses a wrong struct size or a field out of range
+    (-EINVAL) and keeps the previous settings; NULL restores the defaults."""
+    clf = g.Classifier(0, 16, 1)
+    ok = g.make_tune(threads=512, defer=0)
+    assert g.lib.gcl_ctx_tune(clf._ctx, ctypes.byref(ok)) == 0
+    bad = [g.make_tune(threads=300), g.make_tune(depth=3), g.make_tune(defer=3), g.make_tune(grid=0),
+           g.make_tune(loop_phase=(2000, 1, 1)), g.make_tune(loop_phase=(10, 0, 0)), g.make_tune(loop_spec=-5)]
+    half = g.make_tune()
+    half.loop_phase_max = 50  # up / down left AUTO: the three go together
+    bad.append(half)
+    wrong = g.make_tune()
+    wrong.size = 64
+    bad.append(wrong)
+    for t in bad:
+        assert g.lib.gcl_ctx_tune(clf._ctx, ctypes.byref(t)) == -22
+    assert g.lib.gcl_ctx_tune(clf._ctx, None) == 0
+    clf.tune(tables=1, grid=3, depth=1)
+    clf.close()
+
+
 LOOP_GEOMETRIES = [
     {},
-    {"GCL_TUNE_GRID": "3"},
-    {"GCL_TUNE_GRID": "16"},
-    {"GCL_TUNE_GRID": "24", "GCL_TUNE_THREADS": "512"},
-    {"GCL_TUNE_DEPTH": "1", "GCL_TUNE_GRID": "5"},
-    {"GCL_TUNE_DEPTH": "1", "GCL_TUNE_THREADS": "512"},
-    {"GCL_TUNE_THREADS": "1024", "GCL_TUNE_GRID": "7"},
-    {"GCL_TUNE_THREADS": "512", "GCL_TUNE_GRID": "5"},
-    {"GCL_TUNE_BLOCKS_PER_CU": "1"},
+    {"grid": 3},
+    {"grid": 16},
+    {"grid": 24, "threads": 512},
+    {"depth": 1, "grid": 5},
+    {"depth": 1, "threads": 512},
+    {"threads": 1024, "grid": 7},
+    {"threads": 512, "grid": 5},
+    {"blocks_per_cu": 1},
 ]
 
 
 @pytest.mark.parametrize("geo", range(len(LOOP_GEOMETRIES)))
 @pytest.mark.parametrize("general", [False, True, "stride"])
-def test_gpu_loop_geometries(g, orc, monkeypatch, geo, general):
+def test_gpu_loop_geometries(g, orc, geo, general):
     """The loops' edges under every launch shape the geometry knobs allow:
     few blocks walking many tiles (odd counts per block, so the second half
     of the DEPTH-2 loop runs past the end as an empty tile), DEPTH 1,
@@ -1155,13 +1169,7 @@ def test_gpu_loop_geometries(g, orc, monkeypatch, geo, general):
     key = bytes(rng.integers(0, 256, size=40, dtype=np.uint8))
     t = orc.Tables(R, mode, 0, 0x09, key)
     apply_runtimes(t, rts)
-    for kk, vv in env.items():
-        monkeypatch.setenv(kk, vv)
-    try:
-        clf = g.Classifier(0, R, mode, 0, 0x09, key)
-    finally:
-        for kk in env:
-            monkeypatch.delenv(kk)
+    clf = g.Classifier(0, R, mode, 0, 0x09, key, tune=env)
     apply_runtimes(clf, rts)
     if general == "stride":
         n = 30011

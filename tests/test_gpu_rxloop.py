@@ -44,6 +44,18 @@ def tc_map(rts, max_rt):
     return tc
 
 
+def poll_stats_settled(loop, nb, timeout_s=2.0):
+    """The loop's poll counters once all @nb bursts are in them: the writer
+    wave posts them after the bursts' verdict records (gclassify.h), so they
+    may lag the last wait by a few microseconds."""
+    deadline = time.monotonic() + timeout_s
+    ps = loop.poll_stats()
+    while sum(ps.values()) < nb and time.monotonic() < deadline:
+        time.sleep(0.001)
+        ps = loop.poll_stats()
+    return ps
+
+
 LOOP_CASES = [(m, vb, 0, 0) for m in (0, 1, 2) for vb in (8, 4, 2)] + \
     [(m, 8, fl, 0) for m in (0, 1, 2) for fl in (1, 2)] + \
     [(0, 8, 1, 1), (1, 4, 0, 1), (2, 8, 2, 1), (1, 2, 1, 1)] + \
@@ -51,11 +63,19 @@ LOOP_CASES = [(m, vb, 0, 0) for m in (0, 1, 2) for vb in (8, 4, 2)] + \
     [(m, 1, 0, i) for m in (0, 2) for i in (0, 1, 2)] + [(0, 1, 1, 2), (2, 1, 2, 0)]
 
 
+# Python takes longer than the loop's default speculative window (4 us, 1 ms
+# with <= 2 workers) between bursts: tests that want every burst of <= 64
+# taken with its poll (offsets or header records current at the first poll,
+# or re-read after a stale one) open it to 1 s (gcl_tune.loop_spec, 10-ns
+# ticks), so that a burst is never "late" however Python paces the submits
+SPEC_WIDE = 100_000_000
+
+
 @pytest.mark.parametrize("k64", [1, 0])
 @pytest.mark.parametrize("mode,vb,flags,inline", LOOP_CASES)
-def test_rxloop_fuzz_vs_oracle(g, orc, mode, vb, flags, inline, k64, monkeypatch):
+def test_rxloop_fuzz_vs_oracle(g, orc, mode, vb, flags, inline, k64):
     """k64: bursts of <= 64 through rxloop64_kernel (the default for
-    max_burst <= 64), or through the general loop kernel (GCL_TUNE_LOOP64=0);
+    max_burst <= 64), or through the general loop kernel (gcl_tune.loop64 = 0);
     vb: verdict bytes (8 gcl_verdict, 4 VERDICT4, 2 VERDICT2, 1 VERDICT1 with
     16 runtimes x up to 8 kthreads);
     flags: 0 plain, 1 Azure ARP mode (GCL_CFG_AZURE_ARP), 2 16-bit hash;
@@ -82,9 +102,7 @@ def test_rxloop_fuzz_vs_oracle(g, orc, mode, vb, flags, inline, k64, monkeypatch
     # header records, and the offsets of the NIC-mode cases, taken with the
     # poll (see the ragged-burst test); the other cases read after the word
     early = inline == 2 or (inline == 0 and mode == 0)
-    if early:
-        monkeypatch.setenv("GCL_TUNE_LOOP_SPEC", "500000")
-    monkeypatch.setenv("GCL_TUNE_LOOP64", "1" if k64 else "0")
+    clf.tune(loop64=k64, **({"loop_spec": SPEC_WIDE} if early else {}))
     loop = clf.rxloop(frames, slots=8, counts=cnt, stats=st, region_len=flen,
                       flags=LOOP_FLAGS[inline](g))
     try:
@@ -109,9 +127,9 @@ def test_rxloop_fuzz_vs_oracle(g, orc, mode, vb, flags, inline, k64, monkeypatch
                 got.append(rec["verdict"].astype(np.uint8))
             loop.release(tk)
         got = np.concatenate(got)
-        ps = loop.poll_stats()
-        if early:  # the side fields went through the one-round-trip path too
-            assert ps["early"] > 0, ps
+        ps = poll_stats_settled(loop, len(bursts(n)))
+        if early:  # every burst taken with its poll (early, or re-read if stale)
+            assert ps["late"] == 0, ps
     finally:
         loop.stop()
         g.host_unregister(frames)
@@ -127,7 +145,7 @@ LEAN_CASES = [(m, vb, fl, lf) for m in (0, 1, 2) for vb in (8, 4, 2, 1) for fl, 
 
 
 @pytest.mark.parametrize("mode,vb,flags,lflag", LEAN_CASES)
-def test_rxloop_lean_path(g, orc, mode, vb, flags, lflag, monkeypatch):
+def test_rxloop_lean_path(g, orc, mode, vb, flags, lflag):
     """rxloop64_kernel's lean path (classify_lean) against the oracle: bursts
     of plain IPv4 (every packet Ethertype IPv4, IHL 5, no FDIR mark) take it,
     bursts with one FDIR-marked packet, or with dst_ip hints, take
@@ -165,7 +183,7 @@ def test_rxloop_lean_path(g, orc, mode, vb, flags, lflag, monkeypatch):
     g.host_register(frames)
     cnt = torch.zeros(max_rt, dtype=torch.int64, device="cuda")
     st = torch.zeros(g.NR_STATS, dtype=torch.int64, device="cuda")
-    monkeypatch.setenv("GCL_TUNE_LOOP_SPEC", "500000")
+    clf.tune(loop_spec=SPEC_WIDE)
     loop = clf.rxloop(frames, slots=8, counts=cnt, stats=st, flags=LOOP_FLAGS[lflag](g))
     try:
         got = []
@@ -283,7 +301,7 @@ def test_rxloop_workers_pipelined_and_full_ring(g, orc):
 @pytest.mark.parametrize("max_burst,workers,lflag", [(64, 1, 0), (64, 3, 0), (256, 2, 0),
                                                      (64, 1, 2), (64, 3, 2), (256, 2, 2),
                                                      (1024, 2, 0), (1024, 2, 2)])
-def test_rxloop_stamped_offsets_ragged_bursts(g, orc, max_burst, workers, lflag, monkeypatch):
+def test_rxloop_stamped_offsets_ragged_bursts(g, orc, max_burst, workers, lflag):
     """Offsets ride in the slot stamped with the slot's use count, and a
     worker polling a burst of <= 64 takes them with the poll when every stamp
     is current (lflag 2: whole header records, GCL_LOOP_HDR_RECORDS, each
@@ -308,10 +326,9 @@ def test_rxloop_stamped_offsets_ragged_bursts(g, orc, max_burst, workers, lflag,
     clf = g.Classifier(0, max_rt, 1, 0, 0x09)
     apply_runtimes(clf, rts)
     g.host_register(frames)
-    # Python takes longer than the default 4-us speculative window between
-    # bursts: widen it (GCL_TUNE_LOOP_SPEC, 10-ns ticks) so that the bursts
-    # really arrive with the poll here, as they do from a C dataplane loop
-    monkeypatch.setenv("GCL_TUNE_LOOP_SPEC", "500000")
+    # every burst of <= 64 taken with its poll (SPEC_WIDE), as bursts from a C
+    # dataplane loop are
+    clf.tune(loop_spec=SPEC_WIDE)
     loop = clf.rxloop(frames, slots=2, workers=workers, max_burst=max_burst, region_len=flen,
                       flags=LOOP_FLAGS[lflag](g))
     try:
@@ -326,14 +343,16 @@ def test_rxloop_stamped_offsets_ragged_bursts(g, orc, max_burst, workers, lflag,
             got = loop.wait(tk, int(m))
             bad = np.nonzero(got != ve[idx])[0]
             assert not len(bad), f"burst {k} (n {m}): packet {bad[0]} {got[bad[0]]} vs {ve[idx][bad[0]]}"
-        for _ in range(100):  # the counters are posted writes of their own
-            ps = loop.poll_stats()
-            if sum(ps.values()) == nb:
-                break
-            time.sleep(0.001)
+        ps = poll_stats_settled(loop, nb)
         assert sum(ps.values()) == nb, ps
-        if max_burst <= 64:  # the one-round-trip path really ran
-            assert ps["early"] > nb // 4, ps
+        # How many bursts were current at their first poll (early) rather
+        # than re-read after it (stale) depends on how the host paces its
+        # stores against the polls: a measurement (reported), not a gate.
+        # What does not depend on pacing: bursts of <= 64 are all taken with
+        # the poll, longer ones never.
+        print(f"poll stats max_burst={max_burst} workers={workers} lflag={lflag}: {ps}")
+        if max_burst <= 64:
+            assert ps["late"] == 0, ps
         else:
             assert ps["early"] == 0 and ps["stale"] == 0, ps
     finally:
@@ -393,7 +412,7 @@ def test_rxloop_lifetime_and_errors(g):
 
 
 @pytest.mark.parametrize("mode,vb,lflag", [(1, 8, 0), (0, 4, 0), (2, 8, 2), (1, 4, 2)])
-def test_rxloop_transport_hashes(g, orc, mode, vb, lflag, monkeypatch):
+def test_rxloop_transport_hashes(g, orc, mode, vb, lflag):
     """GCL_CFG_TRANS_HASH through the loop: each delivered IPv4 TCP/UDP
     packet's trans_hash_5tuple / _3tuple with its runtime's seed
     (runtime/net/transport.c:29-42, as gcl_classify_ex computes them) come
@@ -419,7 +438,7 @@ def test_rxloop_transport_hashes(g, orc, mode, vb, lflag, monkeypatch):
     assert (te["h5"] != 0).sum() > n // 10
     g.host_register(frames)
     if lflag == 2:
-        monkeypatch.setenv("GCL_TUNE_LOOP_SPEC", "500000")
+        clf.tune(loop_spec=SPEC_WIDE)
     loop = clf.rxloop(frames, slots=8, region_len=flen, flags=LOOP_FLAGS[lflag](g))
     try:
         got, gt = [], []
@@ -446,16 +465,16 @@ def test_rxloop_transport_hashes(g, orc, mode, vb, lflag, monkeypatch):
     assert not len(bad), f"{len(bad)} transport hashes differ, first {bad[0]}: {gt[bad[0]]} vs {te[bad[0]]}"
 
 
-@pytest.mark.parametrize("lflag,spec,use0", [(0, "0", (1 << 23) - 150), (0, "500000", (1 << 23) - 150),
-                                             (2, "500000", (1 << 31) - 150), (2, "0", (1 << 31) - 150)])
-def test_rxloop_stamp_wrap(g, orc, lflag, spec, use0, monkeypatch):
+@pytest.mark.parametrize("lflag,spec,use0", [(0, 0, (1 << 23) - 150), (0, SPEC_WIDE, (1 << 23) - 150),
+                                             (2, SPEC_WIDE, (1 << 31) - 150), (2, 0, (1 << 31) - 150)])
+def test_rxloop_stamp_wrap(g, orc, lflag, spec, use0):
     """The slots' use count crossing the stamps' wrap (2^23 for stamped
     offsets, 2^31 for header records) with the loop started near it
-    (GCL_TUNE_LOOP_T0): stamps are never 0, so a zeroed or never-loaded
+    (gcl_tune.loop_t0): stamps are never 0, so a zeroed or never-loaded
     entry never passes for a current one, with the speculative window closed
     (spec 0: every burst read after its word) or wide open (every burst with
     the poll).  Every verdict equals the oracle's."""
-    rng = np.random.default_rng(7700 + lflag + len(spec))
+    rng = np.random.default_rng(7700 + lflag + len(str(spec)))
     max_rt = 16
     rts = random_runtimes(rng, max_rt, 12)
     n = 2048
@@ -467,8 +486,7 @@ def test_rxloop_stamp_wrap(g, orc, lflag, spec, use0, monkeypatch):
     apply_runtimes(clf, rts)
     g.host_register(frames)
     slots = 2
-    monkeypatch.setenv("GCL_TUNE_LOOP_SPEC", spec)
-    monkeypatch.setenv("GCL_TUNE_LOOP_T0", str(slots * use0))
+    clf.tune(loop_spec=spec, loop_t0=slots * use0)
     loop = clf.rxloop(frames, slots=slots, workers=1, region_len=flen, flags=LOOP_FLAGS[lflag](g))
     try:
         nb = 600  # 300 uses of each slot: across the wrap
@@ -480,24 +498,26 @@ def test_rxloop_stamp_wrap(g, orc, lflag, spec, use0, monkeypatch):
             got = loop.wait(tk, m)
             bad = np.nonzero(got != ve[idx])[0]
             assert not len(bad), f"burst {k} (use {use0 + k // slots + 1}): {got[bad[0]]} vs {ve[idx][bad[0]]}"
-        ps = loop.poll_stats()
-        if spec == "0":
-            assert ps["early"] == 0, ps
+        ps = poll_stats_settled(loop, nb)
+        if spec == 0:
+            assert ps["early"] == 0 and ps["stale"] == 0, ps
+        else:
+            assert ps["late"] == 0, ps
     finally:
         loop.stop()
         g.host_unregister(frames)
 
 
-@pytest.mark.parametrize("phase", [None, "0", "1000,1000,0", "1,1,1"])
+@pytest.mark.parametrize("phase", [None, (0, 16, 1), (1000, 1000, 0), (1, 1, 1)])
 @pytest.mark.parametrize("workers,lflag", [(1, 2), (2, 2), (1, 0), (1, 1)])
-def test_rxloop_phase_delay(g, orc, phase, workers, lflag, monkeypatch):
-    """The poll-phase delay (GCL_TUNE_LOOP_PHASE "max,up,down"; None: the
+def test_rxloop_phase_delay(g, orc, phase, workers, lflag):
+    """The poll-phase delay (gcl_tune.loop_phase_* (max, up, down); None: the
     default, on for loops of 1-2 workers) only moves when a ticket's first
     poll is issued: bursts submitted in a closed loop (each after the last
     one's verdicts), with host-side gaps now and then, come back equal to the
     oracle's whatever the delay does -- off, pinned at 10 us after the first
-    late find ("1000,1000,0"), or one tick."""
-    rng = np.random.default_rng(7900 + workers + 10 * lflag + (len(phase) if phase else 0))
+    late find ((1000, 1000, 0)), or one tick."""
+    rng = np.random.default_rng(7900 + workers + 10 * lflag + (len(",".join(map(str, phase))) if phase else 0))
     max_rt = 16
     rts = random_runtimes(rng, max_rt, 12)
     n = 2048
@@ -509,7 +529,7 @@ def test_rxloop_phase_delay(g, orc, phase, workers, lflag, monkeypatch):
     apply_runtimes(clf, rts)
     g.host_register(frames)
     if phase is not None:
-        monkeypatch.setenv("GCL_TUNE_LOOP_PHASE", phase)
+        clf.tune(loop_phase=phase)
     loop = clf.rxloop(frames, slots=8, workers=workers, region_len=flen, flags=LOOP_FLAGS[lflag](g))
     try:
         for k in range(300):
@@ -526,15 +546,16 @@ def test_rxloop_phase_delay(g, orc, phase, workers, lflag, monkeypatch):
         g.host_unregister(frames)
 
 
-@pytest.mark.parametrize("prefetch", [None, "0", "1"])
+@pytest.mark.parametrize("prefetch", [None, 0, 1])
 @pytest.mark.parametrize("lflag", [0, 2])
-def test_rxloop_prefetch(g, orc, prefetch, lflag, monkeypatch):
+@pytest.mark.parametrize("slots,workers", [(16, 4), (4, 4), (2, 4)])
+def test_rxloop_prefetch(g, orc, prefetch, lflag, slots, workers):
     """The next ticket's poll issued before a burst is classified
-    (GCL_TUNE_LOOP_PREFETCH; None: the default, on for stamped offsets with
+    (gcl_tune.loop_prefetch; None: the default, on for stamped offsets with
     more than two workers): bursts kept 12 deep across 4 workers, so that
     polls find them queued, and drained now and then, so that they catch up;
     every verdict equal to the oracle's."""
-    rng = np.random.default_rng(7950 + lflag + (len(prefetch) if prefetch else 0))
+    rng = np.random.default_rng(7950 + lflag + (3 if prefetch is None else prefetch) + 10 * slots)
     max_rt = 16
     rts = random_runtimes(rng, max_rt, 12)
     n = 2048
@@ -546,21 +567,24 @@ def test_rxloop_prefetch(g, orc, prefetch, lflag, monkeypatch):
     apply_runtimes(clf, rts)
     g.host_register(frames)
     if prefetch is not None:
-        monkeypatch.setenv("GCL_TUNE_LOOP_PREFETCH", prefetch)
-    loop = clf.rxloop(frames, slots=16, workers=4, region_len=flen, flags=LOOP_FLAGS[lflag](g))
+        clf.tune(loop_prefetch=prefetch)
+    loop = clf.rxloop(frames, slots=slots, workers=workers, region_len=flen, flags=LOOP_FLAGS[lflag](g))
+    deep = min(12, slots)  # in flight at most: the ring's slots
     try:
         inflight = []
         for k in range(600):
             m = int(rng.integers(1, 65))
             idx = rng.integers(0, n, size=m)
-            inflight.append((loop.submit(offs[idx], olf[idx], rss[idx]), m, idx))
-            if len(inflight) >= 12 or k % 97 == 96:
+            tk = loop.submit(offs[idx], olf[idx], rss[idx])
+            assert tk > 0, tk
+            inflight.append((tk, m, idx))
+            if len(inflight) >= deep or k % 97 == 96:
                 while inflight:  # every 97th burst: drain, so the workers catch up
                     tk, mm, ii = inflight.pop(0)
                     got = loop.wait(tk, mm)
                     bad = np.nonzero(got != ve[ii])[0]
                     assert not len(bad), f"ticket {tk}: {got[bad[0]]} vs {ve[ii][bad[0]]}"
-                    if len(inflight) < 8 and k % 97 != 96:
+                    if len(inflight) < deep * 2 // 3 and k % 97 != 96:
                         break
         for tk, mm, ii in inflight:
             got = loop.wait(tk, mm)

@@ -1,10 +1,10 @@
 """A/B of the dense tile kernel's verdict writes on the bench's own placed
-buffers, in one process: stored per packet (GCL_TUNE_DEFER=0) against kept
+buffers, in one process: stored per packet (gcl_tune.defer = 0) against kept
 in LDS (and past a full buffer in registers) and written in at most two
 batches per block (1, the default), or in as many as it takes (2).  Round
 5's A/Bs also had an LDS-only form, since folded into 1
 (profiles/r05_defer_ab.jsonl), and the batch writes through LDS, non-temporal
-or plain (GCL_TUNE_VFLUSH, removed: no difference, r05_vflush_ab.jsonl).  One context per form
+or plain (a VFLUSH knob, removed: no difference, r05_vflush_ab.jsonl).  One context per form
 over the same frames and verdict ring, launches interleaved round by round;
 every form's verdicts and counts are checked against form 0's.
 
@@ -33,10 +33,9 @@ def main():
         clfs = {}
         forms = [int(x) for x in os.environ.get("AB_FORMS", ",".join(map(str, FORMS))).split(",")]
         for f in forms:
-            os.environ["GCL_TUNE_DEFER"] = str(f)
             clfs[f] = bench.classifier(dev, w.R, w.T, w.vbytes)
+            clfs[f].tune(defer=f)
             bench.setup_tables(clfs[f], w.R, w.T)
-        os.environ.pop("GCL_TUNE_DEFER", None)
         st = torch.cuda.current_stream().cuda_stream
         ref = None
         for f, clf in clfs.items():  # correctness: same verdicts and counts as form 0

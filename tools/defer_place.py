@@ -2,7 +2,7 @@
 One 32 Mi-entry 1-B verdict ring; K frame pools allocated one after another
 (hipMalloc through gcl_dev_alloc, a growing spacer after every third, as
 gcl_dev_alloc_paired steps past runs of one class); for every pool the udp64
-classify kernel timed with per-packet verdict stores (GCL_TUNE_DEFER=0) and
+classify kernel timed with per-packet verdict stores (gcl_tune.defer = 0) and
 with the deferred batch writes (1), interleaved, plus the placement probe's
 per-packet pattern over the same pair (gcl_access_probe).
 
@@ -29,11 +29,9 @@ def main():
     ring = g.DeviceBuffer(n * vb, 0)
     clfs = {}
     for f in (0, 1):
-        os.environ["GCL_TUNE_DEFER"] = str(f)
         fl, tb = bench.verdict_cfg(vb, R, T)
-        clfs[f] = g.Classifier(0, R, g.HASH_JENKINS, fl, thread_bits=tb)
+        clfs[f] = g.Classifier(0, R, g.HASH_JENKINS, fl, thread_bits=tb, tune={"defer": f})
         bench.setup_tables(clfs[f], R, T)
-    os.environ.pop("GCL_TUNE_DEFER", None)
     st = torch.cuda.current_stream().cuda_stream
     keep = []
     nsp = 0

@@ -27,6 +27,7 @@
 #include <vector>
 
 #include "gclassify.h"
+#include "tune_env.h"
 
 #define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { \
 	fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); exit(1); } } while (0)
@@ -77,6 +78,7 @@ int main(int argc, char **argv)
 	cfg.default_olflags = GCL_F_RSS_HASH | GCL_F_IP_CKSUM_GOOD;
 	struct gcl_ctx *ctx;
 	GCHECK(gcl_open(0, &cfg, &ctx));
+	GCHECK(tune_from_env(ctx));
 	for (uint32_t r = 0; r < R; r++) {
 		uint16_t act[GCL_NCPU], flow[GCL_NCPU];
 		const uint16_t na = (uint16_t)(r % T + 1);

@@ -1,4 +1,4 @@
-"""A/B of classify_pair_kernel's lean path (GCL_TUNE_PAIR_LEAN: waves whose
+"""A/B of classify_pair_kernel's lean path (gcl_tune.pair_lean: waves whose
 packets are all plain IPv4 take classify_lean) on bench.py's integrated
 ingress row: the reference's 131072-mbuf pool (data at element + 344) placed
 in HBM against the verdict ring, 8 Mi descriptors with ol_flags and
@@ -54,10 +54,9 @@ def main():
         region, dv, offs, olf, rss, n, R, T = pool(dev, vb, ws=ws)
         clfs = {}
         for f in (0, 1):
-            os.environ["GCL_TUNE_PAIR_LEAN"] = str(f)
             clfs[f] = bench.classifier(dev, R, T, vb, hash_mode=g.HASH_NIC)
+            clfs[f].tune(pair_lean=f)
             bench.setup_tables(clfs[f], R, T)
-        os.environ.pop("GCL_TUNE_PAIR_LEAN", None)
         ref = None
         for f, clf in clfs.items():
             cnt = torch.zeros(R + g.NR_STATS, dtype=torch.int64, device=dev)

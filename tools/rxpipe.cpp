@@ -38,6 +38,7 @@
 
 #include "gcl_host.h"
 #include "gclassify.h"
+#include "tune_env.h"
 
 #define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { \
 	fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); exit(1); } } while (0)
@@ -221,7 +222,7 @@ int main(int argc, char **argv)
 	cfg.flags = GCL_CFG_VERDICT4;
 	cfg.default_olflags = GCL_F_RSS_HASH | GCL_F_IP_CKSUM_GOOD;
 	struct gcl_ctx *ctx;
-	if (gcl_open(0, &cfg, &ctx))
+	if (gcl_open(0, &cfg, &ctx) || tune_from_env(ctx))
 		return 1;
 
 	/* host side of the runtimes: struct proc slices with one lrpc ring per kthread */
