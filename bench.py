@@ -184,7 +184,7 @@ def compact(result, detail_path=DETAIL_PATH):
     cpu = result.get("cpu_baseline")
     if cpu:
         out["cpu_baseline"] = {**_pick(cpu, "value", "unit", "cores", "kind", "sample", "pinning",
-                                       "cpu_model", "nproc", "seconds", "gpu_over_1core_nic"),
+                                       "cpu_model", "nproc", "seconds", "gpu_over_1core_nic", "error"),
                                "nic_mode": _cpu_mode(cpu.get("nic_mode")),
                                "jenkins_mode": _cpu_mode(cpu.get("jenkins_mode"))}
     grp = result.get("group")
@@ -192,7 +192,8 @@ def compact(result, detail_path=DETAIL_PATH):
         out["group"] = _pick(grp, "n_gpus", "exchange", "value", "gpu_ms_per_step", "counts_check", "error")
     node = result.get("group_node")
     if node:
-        out["group_node"] = _pick(node, "n_gpus", "value", "ms_per_step", "counts_check", "error")
+        out["group_node"] = _pick(node, "n_gpus", "exchange", "rccl_ranks", "value", "ms_per_step",
+                                  "counts_check", "error")
     sec = result.get("secondary")
     if sec:
         s = {"workload": "tcp1500 (config 3)", **_pick(sec, "verdict", "value", "unit", "ms_per_step"),
@@ -667,7 +668,7 @@ def group_bench(w, steps, warmup, device_index, period=EXCHANGE_EVERY, settle=No
         grp.close()
 
 
-def group_node_bench(ndev, steps, warmup, period=EXCHANGE_EVERY, vbytes=VERDICT_BYTES):
+def group_node_bench(ndev, steps, warmup, period=EXCHANGE_EVERY, vbytes=VERDICT_BYTES, shared=False):
     """The single-process multi-GPU step over `ndev` GPUs of this node (run in
     a child process by group_node_line): the udp64 workload sharded
     round-robin in 64 Ki-packet blocks, each GPU's 32 Mi-packet shard
@@ -675,23 +676,28 @@ def group_node_bench(ndev, steps, warmup, period=EXCHANGE_EVERY, vbytes=VERDICT_
     one gcl_group over all of them classifying every GPU's shard per step and
     all-gathering the counts through RCCL (ncclCommInitAll) every `period`
     steps.  Wall time between full synchronisations of every GPU; the
-    node-wide counts read back through the exchange and checked."""
+    node-wide counts read back through the exchange and checked.  `shared`
+    (rehearsals only): fewer GPUs visible than `ndev`, so contexts share them
+    and the exchange is the host sum (RCCL refuses two ranks on one device)."""
     wl, n, stride, R, T, _ = WORKLOADS["udp64"]
     fl, tb = verdict_cfg(vbytes, R, T)
-    devs = list(range(ndev))
+    visible = torch.cuda.device_count()
+    devs = [d % visible for d in range(ndev)] if shared else list(range(ndev))
     frames, verdicts = [], []
-    for d in devs:
+    for i, d in enumerate(devs):
         with torch.cuda.device(d):
             v = g.DeviceBuffer(n * vbytes, d)
             f = g.DeviceBuffer(n * stride, d, partner=v, vbytes=vbytes)
             torch.cuda.synchronize()
             zero_fill(f)
-            g.generate(wl, n, stride, R, f, seed=SEED, rank=d, world=ndev, shard_block=SHARD_BLOCK)
+            g.generate(wl, n, stride, R, f, seed=SEED, rank=i, world=ndev, shard_block=SHARD_BLOCK)
             torch.cuda.synchronize()
             frames.append(f)
             verdicts.append(v)
-    grp = g.Group(devs, R, g.HASH_JENKINS, flags=fl, thread_bits=tb, exchange=g.XCHG_RCCL)
+    xchg = g.XCHG_HOST if shared else g.XCHG_RCCL
+    grp = g.Group(devs, R, g.HASH_JENKINS, flags=fl, thread_bits=tb, exchange=xchg)
     try:
+        rccl_ranks = grp.rccl_ranks()
         rng = np.random.default_rng(SEED)
         for r in range(R):
             act = int(rng.integers(1, T + 1))
@@ -724,8 +730,13 @@ def group_node_bench(ndev, steps, warmup, period=EXCHANGE_EVERY, vbytes=VERDICT_
         ok = (int(c.sum()) == n * ndev * k[0] and int(s[g.RX_PULLED]) == n * ndev * k[0] and
               all(int(per[i, R + g.RX_PULLED]) == n * k[0] for i in range(ndev)))
         return {"what": (f"gcl_group over {ndev} GPU(s) from one process: round-robin 64Ki-pkt shards, "
-                         f"{n} pkts per GPU per step, RCCL ncclAllGather of u64[R+8] every {period} steps"),
-                "n_gpus": ndev, "value": round(n * ndev * steps / el / 1e6, 1), "unit": "Mpkt/s",
+                         f"{n} pkts per GPU per step, "
+                         + (f"RCCL ncclAllGather of u64[R+8] every {period} steps" if not shared else
+                            f"host sum of u64[R+8] every {period} steps (rehearsal: {ndev} contexts on "
+                            f"{visible} GPU(s))")),
+                "n_gpus": ndev, "devices": devs, "exchange": "rccl" if not shared else "host (shared GPU)",
+                "rccl_ranks": rccl_ranks,
+                "value": round(n * ndev * steps / el / 1e6, 1), "unit": "Mpkt/s",
                 "ms_per_step": round(el / steps * 1e3, 4), "steps": steps,
                 "exchanges": int(k[0] // period) + 1,
                 "counts_check": "ok" if ok else "MISMATCH"}
@@ -733,25 +744,70 @@ def group_node_bench(ndev, steps, warmup, period=EXCHANGE_EVERY, vbytes=VERDICT_
         grp.close()
 
 
-def group_node_line(args):
-    """group_node_bench over every visible GPU, in a child process with its
-    own time limit (an RCCL or driver stall there cannot take the bench line
-    down with it).  Only when this node shows more than one GPU."""
+GROUP_CHILD_TIMEOUT_S = 300
+
+
+def group_node_line(args, ngpus):
+    """group_node_bench over exactly @ngpus GPUs (the line's N), in a fresh
+    child process with its own time limit (an RCCL or driver stall there
+    cannot take the bench line down with it): the multi-GPU step as the
+    single-process iokernel links it (include/gcl_group.h), beside the N
+    one-process-per-GPU ranks the line's `value` times.  At N=1 the `group`
+    row already covers one GPU, so only when forced.  More GPUs than visible
+    only with --allow-shared-gpu (a rehearsal: host exchange)."""
     import subprocess
-    ndev = min(torch.cuda.device_count(), 16)
-    if ndev < 2 and not args.group_node_force:
+    if ngpus < 2 and not args.group_node_force:
         return None
-    cmd = [sys.executable, os.path.abspath(__file__), "--group-child", str(max(ndev, 1)),
-           "--steps", str(args.steps), "--warmup", str(args.warmup)]
+    visible = torch.cuda.device_count()  # counting devices does not initialise the GPU
+    shared = ngpus > visible
+    if shared and not args.allow_shared_gpu:
+        return {"n_gpus": ngpus, "error": f"{ngpus} GPUs asked, {visible} visible"}
+    cmd = [sys.executable, os.path.abspath(__file__), "--group-child", str(ngpus),
+           "--steps", str(args.steps), "--warmup", str(args.warmup)] + (["--allow-shared-gpu"] if shared else [])
     try:
-        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=GROUP_CHILD_TIMEOUT_S)
     except subprocess.TimeoutExpired:
-        return {"n_gpus": ndev, "error": "timeout (300 s)"}
+        return {"n_gpus": ngpus, "error": f"timeout ({GROUP_CHILD_TIMEOUT_S} s)"}
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     if r.returncode != 0 or not lines:
-        return {"n_gpus": ndev, "error": (r.stderr.strip()[-300:] or f"rc {r.returncode}")}
+        return {"n_gpus": ngpus, "error": (r.stderr.strip()[-300:] or f"rc {r.returncode}")}
     out = json.loads(lines[-1])
-    out["host_ingress_c"] = grouppipe_run(ndev)
+    if not shared:
+        out["host_ingress_c"] = grouppipe_run(ngpus)
+    return out
+
+
+def cpu_child_line(args, value):
+    """The CPU baseline (cpu_baseline) in a fresh CPU-only child process, for
+    the N>1 lines: rank 0's process holds a GPU context and its rank's
+    buffers, the child only the oracle.  `gpu_over_1core_nic` is this line's
+    whole-job value over one core."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--cpu-child", "--cpu-budget", str(args.cpu_budget)]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=max(120.0, 6 * args.cpu_budget))
+    except subprocess.TimeoutExpired:
+        return {"error": "cpu child timeout"}
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"error": (r.stderr.strip()[-300:] or f"rc {r.returncode}")}
+    cpu = json.loads(lines[-1])
+    if cpu.get("value"):
+        cpu["gpu_over_1core_nic"] = round(value / cpu["value"], 1)
+    return cpu
+
+
+def node_extras(args, world, value):
+    """What an N>1 line carries beside its own ranks' measurement (rank 0,
+    after the process group is gone): the product's multi-GPU path over the
+    same N GPUs (group_node) and the CPU baseline timed on this host."""
+    out = {}
+    if not args.no_group:
+        node = group_node_line(args, world)
+        if node is not None:
+            out["group_node"] = node
+    if not args.no_cpu:
+        out["cpu_baseline"] = cpu_child_line(args, value)
     return out
 
 
@@ -1588,8 +1644,9 @@ def main():
     ap.add_argument("--no-group", action="store_true",
                     help="skip the gcl_group (C ABI + RCCL) lines at N=1")
     ap.add_argument("--group-node-force", action="store_true",
-                    help="run the all-GPU group line even with one GPU visible")
+                    help="run the group_node line (gcl_group over the line's N GPUs) even at N=1")
     ap.add_argument("--group-child", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--cpu-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-budget", type=float, default=30.0)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo only to rehearse N>1 on one GPU")
@@ -1610,8 +1667,12 @@ def main():
         # no launcher: start the N ranks here, before anything touches a GPU
         sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     _claim_stdout()
+    if args.cpu_child:  # cpu_child_line's child: no GPU call, one JSON line
+        emit_json(cpu_baseline(args.cpu_budget))
+        return
     if args.group_child:  # group_node_line's child: one JSON line, nothing else
-        emit_json(group_node_bench(args.group_child, args.steps, args.warmup, args.exchange_every))
+        emit_json(group_node_bench(args.group_child, args.steps, args.warmup, args.exchange_every,
+                                   shared=args.allow_shared_gpu and args.group_child > torch.cuda.device_count()))
         return
 
     rank, world, local = shard.dist_env()
@@ -1690,7 +1751,8 @@ def main():
     }
     if ex is not None:
         result["exchange"] = {"gpu_ms_per_step": round(gms, 4), "period_steps": args.exchange_every,
-                              "periods": ex.k}
+                              "periods": ex.k, "backend": torch.distributed.get_backend(),
+                              "ranks": torch.distributed.get_world_size()}
     if world == 1 and not args.no_group:
         try:
             result["group"] = group_bench(w, args.steps, args.warmup, dev_index, args.exchange_every,
@@ -1700,7 +1762,7 @@ def main():
     del w, ex
     torch.cuda.empty_cache()
     if world == 1 and not args.no_group:
-        node = group_node_line(args)
+        node = group_node_line(args, 1)
         if node is not None:
             result["group_node"] = node
     torch.cuda.empty_cache()
@@ -1779,7 +1841,11 @@ def main():
     if world > 1 and not args.no_e2e:
         result["e2e_multi"] = e2e_multi(device, rank, world, vb)
     if dist_on:
-        shard.finish()
+        shard.finish()  # every rank's GPU work done (barrier), the process group gone
+    if world > 1 and rank == 0:
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        result.update(node_extras(args, world, value))
     if rank == 0:
         emit_result(result)
 

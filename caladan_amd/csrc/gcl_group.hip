@@ -651,6 +651,24 @@ extern "C" int gcl_group_classify_host(struct gcl_group *g, const struct gcl_bat
 	return he.bad() ? -EIO : sr;
 }
 
+extern "C" int gcl_group_rccl_ranks(const struct gcl_group *g, int *ranks)
+{
+	if (!g || !ranks)
+		return -EINVAL;
+	*ranks = 0;
+	if (g->xchg != GCL_XCHG_RCCL)
+		return 0;
+	if (broken(g))
+		return -EIO;
+	for (int i = 0; i < g->n; i++) {
+		int c = 0;
+		if (!g->d[i].comm || ncclCommCount(g->d[i].comm, &c) != ncclSuccess || (i && c != *ranks))
+			return -EIO;
+		*ranks = c;
+	}
+	return 0;
+}
+
 extern "C" int gcl_group_test_fault(struct gcl_group *g, uint32_t what)
 {
 	if (!g || (what & ~(uint32_t)GCL_GROUP_FAULT_EXCHANGE))

@@ -699,6 +699,7 @@ def group_lib():
         "gcl_group_reset": (i32, [vp]),
         "gcl_group_sync": (i32, [vp]),
         "gcl_group_test_fault": (i32, [vp, u32]),
+        "gcl_group_rccl_ranks": (i32, [vp, ctypes.POINTER(i32)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(gl, name)
@@ -818,6 +819,12 @@ class Group:
 
     def sync(self):
         return _check(group_lib().gcl_group_sync(self._g), "gcl_group_sync")
+
+    def rccl_ranks(self):
+        """gcl_group_rccl_ranks: ranks of the RCCL communicators (ncclCommCount), 0 for a host exchange."""
+        r = ctypes.c_int()
+        _check(group_lib().gcl_group_rccl_ranks(self._g, ctypes.byref(r)), "gcl_group_rccl_ranks")
+        return r.value
 
     def test_fault(self, what=GROUP_FAULT_EXCHANGE):
         """gcl_group_test_fault (tests): every later RCCL exchange fails as a

@@ -154,6 +154,12 @@ int gcl_group_reset(struct gcl_group *g);
  * still drained, and the call returns -EIO. */
 int gcl_group_sync(struct gcl_group *g);
 
+/* The rank count of the group's RCCL communicators as RCCL reports it
+ * (ncclCommCount; every GPU's communicator must agree), into @ranks: the
+ * number of GPUs the exchange really spans.  0 for GCL_XCHG_HOST; -EIO on a
+ * failed group or a disagreement. */
+int gcl_group_rccl_ranks(const struct gcl_group *g, int *ranks);
+
 /* Test hook: make every later RCCL exchange of @g fail as a timed-out
  * enqueue would (GCL_GROUP_FAULT_EXCHANGE), to exercise the sticky failure
  * above; 0 clears it.  0 or -EINVAL.  Not for production use. */

@@ -262,3 +262,90 @@ def test_oracle_bench_pinned_runs():
     s = t.bench(frames, n, stride, threads=1, passes=2, olflags=olf, rss=rss, direct=True, cpus=[cpu])
     s2 = t.bench(frames, n, stride, threads=2, passes=2, olflags=olf, rss=rss, direct=True, cpus=[cpu, -1])
     assert s > 0 and s2 > 0
+
+
+def _fake_children(calls):
+    """subprocess.run standing in for bench.py's children: the group child
+    (--group-child N), the CPU child (--cpu-child) and tools/grouppipe."""
+    def run(cmd, **kw):
+        calls.append(cmd)
+        if "--group-child" in cmd:
+            n = int(cmd[cmd.index("--group-child") + 1])
+            line = {"n_gpus": n, "devices": list(range(n)), "exchange": "rccl", "rccl_ranks": n,
+                    "value": 95000.0 * n, "unit": "Mpkt/s", "ms_per_step": 0.35, "counts_check": "ok",
+                    "what": "g" * 200}
+        elif "--cpu-child" in cmd:
+            line = {"value": 60.0, "unit": "Mpkt/s", "cores": 1, "kind": "port", "sample": "s" * 300,
+                    "nic_mode": {"1core_mpps": 60.0, "1core_lrpc_mpps": 55.0, "all_cores_mpps": 900.0},
+                    "jenkins_mode": {"1core_mpps": 50.0, "1core_lrpc_mpps": 42.0, "all_cores_mpps": 800.0},
+                    "streams": {"tcp1500": {"x": "y" * 500}}, "seconds": 25.0}
+        else:  # tools/grouppipe
+            line = {"rows": [{"mode": "zerocopy", "mpps": 700.0}]}
+        return types.SimpleNamespace(returncode=0, stdout="banner\n" + json.dumps(line) + "\n", stderr="")
+    return run
+
+
+def test_n2_line_carries_group_node_and_cpu_baseline(bench, monkeypatch):
+    """an N>1 line carries the product's multi-GPU path
+    (gcl_group over exactly the line's N GPUs, from a fresh child, with the
+    RCCL communicators' own rank count) and the CPU baseline (a CPU-only
+    child), and the merged line stays under the driver's 8 KB."""
+    import subprocess
+    calls = []
+    monkeypatch.setattr(subprocess, "run", _fake_children(calls))
+    monkeypatch.setattr(os, "access", lambda p, m: True)
+    monkeypatch.setattr(bench.torch.cuda, "device_count", lambda: 8)
+    args = types.SimpleNamespace(no_group=False, no_cpu=False, group_node_force=False, allow_shared_gpu=False,
+                                 steps=50, warmup=5, cpu_budget=30.0)
+    ex = bench.node_extras(args, 2, 190000.0)
+    grp = [c for c in calls if "--group-child" in c]
+    assert len(grp) == 1 and grp[0][grp[0].index("--group-child") + 1] == "2"  # N GPUs, not all 8
+    assert "--allow-shared-gpu" not in grp[0]
+    assert any("--cpu-child" in c for c in calls)
+    assert ex["group_node"]["n_gpus"] == 2 and ex["group_node"]["rccl_ranks"] == 2
+    assert ex["cpu_baseline"]["gpu_over_1core_nic"] == round(190000.0 / 60.0, 1)
+    full = _full_result()
+    full["n_gpus"] = 2
+    full.pop("group_node")
+    full.update(ex)
+    full["exchange"] = {"gpu_ms_per_step": 0.34, "period_steps": 8, "periods": 7, "backend": "nccl", "ranks": 2}
+    line = bench.compact(full)
+    assert len(json.dumps(line)) < bench.LINE_LIMIT
+    assert line["group_node"]["n_gpus"] == 2 and line["group_node"]["rccl_ranks"] == 2
+    assert line["group_node"]["exchange"] == "rccl"
+    assert line["cpu_baseline"]["value"] == 60.0 and line["cpu_baseline"]["gpu_over_1core_nic"]
+    assert line["exchange"]["ranks"] == 2
+
+
+def test_group_node_only_at_n_gt_1_unless_forced(bench, monkeypatch):
+    """At N=1 the group row covers one GPU already: no group_node child
+    unless forced; more GPUs than visible only as a shared-GPU rehearsal."""
+    import subprocess
+    calls = []
+    monkeypatch.setattr(subprocess, "run", _fake_children(calls))
+    monkeypatch.setattr(os, "access", lambda p, m: True)
+    monkeypatch.setattr(bench.torch.cuda, "device_count", lambda: 1)
+    args = types.SimpleNamespace(no_group=False, no_cpu=True, group_node_force=False, allow_shared_gpu=False,
+                                 steps=5, warmup=1, cpu_budget=30.0)
+    assert bench.group_node_line(args, 1) is None and not calls
+    assert "error" in bench.group_node_line(args, 2)  # 2 asked, 1 visible, no rehearsal flag
+    args.allow_shared_gpu = True
+    node = bench.group_node_line(args, 2)
+    assert "--allow-shared-gpu" in calls[-1] and node["n_gpus"] == 2
+    args.group_node_force = True
+    assert bench.group_node_line(args, 1)["n_gpus"] == 1
+
+
+def test_cpu_child_runs_without_gpu():
+    """`bench.py --cpu-child` (the N>1 lines' CPU baseline) makes no GPU call:
+    it runs here, on a box without one, and prints one cpu_baseline object."""
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--cpu-child", "--cpu-budget", "1"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-500:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    cpu = json.loads(lines[0])
+    assert cpu["value"] > 0 and cpu["cores"] == 1 and cpu["kind"] == "port"
+    assert cpu["nic_mode"]["1core_lrpc_mpps"] > 0 and "tcp1500" in cpu["streams"]
