@@ -39,9 +39,11 @@ namespace gclk {
  * of the batch), with the frames of the next DEPTH tiles in flight in
  * registers while a tile is parsed.
  */
-template <int MODE, bool TLDS, int DEPTH, int NT>
+template <int MODE, bool TLDS, int DEPTH, int NT, bool WL>
 /* 4 waves per SIMD (<= 128 VGPRs): the 1024 resident lanes per CU the
- * geometry policy plans for, at every tile size */
+ * geometry policy plans for, at every tile size.  WL: each wave stages and
+ * classifies its own 64 packets of the tile (tile_chunk), so a tile needs no
+ * block barrier; the block meets only to write its deferred verdicts. */
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4)))
 classify_kernel(KParams k)
 {
@@ -166,16 +168,37 @@ classify_kernel(KParams k)
 		else
 			nreg++;
 		if (kl == k.vcap && nreg == rcap) {
+			if (WL) /* every wave's verdicts of these tiles are in */
+				__syncthreads();
 			flush_lds();
 			flush_regs();
 			kf += kl + nreg;
 			kl = nreg = 0;
+			if (WL) /* read out before any wave writes the buffer again */
+				__syncthreads();
 		}
 	};
+	/* rx_one_pkt on this lane's row, or (gcl_access_probe) the rows it
+	 * reads folded, after the same drain */
+	auto classify = [&](uint64_t tt) -> uint64_t {
+		if constexpr (MODE == kModeProbe) {
+			dense_drain();
+			const uint4 a = tile[tile_slot(tid, 0)], b = tile[tile_slot(tid, 1)], c = tile[tile_slot(tid, 2)];
+			return a.w ^ b.y ^ b.z ^ b.w ^ c.x ^ c.y ^ c.z;
+		} else {
+			return classify_one<MODE, false>(k, tile, tid, tt * NT + tid, tb, hist, cnt);
+		}
+	};
+	auto tile_sync = [&]() {
+		if (WL)
+			wave_lds_barrier();
+		else
+			__syncthreads();
+	};
 	if (t < t_end)
-		load_tile<NT>(k, t, true, ra);
+		load_tile<NT, WL>(k, t, true, ra);
 	if (DEPTH == 2)
-		load_tile<NT>(k, t + step, t + step < t_end, rb);
+		load_tile<NT, WL>(k, t + step, t + step < t_end, rb);
 
 	while (t < t_end) {
 		/* t opaque to the loop optimiser: without it every per-packet
@@ -184,17 +207,17 @@ classify_kernel(KParams k)
 		if constexpr (DEPTH == 2)
 			asm volatile("" : "+s"(t));
 		dense_drain(); /* once per loop iteration too */
-		stage_tile<NT>(tile, ra);
-		__syncthreads();
+		stage_tile<NT, WL>(tile, ra);
+		tile_sync();
 		const uint64_t nxt = t + DEPTH * step;
 		/* in flight while parsing */
-		load_tile<NT>(k, nxt, nxt < t_end, ra);
+		load_tile<NT, WL>(k, nxt, nxt < t_end, ra);
 		{
 			const bool live = t * NT + tid < k.n;
-			const uint64_t w = live ? classify_one<MODE, false>(k, tile, tid, t * NT + tid, tb, hist, cnt) : 0;
+			const uint64_t w = live ? classify(t) : 0;
 			verdict(t * NT + tid, true, live, w);
 		}
-		__syncthreads();
+		tile_sync();
 		tile_done(t);
 		t += step;
 		if (DEPTH == 2) {
@@ -202,20 +225,21 @@ classify_kernel(KParams k)
 			 * classified) rather than leaving the loop here: a path out of
 			 * the middle of the body, without the rb loads below, would
 			 * make the wait before staging ra wait for everything */
-			stage_tile<NT>(tile, rb);
-			__syncthreads();
-			load_tile<NT>(k, t + 2 * step, t + 2 * step < t_end, rb);
+			stage_tile<NT, WL>(tile, rb);
+			tile_sync();
+			load_tile<NT, WL>(k, t + 2 * step, t + 2 * step < t_end, rb);
 			{
 				const bool live = t < t_end && t * NT + tid < k.n;
-				const uint64_t w =
-				        live ? classify_one<MODE, false>(k, tile, tid, t * NT + tid, tb, hist, cnt) : 0;
+				const uint64_t w = live ? classify(t) : 0;
 				verdict(t * NT + tid, t < t_end, live, w);
 			}
-			__syncthreads();
+			tile_sync();
 			tile_done(t);
 			t += step;
 		}
 	}
+	if (WL) /* every wave's verdicts and histogram adds are in */
+		__syncthreads();
 	if (kl)
 		flush_lds();
 	if (nreg)
@@ -539,6 +563,7 @@ struct Geometry {
 	int defer;    /* classify_kernel with 1-/2-B verdicts kept in LDS (and past a full
 	                 buffer in kVregs registers per lane) and written in batches: 1 where
 	                 that takes <= 2 writes per block, 2 always (tests) */
+	bool wave;    /* classify_kernel with wave-staged tiles (WL) */
 };
 
 /* geo.defer: what the CU's LDS leaves the block at geo.bpc_cap blocks per
@@ -564,7 +589,10 @@ static hipError_t launch_nt(KParams k, bool tlds, uint32_t lds, int num_cus, con
 			lds = base + k.vcap * NT * vb;
 		}
 	}
-	const ClassifyFn fn = tlds ? classify_kernel<MODE, true, DEPTH, NT> : classify_kernel<MODE, false, DEPTH, NT>;
+	const ClassifyFn fn = geo.wave ? (tlds ? classify_kernel<MODE, true, DEPTH, NT, true>
+	                                       : classify_kernel<MODE, false, DEPTH, NT, true>)
+	                               : (tlds ? classify_kernel<MODE, true, DEPTH, NT, false>
+	                                       : classify_kernel<MODE, false, DEPTH, NT, false>);
 	return launch_fn(fn, NT, k, lds, num_cus, geo.bpc_cap, geo.grid, s);
 }
 
@@ -589,13 +617,17 @@ template <int MODE>
 static hipError_t launch_mode(const KParams &k, bool tlds, const Geometry &geo,
                               uint32_t tab_lds, uint32_t hist_bytes, int num_cus, hipStream_t s)
 {
-	if (geo.pair) {
-		const uint32_t lds = hist_bytes + tab_lds;
-		if (geo.threads == 1024)
-			return launch_pair<MODE, 1024>(k, tlds, lds, num_cus, geo, s);
-		if (geo.threads == 512)
-			return launch_pair<MODE, 512>(k, tlds, lds, num_cus, geo, s);
-		return launch_pair<MODE, 256>(k, tlds, lds, num_cus, geo, s);
+	if constexpr (MODE != kModeProbe) { /* the probe's kernel shape is the tile kernel's */
+		if (geo.pair) {
+			const uint32_t lds = hist_bytes + tab_lds;
+			if (geo.threads == 1024)
+				return launch_pair<MODE, 1024>(k, tlds, lds, num_cus, geo, s);
+			if (geo.threads == 512)
+				return launch_pair<MODE, 512>(k, tlds, lds, num_cus, geo, s);
+			return launch_pair<MODE, 256>(k, tlds, lds, num_cus, geo, s);
+		}
+	} else if (geo.pair) {
+		return hipErrorInvalidValue;
 	}
 	const uint32_t lds = (uint32_t)geo.threads * 64 + hist_bytes + tab_lds;
 #define GCL_LAUNCH(D, T) \
@@ -662,6 +694,7 @@ static Geometry choose_geometry(const gcl_ctx *c, uint32_t tab_lds, uint32_t his
 	g.depth = tuned(c->tune.depth, g.depth);
 	g.bpc_cap = tuned(c->tune.blocks_per_cu, g.bpc_cap);
 	g.grid = tuned(c->tune.grid, 0);
+	g.wave = tuned(c->tune.stage, kDefaultStage) == 1;
 	return g;
 }
 
@@ -673,9 +706,21 @@ extern "C" int gcl_classify(struct gcl_ctx *c, const struct gcl_batch *b,
 	return gcl_classify_ex(c, b, &o, hip_stream);
 }
 
+static int batch_launch(gcl_ctx *c, const gcl_batch *b, const gcl_out *out, hipStream_t s, bool probe);
+
+/* a dense batch: fixed slots, no side arrays, every header granule in range
+ * (classify_kernel's batches; the others run on classify_pair_kernel) */
+static bool dense_batch(const gcl_ctx *c, const gcl_batch *b)
+{
+	return !(b->offs || b->olflags || b->fdir_hi || b->dst_hint || (c->cfg.default_olflags & GCL_F_FDIR_ID) ||
+	         b->frames_len < (b->n - 1) * b->stride + GCL_HDR_GRANULE);
+}
+
 extern "C" int gcl_access_probe(struct gcl_ctx *c, const struct gcl_batch *b, void *out,
                                 uint32_t vbytes, void *hip_stream)
 {
+	const bool minimal = vbytes & GCL_PROBE_MIN;
+	vbytes &= ~(uint32_t)GCL_PROBE_MIN;
 	if (!c || !b || !out || (vbytes != 1 && vbytes != 2 && vbytes != 4 && vbytes != 8))
 		return -EINVAL;
 	if (b->n == 0)
@@ -685,6 +730,11 @@ extern "C" int gcl_access_probe(struct gcl_ctx *c, const struct gcl_batch *b, vo
 		return -EINVAL;
 	if (hipSetDevice(c->device) != hipSuccess)
 		return -ENODEV;
+	if (!minimal && vbytes == verdict_bytes(c) && dense_batch(c, b)) {
+		/* the classify launch itself, rx_one_pkt folded away */
+		const struct gcl_out o = {out, nullptr, nullptr, nullptr};
+		return batch_launch(c, b, &o, (hipStream_t)hip_stream, true);
+	}
 	KParams k = {};
 	k.frames = b->frames;
 	k.frames_len = b->frames_len;
@@ -713,11 +763,17 @@ extern "C" int gcl_classify_ex(struct gcl_ctx *c, const struct gcl_batch *b,
 {
 	if (!c || !b || !out)
 		return -EINVAL;
+	return batch_launch(c, b, out, (hipStream_t)hip_stream, false);
+}
+
+/* gcl_classify_ex, or with @probe (gcl_access_probe, dense batches) the same
+ * launch in kModeProbe: no counts, stats or timing */
+static int batch_launch(gcl_ctx *c, const gcl_batch *b, const gcl_out *out, hipStream_t s, bool probe)
+{
 	void *verdicts = out->verdicts;
 	uint64_t *runtime_counts = out->runtime_counts, *stats = out->stats;
 	if (out->trans && !(c->cfg.flags & GCL_CFG_TRANS_HASH))
 		return -EINVAL;
-	hipStream_t s = (hipStream_t)hip_stream;
 	if (b->n == 0)
 		return 0;
 	if (!b->frames || (!b->offs && (b->stride < 16 || (b->stride & 15) || b->stride > (1u << 20))))
@@ -766,9 +822,7 @@ extern "C" int gcl_classify_ex(struct gcl_ctx *c, const struct gcl_batch *b,
 	k.default_flags = c->cfg.default_olflags;
 
 	/* the specialised fast path needs every header granule in range */
-	bool general = b->offs || b->olflags || b->fdir_hi || b->dst_hint ||
-	               (c->cfg.default_olflags & GCL_F_FDIR_ID) ||
-	               b->frames_len < (b->n - 1) * b->stride + GCL_HDR_GRANULE;
+	const bool general = !dense_batch(c, b);
 	uint32_t tab_bytes = c->image_bytes;
 	uint32_t hist_bytes = ((c->cfg.max_runtimes + 3) & ~3u) * 4;
 	const bool tlds = tab_bytes <= kLdsTableBudget && c->tune.tables != 1;
@@ -782,7 +836,7 @@ extern "C" int gcl_classify_ex(struct gcl_ctx *c, const struct gcl_batch *b,
 	HipErr he;
 
 	hipEvent_t e0 = nullptr, e1 = nullptr;
-	if ((c->cfg.flags & GCL_CFG_PROFILE) && c->prof_seq++ % c->prof_every == 0) {
+	if (!probe && (c->cfg.flags & GCL_CFG_PROFILE) && c->prof_seq++ % c->prof_every == 0) {
 		e0 = prof_event(c);
 		e1 = prof_event(c);
 		if (!e0 || !e1) { /* no timing for this launch */
@@ -796,7 +850,10 @@ extern "C" int gcl_classify_ex(struct gcl_ctx *c, const struct gcl_batch *b,
 		}
 	}
 	hipError_t err;
-	switch (c->cfg.hash_mode) {
+	switch (probe ? kModeProbe : (int)c->cfg.hash_mode) {
+	case kModeProbe:
+		err = launch_mode<kModeProbe>(k, tlds, geo, tlds ? tab_bytes : 0, hist_bytes, c->num_cus, s);
+		break;
 	case GCL_HASH_NIC:
 		err = launch_mode<GCL_HASH_NIC>(k, tlds, geo, tlds ? tab_bytes : 0, hist_bytes, c->num_cus, s);
 		break;

@@ -175,7 +175,21 @@ __device__ __forceinline__ uint4 tile_load(const void *p)
  * this tile alone and the next tile's loads stay in flight (DEPTH 2); one
  * conditional load path makes it wait for everything.
  */
-template <int NT>
+/*
+ * Chunk c of a tile is 16-B chunk c & 3 of tile packet c >> 2.  The lane's
+ * j-th chunk: with block staging (!WL) chunk j * NT + tid, so each wave
+ * instruction reads 1 KiB of 64-B slots and the tile is complete only after
+ * a block barrier; with wave staging (WL) chunk 256 w + 64 j + lane of wave
+ * w, the same 1 KiB per instruction but only of the wave's own 64 packets,
+ * which its own lanes classify: no block barrier per tile.
+ */
+template <int NT, bool WL>
+__device__ __forceinline__ uint32_t tile_chunk(int j)
+{
+	return WL ? (threadIdx.x >> 6) * 256 + j * 64 + (threadIdx.x & 63) : j * NT + threadIdx.x;
+}
+
+template <int NT, bool WL>
 __device__ __forceinline__ void load_tile(const KParams &k, uint64_t tile, bool live, uint4 r[4])
 {
 	const uint8_t *dummy = k.tables; /* device table image: >= 16 B, always mapped */
@@ -184,7 +198,7 @@ __device__ __forceinline__ void load_tile(const KParams &k, uint64_t tile, bool 
 	const uint8_t *base = k.frames + t0 * k.stride;
 #pragma unroll
 	for (int j = 0; j < 4; j++) {
-		const uint32_t c = j * NT + threadIdx.x, p = c >> 2;
+		const uint32_t c = tile_chunk<NT, WL>(j), p = c >> 2;
 		const uint8_t *a = p < lim ? base + (p * (uint32_t)k.stride + (c & 3) * 16) : dummy;
 		r[j] = tile_load(a);
 	}
@@ -591,15 +605,31 @@ __device__ __forceinline__ void put_verdict(const KParams &k, uint64_t idx, uint
 		store_wt((uint64_t *)k.verdicts + idx, w);
 }
 
-template <int NT>
+template <int NT, bool WL>
 __device__ __forceinline__ void stage_tile(uint4 *tile, const uint4 r[4])
 {
 #pragma unroll
 	for (int j = 0; j < 4; j++) {
-		int c = j * NT + (int)threadIdx.x;
+		const uint32_t c = tile_chunk<NT, WL>(j);
 		tile[tile_slot(c >> 2, c & 3)] = r[j];
 	}
 }
+
+/* Order a wave's own LDS accesses around a wave-staged tile (the rocPRIM
+ * wave barrier): a wave's LDS operations execute in order, so its lanes see
+ * each other's stores without s_barrier; this only keeps the compiler from
+ * moving the tile's reads above its stores, or the next stores above them. */
+__device__ __forceinline__ void wave_lds_barrier()
+{
+	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+	__builtin_amdgcn_wave_barrier();
+	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+/* classify_kernel's MODE for gcl_access_probe: the same launch -- tiles,
+ * staging, drains, barriers, deferred verdict writes -- with rx_one_pkt
+ * replaced by a fold of the three header rows it reads */
+constexpr int kModeProbe = 3;
 
 /* End of a classify launch: the block's histogram (all its waves' adds
  * done) and every wave's counters into the device totals. */
@@ -645,5 +675,7 @@ constexpr int kDefaultPairLean = 1;
 /* gcl_tune.defer default (Geometry::defer): udp64 328.2-329.1 -> 323.4-324.2
  * us, three fresh processes (profiles/r05_defer_ab.jsonl) */
 constexpr int kDefaultDefer = 1;
+/* gcl_tune.stage default: 0 block-staged tiles, 1 wave-staged */
+constexpr int kDefaultStage = 0;
 
 } // namespace gclk

@@ -32,6 +32,7 @@ V2_Q_MASK, V2_KIND, V2_DELIVER, V2_WAKE, V2_OTHER, V2_QUEUES = 0x3FFF, 0xC000, 0
 V1_Q_MASK, V1_OTHER, V1_QUEUES = 0x7F, 0x80, 0x80
 PAIR_NEW_READS, PAIR_NEW_WRITES, PAIR_TRIES, PAIR_RUN = 0x1, 0x2, 24, 2
 PAIR_QUIET, PAIR_VERBOSE = 0x10000, 0x20000
+PROBE_MIN = 0x100  # gcl_access_probe: the layout's minimal-request probe
 
 F_RSS_HASH, F_FDIR_ID = 0x01, 0x02
 F_IP_CKSUM_MASK, F_IP_CKSUM_UNKNOWN, F_IP_CKSUM_BAD = 0x0C, 0x00, 0x04
@@ -137,11 +138,12 @@ class GclTune(ctypes.Structure):
     (GCL_TUNE_AUTO = -1 everywhere: the library's own choice)."""
     _fields_ = [("size", ctypes.c_uint32), ("tables", ctypes.c_int32), ("depth", ctypes.c_int32),
                 ("threads", ctypes.c_int32), ("grid", ctypes.c_int32), ("blocks_per_cu", ctypes.c_int32),
-                ("defer", ctypes.c_int32), ("pair_lean", ctypes.c_int32), ("loop64", ctypes.c_int32),
+                ("defer", ctypes.c_int32), ("pair_lean", ctypes.c_int32), ("stage", ctypes.c_int32),
+                ("loop64", ctypes.c_int32),
                 ("loop_lean", ctypes.c_int32), ("loop_spec", ctypes.c_int32),
                 ("loop_phase_max", ctypes.c_int32), ("loop_phase_up", ctypes.c_int32),
                 ("loop_phase_down", ctypes.c_int32), ("loop_prefetch", ctypes.c_int32),
-                ("debug", ctypes.c_uint32), ("loop_t0", ctypes.c_uint64)]
+                ("debug", ctypes.c_uint32), ("pad", ctypes.c_uint32), ("loop_t0", ctypes.c_uint64)]
 
 
 TUNE_AUTO = -1
@@ -315,7 +317,7 @@ def make_tune(**kw):
         t.loop_phase_up = ph[1] if len(ph) > 1 else 16
         t.loop_phase_down = ph[2] if len(ph) > 2 else 1
     for k, v in kw.items():
-        if not hasattr(t, k) or k == "size":
+        if not hasattr(t, k) or k in ("size", "pad"):
             raise AttributeError(f"struct gcl_tune has no field {k}")
         setattr(t, k, int(v))
     return t
@@ -595,12 +597,16 @@ class Classifier:
                       "gcl_classify_ex")
 
     def access_probe(self, frames, n, stride=0, out=None, vbytes=None, offs=None, olflags=None,
-                     rss=None, frames_len=None, stream=None):
-        """gcl_access_probe: a classify launch's loads and stores without the
-        classification (the layout's ceiling).  Asynchronous."""
+                     rss=None, frames_len=None, stream=None, minimal=False):
+        """gcl_access_probe: for a dense batch at the context's verdict width,
+        the classify launch itself with rx_one_pkt folded away (the kernel's
+        own ceiling); otherwise, or with @minimal, the fewest requests the
+        frame layout allows (the layout's ceiling).  Asynchronous."""
         vbytes = self.vbytes if vbytes is None else vbytes
         if out is None or _nbytes(out) < vbytes * n:
             raise ValueError("probe output buffer too small")
+        if minimal:
+            vbytes |= PROBE_MIN
         b = GclBatch(frames=_ptr(frames), frames_len=_frames_len(frames, frames_len),
                      stride=stride, offs=_ptr(offs), olflags=_ptr(olflags), rss=_ptr(rss),
                      fdir_hi=None, pkt_len=None, n=n, dst_hint=None)

@@ -384,16 +384,26 @@ int gcl_classify_ex(struct gcl_ctx *ctx, const struct gcl_batch *b, const struct
                     void *hip_stream);
 
 /*
- * gcl_access_probe - the memory requests one gcl_classify launch over @b
- * cannot do without, and nothing else: the ceiling the frame layout itself
- * sets (e.g. one 128-B line fetched per 64-B header of a 1536-B slot).  One
- * 16-B load per packet of the line holding frame byte 0 (plus one of the
- * next line when frame bytes [0, 40) cross into it), @b's offs, olflags and
- * rss when given, and @vbytes (1, 2, 4 or 8) bytes stored per packet to device
- * memory @out (not verdicts: a checksum of the loads).  Asynchronous on
- * @hip_stream; 0, -EINVAL or -EIO.  A measurement aid beside the classify
- * kernel's roofline (bench.py roofline.ceiling_ms), not part of the rx path.
+ * gcl_access_probe - a measurement aid beside the classify kernel's roofline
+ * (bench.py roofline.ceiling_ms), not part of the rx path.  Asynchronous on
+ * @hip_stream; 0, -EINVAL or -EIO.  @out receives @vbytes (1, 2, 4 or 8)
+ * bytes per packet (not verdicts: a fold of the loaded bytes).
+ *
+ * For a dense batch (fixed slots, no side arrays) at the context's own
+ * verdict width: the gcl_classify launch itself -- the same geometry, tile
+ * loads, LDS staging, drains and barriers, and the same verdict writes
+ * (deferred where the context defers them) -- with rx_one_pkt replaced by a
+ * fold of the header words it reads.  So its time is the kernel's memory
+ * shape with nothing computed: the kernel's own ceiling.
+ *
+ * Otherwise, or with GCL_PROBE_MIN or'ed into @vbytes: the memory requests
+ * one launch over @b cannot do without, and nothing else -- the ceiling the
+ * frame layout itself sets (e.g. one 128-B line fetched per 64-B header of a
+ * 1536-B slot).  One 16-B load per packet of the line holding frame byte 0
+ * (plus one of the next line when frame bytes [0, 40) cross into it), @b's
+ * offs, olflags and rss when given, and one write-through store per packet.
  */
+#define GCL_PROBE_MIN 0x100
 int gcl_access_probe(struct gcl_ctx *ctx, const struct gcl_batch *b, void *out, uint32_t vbytes,
                      void *hip_stream);
 
@@ -423,6 +433,8 @@ struct gcl_tune {
 	                            registers and written after the reads where that takes
 	                            <= 2 writes per block (default), 2 always */
 	int32_t pair_lean;       /* classify_pair_kernel: plain-IPv4 waves on the lean path (1) */
+	int32_t stage;           /* classify_kernel tiles: 0 staged by the block (a barrier per
+	                            tile), 1 by each wave for its own 64 packets (no barrier) */
 	/* the persistent loop */
 	int32_t loop64;          /* 0: bursts <= 64 through the general loop kernel */
 	int32_t loop_lean;       /* plain-IPv4 bursts on the lean path (1) */
@@ -432,6 +444,7 @@ struct gcl_tune {
 	int32_t loop_phase_down; /* its step down (<= up) */
 	int32_t loop_prefetch;   /* the next ticket's poll during classification (0 / 1) */
 	uint32_t debug;          /* 1: loop diagnostics to stderr */
+	uint32_t pad;
 	uint64_t loop_t0;        /* tickets start after loop_t0 (rounded down to a multiple of the
 	                            ring's slots): tests of the stamps' wrap */
 };

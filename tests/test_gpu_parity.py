@@ -304,9 +304,10 @@ def test_gpu_dense_verdict1(g, orc, wl, R, T):
 DEFER_FORMS = {0: "per-packet stores", 1: "deferred (<= 2 writes per block, the default)", 2: "deferred always"}
 
 
+@pytest.mark.parametrize("stage", [0, 1])
 @pytest.mark.parametrize("defer", sorted(DEFER_FORMS))
 @pytest.mark.parametrize("wl,R,T,vb", [(0, 16, 8, 1), (0, 16, 8, 2), (1, 1024, 4, 2)])
-def test_gpu_dense_narrow_verdicts(g, orc, wl, R, T, vb, defer):
+def test_gpu_dense_narrow_verdicts(g, orc, wl, R, T, vb, defer, stage):
     """Dense slots' 1- and 2-B verdicts in every form (gcl_tune.defer): the
     tile kernel's write-through byte and short stores per packet, or kept in
     LDS and written 16 B per lane in batches; the partial last tile
@@ -321,7 +322,7 @@ def test_gpu_dense_narrow_verdicts(g, orc, wl, R, T, vb, defer):
     del df
     tb = 3 if vb == 1 else 4
     clf = g.Classifier(0, R, g.HASH_JENKINS, g.CFG_VERDICT1 if vb == 1 else g.CFG_VERDICT2, thread_bits=tb,
-                       tune={"defer": defer})
+                       tune={"defer": defer, "stage": stage})
     t = orc.Tables(R, g.HASH_JENKINS, 0, g.F_RSS_HASH | g.F_IP_CKSUM_GOOD)
     for r in range(R):
         act = r % T
@@ -331,7 +332,7 @@ def test_gpu_dense_narrow_verdicts(g, orc, wl, R, T, vb, defer):
     v, c, st = gpu_run(g, clf, frames, n, stride)
     ve, ce, se = t.classify(frames, n, stride)
     w = to_verdict1(ve, [T] * R, tb) if vb == 1 else to_verdict2(ve, [T] * R, tb)
-    assert_same(v, w, f"narrow verdicts wl={wl} vb={vb} {DEFER_FORMS[defer]}")
+    assert_same(v, w, f"narrow verdicts wl={wl} vb={vb} {DEFER_FORMS[defer]} stage={stage}")
     assert (c == ce).all() and (st == se).all()
 
 
@@ -341,7 +342,11 @@ def test_gpu_dense_narrow_verdicts(g, orc, wl, R, T, vb, defer):
     (2, {"threads": 512, "grid": 7}), (2, {"threads": 1024, "grid": 7}),
     (1, {"grid": 20}), (1, {"grid": 40}), (1, {"grid": 70}),
     (1, {"grid": 20, "depth": 1}), (1, {"threads": 512, "grid": 12}),
-    (1, {"tables": 1, "grid": 40}), (2, {"tables": 1, "grid": 9})])
+    (1, {"tables": 1, "grid": 40}), (2, {"tables": 1, "grid": 9}),
+    # wave-staged tiles: the block meets only around the buffer's writes
+    (1, {"stage": 1}), (2, {"stage": 1, "grid": 3}), (1, {"stage": 1, "grid": 20}),
+    (2, {"stage": 1, "threads": 512, "grid": 7}), (1, {"stage": 1, "threads": 1024, "grid": 7}),
+    (2, {"stage": 1, "grid": 5, "depth": 1}), (1, {"stage": 1, "tables": 1, "grid": 40})])
 @pytest.mark.parametrize("vb", [1, 2])
 def test_gpu_dense_deferred_flushes(g, orc, vb, defer, env):
     """The tile kernel's LDS verdict buffer when a block walks more tiles
@@ -1147,6 +1152,9 @@ LOOP_GEOMETRIES = [
     {"threads": 1024, "grid": 7},
     {"threads": 512, "grid": 5},
     {"blocks_per_cu": 1},
+    {"stage": 1, "grid": 16},
+    {"stage": 1, "depth": 1, "grid": 5},
+    {"stage": 1, "threads": 1024, "grid": 7},
 ]
 
 
@@ -1442,11 +1450,11 @@ def test_gpu_full_size_ingress_pool(g, orc, order):
 
 @pytest.mark.parametrize("vbytes", [2, 4, 8])
 def test_gpu_access_probe(g, vbytes):
-    """gcl_access_probe (the layout-ceiling probe beside the roofline) reads
-    what it claims: packet p's stored word is the XOR of the four dwords of
-    the 16-B chunk holding its frame byte 0 and of the first dword of the next
-    line's chunk when frame bytes [0, 40) cross into it (fixed slots, and
-    offsets that straddle lines)."""
+    """gcl_access_probe's minimal-request form (GCL_PROBE_MIN; the layout's
+    ceiling) reads what it claims: packet p's stored word is the XOR of the
+    four dwords of the 16-B chunk holding its frame byte 0 and of the first
+    dword of the next line's chunk when frame bytes [0, 40) cross into it
+    (fixed slots, and offsets that straddle lines)."""
     rng = np.random.default_rng(99)
     n, stride = 5000, 1536
     frames = rng.integers(0, 256, size=n * stride, dtype=np.uint8)
@@ -1468,7 +1476,7 @@ def test_gpu_access_probe(g, vbytes):
             x[i] = v
         return x & np.uint64(mask)
 
-    clf.access_probe(f, n, stride, out=out, vbytes=vbytes)
+    clf.access_probe(f, n, stride, out=out, vbytes=vbytes, minimal=True)
     torch.cuda.synchronize()
     got = out.cpu().numpy().view(dt).astype(np.uint64)
     assert (got == want(np.arange(n, dtype=np.uint64) * np.uint64(stride))).all()
@@ -1479,6 +1487,38 @@ def test_gpu_access_probe(g, vbytes):
     torch.cuda.synchronize()
     got = out.cpu().numpy().view(dt).astype(np.uint64)
     assert (got == want(offs)).all()
+
+
+@pytest.mark.parametrize("vb,R,T,stride,tune", [(1, 16, 8, 64, {}), (1, 16, 8, 64, {"stage": 1}),
+                                                (2, 16, 8, 64, {"defer": 2, "grid": 7}),
+                                                (2, 1024, 4, 1536, {}), (8, 16, 8, 64, {}),
+                                                (1, 16, 8, 64, {"defer": 0, "stage": 1, "depth": 1})])
+def test_gpu_access_probe_kernel_shape(g, vb, R, T, stride, tune):
+    """gcl_access_probe on a dense batch at the context's verdict width is the
+    classify launch itself with rx_one_pkt folded away (the kernel's own
+    ceiling): packet p's output is the low vb bytes of the XOR of the header
+    dwords rx_one_pkt reads (frame dwords 3 and 5-10), written through the
+    same deferred or per-packet verdict path; the ragged last tile is cut at
+    n (a guard byte past it stays)."""
+    rng = np.random.default_rng(1500 + vb + stride + len(tune))
+    n = (1 << 18) + 77
+    frames = rng.integers(0, 256, size=n * stride, dtype=np.uint8)
+    fl, tb = {1: (g.CFG_VERDICT1, 3), 2: (g.CFG_VERDICT2, 2 if R == 1024 else 3), 8: (0, 0)}[vb]
+    clf = g.Classifier(0, R, 1, fl, thread_bits=tb, tune=tune)
+    clf.runtime_set(0, g.runtime_ip(0), T, T, g.steer_flows(T, list(range(T))))
+    out = torch.full((n * vb + 64,), 0xEE, dtype=torch.uint8, device="cuda")
+    clf.access_probe(dev(frames), n, stride, out=out)
+    torch.cuda.synchronize()
+    d = frames.reshape(n, stride)[:, :44].view(np.uint32)
+    x = d[:, 3] ^ d[:, 5] ^ d[:, 6] ^ d[:, 7] ^ d[:, 8] ^ d[:, 9] ^ d[:, 10]
+    got = out.cpu().numpy()
+    if vb == 8:
+        assert (got[:n * 8].view(np.uint64) == x.astype(np.uint64)).all()
+    else:
+        want = (x & np.uint32((1 << (8 * vb)) - 1)).astype({1: np.uint8, 2: np.uint16}[vb])
+        assert (got[:n * vb].view(want.dtype) == want).all()
+    assert (got[n * vb:] == 0xEE).all()
+    clf.close()
 
 
 def test_gpu_offsets_at_the_top_of_u64(g, orc):
