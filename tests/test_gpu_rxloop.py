@@ -128,6 +128,7 @@ def test_rxloop_fuzz_vs_oracle(g, orc, mode, vb, flags, inline, k64):
             loop.release(tk)
         got = np.concatenate(got)
         ps = poll_stats_settled(loop, len(bursts(n)))
+        assert sum(ps.values()) == len(bursts(n)), ps  # the writer wave took every burst
         if early:  # every burst taken with its poll (early, or re-read if stale)
             assert ps["late"] == 0, ps
     finally:
@@ -137,8 +138,10 @@ def test_rxloop_fuzz_vs_oracle(g, orc, mode, vb, flags, inline, k64):
     bad = np.nonzero(got != w)[0]
     assert not len(bad), f"{len(bad)} differ, first {bad[0]}: {got[bad[0]]} vs {w[bad[0]]}"
     torch.cuda.synchronize()
-    assert (cnt.cpu().numpy().astype(np.uint64) == ce).all()
-    assert (st.cpu().numpy().astype(np.uint64) == se).all()
+    c, s_ = cnt.cpu().numpy().astype(np.uint64), st.cpu().numpy().astype(np.uint64)
+    diff = {int(i): (int(c[i]), int(ce[i])) for i in np.nonzero(c != ce)[0]}
+    assert not diff and (s_ == se).all(), (f"counts (got, want) {diff}; stats {s_.tolist()} vs {se.tolist()}; "
+                                           f"polls {ps}")
 
 
 LEAN_CASES = [(m, vb, fl, lf) for m in (0, 1, 2) for vb in (8, 4, 2, 1) for fl, lf in ((0, 2), (2, 0))]
