@@ -236,6 +236,23 @@ def compact(result, detail_path=DETAIL_PATH):
                          "records_4x8_nic": _pipe_row(rows, 64, 4, rec, "nic"),
                          "records_1x1_jenkins": _pipe_row(rows, 64, 1, rec, "jenkins"),
                          "records_4x8_jenkins": _pipe_row(rows, 64, 4, rec, "jenkins")}
+        ing = e2e.get("rx_burst_pipeline_ingress")
+        if ing:
+            def _ing(rows, **want):
+                for row in rows or ():
+                    if all(row.get(k) == v for k, v in want.items()):
+                        return _pick(row, "mpps_one_core", "burst_latency_p50_us", "burst_latency_p99_us",
+                                     "ns_per_pkt", "nic_wait_frac", "delivered_check", "mpps_samples", "error")
+                return None
+            rec = "read in place, stamped header records in the slot"
+            e["pipeline_cold_headers"] = {
+                "records_1x1_nic": _ing(ing.get("gpu"), workers=1, verdicts=rec),
+                "records_4x8_nic": _ing(ing.get("gpu"), workers=4, verdicts=rec),
+                "records_8x16_nic": _ing(ing.get("gpu"), workers=8, verdicts=rec),
+                "offsets_4x8_nic": _ing(ing.get("gpu"), workers=4, verdicts="read in place"),
+                "cpu_1core_classify_nic": _ing(ing.get("cpu"), post="classify only"),
+                "cpu_1core_lrpc_nic": _ing(ing.get("cpu"), post="classify + rx_make_cmd + lrpc_send"),
+            }
         lp = e2e.get("rxloop", {})
         for k in ("loop_burst64_w1_d1_hdr_records", "loop_burst64_w4_d8_hdr_records"):
             if k in lp:
@@ -940,6 +957,7 @@ def e2e_bench(device, vbytes=VERDICT_BYTES, reps=3):
         torch.cuda.empty_cache()
     out["rxloop"] = rxloop_bench(device, vbytes)
     out["rx_burst_pipeline"] = rxpipe_bench()
+    out["rx_burst_pipeline_ingress"] = ingress_pipeline_bench()
     out["mixed"]["trace_replay"] = trace_replay(device)
     out["ingress_pool"] = ingress_pool_bench(device, INGRESS_VERDICT_BYTES)
     return out
@@ -1045,6 +1063,83 @@ def rxpipe_bench(reps=3):
         row["mpps_samples"] = [x["mpps_one_core"] for x in samples]
         rows.append(row)
     return {"host_cores": 1, "reps_per_row": reps, "reported": "median of the row's runs", "runs": rows}
+
+
+def cpupipe_exe():
+    """tools/cpupipe built for this host (-march=native, as the CPU baseline's
+    oracle is, orc.build(native=True)) on first use, else the portable build
+    __graft_entry__.build() made; None if neither exists."""
+    import subprocess
+    src = os.path.join(ROOT, "tools", "cpupipe.cpp")
+    native = os.path.join(ROOT, "tools", "_build", "cpupipe_native")
+    portable = os.path.join(ROOT, "tools", "cpupipe")
+    if not (os.access(native, os.X_OK) and os.path.getmtime(native) >= os.path.getmtime(src)):
+        try:
+            os.makedirs(os.path.dirname(native), exist_ok=True)
+            obj = native + "_orc.o"
+            subprocess.run(["gcc", "-std=gnu11", "-O3", "-march=native", "-fPIC", "-c",
+                            os.path.join(ROOT, "oracle", "orc.c"), "-o", obj], check=True, capture_output=True,
+                           timeout=120)
+            subprocess.run([os.environ.get("HIPCC", "/opt/rocm/bin/hipcc"), "-O3", "-march=native",
+                            "-I" + os.path.join(ROOT, "include"), "-o", native, src, "-x", "none", obj, "-lpthread"],
+                           check=True, capture_output=True, timeout=300)
+        except (OSError, subprocess.SubprocessError) as e:
+            log("cpupipe native build failed, using the portable build:", e)
+            native = None
+    if native and os.access(native, os.X_OK):
+        return native
+    return portable if os.access(portable, os.X_OK) else None
+
+
+def median_runs(cmd, env, reps, timeout=180):
+    """@reps fresh runs of a pipeline tool: (median row with every run's rate, error row or None)."""
+    import subprocess
+    samples = []
+    for _ in range(reps):
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env)
+        except subprocess.TimeoutExpired:
+            return None, {"cmd": " ".join(cmd[1:]), "error": "timeout"}
+        if r.returncode != 0:
+            return None, {"cmd": " ".join(cmd[1:]), "error": r.stderr.strip()[-200:]}
+        samples.append(json.loads(r.stdout.strip().splitlines()[-1]))
+    samples.sort(key=lambda x: x["mpps_one_core"])
+    row = dict(samples[len(samples) // 2])
+    row["mpps_samples"] = [x["mpps_one_core"] for x in samples]
+    return row, None
+
+
+def ingress_pipeline_bench(reps=3):
+    """The rx_burst replacement and the reference's CPU path on IDENTICAL
+    inputs with cold headers: bursts of 64 mbufs of the
+    reference's pool geometry (data at element + 344 of 9408-B elements,
+    defs.h:503-506) from an emulated NIC that writes every frame with
+    non-temporal stores just before handing its descriptor over (no CPU cache
+    holds the header, as behind a NIC without DDIO) and recycles the mbufs
+    through a mempool (tools/nicsim.h).  GPU rows: tools/rxpipe
+    RXPIPE_POOL=ingress (header records and stamped offsets); CPU rows:
+    tools/cpupipe, the oracle's rx_one_pkt with rx.c's direct loads and
+    prefetch stride 2 (+ lrpc_send) on one core; NIC hash.rss in both."""
+    exe = os.path.join(ROOT, "tools", "rxpipe")
+    cpu_exe = cpupipe_exe()
+    env = {**os.environ, "RXPIPE_POOL": "ingress", "RXPIPE_HASH": "nic"}
+    out = {"inputs": ("NIC-emulated ingress pool: 8192 mbufs at element + 344 of 9408-B elements, frames "
+                      "written by 2 NIC threads with non-temporal stores (cold headers), mempool recycling; "
+                      "NIC hash.rss"), "reps_per_row": reps, "gpu": [], "cpu": []}
+    if os.access(exe, os.X_OK):
+        for cfg in (("64", "1", "1", "20000", "records"), ("64", "4", "8", "20000", "records"),
+                    ("64", "8", "16", "40000", "records"), ("64", "4", "8", "20000"), ("64", "8", "16", "40000")):
+            row, err = median_runs([exe, *cfg], env, reps)
+            out["gpu"].append(row or err)
+            if err:
+                break
+    if cpu_exe:
+        for post in ("classify", "lrpc"):
+            row, err = median_runs([cpu_exe, "100000", post], env, reps)
+            out["cpu"].append(row or err)
+            if err:
+                break
+    return out
 
 
 def rxloop_bench(device, vbytes, iters=2000, rounds=3):

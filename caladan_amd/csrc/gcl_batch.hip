@@ -39,11 +39,9 @@ namespace gclk {
  * of the batch), with the frames of the next DEPTH tiles in flight in
  * registers while a tile is parsed.
  */
-template <int MODE, bool TLDS, int DEPTH, int NT, bool WL>
+template <int MODE, bool TLDS, int DEPTH, int NT>
 /* 4 waves per SIMD (<= 128 VGPRs): the 1024 resident lanes per CU the
- * geometry policy plans for, at every tile size.  WL: each wave stages and
- * classifies its own 64 packets of the tile (tile_chunk), so a tile needs no
- * block barrier; the block meets only to write its deferred verdicts. */
+ * geometry policy plans for, at every tile size */
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4)))
 classify_kernel(KParams k)
 {
@@ -168,37 +166,40 @@ classify_kernel(KParams k)
 		else
 			nreg++;
 		if (kl == k.vcap && nreg == rcap) {
-			if (WL) /* every wave's verdicts of these tiles are in */
-				__syncthreads();
 			flush_lds();
 			flush_regs();
 			kf += kl + nreg;
 			kl = nreg = 0;
-			if (WL) /* read out before any wave writes the buffer again */
-				__syncthreads();
 		}
 	};
 	/* rx_one_pkt on this lane's row, or (gcl_access_probe) the rows it
 	 * reads folded, after the same drain */
+	/* a wave whose packets are all plain IPv4 (IHL 5; a dense batch has no
+	 * FDIR marks or hints) takes classify_lean (k.tlean, one ballot over the
+	 * live lanes), the others classify_core; no transport pre-hash in lean */
+	const bool lean_ok = k.tlean && !k.trans;
 	auto classify = [&](uint64_t tt) -> uint64_t {
 		if constexpr (MODE == kModeProbe) {
 			dense_drain();
 			const uint4 a = tile[tile_slot(tid, 0)], b = tile[tile_slot(tid, 1)], c = tile[tile_slot(tid, 2)];
 			return a.w ^ b.y ^ b.z ^ b.w ^ c.x ^ c.y ^ c.z;
 		} else {
-			return classify_one<MODE, false>(k, tile, tid, tt * NT + tid, tb, hist, cnt);
+			const uint64_t idx = tt * NT + tid;
+			const uint4 w0 = tile[tile_slot(tid, 0)], w1 = tile[tile_slot(tid, 1)], w2 = tile[tile_slot(tid, 2)];
+			HdrWords h;
+			h.d3 = w0.w, h.d5 = w1.y, h.d6 = w1.z, h.d7 = w1.w;
+			h.d8 = w2.x, h.d9 = w2.y, h.d10 = w2.z;
+			if (lean_ok && __all((h.d3 & 0x000FFFFFu) == 0x00050008u)) {
+				const uint32_t rss = MODE == GCL_HASH_NIC && k.rss ? k.rss[idx] : 0u;
+				return classify_lean<MODE, true, true>(k, h, tb, k.default_flags, rss, hist, tid, cnt);
+			}
+			return classify_core<MODE, false, false, false>(k, h, tile, tid, idx, tb, hist, cnt, 0, 64, nullptr);
 		}
 	};
-	auto tile_sync = [&]() {
-		if (WL)
-			wave_lds_barrier();
-		else
-			__syncthreads();
-	};
 	if (t < t_end)
-		load_tile<NT, WL>(k, t, true, ra);
+		load_tile<NT>(k, t, true, ra);
 	if (DEPTH == 2)
-		load_tile<NT, WL>(k, t + step, t + step < t_end, rb);
+		load_tile<NT>(k, t + step, t + step < t_end, rb);
 
 	while (t < t_end) {
 		/* t opaque to the loop optimiser: without it every per-packet
@@ -207,17 +208,17 @@ classify_kernel(KParams k)
 		if constexpr (DEPTH == 2)
 			asm volatile("" : "+s"(t));
 		dense_drain(); /* once per loop iteration too */
-		stage_tile<NT, WL>(tile, ra);
-		tile_sync();
+		stage_tile<NT>(tile, ra);
+		__syncthreads();
 		const uint64_t nxt = t + DEPTH * step;
 		/* in flight while parsing */
-		load_tile<NT, WL>(k, nxt, nxt < t_end, ra);
+		load_tile<NT>(k, nxt, nxt < t_end, ra);
 		{
 			const bool live = t * NT + tid < k.n;
 			const uint64_t w = live ? classify(t) : 0;
 			verdict(t * NT + tid, true, live, w);
 		}
-		tile_sync();
+		__syncthreads();
 		tile_done(t);
 		t += step;
 		if (DEPTH == 2) {
@@ -225,21 +226,19 @@ classify_kernel(KParams k)
 			 * classified) rather than leaving the loop here: a path out of
 			 * the middle of the body, without the rb loads below, would
 			 * make the wait before staging ra wait for everything */
-			stage_tile<NT, WL>(tile, rb);
-			tile_sync();
-			load_tile<NT, WL>(k, t + 2 * step, t + 2 * step < t_end, rb);
+			stage_tile<NT>(tile, rb);
+			__syncthreads();
+			load_tile<NT>(k, t + 2 * step, t + 2 * step < t_end, rb);
 			{
 				const bool live = t < t_end && t * NT + tid < k.n;
 				const uint64_t w = live ? classify(t) : 0;
 				verdict(t * NT + tid, t < t_end, live, w);
 			}
-			tile_sync();
+			__syncthreads();
 			tile_done(t);
 			t += step;
 		}
 	}
-	if (WL) /* every wave's verdicts and histogram adds are in */
-		__syncthreads();
 	if (kl)
 		flush_lds();
 	if (nreg)
@@ -563,7 +562,6 @@ struct Geometry {
 	int defer;    /* classify_kernel with 1-/2-B verdicts kept in LDS (and past a full
 	                 buffer in kVregs registers per lane) and written in batches: 1 where
 	                 that takes <= 2 writes per block, 2 always (tests) */
-	bool wave;    /* classify_kernel with wave-staged tiles (WL) */
 };
 
 /* geo.defer: what the CU's LDS leaves the block at geo.bpc_cap blocks per
@@ -589,10 +587,7 @@ static hipError_t launch_nt(KParams k, bool tlds, uint32_t lds, int num_cus, con
 			lds = base + k.vcap * NT * vb;
 		}
 	}
-	const ClassifyFn fn = geo.wave ? (tlds ? classify_kernel<MODE, true, DEPTH, NT, true>
-	                                       : classify_kernel<MODE, false, DEPTH, NT, true>)
-	                               : (tlds ? classify_kernel<MODE, true, DEPTH, NT, false>
-	                                       : classify_kernel<MODE, false, DEPTH, NT, false>);
+	const ClassifyFn fn = tlds ? classify_kernel<MODE, true, DEPTH, NT> : classify_kernel<MODE, false, DEPTH, NT>;
 	return launch_fn(fn, NT, k, lds, num_cus, geo.bpc_cap, geo.grid, s);
 }
 
@@ -694,7 +689,6 @@ static Geometry choose_geometry(const gcl_ctx *c, uint32_t tab_lds, uint32_t his
 	g.depth = tuned(c->tune.depth, g.depth);
 	g.bpc_cap = tuned(c->tune.blocks_per_cu, g.bpc_cap);
 	g.grid = tuned(c->tune.grid, 0);
-	g.wave = tuned(c->tune.stage, kDefaultStage) == 1;
 	return g;
 }
 
@@ -819,6 +813,7 @@ static int batch_launch(gcl_ctx *c, const gcl_batch *b, const gcl_out *out, hipS
 	k.trans = (uint2 *)out->trans;
 	k.cflags = kernel_cflags(c);
 	k.plean = (uint32_t)tuned(c->tune.pair_lean, kDefaultPairLean);
+	k.tlean = (uint32_t)tuned(c->tune.tile_lean, kDefaultTileLean);
 	k.default_flags = c->cfg.default_olflags;
 
 	/* the specialised fast path needs every header granule in range */

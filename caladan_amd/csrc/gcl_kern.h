@@ -88,6 +88,7 @@ struct KParams {
 	                    holds (0: every verdict stored as it is made) */
 	uint32_t vregs;  /* with vcap: tiles past a full LDS buffer held in registers */
 	uint32_t plean;  /* classify_pair_kernel: plain-IPv4 waves on classify_lean */
+	uint32_t tlean;  /* classify_kernel: plain-IPv4 waves on classify_lean */
 };
 
 /* classify_kernel's verdict registers: kVregs dwords per lane, so 4 * kVregs
@@ -176,20 +177,20 @@ __device__ __forceinline__ uint4 tile_load(const void *p)
  * conditional load path makes it wait for everything.
  */
 /*
- * Chunk c of a tile is 16-B chunk c & 3 of tile packet c >> 2.  The lane's
- * j-th chunk: with block staging (!WL) chunk j * NT + tid, so each wave
- * instruction reads 1 KiB of 64-B slots and the tile is complete only after
- * a block barrier; with wave staging (WL) chunk 256 w + 64 j + lane of wave
- * w, the same 1 KiB per instruction but only of the wave's own 64 packets,
- * which its own lanes classify: no block barrier per tile.
+ * Chunk c of a tile is 16-B chunk c & 3 of tile packet c >> 2; the lane's
+ * j-th chunk is chunk j * NT + tid, so each wave instruction reads 1 KiB of
+ * 64-B slots and the tile is complete after a block barrier.  (Round 6
+ * measured the other mapping -- each wave staging and classifying its own
+ * 64 packets, no barrier per tile -- 3 % slower on udp64 and tcp1500,
+ * profiles/r06_stage_ab.jsonl, and removed it.)
  */
-template <int NT, bool WL>
+template <int NT>
 __device__ __forceinline__ uint32_t tile_chunk(int j)
 {
-	return WL ? (threadIdx.x >> 6) * 256 + j * 64 + (threadIdx.x & 63) : j * NT + threadIdx.x;
+	return j * NT + threadIdx.x;
 }
 
-template <int NT, bool WL>
+template <int NT>
 __device__ __forceinline__ void load_tile(const KParams &k, uint64_t tile, bool live, uint4 r[4])
 {
 	const uint8_t *dummy = k.tables; /* device table image: >= 16 B, always mapped */
@@ -198,7 +199,7 @@ __device__ __forceinline__ void load_tile(const KParams &k, uint64_t tile, bool 
 	const uint8_t *base = k.frames + t0 * k.stride;
 #pragma unroll
 	for (int j = 0; j < 4; j++) {
-		const uint32_t c = tile_chunk<NT, WL>(j), p = c >> 2;
+		const uint32_t c = tile_chunk<NT>(j), p = c >> 2;
 		const uint8_t *a = p < lim ? base + (p * (uint32_t)k.stride + (c & 3) * 16) : dummy;
 		r[j] = tile_load(a);
 	}
@@ -498,7 +499,9 @@ __device__ __forceinline__ uint64_t classify_core(const KParams &k, const HdrWor
  */
 /* HIST: add the packet to the LDS histogram (classify_pair_kernel) rather
  * than hand its runtime to the loop's writer wave in @hist[tid] */
-template <int MODE, bool HIST = false>
+/* DRAIN (classify_kernel's dense slots): dense_drain() before the IP
+ * lookup, where classify_core drains */
+template <int MODE, bool HIST = false, bool DRAIN = false>
 __device__ __forceinline__ uint64_t classify_lean(const KParams &k, const HdrWords &h, const Tables &tb,
                                                   uint32_t flags, uint32_t rss, uint32_t *hist, int tid,
                                                   Counters &cnt)
@@ -521,6 +524,8 @@ __device__ __forceinline__ uint64_t classify_lean(const KParams &k, const HdrWor
 	if (k.cflags & GCL_CFG_HASH16)
 		hash &= 0xFFFF;
 	cnt.hashmiss += !(flags & GCL_F_RSS_HASH); /* rx.c:160-163 */
+	if (DRAIN)
+		dense_drain();
 	const int p = ipt_lookup(tb.ipt, k.ipt_mask, k.ipt_seed, daddr); /* rx.c:197 */
 	const bool miss = p < 0;
 	cnt.unreg += miss;     /* rx.c:205 */
@@ -605,25 +610,14 @@ __device__ __forceinline__ void put_verdict(const KParams &k, uint64_t idx, uint
 		store_wt((uint64_t *)k.verdicts + idx, w);
 }
 
-template <int NT, bool WL>
+template <int NT>
 __device__ __forceinline__ void stage_tile(uint4 *tile, const uint4 r[4])
 {
 #pragma unroll
 	for (int j = 0; j < 4; j++) {
-		const uint32_t c = tile_chunk<NT, WL>(j);
+		const uint32_t c = tile_chunk<NT>(j);
 		tile[tile_slot(c >> 2, c & 3)] = r[j];
 	}
-}
-
-/* Order a wave's own LDS accesses around a wave-staged tile (the rocPRIM
- * wave barrier): a wave's LDS operations execute in order, so its lanes see
- * each other's stores without s_barrier; this only keeps the compiler from
- * moving the tile's reads above its stores, or the next stores above them. */
-__device__ __forceinline__ void wave_lds_barrier()
-{
-	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-	__builtin_amdgcn_wave_barrier();
-	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 /* classify_kernel's MODE for gcl_access_probe: the same launch -- tiles,
@@ -675,7 +669,7 @@ constexpr int kDefaultPairLean = 1;
 /* gcl_tune.defer default (Geometry::defer): udp64 328.2-329.1 -> 323.4-324.2
  * us, three fresh processes (profiles/r05_defer_ab.jsonl) */
 constexpr int kDefaultDefer = 1;
-/* gcl_tune.stage default: 0 block-staged tiles, 1 wave-staged */
-constexpr int kDefaultStage = 0;
+/* gcl_tune.tile_lean default: classify_kernel's plain-IPv4 waves on classify_lean */
+constexpr int kDefaultTileLean = 1;
 
 } // namespace gclk

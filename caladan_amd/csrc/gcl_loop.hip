@@ -1341,6 +1341,13 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 	lp.where = (uint32_t *)d + 8;
 	lp.exited = (uint32_t *)d + 1;
 	lp.polls = (uint32_t *)d + kLoopCtlPolls;
+	/* the caller's counts / stats are typically zeroed on the default stream
+	 * just before (a hipMemsetAsync, torch.zeros): the loop runs on a
+	 * non-blocking stream of its own, so that work is waited for here, or the
+	 * first bursts' counts could land before the zeroing (the loop's rx_burst
+	 * counters read short) */
+	if (hipStreamSynchronize(nullptr) != hipSuccess)
+		goto fail;
 	if (hipStreamCreateWithFlags(&L->st, hipStreamNonBlocking) != hipSuccess)
 		goto fail;
 	{
@@ -1393,7 +1400,20 @@ static void loop_write_records(gcl_rxloop *L, uint64_t t, uint8_t *dst, uint32_t
 		u32x4_h v0, v1;
 		if (o < L->region_len && L->region_len - o >= 44) {
 			memcpy(&v0, L->region + o + 12, 16);
-			memcpy(&v1, L->region + o + 28, 16);
+			uint32_t w[4];
+			memcpy(w, L->region + o + 28, 12);
+			/* d10 (bytes 40-43) is read for ARP's target IP (rx.c:165-167)
+			 * and the ports behind IPv4 options; a plain IPv4 header (IHL 5,
+			 * the kernels' own test) never reads it, so neither does the
+			 * core: in the reference's pool (data at element + 344,
+			 * defs.h:503-506) byte 40 starts the next cache line, a second
+			 * DRAM miss per packet once the NIC has written the frame */
+			w[3] = (v0[0] & 0x000FFFFFu) == 0x00050008u ? 0u : ({
+				uint32_t d;
+				memcpy(&d, L->region + o + 40, 4);
+				d;
+			});
+			memcpy(&v1, w, 16);
 		} else {
 			uint8_t b[32] = {0};
 			if (o < L->region_len && L->region_len - o > 12)

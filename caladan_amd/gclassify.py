@@ -138,8 +138,8 @@ class GclTune(ctypes.Structure):
     (GCL_TUNE_AUTO = -1 everywhere: the library's own choice)."""
     _fields_ = [("size", ctypes.c_uint32), ("tables", ctypes.c_int32), ("depth", ctypes.c_int32),
                 ("threads", ctypes.c_int32), ("grid", ctypes.c_int32), ("blocks_per_cu", ctypes.c_int32),
-                ("defer", ctypes.c_int32), ("pair_lean", ctypes.c_int32), ("stage", ctypes.c_int32),
-                ("loop64", ctypes.c_int32),
+                ("defer", ctypes.c_int32), ("pair_lean", ctypes.c_int32),
+                ("tile_lean", ctypes.c_int32), ("loop64", ctypes.c_int32),
                 ("loop_lean", ctypes.c_int32), ("loop_spec", ctypes.c_int32),
                 ("loop_phase_max", ctypes.c_int32), ("loop_phase_up", ctypes.c_int32),
                 ("loop_phase_down", ctypes.c_int32), ("loop_prefetch", ctypes.c_int32),

@@ -433,8 +433,7 @@ struct gcl_tune {
 	                            registers and written after the reads where that takes
 	                            <= 2 writes per block (default), 2 always */
 	int32_t pair_lean;       /* classify_pair_kernel: plain-IPv4 waves on the lean path (1) */
-	int32_t stage;           /* classify_kernel tiles: 0 staged by the block (a barrier per
-	                            tile), 1 by each wave for its own 64 packets (no barrier) */
+	int32_t tile_lean;       /* classify_kernel: plain-IPv4 waves on the lean path (1) */
 	/* the persistent loop */
 	int32_t loop64;          /* 0: bursts <= 64 through the general loop kernel */
 	int32_t loop_lean;       /* plain-IPv4 bursts on the lean path (1) */
@@ -632,8 +631,11 @@ struct gcl_rxloop_cfg {
 	uint32_t lifetime_ms;  /* kernel lifetime bound: 1..600000 */
 	const void *region;    /* registered host region holding the frames */
 	uint64_t region_len;
-	uint64_t *counts;      /* device u64[max_runtimes] (optional), accumulated */
-	uint64_t *stats;       /* device u64[GCL_NR_STATS] (optional), accumulated */
+	uint64_t *counts;      /* device u64[max_runtimes] (optional), accumulated; the loop
+	                          runs on a stream of its own: gcl_rxloop_start waits for the
+	                          default stream's work (e.g. their zeroing), work on other
+	                          streams must be complete before the call */
+	uint64_t *stats;       /* device u64[GCL_NR_STATS] (optional), accumulated, as counts */
 	uint32_t flags;        /* GCL_LOOP_INLINE_HDRS or GCL_LOOP_HDR_RECORDS */
 	uint32_t pad;
 };

@@ -814,6 +814,35 @@ void orc_classify_lrpc(const struct orc_tables *t, const struct gcl_batch *b,
 	lrpc_set_free(&rs, t);
 }
 
+struct orc_dataplane {
+	const struct orc_tables *t;
+	struct lrpc_set rs;
+};
+
+struct orc_dataplane *orc_dataplane_new(const struct orc_tables *t)
+{
+	struct orc_dataplane *d = calloc(1, sizeof(*d));
+	if (!d)
+		return NULL;
+	d->t = t;
+	lrpc_set_init(&d->rs, t);
+	return d;
+}
+
+void orc_dataplane_free(struct orc_dataplane *d)
+{
+	if (!d)
+		return;
+	lrpc_set_free(&d->rs, d->t);
+	free(d);
+}
+
+void orc_dataplane_burst(struct orc_dataplane *d, const struct gcl_batch *b, struct gcl_verdict *v,
+                         uint64_t *counts, uint64_t *stats, int send)
+{
+	classify_range_lrpc(d->t, b, 0, b->n, v, counts, stats, &d->rs, 1, send ? 2 : 0);
+}
+
 /* ------------------------------------------------------------------------
  * CPU baseline timer.
  */

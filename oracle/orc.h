@@ -115,6 +115,17 @@ double orc_bench_ex(const struct orc_tables *t, const struct gcl_batch *b,
 double orc_bench_pinned(const struct orc_tables *t, const struct gcl_batch *b,
                         int threads, int passes, unsigned int flags, const int *cpus);
 
+/* A CPU dataplane for the pipeline baseline (tools/cpupipe): the lrpc rings
+ * of orc_classify_lrpc kept across bursts, so one rx_burst at a time --
+ * rx_one_pkt with rx.c's direct header loads and prefetch stride 2, plus
+ * (@send) rx_make_cmd + lrpc_send of every delivered packet -- runs as the
+ * reference's dataplane loop does (rx.c:270-290). */
+struct orc_dataplane;
+struct orc_dataplane *orc_dataplane_new(const struct orc_tables *t);
+void orc_dataplane_free(struct orc_dataplane *d);
+void orc_dataplane_burst(struct orc_dataplane *d, const struct gcl_batch *b, struct gcl_verdict *v,
+                         uint64_t *counts, uint64_t *stats, int send);
+
 /* orc_classify through the CPU-baseline form (direct header loads, same
  * preconditions as ORC_BENCH_DIRECT; dst_hint is ignored). */
 void orc_classify_direct(const struct orc_tables *t, const struct gcl_batch *b,

@@ -304,10 +304,10 @@ def test_gpu_dense_verdict1(g, orc, wl, R, T):
 DEFER_FORMS = {0: "per-packet stores", 1: "deferred (<= 2 writes per block, the default)", 2: "deferred always"}
 
 
-@pytest.mark.parametrize("stage", [0, 1])
+@pytest.mark.parametrize("lean", [1, 0])
 @pytest.mark.parametrize("defer", sorted(DEFER_FORMS))
 @pytest.mark.parametrize("wl,R,T,vb", [(0, 16, 8, 1), (0, 16, 8, 2), (1, 1024, 4, 2)])
-def test_gpu_dense_narrow_verdicts(g, orc, wl, R, T, vb, defer, stage):
+def test_gpu_dense_narrow_verdicts(g, orc, wl, R, T, vb, defer, lean):
     """Dense slots' 1- and 2-B verdicts in every form (gcl_tune.defer): the
     tile kernel's write-through byte and short stores per packet, or kept in
     LDS and written 16 B per lane in batches; the partial last tile
@@ -322,7 +322,7 @@ def test_gpu_dense_narrow_verdicts(g, orc, wl, R, T, vb, defer, stage):
     del df
     tb = 3 if vb == 1 else 4
     clf = g.Classifier(0, R, g.HASH_JENKINS, g.CFG_VERDICT1 if vb == 1 else g.CFG_VERDICT2, thread_bits=tb,
-                       tune={"defer": defer, "stage": stage})
+                       tune={"defer": defer, "tile_lean": lean})
     t = orc.Tables(R, g.HASH_JENKINS, 0, g.F_RSS_HASH | g.F_IP_CKSUM_GOOD)
     for r in range(R):
         act = r % T
@@ -332,7 +332,7 @@ def test_gpu_dense_narrow_verdicts(g, orc, wl, R, T, vb, defer, stage):
     v, c, st = gpu_run(g, clf, frames, n, stride)
     ve, ce, se = t.classify(frames, n, stride)
     w = to_verdict1(ve, [T] * R, tb) if vb == 1 else to_verdict2(ve, [T] * R, tb)
-    assert_same(v, w, f"narrow verdicts wl={wl} vb={vb} {DEFER_FORMS[defer]} stage={stage}")
+    assert_same(v, w, f"narrow verdicts wl={wl} vb={vb} {DEFER_FORMS[defer]} lean={lean}")
     assert (c == ce).all() and (st == se).all()
 
 
@@ -343,10 +343,9 @@ def test_gpu_dense_narrow_verdicts(g, orc, wl, R, T, vb, defer, stage):
     (1, {"grid": 20}), (1, {"grid": 40}), (1, {"grid": 70}),
     (1, {"grid": 20, "depth": 1}), (1, {"threads": 512, "grid": 12}),
     (1, {"tables": 1, "grid": 40}), (2, {"tables": 1, "grid": 9}),
-    # wave-staged tiles: the block meets only around the buffer's writes
-    (1, {"stage": 1}), (2, {"stage": 1, "grid": 3}), (1, {"stage": 1, "grid": 20}),
-    (2, {"stage": 1, "threads": 512, "grid": 7}), (1, {"stage": 1, "threads": 1024, "grid": 7}),
-    (2, {"stage": 1, "grid": 5, "depth": 1}), (1, {"stage": 1, "tables": 1, "grid": 40})])
+    # every wave on classify_core (the lean waves off)
+    (1, {"tile_lean": 0}), (2, {"tile_lean": 0, "grid": 3}), (1, {"tile_lean": 0, "grid": 20}),
+    (2, {"tile_lean": 0, "threads": 512, "grid": 7}), (1, {"tile_lean": 0, "grid": 5, "depth": 1})])
 @pytest.mark.parametrize("vb", [1, 2])
 def test_gpu_dense_deferred_flushes(g, orc, vb, defer, env):
     """The tile kernel's LDS verdict buffer when a block walks more tiles
@@ -906,6 +905,53 @@ def test_gpu_ingress_pool_geometry(g, orc):
     assert (counts == ce).all() and (stats == se).all()
 
 
+@pytest.mark.parametrize("tile_lean", [1, 0])
+@pytest.mark.parametrize("mode,vb", [(0, 1), (0, 8), (1, 1), (1, 2), (1, 4), (2, 8), (2, 1)])
+def test_gpu_tile_lean_waves(g, orc, mode, vb, tile_lean):
+    """classify_kernel's lean path (gcl_tune.tile_lean, on by default): dense
+    64-B slots where a wave whose 64 packets are all plain IPv4 (IHL 5) takes
+    classify_lean and every other wave -- one IPv6, ARP, IHL-6 or fragmented
+    frame in it, every 23rd wave -- classify_core; misses, zero-active
+    runtimes (WAKE), non-TCP/UDP and the NIC's hash.rss array in NIC mode;
+    every hash mode and verdict width, both settings, a ragged last tile;
+    bit-exact against the oracle with counts and counters."""
+    rng = np.random.default_rng(1700 + 10 * mode + vb)
+    R, T, n, stride = 16, 8, 200_000 + 37, 64
+    frames, _, rss = orc.generate(0, n, stride, R, seed=41)
+    fr = frames.reshape(n, stride)
+    odd = np.arange(0, n, 64 * 23) + rng.integers(0, 64, size=len(range(0, n, 64 * 23)))
+    odd = odd[odd < n]
+    for j, i in enumerate(odd):
+        kind = j % 5
+        if kind == 0:
+            fr[i, 12:14] = (0x86, 0xDD)  # IPv6: dropped
+        elif kind == 1:
+            fr[i, 12:14] = (0x08, 0x06)  # ARP: looked up by bytes 38-41
+        elif kind == 2:
+            fr[i, 14] = 0x46  # IHL 6: ports at 38
+        elif kind == 3:
+            fr[i, 20] |= 0x20  # MF: a fragment, hash 0
+        else:
+            fr[i, 30:34] = (192, 168, 7, 7)  # unregistered
+    fr[::97, 23] = 1  # ICMP: hash 0
+    tb = g.thread_bits_for(R, T) if vb <= 2 else 0
+    cflags = {8: 0, 4: g.CFG_VERDICT4, 2: g.CFG_VERDICT2, 1: g.CFG_VERDICT1}[vb]
+    t = orc.Tables(R, mode, 0, 0x09, g.CALADAN_RSS_KEY)
+    clf = g.Classifier(0, R, mode, cflags, 0x09, g.CALADAN_RSS_KEY, thread_bits=tb, tune={"tile_lean": tile_lean})
+    for r in range(R):
+        act = (r * 5) % (T + 1)
+        fl = orc.steer_flows(T, list(range(act))) if act else None
+        t.runtime_set(r, orc.runtime_ip(r), T, act, fl)
+        clf.runtime_set(r, g.runtime_ip(r), T, act, fl)
+    kw = {"rss": rss} if mode == 0 else {}
+    ve, ce, se = t.classify(frames, n, stride, **kw)
+    v, c, st = gpu_run(g, clf, frames, n, stride, **kw)
+    want = {8: lambda: ve, 4: lambda: to_verdict4(ve), 2: lambda: to_verdict2(ve, [T] * R, tb),
+            1: lambda: to_verdict1(ve, [T] * R, tb)}[vb]()
+    assert_same(v, want, f"tile lean={tile_lean} mode={mode} vb={vb}")
+    assert (c == ce).all() and (st == se).all()
+
+
 @pytest.mark.parametrize("pair_lean", [1, 0])
 @pytest.mark.parametrize("mode,vb", [(0, 2), (0, 1), (1, 8), (1, 2), (2, 4), (2, 1)])
 def test_gpu_pair_lean_waves(g, orc, mode, vb, pair_lean):
@@ -1152,9 +1198,8 @@ LOOP_GEOMETRIES = [
     {"threads": 1024, "grid": 7},
     {"threads": 512, "grid": 5},
     {"blocks_per_cu": 1},
-    {"stage": 1, "grid": 16},
-    {"stage": 1, "depth": 1, "grid": 5},
-    {"stage": 1, "threads": 1024, "grid": 7},
+    {"tile_lean": 0, "grid": 16},
+    {"tile_lean": 0, "depth": 1, "grid": 5},
 ]
 
 
@@ -1489,10 +1534,9 @@ def test_gpu_access_probe(g, vbytes):
     assert (got == want(offs)).all()
 
 
-@pytest.mark.parametrize("vb,R,T,stride,tune", [(1, 16, 8, 64, {}), (1, 16, 8, 64, {"stage": 1}),
-                                                (2, 16, 8, 64, {"defer": 2, "grid": 7}),
+@pytest.mark.parametrize("vb,R,T,stride,tune", [(1, 16, 8, 64, {}), (2, 16, 8, 64, {"defer": 2, "grid": 7}),
                                                 (2, 1024, 4, 1536, {}), (8, 16, 8, 64, {}),
-                                                (1, 16, 8, 64, {"defer": 0, "stage": 1, "depth": 1})])
+                                                (1, 16, 8, 64, {"defer": 0, "depth": 1})])
 def test_gpu_access_probe_kernel_shape(g, vb, R, T, stride, tune):
     """gcl_access_probe on a dense batch at the context's verdict width is the
     classify launch itself with rx_one_pkt folded away (the kernel's own

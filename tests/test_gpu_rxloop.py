@@ -99,6 +99,10 @@ def test_rxloop_fuzz_vs_oracle(g, orc, mode, vb, flags, inline, k64):
     g.host_register(frames)
     cnt = torch.zeros(max_rt, dtype=torch.int64, device="cuda")
     st = torch.zeros(g.NR_STATS, dtype=torch.int64, device="cuda")
+    # the zero fills run on torch's stream, the loop on a stream of its own:
+    # done before the loop adds to them (gcl_rxloop_start also orders the
+    # default stream's work first)
+    torch.cuda.synchronize()
     # header records, and the offsets of the NIC-mode cases, taken with the
     # poll (see the ragged-burst test); the other cases read after the word
     early = inline == 2 or (inline == 0 and mode == 0)
@@ -186,6 +190,10 @@ def test_rxloop_lean_path(g, orc, mode, vb, flags, lflag):
     g.host_register(frames)
     cnt = torch.zeros(max_rt, dtype=torch.int64, device="cuda")
     st = torch.zeros(g.NR_STATS, dtype=torch.int64, device="cuda")
+    # the zero fills run on torch's stream, the loop on a stream of its own:
+    # done before the loop adds to them (gcl_rxloop_start also orders the
+    # default stream's work first)
+    torch.cuda.synchronize()
     clf.tune(loop_spec=SPEC_WIDE)
     loop = clf.rxloop(frames, slots=8, counts=cnt, stats=st, flags=LOOP_FLAGS[lflag](g))
     try:

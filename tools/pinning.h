@@ -14,6 +14,10 @@
 #include <string.h>
 #include <time.h>
 
+#include <unistd.h>
+
+#include <algorithm>
+#include <utility>
 #include <vector>
 
 /* Idle jiffies of every CPU from /proc/stat (index = CPU), empty on error. */
@@ -132,3 +136,40 @@ static inline int pin_near_gpu(int dev)
 	return sched_setaffinity(0, sizeof(one), &one) ? -1 : pick;
 }
 
+
+/* @k CPUs of our affinity mask for helper threads (the NIC emulation): the
+ * idlest physical cores over 100 ms, one CPU per core, none sharing a core
+ * with @busy (the dataplane's CPU, or -1); fewer when the mask has fewer. */
+static inline std::vector<int> pick_other_cpus(uint32_t k, int busy)
+{
+	std::vector<int> out;
+	cpu_set_t allowed;
+	CPU_ZERO(&allowed);
+	for (int c = 0; c < CPU_SETSIZE; c++) /* the process mask, not this (pinned) thread's */
+		CPU_SET(c, &allowed);
+	if (sched_getaffinity(getpid(), sizeof(allowed), &allowed))
+		return out;
+	std::vector<int> skip = busy >= 0 ? siblings(busy) : std::vector<int>();
+	const std::vector<uint64_t> a = cpu_idle();
+	struct timespec ts = {0, 100 * 1000 * 1000};
+	nanosleep(&ts, nullptr);
+	const std::vector<uint64_t> b = cpu_idle();
+	std::vector<std::pair<int64_t, int>> cand;
+	std::vector<char> seen(CPU_SETSIZE, 0);
+	for (int cpu = 0; cpu < CPU_SETSIZE; cpu++) {
+		if (!CPU_ISSET(cpu, &allowed) || seen[cpu] || std::find(skip.begin(), skip.end(), cpu) != skip.end())
+			continue;
+		int64_t score = 0;
+		for (int sib : siblings(cpu)) {
+			if (sib < CPU_SETSIZE)
+				seen[sib] = 1;
+			if ((size_t)sib < a.size() && a.size() == b.size())
+				score += (int64_t)(b[sib] - a[sib]);
+		}
+		cand.push_back({-score, cpu});
+	}
+	std::sort(cand.begin(), cand.end());
+	for (size_t i = 0; i < cand.size() && out.size() < k; i++)
+		out.push_back(cand[i].second);
+	return out;
+}

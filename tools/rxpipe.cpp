@@ -38,6 +38,7 @@
 
 #include "gcl_host.h"
 #include "gclassify.h"
+#include "nicsim.h"
 #include "pinning.h"
 #include "tune_env.h"
 
@@ -78,7 +79,7 @@ int main(int argc, char **argv)
 	/* RXPIPE_HASH=nic: the flow hash is the mbuf's hash.rss, as rx.c:83 passes
 	 * it (GCL_HASH_NIC, rss[] submitted with the offsets); default: JENKINS, the
 	 * 5-tuple lookup3 computed on the GPU (no NIC in the loop) */
-	const bool nic = getenv("RXPIPE_HASH") && !strcmp(getenv("RXPIPE_HASH"), "nic");
+	const bool nic_hash = getenv("RXPIPE_HASH") && !strcmp(getenv("RXPIPE_HASH"), "nic");
 	/* ingress region: udp64 frames generated on the GPU, copied to pinned host memory */
 	uint8_t *dfr, *region;
 	uint32_t *drss;
@@ -103,12 +104,31 @@ int main(int argc, char **argv)
 
 	struct gcl_cfg cfg = {};
 	cfg.max_runtimes = R;
-	cfg.hash_mode = nic ? GCL_HASH_NIC : GCL_HASH_JENKINS;
+	cfg.hash_mode = nic_hash ? GCL_HASH_NIC : GCL_HASH_JENKINS;
 	cfg.flags = GCL_CFG_VERDICT4;
 	cfg.default_olflags = GCL_F_RSS_HASH | GCL_F_IP_CKSUM_GOOD;
 	struct gcl_ctx *ctx;
 	if (gcl_open(0, &cfg, &ctx) || tune_from_env(ctx))
 		return 1;
+
+	/* RXPIPE_POOL=ingress: the bursts come from the emulated NIC
+	 * (tools/nicsim.h) -- mbufs of the reference's pool geometry (data at
+	 * element + 344 of 9408-B elements), recycled through a mempool, each
+	 * frame freshly written with non-temporal stores so that no CPU cache
+	 * holds its header, as behind a NIC without DDIO -- instead of a static
+	 * 4 MiB region of 64-B slots walked in order (cache-hot headers).
+	 * tools/cpupipe runs the CPU baseline on the same emulation. */
+	const bool ingress = getenv("RXPIPE_POOL") && !strcmp(getenv("RXPIPE_POOL"), "ingress");
+	const uint32_t nic_threads = getenv("RXPIPE_NIC_THREADS") ? (uint32_t)atoi(getenv("RXPIPE_NIC_THREADS")) : 2;
+	const uint32_t pool_mbufs = getenv("RXPIPE_POOL_MBUFS") ? (uint32_t)atoi(getenv("RXPIPE_POOL_MBUFS")) : 8192;
+	nicsim::NicSim nic;
+	if (ingress) {
+		if (!nic.init(pool_mbufs, nic_threads, burst, region, rss.data(), (uint32_t)nframes) ||
+		    gcl_host_register(nic.region, nic.region_len)) {
+			fprintf(stderr, "nicsim init failed\n");
+			return 1;
+		}
+	}
 
 	/* host side of the runtimes: struct proc slices with one lrpc ring per kthread */
 	std::vector<gcl_host_proc> procs(R);
@@ -144,8 +164,8 @@ int main(int argc, char **argv)
 	lc.max_burst = burst;
 	lc.workers = workers;
 	lc.lifetime_ms = 60000;
-	lc.region = region;
-	lc.region_len = nframes * stride;
+	lc.region = ingress ? nic.region : region;
+	lc.region_len = ingress ? nic.region_len : nframes * stride;
 	lc.flags = inline_hdrs ? GCL_LOOP_INLINE_HDRS : hdr_records ? GCL_LOOP_HDR_RECORDS : 0;
 	/* RXPIPE_STAMPS=1: the lone-burst breakdown (depth 1): host submit and
 	 * submit -> records seen on the TSC, the worker's stage times
@@ -168,6 +188,7 @@ int main(int argc, char **argv)
 	for (uint64_t i = 0; i < nframes; i++)
 		offs[i] = i * stride;
 	std::vector<uint16_t> len(burst, 60);
+	std::vector<nicsim::Burst> inflight(ingress ? depth : 0); /* the bursts' descriptors until delivered */
 	std::vector<gcl_verdict4> v(burst);
 	uint64_t stats[GCL_NR_STATS] = {0};
 	std::vector<int64_t> tk(depth);
@@ -214,10 +235,23 @@ int main(int argc, char **argv)
 			while (head < count && head - tail < depth) {
 				const uint32_t b = (uint32_t)((seq + head) % nb);
 				gap_spin();
+				const uint64_t *so = &offs[(size_t)b * burst];
+				const uint32_t *sr = &rss[(size_t)b * burst];
+				if (ingress) { /* rte_eth_rx_burst: the next burst of descriptors */
+					nicsim::Burst &nb_ = nic.pull();
+					nicsim::Burst &f = inflight[head % depth];
+					f.n = nb_.n;
+					f.owner = nb_.owner;
+					memcpy(f.mbuf, nb_.mbuf, 4 * nb_.n);
+					memcpy(f.off, nb_.off, 8 * nb_.n);
+					memcpy(f.rss, nb_.rss, 4 * nb_.n);
+					nic.consumed(nb_);
+					so = f.off;
+					sr = f.rss;
+				}
 				const uint64_t ts = ticks();
 				t_sub[head % depth] = ts;
-				const int64_t r = gcl_rxloop_submit(loop, burst, &offs[(size_t)b * burst], nullptr,
-				                                    nic ? &rss[(size_t)b * burst] : nullptr, nullptr,
+				const int64_t r = gcl_rxloop_submit(loop, burst, so, nullptr, nic_hash ? sr : nullptr, nullptr,
 				                                    nullptr);
 				if (timed && (head & 7) == 0) {
 					t_submit += ticks() - ts;
@@ -233,6 +267,7 @@ int main(int argc, char **argv)
 				head++;
 			}
 			const uint32_t b = (uint32_t)((seq + tail) % nb);
+			const uint64_t *doffs = ingress ? inflight[tail % depth].off : &offs[(size_t)b * burst];
 			const int64_t t = tk[tail % depth];
 			const bool samp = timed && (tail & 7) == 0;
 			const uint64_t tw = samp ? ticks() : 0;
@@ -247,7 +282,7 @@ int main(int argc, char **argv)
 					d0 = ticks();
 				delivered += gcl_host_deliver4(by_id.data(), R, clients.data(), (int)R, v.data(),
 				                               nullptr, len.data(), nullptr, cfg.default_olflags,
-				                               &offs[(size_t)b * burst], burst, nullptr, stats);
+				                               doffs, burst, nullptr, stats);
 				d1 = ticks();
 			} else {
 				const gcl_loop_rec *recs;
@@ -261,9 +296,13 @@ int main(int argc, char **argv)
 					d0 = ticks();
 				delivered += gcl_host_deliver_recs(by_id.data(), R, clients.data(), (int)R, recs, 4, 0,
 				                                   nullptr, len.data(), nullptr, cfg.default_olflags,
-				                                   &offs[(size_t)b * burst], burst, nullptr, stats);
+				                                   doffs, burst, nullptr, stats);
 				d1 = ticks();
 				gcl_rxloop_release(loop, t);
+			}
+			if (ingress) { /* delivered: the mbufs go back to the mempool */
+				const nicsim::Burst &f = inflight[tail % depth];
+				nic.recycle(f.owner, f.mbuf, f.n);
 			}
 			if (samp) {
 				t_deliver += d1 - d0;
@@ -293,15 +332,23 @@ int main(int argc, char **argv)
 	};
 	/* pinned after the runtime's own threads exist (they keep their masks) */
 	const int cpu = pin_near_gpu(0);
+	if (ingress)
+		nic.launch(pick_other_cpus(nic_threads, cpu));
 	const uint32_t warm = 200;
 	pump(warm, false);
+	const uint64_t nic_w0 = nic.wait_ns;
 	const uint64_t t0 = now_ns(), k0 = ticks();
 	pump(nbursts, true);
 	const uint64_t el = now_ns() - t0;
+	const uint64_t nic_waited = nic.wait_ns - nic_w0;
 	const double ns_tick = (double)el / (double)(ticks() - k0);
 	uint64_t ps[3] = {0, 0, 0};
 	gcl_rxloop_poll_stats(loop, ps);
 	gcl_rxloop_stop(loop);
+	if (ingress) {
+		gcl_host_unregister(nic.region);
+		nic.shutdown();
+	}
 	std::sort(lat.begin(), lat.end());
 	const double pkts = (double)burst * nbursts;
 	const double sub_pkts = (double)burst * (n_sub ? n_sub : 1), tail_pkts = (double)burst * (n_tail ? n_tail : 1);
@@ -311,8 +358,9 @@ int main(int argc, char **argv)
 	       "\"burst_latency_p50_us\": %.2f, \"burst_latency_p99_us\": %.2f, "
 	       "\"deliver_ns_per_pkt\": %.2f, \"submit_ns_per_pkt\": %.2f, \"wait_ns_per_pkt\": %.2f, "
 	       "\"delivered_check\": \"%s\", \"unicast_fail\": %llu, \"host_cpu\": %d, "
-	       "\"bursts_early\": %llu, \"bursts_stale\": %llu, \"bursts_late\": %llu}\n",
-	       burst, workers, depth, nbursts, nic ? "nic (hash.rss, rx.c:83)" : "jenkins",
+	       "\"bursts_early\": %llu, \"bursts_stale\": %llu, \"bursts_late\": %llu, \"pool\": \"%s\", "
+	       "\"nic_wait_frac\": %.4f}\n",
+	       burst, workers, depth, nbursts, nic_hash ? "nic (hash.rss, rx.c:83)" : "jenkins",
 	       gap_rand ? (gap_span == 2000 ? "rand [0, 2000)" : gap_env) : gap_env ? gap_env : "0",
 	       copy_out ? "copied out" : inline_hdrs ? "read in place, headers inlined in the slot"
 	       : hdr_records ? "read in place, stamped header records in the slot" : "read in place",
@@ -321,7 +369,11 @@ int main(int argc, char **argv)
 	       t_submit * ns_tick / sub_pkts, t_wait * ns_tick / tail_pkts,
 	       delivered == (uint64_t)burst * (nbursts + warm) ? "ok" : "MISMATCH",
 	       (unsigned long long)stats[GCL_RX_UNICAST_FAIL], cpu, (unsigned long long)ps[0],
-	       (unsigned long long)ps[1], (unsigned long long)ps[2]);
+	       (unsigned long long)ps[1], (unsigned long long)ps[2],
+	       ingress ? "ingress: mbuf pool at element + 344 of 9408-B elements, frames written by NIC threads "
+	                 "with non-temporal stores (cold headers)"
+	               : "static 64-B slots walked in order (cache-hot headers)",
+	       (double)nic_waited / el);
 	if (stamps) {
 		/* medians; the submit -> seen split only on the sampled bursts */
 		auto med = [](std::vector<uint64_t> v, bool drop0) {

@@ -1,14 +1,15 @@
-"""A/B of the dense tile kernel's staging on the bench's own placed buffers,
-in one process: tiles staged by the whole block with a barrier per tile
-(gcl_tune.stage = 0, the round-5 kernel) against each wave staging and
-classifying its own 64 packets (stage = 1, no barrier per tile), each beside
-its own ceiling -- gcl_access_probe in the kernel's shape (the same launch
-with rx_one_pkt folded away) -- and the layout's minimal-request probe.
-Contexts over the same frames and verdict ring, launches interleaved round
-by round; every form's verdicts and counts are checked against form 0's.
+"""A/B of one gcl_tune knob of the dense tile kernel on the bench's own
+placed buffers, in one process: AB_KNOB (default tile_lean, the lean waves)
+at each of AB_VALUES (default "0,1"), each beside its own ceiling --
+gcl_access_probe in the kernel's shape (the same launch with rx_one_pkt
+folded away) -- and the layout's minimal-request probe.  Contexts over the
+same frames and verdict ring, launches interleaved round by round; every
+form's verdicts and counts are checked against the first form's.  (Round 6's
+first use, AB_KNOB=stage: block- against wave-staged tiles,
+profiles/r06_stage_ab.jsonl; the wave form lost and was removed.)
 
-    python tools/stage_ab.py [workload ...]     (default: udp64 tcp1500)
-One JSON line per (workload, round, form).
+    python tools/tile_ab.py [workload ...]     (default: udp64 tcp1500)
+One JSON line per (workload, round).
 """
 import json
 import os
@@ -21,7 +22,8 @@ import torch  # noqa: E402
 
 import bench  # noqa: E402
 
-FORMS = {0: "block-staged tiles (barrier per tile)", 1: "wave-staged tiles"}
+KNOB = os.environ.get("AB_KNOB", "tile_lean")
+FORMS = [int(x) for x in os.environ.get("AB_VALUES", "0,1").split(",")]
 
 
 def main():
@@ -33,7 +35,7 @@ def main():
         clfs = {}
         for f in FORMS:
             clfs[f] = bench.classifier(dev, w.R, w.T, w.vbytes)
-            clfs[f].tune(stage=f)
+            clfs[f].tune(**{KNOB: f})
             bench.setup_tables(clfs[f], w.R, w.T)
         st = torch.cuda.current_stream().cuda_stream
         ref = None
@@ -48,7 +50,7 @@ def main():
             if ref is None:
                 ref = got
             ok = bool(torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1]))
-            print(json.dumps({"workload": name, "form": f, "check": "ok" if ok else "MISMATCH"}), flush=True)
+            print(json.dumps({"workload": name, KNOB: f, "check": "ok" if ok else "MISMATCH"}), flush=True)
         out = torch.zeros(w.n * w.vbytes, dtype=torch.uint8, device=dev)
         alg = w.n * w.bytes_per_pkt
         for rnd in range(int(os.environ.get("AB_ROUNDS", "3"))):
@@ -64,10 +66,10 @@ def main():
                     clf.access_probe(w.frames, w.n, w.stride, out=out, stream=st)
                 _, ms = bench.timed_launches(go, reps)
                 _, pms = bench.timed_launches(probe, reps)
-                row[f"stage{f}"] = {"kernel_us": round(ms * 1e3, 2), "frac": round(alg / (ms * 1e-3) / 8e12, 4),
+                row[f"{KNOB}={f}"] = {"kernel_us": round(ms * 1e3, 2), "frac": round(alg / (ms * 1e-3) / 8e12, 4),
                                     "probe_us": round(pms * 1e3, 2), "kernel_over_probe": round(ms / pms, 4)}
             _, mms = bench.timed_launches(
-                lambda: clfs[0].access_probe(w.frames, w.n, w.stride, out=out, stream=st, minimal=True), reps)
+                lambda: clfs[FORMS[0]].access_probe(w.frames, w.n, w.stride, out=out, stream=st, minimal=True), reps)
             row["minimal_probe_us"] = round(mms * 1e3, 2)
             print(json.dumps(row), flush=True)
         del w, clfs, out
