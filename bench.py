@@ -1123,8 +1123,8 @@ def ingress_pipeline_bench(reps=3):
     exe = os.path.join(ROOT, "tools", "rxpipe")
     cpu_exe = cpupipe_exe()
     env = {**os.environ, "RXPIPE_POOL": "ingress", "RXPIPE_HASH": "nic"}
-    out = {"inputs": ("NIC-emulated ingress pool: 8192 mbufs at element + 344 of 9408-B elements, frames "
-                      "written by 2 NIC threads with non-temporal stores (cold headers), mempool recycling; "
+    out = {"inputs": ("NIC-emulated ingress pool: 16384 mbufs at element + 344 of 9408-B elements, frames "
+                      "written by 4 NIC threads with non-temporal stores (cold headers), mempool recycling; "
                       "NIC hash.rss"), "reps_per_row": reps, "gpu": [], "cpu": []}
     if os.access(exe, os.X_OK):
         for cfg in (("64", "1", "1", "20000", "records"), ("64", "4", "8", "20000", "records"),

@@ -12,7 +12,7 @@
 //   cpupipe <bursts> [classify|lrpc]   -> one JSON line
 //
 // RXPIPE_HASH=nic: NIC mode (hash.rss from the descriptor, rx.c:83); default
-// JENKINS.  RXPIPE_NIC_THREADS (2), RXPIPE_POOL_MBUFS (8192) as in rxpipe.
+// JENKINS.  RXPIPE_NIC_THREADS (4), RXPIPE_POOL_MBUFS (16384) as in rxpipe.
 // Build: hipcc --offload-arch=gfx950 -O3 -march=native -Iinclude -o tools/cpupipe
 //        tools/cpupipe.cpp oracle/orc.c (bench.py builds it on the box, like
 //        the native oracle of cpu_baseline)
@@ -33,8 +33,8 @@ int main(int argc, char **argv)
 	const bool send = !(argc > 2 && !strcmp(argv[2], "classify"));
 	const uint32_t burst = 64, R = 16, T = 8;
 	const bool nic_hash = getenv("RXPIPE_HASH") && !strcmp(getenv("RXPIPE_HASH"), "nic");
-	const uint32_t nthreads = getenv("RXPIPE_NIC_THREADS") ? (uint32_t)atoi(getenv("RXPIPE_NIC_THREADS")) : 2;
-	const uint32_t nmbufs = getenv("RXPIPE_POOL_MBUFS") ? (uint32_t)atoi(getenv("RXPIPE_POOL_MBUFS")) : 8192;
+	const uint32_t nthreads = getenv("RXPIPE_NIC_THREADS") ? (uint32_t)atoi(getenv("RXPIPE_NIC_THREADS")) : 4;
+	const uint32_t nmbufs = getenv("RXPIPE_POOL_MBUFS") ? (uint32_t)atoi(getenv("RXPIPE_POOL_MBUFS")) : 16384;
 
 	/* the template stream: the udp64 frames rxpipe generates on the GPU, the
 	 * same bytes (orc_generate = gcl_generate), with the NIC's hash.rss */

@@ -85,17 +85,37 @@ struct Spsc {
 	bool empty() const { return head.load(std::memory_order_acquire) == tail.load(std::memory_order_relaxed); }
 	T &front() { return buf[tail.load(std::memory_order_relaxed) & mask]; }
 	void pop_commit() { tail.store(tail.load(std::memory_order_relaxed) + 1, std::memory_order_release); }
+	/* @n elements at once, one index update (the caller checked size() / room) */
+	void push_n(const T *v, uint32_t n)
+	{
+		const uint32_t h = head.load(std::memory_order_relaxed);
+		for (uint32_t i = 0; i < n; i++)
+			buf[(h + i) & mask] = v[i];
+		head.store(h + n, std::memory_order_release);
+	}
+	void pop_n(T *v, uint32_t n)
+	{
+		const uint32_t t = tail.load(std::memory_order_relaxed);
+		for (uint32_t i = 0; i < n; i++)
+			v[i] = buf[(t + i) & mask];
+		tail.store(t + n, std::memory_order_release);
+	}
 };
 
-/* a 64-B frame written with non-temporal 8-B stores (frame data is 8-B
- * aligned at element + 344), as DMA leaves it: in DRAM, in no CPU cache */
-inline void nt_write64(uint8_t *dst, const uint8_t *src)
+/* Frame data sits kDataOff % 64 = 24 B into a cache line (elements are
+ * 64-B multiples in 2 MiB pages), so a 64-B frame spans two lines.  DMA
+ * leaves it in DRAM and in no CPU cache: both lines are written WHOLE with
+ * non-temporal 16-B stores from a pre-built 128-B image (the frame's bytes,
+ * zeros around them: the headroom before element + 344 and the rest of the
+ * second line), since a partly written write-combining line drains as a slow
+ * partial write (8-B stores at element + 344 ran ~130 ns per frame) */
+constexpr uint64_t kLineHead = kDataOff % 64;
+static_assert(kEltSize % 64 == 0 && kPage % 64 == 0, "frame data at a fixed offset in its line");
+
+inline void nt_write_lines(uint8_t *line0, const uint8_t *img128)
 {
-	for (int i = 0; i < 8; i++) {
-		long long v;
-		memcpy(&v, src + 8 * i, 8);
-		_mm_stream_si64((long long *)(dst + 8 * i), v);
-	}
+	for (int i = 0; i < 8; i++)
+		_mm_stream_si128((__m128i *)(line0 + 16 * i), _mm_loadu_si128((const __m128i *)(img128 + 16 * i)));
 }
 
 inline uint64_t mono_ns()
@@ -109,9 +129,10 @@ struct NicSim {
 	uint8_t *region = nullptr;
 	uint64_t region_len = 0;
 	uint32_t nmbufs = 0, nthreads = 0, burst = 0;
-	const uint8_t *tmpl = nullptr;     /* ntmpl frames of 64 B */
 	const uint32_t *tmpl_rss = nullptr;
 	uint32_t ntmpl = 0;
+	std::vector<uint8_t> img;          /* the template frames as 128-B line images */
+	std::vector<uint64_t> offs;        /* mbuf data offsets (mbuf_off) */
 	struct Lane {
 		Spsc<Burst> rx;
 		Spsc<uint32_t> free;
@@ -131,11 +152,17 @@ struct NicSim {
 		nmbufs = nmbufs_;
 		nthreads = nthreads_;
 		burst = burst_;
-		tmpl = tmpl_;
 		tmpl_rss = tmpl_rss_;
 		ntmpl = ntmpl_;
-		if (!nthreads || !burst || burst > kMaxBurst || nmbufs < nthreads * burst * (kRxRingBursts + 4))
+		const uint32_t ring = rx_bursts_per_thread();
+		if (!nthreads || !burst || burst > kMaxBurst || nmbufs < nthreads * burst * (ring + 4))
 			return false;
+		img.assign((size_t)ntmpl * 128 + 64, 0);
+		for (uint32_t f = 0; f < ntmpl; f++)
+			memcpy(&img[(size_t)f * 128 + kLineHead], tmpl_ + (size_t)f * 64, 64);
+		offs.resize(nmbufs);
+		for (uint32_t i = 0; i < nmbufs; i++)
+			offs[i] = mbuf_off(i);
 		region_len = region_bytes(nmbufs);
 		region = (uint8_t *)aligned_alloc(kPage, region_len);
 		if (!region)
@@ -144,7 +171,7 @@ struct NicSim {
 		lanes = std::vector<Lane>(nthreads);
 		for (uint32_t k = 0; k < nthreads; k++) {
 			Lane &L = lanes[k];
-			L.rx.init(kRxRingBursts / nthreads ? kRxRingBursts / nthreads : 1);
+			L.rx.init(ring);
 			L.free.init(nmbufs / nthreads + 1);
 			for (uint32_t i = k; i < nmbufs; i += nthreads) { /* this thread's share of the pool */
 				L.free.slot_at_head() = i;
@@ -155,9 +182,24 @@ struct NicSim {
 		return true;
 	}
 
-	/* the NIC threads, thread i pinned to @cpus[i] (absent or -1: not pinned) */
+	uint32_t rx_bursts_per_thread() const
+	{
+		return kRxRingBursts / nthreads >= 4 ? kRxRingBursts / nthreads : 4;
+	}
+
+	cpu_set_t any_cpus;
+	bool any_cpus_set = false;
+
+	/* the NIC threads, thread i pinned to @cpus[i]; threads past the list run
+	 * on any of @cpus (none: unpinned) */
 	void launch(const std::vector<int> &cpus)
 	{
+		CPU_ZERO(&any_cpus);
+		for (int c : cpus)
+			if (c >= 0) {
+				CPU_SET(c, &any_cpus);
+				any_cpus_set = true;
+			}
 		for (uint32_t k = 0; k < nthreads; k++) {
 			lanes[k].cpu = k < cpus.size() ? cpus[k] : -1;
 			lanes[k].th = std::thread([this, k]() { run(k); });
@@ -181,6 +223,8 @@ struct NicSim {
 			CPU_ZERO(&one);
 			CPU_SET(L.cpu, &one);
 			(void)sched_setaffinity(0, sizeof(one), &one);
+		} else if (any_cpus_set) { /* not the dataplane's core (the mask it inherited) */
+			(void)sched_setaffinity(0, sizeof(any_cpus), &any_cpus);
 		}
 		while (!stop.load(std::memory_order_relaxed)) {
 			if (L.rx.full() || L.free.size() < burst) {
@@ -190,15 +234,13 @@ struct NicSim {
 			Burst &b = L.rx.slot_at_head();
 			b.n = burst;
 			b.owner = k;
+			L.free.pop_n(b.mbuf, burst);
 			for (uint32_t i = 0; i < burst; i++) {
-				const uint32_t id = L.free.front();
-				L.free.pop_commit();
 				const uint64_t f = L.seq % ntmpl;
 				L.seq += nthreads;
-				b.mbuf[i] = id;
-				b.off[i] = mbuf_off(id);
+				b.off[i] = offs[b.mbuf[i]];
 				b.rss[i] = tmpl_rss ? tmpl_rss[f] : 0;
-				nt_write64(region + b.off[i], tmpl + 64 * f);
+				nt_write_lines(region + b.off[i] - kLineHead, &img[f * 128]);
 			}
 			_mm_sfence(); /* the frames are in memory before the descriptors say so */
 			L.rx.push_commit();
@@ -227,11 +269,7 @@ struct NicSim {
 	/* mbufs delivered: back to their NIC thread's free list (the mempool) */
 	void recycle(uint32_t owner, const uint32_t *mbuf, uint32_t n)
 	{
-		Spsc<uint32_t> &F = lanes[owner].free;
-		for (uint32_t i = 0; i < n; i++) {
-			F.slot_at_head() = mbuf[i];
-			F.push_commit();
-		}
+		lanes[owner].free.push_n(mbuf, n);
 	}
 
 	void shutdown()

@@ -20,6 +20,11 @@
 #include <utility>
 #include <vector>
 
+/* the process's affinity mask before pin_near_gpu narrowed this thread's
+ * (threads created later inherit the narrowed one) */
+static cpu_set_t g_allowed;
+static bool g_allowed_set = false;
+
 /* Idle jiffies of every CPU from /proc/stat (index = CPU), empty on error. */
 static inline std::vector<uint64_t> cpu_idle()
 {
@@ -85,6 +90,10 @@ static inline int pin_near_gpu(int dev)
 	cpu_set_t allowed;
 	if (sched_getaffinity(0, sizeof(allowed), &allowed))
 		return -1;
+	if (!g_allowed_set) {
+		g_allowed = allowed;
+		g_allowed_set = true;
+	}
 	std::vector<int> cand;
 	char bus[64] = {0}, path[160];
 	if (hipDeviceGetPCIBusId(bus, sizeof(bus), dev) == hipSuccess) {
@@ -144,10 +153,9 @@ static inline std::vector<int> pick_other_cpus(uint32_t k, int busy)
 {
 	std::vector<int> out;
 	cpu_set_t allowed;
-	CPU_ZERO(&allowed);
-	for (int c = 0; c < CPU_SETSIZE; c++) /* the process mask, not this (pinned) thread's */
-		CPU_SET(c, &allowed);
-	if (sched_getaffinity(getpid(), sizeof(allowed), &allowed))
+	if (g_allowed_set) /* the mask before the dataplane thread was pinned */
+		allowed = g_allowed;
+	else if (sched_getaffinity(0, sizeof(allowed), &allowed))
 		return out;
 	std::vector<int> skip = busy >= 0 ? siblings(busy) : std::vector<int>();
 	const std::vector<uint64_t> a = cpu_idle();

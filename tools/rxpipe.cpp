@@ -119,8 +119,8 @@ int main(int argc, char **argv)
 	 * 4 MiB region of 64-B slots walked in order (cache-hot headers).
 	 * tools/cpupipe runs the CPU baseline on the same emulation. */
 	const bool ingress = getenv("RXPIPE_POOL") && !strcmp(getenv("RXPIPE_POOL"), "ingress");
-	const uint32_t nic_threads = getenv("RXPIPE_NIC_THREADS") ? (uint32_t)atoi(getenv("RXPIPE_NIC_THREADS")) : 2;
-	const uint32_t pool_mbufs = getenv("RXPIPE_POOL_MBUFS") ? (uint32_t)atoi(getenv("RXPIPE_POOL_MBUFS")) : 8192;
+	const uint32_t nic_threads = getenv("RXPIPE_NIC_THREADS") ? (uint32_t)atoi(getenv("RXPIPE_NIC_THREADS")) : 4;
+	const uint32_t pool_mbufs = getenv("RXPIPE_POOL_MBUFS") ? (uint32_t)atoi(getenv("RXPIPE_POOL_MBUFS")) : 16384;
 	nicsim::NicSim nic;
 	if (ingress) {
 		if (!nic.init(pool_mbufs, nic_threads, burst, region, rss.data(), (uint32_t)nframes) ||
