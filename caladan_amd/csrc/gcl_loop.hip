@@ -1378,6 +1378,7 @@ fail:
  * header bytes rx_one_pkt reads, prefetching two frames ahead as rx_burst
  * does (rx.c:281-285); bytes past the region read 0. */
 typedef uint32_t u32x4_h __attribute__((vector_size(16), aligned(16)));
+constexpr uint32_t kRecPrefetch = 16; /* header prefetch distance, packets */
 
 static void loop_write_records(gcl_rxloop *L, uint64_t t, uint8_t *dst, uint32_t n,
                                const uint64_t *offs, const uint8_t *olflags, const uint32_t *rss,
@@ -1389,11 +1390,22 @@ static void loop_write_records(gcl_rxloop *L, uint64_t t, uint8_t *dst, uint32_t
 	 * reads a plane, not 64 16-B ones) */
 	const size_t P = L->lp.rec_plane / sizeof(u32x4_h);
 	volatile u32x4_h *q = (volatile u32x4_h *)dst;
-	/* (prefetching 6 ahead, or the record lines for ownership, measured
-	 * the same: profiles/r03_hdr_records_prefetch_ab.jsonl) */
+	/* Headers a NIC has just written miss to DRAM: the core keeps
+	 * kRecPrefetch of them in flight (bytes 12 and 39, the two ends of what
+	 * every packet reads) instead of rx.c's two, which hides one DRAM latency
+	 * per two packets, not per sixteen.  (With cache-hot headers distances
+	 * 2 and 6 measured the same: profiles/r03_hdr_records_prefetch_ab.jsonl.) */
+	auto prefetch_hdr = [&](uint32_t i) {
+		if (offs[i] < L->region_len && L->region_len - offs[i] >= 40) {
+			__builtin_prefetch(L->region + offs[i] + 12, 0, 3);
+			__builtin_prefetch(L->region + offs[i] + 39, 0, 3);
+		}
+	};
+	for (uint32_t i = 0; i < n && i < kRecPrefetch; i++)
+		prefetch_hdr(i);
 	for (uint32_t i = 0; i < n; i++, q++) {
-		if (i + 2 < n && offs[i + 2] < L->region_len)
-			__builtin_prefetch(L->region + offs[i + 2] + 12, 0, 3);
+		if (i + kRecPrefetch < n)
+			prefetch_hdr(i + kRecPrefetch);
 		const uint64_t o = offs[i];
 		/* frame dwords 3-6 and 7-10 (bytes 12-43) in two registers, shuffled
 		 * into the chunks without a trip through memory */

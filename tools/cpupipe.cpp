@@ -99,6 +99,7 @@ int main(int argc, char **argv)
 		one();
 	const uint64_t el = nicsim::mono_ns() - t0;
 	const uint64_t waited = nic.wait_ns - w0;
+	const double huge_frac = (double)nic.huge_bytes() / nic.region_len;
 	nic.shutdown();
 	uint64_t delivered = 0;
 	for (uint32_t r = 0; r < R; r++)
@@ -108,12 +109,12 @@ int main(int argc, char **argv)
 	       "\"pool\": \"ingress: %u mbufs, data at element + 344 of 9408-B elements, frames written by %u NIC "
 	       "threads with non-temporal stores\", "
 	       "\"mpps_one_core\": %.2f, \"ns_per_pkt\": %.2f, \"nic_wait_frac\": %.4f, "
-	       "\"delivered_check\": \"%s\", \"unicast_fail\": %llu, \"host_cpu\": %d}\n",
+	       "\"delivered_check\": \"%s\", \"unicast_fail\": %llu, \"host_cpu\": %d, \"pool_huge_frac\": %.3f}\n",
 	       burst, nbursts, nic_hash ? "nic (hash.rss, rx.c:83)" : "jenkins",
 	       send ? "classify + rx_make_cmd + lrpc_send" : "classify only", nmbufs, nthreads,
 	       pkts / (el * 1e-3), el / pkts, (double)waited / el,
 	       delivered == (uint64_t)pkts && stats[GCL_RX_PULLED] == (uint64_t)pkts ? "ok" : "MISMATCH",
-	       (unsigned long long)stats[GCL_RX_UNICAST_FAIL], cpu);
+	       (unsigned long long)stats[GCL_RX_UNICAST_FAIL], cpu, huge_frac);
 	orc_dataplane_free(d);
 	orc_tables_free(t);
 	return 0;

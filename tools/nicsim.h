@@ -25,7 +25,9 @@
 
 #include <immintrin.h>
 #include <sched.h>
+#include <sys/mman.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
@@ -128,6 +130,7 @@ inline uint64_t mono_ns()
 struct NicSim {
 	uint8_t *region = nullptr;
 	uint64_t region_len = 0;
+	bool huge = false;         /* madvise(MADV_HUGEPAGE) took */
 	uint32_t nmbufs = 0, nthreads = 0, burst = 0;
 	const uint32_t *tmpl_rss = nullptr;
 	uint32_t ntmpl = 0;
@@ -167,6 +170,10 @@ struct NicSim {
 		region = (uint8_t *)aligned_alloc(kPage, region_len);
 		if (!region)
 			return false;
+		/* the pool sits in 2 MiB pages, as the reference's (mempool memory
+		 * from PGSIZE_2MB mappings, defs.h:503-506): one TLB entry per
+		 * 222 mbufs for the dataplane core and the GPU alike */
+		huge = madvise(region, region_len, MADV_HUGEPAGE) == 0;
 		memset(region, 0, region_len);
 		lanes = std::vector<Lane>(nthreads);
 		for (uint32_t k = 0; k < nthreads; k++) {
@@ -180,6 +187,27 @@ struct NicSim {
 			L.seq = k;
 		}
 		return true;
+	}
+
+	/* bytes of the pool region backed by transparent huge pages (smaps) */
+	uint64_t huge_bytes() const
+	{
+		FILE *f = fopen("/proc/self/smaps", "r");
+		if (!f)
+			return 0;
+		char line[512];
+		bool in = false;
+		uint64_t kb = 0;
+		const uintptr_t a = (uintptr_t)region, e = a + region_len;
+		while (fgets(line, sizeof(line), f)) {
+			unsigned long lo, hi;
+			if (sscanf(line, "%lx-%lx ", &lo, &hi) == 2 && strchr(line, '-') < strchr(line, ' '))
+				in = lo < e && hi > a;
+			else if (in && !strncmp(line, "AnonHugePages:", 14))
+				kb += strtoull(line + 14, nullptr, 10);
+		}
+		fclose(f);
+		return kb << 10;
 	}
 
 	uint32_t rx_bursts_per_thread() const

@@ -345,6 +345,7 @@ int main(int argc, char **argv)
 	uint64_t ps[3] = {0, 0, 0};
 	gcl_rxloop_poll_stats(loop, ps);
 	gcl_rxloop_stop(loop);
+	const double huge_frac = ingress && nic.region_len ? (double)nic.huge_bytes() / nic.region_len : 0.0;
 	if (ingress) {
 		gcl_host_unregister(nic.region);
 		nic.shutdown();
@@ -359,7 +360,7 @@ int main(int argc, char **argv)
 	       "\"deliver_ns_per_pkt\": %.2f, \"submit_ns_per_pkt\": %.2f, \"wait_ns_per_pkt\": %.2f, "
 	       "\"delivered_check\": \"%s\", \"unicast_fail\": %llu, \"host_cpu\": %d, "
 	       "\"bursts_early\": %llu, \"bursts_stale\": %llu, \"bursts_late\": %llu, \"pool\": \"%s\", "
-	       "\"nic_wait_frac\": %.4f}\n",
+	       "\"nic_wait_frac\": %.4f, \"pool_huge_frac\": %.3f}\n",
 	       burst, workers, depth, nbursts, nic_hash ? "nic (hash.rss, rx.c:83)" : "jenkins",
 	       gap_rand ? (gap_span == 2000 ? "rand [0, 2000)" : gap_env) : gap_env ? gap_env : "0",
 	       copy_out ? "copied out" : inline_hdrs ? "read in place, headers inlined in the slot"
@@ -373,7 +374,7 @@ int main(int argc, char **argv)
 	       ingress ? "ingress: mbuf pool at element + 344 of 9408-B elements, frames written by NIC threads "
 	                 "with non-temporal stores (cold headers)"
 	               : "static 64-B slots walked in order (cache-hot headers)",
-	       (double)nic_waited / el);
+	       (double)nic_waited / el, huge_frac);
 	if (stamps) {
 		/* medians; the submit -> seen split only on the sampled bursts */
 		auto med = [](std::vector<uint64_t> v, bool drop0) {
