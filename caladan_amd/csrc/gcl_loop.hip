@@ -115,6 +115,10 @@ __host__ __device__ constexpr uint64_t loop_stamp(uint64_t t, uint32_t nslots)
 {
 	return ((((t - 1) >> __builtin_ctz(nslots)) & 0x7FFFFFull) | 0x800000ull) << kLoopStampShift;
 }
+/* gcl_tune.rec_prefetch default: frame headers in flight while the submitting
+ * core writes header records (cold headers behind a NIC: 4 x 8 records
+ * 29 -> 52 Mpkt/s against rx.c's distance 2, profiles/r06_ingress_pipeline.jsonl) */
+constexpr uint32_t kRecPrefetch = 16;
 
 struct LoopImgHdr {        /* first 64 B of a table image buffer */
 	uint32_t bytes, ipt_mask, off_rt, off_flow, off_toep, ipt_seed, off_seed, off_crc, pad[8];
@@ -1111,6 +1115,7 @@ struct gcl_rxloop {
 	bool left;               /* some worker has left: submit no more */
 	bool k64;                /* rxloop64_kernel (bursts <= 64) */
 	bool debug;              /* gcl_tune.debug at start */
+	uint32_t rec_pf;         /* header prefetch distance of loop_write_records */
 };
 
 static uint64_t now_ns()
@@ -1259,6 +1264,7 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 	}
 	L->max_burst = cfg->max_burst;
 	L->debug = tu.debug != 0;
+	L->rec_pf = (uint32_t)tuned(tu.rec_prefetch, (int32_t)kRecPrefetch);
 	L->vbytes = verdict_bytes(c);
 	const uint64_t mb = align16(cfg->max_burst);
 	LoopParams &lp = L->lp;
@@ -1378,7 +1384,6 @@ fail:
  * header bytes rx_one_pkt reads, prefetching two frames ahead as rx_burst
  * does (rx.c:281-285); bytes past the region read 0. */
 typedef uint32_t u32x4_h __attribute__((vector_size(16), aligned(16)));
-constexpr uint32_t kRecPrefetch = 16; /* header prefetch distance, packets */
 
 static void loop_write_records(gcl_rxloop *L, uint64_t t, uint8_t *dst, uint32_t n,
                                const uint64_t *offs, const uint8_t *olflags, const uint32_t *rss,
@@ -1391,21 +1396,23 @@ static void loop_write_records(gcl_rxloop *L, uint64_t t, uint8_t *dst, uint32_t
 	const size_t P = L->lp.rec_plane / sizeof(u32x4_h);
 	volatile u32x4_h *q = (volatile u32x4_h *)dst;
 	/* Headers a NIC has just written miss to DRAM: the core keeps
-	 * kRecPrefetch of them in flight (bytes 12 and 39, the two ends of what
-	 * every packet reads) instead of rx.c's two, which hides one DRAM latency
-	 * per two packets, not per sixteen.  (With cache-hot headers distances
-	 * 2 and 6 measured the same: profiles/r03_hdr_records_prefetch_ab.jsonl.) */
+	 * L->rec_pf of them in flight (bytes 12 and 39, the two ends of what
+	 * every packet reads; gcl_tune.rec_prefetch, kRecPrefetch by default)
+	 * instead of rx.c's two, which pays one DRAM latency per two packets.
+	 * (With cache-hot headers distances 2 and 6 measured the same:
+	 * profiles/r03_hdr_records_prefetch_ab.jsonl.) */
 	auto prefetch_hdr = [&](uint32_t i) {
 		if (offs[i] < L->region_len && L->region_len - offs[i] >= 40) {
 			__builtin_prefetch(L->region + offs[i] + 12, 0, 3);
 			__builtin_prefetch(L->region + offs[i] + 39, 0, 3);
 		}
 	};
-	for (uint32_t i = 0; i < n && i < kRecPrefetch; i++)
+	const uint32_t pf = L->rec_pf;
+	for (uint32_t i = 0; i < n && i < pf; i++)
 		prefetch_hdr(i);
 	for (uint32_t i = 0; i < n; i++, q++) {
-		if (i + kRecPrefetch < n)
-			prefetch_hdr(i + kRecPrefetch);
+		if (i + pf < n)
+			prefetch_hdr(i + pf);
 		const uint64_t o = offs[i];
 		/* frame dwords 3-6 and 7-10 (bytes 12-43) in two registers, shuffled
 		 * into the chunks without a trip through memory */

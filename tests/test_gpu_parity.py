@@ -1174,7 +1174,8 @@ def test_gpu_ctx_tune_validation(g):
     ok = g.make_tune(threads=512, defer=0)
     assert g.lib.gcl_ctx_tune(clf._ctx, ctypes.byref(ok)) == 0
     bad = [g.make_tune(threads=300), g.make_tune(depth=3), g.make_tune(defer=3), g.make_tune(grid=0),
-           g.make_tune(loop_phase=(2000, 1, 1)), g.make_tune(loop_phase=(10, 0, 0)), g.make_tune(loop_spec=-5)]
+           g.make_tune(loop_phase=(2000, 1, 1)), g.make_tune(loop_phase=(10, 0, 0)), g.make_tune(loop_spec=-5),
+           g.make_tune(rec_prefetch=65), g.make_tune(rec_prefetch=-2)]
     half = g.make_tune()
     half.loop_phase_max = 50  # up / down left AUTO: the three go together
     bad.append(half)

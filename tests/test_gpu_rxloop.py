@@ -106,7 +106,10 @@ def test_rxloop_fuzz_vs_oracle(g, orc, mode, vb, flags, inline, k64):
     # header records, and the offsets of the NIC-mode cases, taken with the
     # poll (see the ragged-burst test); the other cases read after the word
     early = inline == 2 or (inline == 0 and mode == 0)
-    clf.tune(loop64=k64, **({"loop_spec": SPEC_WIDE} if early else {}))
+    # header records: the submitting core's header prefetch distance
+    # (gcl_tune.rec_prefetch) none, one, the whole burst and the default
+    pf = {"rec_prefetch": {8: 0, 4: 1, 2: 64}.get(vb, g.TUNE_AUTO)} if inline == 2 else {}
+    clf.tune(loop64=k64, **({"loop_spec": SPEC_WIDE} if early else {}), **pf)
     loop = clf.rxloop(frames, slots=8, counts=cnt, stats=st, region_len=flen,
                       flags=LOOP_FLAGS[inline](g))
     try:
