@@ -116,9 +116,12 @@ __host__ __device__ constexpr uint64_t loop_stamp(uint64_t t, uint32_t nslots)
 	return ((((t - 1) >> __builtin_ctz(nslots)) & 0x7FFFFFull) | 0x800000ull) << kLoopStampShift;
 }
 /* gcl_tune.rec_prefetch default: frame headers in flight while the submitting
- * core writes header records (cold headers behind a NIC: 4 x 8 records
- * 29 -> 52 Mpkt/s against rx.c's distance 2, profiles/r06_ingress_pipeline.jsonl) */
-constexpr uint32_t kRecPrefetch = 16;
+ * core writes header records -- a whole 64-packet burst's, issued before the
+ * first record.  Six interleaved rounds (profiles/r06_rec_prefetch_ab2.jsonl),
+ * medians for distances 2 / 16 / 64: cold headers 4 x 8 34.5 / 35.5 / 44.0
+ * Mpkt/s (submit 12.8 / 12.4 / 9.5 ns per packet), cold 1 x 1 submit 16.7 /
+ * 12.3 / 8.2, cache-hot lone burst 3.31 / 3.27 / 3.19 us p50 */
+constexpr uint32_t kRecPrefetch = 64;
 
 struct LoopImgHdr {        /* first 64 B of a table image buffer */
 	uint32_t bytes, ipt_mask, off_rt, off_flow, off_toep, ipt_seed, off_seed, off_crc, pad[8];

@@ -444,7 +444,7 @@ struct gcl_tune {
 	int32_t loop_prefetch;   /* the next ticket's poll during classification (0 / 1) */
 	uint32_t debug;          /* 1: loop diagnostics to stderr */
 	int32_t rec_prefetch;    /* GCL_LOOP_HDR_RECORDS: frame headers gcl_rxloop_submit keeps
-	                            in flight while it writes the records, 0..64 (16) */
+	                            in flight while it writes the records, 0..64 (64) */
 	uint64_t loop_t0;        /* tickets start after loop_t0 (rounded down to a multiple of the
 	                            ring's slots): tests of the stamps' wrap */
 };
