@@ -162,7 +162,7 @@ def _pipe_row(rows, burst, workers, verdicts, hash_prefix):
         if (r.get("burst") == burst and r.get("workers") == workers and
                 r.get("verdicts") == verdicts and str(r.get("hash", "")).startswith(hash_prefix)):
             return _pick(r, "mpps_one_core", "burst_latency_p50_us", "burst_latency_p99_us",
-                         "delivered_check", "mpps_samples")
+                         "submit_ns_per_pkt", "deliver_ns_per_pkt", "delivered_check", "mpps_samples")
     return None
 
 
@@ -242,7 +242,8 @@ def compact(result, detail_path=DETAIL_PATH):
                 for row in rows or ():
                     if all(row.get(k) == v for k, v in want.items()):
                         return _pick(row, "mpps_one_core", "burst_latency_p50_us", "burst_latency_p99_us",
-                                     "ns_per_pkt", "nic_wait_frac", "delivered_check", "mpps_samples", "error")
+                                     "submit_ns_per_pkt", "ns_per_pkt", "nic_wait_frac", "delivered_check",
+                                     "mpps_samples", "error")
                 return None
             rec = "read in place, stamped header records in the slot"
             e["pipeline_cold_headers"] = {
@@ -250,8 +251,11 @@ def compact(result, detail_path=DETAIL_PATH):
                 "records_4x8_nic": _ing(ing.get("gpu"), workers=4, verdicts=rec),
                 "records_8x16_nic": _ing(ing.get("gpu"), workers=8, verdicts=rec),
                 "offsets_4x8_nic": _ing(ing.get("gpu"), workers=4, verdicts="read in place"),
-                "cpu_1core_classify_nic": _ing(ing.get("cpu"), post="classify only"),
-                "cpu_1core_lrpc_nic": _ing(ing.get("cpu"), post="classify + rx_make_cmd + lrpc_send"),
+                "cpu_1core_classify_nic": _ing(ing.get("cpu"), post="classify only", prefetch="rx.c's stride 2"),
+                "cpu_1core_lrpc_nic": _ing(ing.get("cpu"), post="classify + rx_make_cmd + lrpc_send",
+                                           prefetch="rx.c's stride 2"),
+                "cpu_1core_lrpc_nic_burst_prefetch": _ing(ing.get("cpu"), post="classify + rx_make_cmd + lrpc_send",
+                                                          prefetch="the burst's 64 headers, then rx.c's stride 2"),
             }
         lp = e2e.get("rxloop", {})
         for k in ("loop_burst64_w1_d1_hdr_records", "loop_burst64_w4_d8_hdr_records"):
@@ -1134,8 +1138,11 @@ def ingress_pipeline_bench(reps=3):
             if err:
                 break
     if cpu_exe:
-        for post in ("classify", "lrpc"):
-            row, err = median_runs([cpu_exe, "100000", post], env, reps)
+        # the reference's own loop (rx.c's prefetch stride 2), classify-only
+        # and + lrpc_send; then the latter with the whole burst's headers
+        # prefetched first, the help the records submit gives the GPU's host side
+        for post in (("classify",), ("lrpc",), ("lrpc", "prefetch")):
+            row, err = median_runs([cpu_exe, "100000", *post], env, reps)
             out["cpu"].append(row or err)
             if err:
                 break

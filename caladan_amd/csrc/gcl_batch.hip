@@ -7,8 +7,9 @@
  *                         through an XOR-swizzled LDS tile, one lane per packet
  *   classify_pair_kernel  per-packet offsets or side arrays: bytes [8, 40) of
  *                         each frame by lane pairs with a DPP exchange
- *   access_probe_kernel   the classify launch's own memory shape without the
- *                         classification (the layout's ceiling)
+ *   access_probe_kernel   the fewest requests the frame layout allows
+ *                         (GCL_PROBE_MIN; the kernels' own shapes run in
+ *                         kModeProbe for gcl_access_probe)
  *
  * Layout in HBM: frames are fixed-stride slots (or a u64 offset
  * array, like mbuf data pointers into the 2 GiB ingress region); verdicts are
@@ -364,7 +365,7 @@ classify_pair_kernel(KParams k)
 	auto pref = [&](uint64_t tt, uint32_t pr[2]) {
 		const uint64_t i = ok(tt) ? tt * NT + tid : 0;
 		pr[0] = *(k.olflags ? k.olflags + i : side_dummy<uint8_t>(k, i));
-		if (MODE == GCL_HASH_NIC)
+		if (MODE == GCL_HASH_NIC || (MODE == kModeProbe && k.rss)) /* the probe: a NIC-mode context's */
 			pr[1] = *(k.rss ? k.rss + i : side_dummy<uint32_t>(k, i));
 	};
 	auto issue = [&](uint64_t my, uint4 r[2]) {
@@ -388,17 +389,29 @@ classify_pair_kernel(KParams k)
 	 * classify_lean (one ballot), the others classify_core (k.plean) */
 	const bool lean_ok = k.plean && !k.dst_hint && !k.trans;
 	auto classify = [&](uint64_t tt, const HdrWords &h, const uint32_t pr[2], uint64_t my) {
+		if constexpr (MODE == kModeProbe) {
+			/* gcl_access_probe: the words rx_one_pkt would read, folded, and
+			 * stored as the verdict is (no tables, hashes or histogram) */
+			if (ok(tt))
+				put_verdict_vf<VF>(k, tt * NT + tid,
+				                   h.d3 ^ h.d5 ^ h.d6 ^ h.d7 ^ h.d8 ^ h.d9 ^ (k.olflags ? pr[0] & 0xFF : 0u) ^
+				                           (k.rss ? pr[1] : 0u));
+			return;
+		}
 		const uint32_t fl = k.olflags ? pr[0] & 0xFF : k.default_flags;
 		const bool plain = !ok(tt) || ((h.d3 & 0x000FFFFF) == 0x00050008 && !(fl & GCL_F_FDIR_ID));
-		if (lean_ok && __all(plain)) {
-			if (ok(tt))
-				put_verdict_vf<VF>(k, tt * NT + tid, classify_lean<MODE, true>(k, h, tb, fl, pr[1], hist, tid, cnt));
-		} else if (ok(tt)) {
-			const uint64_t i = tt * NT + tid;
-			/* this packet's frame offset, for the ARP target's extra read */
-			const uint64_t foff = (my >> 63) ? (my & ~kPairBytewise) : my - 8;
-			put_verdict_vf<VF>(k, i, classify_core<MODE, true, false, true, VF>(
-			                                 k, h, nullptr, tid, i, tb, hist, cnt, 0, 40, pr, foff));
+		if constexpr (MODE != kModeProbe) {
+			if (lean_ok && __all(plain)) {
+				if (ok(tt))
+					put_verdict_vf<VF>(k, tt * NT + tid,
+					                   classify_lean<MODE, true>(k, h, tb, fl, pr[1], hist, tid, cnt));
+			} else if (ok(tt)) {
+				const uint64_t i = tt * NT + tid;
+				/* this packet's frame offset, for the ARP target's extra read */
+				const uint64_t foff = (my >> 63) ? (my & ~kPairBytewise) : my - 8;
+				put_verdict_vf<VF>(k, i, classify_core<MODE, true, false, true, VF>(
+				                                 k, h, nullptr, tid, i, tb, hist, cnt, 0, 40, pr, foff));
+			}
 		}
 	};
 
@@ -612,17 +625,13 @@ template <int MODE>
 static hipError_t launch_mode(const KParams &k, bool tlds, const Geometry &geo,
                               uint32_t tab_lds, uint32_t hist_bytes, int num_cus, hipStream_t s)
 {
-	if constexpr (MODE != kModeProbe) { /* the probe's kernel shape is the tile kernel's */
-		if (geo.pair) {
-			const uint32_t lds = hist_bytes + tab_lds;
-			if (geo.threads == 1024)
-				return launch_pair<MODE, 1024>(k, tlds, lds, num_cus, geo, s);
-			if (geo.threads == 512)
-				return launch_pair<MODE, 512>(k, tlds, lds, num_cus, geo, s);
-			return launch_pair<MODE, 256>(k, tlds, lds, num_cus, geo, s);
-		}
-	} else if (geo.pair) {
-		return hipErrorInvalidValue;
+	if (geo.pair) {
+		const uint32_t lds = hist_bytes + tab_lds;
+		if (geo.threads == 1024)
+			return launch_pair<MODE, 1024>(k, tlds, lds, num_cus, geo, s);
+		if (geo.threads == 512)
+			return launch_pair<MODE, 512>(k, tlds, lds, num_cus, geo, s);
+		return launch_pair<MODE, 256>(k, tlds, lds, num_cus, geo, s);
 	}
 	const uint32_t lds = (uint32_t)geo.threads * 64 + hist_bytes + tab_lds;
 #define GCL_LAUNCH(D, T) \
@@ -703,7 +712,8 @@ extern "C" int gcl_classify(struct gcl_ctx *c, const struct gcl_batch *b,
 static int batch_launch(gcl_ctx *c, const gcl_batch *b, const gcl_out *out, hipStream_t s, bool probe);
 
 /* a dense batch: fixed slots, no side arrays, every header granule in range
- * (classify_kernel's batches; the others run on classify_pair_kernel) */
+ * (classify_kernel's batches; the others run on classify_pair_kernel) --
+ * whether gcl_access_probe's kernel shape is the tile or the pair kernel's */
 static bool dense_batch(const gcl_ctx *c, const gcl_batch *b)
 {
 	return !(b->offs || b->olflags || b->fdir_hi || b->dst_hint || (c->cfg.default_olflags & GCL_F_FDIR_ID) ||
@@ -724,8 +734,8 @@ extern "C" int gcl_access_probe(struct gcl_ctx *c, const struct gcl_batch *b, vo
 		return -EINVAL;
 	if (hipSetDevice(c->device) != hipSuccess)
 		return -ENODEV;
-	if (!minimal && vbytes == verdict_bytes(c) && dense_batch(c, b)) {
-		/* the classify launch itself, rx_one_pkt folded away */
+	if (!minimal && vbytes == verdict_bytes(c)) {
+		/* the classify launch itself (tile or pair kernel), rx_one_pkt folded away */
 		const struct gcl_out o = {out, nullptr, nullptr, nullptr};
 		return batch_launch(c, b, &o, (hipStream_t)hip_stream, true);
 	}
@@ -760,8 +770,8 @@ extern "C" int gcl_classify_ex(struct gcl_ctx *c, const struct gcl_batch *b,
 	return batch_launch(c, b, out, (hipStream_t)hip_stream, false);
 }
 
-/* gcl_classify_ex, or with @probe (gcl_access_probe, dense batches) the same
- * launch in kModeProbe: no counts, stats or timing */
+/* gcl_classify_ex, or with @probe (gcl_access_probe) the same launch in
+ * kModeProbe: no counts, stats or timing */
 static int batch_launch(gcl_ctx *c, const gcl_batch *b, const gcl_out *out, hipStream_t s, bool probe)
 {
 	void *verdicts = out->verdicts;
@@ -794,7 +804,8 @@ static int batch_launch(gcl_ctx *c, const gcl_batch *b, const gcl_out *out, hipS
 	k.stride = b->stride;
 	k.offs = b->offs;
 	k.olflags = b->olflags;
-	k.rss = b->rss;
+	/* a probe loads hash.rss where the context's own launch would */
+	k.rss = probe && c->cfg.hash_mode != GCL_HASH_NIC ? nullptr : b->rss;
 	k.fdir = b->fdir_hi;
 	k.dst_hint = b->dst_hint;
 	k.n = b->n;

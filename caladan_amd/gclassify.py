@@ -598,10 +598,10 @@ class Classifier:
 
     def access_probe(self, frames, n, stride=0, out=None, vbytes=None, offs=None, olflags=None,
                      rss=None, frames_len=None, stream=None, minimal=False):
-        """gcl_access_probe: for a dense batch at the context's verdict width,
-        the classify launch itself with rx_one_pkt folded away (the kernel's
-        own ceiling); otherwise, or with @minimal, the fewest requests the
-        frame layout allows (the layout's ceiling).  Asynchronous."""
+        """gcl_access_probe: at the context's verdict width, the classify
+        launch itself (tile or pair kernel) with rx_one_pkt folded away (the
+        kernel's own ceiling); at another width, or with @minimal, the fewest
+        requests the frame layout allows (the layout's ceiling).  Asynchronous."""
         vbytes = self.vbytes if vbytes is None else vbytes
         if out is None or _nbytes(out) < vbytes * n:
             raise ValueError("probe output buffer too small")

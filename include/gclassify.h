@@ -389,14 +389,16 @@ int gcl_classify_ex(struct gcl_ctx *ctx, const struct gcl_batch *b, const struct
  * @hip_stream; 0, -EINVAL or -EIO.  @out receives @vbytes (1, 2, 4 or 8)
  * bytes per packet (not verdicts: a fold of the loaded bytes).
  *
- * For a dense batch (fixed slots, no side arrays) at the context's own
- * verdict width: the gcl_classify launch itself -- the same geometry, tile
- * loads, LDS staging, drains and barriers, and the same verdict writes
+ * At the context's own verdict width: the gcl_classify launch itself -- the
+ * same kernel and geometry, its loads (tiles staged through LDS with their
+ * drains and barriers for a dense batch; lane-pair header loads, offsets and
+ * side arrays for a batch with offsets), and the same verdict writes
  * (deferred where the context defers them) -- with rx_one_pkt replaced by a
- * fold of the header words it reads.  So its time is the kernel's memory
- * shape with nothing computed: the kernel's own ceiling.
+ * fold of the header words it reads (and the batch's ol_flags, and hash.rss
+ * in a NIC-mode context).  So its time is the kernel's memory shape with
+ * nothing computed: the kernel's own ceiling.
  *
- * Otherwise, or with GCL_PROBE_MIN or'ed into @vbytes: the memory requests
+ * At another width, or with GCL_PROBE_MIN or'ed into @vbytes: the memory requests
  * one launch over @b cannot do without, and nothing else -- the ceiling the
  * frame layout itself sets (e.g. one 128-B line fetched per 64-B header of a
  * 1536-B slot).  One 16-B load per packet of the line holding frame byte 0

@@ -1529,7 +1529,7 @@ def test_gpu_access_probe(g, vbytes):
     offs = rng.permutation(n).astype(np.uint64) * np.uint64(stride) + \
         rng.choice([0, 8, 88, 96, 100, 120], size=n).astype(np.uint64)
     out.zero_()
-    clf.access_probe(f, n, 0, out=out, vbytes=vbytes, offs=dev(offs.astype(np.int64)))
+    clf.access_probe(f, n, 0, out=out, vbytes=vbytes, offs=dev(offs.astype(np.int64)), minimal=True)
     torch.cuda.synchronize()
     got = out.cpu().numpy().view(dt).astype(np.uint64)
     assert (got == want(offs)).all()
@@ -1562,6 +1562,45 @@ def test_gpu_access_probe_kernel_shape(g, vb, R, T, stride, tune):
     else:
         want = (x & np.uint32((1 << (8 * vb)) - 1)).astype({1: np.uint8, 2: np.uint16}[vb])
         assert (got[:n * vb].view(want.dtype) == want).all()
+    assert (got[n * vb:] == 0xEE).all()
+    clf.close()
+
+
+@pytest.mark.parametrize("vb,mode,side", [(2, 0, True), (2, 1, True), (8, 0, False), (4, 0, True), (1, 2, True)])
+def test_gpu_access_probe_pair_shape(g, vb, mode, side):
+    """gcl_access_probe on a batch with offsets at the context's verdict
+    width is classify_pair_kernel in probe mode: packet p's output is the low
+    vb bytes of the XOR of frame dwords 3 and 5-9 at its offset (bytes past
+    frames_len read 0; frames at every alignment, some straddling the end),
+    its ol_flags byte, and its hash.rss in a NIC-mode context only."""
+    rng = np.random.default_rng(1700 + vb + 10 * mode + side)
+    n, flen = 20000 + 37, 1 << 21
+    frames = rng.integers(0, 256, size=flen, dtype=np.uint8)
+    offs = rng.integers(0, flen - 40, size=n).astype(np.uint64)
+    offs[:50] = flen - rng.integers(1, 40, size=50)  # ragged at the end
+    offs[50:60] = flen + rng.integers(0, 1000, size=10)  # past it: zeros
+    olf = rng.integers(0, 256, size=n, dtype=np.uint8)
+    rss = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
+    fl = {1: g.CFG_VERDICT1, 2: g.CFG_VERDICT2, 4: g.CFG_VERDICT4, 8: 0}[vb]
+    clf = g.Classifier(0, 16, mode, fl, thread_bits=3)
+    out = torch.full((n * vb + 64,), 0xEE, dtype=torch.uint8, device="cuda")
+    kw = {"olflags": dev(olf), "rss": dev(rss.view(np.int32))} if side else {}
+    clf.access_probe(dev(frames), n, 0, out=out, offs=dev(offs.astype(np.int64)), **kw)
+    torch.cuda.synchronize()
+    pad = np.concatenate([frames, np.zeros(64, dtype=np.uint8)])
+    x = np.zeros(n, dtype=np.uint32)
+    for i, o in enumerate(offs):
+        o = int(o)
+        h = pad[o:o + 40] if o < flen else np.zeros(40, dtype=np.uint8)
+        h = np.concatenate([h[:max(0, flen - o)], np.zeros(40, dtype=np.uint8)])[:40].view(np.uint32)
+        x[i] = h[3] ^ h[5] ^ h[6] ^ h[7] ^ h[8] ^ h[9]
+    if side:
+        x ^= olf.astype(np.uint32)
+        if mode == 0:  # NIC mode: the context's launch loads hash.rss
+            x ^= rss
+    got = out.cpu().numpy()
+    want = {1: x.astype(np.uint8), 2: x.astype(np.uint16), 4: x, 8: x.astype(np.uint64)}[vb]
+    assert (got[:n * vb].view(want.dtype) == want).all()
     assert (got[n * vb:] == 0xEE).all()
     clf.close()
 

@@ -9,7 +9,11 @@
 // behind a real NIC on a host without DDIO.  The CPU baseline leg of
 // bench.py's pipeline rows; test infrastructure, not the product.
 //
-//   cpupipe <bursts> [classify|lrpc]   -> one JSON line
+//   cpupipe <bursts> [classify|lrpc] [prefetch]   -> one JSON line
+//
+// `prefetch`: before each burst, prefetch every frame's header (the records
+// submit's own trick, gcl_tune.rec_prefetch) on top of rx.c's stride 2 -- not
+// the reference's code, the CPU path given the same help as the GPU's host side.
 //
 // RXPIPE_HASH=nic: NIC mode (hash.rss from the descriptor, rx.c:83); default
 // JENKINS.  RXPIPE_NIC_THREADS (4), RXPIPE_POOL_MBUFS (16384) as in rxpipe.
@@ -31,6 +35,7 @@ int main(int argc, char **argv)
 {
 	const uint32_t nbursts = argc > 1 ? (uint32_t)atoi(argv[1]) : 200000;
 	const bool send = !(argc > 2 && !strcmp(argv[2], "classify"));
+	const bool deep = argc > 3 && !strcmp(argv[3], "prefetch");
 	const uint32_t burst = 64, R = 16, T = 8;
 	const bool nic_hash = getenv("RXPIPE_HASH") && !strcmp(getenv("RXPIPE_HASH"), "nic");
 	const uint32_t nthreads = getenv("RXPIPE_NIC_THREADS") ? (uint32_t)atoi(getenv("RXPIPE_NIC_THREADS")) : 4;
@@ -86,6 +91,9 @@ int main(int argc, char **argv)
 		gb.offs = cur.off;
 		gb.rss = nic_hash ? cur.rss : nullptr;
 		gb.n = cur.n;
+		if (deep)
+			for (uint32_t i = 0; i < cur.n; i++)
+				__builtin_prefetch(nic.region + cur.off[i] + 12, 0, 3);
 		orc_dataplane_burst(d, &gb, v.data(), counts, stats, send);
 		nic.recycle(cur.owner, cur.mbuf, cur.n);
 	};
@@ -106,12 +114,13 @@ int main(int argc, char **argv)
 		delivered += counts[r];
 	const double pkts = (double)burst * nbursts;
 	printf("{\"pipeline\": \"cpu\", \"burst\": %u, \"bursts\": %u, \"hash\": \"%s\", \"post\": \"%s\", "
-	       "\"pool\": \"ingress: %u mbufs, data at element + 344 of 9408-B elements, frames written by %u NIC "
+	       "\"prefetch\": \"%s\", \"pool\": \"ingress: %u mbufs, data at element + 344 of 9408-B elements, frames written by %u NIC "
 	       "threads with non-temporal stores\", "
 	       "\"mpps_one_core\": %.2f, \"ns_per_pkt\": %.2f, \"nic_wait_frac\": %.4f, "
 	       "\"delivered_check\": \"%s\", \"unicast_fail\": %llu, \"host_cpu\": %d, \"pool_huge_frac\": %.3f}\n",
 	       burst, nbursts, nic_hash ? "nic (hash.rss, rx.c:83)" : "jenkins",
-	       send ? "classify + rx_make_cmd + lrpc_send" : "classify only", nmbufs, nthreads,
+	       send ? "classify + rx_make_cmd + lrpc_send" : "classify only",
+	       deep ? "the burst's 64 headers, then rx.c's stride 2" : "rx.c's stride 2", nmbufs, nthreads,
 	       pkts / (el * 1e-3), el / pkts, (double)waited / el,
 	       delivered == (uint64_t)pkts && stats[GCL_RX_PULLED] == (uint64_t)pkts ? "ok" : "MISMATCH",
 	       (unsigned long long)stats[GCL_RX_UNICAST_FAIL], cpu, huge_frac);

@@ -32,11 +32,12 @@ KNAME = {"ingress_nic": "_kernel<0,", "ingress_ws": "_kernel<0,"}
 
 
 def is_kernel(wl, name):
-    """The workload's classify kernel -- not classify_kernel<3, ...>, the same
-    launch in gcl_access_probe's mode (kModeProbe), which the bench times as
-    the kernel's ceiling after its own timed steps."""
+    """The workload's classify kernel -- not classify_kernel<3, ...> or
+    classify_pair_kernel<3, ...>, the same launch in gcl_access_probe's mode
+    (kModeProbe), which the bench times as the kernel's ceiling after its own
+    timed steps."""
     n = name.replace(" ", "")
-    return KNAME.get(wl, "classify_kernel") in n and "classify_kernel<3," not in n
+    return KNAME.get(wl, "classify_kernel") in n and "_kernel<3," not in n
 
 
 def rows(path):
