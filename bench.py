@@ -230,6 +230,13 @@ def compact(result, detail_path=DETAIL_PATH):
                 "frac": ing.get("roofline", {}).get("frac"),
                 "frac_of_ceiling": ing.get("roofline", {}).get("frac_of_ceiling"),
                 "zerocopy_mpps": ing.get("zerocopy_mpps"), "counts_check": ing.get("counts_check")}
+        ws = e2e.get("ingress_pool", {}).get("integrated_nic_working_set")
+        if ws:
+            e["ingress_working_set_nic"] = {
+                "device_resident_mpps": ws.get("device_resident_mpps"),
+                "frac_l2": ws.get("roofline", {}).get("frac"),
+                "frac_of_ceiling": ws.get("roofline", {}).get("frac_of_ceiling"),
+                "counts_check": ws.get("counts_check")}
         rows = e2e.get("rx_burst_pipeline", {}).get("runs")
         rec = "read in place, stamped header records in the slot"
         e["pipeline"] = {"records_1x1_nic": _pipe_row(rows, 64, 1, rec, "nic"),
@@ -1361,7 +1368,10 @@ def ingress_pool_bench(device, vbytes, cycles=64, reps=10, zerocopy=True,
             # the working set's frames (~1 MB of header lines) stay in L2:
             # the bound is the L2's, not HBM's (HBM moves 0.26 of its peak)
             "roofline": roofline_obj(n * bpp, gms_w, pmc_traffic("ingress_ws", vbytes, gms_w),
-                                     {"bytes_per_pkt": bpp}, bound="l2", peak=L2_PEAK_GBS)}
+                                     {"bytes_per_pkt": bpp,
+                                      **ceiling(nic, region, n, 0, dv, gms_w, offs=offs_w, olflags=olf_w,
+                                                rss=rss_w)},
+                                     bound="l2", peak=L2_PEAK_GBS)}
         del offs_w, olf_w, rss_w, order_ws
     if not zerocopy or "nic" not in rows:
         del region, offs, olf, rss, dv, nic, jen

@@ -356,11 +356,14 @@ classify_pair_kernel(KParams k)
 	const uint64_t step = gridDim.x;
 	const uint64_t *offs_src = k.offs ? k.offs : (const uint64_t *)k.tables;
 	auto ok = [&](uint64_t tt) { return tt < k.ntiles && tt * NT + tid < k.n; };
+	/* the raw offset: clamped (user_off) where it is used, two half-steps
+	 * later -- clamped here, the compare right after the load made every
+	 * half-step wait for it, and so for every load issued before it */
 	auto ld_off = [&](uint64_t tt) -> uint64_t {
-		return user_off(k, offs_src[k.offs && ok(tt) ? tt * NT + tid : 0]);
+		return offs_src[k.offs && ok(tt) ? tt * NT + tid : 0];
 	};
 	auto src_of = [&](uint64_t tt, uint64_t raw) -> uint64_t {
-		return pair_src(k, !ok(tt) ? kNoOff : k.offs ? raw : (tt * NT + tid) * k.stride);
+		return pair_src(k, !ok(tt) ? kNoOff : k.offs ? user_off(k, raw) : (tt * NT + tid) * k.stride);
 	};
 	auto pref = [&](uint64_t tt, uint32_t pr[2]) {
 		const uint64_t i = ok(tt) ? tt * NT + tid : 0;
@@ -375,6 +378,12 @@ classify_pair_kernel(KParams k)
 	/* the landed halves -> this lane's header dwords (frame bytes 12-39;
 	 * d10, bytes 40-43, is not fetched: avail 40 sends ARP to the frame) */
 	auto unpack = [&](uint4 r[2], uint64_t my, HdrWords &h) {
+		/* every loaded dword live until here: a dword nothing reads (bytes
+		 * 8-11) let the compiler reuse its register right after the load
+		 * was issued, and wait for that load there, a latency per
+		 * half-step */
+		asm volatile("" : "+v"(r[0].x), "+v"(r[0].y), "+v"(r[0].z), "+v"(r[0].w), "+v"(r[1].x), "+v"(r[1].y),
+		             "+v"(r[1].z), "+v"(r[1].w));
 		pair_exchange(r);
 		if ((my >> 63) && my != kNoOff) { /* bytewise (rare) */
 			const uint64_t off = my & ~kPairBytewise;
