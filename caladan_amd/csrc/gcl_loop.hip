@@ -122,6 +122,8 @@ __host__ __device__ constexpr uint64_t loop_stamp(uint64_t t, uint32_t nslots)
  * Mpkt/s (submit 12.8 / 12.4 / 9.5 ns per packet), cold 1 x 1 submit 16.7 /
  * 12.3 / 8.2, cache-hot lone burst 3.31 / 3.27 / 3.19 us p50 */
 constexpr uint32_t kRecPrefetch = 64;
+/* gcl_tune.slot_prefetch default (measured: see prefetch_slot) */
+constexpr uint32_t kDefaultSlotPrefetch = 0;
 
 struct LoopImgHdr {        /* first 64 B of a table image buffer */
 	uint32_t bytes, ipt_mask, off_rt, off_flow, off_toep, ipt_seed, off_seed, off_crc, pad[8];
@@ -1119,6 +1121,8 @@ struct gcl_rxloop {
 	bool k64;                /* rxloop64_kernel (bursts <= 64) */
 	bool debug;              /* gcl_tune.debug at start */
 	uint32_t rec_pf;         /* header prefetch distance of loop_write_records */
+	bool slot_pf;            /* loop_await prefetches the next slot for writing */
+	uint64_t slot_pf_t;      /* ... once per ticket: the last ticket it did so for */
 };
 
 static uint64_t now_ns()
@@ -1268,6 +1272,7 @@ extern "C" int gcl_rxloop_start(struct gcl_ctx *c, const struct gcl_rxloop_cfg *
 	L->max_burst = cfg->max_burst;
 	L->debug = tu.debug != 0;
 	L->rec_pf = (uint32_t)tuned(tu.rec_prefetch, (int32_t)kRecPrefetch);
+	L->slot_pf = tuned(tu.slot_prefetch, (int32_t)kDefaultSlotPrefetch) != 0;
 	L->vbytes = verdict_bytes(c);
 	const uint64_t mb = align16(cfg->max_burst);
 	LoopParams &lp = L->lp;
@@ -1542,9 +1547,31 @@ extern "C" int64_t gcl_rxloop_submit(struct gcl_rxloop *L, uint32_t n, const uin
 	return (int64_t)t;
 }
 
+/* The lines the next submit writes, for ownership, while a host with
+ * nothing else in flight waits for ticket @t (gcl_tune.slot_prefetch): the
+ * GPU's polls of a slot read it over PCIe, and a line that left the core's
+ * caches that way costs a miss when the submit writes it again. */
+static void prefetch_slot(gcl_rxloop *L, uint64_t t)
+{
+	uint8_t *s = (uint8_t *)loop_slot(L, t + 1);
+	__builtin_prefetch(s, 1, 3);
+	if (L->lp.hdr_rec) {
+		for (uint32_t j = 0; j < 4; j++)
+			for (uint32_t b = 0; b < 16 * L->max_burst; b += 64)
+				__builtin_prefetch(s + L->lp.off_hdr + j * L->lp.rec_plane + b, 1, 3);
+	} else {
+		for (uint32_t b = 0; b < 8 * L->max_burst; b += 64)
+			__builtin_prefetch(s + L->lp.off_offs + b, 1, 3);
+	}
+}
+
 /* spin up to @spin_ns for ticket @t's burst: 0, -EAGAIN or -ESHUTDOWN */
 static int loop_await(gcl_rxloop *L, uint64_t t, uint64_t spin_ns)
 {
+	if (L->slot_pf && t == L->next && L->slot_pf_t != t && !burst_complete(L, t)) {
+		L->slot_pf_t = t;
+		prefetch_slot(L, t);
+	}
 	const uint64_t t0 = spin_ns ? now_ns() : 0;
 	uint32_t k = 0;
 	while (!burst_complete(L, t)) {

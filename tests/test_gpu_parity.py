@@ -1175,7 +1175,7 @@ def test_gpu_ctx_tune_validation(g):
     assert g.lib.gcl_ctx_tune(clf._ctx, ctypes.byref(ok)) == 0
     bad = [g.make_tune(threads=300), g.make_tune(depth=3), g.make_tune(defer=3), g.make_tune(grid=0),
            g.make_tune(loop_phase=(2000, 1, 1)), g.make_tune(loop_phase=(10, 0, 0)), g.make_tune(loop_spec=-5),
-           g.make_tune(rec_prefetch=65), g.make_tune(rec_prefetch=-2)]
+           g.make_tune(rec_prefetch=65), g.make_tune(rec_prefetch=-2), g.make_tune(slot_prefetch=2)]
     half = g.make_tune()
     half.loop_phase_max = 50  # up / down left AUTO: the three go together
     bad.append(half)

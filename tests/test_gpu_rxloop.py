@@ -109,6 +109,8 @@ def test_rxloop_fuzz_vs_oracle(g, orc, mode, vb, flags, inline, k64):
     # header records: the submitting core's header prefetch distance
     # (gcl_tune.rec_prefetch) none, one, the whole burst and the default
     pf = {"rec_prefetch": {8: 0, 4: 1, 2: 64}.get(vb, g.TUNE_AUTO)} if inline == 2 else {}
+    # and the next slot taken for writing during a wait (gcl_tune.slot_prefetch)
+    pf["slot_prefetch"] = {8: 1, 2: 1, 4: 0}.get(vb, g.TUNE_AUTO)
     clf.tune(loop64=k64, **({"loop_spec": SPEC_WIDE} if early else {}), **pf)
     loop = clf.rxloop(frames, slots=8, counts=cnt, stats=st, region_len=flen,
                       flags=LOOP_FLAGS[inline](g))
