@@ -122,8 +122,12 @@ __host__ __device__ constexpr uint64_t loop_stamp(uint64_t t, uint32_t nslots)
  * Mpkt/s (submit 12.8 / 12.4 / 9.5 ns per packet), cold 1 x 1 submit 16.7 /
  * 12.3 / 8.2, cache-hot lone burst 3.31 / 3.27 / 3.19 us p50 */
 constexpr uint32_t kRecPrefetch = 64;
-/* gcl_tune.slot_prefetch default (measured: see prefetch_slot) */
-constexpr uint32_t kDefaultSlotPrefetch = 0;
+/* gcl_tune.slot_prefetch default.  Six interleaved rounds of fresh processes
+ * (profiles/r06_slot_prefetch_ab.jsonl), p50 medians off -> on: cache-hot
+ * lone burst, NIC hash 3.35 -> 3.24 us (5 of 6 rounds faster, one equal),
+ * 2 x 2 3.22 -> 3.09; JENKINS 3.30 -> 3.32 and cold headers 4.20 -> 4.21,
+ * within their noise */
+constexpr uint32_t kDefaultSlotPrefetch = 1;
 
 struct LoopImgHdr {        /* first 64 B of a table image buffer */
 	uint32_t bytes, ipt_mask, off_rt, off_flow, off_toep, ipt_seed, off_seed, off_crc, pad[8];

@@ -448,7 +448,7 @@ struct gcl_tune {
 	int32_t rec_prefetch;    /* GCL_LOOP_HDR_RECORDS: frame headers gcl_rxloop_submit keeps
 	                            in flight while it writes the records, 0..64 (64) */
 	int32_t slot_prefetch;   /* a wait with no later ticket submitted takes the next
-	                            ticket's slot lines for writing while it spins (0 / 1) */
+	                            ticket's slot lines for writing while it spins (0 / 1; 1) */
 	uint32_t pad;
 	uint64_t loop_t0;        /* tickets start after loop_t0 (rounded down to a multiple of the
 	                            ring's slots): tests of the stamps' wrap */
