@@ -478,6 +478,23 @@ uint64_t gcl_host_deliver1(struct gcl_host_proc *const *clients_by_id, uint32_t 
 	                       n, ops, stats, sizeof(*v));
 }
 
+void gcl_host_prefetch_rxq(struct gcl_host_proc *const *clients, int nr_clients)
+{
+	for (int c = 0; c < nr_clients; c++) {
+		const struct gcl_host_proc *p = clients[c];
+		if (!p)
+			continue;
+		const unsigned int nt = p->thread_count <= GCL_NCPU ? p->thread_count : GCL_NCPU;
+		for (unsigned int t = 0; t < nt; t++) {
+			struct gcl_lrpc_chan_out *ch = p->rxq[t];
+			if (!ch || !ch->tbl || !ch->size)
+				continue;
+			__builtin_prefetch(ch, 1, 3);
+			__builtin_prefetch(&ch->tbl[ch->send_head & (ch->size - 1)], 1, 3);
+		}
+	}
+}
+
 uint64_t gcl_host_deliver_recs(struct gcl_host_proc *const *clients_by_id, uint32_t max_runtimes,
                                struct gcl_host_proc *const *clients, int nr_clients,
                                const struct gcl_loop_rec *recs, uint8_t vbytes,

@@ -249,6 +249,7 @@ def _load():
         "gcl_verdict1_to4": (ctypes.c_uint32, [ctypes.c_uint8, ctypes.c_uint8]),
         "gcl_host_deliver_recs": (u64, [vp, u32, vp, i32, vp, ctypes.c_uint8, ctypes.c_uint8, vp, vp,
                                         vp, ctypes.c_uint8, vp, u64, ctypes.POINTER(GclHostOps), vp]),
+        "gcl_host_prefetch_rxq": (None, [vp, i32]),
         "gcl_rxloop_peek": (i32, [vp, ctypes.c_int64, u64, ctypes.POINTER(vp), ctypes.POINTER(u32)]),
         "gcl_rxloop_release": (i32, [vp, ctypes.c_int64]),
         "gcl_rxloop_poll_stats": (i32, [vp, vp]),

@@ -162,6 +162,14 @@ uint64_t gcl_host_deliver_recs(struct gcl_host_proc *const *clients_by_id, uint3
                                uint8_t default_olflags, const uint64_t *shmptr, uint64_t n,
                                const struct gcl_host_ops *ops, uint64_t *stats);
 
+/*
+ * gcl_host_prefetch_rxq - a hint for a dataplane thread with time to spare
+ * (waiting for a burst's verdicts): the ring slot each kthread's next message
+ * lands in, and the channel state, taken for writing, so that the post-pass
+ * after the wait writes lines it owns.  No effect on results.
+ */
+void gcl_host_prefetch_rxq(struct gcl_host_proc *const *clients, int nr_clients);
+
 #ifdef __cplusplus
 }
 #endif

@@ -556,6 +556,8 @@ def test_host_deliver4_fast_path(g, orc, meta):
         clients = (ctypes.c_void_p * len(procs))(*[ctypes.addressof(p) for p in procs.values()])
         stats = np.zeros(8, dtype=np.uint64)
         if compact == "recs":  # the fast path over 16-B loop records, in place
+            # (after the wait-time hint on the rings, which changes nothing)
+            g.lib.gcl_host_prefetch_rxq(clients, len(procs))
             rr = np.zeros(n, dtype=g.LOOP_REC_DTYPE)
             rr["verdict"] = v4.view(np.uint32)
             d = g.lib.gcl_host_deliver_recs(by_id, R, clients, len(procs), rr.ctypes.data, 4, 0,

@@ -57,7 +57,11 @@ static uint64_t now_ns()
  * converted with the rate measured over the run. */
 static inline uint64_t ticks()
 {
-	return __builtin_ia32_rdtsc();
+	/* rdtscp: after every earlier instruction has executed, so the wait /
+	 * deliver split does not move a load still in flight (the last records'
+	 * miss) into the deliver side */
+	unsigned int aux;
+	return __builtin_ia32_rdtscp(&aux);
 }
 
 int main(int argc, char **argv)
@@ -202,6 +206,12 @@ int main(int argc, char **argv)
 	 * the submit lands at any phase of the worker's polls (which start when
 	 * it has stored the previous burst's records) as bursts from a NIC do;
 	 * "rand:N": uniform [0, N) ns (sparser traffic) */
+	/* while a lone burst (depth 1) is awaited, the rings' next slots are taken
+	 * for writing (gcl_host_prefetch_rxq); six
+	 * interleaved rounds, cache-hot lone burst NIC: p50 medians 3.27 -> 3.09
+	 * us, submit + deliver 7.2 -> 6.0 ns/pkt (profiles/r06_ring_prefetch_ab.jsonl).
+	 * RXPIPE_RING_PREFETCH=0 leaves it out */
+	const bool ring_pf = depth == 1 && !(getenv("RXPIPE_RING_PREFETCH") && !atoi(getenv("RXPIPE_RING_PREFETCH")));
 	const char *gap_env = getenv("RXPIPE_GAP_NS");
 	const bool gap_rand = gap_env && !strncmp(gap_env, "rand", 4);
 	const uint64_t gap_span = gap_rand && gap_env[4] == ':' ? strtoull(gap_env + 5, nullptr, 0) : 2000;
@@ -287,6 +297,8 @@ int main(int argc, char **argv)
 			} else {
 				const gcl_loop_rec *recs;
 				uint32_t n = 0;
+				if (ring_pf)
+					gcl_host_prefetch_rxq(clients.data(), (int)R);
 				const int w = gcl_rxloop_peek(loop, t, 1000000000ull, &recs, &n);
 				if (w || n != burst) {
 					fprintf(stderr, "peek: %d (n %u)\n", w, n);
