@@ -1246,9 +1246,12 @@ def ceiling(clf, frames, n, stride, out, kernel_ms, reps=10, **kw):
     16-B chunks, the descriptor arrays) and its per-packet stores, no
     classification -- timed like the kernel.  frac_of_ceiling = probe time /
     kernel time: how close the kernel runs to what this frame layout allows
-    (e.g. one 128-B line per header of a 1536-B slot)."""
+    (e.g. one 128-B line per header of a 1536-B slot).  The fastest of
+    three timed rounds: the ceiling is what the shape reaches, and a single
+    round's noise (~1 %) put tcp1500's ratio above 1 (r06p)."""
     st = torch.cuda.current_stream().cuda_stream
-    _, pms = timed_launches(lambda: clf.access_probe(frames, n, stride, out=out, stream=st, **kw), reps)
+    pms = min(timed_launches(lambda: clf.access_probe(frames, n, stride, out=out, stream=st, **kw), reps)[1]
+              for _ in range(3))
     return {"ceiling_ms": round(pms, 4), "frac_of_ceiling": round(pms / kernel_ms, 4),
             "ceiling_what": ("gcl_access_probe on the same buffers: the launch's header loads, "
                              "descriptor loads and per-packet stores without the classification")}
