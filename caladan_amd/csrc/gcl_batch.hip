@@ -242,8 +242,30 @@ classify_kernel(KParams k)
 	}
 	if (kl)
 		flush_lds();
-	if (nreg)
+	if (nreg && k.vstage && nreg <= k.vcap) {
+		/* the registers through the buffer (its stores above have their
+		 * data: a barrier and it is free), then out 16 B per lane like the
+		 * buffer, not one verdict per lane per tile */
+		__syncthreads();
+		for (uint32_t q = 0; q < nreg; q++) {
+			uint8_t *d = vbuf + ((nreg - 1 - q) * NT + tid) * vb;
+			if (vb == 1)
+				*d = (uint8_t)vr[0];
+			else
+				*(uint16_t *)d = (uint16_t)vr[0];
+			const uint32_t sh = 8 * vb;
+#pragma unroll
+			for (int r = 0; r < kVregs - 1; r++)
+				vr[r] = (vr[r] >> sh) | (vr[r + 1] << (32 - sh));
+			vr[kVregs - 1] >>= sh;
+		}
+		__syncthreads();
+		kf += k.vcap;
+		kl = nreg;
+		flush_lds();
+	} else if (nreg) {
 		flush_regs();
+	}
 	flush_counters<NT>(k, hist, cnt);
 }
 
@@ -834,6 +856,7 @@ static int batch_launch(gcl_ctx *c, const gcl_batch *b, const gcl_out *out, hipS
 	k.cflags = kernel_cflags(c);
 	k.plean = (uint32_t)tuned(c->tune.pair_lean, kDefaultPairLean);
 	k.tlean = (uint32_t)tuned(c->tune.tile_lean, kDefaultTileLean);
+	k.vstage = (uint32_t)tuned(c->tune.vstage, kDefaultVstage);
 	k.default_flags = c->cfg.default_olflags;
 
 	/* the specialised fast path needs every header granule in range */

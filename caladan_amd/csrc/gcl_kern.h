@@ -89,6 +89,7 @@ struct KParams {
 	uint32_t vregs;  /* with vcap: tiles past a full LDS buffer held in registers */
 	uint32_t plean;  /* classify_pair_kernel: plain-IPv4 waves on classify_lean */
 	uint32_t tlean;  /* classify_kernel: plain-IPv4 waves on classify_lean */
+	uint32_t vstage; /* classify_kernel: the last register flush staged through LDS */
 };
 
 /* classify_kernel's verdict registers: kVregs dwords per lane, so 4 * kVregs
@@ -671,5 +672,6 @@ constexpr int kDefaultPairLean = 1;
 constexpr int kDefaultDefer = 1;
 /* gcl_tune.tile_lean default: classify_kernel's plain-IPv4 waves on classify_lean */
 constexpr int kDefaultTileLean = 1;
+constexpr int kDefaultVstage = 0; /* gcl_tune.vstage default */
 
 } // namespace gclk

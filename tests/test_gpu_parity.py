@@ -345,7 +345,11 @@ def test_gpu_dense_narrow_verdicts(g, orc, wl, R, T, vb, defer, lean):
     (1, {"tables": 1, "grid": 40}), (2, {"tables": 1, "grid": 9}),
     # every wave on classify_core (the lean waves off)
     (1, {"tile_lean": 0}), (2, {"tile_lean": 0, "grid": 3}), (1, {"tile_lean": 0, "grid": 20}),
-    (2, {"tile_lean": 0, "threads": 512, "grid": 7}), (1, {"tile_lean": 0, "grid": 5, "depth": 1})])
+    (2, {"tile_lean": 0, "threads": 512, "grid": 7}), (1, {"tile_lean": 0, "grid": 5, "depth": 1}),
+    # the last register flush staged through the LDS buffer (gcl_tune.vstage)
+    (1, {"vstage": 1}), (1, {"vstage": 1, "grid": 40}), (1, {"vstage": 1, "grid": 20}),
+    (1, {"vstage": 1, "grid": 40, "depth": 1}), (2, {"vstage": 1, "threads": 512, "grid": 7}),
+    (1, {"vstage": 0, "grid": 40})])
 @pytest.mark.parametrize("vb", [1, 2])
 def test_gpu_dense_deferred_flushes(g, orc, vb, defer, env):
     """The tile kernel's LDS verdict buffer when a block walks more tiles
@@ -1175,7 +1179,8 @@ def test_gpu_ctx_tune_validation(g):
     assert g.lib.gcl_ctx_tune(clf._ctx, ctypes.byref(ok)) == 0
     bad = [g.make_tune(threads=300), g.make_tune(depth=3), g.make_tune(defer=3), g.make_tune(grid=0),
            g.make_tune(loop_phase=(2000, 1, 1)), g.make_tune(loop_phase=(10, 0, 0)), g.make_tune(loop_spec=-5),
-           g.make_tune(rec_prefetch=65), g.make_tune(rec_prefetch=-2), g.make_tune(slot_prefetch=2)]
+           g.make_tune(rec_prefetch=65), g.make_tune(rec_prefetch=-2), g.make_tune(slot_prefetch=2),
+           g.make_tune(vstage=3)]
     half = g.make_tune()
     half.loop_phase_max = 50  # up / down left AUTO: the three go together
     bad.append(half)
@@ -1537,7 +1542,8 @@ def test_gpu_access_probe(g, vbytes):
 
 @pytest.mark.parametrize("vb,R,T,stride,tune", [(1, 16, 8, 64, {}), (2, 16, 8, 64, {"defer": 2, "grid": 7}),
                                                 (2, 1024, 4, 1536, {}), (8, 16, 8, 64, {}),
-                                                (1, 16, 8, 64, {"defer": 0, "depth": 1})])
+                                                (1, 16, 8, 64, {"defer": 0, "depth": 1}),
+                                                (1, 16, 8, 64, {"vstage": 1, "grid": 40})])
 def test_gpu_access_probe_kernel_shape(g, vb, R, T, stride, tune):
     """gcl_access_probe on a dense batch at the context's verdict width is the
     classify launch itself with rx_one_pkt folded away (the kernel's own
