@@ -450,8 +450,8 @@ struct gcl_tune {
 	int32_t slot_prefetch;   /* a wait with no later ticket submitted takes the next
 	                            ticket's slot lines for writing while it spins (0 / 1; 1) */
 	int32_t vstage;          /* deferred verdicts: the register-held part of the last write
-	                            staged through LDS and stored 16 B per lane (1) or stored a
-	                            verdict per lane per tile (0) */
+	                            staged through LDS and stored 16 B per lane (1, default) or
+	                            stored a verdict per lane per tile (0) */
 	uint64_t loop_t0;        /* tickets start after loop_t0 (rounded down to a multiple of the
 	                            ring's slots): tests of the stamps' wrap */
 };
