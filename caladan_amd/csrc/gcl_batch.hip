@@ -25,6 +25,7 @@
 #include <map>
 #include <mutex>
 #include <set>
+#include <type_traits>
 #include <utility>
 
 #include "../../include/gclassify.h"
@@ -348,7 +349,15 @@ __device__ __forceinline__ void pair_exchange(uint4 r[2])
 	r[1] = sel4(odd, r[1], y);
 }
 
-template <int MODE, bool TLDS, int NT, int VF>
+/* I32: a batch whose frames, offsets, side arrays and verdicts all lie within
+ * 2 GiB (pair_i32_ok) runs its per-packet arithmetic in 32 bits: packet
+ * indices and frame offsets as u32, every load and store through a buffer
+ * descriptor with a 32-bit offset (no 64-bit address per lane), one DPP move
+ * per broadcast instead of two */
+constexpr uint32_t kBw32 = 0x80000000u;   /* I32 pair_src: read bytewise */
+constexpr uint32_t kNoOff32 = 0xFFFFFFFFu; /* I32 pair_src: no packet */
+
+template <int MODE, bool TLDS, int NT, int VF, bool I32>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4)))
 classify_pair_kernel(KParams k)
 {
@@ -376,30 +385,119 @@ classify_pair_kernel(KParams k)
 
 	Counters cnt = {0, 0, 0, 0};
 	const uint64_t step = gridDim.x;
+	using Src = std::conditional_t<I32, uint32_t, uint64_t>; /* pair_src's encoding */
 	const uint64_t *offs_src = k.offs ? k.offs : (const uint64_t *)k.tables;
-	auto ok = [&](uint64_t tt) { return tt < k.ntiles && tt * NT + tid < k.n; };
+	/* I32: buffer descriptors (a missing array reads 16 B of the tables) */
+	const __amdgpu_buffer_rsrc_t rs_fr = gcl::host_rsrc(k.frames, I32 ? k.frames_len : 16);
+	const __amdgpu_buffer_rsrc_t rs_off = gcl::host_rsrc(k.offs ? (const void *)k.offs : k.tables,
+	                                                     I32 && k.offs ? 8 * k.n : 16);
+	const __amdgpu_buffer_rsrc_t rs_olf = gcl::host_rsrc(k.olflags ? (const void *)k.olflags : k.tables,
+	                                                     I32 && k.olflags ? k.n : 16);
+	const __amdgpu_buffer_rsrc_t rs_rss = gcl::host_rsrc(k.rss ? (const void *)k.rss : k.tables,
+	                                                     I32 && k.rss ? 4 * k.n : 16);
+	const uint32_t vbytes = VF ? VF : verdict_width(k.cflags);
+	const __amdgpu_buffer_rsrc_t rs_v = gcl::host_rsrc(k.verdicts, I32 ? vbytes * k.n : 16);
+	const uint32_t flen32 = (uint32_t)k.frames_len, n32 = (uint32_t)k.n;
+	const uint32_t fbase3 = (uint32_t)(uintptr_t)k.frames & 3;
+	const uint32_t half16 = 16u * (uint32_t)(tid & 1);
+	auto idx = [&](uint64_t tt) -> uint64_t {
+		if constexpr (I32)
+			return (uint32_t)tt * (uint32_t)NT + (uint32_t)tid;
+		else
+			return tt * NT + tid;
+	};
+	auto ok = [&](uint64_t tt) {
+		if constexpr (I32)
+			return tt < k.ntiles && (uint32_t)idx(tt) < n32;
+		else
+			return tt < k.ntiles && tt * NT + tid < k.n;
+	};
 	/* the raw offset: clamped (user_off) where it is used, two half-steps
 	 * later -- clamped here, the compare right after the load made every
 	 * half-step wait for it, and so for every load issued before it */
 	auto ld_off = [&](uint64_t tt) -> uint64_t {
-		return offs_src[k.offs && ok(tt) ? tt * NT + tid : 0];
+		if constexpr (I32) {
+			const uint32_t o = k.offs && ok(tt) ? 8u * (uint32_t)idx(tt) : 0u;
+			const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs_off, (int)o, 0, 0);
+			return (uint64_t)v[1] << 32 | v[0];
+		} else {
+			return offs_src[k.offs && ok(tt) ? tt * NT + tid : 0];
+		}
 	};
-	auto src_of = [&](uint64_t tt, uint64_t raw) -> uint64_t {
-		return pair_src(k, !ok(tt) ? kNoOff : k.offs ? user_off(k, raw) : (tt * NT + tid) * k.stride);
+	auto src_of = [&](uint64_t tt, uint64_t raw) -> Src {
+		if constexpr (I32) {
+			/* pair_src in 32 bits: frames_len < 2^31 - 64, so off + 8 and
+			 * kBw32 | off never meet each other or kNoOff32 */
+			const uint32_t off = k.offs ? (raw < k.frames_len ? (uint32_t)raw : flen32)
+			                            : (uint32_t)idx(tt) * (uint32_t)k.stride;
+			const bool in = off < flen32;
+			const bool fits = in && flen32 - off >= 40 && ((fbase3 + off) & 3) == 0;
+			const uint32_t my = fits ? off + 8 : kBw32 | (in ? off : flen32);
+			return ok(tt) ? my : kNoOff32;
+		} else {
+			return pair_src(k, !ok(tt) ? kNoOff : k.offs ? user_off(k, raw) : (tt * NT + tid) * k.stride);
+		}
 	};
 	auto pref = [&](uint64_t tt, uint32_t pr[2]) {
-		const uint64_t i = ok(tt) ? tt * NT + tid : 0;
-		pr[0] = *(k.olflags ? k.olflags + i : side_dummy<uint8_t>(k, i));
-		if (MODE == GCL_HASH_NIC || (MODE == kModeProbe && k.rss)) /* the probe: a NIC-mode context's */
-			pr[1] = *(k.rss ? k.rss + i : side_dummy<uint32_t>(k, i));
+		if constexpr (I32) {
+			const uint32_t i = ok(tt) ? (uint32_t)idx(tt) : 0u;
+			pr[0] = __builtin_amdgcn_raw_buffer_load_b8(rs_olf, (int)(k.olflags ? i : 0u), 0, 0);
+			if (MODE == GCL_HASH_NIC || (MODE == kModeProbe && k.rss))
+				pr[1] = __builtin_amdgcn_raw_buffer_load_b32(rs_rss, (int)(k.rss ? 4u * i : 0u), 0, 0);
+		} else {
+			const uint64_t i = ok(tt) ? tt * NT + tid : 0;
+			pr[0] = *(k.olflags ? k.olflags + i : side_dummy<uint8_t>(k, i));
+			if (MODE == GCL_HASH_NIC || (MODE == kModeProbe && k.rss)) /* the probe: a NIC-mode context's */
+				pr[1] = *(k.rss ? k.rss + i : side_dummy<uint32_t>(k, i));
+		}
 	};
-	auto issue = [&](uint64_t my, uint4 r[2]) {
-		r[0] = pair_load<0>(k, my);
-		r[1] = pair_load<1>(k, my);
+	/* load J of this lane: half (lane & 1) of the pair's packet J */
+	auto load32 = [&](uint32_t s) -> uint4 {
+		const uint32_t a = (s >> 31) ? 0u : s + half16;
+		const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs_fr, (int)a, 0, 0);
+		return make_uint4(v[0], v[1], v[2], v[3]);
+	};
+	auto issue = [&](Src my, uint4 r[2]) {
+		if constexpr (I32) {
+			r[0] = load32(mdpp<0xA0>(my)); /* quad_perm [0,0,2,2] */
+			r[1] = load32(mdpp<0xF5>(my)); /* quad_perm [1,1,3,3] */
+		} else {
+			r[0] = pair_load<0>(k, my);
+			r[1] = pair_load<1>(k, my);
+		}
+	};
+	auto bytewise = [&](Src my) {
+		if constexpr (I32)
+			return (my >> 31) && my != kNoOff32;
+		else
+			return (my >> 63) && my != kNoOff;
+	};
+	/* this packet's frame offset from its pair_src encoding */
+	auto frame_off_of = [&](Src my) -> uint64_t {
+		if constexpr (I32)
+			return (my >> 31) ? (uint64_t)(my & ~kBw32) : (uint64_t)my - 8;
+		else
+			return (my >> 63) ? (my & ~kPairBytewise) : my - 8;
+	};
+	auto put = [&](uint64_t i, uint64_t v) {
+		if constexpr (I32) {
+			const int o = (int)((uint32_t)i * vbytes);
+			if (vbytes == 1)
+				__builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, rs_v, o, 0, gcl::kSysAux);
+			else if (vbytes == 2)
+				__builtin_amdgcn_raw_buffer_store_b16((uint16_t)v, rs_v, o, 0, gcl::kSysAux);
+			else if (vbytes == 4)
+				__builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, rs_v, o, 0, gcl::kSysAux);
+			else
+				__builtin_amdgcn_raw_buffer_store_b64(
+				        (gcl::u32x2){(uint32_t)v, (uint32_t)(v >> 32)}, rs_v, o, 0, gcl::kSysAux);
+		} else {
+			put_verdict_vf<VF>(k, i, v);
+		}
 	};
 	/* the landed halves -> this lane's header dwords (frame bytes 12-39;
 	 * d10, bytes 40-43, is not fetched: avail 40 sends ARP to the frame) */
-	auto unpack = [&](uint4 r[2], uint64_t my, HdrWords &h) {
+	auto unpack = [&](uint4 r[2], Src my, HdrWords &h) {
 		/* every loaded dword live until here: a dword nothing reads (bytes
 		 * 8-11) let the compiler reuse its register right after the load
 		 * was issued, and wait for that load there, a latency per
@@ -407,8 +505,8 @@ classify_pair_kernel(KParams k)
 		asm volatile("" : "+v"(r[0].x), "+v"(r[0].y), "+v"(r[0].z), "+v"(r[0].w), "+v"(r[1].x), "+v"(r[1].y),
 		             "+v"(r[1].z), "+v"(r[1].w));
 		pair_exchange(r);
-		if ((my >> 63) && my != kNoOff) { /* bytewise (rare) */
-			const uint64_t off = my & ~kPairBytewise;
+		if (bytewise(my)) { /* bytewise (rare) */
+			const uint64_t off = frame_off_of(my);
 			r[0] = load16_bytes(k, off + 8);
 			r[1] = load16_bytes(k, off + 24);
 		}
@@ -419,14 +517,13 @@ classify_pair_kernel(KParams k)
 	 * batch without dst_ip hints or the transport pre-hash takes
 	 * classify_lean (one ballot), the others classify_core (k.plean) */
 	const bool lean_ok = k.plean && !k.dst_hint && !k.trans;
-	auto classify = [&](uint64_t tt, const HdrWords &h, const uint32_t pr[2], uint64_t my) {
+	auto classify = [&](uint64_t tt, const HdrWords &h, const uint32_t pr[2], Src my) {
 		if constexpr (MODE == kModeProbe) {
 			/* gcl_access_probe: the words rx_one_pkt would read, folded, and
 			 * stored as the verdict is (no tables, hashes or histogram) */
 			if (ok(tt))
-				put_verdict_vf<VF>(k, tt * NT + tid,
-				                   h.d3 ^ h.d5 ^ h.d6 ^ h.d7 ^ h.d8 ^ h.d9 ^ (k.olflags ? pr[0] & 0xFF : 0u) ^
-				                           (k.rss ? pr[1] : 0u));
+				put(idx(tt), h.d3 ^ h.d5 ^ h.d6 ^ h.d7 ^ h.d8 ^ h.d9 ^ (k.olflags ? pr[0] & 0xFF : 0u) ^
+				                     (k.rss ? pr[1] : 0u));
 			return;
 		}
 		const uint32_t fl = k.olflags ? pr[0] & 0xFF : k.default_flags;
@@ -434,14 +531,12 @@ classify_pair_kernel(KParams k)
 		if constexpr (MODE != kModeProbe) {
 			if (lean_ok && __all(plain)) {
 				if (ok(tt))
-					put_verdict_vf<VF>(k, tt * NT + tid,
-					                   classify_lean<MODE, true>(k, h, tb, fl, pr[1], hist, tid, cnt));
+					put(idx(tt), classify_lean<MODE, true>(k, h, tb, fl, pr[1], hist, tid, cnt));
 			} else if (ok(tt)) {
 				const uint64_t i = tt * NT + tid;
 				/* this packet's frame offset, for the ARP target's extra read */
-				const uint64_t foff = (my >> 63) ? (my & ~kPairBytewise) : my - 8;
-				put_verdict_vf<VF>(k, i, classify_core<MODE, true, false, true, VF>(
-				                                 k, h, nullptr, tid, i, tb, hist, cnt, 0, 40, pr, foff));
+				put(i, classify_core<MODE, true, false, true, VF>(k, h, nullptr, tid, i, tb, hist, cnt, 0, 40, pr,
+				                                                   frame_off_of(my)));
 			}
 		}
 	};
@@ -451,11 +546,11 @@ classify_pair_kernel(KParams k)
 	uint32_t pra[2] = {0, 0}, prb[2] = {0, 0};
 	/* prologue: tiles t and t + step in flight, offsets of the two after */
 	uint64_t oa = ld_off(t), ob = ld_off(t + step);
-	uint64_t sa = src_of(t, oa);
+	Src sa = src_of(t, oa);
 	issue(sa, ra);
 	pref(t, pra);
 	oa = ld_off(t + 2 * step);
-	uint64_t sb = src_of(t + step, ob);
+	Src sb = src_of(t + step, ob);
 	issue(sb, rb);
 	pref(t + step, prb);
 	ob = ld_off(t + 3 * step);
@@ -463,7 +558,7 @@ classify_pair_kernel(KParams k)
 		asm volatile("" : "+s"(t));
 		HdrWords h;
 		unpack(ra, sa, h);
-		uint64_t my = sa;
+		Src my = sa;
 		sa = src_of(t + 2 * step, oa);
 		issue(sa, ra);
 		classify(t, h, pra, my);
@@ -603,6 +698,7 @@ struct Geometry {
 	int bpc_cap;  /* blocks per CU */
 	int grid;     /* blocks per launch when > 0 (gcl_tune.grid) */
 	bool pair;    /* classify_pair_kernel (GENERAL batches): [8, 40) per packet by lane pairs */
+	bool i32;     /* ... with 32-bit indices and offsets (pair_i32_ok) */
 	int defer;    /* classify_kernel with 1-/2-B verdicts kept in LDS (and past a full
 	                 buffer in kVregs registers per lane) and written in batches: 1 where
 	                 that takes <= 2 writes per block, 2 always (tests) */
@@ -645,10 +741,12 @@ static hipError_t launch_pair(const KParams &k, bool tlds, uint32_t lds, int num
 	 * unchanged (96.5-97.3 us, profiles/r03_ws_ab_vf2.jsonl): the loop is
 	 * not bound by them */
 	const bool v2 = (k.cflags & GCL_CFG_VERDICT2) != 0;
-	ClassifyFn fn = v2 ? (tlds ? classify_pair_kernel<MODE, true, NT, 2>
-	                           : classify_pair_kernel<MODE, false, NT, 2>)
-	                   : (tlds ? classify_pair_kernel<MODE, true, NT, 0>
-	                           : classify_pair_kernel<MODE, false, NT, 0>);
+#define GCL_PAIR(I) (v2 ? (tlds ? classify_pair_kernel<MODE, true, NT, 2, I> \
+	                        : classify_pair_kernel<MODE, false, NT, 2, I>) \
+	                : (tlds ? classify_pair_kernel<MODE, true, NT, 0, I> \
+	                        : classify_pair_kernel<MODE, false, NT, 0, I>))
+	ClassifyFn fn = geo.i32 ? GCL_PAIR(true) : GCL_PAIR(false);
+#undef GCL_PAIR
 	return launch_fn(fn, NT, k, lds, num_cus, geo.bpc_cap, geo.grid, s);
 }
 
@@ -700,6 +798,7 @@ static Geometry choose_geometry(const gcl_ctx *c, uint32_t tab_lds, uint32_t his
 	 * in round 5: the pair kernel beat both on every row, working set 96
 	 * vs 109-111 us, random pool 181 vs 189, profiles/r03_ws_ab.jsonl.) */
 	g.pair = general;
+	g.i32 = false; /* batch_launch decides */
 	g.defer = defer_ok ? tuned(c->tune.defer, kDefaultDefer) : 0;
 	auto per_block = [&](uint32_t nt) -> uint32_t {
 		if (g.pair)
@@ -870,6 +969,10 @@ static int batch_launch(gcl_ctx *c, const gcl_batch *b, const gcl_out *out, hipS
 	const bool defer_ok = !general && (k.cflags & (GCL_CFG_VERDICT1 | GCL_CFG_VERDICT2)) &&
 	                      ((uintptr_t)verdicts & 15) == 0 && b->n * 2 < (1ull << 32);
 	Geometry geo = choose_geometry(c, tlds ? tab_bytes : 0, hist_bytes, general, defer_ok);
+	/* the pair kernel's 32-bit form: frames (and the largest slot offset),
+	 * offsets, side arrays and verdicts each within 2 GiB */
+	geo.i32 = general && tuned(c->tune.pair_i32, kDefaultPairI32) && b->frames_len < (1ull << 31) - 64 &&
+	          b->n < (1ull << 28) && (b->offs || b->n * (uint64_t)b->stride <= (1ull << 31));
 
 	HipErr he;
 

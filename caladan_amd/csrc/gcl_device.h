@@ -11,6 +11,7 @@
 namespace gcl {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 /* 16-byte streaming load that does not keep the line (read-once frames) */
 __device__ __forceinline__ uint4 load16_nt(const void *p)

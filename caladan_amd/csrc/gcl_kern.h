@@ -575,6 +575,12 @@ __device__ __forceinline__ uint64_t classify_one(const KParams &k, const uint4 *
 	return classify_core<MODE, GENERAL, SYS, false>(k, h, tile, tid, idx, tb, hist, cnt, 0, avail, nullptr);
 }
 
+/* bytes per verdict of the context's format (KParams.cflags) */
+__device__ __forceinline__ uint32_t verdict_width(uint32_t cflags)
+{
+	return (cflags & GCL_CFG_VERDICT1) ? 1u : (cflags & GCL_CFG_VERDICT2) ? 2u : (cflags & GCL_CFG_VERDICT4) ? 4u : 8u;
+}
+
 /* Store verdict word @w (classify_one) of packet @idx in the context's
  * verdict format and store policy. */
 __device__ __forceinline__ void put_verdict(const KParams &k, uint64_t idx, uint64_t w);
@@ -676,5 +682,6 @@ constexpr int kDefaultTileLean = 1;
  * of nine interleaved pairs over three fresh processes
  * (profiles/r06_vstage_ab.jsonl) */
 constexpr int kDefaultVstage = 1;
+constexpr int kDefaultPairI32 = 1; /* gcl_tune.pair_i32 default */
 
 } // namespace gclk

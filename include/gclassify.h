@@ -452,6 +452,9 @@ struct gcl_tune {
 	int32_t vstage;          /* deferred verdicts: the register-held part of the last write
 	                            staged through LDS and stored 16 B per lane (1, default) or
 	                            stored a verdict per lane per tile (0) */
+	int32_t pair_i32;        /* classify_pair_kernel: batches within 2 GiB in 32-bit
+	                            arithmetic through buffer descriptors (1) */
+	uint32_t pad;
 	uint64_t loop_t0;        /* tickets start after loop_t0 (rounded down to a multiple of the
 	                            ring's slots): tests of the stamps' wrap */
 };

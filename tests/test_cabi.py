@@ -726,11 +726,11 @@ def test_tune_struct_and_defaults(g):
     stopped reading GCL_TUNE_* from the environment): the layout the header
     declares, every field GCL_TUNE_AUTO after gcl_tune_init, and
     gcl_ctx_tune refusing a NULL context."""
-    assert ctypes.sizeof(g.GclTune) == 88
+    assert ctypes.sizeof(g.GclTune) == 96
     t = g.make_tune()
-    assert t.size == 88 and t.loop_t0 == 0 and t.debug == 0
+    assert t.size == 96 and t.loop_t0 == 0 and t.debug == 0
     for name, _ in g.GclTune._fields_:
-        if name not in ("size", "loop_t0", "debug"):
+        if name not in ("size", "loop_t0", "debug", "pad"):
             assert getattr(t, name) == g.TUNE_AUTO, name
     t = g.make_tune(defer=2, threads=512, loop_phase=(120, 8, 1))
     assert (t.defer, t.threads, t.loop_phase_max, t.loop_phase_up, t.loop_phase_down) == (2, 512, 120, 8, 1)

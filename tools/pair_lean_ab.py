@@ -1,5 +1,6 @@
-"""A/B of classify_pair_kernel's lean path (gcl_tune.pair_lean: waves whose
-packets are all plain IPv4 take classify_lean) on bench.py's integrated
+"""A/B of a classify_pair_kernel knob (AB_KNOB, default pair_lean: waves
+whose packets are all plain IPv4 take classify_lean; pair_i32: the 32-bit
+form) at forms 0 and 1 on bench.py's integrated
 ingress row: the reference's 131072-mbuf pool (data at element + 344) placed
 in HBM against the verdict ring, 8 Mi descriptors with ol_flags and
 hash.rss, NIC mode, 2-B verdicts.  One context per form over the same
@@ -19,6 +20,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 from caladan_amd import gclassify as g  # noqa: E402
+
+KNOB = os.environ.get("AB_KNOB", "pair_lean")
 
 
 def pool(device, vb, cycles=64, P=g.IOKERNEL_NUM_MBUFS, ws=None):
@@ -55,7 +58,7 @@ def main():
         clfs = {}
         for f in (0, 1):
             clfs[f] = bench.classifier(dev, R, T, vb, hash_mode=g.HASH_NIC)
-            clfs[f].tune(pair_lean=f)
+            clfs[f].tune(**{KNOB: f})
             bench.setup_tables(clfs[f], R, T)
         ref = None
         for f, clf in clfs.items():
@@ -77,8 +80,7 @@ def main():
                     clf.classify(region, n, 0, verdicts=dv, counts=scratch[:R], stats=scratch[R:], offs=offs,
                                  olflags=olf, rss=rss, stream=st)
                 _, ms = bench.timed_launches(go, 20)
-                print(json.dumps({"row": row, "round": rnd, "form": f,
-                                  "what": "classify_lean waves" if f else "classify_core",
+                print(json.dumps({"row": row, "round": rnd, "form": f, "knob": KNOB,
                                   "kernel_us": round(ms * 1e3, 2),
                                   "gpkts": round(n / (ms * 1e-3) / 1e9, 2)}), flush=True)
         del region, dv, clfs

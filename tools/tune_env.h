@@ -6,7 +6,7 @@
  *
  *   GCL_TUNE_TABLES, _DEPTH, _THREADS, _GRID, _BLOCKS_PER_CU, _DEFER,
  *   _PAIR_LEAN, _TILE_LEAN, _LOOP64, _LOOP_LEAN, _LOOP_SPEC, _LOOP_PREFETCH,
- *   _REC_PREFETCH, _SLOT_PREFETCH, _VSTAGE  integers
+ *   _REC_PREFETCH, _SLOT_PREFETCH, _VSTAGE, _PAIR_I32  integers
  *   GCL_TUNE_LOOP_PHASE  "max[,up[,down]]" (ticks; up 16, down 1 by default)
  *   GCL_TUNE_LOOP_T0, GCL_TUNE_DEBUG
  */
@@ -44,6 +44,7 @@ static inline int tune_from_env(struct gcl_ctx *ctx)
 	tune_env_int("GCL_TUNE_REC_PREFETCH", &t.rec_prefetch);
 	tune_env_int("GCL_TUNE_SLOT_PREFETCH", &t.slot_prefetch);
 	tune_env_int("GCL_TUNE_VSTAGE", &t.vstage);
+	tune_env_int("GCL_TUNE_PAIR_I32", &t.pair_i32);
 	if (const char *e = getenv("GCL_TUNE_LOOP_PHASE")) {
 		unsigned m = 0, u = 16, d = 1;
 		if (sscanf(e, "%u,%u,%u", &m, &u, &d) >= 1) {
