@@ -80,7 +80,10 @@ def test_gpu_scenarios(g, s):
 @pytest.mark.parametrize("mode", [0, 1, 2])
 @pytest.mark.parametrize("flags", [0, 1, 2])
 @pytest.mark.parametrize("max_rt", [16, 1024, 4096])
-def test_gpu_fuzz_vs_oracle(g, orc, mode, flags, max_rt):
+@pytest.mark.parametrize("i32", [1, 0])
+def test_gpu_fuzz_vs_oracle(g, orc, mode, flags, max_rt, i32):
+    """i32: the pair kernel's 32-bit form (the default for batches within
+    2 GiB) or its 64-bit form (gcl_tune.pair_i32 = 0, what larger batches run)."""
     rng = np.random.default_rng(1000 * mode + 10 * flags + max_rt)
     rts = random_runtimes(rng, max_rt, min(max_rt, 40 if max_rt == 16 else 300))
     n = 5000
@@ -91,7 +94,7 @@ def test_gpu_fuzz_vs_oracle(g, orc, mode, flags, max_rt):
     cflags = flags | (g.CFG_TRANS_HASH if flags != 1 else 0)
     t = orc.Tables(max_rt, mode, cflags, 0x09, key)
     apply_runtimes(t, rts)
-    clf = g.Classifier(0, max_rt, mode, cflags, 0x09, key)
+    clf = g.Classifier(0, max_rt, mode, cflags, 0x09, key, tune={"pair_i32": i32})
     apply_runtimes(clf, rts)
     want_tr = cflags & g.CFG_TRANS_HASH
     if want_tr:
@@ -114,7 +117,8 @@ def test_gpu_fuzz_vs_oracle(g, orc, mode, flags, max_rt):
 
 @pytest.mark.parametrize("misalign", ["mbuf", "mixed", "lineend"])
 @pytest.mark.parametrize("mode", [0, 1])
-def test_gpu_fuzz_misaligned_offsets(g, orc, misalign, mode):
+@pytest.mark.parametrize("i32", [1, 0])
+def test_gpu_fuzz_misaligned_offsets(g, orc, misalign, mode, i32):
     """Frame offsets that are not 16-B aligned: 8-B aligned like mbuf data in
     the reference's ingress pool (element + 344, iokernel/defs.h:503-506),
     arbitrary byte shifts, and frames whose first 128-B line ends 40-56 bytes
@@ -127,13 +131,13 @@ def test_gpu_fuzz_misaligned_offsets(g, orc, misalign, mode):
         rng, n, rts, 1024, slot=256 if misalign == "lineend" else 128, misalign=misalign)
     t = orc.Tables(1024, mode, g.CFG_TRANS_HASH, 0x09)
     apply_runtimes(t, rts)
-    clf = g.Classifier(0, 1024, mode, g.CFG_TRANS_HASH, 0x09)
+    clf = g.Classifier(0, 1024, mode, g.CFG_TRANS_HASH, 0x09, tune={"pair_i32": i32})
     apply_runtimes(clf, rts)
     ve, ce, se, tre = t.classify(frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir_hi=fdir,
                                  frames_len=flen, dst_hint=hint, trans=True)
     v, c, st, tr = gpu_run(g, clf, frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir=fdir,
                            frames_len=flen, hint=hint, trans=True)
-    assert_same(v, ve, f"misalign={misalign} mode={mode}")
+    assert_same(v, ve, f"misalign={misalign} mode={mode} i32={i32}")
     assert (tr == tre).all() and (c == ce).all() and (st == se).all()
 
 
@@ -1180,7 +1184,7 @@ def test_gpu_ctx_tune_validation(g):
     bad = [g.make_tune(threads=300), g.make_tune(depth=3), g.make_tune(defer=3), g.make_tune(grid=0),
            g.make_tune(loop_phase=(2000, 1, 1)), g.make_tune(loop_phase=(10, 0, 0)), g.make_tune(loop_spec=-5),
            g.make_tune(rec_prefetch=65), g.make_tune(rec_prefetch=-2), g.make_tune(slot_prefetch=2),
-           g.make_tune(vstage=3)]
+           g.make_tune(vstage=3), g.make_tune(pair_i32=2)]
     half = g.make_tune()
     half.loop_phase_max = 50  # up / down left AUTO: the three go together
     bad.append(half)
@@ -1611,10 +1615,12 @@ def test_gpu_access_probe_pair_shape(g, vb, mode, side):
     clf.close()
 
 
-def test_gpu_offsets_at_the_top_of_u64(g, orc):
+@pytest.mark.parametrize("i32", [1, 0])
+def test_gpu_offsets_at_the_top_of_u64(g, orc, i32):
     """Offsets at and near 2^64 - 1 (the kernels' no-packet sentinel, ~0),
     2^63 and frames_len read as frames of zeros like any offset past the
-    buffer in the GENERAL kernel; gcl_classify refuses frames_len == ~0."""
+    buffer in the GENERAL kernel, in its 32- and 64-bit forms; gcl_classify
+    refuses frames_len == ~0."""
     kernel = "pair"
     rng = np.random.default_rng(9501)
     rts = random_runtimes(rng, 16, 12)
@@ -1626,11 +1632,11 @@ def test_gpu_offsets_at_the_top_of_u64(g, orc):
     offs[idx] = top[np.arange(300) % len(top)]
     t = orc.Tables(16, 1, 0, 0x09)
     apply_runtimes(t, rts)
-    clf = g.Classifier(0, 16, 1, 0, 0x09)
+    clf = g.Classifier(0, 16, 1, 0, 0x09, tune={"pair_i32": i32})
     apply_runtimes(clf, rts)
     ve, ce, se = t.classify(frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir_hi=fdir, frames_len=flen)
     v, c, st = gpu_run(g, clf, frames, n, 0, offs=offs, olflags=olf, rss=rss, fdir=fdir, frames_len=flen)
-    assert_same(v, ve, f"top-of-u64 offsets, {kernel}")
+    assert_same(v, ve, f"top-of-u64 offsets, {kernel} i32={i32}")
     assert (c == ce).all() and (st == se).all()
     import ctypes
     f, o = dev(frames), dev(offs.astype(np.int64))
