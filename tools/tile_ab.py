@@ -9,6 +9,7 @@ first use, AB_KNOB=stage: block- against wave-staged tiles,
 profiles/r06_stage_ab.jsonl; the wave form lost and was removed.)
 
     python tools/tile_ab.py [workload ...]     (default: udp64 tcp1500)
+    AB_VBYTES (verdict bytes), AB_HASH (jenkins | toeplitz | nic)
 One JSON line per (workload, round).
 """
 import json
@@ -24,6 +25,11 @@ import bench  # noqa: E402
 
 KNOB = os.environ.get("AB_KNOB", "tile_lean")
 FORMS = [int(x) for x in os.environ.get("AB_VALUES", "0,1").split(",")]
+# AB_FORMS: a JSON list of gcl_tune dicts instead (several knobs per form)
+TUNES = json.loads(os.environ["AB_FORMS"]) if os.environ.get("AB_FORMS") else None
+if TUNES:
+    KNOB = "form"
+    FORMS = list(range(len(TUNES)))
 
 
 def main():
@@ -31,11 +37,14 @@ def main():
     dev = torch.device("cuda", 0)
     reps = int(os.environ.get("AB_REPS", "30"))
     for name in wls:
-        w = bench.Workload(name, 0, 1, dev)
+        vb = int(os.environ["AB_VBYTES"]) if os.environ.get("AB_VBYTES") else None
+        w = bench.Workload(name, 0, 1, dev, vbytes=vb)
+        hmode = {"jenkins": bench.g.HASH_JENKINS, "toeplitz": bench.g.HASH_TOEPLITZ,
+                 "nic": bench.g.HASH_NIC}[os.environ.get("AB_HASH", "jenkins")]
         clfs = {}
         for f in FORMS:
-            clfs[f] = bench.classifier(dev, w.R, w.T, w.vbytes)
-            clfs[f].tune(**{KNOB: f})
+            clfs[f] = bench.classifier(dev, w.R, w.T, w.vbytes, hash_mode=hmode)
+            clfs[f].tune(**(TUNES[f] if TUNES else {KNOB: f}))
             bench.setup_tables(clfs[f], w.R, w.T)
         st = torch.cuda.current_stream().cuda_stream
         ref = None
@@ -50,7 +59,8 @@ def main():
             if ref is None:
                 ref = got
             ok = bool(torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1]))
-            print(json.dumps({"workload": name, KNOB: f, "check": "ok" if ok else "MISMATCH"}), flush=True)
+            print(json.dumps({"workload": name, KNOB: f, **({"tune": TUNES[f]} if TUNES else {}),
+                              "check": "ok" if ok else "MISMATCH"}), flush=True)
         out = torch.zeros(w.n * w.vbytes, dtype=torch.uint8, device=dev)
         alg = w.n * w.bytes_per_pkt
         for rnd in range(int(os.environ.get("AB_ROUNDS", "3"))):
