@@ -707,26 +707,32 @@ struct Geometry {
 /* geo.defer: what the CU's LDS leaves the block at geo.bpc_cap blocks per
  * CU holds k.vcap tiles of verdicts -- at most the block's share of the
  * batch, and only where that takes at most two writes per block */
+static bool plan_defer(const KParams &k, uint32_t &lds, int num_cus, const Geometry &geo, uint32_t nt,
+                       uint32_t &vcap, uint32_t &vregs)
+{
+	vcap = vregs = 0;
+	if (!geo.defer)
+		return false;
+	const uint32_t vb = (k.cflags & GCL_CFG_VERDICT1) ? 1 : 2;
+	const uint32_t base = align16(lds);
+	const uint32_t per_cu = 160 * 1024 / (uint32_t)std::max(geo.bpc_cap, 1);
+	const uint64_t blocks = geo.grid > 0 ? (uint64_t)geo.grid : (uint64_t)num_cus * std::max(geo.bpc_cap, 1);
+	const uint64_t want = ((k.n + nt - 1) / nt + blocks - 1) / blocks;
+	const uint64_t room = per_cu > base ? (per_cu - base) / (nt * vb) : 0;
+	const uint64_t rcap = kVregs * 4 / vb; /* tiles the registers hold past a full buffer */
+	if (!room || (2 * (room + rcap) < want && geo.defer != 2))
+		return false;
+	vcap = (uint32_t)std::min(want, room);
+	vregs = rcap && want > room;
+	lds = base + vcap * nt * vb;
+	return true;
+}
+
 template <int MODE, int DEPTH, int NT>
 static hipError_t launch_nt(KParams k, bool tlds, uint32_t lds, int num_cus, const Geometry &geo,
                             hipStream_t s)
 {
-	k.vcap = 0;
-	k.vregs = 0;
-	if (geo.defer) {
-		const uint32_t vb = (k.cflags & GCL_CFG_VERDICT1) ? 1 : 2;
-		const uint32_t base = align16(lds);
-		const uint32_t per_cu = 160 * 1024 / (uint32_t)std::max(geo.bpc_cap, 1);
-		const uint64_t blocks = geo.grid > 0 ? (uint64_t)geo.grid : (uint64_t)num_cus * std::max(geo.bpc_cap, 1);
-		const uint64_t want = ((k.n + NT - 1) / NT + blocks - 1) / blocks;
-		const uint64_t room = per_cu > base ? (per_cu - base) / (NT * vb) : 0;
-		const uint64_t rcap = kVregs * 4 / vb; /* tiles the registers hold past a full buffer */
-		if (room && (2 * (room + rcap) >= want || geo.defer == 2)) {
-			k.vcap = (uint32_t)std::min(want, room);
-			k.vregs = rcap && want > room;
-			lds = base + k.vcap * NT * vb;
-		}
-	}
+	plan_defer(k, lds, num_cus, geo, NT, k.vcap, k.vregs);
 	const ClassifyFn fn = tlds ? classify_kernel<MODE, true, DEPTH, NT> : classify_kernel<MODE, false, DEPTH, NT>;
 	return launch_fn(fn, NT, k, lds, num_cus, geo.bpc_cap, geo.grid, s);
 }
@@ -805,9 +811,16 @@ static Geometry choose_geometry(const gcl_ctx *c, uint32_t tab_lds, uint32_t his
 			return hist_bytes + tab_lds;
 		return nt * 64 + hist_bytes + tab_lds;
 	};
-	for (int nt = 256; nt <= 1024 && !g.threads; nt *= 2) {
+	/* dense slots: 512-lane tiles, two blocks per CU (one generation of
+	 * blocks over the chip), then 1024 x 1; GENERAL batches (the pair kernel,
+	 * no tile): 256 x 4.  Round 6 re-measured the dense shape with the lean
+	 * waves and the deferred verdicts: 2 x 512 at depth 1 307-318 us on
+	 * udp64 against 317-328 for round 5's 4 x 256 at depth 2, fastest in six
+	 * of six rounds (profiles/r06_geometry_ab.jsonl) */
+	static const int order_dense[] = {512, 1024, 256}, order_pair[] = {256, 512, 1024};
+	for (int nt : g.pair ? order_pair : order_dense) {
 		const uint32_t pb = per_block((uint32_t)nt);
-		if ((lanes_cu / nt) * pb <= lds_cu) {
+		if (!g.threads && (lanes_cu / nt) * pb <= lds_cu) {
 			g.threads = nt;
 			g.bpc_cap = (int)(lanes_cu / (uint32_t)nt);
 		}
@@ -821,7 +834,8 @@ static Geometry choose_geometry(const gcl_ctx *c, uint32_t tab_lds, uint32_t his
 		/* a second tile in flight per block: 1.1-1.7 % faster on udp64 at
 		 * 4 x 256 lanes (profiles/archive/r01_cbench_depth_*); at 2 x 512 lanes (the
 		 * 1024-runtime tables) 1 % on the 8 Mi header-split layout, 3.4 % at
-		 * 32 Mi, and no change on tcp1500 (profiles/archive/r01_hsplit_geometry.jsonl) */
+		 * 32 Mi, and no change on tcp1500 (profiles/archive/r01_hsplit_geometry.jsonl).
+		 * A block that defers its verdicts runs at depth 1 (batch_launch) */
 		g.depth = 2;
 	}
 	g.threads = tuned(c->tune.threads, g.threads);
@@ -969,6 +983,16 @@ static int batch_launch(gcl_ctx *c, const gcl_batch *b, const gcl_out *out, hipS
 	const bool defer_ok = !general && (k.cflags & (GCL_CFG_VERDICT1 | GCL_CFG_VERDICT2)) &&
 	                      ((uintptr_t)verdicts & 15) == 0 && b->n * 2 < (1ull << 32);
 	Geometry geo = choose_geometry(c, tlds ? tab_bytes : 0, hist_bytes, general, defer_ok);
+	if (!general && geo.depth == 2 && c->tune.depth == GCL_TUNE_AUTO && b->stride <= GCL_HDR_GRANULE) {
+		/* a block that keeps its verdicts until after its reads streams a
+		 * dense slab best with one tile in flight (udp64 1-B at 2 x 512:
+		 * 307-318 against 308-319 us at depth 2, profiles/r06_geometry_ab.jsonl);
+		 * per-packet stores, and headers one per line of a wide slot
+		 * (tcp1500: depth 1 3 % slower), keep two */
+		uint32_t l = (uint32_t)geo.threads * 64 + hist_bytes + (tlds ? tab_bytes : 0), vc, vr;
+		if (plan_defer(k, l, c->num_cus, geo, (uint32_t)geo.threads, vc, vr))
+			geo.depth = 1;
+	}
 	/* the pair kernel's 32-bit form: frames (and the largest slot offset),
 	 * offsets, side arrays and verdicts each within 2 GiB */
 	geo.i32 = general && tuned(c->tune.pair_i32, kDefaultPairI32) && b->frames_len < (1ull << 31) - 64 &&
