@@ -22,6 +22,8 @@ import bench  # noqa: E402
 from caladan_amd import gclassify as g  # noqa: E402
 
 KNOB = os.environ.get("AB_KNOB", "pair_lean")
+# AB_FORMS: a JSON list of gcl_tune dicts instead (several knobs per form)
+TUNES = json.loads(os.environ["AB_FORMS"]) if os.environ.get("AB_FORMS") else [{KNOB: 0}, {KNOB: 1}]
 
 
 def pool(device, vb, cycles=64, P=g.IOKERNEL_NUM_MBUFS, ws=None):
@@ -56,9 +58,9 @@ def main():
     for row, ws in (("random_pool", None), ("working_set", 4096)):
         region, dv, offs, olf, rss, n, R, T = pool(dev, vb, ws=ws)
         clfs = {}
-        for f in (0, 1):
+        for f, tn in enumerate(TUNES):
             clfs[f] = bench.classifier(dev, R, T, vb, hash_mode=g.HASH_NIC)
-            clfs[f].tune(**{KNOB: f})
+            clfs[f].tune(**tn)
             bench.setup_tables(clfs[f], R, T)
         ref = None
         for f, clf in clfs.items():
@@ -80,7 +82,7 @@ def main():
                     clf.classify(region, n, 0, verdicts=dv, counts=scratch[:R], stats=scratch[R:], offs=offs,
                                  olflags=olf, rss=rss, stream=st)
                 _, ms = bench.timed_launches(go, 20)
-                print(json.dumps({"row": row, "round": rnd, "form": f, "knob": KNOB,
+                print(json.dumps({"row": row, "round": rnd, "form": f, "tune": TUNES[f],
                                   "kernel_us": round(ms * 1e3, 2),
                                   "gpkts": round(n / (ms * 1e-3) / 1e9, 2)}), flush=True)
         del region, dv, clfs
