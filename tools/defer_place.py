@@ -30,7 +30,8 @@ def main():
     clfs = {}
     for f in (0, 1):
         fl, tb = bench.verdict_cfg(vb, R, T)
-        clfs[f] = g.Classifier(0, R, g.HASH_JENKINS, fl, thread_bits=tb, tune={"defer": f})
+        # form 1: every default (deferred verdicts and the round-6 geometry)
+        clfs[f] = g.Classifier(0, R, g.HASH_JENKINS, fl, thread_bits=tb, tune={"defer": 0} if f == 0 else {})
         bench.setup_tables(clfs[f], R, T)
     st = torch.cuda.current_stream().cuda_stream
     keep = []
@@ -52,8 +53,11 @@ def main():
                     clf.classify(pool, n, stride, verdicts=ring, counts=scratch[:R], stats=scratch[R:], stream=st)
                 _, ms = bench.timed_launches(go, 10)
                 row.setdefault(f"defer{f}_us", []).append(round(ms * 1e3, 1))
-        probe = bench.ceiling(clfs[0], pool, n, stride, ring, 0.33)
-        row["access_probe_us"] = round(probe.get("ceiling_ms", 0) * 1e3, 1)
+        probe = bench.ceiling(clfs[1], pool, n, stride, ring, 0.33)
+        row["kernel_shape_probe_us"] = round(probe.get("ceiling_ms", 0) * 1e3, 1)
+        # the placement criterion (gcl_dev_alloc_paired): the minimal shape
+        mp = bench.ceiling(clfs[0], pool, n, stride, ring, 0.33, minimal=True)
+        row["access_probe_us"] = round(mp.get("ceiling_ms", 0) * 1e3, 1)
         print(json.dumps(row), flush=True)
         keep.append(pool)
 
