@@ -180,7 +180,9 @@ def compact(result, detail_path=DETAIL_PATH):
             out[k] = result[k]
     if "placement" in result:
         p = result["placement"]
-        out["placement"] = _pick(p, "probe_us_chosen", "classes_seen", "replaced")
+        out["placement"] = _pick(p, "policy", "probe_us_chosen", "classes_seen", "replaced")
+        if "policy" in out["placement"] and "probe_us_chosen" in out["placement"]:
+            del out["placement"]["policy"]  # placed: the probe figures say so
     cpu = result.get("cpu_baseline")
     if cpu:
         out["cpu_baseline"] = {**_pick(cpu, "value", "unit", "cores", "kind", "sample", "pinning",
@@ -368,10 +370,16 @@ class Workload:
             self.verdicts = torch.empty(n * vbytes, dtype=torch.uint8, device=device)
         else:  # library-owned hipMalloc (gcl_dev_alloc), zeroed
             # the verdict ring first, then the frame pool placed against it
-            # (gcl_dev_alloc_paired: DESIGN.md §4 "Buffer placement");
-            # GCL_BENCH_PLACEMENT=0 allocates both plainly, for the A/B
+            # (gcl_dev_alloc_paired: DESIGN.md §4 "Buffer placement") where
+            # the kernel stores a verdict per packet (4-/8-B verdicts: placed
+            # 344 against 389 us plain, profiles/r06_placement_ab.jsonl); a
+            # dense slab with 1-/2-B verdicts defers them until after its
+            # reads, which takes the placement class away, and a plain pool
+            # runs faster (udp64 316-320 placed against 307-308 plain, tcp1500
+            # 176-179 against 171-172).  GCL_BENCH_PLACEMENT=0 / 1 forces it
             self.verdicts = g.DeviceBuffer(n * vbytes, device.index or 0)
-            self.paired = os.environ.get("GCL_BENCH_PLACEMENT", "1") != "0"
+            env = os.environ.get("GCL_BENCH_PLACEMENT")
+            self.paired = env != "0" if env is not None else vbytes > 2
             self.frames = self._new_pool()
         self.counts = torch.zeros(R + g.NR_STATS, dtype=torch.int64, device=device)
 
@@ -917,7 +925,8 @@ def placement(w):
     (gcl_dev_alloc_paired: DESIGN.md §4 "Buffer placement")."""
     info = getattr(w.frames, "pair_info", None)
     if info is None:
-        return {"policy": "plain hipMalloc"}
+        return {"policy": "plain hipMalloc (gcl_dev_alloc): the kernel defers its 1-/2-B verdicts, "
+                          "which takes the placement class away"}
     checks = getattr(w, "placement_checks", [])
     return {"policy": "gcl_dev_alloc_paired (frame pool placed against the verdict ring)",
             **info,
