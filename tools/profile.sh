@@ -16,7 +16,7 @@ run_cmd() { # workload, vbytes, steps -> the program and its arguments
   elif [ "$1" = ingress_ws ]; then
     echo "python3 tools/ingress_run.py $3 --ws-only"
   else
-    echo "python3 bench.py --workload $1 --verdict-bytes $2 --no-cpu --no-secondary --no-e2e --no-group --steps $3 --warmup 1"
+    echo "python3 bench.py --workload $1 --verdict-bytes $2 --no-cpu --no-secondary --no-e2e --no-group --steps $3 --warmup ${WARMUP:-100}"
   fi
 }
 for vb in ${VBS:-2 4 8}; do
