@@ -569,6 +569,11 @@ class Exchange:
 
 # GPU time of continuous steps (warmup + settle) before the timed region
 SETTLE_MS = float(os.environ.get("GCL_BENCH_SETTLE_MS", "30"))
+# the shortest timed window of timed_launches: its wall clock also holds the
+# queue's fill before the first launch and the wake-up after the last (~60 us
+# together), which 10 launches of a 56-us kernel bill at 6 us each (r06ah:
+# the ingress working set 62.1 us per launch by the wall, 56.1 by events)
+WINDOW_MS = float(os.environ.get("GCL_BENCH_WINDOW_MS", "10"))
 
 
 def run_timed(w, steps, warmup, world, ex=None):
@@ -1228,9 +1233,10 @@ def rxloop_bench(device, vbytes, iters=2000, rounds=3):
 
 
 def timed_launches(fn, reps):
-    """(wall s, GPU ms) per call of `fn` over `reps` back-to-back calls on the
-    current stream, after untimed calls covering SETTLE_MS (the settle phase
-    of run_timed)."""
+    """(wall s, GPU ms) per call of `fn` over at least `reps` back-to-back
+    calls on the current stream -- more where `reps` calls would take less
+    than WINDOW_MS -- after untimed calls covering SETTLE_MS (the settle
+    phase of run_timed)."""
     t0 = time.perf_counter()
     fn()
     torch.cuda.synchronize()
@@ -1238,6 +1244,13 @@ def timed_launches(fn, reps):
     for _ in range(int(SETTLE_MS / est_ms) + 1):
         fn()
     torch.cuda.synchronize()
+    # the settle phase's own rate, without the single call's sync latency
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    torch.cuda.synchronize()
+    est_ms = max((time.perf_counter() - t0) * 1e3 / reps, 1e-3)
+    reps = max(reps, int(WINDOW_MS / est_ms))
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()

@@ -398,7 +398,11 @@ classify_pair_kernel(KParams k)
 	const uint32_t vbytes = VF ? VF : verdict_width(k.cflags);
 	const __amdgpu_buffer_rsrc_t rs_v = gcl::host_rsrc(k.verdicts, I32 ? vbytes * k.n : 16);
 	const uint32_t flen32 = (uint32_t)k.frames_len, n32 = (uint32_t)k.n;
+	const uint32_t nt32 = (uint32_t)k.ntiles; /* I32: n < 2^28, so every tile index fits */
 	const uint32_t fbase3 = (uint32_t)(uintptr_t)k.frames & 3;
+	/* I32 pair_src: [off + 8, off + 40) fits below frames_len iff off <= fit_lim */
+	const bool fit_any = flen32 >= 40;
+	const uint32_t fit_lim = fit_any ? flen32 - 40 : 0u;
 	const uint32_t half16 = 16u * (uint32_t)(tid & 1);
 	auto idx = [&](uint64_t tt) -> uint64_t {
 		if constexpr (I32)
@@ -407,8 +411,8 @@ classify_pair_kernel(KParams k)
 			return tt * NT + tid;
 	};
 	auto ok = [&](uint64_t tt) {
-		if constexpr (I32)
-			return tt < k.ntiles && (uint32_t)idx(tt) < n32;
+		if constexpr (I32) /* 32-bit compares: the tile test stays scalar */
+			return (uint32_t)tt < nt32 && (uint32_t)idx(tt) < n32;
 		else
 			return tt < k.ntiles && tt * NT + tid < k.n;
 	};
@@ -430,9 +434,10 @@ classify_pair_kernel(KParams k)
 			 * kBw32 | off never meet each other or kNoOff32 */
 			const uint32_t off = k.offs ? (raw < k.frames_len ? (uint32_t)raw : flen32)
 			                            : (uint32_t)idx(tt) * (uint32_t)k.stride;
-			const bool in = off < flen32;
-			const bool fits = in && flen32 - off >= 40 && ((fbase3 + off) & 3) == 0;
-			const uint32_t my = fits ? off + 8 : kBw32 | (in ? off : flen32);
+			/* bitwise, not short-circuit: straight-line selects, no exec-mask
+			 * branches; off <= fit_lim implies off < frames_len */
+			const bool fits = fit_any & (off <= fit_lim) & (((fbase3 + off) & 3) == 0);
+			const uint32_t my = fits ? off + 8 : kBw32 | __builtin_elementwise_min(off, flen32);
 			return ok(tt) ? my : kNoOff32;
 		} else {
 			return pair_src(k, !ok(tt) ? kNoOff : k.offs ? user_off(k, raw) : (tt * NT + tid) * k.stride);
@@ -453,8 +458,11 @@ classify_pair_kernel(KParams k)
 	};
 	/* load J of this lane: half (lane & 1) of the pair's packet J */
 	auto load32 = [&](uint32_t s) -> uint4 {
-		const uint32_t a = (s >> 31) ? 0u : s + half16;
-		const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs_fr, (int)a, 0, 0);
+		/* s with its top bit set (bytewise, or no packet) needs no select:
+		 * kBw32 | o + 16 lies past frames_len (< 2^31 - 64), where the
+		 * descriptor's range check returns zeros, and kNoOff32 + 16 wraps to
+		 * 15, an in-range read nothing uses */
+		const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs_fr, (int)(s + half16), 0, 0);
 		return make_uint4(v[0], v[1], v[2], v[3]);
 	};
 	auto issue = [&](Src my, uint4 r[2]) {
@@ -531,7 +539,7 @@ classify_pair_kernel(KParams k)
 		if constexpr (MODE != kModeProbe) {
 			if (lean_ok && __all(plain)) {
 				if (ok(tt))
-					put(idx(tt), classify_lean<MODE, true>(k, h, tb, fl, pr[1], hist, tid, cnt));
+					put(idx(tt), classify_lean<MODE, true, false, VF>(k, h, tb, fl, pr[1], hist, tid, cnt));
 			} else if (ok(tt)) {
 				const uint64_t i = tt * NT + tid;
 				/* this packet's frame offset, for the ARP target's extra read */
@@ -554,7 +562,7 @@ classify_pair_kernel(KParams k)
 	issue(sb, rb);
 	pref(t + step, prb);
 	ob = ld_off(t + 3 * step);
-	while (t < k.ntiles) {
+	while (I32 ? (uint32_t)t < nt32 : t < k.ntiles) {
 		asm volatile("" : "+s"(t));
 		HdrWords h;
 		unpack(ra, sa, h);

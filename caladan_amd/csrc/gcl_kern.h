@@ -502,7 +502,8 @@ __device__ __forceinline__ uint64_t classify_core(const KParams &k, const HdrWor
  * than hand its runtime to the loop's writer wave in @hist[tid] */
 /* DRAIN (classify_kernel's dense slots): dense_drain() before the IP
  * lookup, where classify_core drains */
-template <int MODE, bool HIST = false, bool DRAIN = false>
+/* VF: the verdict format where the caller knows it (1 / 2 B), else 0 */
+template <int MODE, bool HIST = false, bool DRAIN = false, int VF = 0>
 __device__ __forceinline__ uint64_t classify_lean(const KParams &k, const HdrWords &h, const Tables &tb,
                                                   uint32_t flags, uint32_t rss, uint32_t *hist, int tid,
                                                   Counters &cnt)
@@ -545,9 +546,9 @@ __device__ __forceinline__ uint64_t classify_lean(const KParams &k, const HdrWor
 	if (!HIST)
 		hist[tid] = (uint32_t)p;
 	const uint32_t q = uniq << (k.cflags >> 24) | thr;
-	if (k.cflags & GCL_CFG_VERDICT1)
+	if (VF == 1 || (VF == 0 && (k.cflags & GCL_CFG_VERDICT1)))
 		return miss ? GCL_V1_OTHER | GCL_ACT_DROP_UNREG : q;
-	if (k.cflags & GCL_CFG_VERDICT2)
+	if (VF == 2 || (VF == 0 && (k.cflags & GCL_CFG_VERDICT2)))
 		return miss ? GCL_V2_OTHER | GCL_ACT_DROP_UNREG : action == GCL_ACT_WAKE ? GCL_V2_WAKE | q : q;
 	const uint32_t vlo = uniq | thr << 16 | action << 24;
 	if (k.cflags & GCL_CFG_VERDICT4)
