@@ -149,7 +149,7 @@ def _pick(d, *keys):
 
 def _roof(r, *extra):
     return _pick(r, "bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_source",
-                 "kernel_ms", "bytes_per_pkt", "ceiling_ms", "frac_of_ceiling", *extra)
+                 "kernel_ms", "bytes_per_pkt", "ceiling_ms", "frac_of_ceiling", "read_sol", *extra)
 
 
 def _cpu_mode(m):
@@ -898,8 +898,25 @@ def pmc_traffic(name, vbytes, kernel_ms=None, scale=1.0):
     return traffic * scale, label
 
 
+READ_SOL_PATH = "profiles/r06_read_sol.jsonl"
+
+
+def read_sol():
+    """The HBM read speed of light measured on an MI355X box (tools/read_sol:
+    the fastest of 81 pure streaming-read shapes over a 2 GiB slab, the
+    udp64 slab's size), from the committed file; None without it."""
+    try:
+        with open(os.path.join(ROOT, READ_SOL_PATH)) as f:
+            last = json.loads(f.read().strip().splitlines()[-1])
+        return float(last["best_GBs"])
+    except (OSError, ValueError, KeyError, IndexError):
+        return None
+
+
 def roofline_obj(bytes_per_launch, kernel_ms, traffic, extra=None, bound="hbm", peak=HBM_PEAK_GBS):
-    """@traffic: None, or (bytes, source label) from pmc_traffic."""
+    """@traffic: None, or (bytes, source label) from pmc_traffic.  An HBM-bound
+    row also gets `read_sol`: its algorithmic rate over the measured read
+    speed of light (read_sol)."""
     traffic, source = traffic if isinstance(traffic, tuple) else (traffic, None)
     achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
     r = {"bound": bound, "achieved": round(achieved, 1), "peak": peak, "unit": "GB/s",
@@ -907,6 +924,10 @@ def roofline_obj(bytes_per_launch, kernel_ms, traffic, extra=None, bound="hbm", 
          "kernel_ms": round(kernel_ms, 4)}
     if source:
         r["traffic_source"] = source
+    sol = read_sol() if bound == "hbm" else None
+    if sol:
+        r["read_sol"] = {"GBs": sol, "frac": round(achieved / sol, 4),
+                         "src": f"{READ_SOL_PATH}: committed tools/read_sol run, not this process"}
     if extra:
         r.update(extra)
     if traffic:
