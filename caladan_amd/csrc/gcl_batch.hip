@@ -78,8 +78,17 @@ classify_kernel(KParams k)
 
 	Counters cnt = {0, 0, 0, 0};
 	uint4 ra[4], rb[4];
-	uint64_t t = blockIdx.x;
-	const uint64_t step = gridDim.x, t_end = k.ntiles;
+	/* tiles first, first + step, ... before t_end: dealt round-robin (the
+	 * whole chip sweeps one window of the batch), or with k.contig one run
+	 * of ceil(ntiles / G) tiles per block (each block streams its own part) */
+	uint64_t first = blockIdx.x, step = gridDim.x, t_end = k.ntiles;
+	if (k.contig) {
+		const uint64_t per = (k.ntiles + gridDim.x - 1) / gridDim.x;
+		first = (uint64_t)blockIdx.x * per;
+		step = 1;
+		t_end = std::min(first + per, k.ntiles);
+	}
+	uint64_t t = first;
 	/* k.vcap (1-/2-B verdicts): each tile's verdicts kept in LDS after the
 	 * tables -- and with k.vregs, once vcap tiles are in, the next ones in a
 	 * shift register of kVregs dwords per lane -- and written out when both
@@ -119,7 +128,7 @@ classify_kernel(KParams k)
 	const uint64_t nb = k.n * vb;
 	/* the global byte offset of local tile @j's first verdict */
 	auto tile_off = [&](uint32_t j) -> uint64_t {
-		return ((uint64_t)blockIdx.x + (uint64_t)j * step) * NT * vb;
+		return (first + (uint64_t)j * step) * NT * vb;
 	};
 	/* the buffer to its places, 16 B per lane, write-through like the
 	 * per-packet stores; the batch's last tile up to n only */
@@ -980,6 +989,7 @@ static int batch_launch(gcl_ctx *c, const gcl_batch *b, const gcl_out *out, hipS
 	k.plean = (uint32_t)tuned(c->tune.pair_lean, kDefaultPairLean);
 	k.tlean = (uint32_t)tuned(c->tune.tile_lean, kDefaultTileLean);
 	k.vstage = (uint32_t)tuned(c->tune.vstage, kDefaultVstage);
+	k.contig = (uint32_t)tuned(c->tune.tile_order, kDefaultTileOrder);
 	k.default_flags = c->cfg.default_olflags;
 
 	/* the specialised fast path needs every header granule in range */

@@ -426,7 +426,7 @@ extern "C" void gcl_tune_init(struct gcl_tune *t)
 	t->defer = t->pair_lean = t->tile_lean = GCL_TUNE_AUTO;
 	t->loop64 = t->loop_lean = t->loop_spec = t->loop_prefetch = GCL_TUNE_AUTO;
 	t->loop_phase_max = t->loop_phase_up = t->loop_phase_down = GCL_TUNE_AUTO;
-	t->rec_prefetch = t->slot_prefetch = t->vstage = t->pair_i32 = GCL_TUNE_AUTO;
+	t->rec_prefetch = t->slot_prefetch = t->vstage = t->pair_i32 = t->tile_order = GCL_TUNE_AUTO;
 	t->loop_t0 = 0;
 	t->debug = 0;
 }
@@ -446,7 +446,8 @@ static bool tune_valid(const struct gcl_tune *t)
 	       in(t->grid, 1, 1 << 20) && in(t->blocks_per_cu, 1, 64) && in(t->defer, 0, 2) &&
 	       flag(t->pair_lean) && flag(t->tile_lean) && flag(t->loop64) && flag(t->loop_lean) && in(t->loop_spec, 0, 100000000) &&
 	       flag(t->loop_prefetch) && (ph_auto || ph_set) && t->debug <= 1 && in(t->rec_prefetch, 0, 64) &&
-	       flag(t->slot_prefetch) && flag(t->vstage) && flag(t->pair_i32);
+	       flag(t->slot_prefetch) && flag(t->vstage) && flag(t->pair_i32) &&
+	       flag(t->tile_order);
 }
 
 extern "C" int gcl_ctx_tune(struct gcl_ctx *c, const struct gcl_tune *t)

@@ -90,6 +90,7 @@ struct KParams {
 	uint32_t plean;  /* classify_pair_kernel: plain-IPv4 waves on classify_lean */
 	uint32_t tlean;  /* classify_kernel: plain-IPv4 waves on classify_lean */
 	uint32_t vstage; /* classify_kernel: the last register flush staged through LDS */
+	uint32_t contig; /* classify_kernel: a contiguous run of tiles per block */
 };
 
 /* classify_kernel's verdict registers: kVregs dwords per lane, so 4 * kVregs
@@ -684,5 +685,10 @@ constexpr int kDefaultTileLean = 1;
  * (profiles/r06_vstage_ab.jsonl) */
 constexpr int kDefaultVstage = 1;
 constexpr int kDefaultPairI32 = 1; /* gcl_tune.pair_i32 default */
+/* gcl_tune.tile_order default: round-robin.  One contiguous run per block --
+ * the order tools/read_sol's fastest pure reads use (7.21 against 6.87 TB/s)
+ * -- made udp64 307.0-308.7 -> 334.5-339.3 us and its probe the same way,
+ * tcp1500 1 % slower (profiles/r06_tile_order_ab.jsonl) */
+constexpr int kDefaultTileOrder = 0;
 
 } // namespace gclk

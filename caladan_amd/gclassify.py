@@ -145,7 +145,7 @@ class GclTune(ctypes.Structure):
                 ("loop_phase_down", ctypes.c_int32), ("loop_prefetch", ctypes.c_int32),
                 ("debug", ctypes.c_uint32), ("rec_prefetch", ctypes.c_int32),
                 ("slot_prefetch", ctypes.c_int32), ("vstage", ctypes.c_int32), ("pair_i32", ctypes.c_int32),
-                ("pad", ctypes.c_uint32), ("loop_t0", ctypes.c_uint64)]
+                ("tile_order", ctypes.c_int32), ("loop_t0", ctypes.c_uint64)]
 
 
 TUNE_AUTO = -1

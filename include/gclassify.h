@@ -454,7 +454,8 @@ struct gcl_tune {
 	                            stored a verdict per lane per tile (0) */
 	int32_t pair_i32;        /* classify_pair_kernel: batches within 2 GiB in 32-bit
 	                            arithmetic through buffer descriptors (1) */
-	uint32_t pad;
+	int32_t tile_order;      /* classify_kernel: tiles dealt round-robin over the blocks (0)
+	                            or one contiguous run of tiles per block (1) */
 	uint64_t loop_t0;        /* tickets start after loop_t0 (rounded down to a multiple of the
 	                            ring's slots): tests of the stamps' wrap */
 };

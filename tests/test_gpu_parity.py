@@ -353,7 +353,14 @@ def test_gpu_dense_narrow_verdicts(g, orc, wl, R, T, vb, defer, lean):
     # the last register flush staged through the LDS buffer (gcl_tune.vstage)
     (1, {"vstage": 1}), (1, {"vstage": 1, "grid": 40}), (1, {"vstage": 1, "grid": 20}),
     (1, {"vstage": 1, "grid": 40, "depth": 1}), (2, {"vstage": 1, "threads": 512, "grid": 7}),
-    (1, {"vstage": 0, "grid": 40})])
+    (1, {"vstage": 0, "grid": 40}),
+    # one contiguous run of tiles per block (gcl_tune.tile_order): the buffer
+    # and register flushes land on the block's own run; grid 301 leaves the
+    # last blocks without a tile; defer 0 stores every verdict as it goes
+    (1, {"tile_order": 1}), (2, {"tile_order": 1, "grid": 3}), (1, {"tile_order": 1, "grid": 40}),
+    (1, {"tile_order": 1, "grid": 20, "depth": 1}), (2, {"tile_order": 1, "threads": 512, "grid": 7}),
+    (1, {"tile_order": 1, "blocks_per_cu": 1, "grid": 301}), (0, {"tile_order": 1, "grid": 20}),
+    (1, {"tile_order": 0})])
 @pytest.mark.parametrize("vb", [1, 2])
 def test_gpu_dense_deferred_flushes(g, orc, vb, defer, env):
     """The tile kernel's LDS verdict buffer when a block walks more tiles
@@ -1184,7 +1191,7 @@ def test_gpu_ctx_tune_validation(g):
     bad = [g.make_tune(threads=300), g.make_tune(depth=3), g.make_tune(defer=3), g.make_tune(grid=0),
            g.make_tune(loop_phase=(2000, 1, 1)), g.make_tune(loop_phase=(10, 0, 0)), g.make_tune(loop_spec=-5),
            g.make_tune(rec_prefetch=65), g.make_tune(rec_prefetch=-2), g.make_tune(slot_prefetch=2),
-           g.make_tune(vstage=3), g.make_tune(pair_i32=2)]
+           g.make_tune(vstage=3), g.make_tune(pair_i32=2), g.make_tune(tile_order=2)]
     half = g.make_tune()
     half.loop_phase_max = 50  # up / down left AUTO: the three go together
     bad.append(half)
