@@ -61,12 +61,8 @@ classify_kernel(KParams k)
 	 * memory counter too, so every table lookup would wait for the frame
 	 * loads in flight */
 	const uint8_t *tab = TLDS ? lds_tab : k.tables;
-	if (TLDS) {
-		const uint4 *src = (const uint4 *)k.tables;
-		uint4 *dst = (uint4 *)lds_tab;
-		for (uint32_t i = tid; i < k.tables_lds_bytes / 16; i += NT)
-			dst[i] = src[i];
-	}
+	if (TLDS)
+		stage_tables<NT>(lds_tab, k.tables, k.tables_lds_bytes);
 	Tables tb;
 	tb.ipt = (const uint2 *)tab;
 	tb.rtab = (const RtEntry *)(tab + k.off_rt);
@@ -377,12 +373,8 @@ classify_pair_kernel(KParams k)
 	for (uint32_t i = tid; i < k.max_rt; i += NT)
 		hist[i] = 0;
 	const uint8_t *tab = TLDS ? lds_tab : k.tables;
-	if (TLDS) {
-		const uint4 *src = (const uint4 *)k.tables;
-		uint4 *dst = (uint4 *)lds_tab;
-		for (uint32_t i = tid; i < k.tables_lds_bytes / 16; i += NT)
-			dst[i] = src[i];
-	}
+	if (TLDS)
+		stage_tables<NT>(lds_tab, k.tables, k.tables_lds_bytes);
 	Tables tb;
 	tb.ipt = (const uint2 *)tab;
 	tb.rtab = (const RtEntry *)(tab + k.off_rt);
@@ -1012,6 +1004,16 @@ static int batch_launch(gcl_ctx *c, const gcl_batch *b, const gcl_out *out, hipS
 		uint32_t l = (uint32_t)geo.threads * 64 + hist_bytes + (tlds ? tab_bytes : 0), vc, vr;
 		if (plan_defer(k, l, c->num_cus, geo, (uint32_t)geo.threads, vc, vr))
 			geo.depth = 1;
+	}
+	if (!general && b->stride > GCL_HDR_GRANULE && geo.threads == 512 && c->tune.threads == GCL_TUNE_AUTO &&
+	    c->tune.depth == GCL_TUNE_AUTO) {
+		/* wide slots (one header per 128-B line or more): 256-lane tiles at
+		 * depth 1, still two blocks per CU -- 512 lines (64 KiB) in flight
+		 * per CU, what the dense 2 x 512 shape keeps at 64 B per header,
+		 * instead of 2048: tcp1500 172.3-173.2 -> 164.8-165.7 us, and
+		 * 166.5 at depth 2 (profiles/r06_wide_geometry_ab.jsonl) */
+		geo.threads = 256;
+		geo.depth = 1;
 	}
 	/* the pair kernel's 32-bit form: frames (and the largest slot offset),
 	 * offsets, side arrays and verdicts each within 2 GiB */

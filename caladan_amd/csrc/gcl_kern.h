@@ -94,7 +94,10 @@ struct KParams {
 };
 
 /* classify_kernel's verdict registers: kVregs dwords per lane, so 4 * kVregs
- * tiles of 1-B verdicts (2 * kVregs of 2-B ones) past a full LDS buffer */
+ * tiles of 1-B verdicts (2 * kVregs of 2-B ones) past a full LDS buffer.  16
+ * (one write per block for the 1024-runtime contexts, not two) measured
+ * slower: tcp1500 +2.5 %, header split +2 %, udp64 unchanged
+ * (profiles/r06_vregs16_ab.jsonl) */
 constexpr int kVregs = 10;
 
 /* ------------------------------------------------------------------------
@@ -617,6 +620,33 @@ __device__ __forceinline__ void put_verdict(const KParams &k, uint64_t idx, uint
 		store_wt((uint32_t *)k.verdicts + idx, (uint32_t)w);
 	else
 		store_wt((uint64_t *)k.verdicts + idx, w);
+}
+
+/* The table image into LDS at a batch kernel's start: each lane issues all
+ * eight 16-B loads of a round (128 B x NT per block) before its first LDS
+ * store, so staging the 1024-runtime tables (37 KiB) at 512 lanes costs one
+ * L2 round trip, not one per 16 B x NT (five, each waited for before its store) */
+template <int NT>
+__device__ __forceinline__ void stage_tables(uint8_t *lds_tab, const uint8_t *tables, uint32_t bytes)
+{
+	constexpr int U = 8;
+	const uint4 *src = (const uint4 *)tables;
+	uint4 *dst = (uint4 *)lds_tab;
+	const uint32_t n16 = bytes / 16;
+	for (uint32_t base = 0; base < n16; base += U * NT) {
+		uint4 r[U];
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			const uint32_t i = base + u * NT + threadIdx.x;
+			r[u] = src[i < n16 ? i : 0]; /* every load issued, in range */
+		}
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			const uint32_t i = base + u * NT + threadIdx.x;
+			if (i < n16)
+				dst[i] = r[u];
+		}
+	}
 }
 
 template <int NT>
