@@ -822,18 +822,25 @@ static Geometry choose_geometry(const gcl_ctx *c, uint32_t tab_lds, uint32_t his
 	};
 	/* dense slots: 512-lane tiles, two blocks per CU (one generation of
 	 * blocks over the chip), then 1024 x 1; GENERAL batches (the pair kernel,
-	 * no tile): 2 x 512 too.  Round 6 re-measured the dense shape with the
+	 * no tile): 2 x 256, below.  Round 6 re-measured the dense shape with the
 	 * lean waves and the deferred verdicts: 2 x 512 at depth 1 307-318 us on
 	 * udp64 against 317-328 for round 5's 4 x 256 at depth 2, fastest in six
 	 * of six rounds (profiles/r06_geometry_ab.jsonl); the pair kernel at
 	 * 2 x 512: random pool 151.8-152.5 -> 150.0-151.0 us, working set
 	 * 52.6-53.3 -> 52.0-52.6 (profiles/r06_pair_geometry_ab.jsonl) */
-	static const int order_dense[] = {512, 1024, 256}, order_pair[] = {512, 256, 1024};
+	/* The pair kernel keeps two tiles of frame loads in flight, so half the
+	 * lanes -- 2 x 256 per CU -- halves the lines in flight (as wide slots
+	 * do on the tile kernel, batch_launch): working set 50.2-50.3 ->
+	 * 48.3-48.7 us, random pool 1 % faster; 4 x 256 slower
+	 * (profiles/r06_pair_lanes_ab.jsonl) */
+	static const int order_dense[] = {512, 1024, 256}, order_pair[] = {256, 512, 1024};
+	const uint32_t lanes = g.pair ? 512 : lanes_cu;
 	for (int nt : g.pair ? order_pair : order_dense) {
 		const uint32_t pb = per_block((uint32_t)nt);
-		if (!g.threads && (lanes_cu / nt) * pb <= lds_cu) {
+		const uint32_t bpc = std::max(lanes / (uint32_t)nt, 1u);
+		if (!g.threads && bpc * pb <= lds_cu) {
 			g.threads = nt;
-			g.bpc_cap = (int)(lanes_cu / (uint32_t)nt);
+			g.bpc_cap = (int)bpc;
 		}
 	}
 	if (!g.threads) { /* big tables: as many 256-lane blocks as LDS admits */
